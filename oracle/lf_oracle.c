@@ -1,0 +1,669 @@
+/*
+ * lf_oracle.c -- TEST INFRASTRUCTURE ONLY (see lf_oracle.h).
+ *
+ * CPU restatement of the reference LatticeFold commit+fold arithmetic. Each
+ * function cites the reference file:line it follows (paths relative to
+ * /root/reference/latticeum/crates/):
+ *   GL = stark-rings/crates/ring/src/cyclotomic_ring/models/goldilocks
+ *   SR = stark-rings/crates/ring/src
+ *   LF = latticefold/src
+ *   ZK = zkvm/src
+ * Deliberately simple: u128 arithmetic, no vectorisation, pthreads only where
+ * the reference uses rayon (so it doubles as the "port" CPU baseline).
+ */
+#include "lf_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef unsigned __int128 u128;
+typedef __int128 i128;
+
+#define P 0xFFFFFFFF00000001ull
+
+/* ------------------------------------------------------------------ field */
+uint64_t lfo_add(uint64_t a, uint64_t b) {
+  u128 s = (u128)a + b;
+  if (s >= P) s -= P;
+  return (uint64_t)s;
+}
+uint64_t lfo_sub(uint64_t a, uint64_t b) { return a >= b ? a - b : (uint64_t)((u128)a + P - b); }
+uint64_t lfo_mul(uint64_t a, uint64_t b) { return (uint64_t)(((u128)a * b) % P); }
+static uint64_t neg(uint64_t a) { return a ? P - a : 0; }
+uint64_t lfo_pow(uint64_t a, uint64_t e) {
+  uint64_t r = 1;
+  while (e) {
+    if (e & 1) r = lfo_mul(r, a);
+    a = lfo_mul(a, a);
+    e >>= 1;
+  }
+  return r;
+}
+uint64_t lfo_inv(uint64_t a) { return lfo_pow(a, P - 2); }
+/* ark-ff Fp64<MontBackend>: internal limb = a * R mod p, R = 2^64 mod p. */
+uint64_t lfo_to_mont(uint64_t a) { return (uint64_t)((((u128)a) << 64) % P); }
+uint64_t lfo_from_mont(uint64_t m) { return lfo_mul(m, lfo_inv(0xFFFFFFFFull)); }
+
+/* --------------------------------------------------------- Fq3 (GL/mod.rs:34-54)
+ * Fq[u]/(u^3 - NONRESIDUE), NONRESIDUE = 2^40 = 1099511627776. */
+#define NR 1099511627776ull
+static void fq3_mul(const uint64_t *a, const uint64_t *b, uint64_t *c) {
+  uint64_t a0 = a[0], a1 = a[1], a2 = a[2], b0 = b[0], b1 = b[1], b2 = b[2];
+  uint64_t c0 = lfo_add(lfo_mul(a0, b0), lfo_mul(NR, lfo_add(lfo_mul(a1, b2), lfo_mul(a2, b1))));
+  uint64_t c1 = lfo_add(lfo_add(lfo_mul(a0, b1), lfo_mul(a1, b0)), lfo_mul(NR, lfo_mul(a2, b2)));
+  uint64_t c2 = lfo_add(lfo_add(lfo_mul(a0, b2), lfo_mul(a1, b1)), lfo_mul(a2, b0));
+  c[0] = c0;
+  c[1] = c1;
+  c[2] = c2;
+}
+
+/* ------------------------------------------ Phi_72 CRT (GL/ntt.rs:15-47, 135-346) */
+static uint64_t W24[24]; /* ROOTS_OF_UNITY_24[i] = (2^40)^i  (GL/ntt.rs:15-40) */
+static uint64_t KAPPA_C, EIGHT_INV, FOUR_INV;
+static pthread_once_t once = PTHREAD_ONCE_INIT;
+static void init_consts(void) {
+  W24[0] = 1;
+  for (int i = 1; i < 24; i++) W24[i] = lfo_mul(W24[i - 1], NR);
+  /* GL/ntt.rs:42-43: the literal is 1/(2*ROOT[4] - 1) (its doc comment says 2*ROOT[4]-1;
+   * the value is what the reference computes with, so the literal is used) */
+  KAPPA_C = 12297829382473034411ull;
+  EIGHT_INV = lfo_inv(8);
+  FOUR_INV = lfo_inv(4);
+}
+
+/* GL/ntt.rs:348-437 -- isomorphisms between Fq[X]/(X^3 - w^k) and Fq3 */
+void lfo_phi72_homogenize(uint64_t *c) { /* GL/ntt.rs:326-334 */
+  uint64_t t;
+  c[4] = neg(c[4]);                                  /* 13: c1 = -c1 */
+  c[7] = lfo_mul(c[7], W24[2]);                      /* 7 */
+  c[8] = lfo_mul(c[8], W24[4]);
+  c[10] = lfo_mul(c[10], W24[6]);                    /* 19 */
+  c[11] = lfo_mul(c[11], W24[12]);
+  t = c[13];                                         /* 5 */
+  c[13] = lfo_mul(c[14], W24[3]);
+  c[14] = lfo_mul(t, W24[1]);
+  t = c[16];                                         /* 17 */
+  c[16] = lfo_mul(c[17], W24[11]);
+  c[17] = lfo_mul(t, W24[5]);
+  t = c[19];                                         /* 11 */
+  c[19] = lfo_mul(c[20], W24[7]);
+  c[20] = lfo_mul(t, W24[3]);
+  t = c[22];                                         /* 23 */
+  c[22] = lfo_mul(c[23], W24[15]);
+  c[23] = lfo_mul(t, W24[7]);
+}
+void lfo_phi72_dehomogenize(uint64_t *c) { /* GL/ntt.rs:338-346 */
+  uint64_t t;
+  c[4] = neg(c[4]);
+  c[7] = lfo_mul(c[7], W24[22]);
+  c[8] = lfo_mul(c[8], W24[20]);
+  c[10] = lfo_mul(c[10], W24[18]);
+  c[11] = lfo_mul(c[11], W24[12]);
+  t = c[13];
+  c[13] = lfo_mul(c[14], W24[23]);
+  c[14] = lfo_mul(t, W24[21]);
+  t = c[16];
+  c[16] = lfo_mul(c[17], W24[19]);
+  c[17] = lfo_mul(t, W24[13]);
+  t = c[19];
+  c[19] = lfo_mul(c[20], W24[21]);
+  c[20] = lfo_mul(t, W24[17]);
+  t = c[22];
+  c[22] = lfo_mul(c[23], W24[17]);
+  c[23] = lfo_mul(t, W24[9]);
+}
+
+static void phi72_crt1(uint64_t *c) { /* GL/ntt.rs:135-228 */
+  for (int i = 0; i < 12; i++) { /* f mod X^12 - zeta, X^12 - zeta^5 (:146-152) */
+    uint64_t a = c[i], b = c[12 + i];
+    uint64_t zb = lfo_mul(W24[4], b);
+    c[i] = lfo_add(a, zb);
+    c[12 + i] = lfo_sub(lfo_add(a, b), zb);
+  }
+  for (int i = 0; i < 6; i++) { /* :160-179 */
+    uint64_t a = c[i], b = lfo_mul(W24[2], c[6 + i]);
+    c[i] = lfo_add(a, b);
+    c[6 + i] = lfo_sub(a, b);
+    a = c[12 + i];
+    b = lfo_mul(W24[10], c[18 + i]);
+    c[12 + i] = lfo_add(a, b);
+    c[18 + i] = lfo_sub(a, b);
+  }
+  static const int tw[4] = {1, 7, 5, 11}; /* :186-225 */
+  for (int i = 0; i < 3; i++)
+    for (int q = 0; q < 4; q++) {
+      uint64_t a = c[6 * q + i], b = lfo_mul(W24[tw[q]], c[6 * q + 3 + i]);
+      c[6 * q + i] = lfo_add(a, b);
+      c[6 * q + 3 + i] = lfo_sub(a, b);
+    }
+  lfo_phi72_homogenize(c);
+}
+
+static void phi72_icrt1(uint64_t *c) { /* GL/ntt.rs:240-319 */
+  lfo_phi72_dehomogenize(c);
+  static const int tw[4] = {23, 17, 19, 13}; /* :250-285 */
+  for (int i = 0; i < 3; i++)
+    for (int q = 0; q < 4; q++) {
+      uint64_t a = c[6 * q + i], b = c[6 * q + 3 + i];
+      c[6 * q + i] = lfo_add(a, b);
+      c[6 * q + 3 + i] = lfo_mul(W24[tw[q]], lfo_sub(a, b));
+    }
+  for (int i = 0; i < 6; i++) { /* :291-308 */
+    uint64_t a = c[i], b = c[6 + i];
+    c[i] = lfo_add(a, b);
+    c[6 + i] = lfo_mul(W24[22], lfo_sub(a, b));
+    a = c[12 + i];
+    b = c[18 + i];
+    c[12 + i] = lfo_add(a, b);
+    c[18 + i] = lfo_mul(W24[14], lfo_sub(a, b));
+  }
+  for (int i = 0; i < 12; i++) { /* :311-318 */
+    uint64_t a = c[i], b = c[12 + i];
+    uint64_t kd = lfo_mul(KAPPA_C, lfo_sub(a, b));
+    c[i] = lfo_mul(EIGHT_INV, lfo_sub(lfo_add(a, b), kd));
+    c[12 + i] = lfo_mul(FOUR_INV, kd);
+  }
+}
+
+/* ------------------------------------------- negacyclic X^d + 1 (own convention) */
+static void nega_twiddles(int d, uint64_t *psi, uint64_t *psi_inv) {
+  uint64_t g = lfo_pow(7, (P - 1) / (uint64_t)(2 * d));
+  *psi = g;
+  *psi_inv = lfo_inv(g);
+}
+/* in-place cyclic DFT of size d with root w, natural order in and out */
+static void dft(uint64_t *a, int d, uint64_t w) {
+  for (int i = 1, j = 0; i < d; i++) { /* bit reversal */
+    int bit = d >> 1;
+    for (; j & bit; bit >>= 1) j ^= bit;
+    j ^= bit;
+    if (i < j) {
+      uint64_t t = a[i];
+      a[i] = a[j];
+      a[j] = t;
+    }
+  }
+  for (int len = 2; len <= d; len <<= 1) {
+    uint64_t wl = lfo_pow(w, (uint64_t)(d / len));
+    for (int i = 0; i < d; i += len) {
+      uint64_t x = 1;
+      for (int k = 0; k < len / 2; k++) {
+        uint64_t u = a[i + k], v = lfo_mul(a[i + k + len / 2], x);
+        a[i + k] = lfo_add(u, v);
+        a[i + k + len / 2] = lfo_sub(u, v);
+        x = lfo_mul(x, wl);
+      }
+    }
+  }
+}
+/* F[k] = sum_j f_j psi^((2k+1) j) */
+static void nega_ntt1(uint64_t *a, int d) {
+  uint64_t psi, psii;
+  nega_twiddles(d, &psi, &psii);
+  uint64_t x = 1;
+  for (int j = 0; j < d; j++) {
+    a[j] = lfo_mul(a[j], x);
+    x = lfo_mul(x, psi);
+  }
+  dft(a, d, lfo_mul(psi, psi));
+}
+static void nega_intt1(uint64_t *a, int d) {
+  uint64_t psi, psii;
+  nega_twiddles(d, &psi, &psii);
+  dft(a, d, lfo_mul(psii, psii));
+  uint64_t dinv = lfo_inv((uint64_t)d), x = dinv;
+  for (int j = 0; j < d; j++) {
+    a[j] = lfo_mul(a[j], x);
+    x = lfo_mul(x, psii);
+  }
+}
+
+static int is_pow2(int d) { return d >= 2 && (d & (d - 1)) == 0; }
+
+void lfo_crt(uint64_t *e, size_t n, int d) {
+  pthread_once(&once, init_consts);
+  for (size_t i = 0; i < n; i++) {
+    if (d == 24)
+      phi72_crt1(e + i * 24);
+    else if (is_pow2(d))
+      nega_ntt1(e + i * (size_t)d, d);
+    else
+      abort();
+  }
+}
+void lfo_icrt(uint64_t *e, size_t n, int d) {
+  pthread_once(&once, init_consts);
+  for (size_t i = 0; i < n; i++) {
+    if (d == 24)
+      phi72_icrt1(e + i * 24);
+    else if (is_pow2(d))
+      nega_intt1(e + i * (size_t)d, d);
+    else
+      abort();
+  }
+}
+
+/* SR/cyclotomic_ring/coeff_form.rs:54-67 schoolbook, then reduce:
+ * d=24: GL/mod.rs:75-98 (X^24 = X^12 - 1); d=2^k: X^d = -1 */
+void lfo_poly_mul(const uint64_t *a, const uint64_t *b, uint64_t *out, int d) {
+  uint64_t *t = calloc((size_t)2 * d, sizeof(uint64_t));
+  for (int i = 0; i < d; i++)
+    for (int j = 0; j < d; j++) t[i + j] = lfo_add(t[i + j], lfo_mul(a[i], b[j]));
+  if (d == 24) {
+    for (int i = 0; i < 12; i++) t[i] = lfo_sub(lfo_sub(t[i], t[24 + i]), t[36 + i]);
+    for (int i = 12; i < 24; i++) t[i] = lfo_add(t[i], t[12 + i]);
+  } else {
+    for (int i = 0; i < d; i++) t[i] = lfo_sub(t[i], t[d + i]);
+  }
+  memcpy(out, t, sizeof(uint64_t) * (size_t)d);
+  free(t);
+}
+
+/* SR/cyclotomic_ring/ntt_form.rs:159-175 (zero short-cut is value-neutral) */
+void lfo_slot_mul(const uint64_t *a, const uint64_t *b, uint64_t *out, int d) {
+  if (d == 24) {
+    for (int s = 0; s < 8; s++) fq3_mul(a + 3 * s, b + 3 * s, out + 3 * s);
+  } else {
+    for (int s = 0; s < d; s++) out[s] = lfo_mul(a[s], b[s]);
+  }
+}
+static void slot_mul_acc(const uint64_t *a, const uint64_t *b, uint64_t *acc, int d) {
+  if (d == 24) {
+    uint64_t t[3];
+    for (int s = 0; s < 8; s++) {
+      fq3_mul(a + 3 * s, b + 3 * s, t);
+      for (int c = 0; c < 3; c++) acc[3 * s + c] = lfo_add(acc[3 * s + c], t[c]);
+    }
+  } else {
+    for (int s = 0; s < d; s++) acc[s] = lfo_add(acc[s], lfo_mul(a[s], b[s]));
+  }
+}
+
+/* ------------------------------------ balanced decomposition (SR/balanced_decomposition)
+ * signed representative: fq_convertible.rs:22-34; digits: mod.rs:62-103;
+ * rounded_div: linear_algebra/src/ops.rs:64-80; back to Fq: fq_convertible.rs:38-49 */
+static i128 signed_rep(uint64_t v) {
+  const uint64_t qh = (P - 1) / 2;
+  return v > qh ? (i128)v - (i128)P : (i128)v;
+}
+static uint64_t from_signed(i128 x) {
+  if (x < 0) {
+    i128 r = x % (i128)P;
+    return (uint64_t)(r + (i128)P) % P; /* Fp::from(r + q) */
+  }
+  return (uint64_t)(x % (i128)P);
+}
+static i128 rounded_div(i128 dividend, i128 divisor) {
+  if ((dividend ^ divisor) >= 0) return (dividend + divisor / 2) / divisor;
+  return (dividend - divisor / 2) / divisor;
+}
+int lfo_decompose_balanced(uint64_t v, uint64_t bu, int len, uint64_t *out) {
+  if (bu < 2 || (bu & 1)) return -2;
+  i128 curr = signed_rep(v), b = (i128)bu, bh = b / 2;
+  int i = 0;
+  for (;;) {
+    i128 rem = curr % b; /* Rust % truncates like C */
+    if (i >= len) return -1; /* the reference indexes out of bounds and panics */
+    if ((rem < 0 ? -rem : rem) <= bh) {
+      out[i] = from_signed(rem);
+      curr /= b;
+    } else {
+      out[i] = from_signed(rem < 0 ? rem + b : rem - b);
+      i128 carry = rounded_div(rem, b);
+      curr = curr / b + carry;
+    }
+    i++;
+    if (curr == 0) break;
+  }
+  for (; i < len; i++) out[i] = 0;
+  return 0;
+}
+
+int lfo_gadget_decompose(const uint64_t *in, size_t n, int d, uint64_t b, int len,
+                         uint64_t *out) {
+  uint64_t dig[64];
+  if (len > 64) return -2;
+  for (size_t j = 0; j < n; j++)
+    for (int c = 0; c < d; c++) { /* coeff_form.rs:593-605 */
+      if (lfo_decompose_balanced(in[j * d + c], b, len, dig)) return -1;
+      for (int k = 0; k < len; k++) out[(j * len + k) * d + c] = dig[k];
+    }
+  return 0;
+}
+
+void lfo_gadget_recompose(const uint64_t *in, size_t n_out, int d, uint64_t b, int len,
+                          uint64_t *out) {
+  for (size_t j = 0; j < n_out; j++)
+    for (int c = 0; c < d; c++) { /* recompose(): Horner from the top digit */
+      uint64_t r = 0;
+      for (int k = len - 1; k >= 0; k--) r = lfo_add(lfo_mul(r, b % P), in[(j * len + k) * d + c]);
+      out[j * d + c] = r;
+    }
+}
+
+/* --------------------------------------------------------------- threading */
+typedef struct {
+  void (*fn)(void *, size_t, size_t);
+  void *arg;
+  size_t lo, hi;
+} job_t;
+static void *job_run(void *p) {
+  job_t *j = p;
+  j->fn(j->arg, j->lo, j->hi);
+  return NULL;
+}
+static void parallel_for(size_t n, int nthreads, void (*fn)(void *, size_t, size_t), void *arg) {
+  if (nthreads <= 1 || n < 2) {
+    fn(arg, 0, n);
+    return;
+  }
+  if ((size_t)nthreads > n) nthreads = (int)n;
+  pthread_t th[256];
+  job_t jobs[256];
+  if (nthreads > 256) nthreads = 256;
+  for (int t = 0; t < nthreads; t++) {
+    jobs[t].fn = fn;
+    jobs[t].arg = arg;
+    jobs[t].lo = n * (size_t)t / (size_t)nthreads;
+    jobs[t].hi = n * (size_t)(t + 1) / (size_t)nthreads;
+    pthread_create(&th[t], NULL, job_run, &jobs[t]);
+  }
+  for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+}
+
+/* ------------------------------------------------------ Witness (LF/arith.rs) */
+typedef struct {
+  const uint64_t *in;
+  uint64_t *fc, *f;
+  int d, L;
+  uint64_t B;
+  int err;
+} wit_arg;
+static void wit_from_w_ccs_range(void *p, size_t lo, size_t hi) {
+  wit_arg *a = p;
+  int d = a->d;
+  uint64_t *tmp = malloc(sizeof(uint64_t) * (size_t)d);
+  for (size_t j = lo; j < hi; j++) {
+    memcpy(tmp, a->in + j * d, sizeof(uint64_t) * (size_t)d);
+    lfo_icrt(tmp, 1, d); /* ICRT::elementwise_icrt (:232) */
+    if (lfo_gadget_decompose(tmp, 1, d, a->B, a->L, a->fc + j * a->L * d)) a->err = 1;
+  }
+  free(tmp);
+  /* f = CRT(f_coeff) (:238) -- the reference's CRT loop is sequential */
+  memcpy(a->f + lo * a->L * d, a->fc + lo * a->L * d, sizeof(uint64_t) * (hi - lo) * a->L * d);
+  lfo_crt(a->f + lo * a->L * d, (hi - lo) * a->L, d);
+}
+int lfo_witness_from_w_ccs(const uint64_t *w_ccs, size_t W, int d, uint64_t B, int L,
+                           uint64_t *f_coeff, uint64_t *f, int nthreads) {
+  wit_arg a = {w_ccs, f_coeff, f, d, L, B, 0};
+  parallel_for(W, nthreads, wit_from_w_ccs_range, &a);
+  return a.err ? -1 : 0;
+}
+
+typedef struct {
+  const uint64_t *f;
+  uint64_t *fc, *w;
+  int d, L;
+  uint64_t B;
+} from_f_arg;
+static void from_f_range(void *p, size_t lo, size_t hi) {
+  from_f_arg *a = p;
+  int d = a->d, L = a->L;
+  memcpy(a->fc + lo * L * d, a->f + lo * L * d, sizeof(uint64_t) * (hi - lo) * L * d);
+  lfo_icrt(a->fc + lo * L * d, (hi - lo) * L, d); /* LF/arith.rs:300 */
+  lfo_gadget_recompose(a->f + lo * L * d, hi - lo, d, a->B, L, a->w + lo * d); /* :305 */
+}
+void lfo_witness_from_f(const uint64_t *f, size_t N, int d, uint64_t B, int L,
+                        uint64_t *f_coeff, uint64_t *w_ccs, int nthreads) {
+  from_f_arg a = {f, f_coeff, w_ccs, d, L, B};
+  parallel_for(N / (size_t)L, nthreads, from_f_range, &a);
+}
+
+void lfo_get_fhat_phi72(const uint64_t *f_coeff, size_t N, uint64_t *out) {
+  /* LF/arith.rs:273-297: fhat[j][i] slot s = (f_i.coeff[8j + s], 0, 0) */
+  for (int j = 0; j < 3; j++)
+    for (size_t i = 0; i < N; i++)
+      for (int s = 0; s < 8; s++) {
+        uint64_t *o = out + ((size_t)j * N + i) * 24 + 3 * s;
+        o[0] = f_coeff[i * 24 + 8 * j + s];
+        o[1] = 0;
+        o[2] = 0;
+      }
+}
+
+/* --------------------------------------------------------------- Ajtai commit */
+typedef struct {
+  const uint64_t *A, *f;
+  uint64_t *cm;
+  size_t kappa, ncols, nvec;
+  int d;
+} ajtai_arg;
+static void ajtai_rows(void *p, size_t lo, size_t hi) {
+  ajtai_arg *a = p;
+  int d = a->d;
+  for (size_t v = 0; v < a->nvec; v++)
+    for (size_t i = lo; i < hi; i++) { /* LA/matrix.rs:174-176: row . v */
+      uint64_t *acc = a->cm + (v * a->kappa + i) * d;
+      memset(acc, 0, sizeof(uint64_t) * (size_t)d);
+      for (size_t j = 0; j < a->ncols; j++)
+        slot_mul_acc(a->A + (i * a->ncols + j) * d, a->f + (v * a->ncols + j) * d, acc, d);
+    }
+}
+void lfo_ajtai_commit(const uint64_t *A, size_t kappa, size_t ncols, int d, const uint64_t *f,
+                      size_t nvec, uint64_t *cm, int nthreads) {
+  ajtai_arg a = {A, f, cm, kappa, ncols, nvec, d};
+  parallel_for(kappa, nthreads, ajtai_rows, &a);
+}
+
+/* ------------------------------------------- decomposition (LF/nifs/decomposition.rs) */
+typedef struct {
+  const uint64_t *fc;
+  uint64_t *fck, *fk, *wk;
+  size_t N;
+  int d, L, K;
+  uint64_t B, bs;
+  int err;
+} dec_arg;
+static void dec_range(void *p, size_t lo, size_t hi) {
+  dec_arg *a = p;
+  int d = a->d, L = a->L, K = a->K;
+  size_t N = a->N;
+  uint64_t dig[64];
+  /* decompose_B_vec_into_k_vec (decomposition/utils.rs:45-49): per element,
+   * per coefficient, K balanced base-b_small digits; transpose to K vectors */
+  for (size_t j = lo * L; j < hi * L; j++)
+    for (int c = 0; c < d; c++) {
+      if (lfo_decompose_balanced(a->fc[j * d + c], a->bs, K, dig)) a->err = 1;
+      for (int k = 0; k < K; k++) a->fck[((size_t)k * N + j) * d + c] = dig[k];
+    }
+  /* Witness::from_f_coeff (LF/arith.rs:324-338) per k: f = CRT, w_ccs = recompose */
+  for (int k = 0; k < K; k++) {
+    uint64_t *fk = a->fk + (size_t)k * N * d, *fck = a->fck + (size_t)k * N * d;
+    memcpy(fk + lo * L * d, fck + lo * L * d, sizeof(uint64_t) * (hi - lo) * L * d);
+    lfo_crt(fk + lo * L * d, (hi - lo) * L, d);
+    lfo_gadget_recompose(fk + lo * L * d, hi - lo, d, a->B, L,
+                         a->wk + ((size_t)k * (N / L) + lo) * d);
+  }
+}
+int lfo_decompose_witness(const uint64_t *f_coeff, size_t N, int d, uint64_t B, int L,
+                          uint64_t b_small, int K, uint64_t *f_coeff_k, uint64_t *f_k,
+                          uint64_t *w_ccs_k, int nthreads) {
+  dec_arg a = {f_coeff, f_coeff_k, f_k, w_ccs_k, N, d, L, K, B, b_small, 0};
+  parallel_for(N / (size_t)L, nthreads, dec_range, &a);
+  return a.err ? -1 : 0;
+}
+
+void lfo_commit_witnesses_y0(const uint64_t *cm, uint64_t *y, size_t kappa, int d,
+                             uint64_t b_small, int K) {
+  /* LF/nifs/decomposition.rs:183-200: b_sum = fold_rev((acc + y_i) * b), y_0 = cm - b_sum */
+  size_t n = kappa * (size_t)d;
+  for (size_t c = 0; c < n; c++) {
+    uint64_t acc = 0;
+    for (int k = K - 1; k >= 1; k--) acc = lfo_mul(lfo_add(acc, y[(size_t)k * n + c]), b_small);
+    y[c] = lfo_sub(cm[c], acc);
+  }
+}
+
+/* ---------------------------------------------------------------------- folding */
+int lfo_short_challenge(const uint8_t *bs, size_t nbytes, int d, uint64_t *coeffs) {
+  /* CR/rings/goldilocks.rs:41-67: 3 bytes -> 4 coefficients of 6 bits, minus 32 */
+  if (d % 4 != 0 || nbytes != (size_t)(3 * d / 4)) return -1;
+  for (int i = 0; i < d / 4; i++) {
+    int x[4];
+    x[0] = (bs[3 * i] & 0x3f) - 32;
+    x[1] = (((bs[3 * i] & 0xc0) >> 6) | ((bs[3 * i + 1] & 0x0f) << 2)) - 32;
+    x[2] = (((bs[3 * i + 1] & 0xf0) >> 4) | ((bs[3 * i + 2] & 0x03) << 4)) - 32;
+    x[3] = ((bs[3 * i + 2] & 0xfc) >> 2) - 32;
+    for (int k = 0; k < 4; k++) coeffs[4 * i + k] = x[k] < 0 ? P - (uint64_t)(-x[k]) : (uint64_t)x[k];
+  }
+  return 0;
+}
+
+typedef struct {
+  const uint64_t *rho, *f;
+  uint64_t *f0;
+  size_t nwit, N;
+  int d;
+} fold_arg;
+static void fold_range(void *p, size_t lo, size_t hi) {
+  fold_arg *a = p;
+  int d = a->d;
+  for (size_t j = lo; j < hi; j++) {
+    uint64_t *acc = a->f0 + j * d;
+    memset(acc, 0, sizeof(uint64_t) * (size_t)d);
+    for (size_t i = 0; i < a->nwit; i++) /* LF/nifs/folding.rs:258-268 */
+      slot_mul_acc(a->rho + i * d, a->f + (i * a->N + j) * d, acc, d);
+  }
+}
+void lfo_fold_f0(const uint64_t *rho, const uint64_t *f, size_t nwit, size_t N, int d,
+                 uint64_t *f0, int nthreads) {
+  fold_arg a = {rho, f, f0, nwit, N, d};
+  parallel_for(N, nthreads, fold_range, &a);
+}
+void lfo_fold_cm0(const uint64_t *rho, const uint64_t *cm, size_t nwit, size_t kappa, int d,
+                  uint64_t *cm0) {
+  fold_arg a = {rho, cm, cm0, nwit, kappa, d}; /* folding/utils.rs:470-476 */
+  fold_range(&a, 0, kappa);
+}
+
+/* --------------------------------------------- Poseidon2-16 (ZK/poseidon2.rs) */
+#include "p2_consts.inc"
+static const uint64_t EXT_INIT[64] = LF_P2_EXT_INIT;
+static const uint64_t EXT_TERM[64] = LF_P2_EXT_TERM;
+static const uint64_t INTERNAL[22] = LF_P2_INTERNAL;
+static const uint64_t DIAG_M1[16] = LF_P2_DIAG_M1;
+
+static uint64_t sbox(uint64_t x, uint64_t rc) { /* Plonky3 add_rc_and_sbox_generic: (x+rc)^7 */
+  uint64_t y = lfo_add(x, rc), y2 = lfo_mul(y, y), y4 = lfo_mul(y2, y2);
+  return lfo_mul(lfo_mul(y4, y2), y);
+}
+void lfo_p2_mds16(uint64_t *s) { /* ZK/poseidon2.rs:243-268, MDSMat4 (sages/initial_mds.sage:27-31) */
+  for (int c = 0; c < 16; c += 4) {
+    uint64_t x0 = s[c], x1 = s[c + 1], x2 = s[c + 2], x3 = s[c + 3];
+    uint64_t t = lfo_add(lfo_add(x0, x1), lfo_add(x2, x3));
+    s[c + 0] = lfo_add(t, lfo_add(x0, lfo_add(x1, x1)));           /* 2 3 1 1 */
+    s[c + 1] = lfo_add(t, lfo_add(x1, lfo_add(x2, x2)));           /* 1 2 3 1 */
+    s[c + 2] = lfo_add(t, lfo_add(x2, lfo_add(x3, x3)));           /* 1 1 2 3 */
+    s[c + 3] = lfo_add(t, lfo_add(x3, lfo_add(x0, x0)));           /* 3 1 1 2 */
+  }
+  for (int k = 0; k < 4; k++) {
+    uint64_t sum = lfo_add(lfo_add(s[k], s[4 + k]), lfo_add(s[8 + k], s[12 + k]));
+    for (int j = k; j < 16; j += 4) s[j] = lfo_add(s[j], sum);
+  }
+}
+void lfo_p2_permute(uint64_t *s) { /* ZK/poseidon2.rs:100-173 */
+  lfo_p2_mds16(s);
+  for (int r = 0; r < 4; r++) {
+    for (int i = 0; i < 16; i++) s[i] = sbox(s[i], EXT_INIT[16 * r + i]);
+    lfo_p2_mds16(s);
+  }
+  for (int r = 0; r < 22; r++) {
+    s[0] = sbox(s[0], INTERNAL[r]);
+    uint64_t sum = 0; /* Plonky3 matmul_internal: s_i = s_i * diag_m1_i + sum */
+    for (int i = 0; i < 16; i++) sum = lfo_add(sum, s[i]);
+    for (int i = 0; i < 16; i++) s[i] = lfo_add(lfo_mul(s[i], DIAG_M1[i]), sum);
+  }
+  for (int r = 0; r < 4; r++) {
+    for (int i = 0; i < 16; i++) s[i] = sbox(s[i], EXT_TERM[16 * r + i]);
+    lfo_p2_mds16(s);
+  }
+}
+static void p2_range(void *p, size_t lo, size_t hi) {
+  uint64_t *st = p;
+  for (size_t i = lo; i < hi; i++) lfo_p2_permute(st + 16 * i);
+}
+void lfo_p2_permute_batch(uint64_t *states, size_t n, int nthreads) {
+  parallel_for(n, nthreads, p2_range, states);
+}
+void lfo_p2_hash_iter(const uint64_t *in, size_t n, uint64_t out[4]) {
+  uint64_t s[16] = {0}; /* ZK/poseidon2.rs:210-234 */
+  size_t pos = 0;
+  for (;;) {
+    int i;
+    for (i = 0; i < 12; i++) {
+      if (pos < n) {
+        s[i] = in[pos++];
+      } else {
+        if (i != 0) lfo_p2_permute(s);
+        goto done;
+      }
+    }
+    lfo_p2_permute(s);
+  }
+done:
+  memcpy(out, s, 4 * sizeof(uint64_t));
+}
+
+/* ------------------------- DuplexChallenger<Goldilocks, Perm, 16, 12> (Plonky3; unpinned) */
+void lfo_tr_init(lfo_transcript *t) { memset(t, 0, sizeof(*t)); }
+static void duplexing(lfo_transcript *t) {
+  for (int i = 0; i < t->nin; i++) t->state[i] = t->inbuf[i]; /* overwrite mode */
+  t->nin = 0;
+  lfo_p2_permute(t->state);
+  memcpy(t->outbuf, t->state, 12 * sizeof(uint64_t));
+  t->nout = 12;
+}
+void lfo_tr_observe(lfo_transcript *t, uint64_t v) {
+  t->nout = 0; /* buffered output is invalidated */
+  t->inbuf[t->nin++] = v % P;
+  if (t->nin == 12) duplexing(t);
+}
+uint64_t lfo_tr_sample(lfo_transcript *t) {
+  if (t->nin > 0 || t->nout == 0) duplexing(t);
+  return t->outbuf[--t->nout]; /* pops from the end */
+}
+void lfo_tr_absorb_ring(lfo_transcript *t, const uint64_t *e, size_t n, int d) {
+  /* ZK/fiat_shamir.rs:51-60: each NTT slot's base-field limbs, as raw ark
+   * Montgomery u64s, observed in order */
+  for (size_t i = 0; i < n * (size_t)d; i++) lfo_tr_observe(t, lfo_to_mont(e[i]));
+}
+void lfo_tr_get_challenge(lfo_transcript *t, uint64_t out[3]) {
+  for (int i = 0; i < 3; i++) out[i] = lfo_tr_sample(t); /* fiat_shamir.rs:69-86 */
+  for (int i = 0; i < 3; i++) lfo_tr_observe(t, out[i]);
+}
+void lfo_tr_squeeze_bytes(lfo_transcript *t, uint8_t *out, size_t n) {
+  while (n > 0) { /* fiat_shamir.rs:88-102: canonical little-endian bytes */
+    uint64_t v = lfo_tr_sample(t);
+    size_t take = n < 8 ? n : 8;
+    for (size_t i = 0; i < take; i++) *out++ = (uint8_t)(v >> (8 * i));
+    n -= take;
+  }
+}
+
+/* ----------------------------------------------------------- synthetic inputs */
+static uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+void lfo_fill_uniform(uint64_t *out, size_t n, uint64_t seed) {
+  /* element i = SplitMix64 output for counter i, re-mixed until < p
+   * (index-addressable, so the device generator reproduces it exactly) */
+  const uint64_t G = 0x9e3779b97f4a7c15ull;
+  for (size_t i = 0; i < n; i++) {
+    uint64_t x = mix64(seed + (uint64_t)(i + 1) * G);
+    while (x >= P) x = mix64(x + G);
+    out[i] = x;
+  }
+}

@@ -1,0 +1,253 @@
+"""ctypes wrapper over oracle/liblf_oracle.so -- TEST INFRASTRUCTURE ONLY.
+
+The C oracle (oracle/lf_oracle.c) is a CPU restatement of the reference's
+LatticeFold commit+fold arithmetic, used as the parity checker for the HIP
+product path. Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg may import this module. Arrays are numpy uint64 in AoS layout
+(element-major, d u64 per ring element), canonical values in [0, p).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+P = (1 << 64) - (1 << 32) + 1
+_DIR = Path(__file__).resolve().parent
+_LIB = _DIR / "liblf_oracle.so"
+_lib = None
+
+u64p = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
+u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+SZ, I, U64 = C.c_size_t, C.c_int, C.c_uint64
+
+
+def build() -> Path:
+    """Compile the oracle with its own Makefile (gcc only)."""
+    subprocess.run(["make", "-s", "-C", str(_DIR)], check=True)
+    return _LIB
+
+
+class Transcript(C.Structure):
+    _fields_ = [("state", U64 * 16), ("inbuf", U64 * 12), ("nin", I),
+                ("outbuf", U64 * 12), ("nout", I)]
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not _LIB.exists():
+        build()
+    L = C.CDLL(str(_LIB))
+    sig = {
+        "lfo_add": (U64, [U64, U64]), "lfo_sub": (U64, [U64, U64]),
+        "lfo_mul": (U64, [U64, U64]), "lfo_pow": (U64, [U64, U64]),
+        "lfo_inv": (U64, [U64]), "lfo_to_mont": (U64, [U64]), "lfo_from_mont": (U64, [U64]),
+        "lfo_crt": (None, [u64p, SZ, I]), "lfo_icrt": (None, [u64p, SZ, I]),
+        "lfo_phi72_homogenize": (None, [u64p]), "lfo_phi72_dehomogenize": (None, [u64p]),
+        "lfo_poly_mul": (None, [u64p, u64p, u64p, I]),
+        "lfo_slot_mul": (None, [u64p, u64p, u64p, I]),
+        "lfo_decompose_balanced": (I, [U64, U64, I, u64p]),
+        "lfo_gadget_decompose": (I, [u64p, SZ, I, U64, I, u64p]),
+        "lfo_gadget_recompose": (None, [u64p, SZ, I, U64, I, u64p]),
+        "lfo_witness_from_w_ccs": (I, [u64p, SZ, I, U64, I, u64p, u64p, I]),
+        "lfo_witness_from_f": (None, [u64p, SZ, I, U64, I, u64p, u64p, I]),
+        "lfo_get_fhat_phi72": (None, [u64p, SZ, u64p]),
+        "lfo_ajtai_commit": (None, [u64p, SZ, SZ, I, u64p, SZ, u64p, I]),
+        "lfo_decompose_witness": (I, [u64p, SZ, I, U64, I, U64, I, u64p, u64p, u64p, I]),
+        "lfo_commit_witnesses_y0": (None, [u64p, u64p, SZ, I, U64, I]),
+        "lfo_short_challenge": (I, [u8p, SZ, I, u64p]),
+        "lfo_fold_f0": (None, [u64p, u64p, SZ, SZ, I, u64p, I]),
+        "lfo_fold_cm0": (None, [u64p, u64p, SZ, SZ, I, u64p]),
+        "lfo_p2_mds16": (None, [u64p]), "lfo_p2_permute": (None, [u64p]),
+        "lfo_p2_permute_batch": (None, [u64p, SZ, I]),
+        "lfo_p2_hash_iter": (None, [u64p, SZ, u64p]),
+        "lfo_tr_init": (None, [C.POINTER(Transcript)]),
+        "lfo_tr_observe": (None, [C.POINTER(Transcript), U64]),
+        "lfo_tr_sample": (U64, [C.POINTER(Transcript)]),
+        "lfo_tr_absorb_ring": (None, [C.POINTER(Transcript), u64p, SZ, I]),
+        "lfo_tr_get_challenge": (None, [C.POINTER(Transcript), u64p]),
+        "lfo_tr_squeeze_bytes": (None, [C.POINTER(Transcript), u8p, SZ]),
+        "lfo_fill_uniform": (None, [u64p, SZ, U64]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _u64(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint64))
+
+
+def nthreads_default() -> int:
+    return int(os.environ.get("LF_ORACLE_THREADS", os.cpu_count() or 1))
+
+
+# ---------------------------------------------------------------- ring ops
+def crt(elems, d: int) -> np.ndarray:
+    x = _u64(elems).copy()
+    lib().lfo_crt(x, x.size // d, d)
+    return x
+
+
+def icrt(elems, d: int) -> np.ndarray:
+    x = _u64(elems).copy()
+    lib().lfo_icrt(x, x.size // d, d)
+    return x
+
+
+def poly_mul(a, b, d: int) -> np.ndarray:
+    out = np.zeros(d, np.uint64)
+    lib().lfo_poly_mul(_u64(a), _u64(b), out, d)
+    return out
+
+
+def slot_mul(a, b, d: int) -> np.ndarray:
+    out = np.zeros(d, np.uint64)
+    lib().lfo_slot_mul(_u64(a), _u64(b), out, d)
+    return out
+
+
+def decompose_balanced(v: int, b: int, length: int):
+    out = np.zeros(length, np.uint64)
+    rc = lib().lfo_decompose_balanced(v, b, length, out)
+    if rc:
+        raise ValueError(f"decompose_balanced failed rc={rc}")
+    return out
+
+
+def gadget_decompose(elems, d: int, b: int, length: int) -> np.ndarray:
+    x = _u64(elems)
+    n = x.size // d
+    out = np.zeros(n * length * d, np.uint64)
+    if lib().lfo_gadget_decompose(x, n, d, b, length, out):
+        raise ValueError("gadget_decompose: value needs more digits than padding_size")
+    return out
+
+
+def gadget_recompose(elems, d: int, b: int, length: int) -> np.ndarray:
+    x = _u64(elems)
+    n_out = x.size // (d * length)
+    out = np.zeros(n_out * d, np.uint64)
+    lib().lfo_gadget_recompose(x, n_out, d, b, length, out)
+    return out
+
+
+def witness_from_w_ccs(w_ccs, d: int, B: int, L: int, nthreads: int | None = None):
+    x = _u64(w_ccs)
+    W = x.size // d
+    fc = np.zeros(W * L * d, np.uint64)
+    f = np.zeros(W * L * d, np.uint64)
+    if lib().lfo_witness_from_w_ccs(x, W, d, B, L, fc, f, nthreads or nthreads_default()):
+        raise ValueError("from_w_ccs: decomposition overflow")
+    return fc, f
+
+
+def witness_from_f(f, d: int, B: int, L: int, nthreads: int | None = None):
+    x = _u64(f)
+    N = x.size // d
+    fc = np.zeros(N * d, np.uint64)
+    w = np.zeros((N // L) * d, np.uint64)
+    lib().lfo_witness_from_f(x, N, d, B, L, fc, w, nthreads or nthreads_default())
+    return fc, w
+
+
+def get_fhat_phi72(f_coeff) -> np.ndarray:
+    x = _u64(f_coeff)
+    N = x.size // 24
+    out = np.zeros(3 * N * 24, np.uint64)
+    lib().lfo_get_fhat_phi72(x, N, out)
+    return out
+
+
+def ajtai_commit(A, kappa: int, ncols: int, d: int, f, nvec: int = 1,
+                 nthreads: int | None = None) -> np.ndarray:
+    cm = np.zeros(nvec * kappa * d, np.uint64)
+    lib().lfo_ajtai_commit(_u64(A), kappa, ncols, d, _u64(f), nvec, cm,
+                           nthreads or nthreads_default())
+    return cm
+
+
+def decompose_witness(f_coeff, d: int, B: int, L: int, b_small: int, K: int,
+                      nthreads: int | None = None):
+    x = _u64(f_coeff)
+    N = x.size // d
+    fck = np.zeros(K * N * d, np.uint64)
+    fk = np.zeros(K * N * d, np.uint64)
+    wk = np.zeros(K * (N // L) * d, np.uint64)
+    if lib().lfo_decompose_witness(x, N, d, B, L, b_small, K, fck, fk, wk,
+                                   nthreads or nthreads_default()):
+        raise ValueError("decompose_witness: coefficient exceeds b_small^K range")
+    return fck, fk, wk
+
+
+def commit_witnesses_y0(cm, y, kappa: int, d: int, b_small: int, K: int) -> np.ndarray:
+    yy = _u64(y).copy()
+    lib().lfo_commit_witnesses_y0(_u64(cm), yy, kappa, d, b_small, K)
+    return yy
+
+
+def short_challenge(bs: bytes, d: int) -> np.ndarray:
+    out = np.zeros(d, np.uint64)
+    if lib().lfo_short_challenge(np.frombuffer(bytes(bs), np.uint8).copy(), len(bs), d, out):
+        raise ValueError("short_challenge: wrong byte count")
+    return out
+
+
+def fold_f0(rho, f, nwit: int, N: int, d: int, nthreads: int | None = None) -> np.ndarray:
+    out = np.zeros(N * d, np.uint64)
+    lib().lfo_fold_f0(_u64(rho), _u64(f), nwit, N, d, out, nthreads or nthreads_default())
+    return out
+
+
+def fold_cm0(rho, cm, nwit: int, kappa: int, d: int) -> np.ndarray:
+    out = np.zeros(kappa * d, np.uint64)
+    lib().lfo_fold_cm0(_u64(rho), _u64(cm), nwit, kappa, d, out)
+    return out
+
+
+# ---------------------------------------------------------------- Poseidon2
+def p2_mds16(s) -> np.ndarray:
+    x = _u64(s).copy()
+    lib().lfo_p2_mds16(x)
+    return x
+
+
+def p2_permute(states, nthreads: int = 1) -> np.ndarray:
+    x = _u64(states).copy()
+    lib().lfo_p2_permute_batch(x, x.size // 16, nthreads)
+    return x
+
+
+def p2_hash_iter(vals) -> np.ndarray:
+    out = np.zeros(4, np.uint64)
+    x = _u64(vals) if len(vals) else np.zeros(1, np.uint64)
+    lib().lfo_p2_hash_iter(x, len(vals), out)
+    return out
+
+
+def new_transcript() -> Transcript:
+    t = Transcript()
+    lib().lfo_tr_init(C.byref(t))
+    return t
+
+
+def fill_uniform(n: int, seed: int) -> np.ndarray:
+    out = np.zeros(n, np.uint64)
+    lib().lfo_fill_uniform(out, n, seed)
+    return out
+
+
+def to_mont(a: int) -> int:
+    return lib().lfo_to_mont(a)
+
+
+def from_mont(a: int) -> int:
+    return lib().lfo_from_mont(a)

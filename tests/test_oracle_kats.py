@@ -1,0 +1,175 @@
+"""Pin the CPU oracle against the reference's own known-answer data
+(tests/golden/reference_kats.json, extracted by tools/gen_golden_kats.py)."""
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+P = O.P
+KATS = json.loads((Path(__file__).parent / "golden/reference_kats.json").read_text())
+
+
+@pytest.mark.parametrize("name", ["test_crt", "test_crt2"])
+def test_phi72_crt_kat(name):
+    k = KATS["crt"][name]  # GL/ntt.rs test_crt / test_crt2
+    x = np.array(k["coeffs"], np.uint64)
+    y = O.crt(x, 24)
+    O.lib().lfo_phi72_dehomogenize(y)
+    assert [int(v) for v in y] == k["crt_dehomogenized"]
+
+
+@pytest.mark.parametrize("name", ["test_icrt", "test_icrt_2"])
+def test_phi72_icrt_kat(name):
+    k = KATS["crt"][name]  # GL/ntt.rs test_icrt / test_icrt_2
+    ev = np.array(k["evaluations_dehomogenized"], np.uint64)
+    O.lib().lfo_phi72_homogenize(ev)
+    assert [int(v) for v in O.icrt(ev, 24)] == k["coeffs"]
+
+
+def test_roots_and_constants():
+    # GL/ntt.rs:450-467: w = 2^40 has order 24; GL/ntt.rs:42-47 constants
+    w = 1 << 40
+    assert O.lib().lfo_pow(w, 24) == 1
+    assert all(O.lib().lfo_pow(w, k) != 1 for k in range(1, 24))
+    # KAPPA literal is the inverse of 2*w^4 - 1 (its doc comment omits the inverse)
+    assert O.lib().lfo_inv((2 * O.lib().lfo_pow(w, 4) - 1) % P) == 12297829382473034411
+    assert O.lib().lfo_inv(8) == 16140901060737761281
+    assert O.lib().lfo_inv(4) == 13835058052060938241
+
+
+def test_montgomery_radix():
+    # ark-ff Fp64 stores a*R, R = 2^64 mod p = 2^32 - 1
+    assert O.to_mont(1) == (1 << 32) - 1
+    for a in [0, 1, 2, 12345, P - 1]:
+        assert O.from_mont(O.to_mont(a)) == a
+
+
+def test_phi72_roundtrip_and_mul_crt():
+    # GL/ntt.rs:789-806 round trips; GL/mod.rs:231-247 test_mul_crt
+    rng = np.random.default_rng(1)
+    x = O.fill_uniform(24 * 200, 7)
+    assert np.array_equal(O.icrt(O.crt(x, 24), 24), x)
+    for _ in range(20):
+        a, b = O.fill_uniform(24, rng.integers(1 << 62)), O.fill_uniform(24, rng.integers(1 << 62))
+        prod = O.poly_mul(a, b, 24)
+        via = O.icrt(O.slot_mul(O.crt(a, 24), O.crt(b, 24), 24), 24)
+        assert np.array_equal(prod, via)
+
+
+def test_phi72_one():
+    # GL/mod.rs:193-205: crt(ONE) = ONE (all slots (1,0,0))
+    one = np.zeros(24, np.uint64)
+    one[0] = 1
+    expect = np.zeros(24, np.uint64)
+    expect[0::3] = 1
+    assert np.array_equal(O.crt(one, 24), expect)
+
+
+@pytest.mark.parametrize("d", [16, 64, 1024])
+def test_negacyclic_ntt_definition(d):
+    # own convention (parity unpinned vs reference): slot k = f(psi^(2k+1))
+    f = O.fill_uniform(d, 11 + d)
+    F = O.crt(f, d)
+    psi = O.lib().lfo_pow(7, (P - 1) // (2 * d))
+    for k in [0, 1, d // 2, d - 1]:
+        x = O.lib().lfo_pow(psi, 2 * k + 1)
+        acc = 0
+        for c in reversed(f.tolist()):
+            acc = (acc * x + c) % P
+        assert int(F[k]) == acc
+    assert np.array_equal(O.icrt(F, d), f)
+    g = O.fill_uniform(d, 99 + d)
+    assert np.array_equal(O.icrt(O.slot_mul(F, O.crt(g, d), d), d), O.poly_mul(f, g, d))
+
+
+def test_gadget_kat():
+    k = KATS["gadget"]  # SR/balanced_decomposition/mod.rs:469-515
+    for v, digits in zip(k["input_scalars"], k["expected_digits"]):
+        elem = np.full(24, v, np.uint64)
+        out = O.gadget_decompose(elem, 24, k["b"], k["padding"]).reshape(k["padding"], 24)
+        assert all(int(out[i, 0]) == digits[i] and len(set(out[i].tolist())) == 1 for i in range(4))
+        assert np.array_equal(O.gadget_recompose(out.ravel(), 24, k["b"], k["padding"]), elem)
+
+
+@pytest.mark.parametrize("b", [2, 4, 8, 16, 32, 1 << 15])
+def test_decompose_balanced_properties(b):
+    # SR/balanced_decomposition/mod.rs:405-422: |digit| <= b/2 and recompose == v
+    rng = np.random.default_rng(b)
+    vals = [0, 1, P - 1, (P - 1) // 2, (P + 1) // 2, b // 2, P - b // 2] + \
+        [int(x) for x in rng.integers(0, 1 << 63, 40, dtype=np.uint64)]
+    for v in vals:
+        dig = O.decompose_balanced(v, b, 64)
+        for x in dig.tolist():
+            s = x - P if x > (P - 1) // 2 else x
+            assert abs(s) <= b // 2
+        r = 0
+        for x in reversed(dig.tolist()):
+            r = (r * b + x) % P
+        assert r == v
+
+
+def test_decompose_overflow_detected():
+    with pytest.raises(ValueError):
+        O.decompose_balanced((P - 1) // 2, 2, 8)
+
+
+def test_short_challenge_kat():
+    k = KATS["short_challenge"]  # CR/rings/goldilocks.rs:77-115
+    assert [int(x) for x in O.short_challenge(bytes(k["bytes"]), 24)] == k["coeffs"]
+
+
+def test_ajtai_closed_form():
+    k = KATS["ajtai_closed_form"]  # LF/commitment/commitment_scheme.rs:141-159
+    kappa, n = k["kappa"], 1 << 10  # n reduced from 2^15 for a fast CPU check
+    for d in (24, 16):
+        A = np.zeros((kappa, n, d), np.uint64)
+        vals = (np.arange(kappa)[:, None] * n + np.arange(n)[None, :]).astype(np.uint64)
+        if d == 24:
+            A[:, :, 0::3] = vals[:, :, None]
+        else:
+            A[:, :, :] = vals[:, :, None]
+        f = np.zeros((n, d), np.uint64)
+        if d == 24:
+            f[:, 0::3] = 2
+        else:
+            f[:, :] = 2
+        cm = O.ajtai_commit(A.ravel(), kappa, n, d, f.ravel()).reshape(kappa, d)
+        for i in range(kappa):
+            e = n * (2 * i * n + n - 1) % P
+            assert int(cm[i, 0]) == e and int(cm[i, -1 if d != 24 else 21]) == e
+
+
+def test_get_fhat_kat():
+    k = KATS["get_fhat"]  # LF/arith.rs:455-502
+    fc = np.array(k["f_coeffs"], np.uint64).ravel()
+    out = O.get_fhat_phi72(fc).reshape(3, 2, 8, 3)
+    for j in range(3):
+        for i in range(2):
+            assert [int(x) for x in out[j, i, :, 0]] == k["expected_mle_first_ntt_slots"][j][i]
+            assert not out[j, i, :, 1:].any()
+
+
+def test_poseidon2_mds_kats():
+    p2 = KATS["poseidon2"]
+    assert [int(x) for x in O.p2_mds16(p2["P1_mds"]["input"])] == p2["P1_mds"]["mds16"]
+    assert [int(x) for x in O.p2_mds16(p2["P2_initial_mds"]["input"])] == p2["P2_initial_mds"]["mds16"]
+
+
+def test_poseidon2_round0_kat():
+    k = KATS["poseidon2"]["P3_round0"]
+    s = O.p2_mds16(k["input"])
+    s = [pow((int(x) + c) % P, 7, P) for x, c in zip(s, k["round0_consts"])]
+    assert [int(x) for x in O.p2_mds16(s)] == k["mds_sbox_mds"]
+    # the round-0 constants are the ones the product uses (crypto_consts.rs:129-146)
+    txt = (Path(__file__).parents[1] / "oracle/p2_consts.inc").read_text()
+    first = txt.split("LF_P2_EXT_INIT")[1].split("ull")[0].split("0x")[1]
+    assert int(first, 16) == k["round0_consts"][0]
+
+
+def test_fill_uniform_deterministic():
+    a = O.fill_uniform(1000, 0x4C460003)
+    assert np.array_equal(a, O.fill_uniform(1000, 0x4C460003))
+    assert int(a.max()) < P and len(set(a.tolist())) == 1000
