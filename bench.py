@@ -1,0 +1,220 @@
+"""Benchmark: LatticeFold commit + fold steps per second on MI355X.
+
+A step = zkvm commit(z) (Witness::from_w_ccs + Ajtai A.f) followed by the
+commit+fold arithmetic of fold(): decompose accumulator and new witness into
+K=15 witnesses each, 28 batched Ajtai commitments, y_0 fix-ups, f_0 / cm_0 linear
+fold with 30 short challenges, Witness::from_f(f_0). Inputs are synthetic
+(seeded SplitMix64, SURVEY.md §8d seeds) and resident in HBM before timing.
+
+Default workload (BASELINE.json configs[2], "Ajtai commit + single LatticeFold
+step on 2^14 synthetic CCS witnesses", at the metric's d=1024): ring
+Fq[X]/(X^1024+1), w_ccs = 2^14 ring elements, kappa = 32, B=2^15, L=5, K=15.
+
+Multi-GPU (torchrun, one rank per GPU): independent steps per rank (weak
+scaling); at the end of the timed batch the ranks' folded accumulators
+(cm_0, f_0) are reduced mod p over RCCL (latticeum_amd.dist).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+SEED_W = 0x4C460003
+SEED_A = 0x4C460004
+SEED_RHO = 0x4C460005
+SEED_ACC = 0x4C460006
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--d", type=int, default=1024)
+    ap.add_argument("--w", type=int, default=1 << 14, help="w_ccs length W (ring elements)")
+    ap.add_argument("--kappa", type=int, default=32)
+    ap.add_argument("--cpu-baseline", dest="cpu", action="store_true", default=True)
+    ap.add_argument("--no-cpu-baseline", dest="cpu", action="store_false")
+    ap.add_argument("--cpu-w", type=int, default=0, help="W of the CPU baseline sample (0 = auto)")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    return ap.parse_args()
+
+
+def algorithmic_bytes(d, W, kappa, L=5, K=15):
+    """SURVEY.md §8d bytes/step and the batched-Ajtai launch bytes."""
+    E, N = 8 * d, W * L
+    step = (E * (W + 3 * N + kappa * N + kappa) + 2 * E * (N + K * (2 * N + W))
+            + E * (kappa * N + 2 * (K - 1) * N + 2 * (K - 1) * kappa) + E * (2 * K * N + N)
+            + E * (2 * N + W))
+    nvec = 2 * (K - 1)
+    ajtai_batched = E * (kappa * N + nvec * N + nvec * kappa)
+    ajtai_single = E * (kappa * N + N + kappa)
+    return step, ajtai_batched, ajtai_single
+
+
+def cpu_baseline(d, W_full, kappa, cpu_w, threads):
+    """Time the oracle's restatement of the same step on host cores (bounded sample)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle as O
+
+    B, L, bs, K = 1 << 15, 5, 2, 15
+    W = cpu_w
+    N = W * L
+    A = O.fill_uniform(kappa * N * d, SEED_A)
+    w_ccs = O.fill_uniform(W * d, SEED_W)
+    acc_fc, acc_f = O.witness_from_w_ccs(O.fill_uniform(W * d, SEED_ACC), d, B, L, threads)
+    acc_cm = O.ajtai_commit(A, kappa, N, d, acc_f, 1, threads)
+    rho = O.crt(O.fill_uniform(2 * K * d, SEED_RHO), d)
+    t0 = time.perf_counter()
+    fc, f = O.witness_from_w_ccs(w_ccs, d, B, L, threads)
+    cm = O.ajtai_commit(A, kappa, N, d, f, 1, threads)
+    sides = [O.decompose_witness(x, d, B, L, bs, K, threads) for x in (acc_fc, fc)]
+    vecs = np.concatenate([s[1].reshape(K, N * d)[1:] for s in sides]).ravel()
+    ycat = O.ajtai_commit(A, kappa, N, d, vecs, 2 * (K - 1), threads).reshape(2, K - 1, kappa * d)
+    ys = []
+    for s, c in enumerate((acc_cm, cm)):
+        y = np.zeros((K, kappa * d), np.uint64)
+        y[1:] = ycat[s]
+        ys.append(O.commit_witnesses_y0(c, y.ravel(), kappa, d, bs, K))
+    f0 = O.fold_f0(rho, np.concatenate([s[1] for s in sides]), 2 * K, N, d, threads)
+    O.fold_cm0(rho, np.concatenate(ys), 2 * K, kappa, d)
+    O.witness_from_f(f0, d, B, L, threads)
+    dt = time.perf_counter() - t0
+    steps_per_s = 1.0 / (dt * W_full / W)  # every stage is linear in W
+    return {"value": steps_per_s, "unit": "fold-steps/s", "cores": threads, "kind": "port",
+            "sample": f"1 full step at W={W} (1/{W_full // W} of W={W_full}), d={d}, kappa={kappa}, "
+                      f"{dt:.2f} s on {threads} threads; scaled linearly in W"}
+
+
+def main():
+    args = parse()
+    import torch
+    import latticeum_amd as LA
+    from latticeum_amd import dist as LD
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    pg = LD.init(world)
+
+    d, W, kappa = args.d, args.w, args.kappa
+    pr = LA.goldilocks_dp(d)
+    K, L = pr.K, pr.L
+    N = W * L
+    ctx = LA.Context(local)
+    stream = torch.cuda.current_stream()
+    ctx.set_stream(stream.cuda_stream)
+
+    i64 = dict(dtype=torch.int64, device=f"cuda:{local}")
+    z = lambda n: torch.empty(n, **i64)
+    A = z(kappa * N * d)
+    ctx.dev_fill_uniform(A, SEED_A)
+    sch = LA.AjtaiCommitmentScheme(ctx, device_tensor=A, kappa=kappa, ncols=N, d=d)
+    w_ccs = z(W * d)
+    ctx.dev_fill_uniform(w_ccs, SEED_W + 7919 * rank)
+    # accumulator side: a previous witness built the reference way (from_w_ccs + commit)
+    acc_w = z(W * d)
+    ctx.dev_fill_uniform(acc_w, SEED_ACC)
+    acc_fc, acc_f, acc_cm = z(N * d), z(N * d), z(kappa * d)
+    ctx.check(ctx.lib.lf_dev_witness_from_w_ccs(ctx.h, LA._lib.C.byref(pr), acc_w.data_ptr(), W,
+                                                acc_fc.data_ptr(), acc_f.data_ptr()))
+    ctx.dev_ajtai_commit(sch, [acc_f], acc_cm)
+    del acc_w, acc_f
+    # rho: 29 short challenges from seeded bytes (CR/rings/goldilocks.rs:41-67) + ONE, NTT form
+    rng = np.random.default_rng(SEED_RHO)
+    rc = [LA.short_challenge(rng.integers(0, 256, 3 * d // 4, dtype=np.uint8).tobytes(), d)
+          for _ in range(2 * K - 1)]
+    one = np.zeros(d, np.uint64)
+    one[0] = 1
+    rho = torch.from_numpy(np.concatenate(rc + [one]).view(np.int64)).to(f"cuda:{local}")
+    ctx.dev_crt(rho, d)
+
+    keep = {
+        "w_ccs": w_ccs, "acc_cm": acc_cm, "acc_f_coeff": acc_fc, "rho": rho,
+        "f_coeff": z(N * d), "f": z(N * d), "cm": z(kappa * d),
+        "fk_coeff": [z(K * N * d) for _ in range(2)], "fk": [z(K * N * d) for _ in range(2)],
+        "wk": [z(K * W * d) for _ in range(2)], "y": [z(K * kappa * d) for _ in range(2)],
+        "f0": z(N * d), "f0_coeff": z(N * d), "w_ccs0": z(W * d), "cm0": z(kappa * d),
+    }
+    bufs = LA.LfFoldStepBufs()
+    for k, v in keep.items():
+        if isinstance(v, list):
+            for s in range(2):
+                getattr(bufs, k)[s] = v[s].data_ptr()
+        else:
+            setattr(bufs, k, v.data_ptr())
+    ctx.reserve(kappa, N, d, 2 * (K - 1))
+    ctx.sync()
+
+    for _ in range(args.warmup):
+        ctx.dev_fold_step(sch, pr, W, bufs)
+    ctx.sync()
+    reducer = LD.AccumulatorReducer(ctx, world, [keep["cm0"], keep["f0"]]) if world > 1 else None
+
+    ctx.kernel_timing(True)
+    LD.barrier(pg)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.dev_fold_step(sch, pr, W, bufs)
+    if reducer is not None:
+        reducer.reduce()  # RCCL reduce of the folded accumulators (once per timed batch)
+    torch.cuda.synchronize()
+    LD.barrier(pg)
+    dt = time.perf_counter() - t0
+    ctx.sync()  # surfaces any decomposition overflow
+    dt_max = LD.max_over_ranks(pg, dt)
+    nvec = 2 * (K - 1)
+    ms_b, n_b = ctx.kernel_stats(nvec)
+    ms_1, n_1 = ctx.kernel_stats(1)
+    ctx.kernel_timing(False)
+
+    step_bytes, aj_bytes, aj1_bytes = algorithmic_bytes(d, W, kappa, L, K)
+    avg_ms = ms_b / max(n_b, 1)
+    achieved = aj_bytes / (avg_ms * 1e-3) / 1e9 if n_b else 0.0
+    out = None
+    if rank == 0:
+        cpu = None
+        if args.cpu and world == 1:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            cpu_w = args.cpu_w or max(1, min(W, 64 if d >= 1024 else 2048))
+            cpu = cpu_baseline(d, W, kappa, cpu_w, threads)
+        value = world * args.steps / dt_max
+        out = {
+            "metric": "fold-steps/sec (Ajtai commit+fold) at d=1024",
+            "value": value, "unit": "fold-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt_max / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64 (Goldilocks mod-p integer)",
+            "data": "synthetic (seeded SplitMix64 inputs, random Ajtai matrix)",
+            "config": {"workload": f"commit+fold step, X^{d}+1 ring, w_ccs W={W}, N={N}, kappa={kappa}, "
+                                   f"B=2^15 L=5 K=15, 28 batched Ajtai commits",
+                       "d": d, "W": W, "N": N, "kappa": kappa,
+                       "parallelism": f"{world} independent step streams (weak)"},
+            "hbm_gbs_step_algorithmic": step_bytes * value / world / 1e9,
+            "roofline": {"kernel": "k_ajtai_nega (batched, 28 vectors)" if d != 24 else "k_ajtai_phi72",
+                         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "avg_launch_ms": avg_ms, "launches": n_b,
+                         "bytes_per_launch": aj_bytes,
+                         "single_commit_avg_ms": ms_1 / max(n_1, 1)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    LD.finalize(pg)
+    return out
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,226 @@
+/*
+ * lf.h -- C ABI of latticeum_amd: the MI355X (gfx950) implementation of the
+ * LatticeFold commit+fold hot path of Nesquiko/Latticeum.
+ *
+ * Reference interfaces replaced (paths under latticeum/crates/):
+ *   stark-rings/crates/ring/src/cyclotomic_ring/ring_config.rs:11-35
+ *       CyclotomicConfig::{crt_in_place, icrt_in_place}      -> lf_crt / lf_icrt
+ *   stark-rings/crates/ring/src/cyclotomic_ring/crt.rs:10-45
+ *       CRT::elementwise_crt / ICRT::elementwise_icrt          -> lf_crt / lf_icrt (batched)
+ *   stark-rings/crates/ring/src/cyclotomic_ring/ntt_form.rs:159-189
+ *       RqNTT Mul / MulUnchecked                               -> lf_ring_mul
+ *   latticefold/src/commitment/commitment_scheme.rs:23-78
+ *       AjtaiCommitmentScheme::{new, commit, commit_ntt, kappa, width}
+ *                                                              -> lf_ajtai_*
+ *   latticefold/src/arith.rs:230-338
+ *       Witness::{from_w_ccs, from_f, from_f_coeff}            -> lf_witness_*
+ *   latticefold/src/nifs/decomposition.rs:162-201
+ *       decompose_witness / commit_witnesses                   -> lf_decompose_witness,
+ *                                                                 lf_dev_commit_y0
+ *   latticefold/src/nifs/folding.rs:258-268, folding/utils.rs:456-517
+ *       compute_f_0 / cm_0                                     -> lf_dev_fold
+ *   cyclotomic-rings/src/rings/goldilocks.rs:41-67
+ *       short_challenge_from_random_bytes                      -> lf_short_challenge
+ *   zkvm/src/poseidon2.rs:100-235
+ *       WideZkVMPoseidon2Perm::permute_mut, hash_iter          -> lf_poseidon2_permute,
+ *                                                                 lf_hash_iter
+ *   zkvm/src/fiat_shamir.rs:20-114  Poseidon2Transcript         -> lf_transcript_*
+ *   zkvm/src/main.rs:348-367  commit()                          -> lf_commit
+ *   zkvm/src/main.rs:380-404  fold() (its commit+fold arithmetic) -> lf_fold_hot /
+ *                                                                 lf_dev_fold_step
+ *
+ * Data: a ring element is d u64 (AoS). d = 24 is the reference's Goldilocks
+ * ring Fq[X]/(X^24 - X^12 + 1); its NTT form is 8 Fq3 slots laid out
+ * [s0.c0, s0.c1, s0.c2, s1.c0, ...] exactly as the reference's in-place CRT
+ * (crt.rs:53-77). d in {16, 64, 256, 1024, 4096} selects Fq[X]/(X^d + 1)
+ * (no reference analogue; NTT slot k = f(psi^(2k+1)), psi = 7^((p-1)/2d)).
+ * Host-buffer calls take repr = LF_REPR_MONTGOMERY when the buffers are raw
+ * ark-ff Fp64 limbs (zero-copy from Rust Vec<RqNTT>), LF_REPR_CANONICAL
+ * otherwise. Device (lf_dev_*) calls are canonical and asynchronous on the
+ * context stream; decomposition overflow is reported by lf_ctx_sync().
+ *
+ * Threading: a context is single-threaded (like the reference's &mut
+ * transcript); distinct contexts may be used from distinct threads.
+ */
+#ifndef LATTICEUM_AMD_LF_H
+#define LATTICEUM_AMD_LF_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct lf_ctx lf_ctx;
+typedef struct lf_ajtai lf_ajtai;
+typedef struct lf_transcript lf_transcript;
+
+enum lf_status {
+  LF_OK = 0,
+  LF_ERR_INVALID_ARG = 1,
+  LF_ERR_UNSUPPORTED_RING = 2,
+  LF_ERR_WRONG_WITNESS_LENGTH = 3,    /* CommitmentError::WrongWitnessLength (commitment.rs:16-17) */
+  LF_ERR_WRONG_COMMITMENT_LENGTH = 4, /* CommitmentError::WrongCommitmentLength (commitment.rs:19-20) */
+  LF_ERR_WRONG_AJTAI_DIMENSIONS = 5,  /* CommitmentError::WrongAjtaiMatrixDimensions (:22-25) */
+  LF_ERR_DECOMPOSITION_OVERFLOW = 6,  /* value needs more digits than padding (reference panics) */
+  LF_ERR_INCORRECT_LENGTH = 7,        /* Decomposition/FoldingError::IncorrectLength (nifs/error.rs) */
+  LF_ERR_CHALLENGE_BYTES = 8,         /* ChallengeSetError::TooFewBytes */
+  LF_ERR_DEVICE = 9,                  /* HIP runtime error (see lf_ctx_last_error) */
+  LF_ERR_OUT_OF_MEMORY = 10
+};
+enum lf_repr { LF_REPR_CANONICAL = 0, LF_REPR_MONTGOMERY = 1 };
+
+/* DecompositionParams (latticefold/src/decomposition_parameters.rs:11-20).
+ * The device path needs B and b_small to be powers of two (GoldiLocksDP is). */
+typedef struct {
+  int d;
+  uint64_t B;
+  int L;
+  uint64_t b_small;
+  int K;
+} lf_params;
+
+/* zkvm GoldiLocksDP (zkvm/src/ccs.rs:26-34): B = 2^15, L = 5, B_SMALL = 2, K = 15 */
+lf_params lf_goldilocks_dp(int d);
+
+/* ------------------------------------------------------------ context */
+int lf_ctx_create(int device, lf_ctx **out);
+void lf_ctx_destroy(lf_ctx *ctx);
+const char *lf_status_string(int status);
+const char *lf_ctx_last_error(const lf_ctx *ctx);
+/* stream used by lf_dev_* (hipStream_t); NULL restores the context's own */
+int lf_ctx_set_stream(lf_ctx *ctx, void *hip_stream);
+void *lf_ctx_get_stream(const lf_ctx *ctx);
+/* wait for the stream; returns LF_ERR_DECOMPOSITION_OVERFLOW (and clears it)
+ * if any device decomposition since the last sync ran out of digits */
+int lf_ctx_sync(lf_ctx *ctx);
+/* pre-size internal scratch so no allocation happens inside timed/captured work */
+int lf_ctx_reserve(lf_ctx *ctx, size_t kappa, size_t ncols, int d, int nvec);
+/* kernel timing: HIP events recorded on the stream around every Ajtai matvec
+ * kernel launch (the main kernel only, not its split-K reduction) */
+int lf_ctx_kernel_timing(lf_ctx *ctx, int enable);
+/* device ms summed over, and number of, timed Ajtai launches with nvec
+ * vectors (nvec = 0: all) since timing was enabled; synchronises the stream */
+int lf_ctx_kernel_stats(lf_ctx *ctx, int nvec, double *total_ms, long *count);
+
+/* ------------------------------------------------------------ host-buffer API (synchronous) */
+int lf_crt(lf_ctx *ctx, uint64_t *elems, size_t n, int d, int repr);
+int lf_icrt(lf_ctx *ctx, uint64_t *elems, size_t n, int d, int repr);
+int lf_ring_mul(lf_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t n, int d,
+                int repr);
+
+int lf_ajtai_create(lf_ctx *ctx, const uint64_t *A, size_t kappa, size_t ncols, int d, int repr,
+                    lf_ajtai **out);
+/* wraps a matrix already in device memory (canonical, AoS row-major); not copied */
+int lf_ajtai_create_device(lf_ctx *ctx, const uint64_t *A_dev, size_t kappa, size_t ncols, int d,
+                           lf_ajtai **out);
+void lf_ajtai_destroy(lf_ajtai *aj);
+size_t lf_ajtai_kappa(const lf_ajtai *aj);
+size_t lf_ajtai_width(const lf_ajtai *aj);
+int lf_ajtai_d(const lf_ajtai *aj);
+/* commit_ntt: f has f_len NTT elements (must equal width), cm receives kappa */
+int lf_ajtai_commit(lf_ctx *ctx, const lf_ajtai *aj, const uint64_t *f, size_t f_len, uint64_t *cm,
+                    int repr);
+
+int lf_witness_from_w_ccs(lf_ctx *ctx, const lf_params *pr, const uint64_t *w_ccs, size_t W,
+                          uint64_t *f_coeff, uint64_t *f, int repr);
+int lf_witness_from_f(lf_ctx *ctx, const lf_params *pr, const uint64_t *f, size_t N,
+                      uint64_t *f_coeff, uint64_t *w_ccs, int repr);
+/* f_coeff (N) -> f_coeff_k [K][N], f_k [K][N], w_ccs_k [K][N/L] */
+int lf_decompose_witness(lf_ctx *ctx, const lf_params *pr, const uint64_t *f_coeff, size_t N,
+                         uint64_t *f_coeff_k, uint64_t *f_k, uint64_t *w_ccs_k, int repr);
+
+/* zkvm commit(): z = [x_ccs (l) | 1 | w_ccs (W)] NTT elements; outputs the new
+ * witness (f_coeff, f: W*L each) and the CCCS commitment cm (kappa). */
+int lf_commit(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, const uint64_t *z, size_t z_len,
+              size_t l, uint64_t *f_coeff, uint64_t *f, uint64_t *cm, int repr);
+
+/* The commit+fold arithmetic of zkvm fold() for one step, given the folding
+ * challenges rho (2K NTT elements, rho[2K-1] = ONE as get_rhos produces):
+ *   decompose (acc, w_acc) and (cm_i, w_i) into K witnesses each, commit 2(K-1)
+ *   of them, y_0 = cm - sum b^k y_k, f_0 = sum rho_i f_i, cm_0 = sum rho_i y_i,
+ *   and Witness::from_f(f_0).
+ * Outputs: y (2K x kappa), f0 / f0_coeff (N), w_ccs0 (N/L), cm0 (kappa). */
+int lf_fold_hot(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, const uint64_t *acc_cm,
+                const uint64_t *acc_f_coeff, const uint64_t *cm_i, const uint64_t *wi_f_coeff, size_t N,
+                const uint64_t *rho, uint64_t *y, uint64_t *f0, uint64_t *f0_coeff, uint64_t *w_ccs0,
+                uint64_t *cm0, int repr);
+
+/* short_challenge_from_random_bytes: 3d/4 bytes -> d coefficients in [-32, 32) */
+int lf_short_challenge(const uint8_t *bytes, size_t nbytes, int d, uint64_t *coeffs);
+/* width-16 Poseidon2 permutation of n independent states (16 canonical u64 each) */
+int lf_poseidon2_permute(lf_ctx *ctx, uint64_t *states, size_t n);
+
+/* ------------------------------------------------------------ device-resident API (async) */
+int lf_dev_crt(lf_ctx *ctx, uint64_t *elems, size_t n, int d);
+int lf_dev_icrt(lf_ctx *ctx, uint64_t *elems, size_t n, int d);
+int lf_dev_ring_mul(lf_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t n, int d);
+int lf_dev_to_montgomery(lf_ctx *ctx, uint64_t *x, size_t n);
+int lf_dev_from_montgomery(lf_ctx *ctx, uint64_t *x, size_t n);
+int lf_dev_witness_from_w_ccs(lf_ctx *ctx, const lf_params *pr, const uint64_t *w_ccs, size_t W,
+                              uint64_t *f_coeff, uint64_t *f);
+int lf_dev_witness_from_f(lf_ctx *ctx, const lf_params *pr, const uint64_t *f, size_t N,
+                          uint64_t *f_coeff, uint64_t *w_ccs);
+int lf_dev_decompose_witness(lf_ctx *ctx, const lf_params *pr, const uint64_t *f_coeff, size_t N,
+                             uint64_t *f_coeff_k, uint64_t *f_k, uint64_t *w_ccs_k);
+/* nvec (<= 32) vectors of width() NTT elements each -> cm [nvec][kappa] */
+int lf_dev_ajtai_commit(lf_ctx *ctx, const lf_ajtai *aj, const uint64_t *const *f_vecs, int nvec,
+                        uint64_t *cm);
+/* y [K][kappa]: y[0] = cm - sum_{k>=1} b_small^k y[k] */
+int lf_dev_commit_y0(lf_ctx *ctx, const lf_params *pr, const uint64_t *cm, uint64_t *y, size_t kappa);
+/* out[j] = sum_{i<nwit} rho_i (.) x_i[j], j < n ring elements (nwit <= 32) */
+int lf_dev_fold(lf_ctx *ctx, int d, const uint64_t *rho, const uint64_t *const *x, int nwit, size_t n,
+                uint64_t *out);
+
+/* device buffers of one commit+fold step (all canonical, caller-allocated) */
+typedef struct {
+  /* inputs */
+  const uint64_t *w_ccs;       /* W: the new CCS witness (commit(z) input, NTT form) */
+  const uint64_t *acc_cm;      /* kappa: accumulator commitment (LCCCS.cm) */
+  const uint64_t *acc_f_coeff; /* N: accumulator witness f_coeff */
+  const uint64_t *rho;         /* 2K NTT elements */
+  /* outputs */
+  uint64_t *f_coeff, *f;       /* N each: Witness::from_w_ccs(w_ccs) */
+  uint64_t *cm;                /* kappa: CCCS.cm = A f */
+  uint64_t *fk_coeff[2];       /* [K][N] per side (0 = accumulator, 1 = new instance) */
+  uint64_t *fk[2];             /* [K][N] */
+  uint64_t *wk[2];             /* [K][W] */
+  uint64_t *y[2];              /* [K][kappa] decomposition commitments */
+  uint64_t *f0, *f0_coeff;     /* N each: folded witness */
+  uint64_t *w_ccs0;            /* W */
+  uint64_t *cm0;               /* kappa */
+} lf_fold_step_bufs;
+/* commit(z) followed by the commit+fold arithmetic of fold(), all on device */
+int lf_dev_fold_step(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, size_t W,
+                     const lf_fold_step_bufs *b);
+
+int lf_dev_poseidon2_permute(lf_ctx *ctx, uint64_t *states, size_t n);
+/* synthetic inputs: element i = SplitMix64(seed, i) re-mixed until < p */
+int lf_dev_fill_uniform(lf_ctx *ctx, uint64_t *out, size_t n, uint64_t seed);
+/* out[c] = sum_r in[r][c] mod p  (reduce of all-gathered accumulators) */
+int lf_dev_modp_sum(lf_ctx *ctx, const uint64_t *in, int nparts, size_t len, uint64_t *out);
+
+/* RCCL transport of field vectors: RCCL sums u64 modulo 2^64, so vectors are
+ * all-reduced as 32-bit limbs (lo, hi as u64; <= 2^8 ranks) and joined mod p */
+int lf_dev_limb_split(lf_ctx *ctx, const uint64_t *x, size_t n, uint64_t *lo, uint64_t *hi);
+int lf_dev_limb_join(lf_ctx *ctx, const uint64_t *lo, const uint64_t *hi, size_t n, uint64_t *out);
+
+/* ------------------------------------------------------------ host transcript (sequential) */
+lf_transcript *lf_transcript_new(void);
+void lf_transcript_free(lf_transcript *t);
+void lf_transcript_observe(lf_transcript *t, uint64_t v);
+uint64_t lf_transcript_sample(lf_transcript *t);
+/* Transcript::absorb of NTT ring elements: their base-field limbs observed as
+ * ark Montgomery u64s (fiat_shamir.rs:51-60). repr describes `elems`. */
+void lf_transcript_absorb_ring(lf_transcript *t, const uint64_t *elems, size_t n, int d, int repr);
+void lf_transcript_get_challenge(lf_transcript *t, uint64_t out3[3]);
+void lf_transcript_squeeze_bytes(lf_transcript *t, uint8_t *out, size_t n);
+/* get_small_challenges: count short challenges in coefficient form (count x d) */
+int lf_transcript_get_short_challenges(lf_transcript *t, int d, size_t count, uint64_t *coeffs);
+/* WideZkVMPoseidon2::hash_iter (poseidon2.rs:206-235) */
+void lf_hash_iter(const uint64_t *in, size_t n, uint64_t out4[4]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,303 @@
+"""latticeum_amd -- MI355X-native LatticeFold commit+fold hot path.
+
+Thin Python view of the C ABI (include/lf.h). The names follow the reference
+(Nesquiko/Latticeum): ``AjtaiCommitmentScheme`` (latticefold
+commitment_scheme.rs), ``Witness.from_w_ccs / from_f`` (latticefold arith.rs),
+``commit`` / ``fold`` (zkvm main.rs:348,380), ``Poseidon2Transcript``
+(zkvm fiat_shamir.rs). Every operation runs through the HIP library; there is
+no CPU fallback, and constructing a ``Context`` fails without a GPU.
+
+Host arrays are numpy uint64 in AoS layout (``[n, d]`` ring elements). Device
+arrays are torch int64 tensors on a HIP device (bit patterns of u64).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import LfFoldStepBufs, LfParams, load
+
+P = (1 << 64) - (1 << 32) + 1
+REPR_CANONICAL = 0
+REPR_MONTGOMERY = 1
+SUPPORTED_D = (24, 16, 64, 256, 1024, 4096)
+
+
+class LfError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"lf error {code}: {msg}")
+        self.code = code
+
+
+def goldilocks_dp(d: int = 24) -> LfParams:
+    """zkvm GoldiLocksDP (zkvm/src/ccs.rs:26-34): B=2^15, L=5, B_SMALL=2, K=15."""
+    return load().lf_goldilocks_dp(d)
+
+
+def _u64(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint64))
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _dptr(t) -> int:
+    """device pointer of a torch tensor (or a raw int)."""
+    return t if isinstance(t, int) else t.data_ptr()
+
+
+class Context:
+    """One HIP device + stream (lf_ctx). Not thread-safe; one per thread."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        h = C.c_void_p()
+        rc = self.lib.lf_ctx_create(device, C.byref(h))
+        if rc != 0:
+            raise LfError(rc, f"lf_ctx_create(device={device}) failed: "
+                              f"{self.lib.lf_status_string(rc).decode()}")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.lf_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, rc: int):
+        if rc != 0:
+            msg = self.lib.lf_ctx_last_error(self.h).decode() or self.lib.lf_status_string(rc).decode()
+            raise LfError(rc, msg)
+
+    # ---------------------------------------------------------------- stream / timing
+    def set_stream(self, hip_stream: int | None):
+        self.check(self.lib.lf_ctx_set_stream(self.h, hip_stream))
+
+    def sync(self):
+        self.check(self.lib.lf_ctx_sync(self.h))
+
+    def reserve(self, kappa: int, ncols: int, d: int, nvec: int):
+        self.check(self.lib.lf_ctx_reserve(self.h, kappa, ncols, d, nvec))
+
+    def kernel_timing(self, enable: bool):
+        self.check(self.lib.lf_ctx_kernel_timing(self.h, int(enable)))
+
+    def kernel_stats(self, nvec: int = 0):
+        ms, cnt = C.c_double(), C.c_long()
+        self.check(self.lib.lf_ctx_kernel_stats(self.h, nvec, C.byref(ms), C.byref(cnt)))
+        return ms.value, cnt.value
+
+    # ---------------------------------------------------------------- host-buffer API
+    def crt(self, elems, d: int, repr: int = REPR_CANONICAL) -> np.ndarray:
+        x = _u64(elems).copy()
+        self.check(self.lib.lf_crt(self.h, _ptr(x), x.size // d, d, repr))
+        return x
+
+    def icrt(self, elems, d: int, repr: int = REPR_CANONICAL) -> np.ndarray:
+        x = _u64(elems).copy()
+        self.check(self.lib.lf_icrt(self.h, _ptr(x), x.size // d, d, repr))
+        return x
+
+    def ring_mul(self, a, b, d: int, repr: int = REPR_CANONICAL) -> np.ndarray:
+        a, b = _u64(a), _u64(b)
+        out = np.empty_like(a)
+        self.check(self.lib.lf_ring_mul(self.h, _ptr(a), _ptr(b), _ptr(out), a.size // d, d, repr))
+        return out
+
+    def witness_from_w_ccs(self, w_ccs, params: LfParams, repr: int = REPR_CANONICAL):
+        w = _u64(w_ccs)
+        d, L = params.d, params.L
+        W = w.size // d
+        fc = np.empty(W * L * d, np.uint64)
+        f = np.empty(W * L * d, np.uint64)
+        self.check(self.lib.lf_witness_from_w_ccs(self.h, C.byref(params), _ptr(w), W, _ptr(fc), _ptr(f), repr))
+        return fc, f
+
+    def witness_from_f(self, f, params: LfParams, repr: int = REPR_CANONICAL):
+        x = _u64(f)
+        d, L = params.d, params.L
+        N = x.size // d
+        fc = np.empty(N * d, np.uint64)
+        w = np.empty((N // L) * d, np.uint64)
+        self.check(self.lib.lf_witness_from_f(self.h, C.byref(params), _ptr(x), N, _ptr(fc), _ptr(w), repr))
+        return fc, w
+
+    def decompose_witness(self, f_coeff, params: LfParams, repr: int = REPR_CANONICAL):
+        x = _u64(f_coeff)
+        d, L, K = params.d, params.L, params.K
+        N = x.size // d
+        fck = np.empty(K * N * d, np.uint64)
+        fk = np.empty(K * N * d, np.uint64)
+        wk = np.empty(K * (N // L) * d, np.uint64)
+        self.check(self.lib.lf_decompose_witness(self.h, C.byref(params), _ptr(x), N, _ptr(fck),
+                                                 _ptr(fk), _ptr(wk), repr))
+        return fck, fk, wk
+
+    def commit(self, scheme: "AjtaiCommitmentScheme", z, l: int, params: LfParams,
+               repr: int = REPR_CANONICAL):
+        """zkvm commit() (main.rs:348-367): returns (f_coeff, f, cm)."""
+        zz = _u64(z)
+        d = params.d
+        N = scheme.width
+        fc = np.empty(N * d, np.uint64)
+        f = np.empty(N * d, np.uint64)
+        cm = np.empty(scheme.kappa * d, np.uint64)
+        self.check(self.lib.lf_commit(self.h, scheme.h, C.byref(params), _ptr(zz), zz.size // d, l,
+                                      _ptr(fc), _ptr(f), _ptr(cm), repr))
+        return fc, f, cm
+
+    def fold_hot(self, scheme: "AjtaiCommitmentScheme", params: LfParams, acc_cm, acc_f_coeff,
+                 cm_i, wi_f_coeff, rho, repr: int = REPR_CANONICAL) -> dict:
+        """commit+fold arithmetic of zkvm fold() for one step (see lf.h lf_fold_hot)."""
+        d, K, L = params.d, params.K, params.L
+        a_cm, a_fc, c_i, w_fc, r = map(_u64, (acc_cm, acc_f_coeff, cm_i, wi_f_coeff, rho))
+        N = a_fc.size // d
+        kd = scheme.kappa * d
+        out = {
+            "y": np.empty(2 * K * kd, np.uint64), "f0": np.empty(N * d, np.uint64),
+            "f0_coeff": np.empty(N * d, np.uint64), "w_ccs0": np.empty((N // L) * d, np.uint64),
+            "cm0": np.empty(kd, np.uint64),
+        }
+        self.check(self.lib.lf_fold_hot(
+            self.h, scheme.h, C.byref(params), _ptr(a_cm), _ptr(a_fc), _ptr(c_i), _ptr(w_fc), N,
+            _ptr(r), _ptr(out["y"]), _ptr(out["f0"]), _ptr(out["f0_coeff"]), _ptr(out["w_ccs0"]),
+            _ptr(out["cm0"]), repr))
+        return out
+
+    def poseidon2_permute(self, states) -> np.ndarray:
+        s = _u64(states).copy()
+        self.check(self.lib.lf_poseidon2_permute(self.h, _ptr(s), s.size // 16))
+        return s
+
+    # ---------------------------------------------------------------- device API (torch tensors)
+    def dev_crt(self, t, d: int):
+        self.check(self.lib.lf_dev_crt(self.h, _dptr(t), t.numel() // d, d))
+
+    def dev_icrt(self, t, d: int):
+        self.check(self.lib.lf_dev_icrt(self.h, _dptr(t), t.numel() // d, d))
+
+    def dev_fill_uniform(self, t, seed: int):
+        self.check(self.lib.lf_dev_fill_uniform(self.h, _dptr(t), t.numel(), seed))
+
+    def dev_ajtai_commit(self, scheme: "AjtaiCommitmentScheme", vecs, cm):
+        arr = (C.c_void_p * len(vecs))(*[_dptr(v) for v in vecs])
+        self.check(self.lib.lf_dev_ajtai_commit(self.h, scheme.h, arr, len(vecs), _dptr(cm)))
+
+    def dev_fold_step(self, scheme: "AjtaiCommitmentScheme", params: LfParams, W: int,
+                      bufs: LfFoldStepBufs):
+        self.check(self.lib.lf_dev_fold_step(self.h, scheme.h, C.byref(params), W, C.byref(bufs)))
+
+    def dev_poseidon2_permute(self, t):
+        self.check(self.lib.lf_dev_poseidon2_permute(self.h, _dptr(t), t.numel() // 16))
+
+    def dev_modp_sum(self, inp, nparts: int, length: int, out):
+        self.check(self.lib.lf_dev_modp_sum(self.h, _dptr(inp), nparts, length, _dptr(out)))
+
+
+class AjtaiCommitmentScheme:
+    """latticefold commitment_scheme.rs:17-78 -- kappa x n Ajtai matrix (NTT form)."""
+
+    def __init__(self, ctx: Context, matrix=None, *, kappa: int | None = None, ncols: int | None = None,
+                 d: int | None = None, device_tensor=None, repr: int = REPR_CANONICAL):
+        self.ctx = ctx
+        h = C.c_void_p()
+        if device_tensor is not None:
+            self._keep = device_tensor
+            ctx.check(ctx.lib.lf_ajtai_create_device(ctx.h, _dptr(device_tensor), kappa, ncols, d, C.byref(h)))
+        else:
+            m = _u64(matrix)
+            kappa, ncols, d = (m.shape if m.ndim == 3 else (kappa, ncols, d))
+            ctx.check(ctx.lib.lf_ajtai_create(ctx.h, _ptr(m), kappa, ncols, d, repr, C.byref(h)))
+        self.h = h
+        self.kappa, self.width, self.d = kappa, ncols, d
+
+    def commit_ntt(self, f, repr: int = REPR_CANONICAL) -> np.ndarray:
+        x = _u64(f)
+        cm = np.empty(self.kappa * self.d, np.uint64)
+        self.ctx.check(self.ctx.lib.lf_ajtai_commit(self.ctx.h, self.h, _ptr(x), x.size // self.d,
+                                                    _ptr(cm), repr))
+        return cm
+
+    commit = commit_ntt
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.ctx.lib.lf_ajtai_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+class Poseidon2Transcript:
+    """zkvm fiat_shamir.rs:20-114 (host-side sequential sponge)."""
+
+    def __init__(self):
+        self.lib = load()
+        self.h = self.lib.lf_transcript_new()
+
+    def __del__(self):
+        try:
+            self.lib.lf_transcript_free(self.h)
+        except Exception:
+            pass
+
+    def observe(self, v: int):
+        self.lib.lf_transcript_observe(self.h, v)
+
+    def sample(self) -> int:
+        return self.lib.lf_transcript_sample(self.h)
+
+    def absorb_ring(self, elems, d: int, repr: int = REPR_CANONICAL):
+        x = _u64(elems)
+        self.lib.lf_transcript_absorb_ring(self.h, _ptr(x), x.size // d, d, repr)
+
+    def get_challenge(self):
+        out = np.zeros(3, np.uint64)
+        self.lib.lf_transcript_get_challenge(self.h, _ptr(out))
+        return out
+
+    def squeeze_bytes(self, n: int) -> bytes:
+        out = np.zeros(n, np.uint8)
+        self.lib.lf_transcript_squeeze_bytes(self.h, _ptr(out), n)
+        return out.tobytes()
+
+    def get_short_challenges(self, d: int, count: int) -> np.ndarray:
+        out = np.zeros(count * d, np.uint64)
+        rc = self.lib.lf_transcript_get_short_challenges(self.h, d, count, _ptr(out))
+        if rc:
+            raise LfError(rc, "get_short_challenges")
+        return out
+
+
+def short_challenge(bs: bytes, d: int = 24) -> np.ndarray:
+    """cyclotomic-rings goldilocks.rs:41-67."""
+    lib = load()
+    b = np.frombuffer(bytes(bs), np.uint8).copy()
+    out = np.zeros(d, np.uint64)
+    rc = lib.lf_short_challenge(_ptr(b), b.size, d, _ptr(out))
+    if rc:
+        raise LfError(rc, lib.lf_status_string(rc).decode())
+    return out
+
+
+def hash_iter(vals) -> np.ndarray:
+    """zkvm poseidon2.rs:206-235 WideZkVMPoseidon2::hash_iter."""
+    x = _u64(vals) if len(vals) else np.zeros(1, np.uint64)
+    out = np.zeros(4, np.uint64)
+    load().lf_hash_iter(_ptr(x), len(vals), _ptr(out))
+    return out
+
+
+__all__ = ["Context", "AjtaiCommitmentScheme", "Poseidon2Transcript", "LfParams", "LfFoldStepBufs",
+           "LfError", "goldilocks_dp", "short_challenge", "hash_iter", "P", "REPR_CANONICAL",
+           "REPR_MONTGOMERY", "load"]

@@ -1,0 +1,119 @@
+"""ctypes binding of the C ABI in include/lf.h (liblatticeum_amd.so, built in-tree).
+
+This module only loads the shared library and declares signatures; there is no
+Python compute fallback. Loading fails loudly if the library is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = PKG / "liblatticeum_amd.so"
+
+SZ, I, U64, VP = C.c_size_t, C.c_int, C.c_uint64, C.c_void_p
+U64P = C.POINTER(C.c_uint64)
+U8P = C.POINTER(C.c_uint8)
+
+
+class LfParams(C.Structure):
+    _fields_ = [("d", I), ("B", U64), ("L", I), ("b_small", U64), ("K", I)]
+
+
+class LfFoldStepBufs(C.Structure):
+    _fields_ = [
+        ("w_ccs", VP), ("acc_cm", VP), ("acc_f_coeff", VP), ("rho", VP),
+        ("f_coeff", VP), ("f", VP), ("cm", VP),
+        ("fk_coeff", VP * 2), ("fk", VP * 2), ("wk", VP * 2), ("y", VP * 2),
+        ("f0", VP), ("f0_coeff", VP), ("w_ccs0", VP), ("cm0", VP),
+    ]
+
+
+# every function exported by include/lf.h: name -> (restype, argtypes)
+SIGNATURES = {
+    "lf_goldilocks_dp": (LfParams, [I]),
+    "lf_ctx_create": (I, [I, C.POINTER(VP)]),
+    "lf_ctx_destroy": (None, [VP]),
+    "lf_status_string": (C.c_char_p, [I]),
+    "lf_ctx_last_error": (C.c_char_p, [VP]),
+    "lf_ctx_set_stream": (I, [VP, VP]),
+    "lf_ctx_get_stream": (VP, [VP]),
+    "lf_ctx_sync": (I, [VP]),
+    "lf_ctx_reserve": (I, [VP, SZ, SZ, I, I]),
+    "lf_ctx_kernel_timing": (I, [VP, I]),
+    "lf_ctx_kernel_stats": (I, [VP, I, C.POINTER(C.c_double), C.POINTER(C.c_long)]),
+    "lf_crt": (I, [VP, VP, SZ, I, I]),
+    "lf_icrt": (I, [VP, VP, SZ, I, I]),
+    "lf_ring_mul": (I, [VP, VP, VP, VP, SZ, I, I]),
+    "lf_ajtai_create": (I, [VP, VP, SZ, SZ, I, I, C.POINTER(VP)]),
+    "lf_ajtai_create_device": (I, [VP, VP, SZ, SZ, I, C.POINTER(VP)]),
+    "lf_ajtai_destroy": (None, [VP]),
+    "lf_ajtai_kappa": (SZ, [VP]),
+    "lf_ajtai_width": (SZ, [VP]),
+    "lf_ajtai_d": (I, [VP]),
+    "lf_ajtai_commit": (I, [VP, VP, VP, SZ, VP, I]),
+    "lf_witness_from_w_ccs": (I, [VP, C.POINTER(LfParams), VP, SZ, VP, VP, I]),
+    "lf_witness_from_f": (I, [VP, C.POINTER(LfParams), VP, SZ, VP, VP, I]),
+    "lf_decompose_witness": (I, [VP, C.POINTER(LfParams), VP, SZ, VP, VP, VP, I]),
+    "lf_commit": (I, [VP, VP, C.POINTER(LfParams), VP, SZ, SZ, VP, VP, VP, I]),
+    "lf_fold_hot": (I, [VP, VP, C.POINTER(LfParams), VP, VP, VP, VP, SZ, VP, VP, VP, VP, VP, VP, I]),
+    "lf_short_challenge": (I, [VP, SZ, I, VP]),
+    "lf_poseidon2_permute": (I, [VP, VP, SZ]),
+    "lf_dev_crt": (I, [VP, VP, SZ, I]),
+    "lf_dev_icrt": (I, [VP, VP, SZ, I]),
+    "lf_dev_ring_mul": (I, [VP, VP, VP, VP, SZ, I]),
+    "lf_dev_to_montgomery": (I, [VP, VP, SZ]),
+    "lf_dev_from_montgomery": (I, [VP, VP, SZ]),
+    "lf_dev_witness_from_w_ccs": (I, [VP, C.POINTER(LfParams), VP, SZ, VP, VP]),
+    "lf_dev_witness_from_f": (I, [VP, C.POINTER(LfParams), VP, SZ, VP, VP]),
+    "lf_dev_decompose_witness": (I, [VP, C.POINTER(LfParams), VP, SZ, VP, VP, VP]),
+    "lf_dev_ajtai_commit": (I, [VP, VP, C.POINTER(VP), I, VP]),
+    "lf_dev_commit_y0": (I, [VP, C.POINTER(LfParams), VP, VP, SZ]),
+    "lf_dev_fold": (I, [VP, I, VP, C.POINTER(VP), I, SZ, VP]),
+    "lf_dev_fold_step": (I, [VP, VP, C.POINTER(LfParams), SZ, C.POINTER(LfFoldStepBufs)]),
+    "lf_dev_poseidon2_permute": (I, [VP, VP, SZ]),
+    "lf_dev_fill_uniform": (I, [VP, VP, SZ, U64]),
+    "lf_dev_modp_sum": (I, [VP, VP, I, SZ, VP]),
+    "lf_dev_limb_split": (I, [VP, VP, SZ, VP, VP]),
+    "lf_dev_limb_join": (I, [VP, VP, VP, SZ, VP]),
+    "lf_transcript_new": (VP, []),
+    "lf_transcript_free": (None, [VP]),
+    "lf_transcript_observe": (None, [VP, U64]),
+    "lf_transcript_sample": (U64, [VP]),
+    "lf_transcript_absorb_ring": (None, [VP, VP, SZ, I, I]),
+    "lf_transcript_get_challenge": (None, [VP, VP]),
+    "lf_transcript_squeeze_bytes": (None, [VP, VP, SZ]),
+    "lf_transcript_get_short_challenges": (I, [VP, I, SZ, VP]),
+    "lf_hash_iter": (None, [VP, SZ, VP]),
+}
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load liblatticeum_amd.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    # One HIP runtime per process: torch bundles libamdhip64.so.7 /
+    # libhsa-runtime64.so.1 (same SONAMEs as /opt/rocm). Importing torch first
+    # makes the dynamic linker bind this library to torch's already-loaded
+    # runtime, so device pointers, streams and events are shared with torch
+    # (which provides allocation and RCCL plumbing) instead of two HSA runtimes.
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # plain C-ABI use without torch binds /opt/rocm's runtime
+        pass
+    path = Path(os.environ.get("LATTICEUM_AMD_LIB", LIB_PATH))
+    if not path.exists():
+        raise ImportError(
+            f"latticeum_amd: native library {path} not found -- build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+    lib = C.CDLL(str(path))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib

@@ -1,0 +1,146 @@
+// gl.hpp -- Goldilocks field arithmetic for gfx950 (and the host side of the
+// library). p = 2^64 - 2^32 + 1 (reference: stark-rings goldilocks/mod.rs:16-27).
+//
+// Device representation is canonical u64 in [0, p). Internally a value may be
+// carried "weakly reduced" (any u64, congruent mod p); gl_canon() fixes it.
+// Reduction uses 2^64 == 2^32 - 1 and 2^96 == -1 (mod p), so a 128-bit product
+// folds into 64 bits with two 32-bit pieces and two carry fix-ups.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define LF_HD __host__ __device__ __forceinline__
+
+namespace gl {
+
+constexpr uint64_t P = 0xFFFFFFFF00000001ull;
+constexpr uint64_t EPS = 0xFFFFFFFFull;  // 2^64 mod p
+
+LF_HD uint64_t canon(uint64_t x) { return x >= P ? x - P : x; }
+
+LF_HD uint64_t add(uint64_t a, uint64_t b) {  // canonical in -> canonical out
+  uint64_t s = a + b;
+  // overflow past 2^64: add EPS (2^64 == EPS); result < p since a,b < p
+  s += (s < a) ? EPS : 0;
+  return canon(s);
+}
+
+LF_HD uint64_t sub(uint64_t a, uint64_t b) {
+  uint64_t d = a - b;
+  d -= (a < b) ? EPS : 0;  // borrow: d wrapped by +2^64 == +EPS, remove it
+  return d;
+}
+
+LF_HD uint64_t neg(uint64_t a) { return a ? P - a : 0; }
+
+LF_HD void mul_wide(uint64_t a, uint64_t b, uint64_t &lo, uint64_t &hi) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  lo = a * b;
+  hi = __umul64hi(a, b);
+#else
+  unsigned __int128 t = (unsigned __int128)a * b;
+  lo = (uint64_t)t;
+  hi = (uint64_t)(t >> 64);
+#endif
+}
+
+// x = lo + 2^64 hi  ->  weakly reduced u64 congruent to x
+LF_HD uint64_t reduce128(uint64_t lo, uint64_t hi) {
+  uint64_t hh = hi >> 32;
+  uint64_t hl = hi & EPS;
+  uint64_t t0 = lo - hh;
+  t0 -= (lo < hh) ? EPS : 0;            // 2^96 == -1
+  uint64_t t1 = (hl << 32) - hl;         // hl * (2^32 - 1), < 2^64
+  uint64_t r = t0 + t1;
+  r += (r < t1) ? EPS : 0;               // carry 2^64 == EPS
+  return r;
+}
+
+LF_HD uint64_t mul(uint64_t a, uint64_t b) {
+  uint64_t lo, hi;
+  mul_wide(a, b, lo, hi);
+  return canon(reduce128(lo, hi));
+}
+
+// multiply by 2^s, 0 <= s < 192, any u64 input; canonical output.
+// 2^96 == -1, so 2^s for s in [96,192) is -(2^(s-96)); 2^128 == -2^32.
+LF_HD uint64_t mul_pow2(uint64_t a, int s) {
+  bool negate = s >= 96;
+  if (negate) s -= 96;
+  uint64_t r;
+  if (s < 64) {
+    uint64_t lo = s ? (a << s) : a, hi = s ? (a >> (64 - s)) : 0;
+    r = canon(reduce128(lo, hi));
+  } else {  // a*2^s = (a<<t)*2^64 with t = s-64 < 32: limbs [0, lo, hi<2^32]
+    int t = s - 64;
+    uint64_t lo = t ? (a << t) : a, hi = t ? (a >> (64 - t)) : 0;
+    r = sub(canon(reduce128(0, lo)), canon(hi << 32));
+  }
+  return negate ? neg(r) : r;
+}
+
+LF_HD uint64_t pow(uint64_t a, uint64_t e) {
+  uint64_t r = 1;
+  while (e) {
+    if (e & 1) r = mul(r, a);
+    a = mul(a, a);
+    e >>= 1;
+  }
+  return r;
+}
+LF_HD uint64_t inv(uint64_t a) { return pow(a, P - 2); }
+
+// ark-ff Montgomery limb <-> canonical (R = 2^64 mod p = EPS)
+LF_HD uint64_t to_mont(uint64_t a) { return mul(a, EPS); }
+constexpr uint64_t R_INV = 0xFFFFFFFE00000001ull;  // (2^32 - 1)^-1 mod p
+LF_HD uint64_t from_mont(uint64_t m) { return mul(canon(m), R_INV); }
+
+// ---- Fq3 = Fq[u]/(u^3 - 2^40)  (reference goldilocks/mod.rs:34-54) ----
+LF_HD void fq3_mul(const uint64_t *a, const uint64_t *b, uint64_t *c) {
+  uint64_t a0 = a[0], a1 = a[1], a2 = a[2], b0 = b[0], b1 = b[1], b2 = b[2];
+  uint64_t t0 = add(mul(a1, b2), mul(a2, b1));
+  uint64_t c0 = add(mul(a0, b0), mul_pow2(t0, 40));
+  uint64_t c1 = add(add(mul(a0, b1), mul(a1, b0)), mul_pow2(mul(a2, b2), 40));
+  uint64_t c2 = add(add(mul(a0, b2), mul(a1, b1)), mul(a2, b0));
+  c[0] = c0;
+  c[1] = c1;
+  c[2] = c2;
+}
+
+// ---- lazy 128-bit multiply-accumulate: acc = sum of a_i*b_i as
+// (lo:64, hi:64, top:32) -- reduce once at the end ----
+struct Acc {
+  uint64_t lo, hi;
+  uint32_t top;
+};
+LF_HD void acc_zero(Acc &s) {
+  s.lo = 0;
+  s.hi = 0;
+  s.top = 0;
+}
+LF_HD void acc_mad(Acc &s, uint64_t a, uint64_t b) {
+  uint64_t lo, hi;
+  mul_wide(a, b, lo, hi);
+  uint64_t nlo = s.lo + lo;
+  hi += (nlo < lo) ? 1 : 0;  // hi <= 2^64-2 so no wrap
+  s.lo = nlo;
+  uint64_t nhi = s.hi + hi;
+  s.top += (nhi < hi) ? 1 : 0;
+  s.hi = nhi;
+}
+LF_HD void acc_add(Acc &s, uint64_t v) {
+  uint64_t nlo = s.lo + v;
+  uint64_t c = (nlo < v) ? 1 : 0;
+  s.lo = nlo;
+  uint64_t nhi = s.hi + c;
+  s.top += (nhi < c) ? 1 : 0;
+  s.hi = nhi;
+}
+// value = lo + 2^64 hi + 2^128 top;  2^128 == (2^64)^2 == EPS^2 == 2^64 - 2^33 + 1 == -2^32 (mod p)
+LF_HD uint64_t acc_reduce(const Acc &s) {
+  uint64_t r = canon(reduce128(s.lo, s.hi));
+  uint64_t t = canon(((uint64_t)s.top) << 32);
+  return sub(r, t);
+}
+
+}  // namespace gl

@@ -1,0 +1,854 @@
+// kernels.hip -- hand-written gfx950 kernels for the LatticeFold commit+fold
+// hot path. Data layout in HBM: AoS ring elements, d u64 each (d = 24 for
+// Phi_72 in the reference's in-place CRT layout [s0.c0, s0.c1, s0.c2, s1.c0, ..]
+// (stark-rings crt.rs:53-77), d = 4^k for the negacyclic rings), canonical
+// values. Every launcher returns hipError_t and takes the stream explicitly.
+#include "kernels.hpp"
+#include "ring.hpp"
+
+namespace lfk {
+
+using gl::Acc;
+
+// ============================================================ error flags
+// bit 0: a balanced decomposition needed more digits than provided
+// (the reference indexes out of bounds and panics:
+//  stark-rings balanced_decomposition/mod.rs:85-87)
+__device__ __forceinline__ void raise(int *err, int bit) {
+  if (err) atomicOr(err, bit);
+}
+
+// ============================================================ helpers
+__device__ __forceinline__ int64_t signed_rep(uint64_t v) {
+  // fq_convertible.rs:22-34: (q-1)/2 < v  ->  v - q  (fits in int64)
+  return v > (gl::P - 1) / 2 ? (int64_t)(v - gl::P) : (int64_t)v;
+}
+__device__ __forceinline__ uint64_t from_signed(int64_t x) {
+  return x < 0 ? gl::P - (uint64_t)(-x) : (uint64_t)x;
+}
+// one balanced digit step (balanced_decomposition/mod.rs:76-91) for b = 2^lb
+__device__ __forceinline__ int64_t bal_digit(int64_t &curr, int lb) {
+  const int64_t b = (int64_t)1 << lb, bh = b >> 1;
+  int64_t rem = curr % b;  // truncating, like Rust
+  int64_t q = curr / b;    // truncating
+  int64_t ar = rem < 0 ? -rem : rem;
+  if (ar <= bh) {
+    curr = q;
+    return rem;
+  }
+  // rounded_div(rem, b) = sign(rem) since b/2 < |rem| < b  (linear_algebra ops.rs:64-80)
+  int64_t sg = rem < 0 ? -1 : 1;
+  curr = q + sg;
+  return rem - sg * b;
+}
+
+// ============================================================ Phi_72 transforms
+// one thread per ring element; 16-B vector loads of the 192-B element
+template <bool FWD>
+__global__ void __launch_bounds__(256) k_phi72_transform(uint64_t *data, size_t n) {
+  size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  uint64_t c[24];
+  const ulonglong2 *src = reinterpret_cast<const ulonglong2 *>(data + e * 24);
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    ulonglong2 v = src[i];
+    c[2 * i] = v.x;
+    c[2 * i + 1] = v.y;
+  }
+  if (FWD)
+    ring::phi72_crt(c);
+  else
+    ring::phi72_icrt(c);
+  ulonglong2 *dst = reinterpret_cast<ulonglong2 *>(data + e * 24);
+#pragma unroll
+  for (int i = 0; i < 12; i++) dst[i] = make_ulonglong2(c[2 * i], c[2 * i + 1]);
+}
+
+// ============================================================ negacyclic transforms
+template <int D>
+struct NT {
+  static constexpr int T = D / 4 < 256 ? D / 4 : 256;  // threads per element
+};
+
+template <int D, bool FWD>
+__global__ void __launch_bounds__(NT<D>::T) k_nega_transform(uint64_t *data, size_t n,
+                                                            ring::NegaTables tb) {
+  constexpr int T = NT<D>::T;
+  __shared__ uint64_t buf[2][D];
+  const int tid = threadIdx.x;
+  for (size_t e = blockIdx.x; e < n; e += gridDim.x) {
+    uint64_t *g = data + e * D;
+#pragma unroll
+    for (int i = tid; i < D; i += T) {
+      uint64_t v = g[i];
+      buf[0][i] = FWD ? gl::mul(v, tb.twist[i]) : v;
+    }
+    __syncthreads();
+    uint64_t *r = ring::stockham4<D, T>(buf[0], buf[1], tb.roots, tid);
+#pragma unroll
+    for (int i = tid; i < D; i += T) g[i] = FWD ? r[i] : gl::mul(r[i], tb.twist[i]);
+    __syncthreads();
+  }
+}
+
+// ============================================================ slot-wise ring product
+__global__ void k_slot_mul_phi72(const uint64_t *a, const uint64_t *b, uint64_t *out, size_t nslots) {
+  size_t s = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (s >= nslots) return;
+  uint64_t x[3] = {a[3 * s], a[3 * s + 1], a[3 * s + 2]};
+  uint64_t y[3] = {b[3 * s], b[3 * s + 1], b[3 * s + 2]};
+  uint64_t z[3];
+  gl::fq3_mul(x, y, z);
+  out[3 * s] = z[0];
+  out[3 * s + 1] = z[1];
+  out[3 * s + 2] = z[2];
+}
+__global__ void k_slot_mul_nega(const uint64_t *a, const uint64_t *b, uint64_t *out, size_t n) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i < n) out[i] = gl::mul(a[i], b[i]);
+}
+
+// ============================================================ Montgomery edge
+__global__ void k_mont(uint64_t *x, size_t n, int to) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i < n) x[i] = to ? gl::to_mont(gl::canon(x[i])) : gl::from_mont(x[i]);
+}
+
+// ============================================================ Witness::from_w_ccs
+// LF/arith.rs:230-248: ICRT -> gadget_decompose(B, L) -> CRT.
+// Phi_72: one thread per w_ccs element, all 24 coefficients in registers.
+__global__ void __launch_bounds__(128) k_from_w_ccs_phi72(const uint64_t *w_ccs, size_t W, int lb,
+                                                         int L, uint64_t *f_coeff, uint64_t *f,
+                                                         int *err) {
+  size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (j >= W) return;
+  uint64_t c[24];
+  const ulonglong2 *src = reinterpret_cast<const ulonglong2 *>(w_ccs + j * 24);
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    ulonglong2 v = src[i];
+    c[2 * i] = v.x;
+    c[2 * i + 1] = v.y;
+  }
+  ring::phi72_icrt(c);
+  int64_t cur[24];
+#pragma unroll
+  for (int i = 0; i < 24; i++) cur[i] = signed_rep(c[i]);
+  for (int l = 0; l < L; l++) {
+#pragma unroll
+    for (int i = 0; i < 24; i++) c[i] = from_signed(bal_digit(cur[i], lb));
+    ulonglong2 *dc = reinterpret_cast<ulonglong2 *>(f_coeff + (j * L + l) * 24);
+#pragma unroll
+    for (int i = 0; i < 12; i++) dc[i] = make_ulonglong2(c[2 * i], c[2 * i + 1]);
+    ring::phi72_crt(c);
+    ulonglong2 *df = reinterpret_cast<ulonglong2 *>(f + (j * L + l) * 24);
+#pragma unroll
+    for (int i = 0; i < 12; i++) df[i] = make_ulonglong2(c[2 * i], c[2 * i + 1]);
+  }
+  bool bad = false;
+#pragma unroll
+  for (int i = 0; i < 24; i++) bad |= cur[i] != 0;
+  if (bad) raise(err, 1);
+}
+
+// negacyclic: one workgroup per w_ccs element.
+template <int D>
+__global__ void __launch_bounds__(NT<D>::T) k_from_w_ccs_nega(const uint64_t *w_ccs, size_t W,
+                                                             int lb, int L, uint64_t *f_coeff,
+                                                             uint64_t *f, ring::NegaTables fwd,
+                                                             ring::NegaTables inv, int *err) {
+  constexpr int T = NT<D>::T, PER = D / T;
+  __shared__ uint64_t buf[2][D];
+  const int tid = threadIdx.x;
+  for (size_t j = blockIdx.x; j < W; j += gridDim.x) {
+    const uint64_t *g = w_ccs + j * D;
+#pragma unroll
+    for (int i = tid; i < D; i += T) buf[0][i] = g[i];
+    __syncthreads();
+    uint64_t *r = ring::stockham4<D, T>(buf[0], buf[1], inv.roots, tid);
+    int64_t cur[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) cur[q] = signed_rep(gl::mul(r[tid + q * T], inv.twist[tid + q * T]));
+    __syncthreads();
+    for (int l = 0; l < L; l++) {
+      uint64_t *oc = f_coeff + (j * L + l) * D;
+#pragma unroll
+      for (int q = 0; q < PER; q++) {
+        const int i = tid + q * T;
+        uint64_t dgt = from_signed(bal_digit(cur[q], lb));
+        oc[i] = dgt;
+        buf[0][i] = gl::mul(dgt, fwd.twist[i]);
+      }
+      __syncthreads();
+      uint64_t *rr = ring::stockham4<D, T>(buf[0], buf[1], fwd.roots, tid);
+      uint64_t *of = f + (j * L + l) * D;
+#pragma unroll
+      for (int q = 0; q < PER; q++) of[tid + q * T] = rr[tid + q * T];
+      __syncthreads();
+    }
+    bool bad = false;
+#pragma unroll
+    for (int q = 0; q < PER; q++) bad |= cur[q] != 0;
+    if (bad) raise(err, 1);
+  }
+}
+
+// ============================================================ Witness::from_f
+// LF/arith.rs:299-313: f_coeff = ICRT(f); w_ccs = gadget_recompose(f, B, L).
+__global__ void __launch_bounds__(128) k_from_f_phi72(const uint64_t *f, size_t W, int lb, int L,
+                                                     uint64_t *f_coeff, uint64_t *w_ccs) {
+  size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (j >= W) return;
+  uint64_t acc[24];
+  for (int l = L - 1; l >= 0; l--) {
+    uint64_t c[24];
+    const ulonglong2 *src = reinterpret_cast<const ulonglong2 *>(f + (j * L + l) * 24);
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+      ulonglong2 v = src[i];
+      c[2 * i] = v.x;
+      c[2 * i + 1] = v.y;
+    }
+#pragma unroll
+    for (int i = 0; i < 24; i++)  // Horner: recompose() (balanced_decomposition/mod.rs:105-117)
+      acc[i] = (l == L - 1) ? c[i] : gl::add(gl::mul_pow2(acc[i], lb), c[i]);
+    ring::phi72_icrt(c);
+    ulonglong2 *dc = reinterpret_cast<ulonglong2 *>(f_coeff + (j * L + l) * 24);
+#pragma unroll
+    for (int i = 0; i < 12; i++) dc[i] = make_ulonglong2(c[2 * i], c[2 * i + 1]);
+  }
+  ulonglong2 *dw = reinterpret_cast<ulonglong2 *>(w_ccs + j * 24);
+#pragma unroll
+  for (int i = 0; i < 12; i++) dw[i] = make_ulonglong2(acc[2 * i], acc[2 * i + 1]);
+}
+
+template <int D>
+__global__ void __launch_bounds__(NT<D>::T) k_from_f_nega(const uint64_t *f, size_t W, int lb, int L,
+                                                         uint64_t *f_coeff, uint64_t *w_ccs,
+                                                         ring::NegaTables inv) {
+  constexpr int T = NT<D>::T, PER = D / T;
+  __shared__ uint64_t buf[2][D];
+  const int tid = threadIdx.x;
+  for (size_t j = blockIdx.x; j < W; j += gridDim.x) {
+    uint64_t acc[PER];
+    for (int l = L - 1; l >= 0; l--) {
+      const uint64_t *g = f + (j * L + l) * D;
+#pragma unroll
+      for (int q = 0; q < PER; q++) {
+        const int i = tid + q * T;
+        uint64_t v = g[i];
+        buf[0][i] = v;
+        acc[q] = (l == L - 1) ? v : gl::add(gl::mul_pow2(acc[q], lb), v);
+      }
+      __syncthreads();
+      uint64_t *r = ring::stockham4<D, T>(buf[0], buf[1], inv.roots, tid);
+      uint64_t *oc = f_coeff + (j * L + l) * D;
+#pragma unroll
+      for (int q = 0; q < PER; q++) oc[tid + q * T] = gl::mul(r[tid + q * T], inv.twist[tid + q * T]);
+      __syncthreads();
+    }
+    uint64_t *ow = w_ccs + j * D;
+#pragma unroll
+    for (int q = 0; q < PER; q++) ow[tid + q * T] = acc[q];
+  }
+}
+
+// ============================================================ decompose_witness
+// LF/nifs/decomposition.rs:162-167 + decomposition/utils.rs:45-49 + arith.rs:324-338:
+// K balanced base-b_small digit vectors of f_coeff; per digit vector:
+// f_k = CRT(f_coeff_k), w_ccs_k = recompose(f_k, B, L).
+// Phi_72: one thread per element, 64 groups of L elements per block; the
+// recompose across the L elements of a group goes through LDS.
+constexpr int DEC_GROUPS = 32;
+__global__ void __launch_bounds__(256) k_decompose_phi72(const uint64_t *f_coeff, size_t N, int lb,
+                                                        int L, int lbs, int K, uint64_t *f_coeff_k,
+                                                        uint64_t *f_k, uint64_t *w_ccs_k, int *err) {
+  extern __shared__ uint64_t lds[];  // [DEC_GROUPS * L][25]
+  const int t = threadIdx.x;
+  const size_t W = N / L;
+  const size_t j = (size_t)blockIdx.x * DEC_GROUPS * L + t;  // element index
+  const bool act = t < DEC_GROUPS * L && j < N;
+  int64_t cur[24];
+  if (act) {
+    const ulonglong2 *src = reinterpret_cast<const ulonglong2 *>(f_coeff + j * 24);
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+      ulonglong2 v = src[i];
+      cur[2 * i] = signed_rep(v.x);
+      cur[2 * i + 1] = signed_rep(v.y);
+    }
+  }
+  for (int k = 0; k < K; k++) {
+    if (act) {
+      uint64_t c[24];
+#pragma unroll
+      for (int i = 0; i < 24; i++) c[i] = from_signed(bal_digit(cur[i], lbs));
+      ulonglong2 *dc = reinterpret_cast<ulonglong2 *>(f_coeff_k + ((size_t)k * N + j) * 24);
+#pragma unroll
+      for (int i = 0; i < 12; i++) dc[i] = make_ulonglong2(c[2 * i], c[2 * i + 1]);
+      ring::phi72_crt(c);
+      ulonglong2 *df = reinterpret_cast<ulonglong2 *>(f_k + ((size_t)k * N + j) * 24);
+#pragma unroll
+      for (int i = 0; i < 12; i++) df[i] = make_ulonglong2(c[2 * i], c[2 * i + 1]);
+#pragma unroll
+      for (int i = 0; i < 24; i++) lds[t * 25 + i] = c[i];
+    }
+    __syncthreads();
+    // recompose: one thread per (group, coefficient)
+    for (int u = t; u < DEC_GROUPS * 24; u += blockDim.x) {
+      const int g = u / 24, i = u % 24;
+      const size_t wj = (size_t)blockIdx.x * DEC_GROUPS + g;
+      if (wj < W) {
+        uint64_t a = lds[(g * L + L - 1) * 25 + i];
+        for (int l = L - 2; l >= 0; l--) a = gl::add(gl::mul_pow2(a, lb), lds[(g * L + l) * 25 + i]);
+        w_ccs_k[((size_t)k * W + wj) * 24 + i] = a;
+      }
+    }
+    __syncthreads();
+  }
+  if (act) {
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < 24; i++) bad |= cur[i] != 0;
+    if (bad) raise(err, 1);
+  }
+}
+
+// negacyclic: one workgroup per group of L elements; coefficients of the
+// group kept in registers as int64 "cur" (|v| < 2^K for a valid witness).
+template <int D>
+__global__ void __launch_bounds__(NT<D>::T) k_decompose_nega(const uint64_t *f_coeff, size_t N, int lb,
+                                                            int L, int lbs, int K, uint64_t *f_coeff_k,
+                                                            uint64_t *f_k, uint64_t *w_ccs_k,
+                                                            ring::NegaTables fwd, int *err) {
+  constexpr int T = NT<D>::T, PER = D / T, LMAX = 8;
+  __shared__ uint64_t buf[2][D];
+  const int tid = threadIdx.x;
+  const size_t W = N / L;
+  for (size_t g = blockIdx.x; g < W; g += gridDim.x) {
+    int64_t cur[LMAX][PER];
+#pragma unroll
+    for (int l = 0; l < LMAX; l++)
+      if (l < L)
+#pragma unroll
+        for (int q = 0; q < PER; q++) cur[l][q] = signed_rep(f_coeff[(g * L + l) * D + tid + q * T]);
+    for (int k = 0; k < K; k++) {
+      uint64_t acc[PER];
+#pragma unroll
+      for (int l = LMAX - 1; l >= 0; l--) {
+        if (l >= L) continue;
+        const size_t e = (size_t)k * N + g * L + l;
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+          const int i = tid + q * T;
+          int64_t dg = bal_digit(cur[l][q], lbs);
+          f_coeff_k[e * D + i] = from_signed(dg);
+          uint64_t tw = fwd.twist[i];
+          buf[0][i] = dg == 0 ? 0 : (dg == 1 ? tw : (dg == -1 ? gl::neg(tw) : gl::mul(from_signed(dg), tw)));
+        }
+        __syncthreads();
+        uint64_t *r = ring::stockham4<D, T>(buf[0], buf[1], fwd.roots, tid);
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+          uint64_t v = r[tid + q * T];
+          f_k[e * D + tid + q * T] = v;
+          acc[q] = (l == L - 1) ? v : gl::add(gl::mul_pow2(acc[q], lb), v);
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int q = 0; q < PER; q++) w_ccs_k[((size_t)k * W + g) * D + tid + q * T] = acc[q];
+    }
+    bool bad = false;
+#pragma unroll
+    for (int l = 0; l < LMAX; l++)
+      if (l < L)
+#pragma unroll
+        for (int q = 0; q < PER; q++) bad |= cur[l][q] != 0;
+    if (bad) raise(err, 1);
+  }
+}
+
+// ============================================================ Ajtai commitment
+// LF/commitment/commitment_scheme.rs:37-54 -> LA/matrix.rs:168-178:
+//   cm[v][i] = sum_j A[i][j] (.) f_v[j]    (slot-wise products)
+// Split over (slot chunk, row tile, vector tile, column split); each thread
+// owns one slot position and an R x V tile of lazy 128-bit accumulators; the
+// column-split partials are reduced mod p by k_ajtai_reduce.
+template <int R, int V>
+__global__ void __launch_bounds__(256) k_ajtai_nega(const uint64_t *A, size_t kappa, size_t ncols,
+                                                   int d, VecPtrs fv, int nvec, size_t jchunk,
+                                                   uint64_t *partial) {
+  const int s = blockIdx.x * 256 + threadIdx.x;  // slot
+  const int i0 = blockIdx.y * R;
+  const int nvt = (nvec + V - 1) / V;
+  const int v0 = (blockIdx.z % nvt) * V;
+  const int js = blockIdx.z / nvt;
+  if (s >= d) return;
+  const size_t j0 = (size_t)js * jchunk, j1 = min(ncols, j0 + jchunk);
+  Acc acc[R][V];
+#pragma unroll
+  for (int r = 0; r < R; r++)
+#pragma unroll
+    for (int v = 0; v < V; v++) gl::acc_zero(acc[r][v]);
+  for (size_t j = j0; j < j1; j++) {
+    uint64_t a[R], b[V];
+#pragma unroll
+    for (int r = 0; r < R; r++) a[r] = (i0 + r < (int)kappa) ? A[((i0 + r) * ncols + j) * d + s] : 0;
+#pragma unroll
+    for (int v = 0; v < V; v++) b[v] = (v0 + v < nvec) ? fv.p[v0 + v][j * d + s] : 0;
+#pragma unroll
+    for (int r = 0; r < R; r++)
+#pragma unroll
+      for (int v = 0; v < V; v++) gl::acc_mad(acc[r][v], a[r], b[v]);
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++)
+#pragma unroll
+    for (int v = 0; v < V; v++)
+      if (i0 + r < (int)kappa && v0 + v < nvec)
+        partial[(((size_t)js * nvec + v0 + v) * kappa + i0 + r) * d + s] = gl::acc_reduce(acc[r][v]);
+}
+
+// Phi_72: lanes = 8 Fq3 slots x 8 column phases; R x V tile of Fq3 accumulators.
+template <int R, int V>
+__global__ void __launch_bounds__(256) k_ajtai_phi72(const uint64_t *A, size_t kappa, size_t ncols,
+                                                    VecPtrs fv, int nvec, size_t jchunk,
+                                                    uint64_t *partial) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int slot = lane & 7, ph = lane >> 3;  // column phase 0..7
+  const int i0 = blockIdx.y * R;
+  const int nvt = (nvec + V - 1) / V;
+  const int v0 = (blockIdx.z % nvt) * V;
+  const int js = blockIdx.x * 4 + wave;  // column split index
+  const size_t j0 = (size_t)js * jchunk, j1 = min(ncols, j0 + jchunk);
+  ring::Fq3Acc acc[R][V];
+#pragma unroll
+  for (int r = 0; r < R; r++)
+#pragma unroll
+    for (int v = 0; v < V; v++) ring::fq3acc_zero(acc[r][v]);
+  if (j0 < ncols) {
+    for (size_t j = j0 + ph; j < j1; j += 8) {
+      uint64_t a[R][3], b[V][3];
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        const uint64_t *pa = A + ((size_t)(i0 + r) * ncols + j) * 24 + 3 * slot;
+        bool ok = i0 + r < (int)kappa;
+        a[r][0] = ok ? pa[0] : 0;
+        a[r][1] = ok ? pa[1] : 0;
+        a[r][2] = ok ? pa[2] : 0;
+      }
+#pragma unroll
+      for (int v = 0; v < V; v++) {
+        bool ok = v0 + v < nvec;
+        const uint64_t *pb = ok ? fv.p[v0 + v] + j * 24 + 3 * slot : nullptr;
+        b[v][0] = ok ? pb[0] : 0;
+        b[v][1] = ok ? pb[1] : 0;
+        b[v][2] = ok ? pb[2] : 0;
+      }
+#pragma unroll
+      for (int r = 0; r < R; r++)
+#pragma unroll
+        for (int v = 0; v < V; v++)
+          ring::fq3acc_mad(acc[r][v], a[r][0], a[r][1], a[r][2], b[v][0], b[v][1], b[v][2]);
+    }
+  }
+  // reduce each tile entry to canonical Fq3, then sum the 8 column phases (mod p)
+#pragma unroll
+  for (int r = 0; r < R; r++)
+#pragma unroll
+    for (int v = 0; v < V; v++) {
+      uint64_t c[3];
+      ring::fq3acc_final(acc[r][v], c);
+#pragma unroll
+      for (int off = 8; off < 64; off <<= 1)
+#pragma unroll
+        for (int q = 0; q < 3; q++) c[q] = gl::add(c[q], __shfl_xor(c[q], off));
+      if (ph == 0 && i0 + r < (int)kappa && v0 + v < nvec) {  // empty splits write zeros
+        uint64_t *o = partial + (((size_t)js * nvec + v0 + v) * kappa + i0 + r) * 24 + 3 * slot;
+        o[0] = c[0];
+        o[1] = c[1];
+        o[2] = c[2];
+      }
+    }
+}
+
+// sum nsplit partial planes of len u64 each (mod p)
+__global__ void k_sum_planes(const uint64_t *partial, int nsplit, size_t len, uint64_t *out,
+                             size_t out_stride_vec, size_t per_vec) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= len) return;
+  Acc a;
+  gl::acc_zero(a);
+  for (int s = 0; s < nsplit; s++) gl::acc_add(a, partial[(size_t)s * len + i]);
+  size_t v = i / per_vec, r = i % per_vec;
+  out[v * out_stride_vec + r] = gl::acc_reduce(a);
+}
+
+// ============================================================ commit_witnesses y_0
+// LF/nifs/decomposition.rs:183-200: y_0 = cm - sum_{k>=1} b^k y_k (scalar b)
+__global__ void k_commit_y0(const uint64_t *cm, uint64_t *y, size_t n, int lbs, int K) {
+  size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  uint64_t acc = 0;
+  for (int k = K - 1; k >= 1; k--) acc = gl::mul_pow2(gl::add(acc, y[(size_t)k * n + c]), lbs);
+  y[c] = gl::sub(cm[c], acc);
+}
+
+// ============================================================ linear fold
+// LF/nifs/folding.rs:258-268 (f_0) and folding/utils.rs:470-476 (cm_0):
+//   out[j] = sum_i rho_i (.) x_i[j]
+__global__ void __launch_bounds__(256) k_fold_nega(const uint64_t *rho, VecPtrs x, int nwit, size_t n,
+                                                  int d, uint64_t *out) {
+  size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (c >= n * (size_t)d) return;
+  const int s = c % d;
+  Acc a;
+  gl::acc_zero(a);
+  for (int i = 0; i < nwit; i++) gl::acc_mad(a, rho[i * d + s], x.p[i][c]);
+  out[c] = gl::acc_reduce(a);
+}
+__global__ void __launch_bounds__(256) k_fold_phi72(const uint64_t *rho, VecPtrs x, int nwit, size_t n,
+                                                   uint64_t *out) {
+  size_t u = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // Fq3 slot index
+  if (u >= n * 8) return;
+  const int s = u % 8;
+  ring::Fq3Acc a;
+  ring::fq3acc_zero(a);
+  for (int i = 0; i < nwit; i++) {
+    const uint64_t *r = rho + i * 24 + 3 * s, *p = x.p[i] + 3 * u;
+    ring::fq3acc_mad(a, r[0], r[1], r[2], p[0], p[1], p[2]);
+  }
+  uint64_t c[3];
+  ring::fq3acc_final(a, c);
+  out[3 * u] = c[0];
+  out[3 * u + 1] = c[1];
+  out[3 * u + 2] = c[2];
+}
+
+// ============================================================ Poseidon2-16
+// zkvm/src/poseidon2.rs:100-173 (+ Plonky3 add_rc_and_sbox_generic, matmul_internal)
+#include "p2_consts.inc"
+__constant__ uint64_t P2_EXT_INIT[64] = LF_P2_EXT_INIT;
+__constant__ uint64_t P2_EXT_TERM[64] = LF_P2_EXT_TERM;
+__constant__ uint64_t P2_INTERNAL[22] = LF_P2_INTERNAL;
+__constant__ uint64_t P2_DIAG_M1[16] = LF_P2_DIAG_M1;
+
+__device__ __forceinline__ uint64_t sbox7(uint64_t x) {
+  uint64_t x2 = gl::mul(x, x), x4 = gl::mul(x2, x2);
+  return gl::mul(gl::mul(x4, x2), x);
+}
+__device__ __forceinline__ void mds16(uint64_t *s) {  // poseidon2.rs:243-268
+#pragma unroll
+  for (int c = 0; c < 16; c += 4) {
+    uint64_t x0 = s[c], x1 = s[c + 1], x2 = s[c + 2], x3 = s[c + 3];
+    uint64_t t = gl::add(gl::add(x0, x1), gl::add(x2, x3));
+    s[c] = gl::add(t, gl::add(x0, gl::add(x1, x1)));
+    s[c + 1] = gl::add(t, gl::add(x1, gl::add(x2, x2)));
+    s[c + 2] = gl::add(t, gl::add(x2, gl::add(x3, x3)));
+    s[c + 3] = gl::add(t, gl::add(x3, gl::add(x0, x0)));
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint64_t sum = gl::add(gl::add(s[k], s[4 + k]), gl::add(s[8 + k], s[12 + k]));
+#pragma unroll
+    for (int j = k; j < 16; j += 4) s[j] = gl::add(s[j], sum);
+  }
+}
+__global__ void __launch_bounds__(256) k_p2_permute(uint64_t *states, size_t n) {
+  size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  uint64_t s[16];
+  const ulonglong2 *src = reinterpret_cast<const ulonglong2 *>(states + e * 16);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    ulonglong2 v = src[i];
+    s[2 * i] = gl::canon(v.x);
+    s[2 * i + 1] = gl::canon(v.y);
+  }
+  mds16(s);
+#pragma unroll 1
+  for (int r = 0; r < 4; r++) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) s[i] = sbox7(gl::add(s[i], P2_EXT_INIT[16 * r + i]));
+    mds16(s);
+  }
+#pragma unroll 1
+  for (int r = 0; r < 22; r++) {
+    s[0] = sbox7(gl::add(s[0], P2_INTERNAL[r]));
+    uint64_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) sum = gl::add(sum, s[i]);
+#pragma unroll
+    for (int i = 0; i < 16; i++) s[i] = gl::add(gl::mul(s[i], P2_DIAG_M1[i]), sum);
+  }
+#pragma unroll 1
+  for (int r = 0; r < 4; r++) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) s[i] = sbox7(gl::add(s[i], P2_EXT_TERM[16 * r + i]));
+    mds16(s);
+  }
+  ulonglong2 *dst = reinterpret_cast<ulonglong2 *>(states + e * 16);
+#pragma unroll
+  for (int i = 0; i < 8; i++) dst[i] = make_ulonglong2(s[2 * i], s[2 * i + 1]);
+}
+
+// ============================================================ synthetic inputs / reductions
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+// element i = SplitMix64(counter i) re-mixed until < p (oracle lfo_fill_uniform)
+__global__ void k_fill_uniform(uint64_t *out, size_t n, uint64_t seed) {
+  const uint64_t G = 0x9e3779b97f4a7c15ull;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint64_t x = mix64(seed + (uint64_t)(i + 1) * G);
+    while (x >= gl::P) x = mix64(x + G);
+    out[i] = x;
+  }
+}
+// out[c] = sum_r in[r*len + c] mod p  (cross-rank accumulator reduce)
+__global__ void k_modp_sum(const uint64_t *in, int nparts, size_t len, uint64_t *out) {
+  size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (c >= len) return;
+  Acc a;
+  gl::acc_zero(a);
+  for (int r = 0; r < nparts; r++) gl::acc_add(a, gl::canon(in[(size_t)r * len + c]));
+  out[c] = gl::acc_reduce(a);
+}
+
+// ============================================================ RCCL limb transport
+// RCCL sums u64 mod 2^64, not mod p: ship 32-bit limbs (sums of <= 2^8 ranks
+// stay < 2^40) and fold the limb sums back into the field afterwards.
+__global__ void k_limb_split(const uint64_t *x, size_t n, uint64_t *lo, uint64_t *hi) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t v = x[i];
+  lo[i] = v & 0xFFFFFFFFull;
+  hi[i] = v >> 32;
+}
+__global__ void k_limb_join(const uint64_t *lo, const uint64_t *hi, size_t n, uint64_t *out) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t h = hi[i], wl = h << 32, wh = h >> 32;  // h * 2^32 as 128 bits
+  uint64_t s = wl + lo[i];
+  wh += s < wl ? 1 : 0;
+  out[i] = gl::canon(gl::reduce128(s, wh));
+}
+
+// ============================================================ launchers
+static inline unsigned blocks(size_t n, int t) { return (unsigned)((n + t - 1) / t); }
+static inline unsigned grid_cap(size_t n) { return (unsigned)(n < 65536 ? n : 65536); }
+
+hipError_t transform(uint64_t *data, size_t n, int d, bool fwd, const ring::NegaTables &tb,
+                     hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (d == 24) {
+    if (fwd)
+      hipLaunchKernelGGL(k_phi72_transform<true>, dim3(blocks(n, 256)), dim3(256), 0, st, data, n);
+    else
+      hipLaunchKernelGGL(k_phi72_transform<false>, dim3(blocks(n, 256)), dim3(256), 0, st, data, n);
+    return hipGetLastError();
+  }
+#define LF_NEGA_T(DD)                                                                             \
+  case DD:                                                                                        \
+    if (fwd)                                                                                      \
+      hipLaunchKernelGGL((k_nega_transform<DD, true>), dim3(grid_cap(n)), dim3(NT<DD>::T), 0, st, \
+                         data, n, tb);                                                            \
+    else                                                                                          \
+      hipLaunchKernelGGL((k_nega_transform<DD, false>), dim3(grid_cap(n)), dim3(NT<DD>::T), 0,    \
+                         st, data, n, tb);                                                        \
+    break;
+  switch (d) {
+    LF_NEGA_T(16)
+    LF_NEGA_T(64)
+    LF_NEGA_T(256)
+    LF_NEGA_T(1024)
+    LF_NEGA_T(4096)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef LF_NEGA_T
+  return hipGetLastError();
+}
+
+hipError_t slot_mul(const uint64_t *a, const uint64_t *b, uint64_t *out, size_t n, int d,
+                    hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (d == 24)
+    hipLaunchKernelGGL(k_slot_mul_phi72, dim3(blocks(n * 8, 256)), dim3(256), 0, st, a, b, out, n * 8);
+  else
+    hipLaunchKernelGGL(k_slot_mul_nega, dim3(blocks(n * d, 256)), dim3(256), 0, st, a, b, out, n * d);
+  return hipGetLastError();
+}
+
+hipError_t mont(uint64_t *x, size_t n, bool to, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_mont, dim3(blocks(n, 256)), dim3(256), 0, st, x, n, to ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t from_w_ccs(const uint64_t *w_ccs, size_t W, int d, int lb, int L, uint64_t *f_coeff,
+                      uint64_t *f, const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err,
+                      hipStream_t st) {
+  if (W == 0) return hipSuccess;
+  if (d == 24) {
+    hipLaunchKernelGGL(k_from_w_ccs_phi72, dim3(blocks(W, 128)), dim3(128), 0, st, w_ccs, W, lb, L,
+                       f_coeff, f, err);
+    return hipGetLastError();
+  }
+#define LF_CASE(DD)                                                                                \
+  case DD:                                                                                         \
+    hipLaunchKernelGGL((k_from_w_ccs_nega<DD>), dim3(grid_cap(W)), dim3(NT<DD>::T), 0, st, w_ccs, W, \
+                       lb, L, f_coeff, f, fwd, inv, err);                                          \
+    break;
+  switch (d) {
+    LF_CASE(16) LF_CASE(64) LF_CASE(256) LF_CASE(1024) LF_CASE(4096) default : return hipErrorInvalidValue;
+  }
+#undef LF_CASE
+  return hipGetLastError();
+}
+
+hipError_t from_f(const uint64_t *f, size_t N, int d, int lb, int L, uint64_t *f_coeff,
+                  uint64_t *w_ccs, const ring::NegaTables &inv, hipStream_t st) {
+  const size_t W = N / L;
+  if (W == 0) return hipSuccess;
+  if (d == 24) {
+    hipLaunchKernelGGL(k_from_f_phi72, dim3(blocks(W, 128)), dim3(128), 0, st, f, W, lb, L, f_coeff,
+                       w_ccs);
+    return hipGetLastError();
+  }
+#define LF_CASE(DD)                                                                              \
+  case DD:                                                                                       \
+    hipLaunchKernelGGL((k_from_f_nega<DD>), dim3(grid_cap(W)), dim3(NT<DD>::T), 0, st, f, W, lb, L, \
+                       f_coeff, w_ccs, inv);                                                     \
+    break;
+  switch (d) {
+    LF_CASE(16) LF_CASE(64) LF_CASE(256) LF_CASE(1024) LF_CASE(4096) default : return hipErrorInvalidValue;
+  }
+#undef LF_CASE
+  return hipGetLastError();
+}
+
+hipError_t decompose_witness(const uint64_t *f_coeff, size_t N, int d, int lb, int L, int lbs, int K,
+                             uint64_t *f_coeff_k, uint64_t *f_k, uint64_t *w_ccs_k,
+                             const ring::NegaTables &fwd, int *err, hipStream_t st) {
+  const size_t W = N / L;
+  if (W == 0) return hipSuccess;
+  if (d == 24) {
+    if (DEC_GROUPS * L > 256) return hipErrorInvalidValue;
+    size_t lds = (size_t)DEC_GROUPS * L * 25 * sizeof(uint64_t);
+    hipLaunchKernelGGL(k_decompose_phi72, dim3(blocks(W, DEC_GROUPS)), dim3(256), lds, st, f_coeff, N,
+                       lb, L, lbs, K, f_coeff_k, f_k, w_ccs_k, err);
+    return hipGetLastError();
+  }
+  if (L > 8) return hipErrorInvalidValue;
+#define LF_CASE(DD)                                                                                  \
+  case DD:                                                                                           \
+    hipLaunchKernelGGL((k_decompose_nega<DD>), dim3(grid_cap(W)), dim3(NT<DD>::T), 0, st, f_coeff, N, \
+                       lb, L, lbs, K, f_coeff_k, f_k, w_ccs_k, fwd, err);                            \
+    break;
+  switch (d) {
+    LF_CASE(16) LF_CASE(64) LF_CASE(256) LF_CASE(1024) LF_CASE(4096) default : return hipErrorInvalidValue;
+  }
+#undef LF_CASE
+  return hipGetLastError();
+}
+
+size_t ajtai_partial_elems(size_t kappa, size_t ncols, int d, int nvec) {
+  size_t nsplit = ajtai_nsplit(ncols, d, nvec);
+  return nsplit * (size_t)nvec * kappa * (size_t)d;
+}
+int ajtai_nsplit(size_t ncols, int d, int nvec) {
+  if (d == 24) {
+    // one wave per column split; ~64 columns per lane phase minimum
+    size_t want = (ncols + 511) / 512;
+    if (want > 1024) want = 1024;
+    return (int)((want + 3) / 4 * 4);
+  }
+  size_t want = (ncols + 255) / 256;
+  if (want > 64) want = 64;
+  if (want < 1) want = 1;
+  return (int)want;
+}
+
+hipError_t ajtai_commit(const uint64_t *A, size_t kappa, size_t ncols, int d, const VecPtrs &fv,
+                        int nvec, uint64_t *partial, uint64_t *cm, hipStream_t st, hipEvent_t ev0,
+                        hipEvent_t ev1) {
+  if (nvec <= 0 || nvec > LF_MAX_VECS) return hipErrorInvalidValue;
+  if (ev0) (void)hipEventRecord(ev0, st);
+  const int nsplit = ajtai_nsplit(ncols, d, nvec);
+  const size_t jchunk = (ncols + nsplit - 1) / nsplit;
+  if (d == 24) {
+    constexpr int R = 2, V = 2;
+    const int nvt = (nvec + V - 1) / V;
+    dim3 grid(nsplit / 4, (unsigned)((kappa + R - 1) / R), nvt);
+    hipLaunchKernelGGL((k_ajtai_phi72<R, V>), grid, dim3(256), 0, st, A, kappa, ncols, fv, nvec, jchunk,
+                       partial);
+  } else {
+    constexpr int R = 4, V = 4;
+    const int nvt = (nvec + V - 1) / V;
+    dim3 grid((unsigned)((d + 255) / 256), (unsigned)((kappa + R - 1) / R), (unsigned)(nvt * nsplit));
+    hipLaunchKernelGGL((k_ajtai_nega<R, V>), grid, dim3(256), 0, st, A, kappa, ncols, d, fv, nvec, jchunk,
+                       partial);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (ev1) (void)hipEventRecord(ev1, st);
+  const size_t len = (size_t)nvec * kappa * d;
+  hipLaunchKernelGGL(k_sum_planes, dim3(blocks(len, 256)), dim3(256), 0, st, partial, nsplit, len, cm,
+                     kappa * (size_t)d, kappa * (size_t)d);
+  return hipGetLastError();
+}
+
+hipError_t commit_y0(const uint64_t *cm, uint64_t *y, size_t kappa, int d, int lbs, int K,
+                     hipStream_t st) {
+  size_t n = kappa * (size_t)d;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_commit_y0, dim3(blocks(n, 256)), dim3(256), 0, st, cm, y, n, lbs, K);
+  return hipGetLastError();
+}
+
+hipError_t fold(const uint64_t *rho, const VecPtrs &x, int nwit, size_t n, int d, uint64_t *out,
+                hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (nwit <= 0 || nwit > LF_MAX_VECS) return hipErrorInvalidValue;
+  if (d == 24)
+    hipLaunchKernelGGL(k_fold_phi72, dim3(blocks(n * 8, 256)), dim3(256), 0, st, rho, x, nwit, n, out);
+  else
+    hipLaunchKernelGGL(k_fold_nega, dim3(blocks(n * d, 256)), dim3(256), 0, st, rho, x, nwit, n, d, out);
+  return hipGetLastError();
+}
+
+hipError_t p2_permute(uint64_t *states, size_t n, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_p2_permute, dim3(blocks(n, 256)), dim3(256), 0, st, states, n);
+  return hipGetLastError();
+}
+
+hipError_t fill_uniform(uint64_t *out, size_t n, uint64_t seed, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fill_uniform, dim3(grid_cap(blocks(n, 256))), dim3(256), 0, st, out, n, seed);
+  return hipGetLastError();
+}
+
+hipError_t modp_sum(const uint64_t *in, int nparts, size_t len, uint64_t *out, hipStream_t st) {
+  if (len == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_modp_sum, dim3(blocks(len, 256)), dim3(256), 0, st, in, nparts, len, out);
+  return hipGetLastError();
+}
+
+hipError_t limb_split(const uint64_t *x, size_t n, uint64_t *lo, uint64_t *hi, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_limb_split, dim3(blocks(n, 256)), dim3(256), 0, st, x, n, lo, hi);
+  return hipGetLastError();
+}
+hipError_t limb_join(const uint64_t *lo, const uint64_t *hi, size_t n, uint64_t *out, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_limb_join, dim3(blocks(n, 256)), dim3(256), 0, st, lo, hi, n, out);
+  return hipGetLastError();
+}
+
+}  // namespace lfk

@@ -1,0 +1,47 @@
+// kernels.hpp -- launcher declarations for kernels.hip (internal to the library).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "ring.hpp"
+
+#define LF_MAX_VECS 32
+
+namespace lfk {
+
+// table of up to LF_MAX_VECS device vectors, passed by value as a kernel argument
+struct VecPtrs {
+  const uint64_t *p[LF_MAX_VECS];
+};
+
+hipError_t transform(uint64_t *data, size_t n, int d, bool fwd, const ring::NegaTables &tb,
+                     hipStream_t st);
+hipError_t slot_mul(const uint64_t *a, const uint64_t *b, uint64_t *out, size_t n, int d,
+                    hipStream_t st);
+hipError_t mont(uint64_t *x, size_t n, bool to, hipStream_t st);
+hipError_t from_w_ccs(const uint64_t *w_ccs, size_t W, int d, int lb, int L, uint64_t *f_coeff,
+                      uint64_t *f, const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err,
+                      hipStream_t st);
+hipError_t from_f(const uint64_t *f, size_t N, int d, int lb, int L, uint64_t *f_coeff,
+                  uint64_t *w_ccs, const ring::NegaTables &inv, hipStream_t st);
+hipError_t decompose_witness(const uint64_t *f_coeff, size_t N, int d, int lb, int L, int lbs, int K,
+                             uint64_t *f_coeff_k, uint64_t *f_k, uint64_t *w_ccs_k,
+                             const ring::NegaTables &fwd, int *err, hipStream_t st);
+int ajtai_nsplit(size_t ncols, int d, int nvec);
+size_t ajtai_partial_elems(size_t kappa, size_t ncols, int d, int nvec);
+hipError_t ajtai_commit(const uint64_t *A, size_t kappa, size_t ncols, int d, const VecPtrs &fv,
+                        int nvec, uint64_t *partial, uint64_t *cm, hipStream_t st,
+                        hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+hipError_t commit_y0(const uint64_t *cm, uint64_t *y, size_t kappa, int d, int lbs, int K,
+                     hipStream_t st);
+hipError_t fold(const uint64_t *rho, const VecPtrs &x, int nwit, size_t n, int d, uint64_t *out,
+                hipStream_t st);
+hipError_t p2_permute(uint64_t *states, size_t n, hipStream_t st);
+hipError_t fill_uniform(uint64_t *out, size_t n, uint64_t seed, hipStream_t st);
+hipError_t modp_sum(const uint64_t *in, int nparts, size_t len, uint64_t *out, hipStream_t st);
+
+hipError_t limb_split(const uint64_t *x, size_t n, uint64_t *lo, uint64_t *hi, hipStream_t st);
+hipError_t limb_join(const uint64_t *lo, const uint64_t *hi, size_t n, uint64_t *out, hipStream_t st);
+
+}  // namespace lfk

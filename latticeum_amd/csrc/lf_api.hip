@@ -1,0 +1,739 @@
+// lf_api.hip -- the extern "C" boundary (include/lf.h): context, twiddle
+// tables, host-buffer wrappers, the device-resident commit+fold step, and the
+// host-side transcript. No CPU compute fallback exists: every ring/commit/fold
+// operation runs on the GPU, and creating a context fails loudly without one.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/lf.h"
+#include "gl.hpp"
+#include "kernels.hpp"
+
+namespace {
+
+struct Tables {
+  uint64_t *mem = nullptr;  // 4*d u64: fwd twist | fwd roots | inv twist | inv roots
+  ring::NegaTables fwd{}, inv{};
+};
+
+struct TimedLaunch {
+  hipEvent_t a, b;
+  int nvec;
+};
+
+}  // namespace
+
+struct lf_ctx {
+  int device = 0;
+  hipStream_t own = nullptr, cur = nullptr;
+  int *d_err = nullptr;
+  std::string last_error;
+  std::map<int, Tables> tables;
+  uint64_t *scratch = nullptr;
+  size_t scratch_elems = 0;
+  bool timing = false;
+  std::vector<TimedLaunch> pending;
+  std::map<int, std::pair<double, long>> stats;  // nvec -> (ms, count)
+};
+
+struct lf_ajtai {
+  const uint64_t *A = nullptr;
+  bool owned = false;
+  size_t kappa = 0, ncols = 0;
+  int d = 0;
+};
+
+namespace {
+
+int fail(lf_ctx *c, int code, const std::string &msg) {
+  if (c) c->last_error = msg;
+  return code;
+}
+
+#define LF_HIP(ctx, call)                                                                         \
+  do {                                                                                            \
+    hipError_t e_ = (call);                                                                       \
+    if (e_ != hipSuccess)                                                                         \
+      return fail((ctx), e_ == hipErrorOutOfMemory ? LF_ERR_OUT_OF_MEMORY : LF_ERR_DEVICE,        \
+                  std::string(#call) + ": " + hipGetErrorString(e_));                            \
+  } while (0)
+
+#define LF_TRY(expr)          \
+  do {                        \
+    int r_ = (expr);          \
+    if (r_ != LF_OK) return r_; \
+  } while (0)
+
+bool ring_ok(int d) { return d == 24 || d == 16 || d == 64 || d == 256 || d == 1024 || d == 4096; }
+
+int log2_exact(uint64_t v) {
+  if (v < 2 || (v & (v - 1))) return -1;
+  int l = 0;
+  while ((1ull << l) != v) l++;
+  return l;
+}
+
+int check_params(lf_ctx *c, const lf_params *pr, int &lb, int &lbs) {
+  if (!pr) return fail(c, LF_ERR_INVALID_ARG, "null params");
+  if (!ring_ok(pr->d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  lb = log2_exact(pr->B);
+  lbs = log2_exact(pr->b_small);
+  if (lb < 1 || lb > 62 || lbs < 1 || lbs > 62 || pr->L < 1 || pr->K < 1 || pr->L > 8 || pr->K > 64)
+    return fail(c, LF_ERR_INVALID_ARG, "device path needs power-of-two B, b_small and L<=8, K<=64");
+  return LF_OK;
+}
+
+// negacyclic twiddle tables for degree d (built on the host once per context)
+int get_tables(lf_ctx *c, int d, Tables *&out) {
+  auto it = c->tables.find(d);
+  if (it != c->tables.end()) {
+    out = &it->second;
+    return LF_OK;
+  }
+  Tables t;
+  if (d != 24) {
+    std::vector<uint64_t> h(4 * (size_t)d);
+    const uint64_t psi = gl::pow(7, (gl::P - 1) / (2 * (uint64_t)d));
+    const uint64_t psi_inv = gl::inv(psi), w = gl::mul(psi, psi), w_inv = gl::mul(psi_inv, psi_inv);
+    const uint64_t dinv = gl::inv((uint64_t)d);
+    uint64_t a = 1, b = 1, x = dinv, y = 1;
+    for (int j = 0; j < d; j++) {
+      h[j] = a;                // psi^j
+      h[d + j] = b;            // w^j
+      h[2 * d + j] = x;        // d^-1 psi^-j
+      h[3 * d + j] = y;        // w^-j
+      a = gl::mul(a, psi);
+      b = gl::mul(b, w);
+      x = gl::mul(x, psi_inv);
+      y = gl::mul(y, w_inv);
+    }
+    LF_HIP(c, hipMalloc(&t.mem, h.size() * 8));
+    LF_HIP(c, hipMemcpy(t.mem, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+    t.fwd = {t.mem, t.mem + d};
+    t.inv = {t.mem + 2 * d, t.mem + 3 * d};
+  }
+  out = &(c->tables[d] = t);
+  return LF_OK;
+}
+
+int reserve(lf_ctx *c, size_t elems) {
+  if (elems <= c->scratch_elems) return LF_OK;
+  if (c->scratch) {
+    LF_HIP(c, hipStreamSynchronize(c->cur));
+    LF_HIP(c, hipFree(c->scratch));
+    c->scratch = nullptr;
+    c->scratch_elems = 0;
+  }
+  LF_HIP(c, hipMalloc(&c->scratch, elems * 8));
+  c->scratch_elems = elems;
+  return LF_OK;
+}
+
+// RAII device buffer for the synchronous host API
+struct DevBuf {
+  uint64_t *p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+int dev_alloc(lf_ctx *c, DevBuf &b, size_t elems) {
+  LF_HIP(c, hipMalloc(&b.p, (elems ? elems : 1) * 8));
+  return LF_OK;
+}
+int upload(lf_ctx *c, DevBuf &b, const uint64_t *h, size_t elems, int repr) {
+  LF_TRY(dev_alloc(c, b, elems));
+  if (elems) {
+    LF_HIP(c, hipMemcpyAsync(b.p, h, elems * 8, hipMemcpyHostToDevice, c->cur));
+    if (repr == LF_REPR_MONTGOMERY) LF_HIP(c, lfk::mont(b.p, elems, false, c->cur));
+  }
+  return LF_OK;
+}
+int download(lf_ctx *c, uint64_t *h, DevBuf &b, size_t elems, int repr) {
+  if (!elems) return LF_OK;
+  if (repr == LF_REPR_MONTGOMERY) LF_HIP(c, lfk::mont(b.p, elems, true, c->cur));
+  LF_HIP(c, hipMemcpyAsync(h, b.p, elems * 8, hipMemcpyDeviceToHost, c->cur));
+  return LF_OK;
+}
+int check_repr(lf_ctx *c, int repr) {
+  if (repr != LF_REPR_CANONICAL && repr != LF_REPR_MONTGOMERY)
+    return fail(c, LF_ERR_INVALID_ARG, "repr must be LF_REPR_CANONICAL or LF_REPR_MONTGOMERY");
+  return LF_OK;
+}
+
+int ajtai_launch(lf_ctx *c, const lf_ajtai *aj, const uint64_t *const *vecs, int nvec, uint64_t *cm) {
+  if (nvec < 1 || nvec > LF_MAX_VECS) return fail(c, LF_ERR_INVALID_ARG, "nvec must be in [1, 32]");
+  lfk::VecPtrs vp{};
+  for (int v = 0; v < nvec; v++) vp.p[v] = vecs[v];
+  LF_TRY(reserve(c, lfk::ajtai_partial_elems(aj->kappa, aj->ncols, aj->d, nvec)));
+  hipEvent_t a = nullptr, b = nullptr;
+  if (c->timing) {
+    LF_HIP(c, hipEventCreate(&a));
+    LF_HIP(c, hipEventCreate(&b));
+  }
+  LF_HIP(c, lfk::ajtai_commit(aj->A, aj->kappa, aj->ncols, aj->d, vp, nvec, c->scratch, cm, c->cur, a, b));
+  if (c->timing) c->pending.push_back({a, b, nvec});
+  return LF_OK;
+}
+
+int drain_timing(lf_ctx *c) {
+  if (c->pending.empty()) return LF_OK;
+  LF_HIP(c, hipStreamSynchronize(c->cur));
+  for (auto &t : c->pending) {
+    float ms = 0;
+    LF_HIP(c, hipEventElapsedTime(&ms, t.a, t.b));
+    auto &s = c->stats[t.nvec];
+    s.first += ms;
+    s.second += 1;
+    (void)hipEventDestroy(t.a);
+    (void)hipEventDestroy(t.b);
+  }
+  c->pending.clear();
+  return LF_OK;
+}
+
+// the commit+fold arithmetic of fold() on device buffers (everything but commit(z))
+int fold_core(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lbs, size_t W,
+              const lf_fold_step_bufs *b, const uint64_t *cm_i, const uint64_t *wi_f_coeff) {
+  const int d = pr->d, L = pr->L, K = pr->K;
+  const size_t N = W * (size_t)L, kappa = aj->kappa;
+  if (2 * K > LF_MAX_VECS) return fail(c, LF_ERR_INVALID_ARG, "2K must be <= 32");
+  if (aj->ncols != N) return fail(c, LF_ERR_WRONG_WITNESS_LENGTH, "witness length != Ajtai width");
+  Tables *t;
+  LF_TRY(get_tables(c, d, t));
+  // decompose_witness for both sides (decomposition.rs:162-167)
+  const uint64_t *fc_side[2] = {b->acc_f_coeff, wi_f_coeff};
+  for (int s = 0; s < 2; s++)
+    LF_HIP(c, lfk::decompose_witness(fc_side[s], N, d, lb, L, lbs, K, b->fk_coeff[s], b->fk[s], b->wk[s],
+                                     t->fwd, c->d_err, c->cur));
+  // commit_witnesses: 2(K-1) commitments sharing one pass over A (decomposition.rs:185-188)
+  std::vector<const uint64_t *> vecs;
+  for (int s = 0; s < 2; s++)
+    for (int k = 1; k < K; k++) vecs.push_back(b->fk[s] + (size_t)k * N * d);
+  const size_t kd = kappa * (size_t)d;
+  uint64_t *ycat = nullptr;
+  // ycat lives after the Ajtai partials in scratch
+  const size_t part = lfk::ajtai_partial_elems(kappa, aj->ncols, d, (int)vecs.size());
+  LF_TRY(reserve(c, part + vecs.size() * kd));
+  ycat = c->scratch + part;
+  {
+    lfk::VecPtrs vp{};
+    for (size_t v = 0; v < vecs.size(); v++) vp.p[v] = vecs[v];
+    hipEvent_t ea = nullptr, eb = nullptr;
+    if (c->timing) {
+      LF_HIP(c, hipEventCreate(&ea));
+      LF_HIP(c, hipEventCreate(&eb));
+    }
+    LF_HIP(c, lfk::ajtai_commit(aj->A, kappa, aj->ncols, d, vp, (int)vecs.size(), c->scratch, ycat, c->cur,
+                                ea, eb));
+    if (c->timing) c->pending.push_back({ea, eb, (int)vecs.size()});
+  }
+  const uint64_t *cm_side[2] = {b->acc_cm, cm_i};
+  for (int s = 0; s < 2; s++) {
+    LF_HIP(c, hipMemcpyAsync(b->y[s] + kd, ycat + (size_t)s * (K - 1) * kd, (size_t)(K - 1) * kd * 8,
+                             hipMemcpyDeviceToDevice, c->cur));
+    LF_HIP(c, lfk::commit_y0(cm_side[s], b->y[s], kappa, d, lbs, K, c->cur));
+  }
+  // f_0 = sum rho_i f_i, cm_0 = sum rho_i y_i   (folding.rs:258-268, folding/utils.rs:470-476)
+  lfk::VecPtrs fx{}, yx{};
+  for (int s = 0; s < 2; s++)
+    for (int k = 0; k < K; k++) {
+      fx.p[s * K + k] = b->fk[s] + (size_t)k * N * d;
+      yx.p[s * K + k] = b->y[s] + (size_t)k * kd;
+    }
+  LF_HIP(c, lfk::fold(b->rho, fx, 2 * K, N, d, b->f0, c->cur));
+  LF_HIP(c, lfk::fold(b->rho, yx, 2 * K, kappa, d, b->cm0, c->cur));
+  // Witness::from_f(f_0) (arith.rs:299-313)
+  LF_HIP(c, lfk::from_f(b->f0, N, d, lb, L, b->f0_coeff, b->w_ccs0, t->inv, c->cur));
+  return LF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+lf_params lf_goldilocks_dp(int d) {
+  lf_params p;
+  p.d = d;
+  p.B = 1ull << 15;
+  p.L = 5;
+  p.b_small = 2;
+  p.K = 15;
+  return p;
+}
+
+const char *lf_status_string(int s) {
+  switch (s) {
+    case LF_OK: return "ok";
+    case LF_ERR_INVALID_ARG: return "invalid argument";
+    case LF_ERR_UNSUPPORTED_RING: return "unsupported ring degree";
+    case LF_ERR_WRONG_WITNESS_LENGTH: return "wrong length of the witness";
+    case LF_ERR_WRONG_COMMITMENT_LENGTH: return "wrong length of the commitment";
+    case LF_ERR_WRONG_AJTAI_DIMENSIONS: return "Ajtai matrix has wrong dimensions";
+    case LF_ERR_DECOMPOSITION_OVERFLOW: return "balanced decomposition ran out of digits";
+    case LF_ERR_INCORRECT_LENGTH: return "incorrect length";
+    case LF_ERR_CHALLENGE_BYTES: return "wrong number of challenge bytes";
+    case LF_ERR_DEVICE: return "HIP device error";
+    case LF_ERR_OUT_OF_MEMORY: return "out of device memory";
+  }
+  return "unknown status";
+}
+
+int lf_ctx_create(int device, lf_ctx **out) {
+  if (!out) return LF_ERR_INVALID_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) {
+    fprintf(stderr, "latticeum_amd: no HIP device %d available (count=%d)\n", device, n);
+    return LF_ERR_DEVICE;
+  }
+  auto c = std::make_unique<lf_ctx>();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess) return LF_ERR_DEVICE;
+  if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) return LF_ERR_DEVICE;
+  c->cur = c->own;
+  if (hipMalloc(&c->d_err, sizeof(int)) != hipSuccess) return LF_ERR_OUT_OF_MEMORY;
+  if (hipMemset(c->d_err, 0, sizeof(int)) != hipSuccess) return LF_ERR_DEVICE;
+  *out = c.release();
+  return LF_OK;
+}
+
+void lf_ctx_destroy(lf_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->cur);
+  for (auto &t : c->pending) {
+    (void)hipEventDestroy(t.a);
+    (void)hipEventDestroy(t.b);
+  }
+  for (auto &kv : c->tables)
+    if (kv.second.mem) (void)hipFree(kv.second.mem);
+  if (c->scratch) (void)hipFree(c->scratch);
+  if (c->d_err) (void)hipFree(c->d_err);
+  if (c->own) (void)hipStreamDestroy(c->own);
+  delete c;
+}
+
+const char *lf_ctx_last_error(const lf_ctx *c) { return c ? c->last_error.c_str() : ""; }
+
+int lf_ctx_set_stream(lf_ctx *c, void *s) {
+  if (!c) return LF_ERR_INVALID_ARG;
+  c->cur = s ? (hipStream_t)s : c->own;
+  return LF_OK;
+}
+void *lf_ctx_get_stream(const lf_ctx *c) { return c ? (void *)c->cur : nullptr; }
+
+int lf_ctx_sync(lf_ctx *c) {
+  if (!c) return LF_ERR_INVALID_ARG;
+  LF_HIP(c, hipStreamSynchronize(c->cur));
+  int e = 0;
+  LF_HIP(c, hipMemcpy(&e, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
+  if (e) {
+    LF_HIP(c, hipMemset(c->d_err, 0, sizeof(int)));
+    return fail(c, LF_ERR_DECOMPOSITION_OVERFLOW, "a coefficient needed more digits than padding_size");
+  }
+  return LF_OK;
+}
+
+int lf_ctx_reserve(lf_ctx *c, size_t kappa, size_t ncols, int d, int nvec) {
+  if (!c || !ring_ok(d) || nvec < 1 || nvec > LF_MAX_VECS) return LF_ERR_INVALID_ARG;
+  Tables *t;
+  LF_TRY(get_tables(c, d, t));
+  return reserve(c, lfk::ajtai_partial_elems(kappa, ncols, d, nvec) + (size_t)nvec * kappa * d);
+}
+
+int lf_ctx_kernel_timing(lf_ctx *c, int enable) {
+  if (!c) return LF_ERR_INVALID_ARG;
+  LF_TRY(drain_timing(c));
+  c->timing = enable != 0;
+  c->stats.clear();
+  return LF_OK;
+}
+
+int lf_ctx_kernel_stats(lf_ctx *c, int nvec, double *ms, long *count) {
+  if (!c || !ms || !count) return LF_ERR_INVALID_ARG;
+  LF_TRY(drain_timing(c));
+  *ms = 0;
+  *count = 0;
+  for (auto &kv : c->stats)
+    if (nvec == 0 || kv.first == nvec) {
+      *ms += kv.second.first;
+      *count += kv.second.second;
+    }
+  return LF_OK;
+}
+
+// ---------------------------------------------------------------- host-buffer API
+static int xform_host(lf_ctx *c, uint64_t *e, size_t n, int d, int repr, bool fwd) {
+  if (!c || (!e && n)) return LF_ERR_INVALID_ARG;
+  LF_TRY(check_repr(c, repr));
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  Tables *t;
+  LF_TRY(get_tables(c, d, t));
+  DevBuf b;
+  LF_TRY(upload(c, b, e, n * d, repr));
+  LF_HIP(c, lfk::transform(b.p, n, d, fwd, fwd ? t->fwd : t->inv, c->cur));
+  LF_TRY(download(c, e, b, n * d, repr));
+  return lf_ctx_sync(c);
+}
+int lf_crt(lf_ctx *c, uint64_t *e, size_t n, int d, int repr) { return xform_host(c, e, n, d, repr, true); }
+int lf_icrt(lf_ctx *c, uint64_t *e, size_t n, int d, int repr) { return xform_host(c, e, n, d, repr, false); }
+
+int lf_ring_mul(lf_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t n, int d, int repr) {
+  if (!c || ((!a || !b || !out) && n)) return LF_ERR_INVALID_ARG;
+  LF_TRY(check_repr(c, repr));
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  DevBuf da, db, dout;
+  LF_TRY(upload(c, da, a, n * d, repr));
+  LF_TRY(upload(c, db, b, n * d, repr));
+  LF_TRY(dev_alloc(c, dout, n * d));
+  LF_HIP(c, lfk::slot_mul(da.p, db.p, dout.p, n, d, c->cur));
+  LF_TRY(download(c, out, dout, n * d, repr));
+  return lf_ctx_sync(c);
+}
+
+int lf_ajtai_create(lf_ctx *c, const uint64_t *A, size_t kappa, size_t ncols, int d, int repr,
+                    lf_ajtai **out) {
+  if (!c || !A || !out || !kappa || !ncols) return LF_ERR_INVALID_ARG;
+  LF_TRY(check_repr(c, repr));
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  DevBuf b;
+  LF_TRY(upload(c, b, A, kappa * ncols * d, repr));
+  LF_TRY(lf_ctx_sync(c));
+  auto *aj = new lf_ajtai;
+  aj->A = b.p;
+  b.p = nullptr;
+  aj->owned = true;
+  aj->kappa = kappa;
+  aj->ncols = ncols;
+  aj->d = d;
+  *out = aj;
+  return LF_OK;
+}
+
+int lf_ajtai_create_device(lf_ctx *c, const uint64_t *A_dev, size_t kappa, size_t ncols, int d,
+                           lf_ajtai **out) {
+  if (!c || !A_dev || !out || !kappa || !ncols) return LF_ERR_INVALID_ARG;
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  auto *aj = new lf_ajtai;
+  aj->A = A_dev;
+  aj->kappa = kappa;
+  aj->ncols = ncols;
+  aj->d = d;
+  *out = aj;
+  return LF_OK;
+}
+
+void lf_ajtai_destroy(lf_ajtai *aj) {
+  if (!aj) return;
+  if (aj->owned) (void)hipFree((void *)aj->A);
+  delete aj;
+}
+size_t lf_ajtai_kappa(const lf_ajtai *aj) { return aj ? aj->kappa : 0; }
+size_t lf_ajtai_width(const lf_ajtai *aj) { return aj ? aj->ncols : 0; }
+int lf_ajtai_d(const lf_ajtai *aj) { return aj ? aj->d : 0; }
+
+int lf_ajtai_commit(lf_ctx *c, const lf_ajtai *aj, const uint64_t *f, size_t f_len, uint64_t *cm, int repr) {
+  if (!c || !aj || !f || !cm) return LF_ERR_INVALID_ARG;
+  LF_TRY(check_repr(c, repr));
+  if (f_len != aj->ncols)  // commitment_scheme.rs:38-43
+    return fail(c, LF_ERR_WRONG_WITNESS_LENGTH, "Wrong length of the witness");
+  DevBuf df, dcm;
+  LF_TRY(upload(c, df, f, f_len * aj->d, repr));
+  LF_TRY(dev_alloc(c, dcm, aj->kappa * aj->d));
+  const uint64_t *v = df.p;
+  LF_TRY(ajtai_launch(c, aj, &v, 1, dcm.p));
+  LF_TRY(download(c, cm, dcm, aj->kappa * aj->d, repr));
+  return lf_ctx_sync(c);
+}
+
+int lf_witness_from_w_ccs(lf_ctx *c, const lf_params *pr, const uint64_t *w, size_t W, uint64_t *fc,
+                          uint64_t *f, int repr) {
+  if (!c || (!w && W) || !fc || !f) return LF_ERR_INVALID_ARG;
+  LF_TRY(check_repr(c, repr));
+  int lb, lbs;
+  LF_TRY(check_params(c, pr, lb, lbs));
+  const int d = pr->d;
+  const size_t N = W * pr->L;
+  DevBuf dw, dfc, df;
+  LF_TRY(upload(c, dw, w, W * d, repr));
+  LF_TRY(dev_alloc(c, dfc, N * d));
+  LF_TRY(dev_alloc(c, df, N * d));
+  LF_TRY(lf_dev_witness_from_w_ccs(c, pr, dw.p, W, dfc.p, df.p));
+  LF_TRY(download(c, fc, dfc, N * d, repr));
+  LF_TRY(download(c, f, df, N * d, repr));
+  return lf_ctx_sync(c);
+}
+
+int lf_witness_from_f(lf_ctx *c, const lf_params *pr, const uint64_t *f, size_t N, uint64_t *fc,
+                      uint64_t *w, int repr) {
+  if (!c || (!f && N) || !fc || !w) return LF_ERR_INVALID_ARG;
+  LF_TRY(check_repr(c, repr));
+  int lb, lbs;
+  LF_TRY(check_params(c, pr, lb, lbs));
+  if (N % pr->L) return fail(c, LF_ERR_INCORRECT_LENGTH, "N must be a multiple of L");
+  const int d = pr->d;
+  DevBuf df, dfc, dw;
+  LF_TRY(upload(c, df, f, N * d, repr));
+  LF_TRY(dev_alloc(c, dfc, N * d));
+  LF_TRY(dev_alloc(c, dw, N / pr->L * d));
+  LF_TRY(lf_dev_witness_from_f(c, pr, df.p, N, dfc.p, dw.p));
+  LF_TRY(download(c, fc, dfc, N * d, repr));
+  LF_TRY(download(c, w, dw, N / pr->L * d, repr));
+  return lf_ctx_sync(c);
+}
+
+int lf_decompose_witness(lf_ctx *c, const lf_params *pr, const uint64_t *fc, size_t N, uint64_t *fck,
+                         uint64_t *fk, uint64_t *wk, int repr) {
+  if (!c || (!fc && N) || !fck || !fk || !wk) return LF_ERR_INVALID_ARG;
+  LF_TRY(check_repr(c, repr));
+  int lb, lbs;
+  LF_TRY(check_params(c, pr, lb, lbs));
+  if (N % pr->L) return fail(c, LF_ERR_INCORRECT_LENGTH, "N must be a multiple of L");
+  const int d = pr->d, K = pr->K;
+  DevBuf dfc, dfck, dfk, dwk;
+  LF_TRY(upload(c, dfc, fc, N * d, repr));
+  LF_TRY(dev_alloc(c, dfck, K * N * d));
+  LF_TRY(dev_alloc(c, dfk, K * N * d));
+  LF_TRY(dev_alloc(c, dwk, K * (N / pr->L) * d));
+  LF_TRY(lf_dev_decompose_witness(c, pr, dfc.p, N, dfck.p, dfk.p, dwk.p));
+  LF_TRY(download(c, fck, dfck, K * N * d, repr));
+  LF_TRY(download(c, fk, dfk, K * N * d, repr));
+  LF_TRY(download(c, wk, dwk, K * (N / pr->L) * d, repr));
+  return lf_ctx_sync(c);
+}
+
+int lf_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, const uint64_t *z, size_t z_len, size_t l,
+              uint64_t *fc, uint64_t *f, uint64_t *cm, int repr) {
+  if (!c || !aj || !z || !fc || !f || !cm) return LF_ERR_INVALID_ARG;
+  LF_TRY(check_repr(c, repr));
+  int lb, lbs;
+  LF_TRY(check_params(c, pr, lb, lbs));
+  if (pr->d != aj->d) return fail(c, LF_ERR_INVALID_ARG, "params ring != Ajtai ring");
+  if (z_len < l + 1) return fail(c, LF_ERR_INCORRECT_LENGTH, "z shorter than l + 1");
+  const int d = pr->d;
+  const size_t W = z_len - l - 1, N = W * pr->L;  // main.rs:354-355: w_ccs = z[l+1..]
+  if (N != aj->ncols) return fail(c, LF_ERR_WRONG_WITNESS_LENGTH, "Wrong length of the witness");
+  DevBuf dw, dfc, df, dcm;
+  LF_TRY(upload(c, dw, z + (l + 1) * d, W * d, repr));
+  LF_TRY(dev_alloc(c, dfc, N * d));
+  LF_TRY(dev_alloc(c, df, N * d));
+  LF_TRY(dev_alloc(c, dcm, aj->kappa * d));
+  LF_TRY(lf_dev_witness_from_w_ccs(c, pr, dw.p, W, dfc.p, df.p));
+  const uint64_t *v = df.p;
+  LF_TRY(ajtai_launch(c, aj, &v, 1, dcm.p));
+  LF_TRY(download(c, fc, dfc, N * d, repr));
+  LF_TRY(download(c, f, df, N * d, repr));
+  LF_TRY(download(c, cm, dcm, aj->kappa * d, repr));
+  return lf_ctx_sync(c);
+}
+
+int lf_fold_hot(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, const uint64_t *acc_cm,
+                const uint64_t *acc_fc, const uint64_t *cm_i, const uint64_t *wi_fc, size_t N,
+                const uint64_t *rho, uint64_t *y, uint64_t *f0, uint64_t *f0c, uint64_t *w0, uint64_t *cm0,
+                int repr) {
+  if (!c || !aj || !acc_cm || !acc_fc || !cm_i || !wi_fc || !rho || !y || !f0 || !f0c || !w0 || !cm0)
+    return LF_ERR_INVALID_ARG;
+  LF_TRY(check_repr(c, repr));
+  int lb, lbs;
+  LF_TRY(check_params(c, pr, lb, lbs));
+  if (pr->d != aj->d) return fail(c, LF_ERR_INVALID_ARG, "params ring != Ajtai ring");
+  if (N % pr->L) return fail(c, LF_ERR_INCORRECT_LENGTH, "N must be a multiple of L");
+  const int d = pr->d, K = pr->K;
+  const size_t W = N / pr->L, kd = aj->kappa * d;
+  DevBuf dacm, dafc, dcmi, dwfc, drho, dfck[2], dfk[2], dwk[2], dy, df0, df0c, dw0, dcm0;
+  LF_TRY(upload(c, dacm, acc_cm, kd, repr));
+  LF_TRY(upload(c, dafc, acc_fc, N * d, repr));
+  LF_TRY(upload(c, dcmi, cm_i, kd, repr));
+  LF_TRY(upload(c, dwfc, wi_fc, N * d, repr));
+  LF_TRY(upload(c, drho, rho, 2 * (size_t)K * d, repr));
+  for (int s = 0; s < 2; s++) {
+    LF_TRY(dev_alloc(c, dfck[s], K * N * d));
+    LF_TRY(dev_alloc(c, dfk[s], K * N * d));
+    LF_TRY(dev_alloc(c, dwk[s], K * W * d));
+  }
+  LF_TRY(dev_alloc(c, dy, 2 * K * kd));
+  LF_TRY(dev_alloc(c, df0, N * d));
+  LF_TRY(dev_alloc(c, df0c, N * d));
+  LF_TRY(dev_alloc(c, dw0, W * d));
+  LF_TRY(dev_alloc(c, dcm0, kd));
+  lf_fold_step_bufs b{};
+  b.acc_cm = dacm.p;
+  b.acc_f_coeff = dafc.p;
+  b.rho = drho.p;
+  for (int s = 0; s < 2; s++) {
+    b.fk_coeff[s] = dfck[s].p;
+    b.fk[s] = dfk[s].p;
+    b.wk[s] = dwk[s].p;
+    b.y[s] = dy.p + (size_t)s * K * kd;
+  }
+  b.f0 = df0.p;
+  b.f0_coeff = df0c.p;
+  b.w_ccs0 = dw0.p;
+  b.cm0 = dcm0.p;
+  LF_TRY(fold_core(c, aj, pr, lb, lbs, W, &b, dcmi.p, dwfc.p));
+  LF_TRY(download(c, y, dy, 2 * K * kd, repr));
+  LF_TRY(download(c, f0, df0, N * d, repr));
+  LF_TRY(download(c, f0c, df0c, N * d, repr));
+  LF_TRY(download(c, w0, dw0, W * d, repr));
+  LF_TRY(download(c, cm0, dcm0, kd, repr));
+  return lf_ctx_sync(c);
+}
+
+int lf_short_challenge(const uint8_t *bs, size_t nbytes, int d, uint64_t *coeffs) {
+  // cyclotomic-rings rings/goldilocks.rs:41-67 (3 bytes -> 4 six-bit coefficients - 32)
+  if (!bs || !coeffs || d % 4) return LF_ERR_INVALID_ARG;
+  if (nbytes != (size_t)(3 * d / 4)) return LF_ERR_CHALLENGE_BYTES;
+  for (int i = 0; i < d / 4; i++) {
+    int x[4];
+    x[0] = (bs[3 * i] & 0x3f) - 32;
+    x[1] = (((bs[3 * i] & 0xc0) >> 6) | ((bs[3 * i + 1] & 0x0f) << 2)) - 32;
+    x[2] = (((bs[3 * i + 1] & 0xf0) >> 4) | ((bs[3 * i + 2] & 0x03) << 4)) - 32;
+    x[3] = ((bs[3 * i + 2] & 0xfc) >> 2) - 32;
+    for (int k = 0; k < 4; k++) coeffs[4 * i + k] = x[k] < 0 ? gl::P - (uint64_t)(-x[k]) : (uint64_t)x[k];
+  }
+  return LF_OK;
+}
+
+int lf_poseidon2_permute(lf_ctx *c, uint64_t *states, size_t n) {
+  if (!c || (!states && n)) return LF_ERR_INVALID_ARG;
+  DevBuf b;
+  LF_TRY(upload(c, b, states, 16 * n, LF_REPR_CANONICAL));
+  LF_HIP(c, lfk::p2_permute(b.p, n, c->cur));
+  LF_TRY(download(c, states, b, 16 * n, LF_REPR_CANONICAL));
+  return lf_ctx_sync(c);
+}
+
+// ---------------------------------------------------------------- device API
+int lf_dev_crt(lf_ctx *c, uint64_t *e, size_t n, int d) {
+  if (!c || (!e && n)) return LF_ERR_INVALID_ARG;
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  Tables *t;
+  LF_TRY(get_tables(c, d, t));
+  LF_HIP(c, lfk::transform(e, n, d, true, t->fwd, c->cur));
+  return LF_OK;
+}
+int lf_dev_icrt(lf_ctx *c, uint64_t *e, size_t n, int d) {
+  if (!c || (!e && n)) return LF_ERR_INVALID_ARG;
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  Tables *t;
+  LF_TRY(get_tables(c, d, t));
+  LF_HIP(c, lfk::transform(e, n, d, false, t->inv, c->cur));
+  return LF_OK;
+}
+int lf_dev_ring_mul(lf_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t n, int d) {
+  if (!c) return LF_ERR_INVALID_ARG;
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  LF_HIP(c, lfk::slot_mul(a, b, out, n, d, c->cur));
+  return LF_OK;
+}
+int lf_dev_to_montgomery(lf_ctx *c, uint64_t *x, size_t n) {
+  if (!c) return LF_ERR_INVALID_ARG;
+  LF_HIP(c, lfk::mont(x, n, true, c->cur));
+  return LF_OK;
+}
+int lf_dev_from_montgomery(lf_ctx *c, uint64_t *x, size_t n) {
+  if (!c) return LF_ERR_INVALID_ARG;
+  LF_HIP(c, lfk::mont(x, n, false, c->cur));
+  return LF_OK;
+}
+int lf_dev_witness_from_w_ccs(lf_ctx *c, const lf_params *pr, const uint64_t *w, size_t W, uint64_t *fc,
+                              uint64_t *f) {
+  if (!c) return LF_ERR_INVALID_ARG;
+  int lb, lbs;
+  LF_TRY(check_params(c, pr, lb, lbs));
+  Tables *t;
+  LF_TRY(get_tables(c, pr->d, t));
+  LF_HIP(c, lfk::from_w_ccs(w, W, pr->d, lb, pr->L, fc, f, t->fwd, t->inv, c->d_err, c->cur));
+  return LF_OK;
+}
+int lf_dev_witness_from_f(lf_ctx *c, const lf_params *pr, const uint64_t *f, size_t N, uint64_t *fc,
+                          uint64_t *w) {
+  if (!c) return LF_ERR_INVALID_ARG;
+  int lb, lbs;
+  LF_TRY(check_params(c, pr, lb, lbs));
+  if (N % pr->L) return fail(c, LF_ERR_INCORRECT_LENGTH, "N must be a multiple of L");
+  Tables *t;
+  LF_TRY(get_tables(c, pr->d, t));
+  LF_HIP(c, lfk::from_f(f, N, pr->d, lb, pr->L, fc, w, t->inv, c->cur));
+  return LF_OK;
+}
+int lf_dev_decompose_witness(lf_ctx *c, const lf_params *pr, const uint64_t *fc, size_t N, uint64_t *fck,
+                             uint64_t *fk, uint64_t *wk) {
+  if (!c) return LF_ERR_INVALID_ARG;
+  int lb, lbs;
+  LF_TRY(check_params(c, pr, lb, lbs));
+  if (N % pr->L) return fail(c, LF_ERR_INCORRECT_LENGTH, "N must be a multiple of L");
+  Tables *t;
+  LF_TRY(get_tables(c, pr->d, t));
+  LF_HIP(c, lfk::decompose_witness(fc, N, pr->d, lb, pr->L, lbs, pr->K, fck, fk, wk, t->fwd, c->d_err, c->cur));
+  return LF_OK;
+}
+int lf_dev_ajtai_commit(lf_ctx *c, const lf_ajtai *aj, const uint64_t *const *vecs, int nvec, uint64_t *cm) {
+  if (!c || !aj || !vecs || !cm) return LF_ERR_INVALID_ARG;
+  return ajtai_launch(c, aj, vecs, nvec, cm);
+}
+int lf_dev_commit_y0(lf_ctx *c, const lf_params *pr, const uint64_t *cm, uint64_t *y, size_t kappa) {
+  if (!c) return LF_ERR_INVALID_ARG;
+  int lb, lbs;
+  LF_TRY(check_params(c, pr, lb, lbs));
+  LF_HIP(c, lfk::commit_y0(cm, y, kappa, pr->d, lbs, pr->K, c->cur));
+  return LF_OK;
+}
+int lf_dev_fold(lf_ctx *c, int d, const uint64_t *rho, const uint64_t *const *x, int nwit, size_t n,
+                uint64_t *out) {
+  if (!c || !rho || !x || !out || nwit < 1 || nwit > LF_MAX_VECS) return LF_ERR_INVALID_ARG;
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  lfk::VecPtrs vp{};
+  for (int i = 0; i < nwit; i++) vp.p[i] = x[i];
+  LF_HIP(c, lfk::fold(rho, vp, nwit, n, d, out, c->cur));
+  return LF_OK;
+}
+
+int lf_dev_fold_step(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t W, const lf_fold_step_bufs *b) {
+  if (!c || !aj || !b) return LF_ERR_INVALID_ARG;
+  int lb, lbs;
+  LF_TRY(check_params(c, pr, lb, lbs));
+  if (pr->d != aj->d) return fail(c, LF_ERR_INVALID_ARG, "params ring != Ajtai ring");
+  if (W * (size_t)pr->L != aj->ncols) return fail(c, LF_ERR_WRONG_WITNESS_LENGTH, "W*L != Ajtai width");
+  // commit(z) (zkvm main.rs:348-367): Witness::from_w_ccs + A f
+  LF_TRY(lf_dev_witness_from_w_ccs(c, pr, b->w_ccs, W, b->f_coeff, b->f));
+  const uint64_t *v = b->f;
+  LF_TRY(ajtai_launch(c, aj, &v, 1, b->cm));
+  // fold() commit+fold arithmetic
+  return fold_core(c, aj, pr, lb, lbs, W, b, b->cm, b->f_coeff);
+}
+
+int lf_dev_poseidon2_permute(lf_ctx *c, uint64_t *states, size_t n) {
+  if (!c) return LF_ERR_INVALID_ARG;
+  LF_HIP(c, lfk::p2_permute(states, n, c->cur));
+  return LF_OK;
+}
+int lf_dev_fill_uniform(lf_ctx *c, uint64_t *out, size_t n, uint64_t seed) {
+  if (!c) return LF_ERR_INVALID_ARG;
+  LF_HIP(c, lfk::fill_uniform(out, n, seed, c->cur));
+  return LF_OK;
+}
+int lf_dev_modp_sum(lf_ctx *c, const uint64_t *in, int nparts, size_t len, uint64_t *out) {
+  if (!c || nparts < 1) return LF_ERR_INVALID_ARG;
+  LF_HIP(c, lfk::modp_sum(in, nparts, len, out, c->cur));
+  return LF_OK;
+}
+
+int lf_dev_limb_split(lf_ctx *c, const uint64_t *x, size_t n, uint64_t *lo, uint64_t *hi) {
+  if (!c) return LF_ERR_INVALID_ARG;
+  LF_HIP(c, lfk::limb_split(x, n, lo, hi, c->cur));
+  return LF_OK;
+}
+int lf_dev_limb_join(lf_ctx *c, const uint64_t *lo, const uint64_t *hi, size_t n, uint64_t *out) {
+  if (!c) return LF_ERR_INVALID_ARG;
+  LF_HIP(c, lfk::limb_join(lo, hi, n, out, c->cur));
+  return LF_OK;
+}
+
+}  // extern "C"

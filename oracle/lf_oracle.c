@@ -75,6 +75,7 @@ static void init_consts(void) {
 /* GL/ntt.rs:348-437 -- isomorphisms between Fq[X]/(X^3 - w^k) and Fq3 */
 void lfo_phi72_homogenize(uint64_t *c) { /* GL/ntt.rs:326-334 */
   uint64_t t;
+  pthread_once(&once, init_consts);
   c[4] = neg(c[4]);                                  /* 13: c1 = -c1 */
   c[7] = lfo_mul(c[7], W24[2]);                      /* 7 */
   c[8] = lfo_mul(c[8], W24[4]);
@@ -95,6 +96,7 @@ void lfo_phi72_homogenize(uint64_t *c) { /* GL/ntt.rs:326-334 */
 }
 void lfo_phi72_dehomogenize(uint64_t *c) { /* GL/ntt.rs:338-346 */
   uint64_t t;
+  pthread_once(&once, init_consts);
   c[4] = neg(c[4]);
   c[7] = lfo_mul(c[7], W24[22]);
   c[8] = lfo_mul(c[8], W24[20]);
