@@ -143,4 +143,57 @@ LF_HD uint64_t acc_reduce(const Acc &s) {
   return sub(r, t);
 }
 
+// ---- column accumulator: sum of 64x64-bit products kept as
+//   S0 + 2^64 c0  (sum a0*b0)  +  2^32 (S1 + 2^64 c1)  (sum a0*b1 + a1*b0)
+//   + 2^64 (S2 + 2^64 c2)  (sum a1*b1)
+// On the device each 32x32 partial product is one v_mad_u64_u32 whose carry-out
+// feeds a v_addc_co_u32 counter: 8 VALU instructions per multiply-accumulate
+// (the compiler's own lowering of a*b / __umul64hi needs ~22).
+struct CAcc {
+  uint64_t s0, s1, s2;
+  uint32_t c0, c1, c2;
+};
+LF_HD void cacc_zero(CAcc &a) {
+  a.s0 = a.s1 = a.s2 = 0;
+  a.c0 = a.c1 = a.c2 = 0;
+}
+LF_HD void cacc_mad(CAcc &a, uint64_t x, uint64_t y) {
+  uint32_t x0 = (uint32_t)x, x1 = (uint32_t)(x >> 32), y0 = (uint32_t)y, y1 = (uint32_t)(y >> 32);
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t cc;
+  asm volatile(
+      "v_mad_u64_u32 %0, %6, %7, %9, %0\n\t"
+      "v_addc_co_u32_e64 %3, %6, 0, %3, %6\n\t"
+      "v_mad_u64_u32 %1, %6, %7, %10, %1\n\t"
+      "v_addc_co_u32_e64 %4, %6, 0, %4, %6\n\t"
+      "v_mad_u64_u32 %1, %6, %8, %9, %1\n\t"
+      "v_addc_co_u32_e64 %4, %6, 0, %4, %6\n\t"
+      "v_mad_u64_u32 %2, %6, %8, %10, %2\n\t"
+      "v_addc_co_u32_e64 %5, %6, 0, %5, %6"
+      : "+v"(a.s0), "+v"(a.s1), "+v"(a.s2), "+v"(a.c0), "+v"(a.c1), "+v"(a.c2), "=&s"(cc)
+      : "v"(x0), "v"(x1), "v"(y0), "v"(y1));
+#else
+  auto addc = [](uint64_t &s, uint32_t &c, uint64_t p) {
+    s += p;
+    c += s < p;
+  };
+  addc(a.s0, a.c0, (uint64_t)x0 * y0);
+  addc(a.s1, a.c1, (uint64_t)x0 * y1);
+  addc(a.s1, a.c1, (uint64_t)x1 * y0);
+  addc(a.s2, a.c2, (uint64_t)x1 * y1);
+#endif
+}
+// mod p: 2^64 == EPS, 2^96 == -1, 2^128 == -2^32
+LF_HD uint64_t cacc_reduce(const CAcc &a) {
+  uint64_t r = canon(a.s0);
+  r = add(r, canon((uint64_t)a.c0 * EPS));                      // c0 2^64
+  uint64_t s1l = a.s1 & EPS, s1h = a.s1 >> 32;                 // S1 2^32 = s1l 2^32 + s1h 2^64
+  r = add(r, canon(s1l << 32));
+  r = add(r, canon(s1h * EPS));
+  r = sub(r, canon((uint64_t)a.c1));                           // c1 2^96 = -c1
+  r = add(r, canon(reduce128(0, a.s2)));                       // S2 2^64
+  r = sub(r, canon((uint64_t)a.c2 << 32));                     // c2 2^128 = -c2 2^32
+  return r;
+}
+
 }  // namespace gl

@@ -373,45 +373,87 @@ __global__ void __launch_bounds__(NT<D>::T) k_decompose_nega(const uint64_t *f_c
 // ============================================================ Ajtai commitment
 // LF/commitment/commitment_scheme.rs:37-54 -> LA/matrix.rs:168-178:
 //   cm[v][i] = sum_j A[i][j] (.) f_v[j]    (slot-wise products)
-// Split over (slot chunk, row tile, vector tile, column split); each thread
-// owns one slot position and an R x V tile of lazy 128-bit accumulators; the
-// column-split partials are reduced mod p by k_ajtai_reduce.
+// Work units: (slot chunk, row tile, column split) x vector tile. Each thread
+// owns one slot position and an R x V tile of column accumulators (gl::CAcc,
+// 8 VALU ops per 64x64 MAC). Units that read the same A tile (same slot
+// chunk / row tile / column split, different vector tiles) get block ids
+// that are congruent mod 8, i.e. land on one XCD under round-robin dispatch,
+// so A is re-read from that XCD's L2 rather than HBM (speed only). Loads of
+// column j+1 are issued before the MACs of column j.
+struct AjtaiGrid {
+  int nsc, nrt, nsplit, nvt;  // slot chunks, row tiles, column splits, vector tiles
+  __host__ __device__ int others() const { return nsc * nrt * nsplit; }
+  __host__ __device__ unsigned blocks() const { return (unsigned)(((others() + 7) / 8) * nvt * 8); }
+};
+__device__ __forceinline__ bool ajtai_unit(const AjtaiGrid &g, int &sc, int &rt, int &js, int &vt) {
+  const int L = blockIdx.x;
+  const int lo = L % 8, hi = L / 8;
+  vt = hi % g.nvt;
+  const int other = (hi / g.nvt) * 8 + lo;
+  if (other >= g.others()) return false;
+  sc = other % g.nsc;
+  rt = (other / g.nsc) % g.nrt;
+  js = other / (g.nsc * g.nrt);
+  return true;
+}
+
 template <int R, int V>
 __global__ void __launch_bounds__(256) k_ajtai_nega(const uint64_t *A, size_t kappa, size_t ncols,
                                                    int d, VecPtrs fv, int nvec, size_t jchunk,
-                                                   uint64_t *partial) {
-  const int s = blockIdx.x * 256 + threadIdx.x;  // slot
-  const int i0 = blockIdx.y * R;
-  const int nvt = (nvec + V - 1) / V;
-  const int v0 = (blockIdx.z % nvt) * V;
-  const int js = blockIdx.z / nvt;
+                                                   AjtaiGrid g, uint64_t *partial) {
+  int sc, rt, js, vt;
+  if (!ajtai_unit(g, sc, rt, js, vt)) return;
+  const int s = sc * 256 + threadIdx.x;  // slot
   if (s >= d) return;
+  const int i0 = rt * R, v0 = vt * V;
   const size_t j0 = (size_t)js * jchunk, j1 = min(ncols, j0 + jchunk);
-  Acc acc[R][V];
+  const uint64_t *pa[R];
+  const uint64_t *pb[V];
+#pragma unroll
+  for (int r = 0; r < R; r++) pa[r] = A + ((size_t)min(i0 + r, (int)kappa - 1) * ncols) * d + s;
+#pragma unroll
+  for (int v = 0; v < V; v++) pb[v] = fv.p[min(v0 + v, nvec - 1)] + s;
+  gl::CAcc acc[R][V];
 #pragma unroll
   for (int r = 0; r < R; r++)
 #pragma unroll
-    for (int v = 0; v < V; v++) gl::acc_zero(acc[r][v]);
+    for (int v = 0; v < V; v++) gl::cacc_zero(acc[r][v]);
+  uint64_t a[R], b[V];
+  if (j0 < j1) {
+#pragma unroll
+    for (int r = 0; r < R; r++) a[r] = pa[r][j0 * d];
+#pragma unroll
+    for (int v = 0; v < V; v++) b[v] = pb[v][j0 * d];
+  }
   for (size_t j = j0; j < j1; j++) {
-    uint64_t a[R], b[V];
+    uint64_t an[R], bn[V];
+    const size_t jn = (j + 1 < j1 ? j + 1 : j) * d;
 #pragma unroll
-    for (int r = 0; r < R; r++) a[r] = (i0 + r < (int)kappa) ? A[((i0 + r) * ncols + j) * d + s] : 0;
+    for (int r = 0; r < R; r++) an[r] = pa[r][jn];
 #pragma unroll
-    for (int v = 0; v < V; v++) b[v] = (v0 + v < nvec) ? fv.p[v0 + v][j * d + s] : 0;
+    for (int v = 0; v < V; v++) bn[v] = pb[v][jn];
 #pragma unroll
     for (int r = 0; r < R; r++)
 #pragma unroll
-      for (int v = 0; v < V; v++) gl::acc_mad(acc[r][v], a[r], b[v]);
+      for (int v = 0; v < V; v++) gl::cacc_mad(acc[r][v], a[r], b[v]);
+#pragma unroll
+    for (int r = 0; r < R; r++) a[r] = an[r];
+#pragma unroll
+    for (int v = 0; v < V; v++) b[v] = bn[v];
   }
 #pragma unroll
   for (int r = 0; r < R; r++)
 #pragma unroll
     for (int v = 0; v < V; v++)
       if (i0 + r < (int)kappa && v0 + v < nvec)
-        partial[(((size_t)js * nvec + v0 + v) * kappa + i0 + r) * d + s] = gl::acc_reduce(acc[r][v]);
+        partial[(((size_t)js * nvec + v0 + v) * kappa + i0 + r) * d + s] = gl::cacc_reduce(acc[r][v]);
 }
 
-// Phi_72: lanes = 8 Fq3 slots x 8 column phases; R x V tile of Fq3 accumulators.
+// Phi_72: lanes = 8 Fq3 slots x 8 column phases; R x V tile of Fq3 accumulators
+// (9 column-accumulated products per Fq3 MAC into 5 sums, ring::fq3acc layout).
+struct Fq3CAcc {
+  gl::CAcc s00, s0n, s1, s1n, s2;
+};
 template <int R, int V>
 __global__ void __launch_bounds__(256) k_ajtai_phi72(const uint64_t *A, size_t kappa, size_t ncols,
                                                     VecPtrs fv, int nvec, size_t jchunk,
@@ -423,48 +465,63 @@ __global__ void __launch_bounds__(256) k_ajtai_phi72(const uint64_t *A, size_t k
   const int v0 = (blockIdx.z % nvt) * V;
   const int js = blockIdx.x * 4 + wave;  // column split index
   const size_t j0 = (size_t)js * jchunk, j1 = min(ncols, j0 + jchunk);
-  ring::Fq3Acc acc[R][V];
-#pragma unroll
-  for (int r = 0; r < R; r++)
-#pragma unroll
-    for (int v = 0; v < V; v++) ring::fq3acc_zero(acc[r][v]);
-  if (j0 < ncols) {
-    for (size_t j = j0 + ph; j < j1; j += 8) {
-      uint64_t a[R][3], b[V][3];
-#pragma unroll
-      for (int r = 0; r < R; r++) {
-        const uint64_t *pa = A + ((size_t)(i0 + r) * ncols + j) * 24 + 3 * slot;
-        bool ok = i0 + r < (int)kappa;
-        a[r][0] = ok ? pa[0] : 0;
-        a[r][1] = ok ? pa[1] : 0;
-        a[r][2] = ok ? pa[2] : 0;
-      }
-#pragma unroll
-      for (int v = 0; v < V; v++) {
-        bool ok = v0 + v < nvec;
-        const uint64_t *pb = ok ? fv.p[v0 + v] + j * 24 + 3 * slot : nullptr;
-        b[v][0] = ok ? pb[0] : 0;
-        b[v][1] = ok ? pb[1] : 0;
-        b[v][2] = ok ? pb[2] : 0;
-      }
-#pragma unroll
-      for (int r = 0; r < R; r++)
-#pragma unroll
-        for (int v = 0; v < V; v++)
-          ring::fq3acc_mad(acc[r][v], a[r][0], a[r][1], a[r][2], b[v][0], b[v][1], b[v][2]);
-    }
-  }
-  // reduce each tile entry to canonical Fq3, then sum the 8 column phases (mod p)
+  Fq3CAcc acc[R][V];
 #pragma unroll
   for (int r = 0; r < R; r++)
 #pragma unroll
     for (int v = 0; v < V; v++) {
+      gl::cacc_zero(acc[r][v].s00);
+      gl::cacc_zero(acc[r][v].s0n);
+      gl::cacc_zero(acc[r][v].s1);
+      gl::cacc_zero(acc[r][v].s1n);
+      gl::cacc_zero(acc[r][v].s2);
+    }
+  for (size_t j = j0 + ph; j < j1; j += 8) {
+    uint64_t a[R][3], b[V][3];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const uint64_t *p = A + ((size_t)min(i0 + r, (int)kappa - 1) * ncols + j) * 24 + 3 * slot;
+      a[r][0] = p[0];
+      a[r][1] = p[1];
+      a[r][2] = p[2];
+    }
+#pragma unroll
+    for (int v = 0; v < V; v++) {
+      const uint64_t *p = fv.p[min(v0 + v, nvec - 1)] + j * 24 + 3 * slot;
+      b[v][0] = p[0];
+      b[v][1] = p[1];
+      b[v][2] = p[2];
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++)
+#pragma unroll
+      for (int v = 0; v < V; v++) {
+        Fq3CAcc &q = acc[r][v];
+        gl::cacc_mad(q.s00, a[r][0], b[v][0]);
+        gl::cacc_mad(q.s0n, a[r][1], b[v][2]);
+        gl::cacc_mad(q.s0n, a[r][2], b[v][1]);
+        gl::cacc_mad(q.s1, a[r][0], b[v][1]);
+        gl::cacc_mad(q.s1, a[r][1], b[v][0]);
+        gl::cacc_mad(q.s1n, a[r][2], b[v][2]);
+        gl::cacc_mad(q.s2, a[r][0], b[v][2]);
+        gl::cacc_mad(q.s2, a[r][1], b[v][1]);
+        gl::cacc_mad(q.s2, a[r][2], b[v][0]);
+      }
+  }
+  // c0 = s00 + 2^40 s0n, c1 = s1 + 2^40 s1n, c2 = s2; then sum the 8 column phases
+#pragma unroll
+  for (int r = 0; r < R; r++)
+#pragma unroll
+    for (int v = 0; v < V; v++) {
+      const Fq3CAcc &q = acc[r][v];
       uint64_t c[3];
-      ring::fq3acc_final(acc[r][v], c);
+      c[0] = gl::add(gl::cacc_reduce(q.s00), gl::mul_pow2(gl::cacc_reduce(q.s0n), 40));
+      c[1] = gl::add(gl::cacc_reduce(q.s1), gl::mul_pow2(gl::cacc_reduce(q.s1n), 40));
+      c[2] = gl::cacc_reduce(q.s2);
 #pragma unroll
       for (int off = 8; off < 64; off <<= 1)
 #pragma unroll
-        for (int q = 0; q < 3; q++) c[q] = gl::add(c[q], __shfl_xor(c[q], off));
+        for (int k = 0; k < 3; k++) c[k] = gl::add(c[k], __shfl_xor(c[k], off));
       if (ph == 0 && i0 + r < (int)kappa && v0 + v < nvec) {  // empty splits write zeros
         uint64_t *o = partial + (((size_t)js * nvec + v0 + v) * kappa + i0 + r) * 24 + 3 * slot;
         o[0] = c[0];
@@ -757,10 +814,6 @@ hipError_t decompose_witness(const uint64_t *f_coeff, size_t N, int d, int lb, i
   return hipGetLastError();
 }
 
-size_t ajtai_partial_elems(size_t kappa, size_t ncols, int d, int nvec) {
-  size_t nsplit = ajtai_nsplit(ncols, d, nvec);
-  return nsplit * (size_t)nvec * kappa * (size_t)d;
-}
 int ajtai_nsplit(size_t ncols, int d, int nvec) {
   if (d == 24) {
     // one wave per column split; ~64 columns per lane phase minimum
@@ -768,31 +821,40 @@ int ajtai_nsplit(size_t ncols, int d, int nvec) {
     if (want > 1024) want = 1024;
     return (int)((want + 3) / 4 * 4);
   }
-  size_t want = (ncols + 255) / 256;
-  if (want > 64) want = 64;
+  // enough units to fill 256 CUs: (d/256) slot chunks x (kappa/R) row tiles x nsplit x nvt
+  size_t want = (ncols + 127) / 128;
+  if (want > 40) want = 40;
   if (want < 1) want = 1;
   return (int)want;
+}
+size_t ajtai_partial_elems(size_t kappa, size_t ncols, int d, int nvec) {
+  size_t nsplit = ajtai_nsplit(ncols, d, nvec);
+  return nsplit * (size_t)nvec * kappa * (size_t)d;
 }
 
 hipError_t ajtai_commit(const uint64_t *A, size_t kappa, size_t ncols, int d, const VecPtrs &fv,
                         int nvec, uint64_t *partial, uint64_t *cm, hipStream_t st, hipEvent_t ev0,
                         hipEvent_t ev1) {
   if (nvec <= 0 || nvec > LF_MAX_VECS) return hipErrorInvalidValue;
-  if (ev0) (void)hipEventRecord(ev0, st);
   const int nsplit = ajtai_nsplit(ncols, d, nvec);
   const size_t jchunk = (ncols + nsplit - 1) / nsplit;
+  if (ev0) (void)hipEventRecord(ev0, st);
   if (d == 24) {
     constexpr int R = 2, V = 2;
     const int nvt = (nvec + V - 1) / V;
     dim3 grid(nsplit / 4, (unsigned)((kappa + R - 1) / R), nvt);
     hipLaunchKernelGGL((k_ajtai_phi72<R, V>), grid, dim3(256), 0, st, A, kappa, ncols, fv, nvec, jchunk,
                        partial);
+  } else if (nvec == 1) {
+    constexpr int R = 8, V = 1;
+    AjtaiGrid g{(d + 255) / 256, (int)((kappa + R - 1) / R), nsplit, 1};
+    hipLaunchKernelGGL((k_ajtai_nega<R, V>), dim3(g.blocks()), dim3(256), 0, st, A, kappa, ncols, d, fv,
+                       nvec, jchunk, g, partial);
   } else {
     constexpr int R = 4, V = 4;
-    const int nvt = (nvec + V - 1) / V;
-    dim3 grid((unsigned)((d + 255) / 256), (unsigned)((kappa + R - 1) / R), (unsigned)(nvt * nsplit));
-    hipLaunchKernelGGL((k_ajtai_nega<R, V>), grid, dim3(256), 0, st, A, kappa, ncols, d, fv, nvec, jchunk,
-                       partial);
+    AjtaiGrid g{(d + 255) / 256, (int)((kappa + R - 1) / R), nsplit, (nvec + V - 1) / V};
+    hipLaunchKernelGGL((k_ajtai_nega<R, V>), dim3(g.blocks()), dim3(256), 0, st, A, kappa, ncols, d, fv,
+                       nvec, jchunk, g, partial);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

@@ -197,12 +197,17 @@ int drain_timing(lf_ctx *c) {
   return LF_OK;
 }
 
-// the commit+fold arithmetic of fold() on device buffers (everything but commit(z))
+// The commit+fold arithmetic of fold() on device buffers. When `commit_f` is
+// given (the fused device step), commit(z)'s A.f rides in the same pass over A
+// as the 2(K-1) decomposition commitments (29 vectors, one read of A) and its
+// result lands in `commit_cm`, which is then cm_i.
 int fold_core(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lbs, size_t W,
-              const lf_fold_step_bufs *b, const uint64_t *cm_i, const uint64_t *wi_f_coeff) {
+              const lf_fold_step_bufs *b, const uint64_t *cm_i, const uint64_t *wi_f_coeff,
+              const uint64_t *commit_f = nullptr, uint64_t *commit_cm = nullptr) {
   const int d = pr->d, L = pr->L, K = pr->K;
   const size_t N = W * (size_t)L, kappa = aj->kappa;
-  if (2 * K > LF_MAX_VECS) return fail(c, LF_ERR_INVALID_ARG, "2K must be <= 32");
+  if (2 * K > LF_MAX_VECS || 2 * (K - 1) + (commit_f ? 1 : 0) > LF_MAX_VECS)
+    return fail(c, LF_ERR_INVALID_ARG, "2K must be <= 32");
   if (aj->ncols != N) return fail(c, LF_ERR_WRONG_WITNESS_LENGTH, "witness length != Ajtai width");
   Tables *t;
   LF_TRY(get_tables(c, d, t));
@@ -213,6 +218,11 @@ int fold_core(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lb
                                      t->fwd, c->d_err, c->cur));
   // commit_witnesses: 2(K-1) commitments sharing one pass over A (decomposition.rs:185-188)
   std::vector<const uint64_t *> vecs;
+  const int extra = commit_f ? 1 : 0;
+  if (commit_f) {
+    vecs.push_back(commit_f);
+    cm_i = commit_cm;
+  }
   for (int s = 0; s < 2; s++)
     for (int k = 1; k < K; k++) vecs.push_back(b->fk[s] + (size_t)k * N * d);
   const size_t kd = kappa * (size_t)d;
@@ -233,9 +243,10 @@ int fold_core(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lb
                                 ea, eb));
     if (c->timing) c->pending.push_back({ea, eb, (int)vecs.size()});
   }
+  if (commit_f) LF_HIP(c, hipMemcpyAsync(commit_cm, ycat, kd * 8, hipMemcpyDeviceToDevice, c->cur));
   const uint64_t *cm_side[2] = {b->acc_cm, cm_i};
   for (int s = 0; s < 2; s++) {
-    LF_HIP(c, hipMemcpyAsync(b->y[s] + kd, ycat + (size_t)s * (K - 1) * kd, (size_t)(K - 1) * kd * 8,
+    LF_HIP(c, hipMemcpyAsync(b->y[s] + kd, ycat + (extra + (size_t)s * (K - 1)) * kd, (size_t)(K - 1) * kd * 8,
                              hipMemcpyDeviceToDevice, c->cur));
     LF_HIP(c, lfk::commit_y0(cm_side[s], b->y[s], kappa, d, lbs, K, c->cur));
   }
@@ -701,12 +712,10 @@ int lf_dev_fold_step(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t 
   LF_TRY(check_params(c, pr, lb, lbs));
   if (pr->d != aj->d) return fail(c, LF_ERR_INVALID_ARG, "params ring != Ajtai ring");
   if (W * (size_t)pr->L != aj->ncols) return fail(c, LF_ERR_WRONG_WITNESS_LENGTH, "W*L != Ajtai width");
-  // commit(z) (zkvm main.rs:348-367): Witness::from_w_ccs + A f
+  // commit(z) (zkvm main.rs:348-367): Witness::from_w_ccs; its A f is batched
+  // with the decomposition commitments of fold() in a single pass over A
   LF_TRY(lf_dev_witness_from_w_ccs(c, pr, b->w_ccs, W, b->f_coeff, b->f));
-  const uint64_t *v = b->f;
-  LF_TRY(ajtai_launch(c, aj, &v, 1, b->cm));
-  // fold() commit+fold arithmetic
-  return fold_core(c, aj, pr, lb, lbs, W, b, b->cm, b->f_coeff);
+  return fold_core(c, aj, pr, lb, lbs, W, b, b->cm, b->f_coeff, b->f, b->cm);
 }
 
 int lf_dev_poseidon2_permute(lf_ctx *c, uint64_t *states, size_t n) {

@@ -1,0 +1,102 @@
+"""Summarise rocprofv3 outputs into profiles/ (committed evidence).
+
+usage:
+  python tools/prof_summary.py stats  <prof_dir> <out.md>
+  python tools/prof_summary.py traffic <fetch_dir> <write_dir> <out.json> [--kernel k_ajtai_nega]
+
+`traffic` follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE come from
+separate --pmc passes (TCC slot limits); both are in KiB; on gfx950 FETCH_SIZE
+reports 1/2 of the bytes of a wide coalesced streaming read, so it is doubled.
+"""
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+from collections import defaultdict
+
+
+def find(dirname, suffix):
+    hits = sorted(glob.glob(os.path.join(dirname, "**", f"*{suffix}"), recursive=True))
+    if not hits:
+        raise SystemExit(f"no *{suffix} under {dirname}")
+    return hits[0]
+
+
+def grid(r):
+    if "Grid_Size_X" in r:
+        return f"{r['Grid_Size_X']}x{r.get('Grid_Size_Y', 1)}x{r.get('Grid_Size_Z', 1)}"
+    return str(r.get("Grid_Size", "?"))
+
+
+def short(name):
+    n = name.split("(")[0]
+    return n.replace("void ", "").strip()
+
+
+def stats(prof_dir, out_md):
+    rows = list(csv.DictReader(open(find(prof_dir, "kernel_stats.csv"))))
+    lines = ["| kernel | calls | avg us | total ms | % |", "|---|---|---|---|---|"]
+    for r in rows:
+        lines.append(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
+                     f"{float(r['TotalDurationNs']) / 1e6:.2f} | {float(r['Percentage']):.2f} |")
+    # per-grid breakdown of the Ajtai kernel (batched vs single launches differ in grid)
+    trace = list(csv.DictReader(open(find(prof_dir, "kernel_trace.csv"))))
+    by = defaultdict(list)
+    for t in trace:
+        if "ajtai" in t["Kernel_Name"]:
+            key = (short(t["Kernel_Name"]), grid(t))
+            by[key].append((int(t["End_Timestamp"]) - int(t["Start_Timestamp"])) / 1e3)
+    if by:
+        lines += ["", "| Ajtai launch kind (kernel, grid) | launches | avg us |", "|---|---|---|"]
+        for (k, g), v in sorted(by.items()):
+            lines.append(f"| `{k}` grid={g} | {len(v)} | {sum(v) / len(v):.1f} |")
+    open(out_md, "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+def counter_per_dispatch(d, counter, kernel):
+    f = find(d, "counter_collection.csv")
+    out = defaultdict(float)
+    grids = {}
+    for r in csv.DictReader(open(f)):
+        if kernel not in r["Kernel_Name"] or r["Counter_Name"] != counter:
+            continue
+        did = r["Dispatch_Id"]
+        out[did] += float(r["Counter_Value"])
+        grids[did] = grid(r)
+    return out, grids
+
+
+def traffic(fetch_dir, write_dir, out_json, kernel):
+    fetch, grids = counter_per_dispatch(fetch_dir, "FETCH_SIZE", kernel)
+    write, grids_w = counter_per_dispatch(write_dir, "WRITE_SIZE", kernel)
+    res = defaultdict(lambda: {"fetch_kib": [], "write_kib": []})
+    for did, v in fetch.items():
+        res[grids[did]]["fetch_kib"].append(v)
+    for did, v in write.items():
+        res[grids_w[did]]["write_kib"].append(v)
+    summary = {}
+    for g, r in res.items():
+        fk = sum(r["fetch_kib"]) / max(len(r["fetch_kib"]), 1)
+        wk = sum(r["write_kib"]) / max(len(r["write_kib"]), 1)
+        summary[g] = {"launches": len(r["fetch_kib"]), "fetch_kib_raw": fk, "write_kib": wk,
+                      "hbm_bytes_per_launch": (2 * fk + wk) * 1024}
+    try:
+        rev = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
+    except Exception:
+        rev = "?"
+    doc = {"kernel": kernel, "by_grid": summary, "git": rev,
+           "method": "separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes; bytes = (2*FETCH_SIZE + "
+                     "WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE counts 1/2 of wide streaming reads)"}
+    json.dump(doc, open(out_json, "w"), indent=1)
+    print(json.dumps(doc, indent=1))
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "stats":
+        stats(sys.argv[2], sys.argv[3])
+    elif sys.argv[1] == "traffic":
+        k = sys.argv[sys.argv.index("--kernel") + 1] if "--kernel" in sys.argv else "k_ajtai"
+        traffic(sys.argv[2], sys.argv[3], sys.argv[4], k)
