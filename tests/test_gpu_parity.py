@@ -320,3 +320,24 @@ def test_fill_uniform_and_modp_sum(ctx):
     ctx.sync()
     hp = parts.cpu().numpy().view(np.uint64).reshape(4, 1000).astype(object)
     assert [int(v) for v in out.cpu().numpy().view(np.uint64)] == [int(v) % P for v in hp.sum(0)]
+
+
+def test_limb_transport_roundtrip(ctx):
+    # RCCL transport of field vectors (latticeum_amd.dist): limb sums over ranks join mod p
+    import torch
+    from latticeum_amd.dist import HipLimbOps
+    ops = HipLimbOps(ctx)
+    parts = [rand(5000, 40 + r) for r in range(3)]
+    lo_sum = torch.zeros(5000, dtype=torch.int64, device="cuda")
+    hi_sum = torch.zeros(5000, dtype=torch.int64, device="cuda")
+    for x in parts:
+        t = torch.from_numpy(x.view(np.int64).copy()).cuda()
+        lo, hi = torch.empty_like(t), torch.empty_like(t)
+        ops.split(t, lo, hi)
+        lo_sum += lo
+        hi_sum += hi
+    out = torch.empty_like(lo_sum)
+    ops.join(lo_sum, hi_sum, out)
+    ctx.sync()
+    want = sum(x.astype(object) for x in parts) % P
+    assert [int(v) for v in out.cpu().numpy().view(np.uint64)] == [int(v) for v in want]
