@@ -88,7 +88,9 @@ int lf_ctx_create(int device, lf_ctx **out);
 void lf_ctx_destroy(lf_ctx *ctx);
 const char *lf_status_string(int status);
 const char *lf_ctx_last_error(const lf_ctx *ctx);
-/* stream used by lf_dev_* (hipStream_t); NULL restores the context's own */
+/* stream used by all work of this context (hipStream_t). A new context uses a
+ * non-blocking stream of its own; NULL selects the HIP default (null) stream,
+ * which is what torch's default current stream is. */
 int lf_ctx_set_stream(lf_ctx *ctx, void *hip_stream);
 void *lf_ctx_get_stream(const lf_ctx *ctx);
 /* wait for the stream; returns LF_ERR_DECOMPOSITION_OVERFLOW (and clears it)
@@ -118,6 +120,10 @@ void lf_ajtai_destroy(lf_ajtai *aj);
 size_t lf_ajtai_kappa(const lf_ajtai *aj);
 size_t lf_ajtai_width(const lf_ajtai *aj);
 int lf_ajtai_d(const lf_ajtai *aj);
+/* 1 when the scheme keeps A in i8-MFMA fragment order (X^d+1 rings, kappa <= 32;
+ * the AoS matrix given to lf_ajtai_create_device is then no longer read and may
+ * be freed), 0 when commitments run on the VALU from the AoS matrix */
+int lf_ajtai_layout(const lf_ajtai *aj);
 /* commit_ntt: f has f_len NTT elements (must equal width), cm receives kappa */
 int lf_ajtai_commit(lf_ctx *ctx, const lf_ajtai *aj, const uint64_t *f, size_t f_len, uint64_t *cm,
                     int repr);

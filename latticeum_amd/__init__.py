@@ -219,6 +219,11 @@ class AjtaiCommitmentScheme:
             ctx.check(ctx.lib.lf_ajtai_create(ctx.h, _ptr(m), kappa, ncols, d, repr, C.byref(h)))
         self.h = h
         self.kappa, self.width, self.d = kappa, ncols, d
+        # with the MFMA layout the scheme owns a fragment-order copy of A, so the
+        # caller's AoS device matrix is no longer read (lf_ajtai_layout == 1)
+        self.layout = ctx.lib.lf_ajtai_layout(h)
+        if self.layout == 1:
+            self._keep = None
 
     def commit_ntt(self, f, repr: int = REPR_CANONICAL) -> np.ndarray:
         x = _u64(f)

@@ -52,6 +52,7 @@ SIGNATURES = {
     "lf_ajtai_kappa": (SZ, [VP]),
     "lf_ajtai_width": (SZ, [VP]),
     "lf_ajtai_d": (I, [VP]),
+    "lf_ajtai_layout": (I, [VP]),
     "lf_ajtai_commit": (I, [VP, VP, VP, SZ, VP, I]),
     "lf_witness_from_w_ccs": (I, [VP, C.POINTER(LfParams), VP, SZ, VP, VP, I]),
     "lf_witness_from_f": (I, [VP, C.POINTER(LfParams), VP, SZ, VP, VP, I]),

@@ -29,8 +29,9 @@ __device__ __forceinline__ uint64_t from_signed(int64_t x) {
 // one balanced digit step (balanced_decomposition/mod.rs:76-91) for b = 2^lb
 __device__ __forceinline__ int64_t bal_digit(int64_t &curr, int lb) {
   const int64_t b = (int64_t)1 << lb, bh = b >> 1;
-  int64_t rem = curr % b;  // truncating, like Rust
-  int64_t q = curr / b;    // truncating
+  // truncating division / remainder by 2^lb (Rust `/` and `%` semantics)
+  int64_t q = (curr + ((curr >> 63) & (b - 1))) >> lb;
+  int64_t rem = curr - (q << lb);
   int64_t ar = rem < 0 ? -rem : rem;
   if (ar <= bh) {
     curr = q;
@@ -702,6 +703,7 @@ static inline unsigned grid_cap(size_t n) { return (unsigned)(n < 65536 ? n : 65
 hipError_t transform(uint64_t *data, size_t n, int d, bool fwd, const ring::NegaTables &tb,
                      hipStream_t st) {
   if (n == 0) return hipSuccess;
+  if (d == 1024 && tb.tw1) return transform_w1024(data, n, fwd, tb, st);
   if (d == 24) {
     if (fwd)
       hipLaunchKernelGGL(k_phi72_transform<true>, dim3(blocks(n, 256)), dim3(256), 0, st, data, n);
@@ -751,6 +753,7 @@ hipError_t from_w_ccs(const uint64_t *w_ccs, size_t W, int d, int lb, int L, uin
                       uint64_t *f, const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err,
                       hipStream_t st) {
   if (W == 0) return hipSuccess;
+  if (d == 1024 && fwd.tw1 && inv.tw1) return from_w_ccs_w1024(w_ccs, W, lb, L, f_coeff, f, fwd, inv, err, st);
   if (d == 24) {
     hipLaunchKernelGGL(k_from_w_ccs_phi72, dim3(blocks(W, 128)), dim3(128), 0, st, w_ccs, W, lb, L,
                        f_coeff, f, err);
@@ -772,6 +775,7 @@ hipError_t from_f(const uint64_t *f, size_t N, int d, int lb, int L, uint64_t *f
                   uint64_t *w_ccs, const ring::NegaTables &inv, hipStream_t st) {
   const size_t W = N / L;
   if (W == 0) return hipSuccess;
+  if (d == 1024 && inv.tw1) return from_f_w1024(f, W, lb, L, f_coeff, w_ccs, inv, st);
   if (d == 24) {
     hipLaunchKernelGGL(k_from_f_phi72, dim3(blocks(W, 128)), dim3(128), 0, st, f, W, lb, L, f_coeff,
                        w_ccs);
@@ -794,6 +798,8 @@ hipError_t decompose_witness(const uint64_t *f_coeff, size_t N, int d, int lb, i
                              const ring::NegaTables &fwd, int *err, hipStream_t st) {
   const size_t W = N / L;
   if (W == 0) return hipSuccess;
+  if (d == 1024 && fwd.tw1 && lbs == 1 && K <= 15 && L <= 8)
+    return decompose_w1024(f_coeff, N, lb, L, K, f_coeff_k, f_k, w_ccs_k, fwd, err, st);
   if (d == 24) {
     if (DEC_GROUPS * L > 256) return hipErrorInvalidValue;
     size_t lds = (size_t)DEC_GROUPS * L * 25 * sizeof(uint64_t);
@@ -862,6 +868,12 @@ hipError_t ajtai_commit(const uint64_t *A, size_t kappa, size_t ncols, int d, co
   const size_t len = (size_t)nvec * kappa * d;
   hipLaunchKernelGGL(k_sum_planes, dim3(blocks(len, 256)), dim3(256), 0, st, partial, nsplit, len, cm,
                      kappa * (size_t)d, kappa * (size_t)d);
+  return hipGetLastError();
+}
+
+hipError_t sum_planes(const uint64_t *partial, int nsplit, size_t len, uint64_t *out, hipStream_t st) {
+  if (len == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sum_planes, dim3(blocks(len, 256)), dim3(256), 0, st, partial, nsplit, len, out, len, len);
   return hipGetLastError();
 }
 

@@ -44,4 +44,25 @@ hipError_t modp_sum(const uint64_t *in, int nparts, size_t len, uint64_t *out, h
 hipError_t limb_split(const uint64_t *x, size_t n, uint64_t *lo, uint64_t *hi, hipStream_t st);
 hipError_t limb_join(const uint64_t *lo, const uint64_t *hi, size_t n, uint64_t *out, hipStream_t st);
 
+hipError_t sum_planes(const uint64_t *partial, int nsplit, size_t len, uint64_t *out, hipStream_t st);
+
+// i8-MFMA Ajtai (ajtai_mfma.hip): negacyclic rings, kappa <= 32, nvec <= 32
+size_t frag_elems(size_t ncols, int d);  // uint4 per fragment buffer
+int mfma_nsplit(size_t ncols);
+hipError_t to_frag(const VecPtrs &rows, int nrows, size_t ncols, int d, uint4 *frag, hipStream_t st);
+hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, size_t ncols, int d, const VecPtrs &fv, int nvec,
+                      uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st, hipEvent_t ev0 = nullptr,
+                      hipEvent_t ev1 = nullptr);
+
+// d = 1024 one-wave-DFT kernels (kernels_w1024.hip)
+hipError_t transform_w1024(uint64_t *data, size_t n, bool fwd, const ring::NegaTables &tb, hipStream_t st);
+hipError_t from_w_ccs_w1024(const uint64_t *w_ccs, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *f,
+                            const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err,
+                            hipStream_t st);
+hipError_t from_f_w1024(const uint64_t *f, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *w_ccs,
+                        const ring::NegaTables &inv, hipStream_t st);
+hipError_t decompose_w1024(const uint64_t *f_coeff, size_t N, int lb, int L, int K, uint64_t *f_coeff_k,
+                           uint64_t *f_k, uint64_t *w_ccs_k, const ring::NegaTables &fwd, int *err,
+                           hipStream_t st);
+
 }  // namespace lfk

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -35,8 +36,12 @@ struct lf_ctx {
   int *d_err = nullptr;
   std::string last_error;
   std::map<int, Tables> tables;
-  uint64_t *scratch = nullptr;
+  uint64_t *scratch = nullptr;  // Ajtai split partial sums
   size_t scratch_elems = 0;
+  uint64_t *ybuf = nullptr;     // batched commitments before they are scattered to y / cm
+  size_t ybuf_elems = 0;
+  uint4 *frag = nullptr;        // vectors in MFMA fragment order (ajtai_mfma.hip)
+  size_t frag_elems = 0;
   bool timing = false;
   std::vector<TimedLaunch> pending;
   std::map<int, std::pair<double, long>> stats;  // nvec -> (ms, count)
@@ -44,6 +49,7 @@ struct lf_ctx {
 
 struct lf_ajtai {
   const uint64_t *A = nullptr;
+  uint4 *Af = nullptr;  // A in i8-MFMA fragment order (negacyclic rings, kappa <= 32)
   bool owned = false;
   size_t kappa = 0, ncols = 0;
   int d = 0;
@@ -98,7 +104,8 @@ int get_tables(lf_ctx *c, int d, Tables *&out) {
   }
   Tables t;
   if (d != 24) {
-    std::vector<uint64_t> h(4 * (size_t)d);
+    const size_t extra = d == 1024 ? 2048 : 0;  // one-wave DFT pass-1 twiddles
+    std::vector<uint64_t> h(4 * (size_t)d + extra);
     const uint64_t psi = gl::pow(7, (gl::P - 1) / (2 * (uint64_t)d));
     const uint64_t psi_inv = gl::inv(psi), w = gl::mul(psi, psi), w_inv = gl::mul(psi_inv, psi_inv);
     const uint64_t dinv = gl::inv((uint64_t)d);
@@ -113,26 +120,48 @@ int get_tables(lf_ctx *c, int d, Tables *&out) {
       x = gl::mul(x, psi_inv);
       y = gl::mul(y, w_inv);
     }
+    if (extra) {
+      // ntt1024.hpp relies on w^64 = 2^156, w^16 = 2^39 (all roots of order <= 64 are shifts)
+      if (gl::pow(w, 64) != gl::mul_pow2(1, 156) || gl::pow(w, 16) != gl::mul_pow2(1, 39))
+        return fail(c, LF_ERR_DEVICE, "unexpected root of unity for the one-wave DFT");
+      for (int lane = 0; lane < 64; lane++)
+        for (int k2 = 0; k2 < 16; k2++) {
+          h[4 * d + lane * 16 + k2] = gl::pow(w, (uint64_t)lane * k2);
+          h[4 * d + 1024 + lane * 16 + k2] = gl::pow(w_inv, (uint64_t)lane * k2);
+        }
+    }
     LF_HIP(c, hipMalloc(&t.mem, h.size() * 8));
     LF_HIP(c, hipMemcpy(t.mem, h.data(), h.size() * 8, hipMemcpyHostToDevice));
-    t.fwd = {t.mem, t.mem + d};
-    t.inv = {t.mem + 2 * d, t.mem + 3 * d};
+    // d = 1024 transforms run the workgroup radix-4 Stockham kernels (measured
+    // 112 M NTT/s vs 74 M NTT/s for the one-wave DFT, tools/kbench.py);
+    // LATTICEUM_AMD_NTT=wave selects the one-wave DFT kernels (kernels_w1024.hip)
+    const char *sel = getenv("LATTICEUM_AMD_NTT");
+    const bool wave = extra && sel && strcmp(sel, "wave") == 0;
+    t.fwd = {t.mem, t.mem + d, wave ? t.mem + 4 * d : nullptr};
+    t.inv = {t.mem + 2 * d, t.mem + 3 * d, wave ? t.mem + 4 * d + 1024 : nullptr};
   }
   out = &(c->tables[d] = t);
   return LF_OK;
 }
 
-int reserve(lf_ctx *c, size_t elems) {
-  if (elems <= c->scratch_elems) return LF_OK;
-  if (c->scratch) {
+template <class T>
+int grow(lf_ctx *c, T *&buf, size_t &have, size_t need) {
+  if (need <= have) return LF_OK;
+  if (buf) {
     LF_HIP(c, hipStreamSynchronize(c->cur));
-    LF_HIP(c, hipFree(c->scratch));
-    c->scratch = nullptr;
-    c->scratch_elems = 0;
+    LF_HIP(c, hipFree(buf));
+    buf = nullptr;
+    have = 0;
   }
-  LF_HIP(c, hipMalloc(&c->scratch, elems * 8));
-  c->scratch_elems = elems;
+  LF_HIP(c, hipMalloc((void **)&buf, need * sizeof(T)));
+  have = need;
   return LF_OK;
+}
+int reserve(lf_ctx *c, size_t elems) { return grow(c, c->scratch, c->scratch_elems, elems); }
+
+bool use_mfma(int d, size_t kappa) {
+  const char *sel = getenv("LATTICEUM_AMD_AJTAI");
+  return d != 24 && d % 16 == 0 && kappa <= 32 && !(sel && strcmp(sel, "valu") == 0);
 }
 
 // RAII device buffer for the synchronous host API
@@ -166,18 +195,40 @@ int check_repr(lf_ctx *c, int repr) {
   return LF_OK;
 }
 
+size_t partial_elems(const lf_ajtai *aj, int nvec) {
+  if (aj->Af) return (size_t)lfk::mfma_nsplit(aj->ncols) * nvec * aj->kappa * aj->d;
+  return lfk::ajtai_partial_elems(aj->kappa, aj->ncols, aj->d, nvec);
+}
+
+// cm[v] = A f_v for nvec vectors, on the matrix cores when the scheme has fragments
 int ajtai_launch(lf_ctx *c, const lf_ajtai *aj, const uint64_t *const *vecs, int nvec, uint64_t *cm) {
   if (nvec < 1 || nvec > LF_MAX_VECS) return fail(c, LF_ERR_INVALID_ARG, "nvec must be in [1, 32]");
   lfk::VecPtrs vp{};
   for (int v = 0; v < nvec; v++) vp.p[v] = vecs[v];
-  LF_TRY(reserve(c, lfk::ajtai_partial_elems(aj->kappa, aj->ncols, aj->d, nvec)));
+  LF_TRY(reserve(c, partial_elems(aj, nvec)));
+  if (aj->Af) LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->ncols, aj->d)));
   hipEvent_t a = nullptr, b = nullptr;
   if (c->timing) {
     LF_HIP(c, hipEventCreate(&a));
     LF_HIP(c, hipEventCreate(&b));
   }
-  LF_HIP(c, lfk::ajtai_commit(aj->A, aj->kappa, aj->ncols, aj->d, vp, nvec, c->scratch, cm, c->cur, a, b));
+  if (aj->Af)
+    LF_HIP(c, lfk::ajtai_mfma(aj->Af, aj->kappa, aj->ncols, aj->d, vp, nvec, c->frag, c->scratch, cm, c->cur, a, b));
+  else
+    LF_HIP(c, lfk::ajtai_commit(aj->A, aj->kappa, aj->ncols, aj->d, vp, nvec, c->scratch, cm, c->cur, a, b));
   if (c->timing) c->pending.push_back({a, b, nvec});
+  return LF_OK;
+}
+
+// build the MFMA fragment copy of A (scheme creation)
+int ajtai_prepare(lf_ctx *c, lf_ajtai *aj) {
+  if (!use_mfma(aj->d, aj->kappa)) return LF_OK;
+  const size_t n = lfk::frag_elems(aj->ncols, aj->d);
+  LF_HIP(c, hipMalloc((void **)&aj->Af, n * sizeof(uint4)));
+  lfk::VecPtrs rows{};
+  for (size_t i = 0; i < aj->kappa; i++) rows.p[i] = aj->A + i * aj->ncols * aj->d;
+  LF_HIP(c, lfk::to_frag(rows, (int)aj->kappa, aj->ncols, aj->d, aj->Af, c->cur));
+  LF_HIP(c, hipStreamSynchronize(c->cur));
   return LF_OK;
 }
 
@@ -226,23 +277,9 @@ int fold_core(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lb
   for (int s = 0; s < 2; s++)
     for (int k = 1; k < K; k++) vecs.push_back(b->fk[s] + (size_t)k * N * d);
   const size_t kd = kappa * (size_t)d;
-  uint64_t *ycat = nullptr;
-  // ycat lives after the Ajtai partials in scratch
-  const size_t part = lfk::ajtai_partial_elems(kappa, aj->ncols, d, (int)vecs.size());
-  LF_TRY(reserve(c, part + vecs.size() * kd));
-  ycat = c->scratch + part;
-  {
-    lfk::VecPtrs vp{};
-    for (size_t v = 0; v < vecs.size(); v++) vp.p[v] = vecs[v];
-    hipEvent_t ea = nullptr, eb = nullptr;
-    if (c->timing) {
-      LF_HIP(c, hipEventCreate(&ea));
-      LF_HIP(c, hipEventCreate(&eb));
-    }
-    LF_HIP(c, lfk::ajtai_commit(aj->A, kappa, aj->ncols, d, vp, (int)vecs.size(), c->scratch, ycat, c->cur,
-                                ea, eb));
-    if (c->timing) c->pending.push_back({ea, eb, (int)vecs.size()});
-  }
+  LF_TRY(grow(c, c->ybuf, c->ybuf_elems, vecs.size() * kd));
+  uint64_t *ycat = c->ybuf;
+  LF_TRY(ajtai_launch(c, aj, vecs.data(), (int)vecs.size(), ycat));
   if (commit_f) LF_HIP(c, hipMemcpyAsync(commit_cm, ycat, kd * 8, hipMemcpyDeviceToDevice, c->cur));
   const uint64_t *cm_side[2] = {b->acc_cm, cm_i};
   for (int s = 0; s < 2; s++) {
@@ -325,6 +362,8 @@ void lf_ctx_destroy(lf_ctx *c) {
   for (auto &kv : c->tables)
     if (kv.second.mem) (void)hipFree(kv.second.mem);
   if (c->scratch) (void)hipFree(c->scratch);
+  if (c->ybuf) (void)hipFree(c->ybuf);
+  if (c->frag) (void)hipFree(c->frag);
   if (c->d_err) (void)hipFree(c->d_err);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
@@ -334,7 +373,7 @@ const char *lf_ctx_last_error(const lf_ctx *c) { return c ? c->last_error.c_str(
 
 int lf_ctx_set_stream(lf_ctx *c, void *s) {
   if (!c) return LF_ERR_INVALID_ARG;
-  c->cur = s ? (hipStream_t)s : c->own;
+  c->cur = (hipStream_t)s;  // NULL = the HIP default (null) stream, e.g. torch's default stream
   return LF_OK;
 }
 void *lf_ctx_get_stream(const lf_ctx *c) { return c ? (void *)c->cur : nullptr; }
@@ -355,7 +394,16 @@ int lf_ctx_reserve(lf_ctx *c, size_t kappa, size_t ncols, int d, int nvec) {
   if (!c || !ring_ok(d) || nvec < 1 || nvec > LF_MAX_VECS) return LF_ERR_INVALID_ARG;
   Tables *t;
   LF_TRY(get_tables(c, d, t));
-  return reserve(c, lfk::ajtai_partial_elems(kappa, ncols, d, nvec) + (size_t)nvec * kappa * d);
+  lf_ajtai probe;
+  probe.kappa = kappa;
+  probe.ncols = ncols;
+  probe.d = d;
+  if (use_mfma(d, kappa)) {
+    probe.Af = reinterpret_cast<uint4 *>(1);  // sizing only
+    LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(ncols, d)));
+  }
+  LF_TRY(reserve(c, partial_elems(&probe, nvec)));
+  return grow(c, c->ybuf, c->ybuf_elems, (size_t)nvec * kappa * d);
 }
 
 int lf_ctx_kernel_timing(lf_ctx *c, int enable) {
@@ -423,6 +471,11 @@ int lf_ajtai_create(lf_ctx *c, const uint64_t *A, size_t kappa, size_t ncols, in
   aj->kappa = kappa;
   aj->ncols = ncols;
   aj->d = d;
+  int rc = ajtai_prepare(c, aj);
+  if (rc != LF_OK) {
+    lf_ajtai_destroy(aj);
+    return rc;
+  }
   *out = aj;
   return LF_OK;
 }
@@ -436,6 +489,11 @@ int lf_ajtai_create_device(lf_ctx *c, const uint64_t *A_dev, size_t kappa, size_
   aj->kappa = kappa;
   aj->ncols = ncols;
   aj->d = d;
+  int rc = ajtai_prepare(c, aj);
+  if (rc != LF_OK) {
+    lf_ajtai_destroy(aj);
+    return rc;
+  }
   *out = aj;
   return LF_OK;
 }
@@ -443,11 +501,13 @@ int lf_ajtai_create_device(lf_ctx *c, const uint64_t *A_dev, size_t kappa, size_
 void lf_ajtai_destroy(lf_ajtai *aj) {
   if (!aj) return;
   if (aj->owned) (void)hipFree((void *)aj->A);
+  if (aj->Af) (void)hipFree(aj->Af);
   delete aj;
 }
 size_t lf_ajtai_kappa(const lf_ajtai *aj) { return aj ? aj->kappa : 0; }
 size_t lf_ajtai_width(const lf_ajtai *aj) { return aj ? aj->ncols : 0; }
 int lf_ajtai_d(const lf_ajtai *aj) { return aj ? aj->d : 0; }
+int lf_ajtai_layout(const lf_ajtai *aj) { return aj && aj->Af ? 1 : 0; }
 
 int lf_ajtai_commit(lf_ctx *c, const lf_ajtai *aj, const uint64_t *f, size_t f_len, uint64_t *cm, int repr) {
   if (!c || !aj || !f || !cm) return LF_ERR_INVALID_ARG;

@@ -161,6 +161,7 @@ __device__ __forceinline__ void fq3acc_final(const Fq3Acc &s, uint64_t *c) {
 struct NegaTables {
   const uint64_t *twist;      // fwd: psi^j ; inv: d^-1 psi^-j
   const uint64_t *roots;      // fwd: omega^e ; inv: omega^-e   (omega = psi^2), e < d
+  const uint64_t *tw1;        // d = 1024 only: [lane][k2] = omega^(+-lane k2) (ntt1024.hpp pass 1)
 };
 
 // Radix-4 Stockham DFT of size D over LDS buffers x -> y (ping-pong), T threads.

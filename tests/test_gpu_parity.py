@@ -341,3 +341,42 @@ def test_limb_transport_roundtrip(ctx):
     ctx.sync()
     want = sum(x.astype(object) for x in parts) % P
     assert [int(v) for v in out.cpu().numpy().view(np.uint64)] == [int(v) for v in want]
+
+
+@pytest.mark.parametrize("layout", ["mfma", "valu"])
+@pytest.mark.parametrize("d,kappa,ncols,nvec", [(16, 3, 40, 5), (64, 32, 70, 29), (1024, 7, 33, 1),
+                                                (1024, 32, 96, 29), (256, 17, 64, 32)])
+def test_ajtai_layouts(ctx, monkeypatch, layout, d, kappa, ncols, nvec):
+    # the i8-MFMA contraction (signed base-256 limbs) and the VALU path agree with the oracle
+    import torch
+    if layout == "valu":
+        monkeypatch.setenv("LATTICEUM_AMD_AJTAI", "valu")
+    A = rand(kappa * ncols * d, 21 + d + kappa).reshape(kappa, ncols, d)
+    # edge values in A: 0, p-1 and the D8 digit boundaries
+    A.reshape(-1)[:6] = [0, P - 1, 0x7F7F7F7F7F7F7F7F, 0x7F7F7F7F7F7F7F80, (P - 1) // 2, 1]
+    sch = LA.AjtaiCommitmentScheme(ctx, A)
+    assert sch.layout == (1 if layout == "mfma" else 0)
+    F = rand(nvec * ncols * d, 31 + d)
+    F[:4] = [P - 1, 0x7F7F7F7F7F7F7F7F, 0x7F7F7F7F7F7F7F80, 0]
+    Ft = torch.from_numpy(F.view(np.int64)).cuda()
+    cm = torch.zeros(nvec * kappa * d, dtype=torch.int64, device="cuda")
+    ctx.dev_ajtai_commit(sch, [Ft[v * ncols * d:(v + 1) * ncols * d] for v in range(nvec)], cm)
+    ctx.sync()
+    want = O.ajtai_commit(A, kappa, ncols, d, F, nvec)
+    assert np.array_equal(cm.cpu().numpy().view(np.uint64), want)
+
+
+def test_ajtai_mfma_extreme_digits(ctx):
+    # all-(-128) digit products stress the i32 weight accumulators over a full column split
+    import torch
+    d, kappa, ncols, nvec = 16, 32, 320 * 32, 32
+    A = np.full(kappa * ncols * d, P - 1, np.uint64).reshape(kappa, ncols, d)
+    F = np.full(nvec * ncols * d, P - 1, np.uint64)
+    sch = LA.AjtaiCommitmentScheme(ctx, A)
+    assert sch.layout == 1
+    Ft = torch.from_numpy(F.view(np.int64)).cuda()
+    cm = torch.zeros(nvec * kappa * d, dtype=torch.int64, device="cuda")
+    ctx.dev_ajtai_commit(sch, [Ft[v * ncols * d:(v + 1) * ncols * d] for v in range(nvec)], cm)
+    ctx.sync()
+    # (p-1)^2 = 1 per column, so every entry is ncols mod p
+    assert set(cm.cpu().numpy().view(np.uint64).tolist()) == {ncols}
