@@ -28,57 +28,63 @@ __device__ __forceinline__ uint64_t d8(uint64_t x) {
 }
 
 // ---------------------------------------------------------------- to fragment order
-// block = (chunk c, 16-slot block); LDS tile [row r][column j][slot] with the
-// row stride padded to 513 u64 so the per-lane column reads are conflict-free.
-constexpr int TF_S = 16;
-constexpr int TF_RS = 32 * TF_S + 1;
-__global__ void __launch_bounds__(512) k_to_frag(VecPtrs rows, int nrows, size_t N, int d, int nch,
+// block = (16-slot block, 32-column chunk c, group of 8 rows). LDS tile
+// [row][slot][column] of D8 words, rows padded to 34 words so the 16-B
+// column reads of the emit phase are aligned. Rows >= nrows are never
+// written: they only feed MFMA output columns (or rows) that are discarded.
+constexpr int TF_S = 16, TF_R = 8, TF_J = 34;
+__global__ void __launch_bounds__(256) k_to_frag(VecPtrs rows, int nrows, size_t N, int d, int nch,
                                                  uint4 *frag) {
-  __shared__ uint64_t tile[32 * TF_RS];
-  const int c = blockIdx.y, sb = blockIdx.x, tid = threadIdx.x;
-  // load: 32 rows x 32 columns x 16 slots, 16-B pieces (8 per 128-B row segment)
-  for (int p = tid; p < 32 * 32 * 8; p += blockDim.x) {
+  __shared__ uint64_t tile[TF_R * TF_S * TF_J];
+  const int sb = blockIdx.x, c = blockIdx.y, r0 = blockIdx.z * TF_R, tid = threadIdx.x;
+  // load: 8 rows x 32 columns x (16 slots = 128 B = 8 pieces of 16 B)
+#pragma unroll
+  for (int it = 0; it < TF_R * 32 * 8 / 256; it++) {
+    const int p = it * 256 + tid;
     const int r = p >> 8, j = (p >> 3) & 31, q = p & 7;
     const size_t col = (size_t)c * 32 + j;
     ulonglong2 v = make_ulonglong2(0, 0);
-    if (r < nrows && col < N)
-      v = *reinterpret_cast<const ulonglong2 *>(rows.p[r] + col * d + (size_t)sb * TF_S + 2 * q);
-    uint64_t *t = tile + r * TF_RS + j * TF_S + 2 * q;
+    if (r0 + r < nrows && col < N)
+      v = *reinterpret_cast<const ulonglong2 *>(rows.p[r0 + r] + col * d + (size_t)sb * TF_S + 2 * q);
+    uint64_t *t = tile + (r * TF_S + 2 * q) * TF_J + j;
     t[0] = d8(v.x);
-    t[1] = d8(v.y);
+    t[TF_J] = d8(v.y);
   }
   __syncthreads();
-  // each wave emits two slots: lane (r, h) gathers 16 columns and transposes bytes
-  const int lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
-  for (int sl = wave; sl < TF_S; sl += blockDim.x / 64) {
-    uint32_t lo[16], hi[16];
+  // emit: thread = (slot sl, half h, row r); lane (r, h) of the MFMA operand
+  // holds columns 16h..16h+15 of one slot as 16 bytes per digit
+  const int r = tid & 7, h = (tid >> 3) & 1, sl = tid >> 4;
+  if (r0 + r >= nrows) return;
+  const ulonglong2 *src = reinterpret_cast<const ulonglong2 *>(tile + (r * TF_S + sl) * TF_J + 16 * h);
+  uint32_t lo[16], hi[16];
 #pragma unroll
-    for (int jj = 0; jj < 16; jj++) {
-      const uint64_t x = tile[r * TF_RS + (16 * h + jj) * TF_S + sl];
-      lo[jj] = (uint32_t)x;
-      hi[jj] = (uint32_t)(x >> 32);
-    }
-    const size_t s = (size_t)sb * TF_S + sl;
-    uint4 *out = frag + ((s * nch + c) * 8) * 64 + lane;
+  for (int q = 0; q < 8; q++) {
+    const ulonglong2 x = src[q];
+    lo[2 * q] = (uint32_t)x.x;
+    hi[2 * q] = (uint32_t)(x.x >> 32);
+    lo[2 * q + 1] = (uint32_t)x.y;
+    hi[2 * q + 1] = (uint32_t)(x.y >> 32);
+  }
+  const size_t s = (size_t)sb * TF_S + sl;
+  uint4 *out = frag + ((s * nch + c) * 8) * 64 + r0 + r + 32 * h;
 #pragma unroll
-    for (int half = 0; half < 2; half++) {
-      const uint32_t *w = half ? hi : lo;
+  for (int half = 0; half < 2; half++) {
+    const uint32_t *w = half ? hi : lo;
 #pragma unroll
-      for (int bb = 0; bb < 4; bb += 2) {  // digits 4*half + bb and + bb + 1
-        uint32_t dw0[4], dw1[4];
+    for (int bb = 0; bb < 4; bb += 2) {  // digits 4*half + bb and + bb + 1
+      uint32_t dw0[4], dw1[4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          // [x0_b, x1_b, x0_b+1, x1_b+1] and [x2_b, x3_b, x2_b+1, x3_b+1]
-          const uint32_t sel = (uint32_t)bb | ((uint32_t)(4 + bb) << 8) | ((uint32_t)(bb + 1) << 16) |
-                               ((uint32_t)(5 + bb) << 24);
-          const uint32_t t01 = __builtin_amdgcn_perm(w[4 * q + 1], w[4 * q], sel);
-          const uint32_t t23 = __builtin_amdgcn_perm(w[4 * q + 3], w[4 * q + 2], sel);
-          dw0[q] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
-          dw1[q] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
-        }
-        out[(4 * half + bb) * 64] = make_uint4(dw0[0], dw0[1], dw0[2], dw0[3]);
-        out[(4 * half + bb + 1) * 64] = make_uint4(dw1[0], dw1[1], dw1[2], dw1[3]);
+      for (int q = 0; q < 4; q++) {
+        // [x0_b, x1_b, x0_b+1, x1_b+1] and [x2_b, x3_b, x2_b+1, x3_b+1]
+        const uint32_t sel = (uint32_t)bb | ((uint32_t)(4 + bb) << 8) | ((uint32_t)(bb + 1) << 16) |
+                             ((uint32_t)(5 + bb) << 24);
+        const uint32_t t01 = __builtin_amdgcn_perm(w[4 * q + 1], w[4 * q], sel);
+        const uint32_t t23 = __builtin_amdgcn_perm(w[4 * q + 3], w[4 * q + 2], sel);
+        dw0[q] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
+        dw1[q] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
       }
+      out[(4 * half + bb) * 64] = make_uint4(dw0[0], dw0[1], dw0[2], dw0[3]);
+      out[(4 * half + bb + 1) * 64] = make_uint4(dw1[0], dw1[1], dw1[2], dw1[3]);
     }
   }
 }
@@ -158,9 +164,10 @@ int mfma_nsplit(size_t ncols) {
 }
 
 hipError_t to_frag(const VecPtrs &rows, int nrows, size_t ncols, int d, uint4 *frag, hipStream_t st) {
-  if (nrows < 0 || nrows > 32 || d % TF_S) return hipErrorInvalidValue;
+  if (nrows < 1 || nrows > 32 || d % TF_S) return hipErrorInvalidValue;
   const int nch = (int)((ncols + 31) / 32);
-  hipLaunchKernelGGL(k_to_frag, dim3(d / TF_S, nch), dim3(512), 0, st, rows, nrows, ncols, d, nch, frag);
+  hipLaunchKernelGGL(k_to_frag, dim3(d / TF_S, nch, (nrows + TF_R - 1) / TF_R), dim3(256), 0, st, rows, nrows,
+                     ncols, d, nch, frag);
   return hipGetLastError();
 }
 

@@ -16,27 +16,46 @@ namespace gl {
 constexpr uint64_t P = 0xFFFFFFFF00000001ull;
 constexpr uint64_t EPS = 0xFFFFFFFFull;  // 2^64 mod p
 
-LF_HD uint64_t canon(uint64_t x) { return x >= P ? x - P : x; }
-
-LF_HD uint64_t add(uint64_t a, uint64_t b) {  // canonical in -> canonical out
-  uint64_t s = a + b;
-  // overflow past 2^64: add EPS (2^64 == EPS); result < p since a,b < p
-  s += (s < a) ? EPS : 0;
-  return canon(s);
+LF_HD uint64_t canon(uint64_t x) {  // x >= p  <=>  x + EPS carries; then x - p == x + EPS
+  uint64_t u;
+  return __builtin_uaddll_overflow(x, EPS, reinterpret_cast<unsigned long long *>(&u)) ? u : x;
 }
 
-LF_HD uint64_t sub(uint64_t a, uint64_t b) {
-  uint64_t d = a - b;
-  d -= (a < b) ? EPS : 0;  // borrow: d wrapped by +2^64 == +EPS, remove it
-  return d;
+// a + b with the carry out (lowers to one 64-bit add + carry compare on gfx950)
+LF_HD bool addc64(uint64_t a, uint64_t b, uint64_t &r) {
+  return __builtin_uaddll_overflow(a, b, reinterpret_cast<unsigned long long *>(&r));
+}
+LF_HD bool subb64(uint64_t a, uint64_t b, uint64_t &r) {
+  return __builtin_usubll_overflow(a, b, reinterpret_cast<unsigned long long *>(&r));
+}
+
+LF_HD uint64_t add(uint64_t a, uint64_t b) {  // canonical in -> canonical out
+  // t = a + b; the result is t - p exactly when a + b >= p, i.e. when the sum
+  // carried out of 64 bits (t - p = t + EPS) or t + EPS carries (t >= p)
+  uint64_t t, u;
+  const bool c1 = addc64(a, b, t);
+  const bool c2 = addc64(t, EPS, u);
+  return (c1 | c2) ? u : t;
+}
+
+LF_HD uint64_t sub(uint64_t a, uint64_t b) {  // canonical in -> canonical out
+  uint64_t d;
+  const bool br = subb64(a, b, d);
+  return br ? d - EPS : d;  // borrow: d wrapped by +2^64 == +EPS, remove it
 }
 
 LF_HD uint64_t neg(uint64_t a) { return a ? P - a : 0; }
 
+// 64x64 -> 128 from four 32x32 -> 64 multiply-adds (v_mad_u64_u32 each; no
+// intermediate sum overflows: (2^32-1)^2 + 2 (2^32-1) = 2^64 - 1)
 LF_HD void mul_wide(uint64_t a, uint64_t b, uint64_t &lo, uint64_t &hi) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  lo = a * b;
-  hi = __umul64hi(a, b);
+  const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+  const uint64_t p0 = (uint64_t)a0 * b0;
+  const uint64_t t = (uint64_t)a0 * b1 + (p0 >> 32);
+  const uint64_t u = (uint64_t)a1 * b0 + (uint32_t)t;
+  hi = (uint64_t)a1 * b1 + (t >> 32) + (u >> 32);
+  lo = (u << 32) | (uint32_t)p0;
 #else
   unsigned __int128 t = (unsigned __int128)a * b;
   lo = (uint64_t)t;
@@ -44,16 +63,14 @@ LF_HD void mul_wide(uint64_t a, uint64_t b, uint64_t &lo, uint64_t &hi) {
 #endif
 }
 
-// x = lo + 2^64 hi  ->  weakly reduced u64 congruent to x
+// x = lo + 2^64 hi  ->  weakly reduced u64 congruent to x:
+//   hi = h0 + 2^32 h1:  x == lo + h0 (2^32 - 1) - h1   (2^64 == EPS, 2^96 == -1)
 LF_HD uint64_t reduce128(uint64_t lo, uint64_t hi) {
-  uint64_t hh = hi >> 32;
-  uint64_t hl = hi & EPS;
-  uint64_t t0 = lo - hh;
-  t0 -= (lo < hh) ? EPS : 0;            // 2^96 == -1
-  uint64_t t1 = (hl << 32) - hl;         // hl * (2^32 - 1), < 2^64
-  uint64_t r = t0 + t1;
-  r += (r < t1) ? EPS : 0;               // carry 2^64 == EPS
-  return r;
+  const uint64_t h0 = hi & EPS, h1 = hi >> 32;
+  uint64_t r, s;
+  if (addc64(lo, h0 * EPS, r)) r += EPS;  // r + EPS < 2^64 after a carry
+  if (subb64(r, h1, s)) s -= EPS;         // s >= p after a borrow
+  return s;
 }
 
 LF_HD uint64_t mul(uint64_t a, uint64_t b) {

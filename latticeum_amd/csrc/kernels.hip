@@ -3,45 +3,13 @@
 // Phi_72 in the reference's in-place CRT layout [s0.c0, s0.c1, s0.c2, s1.c0, ..]
 // (stark-rings crt.rs:53-77), d = 4^k for the negacyclic rings), canonical
 // values. Every launcher returns hipError_t and takes the stream explicitly.
+#include "digits.hpp"
 #include "kernels.hpp"
 #include "ring.hpp"
 
 namespace lfk {
 
 using gl::Acc;
-
-// ============================================================ error flags
-// bit 0: a balanced decomposition needed more digits than provided
-// (the reference indexes out of bounds and panics:
-//  stark-rings balanced_decomposition/mod.rs:85-87)
-__device__ __forceinline__ void raise(int *err, int bit) {
-  if (err) atomicOr(err, bit);
-}
-
-// ============================================================ helpers
-__device__ __forceinline__ int64_t signed_rep(uint64_t v) {
-  // fq_convertible.rs:22-34: (q-1)/2 < v  ->  v - q  (fits in int64)
-  return v > (gl::P - 1) / 2 ? (int64_t)(v - gl::P) : (int64_t)v;
-}
-__device__ __forceinline__ uint64_t from_signed(int64_t x) {
-  return x < 0 ? gl::P - (uint64_t)(-x) : (uint64_t)x;
-}
-// one balanced digit step (balanced_decomposition/mod.rs:76-91) for b = 2^lb
-__device__ __forceinline__ int64_t bal_digit(int64_t &curr, int lb) {
-  const int64_t b = (int64_t)1 << lb, bh = b >> 1;
-  // truncating division / remainder by 2^lb (Rust `/` and `%` semantics)
-  int64_t q = (curr + ((curr >> 63) & (b - 1))) >> lb;
-  int64_t rem = curr - (q << lb);
-  int64_t ar = rem < 0 ? -rem : rem;
-  if (ar <= bh) {
-    curr = q;
-    return rem;
-  }
-  // rounded_div(rem, b) = sign(rem) since b/2 < |rem| < b  (linear_algebra ops.rs:64-80)
-  int64_t sg = rem < 0 ? -1 : 1;
-  curr = q + sg;
-  return rem - sg * b;
-}
 
 // ============================================================ Phi_72 transforms
 // one thread per ring element; 16-B vector loads of the 192-B element
@@ -86,7 +54,7 @@ __global__ void __launch_bounds__(NT<D>::T) k_nega_transform(uint64_t *data, siz
       buf[0][i] = FWD ? gl::mul(v, tb.twist[i]) : v;
     }
     __syncthreads();
-    uint64_t *r = ring::stockham4<D, T>(buf[0], buf[1], tb.roots, tid);
+    uint64_t *r = ring::stockham4<D, T, !FWD>(buf[0], buf[1], tb.roots, tid);
 #pragma unroll
     for (int i = tid; i < D; i += T) g[i] = FWD ? r[i] : gl::mul(r[i], tb.twist[i]);
     __syncthreads();
@@ -167,7 +135,7 @@ __global__ void __launch_bounds__(NT<D>::T) k_from_w_ccs_nega(const uint64_t *w_
 #pragma unroll
     for (int i = tid; i < D; i += T) buf[0][i] = g[i];
     __syncthreads();
-    uint64_t *r = ring::stockham4<D, T>(buf[0], buf[1], inv.roots, tid);
+    uint64_t *r = ring::stockham4<D, T, true>(buf[0], buf[1], inv.roots, tid);
     int64_t cur[PER];
 #pragma unroll
     for (int q = 0; q < PER; q++) cur[q] = signed_rep(gl::mul(r[tid + q * T], inv.twist[tid + q * T]));
@@ -182,7 +150,7 @@ __global__ void __launch_bounds__(NT<D>::T) k_from_w_ccs_nega(const uint64_t *w_
         buf[0][i] = gl::mul(dgt, fwd.twist[i]);
       }
       __syncthreads();
-      uint64_t *rr = ring::stockham4<D, T>(buf[0], buf[1], fwd.roots, tid);
+      uint64_t *rr = ring::stockham4<D, T, false>(buf[0], buf[1], fwd.roots, tid);
       uint64_t *of = f + (j * L + l) * D;
 #pragma unroll
       for (int q = 0; q < PER; q++) of[tid + q * T] = rr[tid + q * T];
@@ -243,7 +211,7 @@ __global__ void __launch_bounds__(NT<D>::T) k_from_f_nega(const uint64_t *f, siz
         acc[q] = (l == L - 1) ? v : gl::add(gl::mul_pow2(acc[q], lb), v);
       }
       __syncthreads();
-      uint64_t *r = ring::stockham4<D, T>(buf[0], buf[1], inv.roots, tid);
+      uint64_t *r = ring::stockham4<D, T, true>(buf[0], buf[1], inv.roots, tid);
       uint64_t *oc = f_coeff + (j * L + l) * D;
 #pragma unroll
       for (int q = 0; q < PER; q++) oc[tid + q * T] = gl::mul(r[tid + q * T], inv.twist[tid + q * T]);
@@ -349,7 +317,7 @@ __global__ void __launch_bounds__(NT<D>::T) k_decompose_nega(const uint64_t *f_c
           buf[0][i] = dg == 0 ? 0 : (dg == 1 ? tw : (dg == -1 ? gl::neg(tw) : gl::mul(from_signed(dg), tw)));
         }
         __syncthreads();
-        uint64_t *r = ring::stockham4<D, T>(buf[0], buf[1], fwd.roots, tid);
+        uint64_t *r = ring::stockham4<D, T, false>(buf[0], buf[1], fwd.roots, tid);
 #pragma unroll
         for (int q = 0; q < PER; q++) {
           uint64_t v = r[tid + q * T];
@@ -703,7 +671,7 @@ static inline unsigned grid_cap(size_t n) { return (unsigned)(n < 65536 ? n : 65
 hipError_t transform(uint64_t *data, size_t n, int d, bool fwd, const ring::NegaTables &tb,
                      hipStream_t st) {
   if (n == 0) return hipSuccess;
-  if (d == 1024 && tb.tw1) return transform_w1024(data, n, fwd, tb, st);
+  if (d == 1024 && tb.mid) return transform_n32(data, n, fwd, tb, st);
   if (d == 24) {
     if (fwd)
       hipLaunchKernelGGL(k_phi72_transform<true>, dim3(blocks(n, 256)), dim3(256), 0, st, data, n);
@@ -753,7 +721,7 @@ hipError_t from_w_ccs(const uint64_t *w_ccs, size_t W, int d, int lb, int L, uin
                       uint64_t *f, const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err,
                       hipStream_t st) {
   if (W == 0) return hipSuccess;
-  if (d == 1024 && fwd.tw1 && inv.tw1) return from_w_ccs_w1024(w_ccs, W, lb, L, f_coeff, f, fwd, inv, err, st);
+  if (d == 1024 && fwd.mid && inv.mid) return from_w_ccs_n32(w_ccs, W, lb, L, f_coeff, f, fwd, inv, err, st);
   if (d == 24) {
     hipLaunchKernelGGL(k_from_w_ccs_phi72, dim3(blocks(W, 128)), dim3(128), 0, st, w_ccs, W, lb, L,
                        f_coeff, f, err);
@@ -775,7 +743,7 @@ hipError_t from_f(const uint64_t *f, size_t N, int d, int lb, int L, uint64_t *f
                   uint64_t *w_ccs, const ring::NegaTables &inv, hipStream_t st) {
   const size_t W = N / L;
   if (W == 0) return hipSuccess;
-  if (d == 1024 && inv.tw1) return from_f_w1024(f, W, lb, L, f_coeff, w_ccs, inv, st);
+  if (d == 1024 && inv.mid) return from_f_n32(f, W, lb, L, f_coeff, w_ccs, inv, st);
   if (d == 24) {
     hipLaunchKernelGGL(k_from_f_phi72, dim3(blocks(W, 128)), dim3(128), 0, st, f, W, lb, L, f_coeff,
                        w_ccs);
@@ -798,8 +766,8 @@ hipError_t decompose_witness(const uint64_t *f_coeff, size_t N, int d, int lb, i
                              const ring::NegaTables &fwd, int *err, hipStream_t st) {
   const size_t W = N / L;
   if (W == 0) return hipSuccess;
-  if (d == 1024 && fwd.tw1 && lbs == 1 && K <= 15 && L <= 8)
-    return decompose_w1024(f_coeff, N, lb, L, K, f_coeff_k, f_k, w_ccs_k, fwd, err, st);
+  if (d == 1024 && fwd.mid && lbs == 1 && K <= 15 && L <= 8)
+    return decompose_n32(f_coeff, N, lb, L, K, f_coeff_k, f_k, w_ccs_k, fwd, err, st);
   if (d == 24) {
     if (DEC_GROUPS * L > 256) return hipErrorInvalidValue;
     size_t lds = (size_t)DEC_GROUPS * L * 25 * sizeof(uint64_t);

@@ -54,15 +54,14 @@ hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, size_t ncols, int d, const 
                       uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st, hipEvent_t ev0 = nullptr,
                       hipEvent_t ev1 = nullptr);
 
-// d = 1024 one-wave-DFT kernels (kernels_w1024.hip)
-hipError_t transform_w1024(uint64_t *data, size_t n, bool fwd, const ring::NegaTables &tb, hipStream_t st);
-hipError_t from_w_ccs_w1024(const uint64_t *w_ccs, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *f,
-                            const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err,
-                            hipStream_t st);
-hipError_t from_f_w1024(const uint64_t *f, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *w_ccs,
-                        const ring::NegaTables &inv, hipStream_t st);
-hipError_t decompose_w1024(const uint64_t *f_coeff, size_t N, int lb, int L, int K, uint64_t *f_coeff_k,
-                           uint64_t *f_k, uint64_t *w_ccs_k, const ring::NegaTables &fwd, int *err,
-                           hipStream_t st);
+// d = 1024 kernels on the register-resident 32 x 32 NTT (kernels_n32.hip)
+hipError_t transform_n32(uint64_t *data, size_t n, bool fwd, const ring::NegaTables &tb, hipStream_t st);
+hipError_t from_w_ccs_n32(const uint64_t *w_ccs, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *f,
+                          const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err, hipStream_t st);
+hipError_t from_f_n32(const uint64_t *f, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *w_ccs,
+                      const ring::NegaTables &inv, hipStream_t st);
+hipError_t decompose_n32(const uint64_t *f_coeff, size_t N, int lb, int L, int K, uint64_t *f_coeff_k,
+                         uint64_t *f_k, uint64_t *w_ccs_k, const ring::NegaTables &fwd, int *err,
+                         hipStream_t st);
 
 }  // namespace lfk

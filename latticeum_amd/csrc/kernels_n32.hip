@@ -1,0 +1,316 @@
+// kernels_n32.hip -- the X^1024 + 1 ring on the register-resident 32 x 32 NTT
+// (ntt32.hpp). Half a wave owns one ring element (transforms, from_w_ccs) or
+// one group of L elements (decompose, from_f); waves never synchronise with
+// each other and there is no s_barrier on this path. Every global access is a
+// 256-B row per half-wave (lane r touches x[r + 32 k]).
+#include "digits.hpp"
+#include "kernels.hpp"
+#include "ntt32.hpp"
+
+namespace lfk {
+
+namespace {
+constexpr int WPB = 4;  // waves per block
+constexpr int D = 1024;
+
+struct Half {
+  int r, h;        // lane & 31, half of the wave
+  size_t unit;     // this half's work unit (ring element or group)
+  size_t stride;   // units per grid-stride step
+  uint64_t *lds;   // this half's transpose tile
+};
+__device__ __forceinline__ Half half_ctx(uint64_t *lds_all) {
+  Half x;
+  const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+  x.r = lane & 31;
+  x.h = lane >> 5;
+  x.unit = ((size_t)blockIdx.x * WPB + wib) * 2 + x.h;
+  x.stride = (size_t)gridDim.x * WPB * 2;
+  x.lds = lds_all + wib * n32::WAVE_U64 + x.h * n32::HALF_U64;
+  return x;
+}
+// issue 32 row loads before the first use: the asm consumes the values in
+// groups of 8, so the scheduler cannot interleave load -> wait -> use per value
+__device__ __forceinline__ void load_row32(const uint64_t *p, uint64_t *v) {
+#pragma unroll
+  for (int k = 0; k < 32; k++) v[k] = p[32 * k];
+#pragma unroll
+  for (int k = 0; k < 32; k += 8)
+    asm volatile("" : "+v"(v[k]), "+v"(v[k + 1]), "+v"(v[k + 2]), "+v"(v[k + 3]), "+v"(v[k + 4]), "+v"(v[k + 5]),
+                 "+v"(v[k + 6]), "+v"(v[k + 7]));
+}
+// the loop bound every lane of a wave agrees on (both halves iterate together)
+__device__ __forceinline__ size_t pair_bound(size_t n) { return (n + 1) & ~(size_t)1; }
+}  // namespace
+
+// ---------------------------------------------------------------- transforms
+template <bool FWD>
+__global__ void __launch_bounds__(256) k_xform_n32(uint64_t *data, size_t n, const uint64_t *mid_g) {
+  __shared__ uint64_t lds_all[WPB * n32::WAVE_U64];
+  __shared__ uint64_t mid[n32::MID_U64];
+  n32::stage_mid(mid, mid_g);
+  __syncthreads();
+  Half x = half_ctx(lds_all);
+  // the next element's row loads are issued before this element's stores, so
+  // the wait for them does not also wait for the stores to drain
+  uint64_t nx[32];
+  {
+    const uint64_t *g = data + (x.unit < n ? x.unit : 0) * D + x.r;
+#pragma unroll
+    for (int k = 0; k < 32; k++) nx[k] = g[32 * k];
+  }
+  for (size_t e = x.unit; e < pair_bound(n); e += x.stride) {
+    const bool ok = e < n;
+    uint64_t *g = data + (ok ? e : 0) * D + x.r;
+    uint64_t v[32];
+#pragma unroll
+    for (int k = 0; k < 32; k++) v[k] = nx[k];
+    if (FWD)
+      n32::forward(v, mid, x.lds, x.r);
+    else
+      n32::inverse(v, mid, x.lds, x.r);
+    const size_t en = e + x.stride;
+    const uint64_t *gn = data + (en < n ? en : 0) * D + x.r;
+#pragma unroll
+    for (int k = 0; k < 32; k++) nx[k] = gn[32 * k];
+    if (ok) {
+      if (FWD) {
+#pragma unroll
+        for (int i = 0; i < 32; i++) g[32 * n32::brv5(i)] = v[i];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 32; k++) g[32 * k] = v[k];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- Witness::from_w_ccs
+// LF/arith.rs:230-248: ICRT -> gadget_decompose(B = 2^lb, L) -> CRT; one half-wave per element
+__global__ void __launch_bounds__(256) k_from_w_ccs_n32(const uint64_t *w_ccs, size_t W, int lb, int L,
+                                                       uint64_t *f_coeff, uint64_t *f, const uint64_t *mid_fg,
+                                                       const uint64_t *mid_ig, int *err) {
+  __shared__ uint64_t lds_all[WPB * n32::WAVE_U64];
+  __shared__ uint64_t mid_f[n32::MID_U64], mid_i[n32::MID_U64];
+  n32::stage_mid(mid_f, mid_fg);
+  n32::stage_mid(mid_i, mid_ig);
+  __syncthreads();
+  Half x = half_ctx(lds_all);
+  uint64_t nx[32];
+  {
+    const uint64_t *g = w_ccs + (x.unit < W ? x.unit : 0) * D + x.r;
+#pragma unroll
+    for (int k = 0; k < 32; k++) nx[k] = g[32 * k];
+  }
+  for (size_t j = x.unit; j < pair_bound(W); j += x.stride) {
+    const bool ok = j < W;
+    uint64_t v[32];
+#pragma unroll
+    for (int k = 0; k < 32; k++) v[k] = nx[k];
+    n32::inverse(v, mid_i, x.lds, x.r);
+    {  // next element's loads ahead of this element's stores
+      const size_t jn = j + x.stride;
+      const uint64_t *g = w_ccs + (jn < W ? jn : 0) * D + x.r;
+#pragma unroll
+      for (int k = 0; k < 32; k++) nx[k] = g[32 * k];
+    }
+    int64_t cur[32];
+#pragma unroll
+    for (int k = 0; k < 32; k++) cur[k] = signed_rep(v[k]);
+    for (int l = 0; l < L; l++) {
+      uint64_t *oc = f_coeff + ((ok ? j : 0) * L + l) * D + x.r;
+#pragma unroll
+      for (int k = 0; k < 32; k++) {
+        v[k] = from_signed(bal_digit(cur[k], lb));
+        if (ok) oc[32 * k] = v[k];
+      }
+      n32::forward(v, mid_f, x.lds, x.r);
+      if (ok) {
+        uint64_t *of = f + (j * L + l) * D + x.r;
+#pragma unroll
+        for (int i = 0; i < 32; i++) of[32 * n32::brv5(i)] = v[i];
+      }
+    }
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < 32; k++) bad |= cur[k] != 0;
+    if (ok && bad) raise(err, 1);
+  }
+}
+
+// ---------------------------------------------------------------- Witness::from_f
+// LF/arith.rs:299-313: f_coeff = ICRT(f), w_ccs = recompose(f) in slot form; one half-wave per group
+__global__ void __launch_bounds__(256) k_from_f_n32(const uint64_t *f, size_t W, int lb, int L,
+                                                   uint64_t *f_coeff, uint64_t *w_ccs, const uint64_t *mid_ig) {
+  __shared__ uint64_t lds_all[WPB * n32::WAVE_U64];
+  __shared__ uint64_t mid_i[n32::MID_U64];
+  n32::stage_mid(mid_i, mid_ig);
+  __syncthreads();
+  Half x = half_ctx(lds_all);
+  for (size_t g = x.unit; g < pair_bound(W); g += x.stride) {
+    const bool ok = g < W;
+    const size_t gg = ok ? g : 0;
+    uint64_t acc[32], nx[32];
+    {
+      const uint64_t *src = f + (gg * L + L - 1) * D + x.r;
+#pragma unroll
+      for (int k = 0; k < 32; k++) nx[k] = src[32 * k];
+    }
+    for (int l = L - 1; l >= 0; l--) {
+      uint64_t v[32];
+#pragma unroll
+      for (int k = 0; k < 32; k++) {
+        v[k] = nx[k];
+        acc[k] = (l == L - 1) ? v[k] : gl::add(gl::mul_pow2(acc[k], lb), v[k]);
+      }
+      n32::inverse(v, mid_i, x.lds, x.r);
+      if (l > 0) {  // next limb's loads ahead of this limb's stores
+        const uint64_t *src = f + (gg * L + l - 1) * D + x.r;
+#pragma unroll
+        for (int k = 0; k < 32; k++) nx[k] = src[32 * k];
+      }
+      if (ok) {
+        uint64_t *oc = f_coeff + (g * L + l) * D + x.r;
+#pragma unroll
+        for (int k = 0; k < 32; k++) oc[32 * k] = v[k];
+      }
+    }
+    if (ok) {
+      uint64_t *ow = w_ccs + g * D + x.r;
+#pragma unroll
+      for (int k = 0; k < 32; k++) ow[32 * k] = acc[k];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- decompose_witness
+// LF/nifs/decomposition.rs:162-167, decomposition/utils.rs:45-49, arith.rs:324-338,
+// specialised to b_small = 2 (GoldiLocksDP): the balanced base-2 digits of v are
+// sign(v) * bit_k(|v|) (|rem| <= b/2 always, so no carries), so each digit plane
+// is read straight off |v| kept as 16-bit sign|magnitude (K <= 15; |v| < 2^K is
+// checked -- the reference panics otherwise). One half-wave per group of L
+// elements; the first two NTT levels of a digit plane run exactly in int64
+// (n32::neg_ct32_digits), and w_ccs_k = sum_l B^l f_k[gL + l] is accumulated in
+// slot form as the planes are produced.
+template <int L>
+__global__ void __launch_bounds__(256, 1) k_decompose_n32(const uint64_t *f_coeff, size_t N, int lb, int K,
+                                                         uint64_t *f_coeff_k, uint64_t *f_k, uint64_t *w_ccs_k,
+                                                         const uint64_t *mid_fg, int *err) {
+  __shared__ uint64_t lds_all[WPB * n32::WAVE_U64];
+  __shared__ uint64_t mid_f[n32::MID_U64];
+  n32::stage_mid(mid_f, mid_fg);
+  __syncthreads();
+  Half x = half_ctx(lds_all);
+  const size_t W = N / L;
+  for (size_t g = x.unit; g < pair_bound(W); g += x.stride) {
+    const bool ok = g < W;
+    const size_t gg = ok ? g : 0;
+    // sm[i] holds limb L-1-i as 16-bit sign|magnitude of x[r + 32 k] (two per
+    // word); the limb loop below always reads sm[0] and rotates the array, so
+    // no register array is indexed by a loop variable
+    uint32_t sm[L][16];
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < L; i++) {
+      uint64_t raw[32];
+      load_row32(f_coeff + (gg * L + (L - 1 - i)) * D + x.r, raw);
+#pragma unroll
+      for (int k = 0; k < 32; k += 2) {
+        const int64_t a = signed_rep(raw[k]), c = signed_rep(raw[k + 1]);
+        const uint64_t ma = a < 0 ? (uint64_t)(-a) : (uint64_t)a, mc = c < 0 ? (uint64_t)(-c) : (uint64_t)c;
+        bad |= (ma >> K) != 0 || (mc >> K) != 0;
+        const uint32_t ea = (uint32_t)(ma & 0x7FFF) | (a < 0 ? 0x8000u : 0u);
+        const uint32_t ec = (uint32_t)(mc & 0x7FFF) | (c < 0 ? 0x8000u : 0u);
+        sm[i][k >> 1] = ea | (ec << 16);
+      }
+    }
+    if (ok && bad) raise(err, 1);
+    for (int kb = 0; kb < K; kb++) {
+      uint64_t acc[32];
+#pragma unroll 1
+      for (int l = L - 1; l >= 0; l--) {
+        const size_t e = (size_t)kb * N + gg * L + l;
+        int32_t dg[32];
+#pragma unroll
+        for (int k = 0; k < 32; k++) {
+          const uint32_t hw = (sm[0][k >> 1] >> ((k & 1) * 16)) & 0xFFFF;
+          const int32_t bit = (hw >> kb) & 1;
+          dg[k] = (hw & 0x8000) ? -bit : bit;
+        }
+        // rotate: the next limb moves to sm[0]
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+          const uint32_t t0 = sm[0][q];
+#pragma unroll
+          for (int i = 0; i + 1 < L; i++) sm[i][q] = sm[i + 1][q];
+          sm[L - 1][q] = t0;
+        }
+        if (ok) {
+          uint64_t *oc = f_coeff_k + e * D + x.r;
+#pragma unroll
+          for (int k = 0; k < 32; k++) oc[32 * k] = from_signed(dg[k]);
+        }
+        uint64_t v[32];
+        n32::neg_ct32_digits(dg, v);
+        n32::forward<false>(v, mid_f, x.lds, x.r);
+        if (ok) {
+          uint64_t *of = f_k + e * D + x.r;
+#pragma unroll
+          for (int i = 0; i < 32; i++) of[32 * n32::brv5(i)] = v[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 32; i++) acc[i] = (l == L - 1) ? v[i] : gl::add(gl::mul_pow2(acc[i], lb), v[i]);
+      }
+      if (ok) {
+        uint64_t *ow = w_ccs_k + ((size_t)kb * W + g) * D + x.r;
+#pragma unroll
+        for (int i = 0; i < 32; i++) ow[32 * n32::brv5(i)] = acc[i];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- launchers
+static unsigned half_blocks(size_t units, unsigned cap) {
+  size_t b = (units + 2 * WPB - 1) / (2 * WPB);
+  if (b < 1) b = 1;
+  return (unsigned)(b < cap ? b : cap);
+}
+
+hipError_t transform_n32(uint64_t *data, size_t n, bool fwd, const ring::NegaTables &tb, hipStream_t st) {
+  if (fwd)
+    hipLaunchKernelGGL(k_xform_n32<true>, dim3(half_blocks(n, 4096)), dim3(256), 0, st, data, n, tb.mid);
+  else
+    hipLaunchKernelGGL(k_xform_n32<false>, dim3(half_blocks(n, 4096)), dim3(256), 0, st, data, n, tb.mid);
+  return hipGetLastError();
+}
+hipError_t from_w_ccs_n32(const uint64_t *w_ccs, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *f,
+                          const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err, hipStream_t st) {
+  hipLaunchKernelGGL(k_from_w_ccs_n32, dim3(half_blocks(W, 4096)), dim3(256), 0, st, w_ccs, W, lb, L, f_coeff,
+                     f, fwd.mid, inv.mid, err);
+  return hipGetLastError();
+}
+hipError_t from_f_n32(const uint64_t *f, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *w_ccs,
+                      const ring::NegaTables &inv, hipStream_t st) {
+  hipLaunchKernelGGL(k_from_f_n32, dim3(half_blocks(W, 4096)), dim3(256), 0, st, f, W, lb, L, f_coeff, w_ccs,
+                     inv.mid);
+  return hipGetLastError();
+}
+hipError_t decompose_n32(const uint64_t *f_coeff, size_t N, int lb, int L, int K, uint64_t *f_coeff_k,
+                         uint64_t *f_k, uint64_t *w_ccs_k, const ring::NegaTables &fwd, int *err,
+                         hipStream_t st) {
+  if (K > 15) return hipErrorInvalidValue;
+  const unsigned nb = half_blocks(N / L, 4096);
+#define LF_DN(LL)                                                                                        \
+  case LL:                                                                                               \
+    hipLaunchKernelGGL(k_decompose_n32<LL>, dim3(nb), dim3(256), 0, st, f_coeff, N, lb, K, f_coeff_k, f_k, \
+                       w_ccs_k, fwd.mid, err);                                                           \
+    break;
+  switch (L) {
+    LF_DN(1) LF_DN(2) LF_DN(3) LF_DN(4) LF_DN(5) LF_DN(6) LF_DN(7) LF_DN(8) default : return hipErrorInvalidValue;
+  }
+#undef LF_DN
+  return hipGetLastError();
+}
+
+}  // namespace lfk

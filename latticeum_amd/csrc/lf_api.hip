@@ -104,7 +104,7 @@ int get_tables(lf_ctx *c, int d, Tables *&out) {
   }
   Tables t;
   if (d != 24) {
-    const size_t extra = d == 1024 ? 2048 : 0;  // one-wave DFT pass-1 twiddles
+    const size_t extra = d == 1024 ? 2048 : 0;  // 32 x 32 NTT middle factors (fwd, inv)
     std::vector<uint64_t> h(4 * (size_t)d + extra);
     const uint64_t psi = gl::pow(7, (gl::P - 1) / (2 * (uint64_t)d));
     const uint64_t psi_inv = gl::inv(psi), w = gl::mul(psi, psi), w_inv = gl::mul(psi_inv, psi_inv);
@@ -120,25 +120,29 @@ int get_tables(lf_ctx *c, int d, Tables *&out) {
       x = gl::mul(x, psi_inv);
       y = gl::mul(y, w_inv);
     }
+    // ring.hpp stockham4: omega^(d/4) is the shift 2^48
+    if (h[d + d / 4] != gl::mul_pow2(1, 48) || h[3 * d + d / 4] != gl::mul_pow2(1, 144))
+      return fail(c, LF_ERR_DEVICE, "unexpected 4th root of unity");
     if (extra) {
-      // ntt1024.hpp relies on w^64 = 2^156, w^16 = 2^39 (all roots of order <= 64 are shifts)
-      if (gl::pow(w, 64) != gl::mul_pow2(1, 156) || gl::pow(w, 16) != gl::mul_pow2(1, 39))
-        return fail(c, LF_ERR_DEVICE, "unexpected root of unity for the one-wave DFT");
-      for (int lane = 0; lane < 64; lane++)
-        for (int k2 = 0; k2 < 16; k2++) {
-          h[4 * d + lane * 16 + k2] = gl::pow(w, (uint64_t)lane * k2);
-          h[4 * d + 1024 + lane * 16 + k2] = gl::pow(w_inv, (uint64_t)lane * k2);
+      // ntt32.hpp relies on psi^32 = 2^39 and psi^64 = 2^78 (shift-only 32-point stages)
+      if (gl::pow(psi, 32) != gl::mul_pow2(1, 39) || gl::pow(psi, 64) != gl::mul_pow2(1, 78))
+        return fail(c, LF_ERR_DEVICE, "unexpected root of unity for the 32 x 32 NTT");
+      auto brv5 = [](int i) { return ((i & 1) << 4) | ((i & 2) << 2) | (i & 4) | ((i & 8) >> 2) | ((i & 16) >> 4); };
+      for (int r = 0; r < 32; r++)
+        for (int i = 0; i < 32; i++) {
+          // forward: psi^((2 brv5(i) + 1) r);  inverse: d^-1 psi^-((2r + 1) brv5(i))
+          h[4 * d + r * 32 + i] = gl::pow(psi, (uint64_t)(2 * brv5(i) + 1) * r);
+          h[4 * d + 1024 + r * 32 + i] = gl::mul(dinv, gl::pow(psi_inv, (uint64_t)(2 * r + 1) * brv5(i)));
         }
     }
     LF_HIP(c, hipMalloc(&t.mem, h.size() * 8));
     LF_HIP(c, hipMemcpy(t.mem, h.data(), h.size() * 8, hipMemcpyHostToDevice));
-    // d = 1024 transforms run the workgroup radix-4 Stockham kernels (measured
-    // 112 M NTT/s vs 74 M NTT/s for the one-wave DFT, tools/kbench.py);
-    // LATTICEUM_AMD_NTT=wave selects the one-wave DFT kernels (kernels_w1024.hip)
+    // d = 1024 runs the register-resident 32 x 32 NTT kernels (kernels_n32.hip);
+    // LATTICEUM_AMD_NTT=stockham selects the workgroup radix-4 Stockham kernels
     const char *sel = getenv("LATTICEUM_AMD_NTT");
-    const bool wave = extra && sel && strcmp(sel, "wave") == 0;
-    t.fwd = {t.mem, t.mem + d, wave ? t.mem + 4 * d : nullptr};
-    t.inv = {t.mem + 2 * d, t.mem + 3 * d, wave ? t.mem + 4 * d + 1024 : nullptr};
+    const bool n32 = extra && !(sel && strcmp(sel, "stockham") == 0);
+    t.fwd = {t.mem, t.mem + d, n32 ? t.mem + 4 * d : nullptr};
+    t.inv = {t.mem + 2 * d, t.mem + 3 * d, n32 ? t.mem + 4 * d + 1024 : nullptr};
   }
   out = &(c->tables[d] = t);
   return LF_OK;

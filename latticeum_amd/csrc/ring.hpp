@@ -161,16 +161,18 @@ __device__ __forceinline__ void fq3acc_final(const Fq3Acc &s, uint64_t *c) {
 struct NegaTables {
   const uint64_t *twist;      // fwd: psi^j ; inv: d^-1 psi^-j
   const uint64_t *roots;      // fwd: omega^e ; inv: omega^-e   (omega = psi^2), e < d
-  const uint64_t *tw1;        // d = 1024 only: [lane][k2] = omega^(+-lane k2) (ntt1024.hpp pass 1)
+  const uint64_t *mid;        // d = 1024 only: 32 x 32 middle factors of the four-step NTT (ntt32.hpp)
 };
 
 // Radix-4 Stockham DFT of size D over LDS buffers x -> y (ping-pong), T threads.
 // Returns the buffer holding the result. Caller has already applied the twist
-// (forward) and applies the inverse twist afterwards (inverse).
-template <int D, int T>
+// (forward) and applies the inverse twist afterwards (inverse). The 4th root
+// omega^(D/4) = 7^((p-1)/4) = 2^48 for every D (checked when the tables are
+// built), so that factor is a shift; the inverse uses 2^-48 = 2^144.
+template <int D, int T, bool INV>
 __device__ __forceinline__ uint64_t *stockham4(uint64_t *x, uint64_t *y, const uint64_t *roots,
                                                int tid) {
-  const uint64_t w4 = roots[D / 4];
+  constexpr int E4 = INV ? 144 : 48;
 #pragma unroll 1
   for (int p = 1; p < D; p <<= 2) {
     const int s = D / (4 * p);
@@ -184,7 +186,7 @@ __device__ __forceinline__ uint64_t *stockham4(uint64_t *x, uint64_t *y, const u
         a3 = gl::mul(a3, roots[3 * s * k]);
       }
       uint64_t t0 = gl::add(a0, a2), t1 = gl::sub(a0, a2);
-      uint64_t t2 = gl::add(a1, a3), t3 = gl::mul(gl::sub(a1, a3), w4);
+      uint64_t t2 = gl::add(a1, a3), t3 = gl::mul_pow2(gl::sub(a1, a3), E4);
       const int j = ((i - k) << 2) + k;
       y[j] = gl::add(t0, t2);
       y[j + p] = gl::add(t1, t3);

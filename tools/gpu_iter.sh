@@ -11,6 +11,9 @@ echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_$TAG.log
 timeout -k 10 400 python bench.py ${BENCH_ARGS} > gpurun_out/bench_$TAG.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench_$TAG.log
 [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python tools/kbench.py > gpurun_out/kb_$TAG.json 2>&1
+rc=$?; echo "kbench rc=$rc"; tail -1 gpurun_out/kb_$TAG.json
+[ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- \
   python bench.py --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/benchprof_$TAG.log 2>&1
 echo "prof rc=$?"
