@@ -766,7 +766,7 @@ hipError_t decompose_witness(const uint64_t *f_coeff, size_t N, int d, int lb, i
                              const ring::NegaTables &fwd, int *err, hipStream_t st) {
   const size_t W = N / L;
   if (W == 0) return hipSuccess;
-  if (d == 1024 && fwd.mid && lbs == 1 && K <= 15 && L <= 8)
+  if (d == 1024 && fwd.mid && lbs == 1 && K <= 15 && L <= 5)
     return decompose_n32(f_coeff, N, lb, L, K, f_coeff_k, f_k, w_ccs_k, fwd, err, st);
   if (d == 24) {
     if (DEC_GROUPS * L > 256) return hipErrorInvalidValue;

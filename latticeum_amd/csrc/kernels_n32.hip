@@ -147,6 +147,7 @@ __global__ void __launch_bounds__(256) k_from_f_n32(const uint64_t *f, size_t W,
   n32::stage_mid(mid_i, mid_ig);
   __syncthreads();
   Half x = half_ctx(lds_all);
+  const uint64_t b_pow = gl::mul_pow2(1, lb);  // B = 2^lb
   for (size_t g = x.unit; g < pair_bound(W); g += x.stride) {
     const bool ok = g < W;
     const size_t gg = ok ? g : 0;
@@ -161,7 +162,7 @@ __global__ void __launch_bounds__(256) k_from_f_n32(const uint64_t *f, size_t W,
 #pragma unroll
       for (int k = 0; k < 32; k++) {
         v[k] = nx[k];
-        acc[k] = (l == L - 1) ? v[k] : gl::add(gl::mul_pow2(acc[k], lb), v[k]);
+        acc[k] = (l == L - 1) ? v[k] : gl::add(gl::mul(acc[k], b_pow), v[k]);
       }
       n32::inverse(v, mid_i, x.lds, x.r);
       if (l > 0) {  // next limb's loads ahead of this limb's stores
@@ -198,22 +199,24 @@ __global__ void __launch_bounds__(256, 1) k_decompose_n32(const uint64_t *f_coef
                                                          const uint64_t *mid_fg, int *err) {
   __shared__ uint64_t lds_all[WPB * n32::WAVE_U64];
   __shared__ uint64_t mid_f[n32::MID_U64];
+  // the group's coefficients as 16-bit sign|magnitude, two per word:
+  // sm[wave][l][q][lane] = x[r + 32 (2q)] | x[r + 32 (2q + 1)] << 16 of limb l
+  // (kept in LDS: in registers they crowd out the NTT's temporaries)
+  __shared__ uint32_t sm_all[WPB][L][16][64];
   n32::stage_mid(mid_f, mid_fg);
   __syncthreads();
   Half x = half_ctx(lds_all);
+  const int lane = threadIdx.x & 63;
+  uint32_t (*sm)[16][64] = sm_all[threadIdx.x >> 6];
   const size_t W = N / L;
+  const uint64_t b_pow = gl::mul_pow2(1, lb);  // B = 2^lb
   for (size_t g = x.unit; g < pair_bound(W); g += x.stride) {
     const bool ok = g < W;
     const size_t gg = ok ? g : 0;
-    // sm[i] holds limb L-1-i as 16-bit sign|magnitude of x[r + 32 k] (two per
-    // word); the limb loop below always reads sm[0] and rotates the array, so
-    // no register array is indexed by a loop variable
-    uint32_t sm[L][16];
     bool bad = false;
-#pragma unroll
-    for (int i = 0; i < L; i++) {
+    for (int l = 0; l < L; l++) {
       uint64_t raw[32];
-      load_row32(f_coeff + (gg * L + (L - 1 - i)) * D + x.r, raw);
+      load_row32(f_coeff + (gg * L + l) * D + x.r, raw);
 #pragma unroll
       for (int k = 0; k < 32; k += 2) {
         const int64_t a = signed_rep(raw[k]), c = signed_rep(raw[k + 1]);
@@ -221,29 +224,27 @@ __global__ void __launch_bounds__(256, 1) k_decompose_n32(const uint64_t *f_coef
         bad |= (ma >> K) != 0 || (mc >> K) != 0;
         const uint32_t ea = (uint32_t)(ma & 0x7FFF) | (a < 0 ? 0x8000u : 0u);
         const uint32_t ec = (uint32_t)(mc & 0x7FFF) | (c < 0 ? 0x8000u : 0u);
-        sm[i][k >> 1] = ea | (ec << 16);
+        sm[l][k >> 1][lane] = ea | (ec << 16);
       }
     }
     if (ok && bad) raise(err, 1);
     for (int kb = 0; kb < K; kb++) {
       uint64_t acc[32];
+#pragma unroll
+      for (int i = 0; i < 32; i++) acc[i] = 0;  // Horner from 0: no per-limb branch
 #pragma unroll 1
       for (int l = L - 1; l >= 0; l--) {
         const size_t e = (size_t)kb * N + gg * L + l;
         int32_t dg[32];
 #pragma unroll
-        for (int k = 0; k < 32; k++) {
-          const uint32_t hw = (sm[0][k >> 1] >> ((k & 1) * 16)) & 0xFFFF;
-          const int32_t bit = (hw >> kb) & 1;
-          dg[k] = (hw & 0x8000) ? -bit : bit;
-        }
-        // rotate: the next limb moves to sm[0]
-#pragma unroll
         for (int q = 0; q < 16; q++) {
-          const uint32_t t0 = sm[0][q];
+          const uint32_t w = sm[l][q][lane];
 #pragma unroll
-          for (int i = 0; i + 1 < L; i++) sm[i][q] = sm[i + 1][q];
-          sm[L - 1][q] = t0;
+          for (int t = 0; t < 2; t++) {
+            const uint32_t hw = w >> (16 * t);
+            const int32_t bit = (hw >> kb) & 1;
+            dg[2 * q + t] = (hw & 0x8000) ? -bit : bit;
+          }
         }
         if (ok) {
           uint64_t *oc = f_coeff_k + e * D + x.r;
@@ -259,7 +260,7 @@ __global__ void __launch_bounds__(256, 1) k_decompose_n32(const uint64_t *f_coef
           for (int i = 0; i < 32; i++) of[32 * n32::brv5(i)] = v[i];
         }
 #pragma unroll
-        for (int i = 0; i < 32; i++) acc[i] = (l == L - 1) ? v[i] : gl::add(gl::mul_pow2(acc[i], lb), v[i]);
+        for (int i = 0; i < 32; i++) acc[i] = gl::add(gl::mul(acc[i], b_pow), v[i]);
       }
       if (ok) {
         uint64_t *ow = w_ccs_k + ((size_t)kb * W + g) * D + x.r;
@@ -299,7 +300,7 @@ hipError_t from_f_n32(const uint64_t *f, size_t W, int lb, int L, uint64_t *f_co
 hipError_t decompose_n32(const uint64_t *f_coeff, size_t N, int lb, int L, int K, uint64_t *f_coeff_k,
                          uint64_t *f_k, uint64_t *w_ccs_k, const ring::NegaTables &fwd, int *err,
                          hipStream_t st) {
-  if (K > 15) return hipErrorInvalidValue;
+  if (K > 15 || L > 5) return hipErrorInvalidValue;  // LDS: 4 waves x L x 4 KiB of packed limbs
   const unsigned nb = half_blocks(N / L, 4096);
 #define LF_DN(LL)                                                                                        \
   case LL:                                                                                               \
@@ -307,7 +308,7 @@ hipError_t decompose_n32(const uint64_t *f_coeff, size_t N, int lb, int L, int K
                        w_ccs_k, fwd.mid, err);                                                           \
     break;
   switch (L) {
-    LF_DN(1) LF_DN(2) LF_DN(3) LF_DN(4) LF_DN(5) LF_DN(6) LF_DN(7) LF_DN(8) default : return hipErrorInvalidValue;
+    LF_DN(1) LF_DN(2) LF_DN(3) LF_DN(4) LF_DN(5) default : return hipErrorInvalidValue;
   }
 #undef LF_DN
   return hipGetLastError();
