@@ -11,40 +11,63 @@
 // over AJ_CPS chunks) and are folded mod p once per wave.
 //
 // Operands are stored in MFMA fragment order (lane map verified on gfx950 by
-// tools/probe/probe_mfma_i8.hip): for slot s, 32-column chunk c, digit k, a
-// 1 KiB tile where lane l (r = l & 31, h = l >> 5) holds element (r, 16h..16h+15)
-// -- row r of A, or vector r of F -- as 16 bytes. The matrix is converted once
-// when the scheme is created; the vectors are converted by k_to_frag per call.
+// tools/probe/probe_mfma_i8.hip): lane l (r = l & 31, h = l >> 5) of the
+// operand for slot s, 32-column chunk c, digit k holds element (r, 16h..16h+15)
+// -- row r of A, or vector r of F -- as 16 bytes.
+//  * A ("row-interleaved"): [s][c][k][lane] -- one 1 KiB tile per digit, so
+//    each load instruction is one contiguous KiB. Built once per scheme.
+//  * F ("vector-major"):    [s/4][c][r][h][k][s%4] -- one vector's pieces for
+//    4 consecutive slots are 64 contiguous bytes, so a producer that emits one
+//    vector at a time for consecutive slots (the fused decomposition,
+//    kernels_n32.hip) writes whole 64-B segments; the 4 waves of a contraction
+//    block take 4 consecutive slots and share every fetched line.
+// Contraction order: the 32 columns of chunk c are the 16-column units
+// u = 2c and 2c + 1; unit u = (G, l) = (u / Lp, u % Lp) holds limb l of the
+// groups 16G .. 16G + 15 (column g Lp + l). With Lp = L (the gadget length)
+// one unit is one limb of 16 consecutive groups, which is what a block of the
+// fused decomposition holds at once; Lp = 1 is the natural column order. A and
+// F use the same order, so the contraction is unchanged.
+#include "frag.hpp"
 #include "kernels.hpp"
 
 namespace lfk {
 
-typedef int v4i __attribute__((ext_vector_type(4)));
-typedef int v16i __attribute__((ext_vector_type(16)));
-
-__device__ __forceinline__ uint64_t d8(uint64_t x) {
-  const uint64_t t = x <= 0x7F7F7F7F7F7F7F7Full ? x : x + 0xFFFFFFFFull;
-  return (t + 0x8080808080808080ull) ^ 0x8080808080808080ull;
-}
 
 // ---------------------------------------------------------------- to fragment order
+FragGeom frag_geom(size_t ncols, int Lp) {
+  FragGeom g;
+  g.Lp = Lp;
+  g.Wp = ncols / Lp;
+  const size_t units = (g.Wp + 15) / 16 * Lp;
+  g.nch = (int)((units + 1) / 2);
+  return g;
+}
+__device__ __forceinline__ size_t frag_column(int c, int t, int Lp, size_t Wp, bool &ok) {
+  const size_t u = 2 * (size_t)c + (t >> 4);
+  const size_t G = u / Lp, l = u % Lp, g = 16 * G + (t & 15);
+  ok = g < Wp;
+  return g * Lp + l;
+}
+
 // block = (16-slot block, 32-column chunk c, group of 8 rows). LDS tile
 // [row][slot][column] of D8 words, rows padded to 34 words so the 16-B
 // column reads of the emit phase are aligned. Rows >= nrows are never
 // written: they only feed MFMA output columns (or rows) that are discarded.
 constexpr int TF_S = 16, TF_R = 8, TF_J = 34;
-__global__ void __launch_bounds__(256) k_to_frag(VecPtrs rows, int nrows, size_t N, int d, int nch,
+template <bool VMAJOR>
+__global__ void __launch_bounds__(256) k_to_frag(VecPtrs rows, int rlo, int rhi, int d, int nch, int Lp, size_t Wp,
                                                  uint4 *frag) {
   __shared__ uint64_t tile[TF_R * TF_S * TF_J];
-  const int sb = blockIdx.x, c = blockIdx.y, r0 = blockIdx.z * TF_R, tid = threadIdx.x;
+  const int sb = blockIdx.x, c = blockIdx.y, r0 = (rlo & ~(TF_R - 1)) + blockIdx.z * TF_R, tid = threadIdx.x;
   // load: 8 rows x 32 columns x (16 slots = 128 B = 8 pieces of 16 B)
 #pragma unroll
   for (int it = 0; it < TF_R * 32 * 8 / 256; it++) {
     const int p = it * 256 + tid;
     const int r = p >> 8, j = (p >> 3) & 31, q = p & 7;
-    const size_t col = (size_t)c * 32 + j;
+    bool ok;
+    const size_t col = frag_column(c, j, Lp, Wp, ok);
     ulonglong2 v = make_ulonglong2(0, 0);
-    if (r0 + r < nrows && col < N)
+    if (r0 + r >= rlo && r0 + r < rhi && ok)
       v = *reinterpret_cast<const ulonglong2 *>(rows.p[r0 + r] + col * d + (size_t)sb * TF_S + 2 * q);
     uint64_t *t = tile + (r * TF_S + 2 * q) * TF_J + j;
     t[0] = d8(v.x);
@@ -54,45 +77,33 @@ __global__ void __launch_bounds__(256) k_to_frag(VecPtrs rows, int nrows, size_t
   // emit: thread = (slot sl, half h, row r); lane (r, h) of the MFMA operand
   // holds columns 16h..16h+15 of one slot as 16 bytes per digit
   const int r = tid & 7, h = (tid >> 3) & 1, sl = tid >> 4;
-  if (r0 + r >= nrows) return;
+  if (r0 + r < rlo || r0 + r >= rhi) return;
   const ulonglong2 *src = reinterpret_cast<const ulonglong2 *>(tile + (r * TF_S + sl) * TF_J + 16 * h);
-  uint32_t lo[16], hi[16];
+  uint64_t x[16];
 #pragma unroll
   for (int q = 0; q < 8; q++) {
-    const ulonglong2 x = src[q];
-    lo[2 * q] = (uint32_t)x.x;
-    hi[2 * q] = (uint32_t)(x.x >> 32);
-    lo[2 * q + 1] = (uint32_t)x.y;
-    hi[2 * q + 1] = (uint32_t)(x.y >> 32);
+    const ulonglong2 t = src[q];
+    x[2 * q] = t.x;
+    x[2 * q + 1] = t.y;
   }
+  uint4 u[8];
+  d8_transpose16(x, u);
   const size_t s = (size_t)sb * TF_S + sl;
-  uint4 *out = frag + ((s * nch + c) * 8) * 64 + r0 + r + 32 * h;
+  if (VMAJOR) {
+    uint4 *out = frag + fv_index(s, nch, c, r0 + r, h);
 #pragma unroll
-  for (int half = 0; half < 2; half++) {
-    const uint32_t *w = half ? hi : lo;
+    for (int b = 0; b < 8; b++) out[4 * b] = u[b];
+  } else {
+    uint4 *out = frag + ((s * nch + c) * 8) * 64 + r0 + r + 32 * h;
 #pragma unroll
-    for (int bb = 0; bb < 4; bb += 2) {  // digits 4*half + bb and + bb + 1
-      uint32_t dw0[4], dw1[4];
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        // [x0_b, x1_b, x0_b+1, x1_b+1] and [x2_b, x3_b, x2_b+1, x3_b+1]
-        const uint32_t sel = (uint32_t)bb | ((uint32_t)(4 + bb) << 8) | ((uint32_t)(bb + 1) << 16) |
-                             ((uint32_t)(5 + bb) << 24);
-        const uint32_t t01 = __builtin_amdgcn_perm(w[4 * q + 1], w[4 * q], sel);
-        const uint32_t t23 = __builtin_amdgcn_perm(w[4 * q + 3], w[4 * q + 2], sel);
-        dw0[q] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
-        dw1[q] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
-      }
-      out[(4 * half + bb) * 64] = make_uint4(dw0[0], dw0[1], dw0[2], dw0[3]);
-      out[(4 * half + bb + 1) * 64] = make_uint4(dw1[0], dw1[1], dw1[2], dw1[3]);
-    }
+    for (int b = 0; b < 8; b++) out[b * 64] = u[b];
   }
 }
 
 // ---------------------------------------------------------------- the contraction
 // one wave = one slot x one column split; one wave per SIMD (15 i32 32x32
 // accumulators = 240 registers). Fragments of chunk c+1 load while chunk c's
-// 64 MFMAs run.
+// 64 MFMAs run. A is row-interleaved, F vector-major (see the top of the file).
 constexpr int AJ_CPS = 320;  // chunks per split (i32 bound: < 512)
 __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const uint4 *Ff, int d, int nch,
                                                       int nvec, int kappa, uint64_t *partial) {
@@ -106,11 +117,11 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const ui
   for (int t = 0; t < 15; t++) acc[t] = (v16i){0};
   if (c0 < c1) {
     const uint4 *pa = Af + ((size_t)s * nch * 8) * 64 + lane;
-    const uint4 *pf = Ff + ((size_t)s * nch * 8) * 64 + lane;
+    const uint4 *pf = Ff + fv_index(s, nch, 0, lane & 31, lane >> 5);
     v4i a[8], b[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-      uint4 x = pa[((size_t)c0 * 8 + k) * 64], y = pf[((size_t)c0 * 8 + k) * 64];
+      uint4 x = pa[((size_t)c0 * 8 + k) * 64], y = pf[(size_t)c0 * FV_CHUNK + 4 * k];
       a[k] = (v4i){(int)x.x, (int)x.y, (int)x.z, (int)x.w};
       b[k] = (v4i){(int)y.x, (int)y.y, (int)y.z, (int)y.w};
     }
@@ -119,7 +130,7 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const ui
       const int cn = c + 1 < c1 ? c + 1 : c;
 #pragma unroll
       for (int k = 0; k < 8; k++) {
-        uint4 x = pa[((size_t)cn * 8 + k) * 64], y = pf[((size_t)cn * 8 + k) * 64];
+        uint4 x = pa[((size_t)cn * 8 + k) * 64], y = pf[(size_t)cn * FV_CHUNK + 4 * k];
         an[k] = (v4i){(int)x.x, (int)x.y, (int)x.z, (int)x.w};
         bn[k] = (v4i){(int)y.x, (int)y.y, (int)y.z, (int)y.w};
       }
@@ -154,35 +165,38 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const ui
 }
 
 // ---------------------------------------------------------------- launchers
-size_t frag_elems(size_t ncols, int d) {  // uint4 count of one fragment buffer
-  const size_t nch = (ncols + 31) / 32;
-  return (size_t)d * nch * 8 * 64;
-}
-int mfma_nsplit(size_t ncols) {
-  const int nch = (int)((ncols + 31) / 32);
-  return (nch + AJ_CPS - 1) / AJ_CPS;
-}
+size_t frag_elems(const FragGeom &g, int d) { return (size_t)d * g.nch * 8 * 64; }  // uint4 per buffer
+int mfma_nsplit(const FragGeom &g) { return (g.nch + AJ_CPS - 1) / AJ_CPS; }
 
-hipError_t to_frag(const VecPtrs &rows, int nrows, size_t ncols, int d, uint4 *frag, hipStream_t st) {
-  if (nrows < 1 || nrows > 32 || d % TF_S) return hipErrorInvalidValue;
-  const int nch = (int)((ncols + 31) / 32);
-  hipLaunchKernelGGL(k_to_frag, dim3(d / TF_S, nch, (nrows + TF_R - 1) / TF_R), dim3(256), 0, st, rows, nrows,
-                     ncols, d, nch, frag);
+// operand rows row0 .. row0 + nrows - 1 <- rows.p[0 .. nrows - 1]
+hipError_t to_frag(const VecPtrs &rows, int nrows, int row0, const FragGeom &g, int d, bool vmajor, uint4 *frag,
+                   hipStream_t st) {
+  if (nrows < 1 || row0 < 0 || row0 + nrows > 32 || d % TF_S) return hipErrorInvalidValue;
+  VecPtrs abs{};
+  for (int i = 0; i < nrows; i++) abs.p[row0 + i] = rows.p[i];
+  const int rhi = row0 + nrows, ztiles = (rhi + TF_R - 1) / TF_R - row0 / TF_R;
+  const dim3 grid(d / TF_S, g.nch, ztiles);
+  if (vmajor)
+    hipLaunchKernelGGL(k_to_frag<true>, grid, dim3(256), 0, st, abs, row0, rhi, d, g.nch, g.Lp, g.Wp, frag);
+  else
+    hipLaunchKernelGGL(k_to_frag<false>, grid, dim3(256), 0, st, abs, row0, rhi, d, g.nch, g.Lp, g.Wp, frag);
   return hipGetLastError();
 }
 
-hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, size_t ncols, int d, const VecPtrs &fv, int nvec,
-                      uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st, hipEvent_t ev0,
+hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, const VecPtrs &fv, int nvec,
+                      bool f_ready, uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st, hipEvent_t ev0,
                       hipEvent_t ev1) {
   if (kappa > 32 || nvec < 1 || nvec > 32) return hipErrorInvalidValue;
-  hipError_t e = to_frag(fv, nvec, ncols, d, Ff, st);
-  if (e != hipSuccess) return e;
-  const int nch = (int)((ncols + 31) / 32), nsplit = mfma_nsplit(ncols);
+  if (!f_ready) {
+    hipError_t e = to_frag(fv, nvec, 0, g, d, true, Ff, st);
+    if (e != hipSuccess) return e;
+  }
+  const int nsplit = mfma_nsplit(g);
   if (ev0) (void)hipEventRecord(ev0, st);
   const size_t waves = (size_t)d * nsplit;
-  hipLaunchKernelGGL(k_ajtai_mfma, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, Af, Ff, d, nch, nvec,
+  hipLaunchKernelGGL(k_ajtai_mfma, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, Af, Ff, d, g.nch, nvec,
                      (int)kappa, partial);
-  e = hipGetLastError();
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (ev1) (void)hipEventRecord(ev1, st);
   return sum_planes(partial, nsplit, (size_t)nvec * kappa * d, cm, st);

@@ -1,0 +1,56 @@
+// frag.hpp -- the signed base-256 digit form (D8) of a residue and the byte
+// transposition into i8-MFMA operand pieces (ajtai_mfma.hip, kernels_n32.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lfk {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+// x == sum_k d_k 256^k (mod p) with digits d_k in [-128, 127], stored as bytes:
+//   t = x <= 0x7F..7F ? x : x + 2^32 - 1;  digits = bytes of (t + 0x80..80) ^ 0x80..80
+__device__ __forceinline__ uint64_t d8(uint64_t x) {
+  const uint64_t t = x <= 0x7F7F7F7F7F7F7F7Full ? x : x + 0xFFFFFFFFull;
+  return (t + 0x8080808080808080ull) ^ 0x8080808080808080ull;
+}
+
+// 16 D8 words (16 columns of one slot) -> 8 operand pieces: u[b] holds digit b
+// of the 16 columns, column jj in byte jj
+__device__ __forceinline__ void d8_transpose16(const uint64_t *x, uint4 *u) {
+  uint32_t lo[16], hi[16];
+#pragma unroll
+  for (int jj = 0; jj < 16; jj++) {
+    lo[jj] = (uint32_t)x[jj];
+    hi[jj] = (uint32_t)(x[jj] >> 32);
+  }
+#pragma unroll
+  for (int half = 0; half < 2; half++) {
+    const uint32_t *w = half ? hi : lo;
+#pragma unroll
+    for (int bb = 0; bb < 4; bb += 2) {  // digits 4*half + bb and + bb + 1
+      uint32_t dw0[4], dw1[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        // [x0_b, x1_b, x0_b+1, x1_b+1] and [x2_b, x3_b, x2_b+1, x3_b+1]
+        const uint32_t sel = (uint32_t)bb | ((uint32_t)(4 + bb) << 8) | ((uint32_t)(bb + 1) << 16) |
+                             ((uint32_t)(5 + bb) << 24);
+        const uint32_t t01 = __builtin_amdgcn_perm(w[4 * q + 1], w[4 * q], sel);
+        const uint32_t t23 = __builtin_amdgcn_perm(w[4 * q + 3], w[4 * q + 2], sel);
+        dw0[q] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
+        dw1[q] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
+      }
+      u[4 * half + bb] = make_uint4(dw0[0], dw0[1], dw0[2], dw0[3]);
+      u[4 * half + bb + 1] = make_uint4(dw1[0], dw1[1], dw1[2], dw1[3]);
+    }
+  }
+}
+
+// vector-major operand layout (uint4 index of digit 0; digit k adds 4k, chunk c adds c FV_CHUNK)
+constexpr size_t FV_CHUNK = 32 * 2 * 8 * 4;
+__device__ __forceinline__ size_t fv_index(size_t s, int nch, int c, int r, int h) {
+  return ((((s >> 2) * nch + c) * 32 + r) * 2 + h) * 32 + (s & 3);
+}
+
+}  // namespace lfk

@@ -46,13 +46,22 @@ hipError_t limb_join(const uint64_t *lo, const uint64_t *hi, size_t n, uint64_t 
 
 hipError_t sum_planes(const uint64_t *partial, int nsplit, size_t len, uint64_t *out, hipStream_t st);
 
-// i8-MFMA Ajtai (ajtai_mfma.hip): negacyclic rings, kappa <= 32, nvec <= 32
-size_t frag_elems(size_t ncols, int d);  // uint4 per fragment buffer
-int mfma_nsplit(size_t ncols);
-hipError_t to_frag(const VecPtrs &rows, int nrows, size_t ncols, int d, uint4 *frag, hipStream_t st);
-hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, size_t ncols, int d, const VecPtrs &fv, int nvec,
-                      uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st, hipEvent_t ev0 = nullptr,
-                      hipEvent_t ev1 = nullptr);
+// i8-MFMA Ajtai (ajtai_mfma.hip): negacyclic rings, kappa <= 32, nvec <= 32.
+// Column (contraction) order: 16-column units u = (u / Lp, u % Lp) = limb l of
+// groups 16G..16G+15; nch 32-column chunks.
+struct FragGeom {
+  int Lp;
+  size_t Wp;
+  int nch;
+};
+FragGeom frag_geom(size_t ncols, int Lp);
+size_t frag_elems(const FragGeom &g, int d);  // uint4 per fragment buffer
+int mfma_nsplit(const FragGeom &g);
+hipError_t to_frag(const VecPtrs &rows, int nrows, int row0, const FragGeom &g, int d, bool vmajor, uint4 *frag,
+                   hipStream_t st);
+hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, const VecPtrs &fv, int nvec,
+                      bool f_ready, uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st,
+                      hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 
 // d = 1024 kernels on the register-resident 32 x 32 NTT (kernels_n32.hip)
 hipError_t transform_n32(uint64_t *data, size_t n, bool fwd, const ring::NegaTables &tb, hipStream_t st);
@@ -63,5 +72,11 @@ hipError_t from_f_n32(const uint64_t *f, size_t W, int lb, int L, uint64_t *f_co
 hipError_t decompose_n32(const uint64_t *f_coeff, size_t N, int lb, int L, int K, uint64_t *f_coeff_k,
                          uint64_t *f_k, uint64_t *w_ccs_k, const ring::NegaTables &fwd, int *err,
                          hipStream_t st);
+// b_small = 2, d = 1024: decomposition that also writes digit planes 1..K-1 as
+// i8-MFMA operand rows row0 .. row0 + K - 2 (vector-major, Lp = L order);
+// smg: N * 512 u32 scratch for the packed coefficients
+hipError_t decompose_fused(const uint64_t *f_coeff, size_t N, int lb, int L, int K, uint32_t *smg,
+                           uint64_t *f_coeff_k, uint64_t *f_k, uint64_t *w_ccs_k, const ring::NegaTables &fwd,
+                           uint4 *frag, int nch, int row0, int *err, hipStream_t st);
 
 }  // namespace lfk

@@ -4,6 +4,7 @@
 // each other and there is no s_barrier on this path. Every global access is a
 // 256-B row per half-wave (lane r touches x[r + 32 k]).
 #include "digits.hpp"
+#include "frag.hpp"
 #include "kernels.hpp"
 #include "ntt32.hpp"
 
@@ -271,7 +272,142 @@ __global__ void __launch_bounds__(256, 1) k_decompose_n32(const uint64_t *f_coef
   }
 }
 
+// ---------------------------------------------------------------- fused decomposition + Ajtai operands
+// The same decomposition, organised for the i8-MFMA commitment: a block of 8
+// waves owns 16 consecutive groups (one per half-wave), so for each digit
+// plane k >= 1 and limb l the block holds one 16-column unit of the Ajtai
+// contraction order (ajtai_mfma.hip, Lp = L) and writes it straight into the
+// vector-major operand buffer -- the planes never make a second trip through
+// HBM to be re-laid out. Per (k, l): NTT (per-wave transpose tile T), then the
+// D8 words of the 16 outputs go through a slot-major staging tile S that
+// overlaps T (three barriers separate the uses), and each thread emits two
+// slots' 128-byte operand pieces.
+//
+// The group's coefficients come pre-packed as 16-bit sign|magnitude
+// (k_pack_sm: smg[(col 16 + q) 32 + r] = x[r + 32(2q)] | x[r + 32(2q+1)] << 16),
+// read back per (k, l), one plane ahead.
+constexpr int FD_WAVES = 8;
+constexpr int FD_SROW = 17;  // staging row stride in u64 (16 columns + pad: conflict-free)
+constexpr int FD_T_U64 = FD_WAVES * n32::WAVE_U64;
+constexpr int FD_S_U64 = D * FD_SROW;
+constexpr int FD_LDS_U64 = FD_T_U64 > FD_S_U64 ? FD_T_U64 : FD_S_U64;
+
+__global__ void k_pack_sm(const uint64_t *f_coeff, size_t N, int K, uint32_t *smg, int *err) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // (col, q, r)
+  if (t >= N * 512) return;
+  const size_t col = t >> 9;
+  const int q = (t >> 5) & 15, r = t & 31;
+  const uint64_t *x = f_coeff + col * D + r + 64 * q;
+  const int64_t a = signed_rep(x[0]), c = signed_rep(x[32]);
+  const uint64_t ma = a < 0 ? (uint64_t)(-a) : (uint64_t)a, mc = c < 0 ? (uint64_t)(-c) : (uint64_t)c;
+  if ((ma >> K) != 0 || (mc >> K) != 0) raise(err, 1);
+  const uint32_t ea = (uint32_t)(ma & 0x7FFF) | (a < 0 ? 0x8000u : 0u);
+  const uint32_t ec = (uint32_t)(mc & 0x7FFF) | (c < 0 ? 0x8000u : 0u);
+  smg[t] = ea | (ec << 16);
+}
+
+__global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg, size_t N, int L, int lb, int K,
+                                                           uint64_t *f_coeff_k, uint64_t *f_k, uint64_t *w_ccs_k,
+                                                           const uint64_t *mid_fg, uint4 *frag, int nch,
+                                                           int row0) {
+  __shared__ uint64_t lds_all[FD_LDS_U64];
+  __shared__ uint64_t mid_f[n32::MID_U64];
+  n32::stage_mid(mid_f, mid_fg);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5, hw = 2 * wib + h;  // hw: this half's group within the block
+  uint64_t *T = lds_all + wib * n32::WAVE_U64 + h * n32::HALF_U64;
+  uint64_t *S = lds_all;
+  const size_t W = N / L, nblk = (W + 15) / 16;
+  const uint64_t b_pow = gl::mul_pow2(1, lb);  // B = 2^lb
+  for (size_t B = blockIdx.x; B < nblk; B += gridDim.x) {
+    const size_t g = 16 * B + hw;
+    const bool ok = g < W;
+    const size_t gg = ok ? g : 0;
+    uint32_t wn[16];  // next plane's packed words
+#pragma unroll
+    for (int q = 0; q < 16; q++) wn[q] = smg[((gg * L + L - 1) * 16 + q) * 32 + r];
+    for (int kb = 0; kb < K; kb++) {
+      uint64_t acc[32];
+#pragma unroll
+      for (int i = 0; i < 32; i++) acc[i] = 0;
+      for (int l = L - 1; l >= 0; l--) {
+        const size_t e = (size_t)kb * N + gg * L + l;
+        int32_t dg[32];
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+#pragma unroll
+          for (int t = 0; t < 2; t++) {
+            const uint32_t hwd = wn[q] >> (16 * t);
+            const int32_t bit = (hwd >> kb) & 1;
+            dg[2 * q + t] = (hwd & 0x8000) ? -bit : bit;
+          }
+        }
+        {  // words for the next (kb, l): limb l - 1, or limb L - 1 of the next plane
+          const int ln = l > 0 ? l - 1 : L - 1;
+#pragma unroll
+          for (int q = 0; q < 16; q++) wn[q] = smg[((gg * L + ln) * 16 + q) * 32 + r];
+        }
+        if (ok) {
+          uint64_t *oc = f_coeff_k + e * D + r;
+#pragma unroll
+          for (int k = 0; k < 32; k++) oc[32 * k] = from_signed(dg[k]);
+        }
+        uint64_t v[32];
+        n32::neg_ct32_digits(dg, v);
+        n32::forward<false>(v, mid_f, T, r);
+        if (ok) {
+          uint64_t *of = f_k + e * D + r;
+#pragma unroll
+          for (int i = 0; i < 32; i++) of[32 * n32::brv5(i)] = v[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 32; i++) acc[i] = gl::add(gl::mul(acc[i], b_pow), v[i]);
+        if (frag && kb > 0) {
+          __syncthreads();  // every wave is past its transpose: S may overwrite T
+#pragma unroll
+          for (int i = 0; i < 32; i++) S[(r + 32 * n32::brv5(i)) * FD_SROW + hw] = d8(v[i]);
+          __syncthreads();
+          const size_t u = B * L + l;  // contraction unit of these 16 columns
+          const int c = (int)(u >> 1), uh = (int)(u & 1), row = row0 + kb - 1;
+#pragma unroll
+          for (int rep = 0; rep < 2; rep++) {
+            const int s = threadIdx.x + 512 * rep;
+            const uint64_t *src = S + s * FD_SROW;
+            uint64_t x[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) x[j] = src[j];
+            uint4 pu[8];
+            d8_transpose16(x, pu);
+            uint4 *out = frag + fv_index(s, nch, c, row, uh);
+#pragma unroll
+            for (int b = 0; b < 8; b++) out[4 * b] = pu[b];
+          }
+          __syncthreads();  // S consumed before the next transpose
+        }
+      }
+      if (ok) {
+        uint64_t *ow = w_ccs_k + ((size_t)kb * W + g) * D + r;
+#pragma unroll
+        for (int i = 0; i < 32; i++) ow[32 * n32::brv5(i)] = acc[i];
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- launchers
+hipError_t decompose_fused(const uint64_t *f_coeff, size_t N, int lb, int L, int K, uint32_t *smg,
+                           uint64_t *f_coeff_k, uint64_t *f_k, uint64_t *w_ccs_k, const ring::NegaTables &fwd,
+                           uint4 *frag, int nch, int row0, int *err, hipStream_t st) {
+  if (K > 15 || !fwd.mid) return hipErrorInvalidValue;
+  const size_t words = N * 512;
+  hipLaunchKernelGGL(k_pack_sm, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st, f_coeff, N, K, smg, err);
+  const size_t nblk = (N / L + 15) / 16;
+  const unsigned grid = (unsigned)(nblk < 2048 ? nblk : 2048);
+  hipLaunchKernelGGL(k_decompose_fused, dim3(grid), dim3(512), 0, st, smg, N, L, lb, K, f_coeff_k, f_k, w_ccs_k,
+                     fwd.mid, frag, nch, row0);
+  return hipGetLastError();
+}
 static unsigned half_blocks(size_t units, unsigned cap) {
   size_t b = (units + 2 * WPB - 1) / (2 * WPB);
   if (b < 1) b = 1;

@@ -42,6 +42,8 @@ struct lf_ctx {
   size_t ybuf_elems = 0;
   uint4 *frag = nullptr;        // vectors in MFMA fragment order (ajtai_mfma.hip)
   size_t frag_elems = 0;
+  uint32_t *smg = nullptr;      // packed coefficients for the fused decomposition
+  size_t smg_elems = 0;
   bool timing = false;
   std::vector<TimedLaunch> pending;
   std::map<int, std::pair<double, long>> stats;  // nvec -> (ms, count)
@@ -50,6 +52,7 @@ struct lf_ctx {
 struct lf_ajtai {
   const uint64_t *A = nullptr;
   uint4 *Af = nullptr;  // A in i8-MFMA fragment order (negacyclic rings, kappa <= 32)
+  lfk::FragGeom geom{};  // contraction order of the fragments (ajtai_mfma.hip)
   bool owned = false;
   size_t kappa = 0, ncols = 0;
   int d = 0;
@@ -199,8 +202,12 @@ int check_repr(lf_ctx *c, int repr) {
   return LF_OK;
 }
 
+// fragment column order: units of 16 groups at one limb for the GoldiLocksDP
+// gadget length L = 5 (what the fused decomposition emits), else natural order
+lfk::FragGeom ajtai_geom(size_t ncols) { return lfk::frag_geom(ncols, ncols % 5 == 0 ? 5 : 1); }
+
 size_t partial_elems(const lf_ajtai *aj, int nvec) {
-  if (aj->Af) return (size_t)lfk::mfma_nsplit(aj->ncols) * nvec * aj->kappa * aj->d;
+  if (aj->Af) return (size_t)lfk::mfma_nsplit(aj->geom) * nvec * aj->kappa * aj->d;
   return lfk::ajtai_partial_elems(aj->kappa, aj->ncols, aj->d, nvec);
 }
 
@@ -210,14 +217,15 @@ int ajtai_launch(lf_ctx *c, const lf_ajtai *aj, const uint64_t *const *vecs, int
   lfk::VecPtrs vp{};
   for (int v = 0; v < nvec; v++) vp.p[v] = vecs[v];
   LF_TRY(reserve(c, partial_elems(aj, nvec)));
-  if (aj->Af) LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->ncols, aj->d)));
+  if (aj->Af) LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->geom, aj->d)));
   hipEvent_t a = nullptr, b = nullptr;
   if (c->timing) {
     LF_HIP(c, hipEventCreate(&a));
     LF_HIP(c, hipEventCreate(&b));
   }
   if (aj->Af)
-    LF_HIP(c, lfk::ajtai_mfma(aj->Af, aj->kappa, aj->ncols, aj->d, vp, nvec, c->frag, c->scratch, cm, c->cur, a, b));
+    LF_HIP(c, lfk::ajtai_mfma(aj->Af, aj->kappa, aj->geom, aj->d, vp, nvec, false, c->frag, c->scratch, cm, c->cur,
+                              a, b));
   else
     LF_HIP(c, lfk::ajtai_commit(aj->A, aj->kappa, aj->ncols, aj->d, vp, nvec, c->scratch, cm, c->cur, a, b));
   if (c->timing) c->pending.push_back({a, b, nvec});
@@ -227,11 +235,12 @@ int ajtai_launch(lf_ctx *c, const lf_ajtai *aj, const uint64_t *const *vecs, int
 // build the MFMA fragment copy of A (scheme creation)
 int ajtai_prepare(lf_ctx *c, lf_ajtai *aj) {
   if (!use_mfma(aj->d, aj->kappa)) return LF_OK;
-  const size_t n = lfk::frag_elems(aj->ncols, aj->d);
+  aj->geom = ajtai_geom(aj->ncols);
+  const size_t n = lfk::frag_elems(aj->geom, aj->d);
   LF_HIP(c, hipMalloc((void **)&aj->Af, n * sizeof(uint4)));
   lfk::VecPtrs rows{};
   for (size_t i = 0; i < aj->kappa; i++) rows.p[i] = aj->A + i * aj->ncols * aj->d;
-  LF_HIP(c, lfk::to_frag(rows, (int)aj->kappa, aj->ncols, aj->d, aj->Af, c->cur));
+  LF_HIP(c, lfk::to_frag(rows, (int)aj->kappa, 0, aj->geom, aj->d, false, aj->Af, c->cur));
   LF_HIP(c, hipStreamSynchronize(c->cur));
   return LF_OK;
 }
@@ -268,22 +277,45 @@ int fold_core(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lb
   LF_TRY(get_tables(c, d, t));
   // decompose_witness for both sides (decomposition.rs:162-167)
   const uint64_t *fc_side[2] = {b->acc_f_coeff, wi_f_coeff};
-  for (int s = 0; s < 2; s++)
-    LF_HIP(c, lfk::decompose_witness(fc_side[s], N, d, lb, L, lbs, K, b->fk_coeff[s], b->fk[s], b->wk[s],
-                                     t->fwd, c->d_err, c->cur));
-  // commit_witnesses: 2(K-1) commitments sharing one pass over A (decomposition.rs:185-188)
-  std::vector<const uint64_t *> vecs;
   const int extra = commit_f ? 1 : 0;
-  if (commit_f) {
-    vecs.push_back(commit_f);
-    cm_i = commit_cm;
-  }
-  for (int s = 0; s < 2; s++)
-    for (int k = 1; k < K; k++) vecs.push_back(b->fk[s] + (size_t)k * N * d);
+  const int nvec = extra + 2 * (K - 1);
   const size_t kd = kappa * (size_t)d;
-  LF_TRY(grow(c, c->ybuf, c->ybuf_elems, vecs.size() * kd));
+  LF_TRY(grow(c, c->ybuf, c->ybuf_elems, (size_t)nvec * kd));
   uint64_t *ycat = c->ybuf;
-  LF_TRY(ajtai_launch(c, aj, vecs.data(), (int)vecs.size(), ycat));
+  // fused path (d = 1024, b_small = 2, fragment order grouped by this L): the
+  // decomposition writes its digit planes straight into the MFMA operand buffer
+  const bool fused = aj->Af && aj->geom.Lp == L && d == 1024 && lbs == 1 && K <= 15 && t->fwd.mid;
+  if (fused) {
+    LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->geom, d)));
+    LF_TRY(grow(c, c->smg, c->smg_elems, N * 512));
+    for (int s = 0; s < 2; s++)
+      LF_HIP(c, lfk::decompose_fused(fc_side[s], N, lb, L, K, c->smg, b->fk_coeff[s], b->fk[s], b->wk[s], t->fwd,
+                                     c->frag, aj->geom.nch, extra + s * (K - 1), c->d_err, c->cur));
+    lfk::VecPtrs vp{};
+    if (commit_f) {
+      vp.p[0] = commit_f;
+      LF_HIP(c, lfk::to_frag(vp, 1, 0, aj->geom, d, true, c->frag, c->cur));
+    }
+    LF_TRY(reserve(c, partial_elems(aj, nvec)));
+    hipEvent_t ea = nullptr, eb = nullptr;
+    if (c->timing) {
+      LF_HIP(c, hipEventCreate(&ea));
+      LF_HIP(c, hipEventCreate(&eb));
+    }
+    LF_HIP(c, lfk::ajtai_mfma(aj->Af, kappa, aj->geom, d, vp, nvec, true, c->frag, c->scratch, ycat, c->cur, ea, eb));
+    if (c->timing) c->pending.push_back({ea, eb, nvec});
+  } else {
+    for (int s = 0; s < 2; s++)
+      LF_HIP(c, lfk::decompose_witness(fc_side[s], N, d, lb, L, lbs, K, b->fk_coeff[s], b->fk[s], b->wk[s],
+                                       t->fwd, c->d_err, c->cur));
+    // commit_witnesses: 2(K-1) commitments sharing one pass over A (decomposition.rs:185-188)
+    std::vector<const uint64_t *> vecs;
+    if (commit_f) vecs.push_back(commit_f);
+    for (int s = 0; s < 2; s++)
+      for (int k = 1; k < K; k++) vecs.push_back(b->fk[s] + (size_t)k * N * d);
+    LF_TRY(ajtai_launch(c, aj, vecs.data(), (int)vecs.size(), ycat));
+  }
+  if (commit_f) cm_i = commit_cm;
   if (commit_f) LF_HIP(c, hipMemcpyAsync(commit_cm, ycat, kd * 8, hipMemcpyDeviceToDevice, c->cur));
   const uint64_t *cm_side[2] = {b->acc_cm, cm_i};
   for (int s = 0; s < 2; s++) {
@@ -368,6 +400,7 @@ void lf_ctx_destroy(lf_ctx *c) {
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->ybuf) (void)hipFree(c->ybuf);
   if (c->frag) (void)hipFree(c->frag);
+  if (c->smg) (void)hipFree(c->smg);
   if (c->d_err) (void)hipFree(c->d_err);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
@@ -404,7 +437,8 @@ int lf_ctx_reserve(lf_ctx *c, size_t kappa, size_t ncols, int d, int nvec) {
   probe.d = d;
   if (use_mfma(d, kappa)) {
     probe.Af = reinterpret_cast<uint4 *>(1);  // sizing only
-    LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(ncols, d)));
+    probe.geom = ajtai_geom(ncols);
+    LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(probe.geom, d)));
   }
   LF_TRY(reserve(c, partial_elems(&probe, nvec)));
   return grow(c, c->ybuf, c->ybuf_elems, (size_t)nvec * kappa * d);

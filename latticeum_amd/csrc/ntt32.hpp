@@ -149,16 +149,19 @@ __device__ __forceinline__ void stage_mid(uint64_t *midT, const uint64_t *mid) {
   }
 }
 __device__ __forceinline__ void mul_mid(uint64_t *v, const uint64_t *midT, int r) {
-  // all 32 reads issued before the first product (one LDS wait, not 16)
-  uint64_t t[32];
+  // reads issued 16 at a time before their products (two LDS waits, not 16)
 #pragma unroll
-  for (int i = 0; i < 32; i++) t[i] = midT[i * 32 + r];
+  for (int i0 = 0; i0 < 32; i0 += 16) {
+    uint64_t t[16];
 #pragma unroll
-  for (int i = 0; i < 32; i += 8)
-    asm volatile("" : "+v"(t[i]), "+v"(t[i + 1]), "+v"(t[i + 2]), "+v"(t[i + 3]), "+v"(t[i + 4]), "+v"(t[i + 5]),
-                 "+v"(t[i + 6]), "+v"(t[i + 7]));
+    for (int i = 0; i < 16; i++) t[i] = midT[(i0 + i) * 32 + r];
 #pragma unroll
-  for (int i = 0; i < 32; i++) v[i] = gl::mul(v[i], t[i]);
+    for (int i = 0; i < 16; i += 8)
+      asm volatile("" : "+v"(t[i]), "+v"(t[i + 1]), "+v"(t[i + 2]), "+v"(t[i + 3]), "+v"(t[i + 4]), "+v"(t[i + 5]),
+                   "+v"(t[i + 6]), "+v"(t[i + 7]));
+#pragma unroll
+    for (int i = 0; i < 16; i++) v[i0 + i] = gl::mul(v[i0 + i], t[i]);
+  }
 }
 
 // forward from coefficient layout to slot layout (stage 1 done by the caller
