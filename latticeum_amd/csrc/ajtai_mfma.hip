@@ -105,59 +105,92 @@ __global__ void __launch_bounds__(256) k_to_frag(VecPtrs rows, int rlo, int rhi,
 // accumulators = 240 registers). Fragments of chunk c+1 load while chunk c's
 // 64 MFMAs run. A is row-interleaved, F vector-major (see the top of the file).
 constexpr int AJ_CPS = 320;  // chunks per split (i32 bound: < 512)
+// The 4 waves of a block take 4 consecutive slots (same split). Both operands
+// stream into LDS with global_load_lds_dwordx4 (no staging registers):
+//  * A: each wave copies its 8 KiB (8 one-KiB tiles, lane order) per chunk;
+//  * F: the 4 slots' pieces form one contiguous 32 KiB tile per chunk; the
+//    block copies it in 32 one-KiB pieces, lane i of piece j taking global
+//    piece 64 j + pi_j(i), pi_j(i) = i ^ (2 (j & 7) | (i >> 5 & 1)) (an
+//    involution inside the KiB, so every copy stays one coalesced KiB); a wave
+//    then reads its operand for digit k with 64 lanes over 16 distinct bank
+//    groups per 16 lanes (conflict-free ds_read_b128).
+typedef __attribute__((address_space(3))) void lds_void;
+__device__ __forceinline__ int fl_pi(int j, int i) { return i ^ (((j & 7) << 1) | ((i >> 5) & 1)); }
+
 __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const uint4 *Ff, int d, int nch,
                                                       int nvec, int kappa, uint64_t *partial) {
-  const int lane = threadIdx.x & 63;
-  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int s = gw % d, js = gw / d;
-  if (js >= (nch + AJ_CPS - 1) / AJ_CPS) return;
+  __shared__ uint4 Al[2][4][8 * 64];
+  __shared__ uint4 Fl[2][32 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int gw = blockIdx.x * 4 + w;
+  const int s = gw % d, js = gw / d;  // d % 4 == 0: one split per block, slots 4i .. 4i + 3
+  if (js >= (nch + AJ_CPS - 1) / AJ_CPS) return;  // uniform over the block
   const int c0 = js * AJ_CPS, c1 = min(nch, c0 + AJ_CPS);
   v16i acc[15];
 #pragma unroll
   for (int t = 0; t < 15; t++) acc[t] = (v16i){0};
-  if (c0 < c1) {
-    const uint4 *pa = Af + ((size_t)s * nch * 8) * 64 + lane;
-    const uint4 *pf = Ff + fv_index(s, nch, 0, lane & 31, lane >> 5);
+  const uint4 *pa = Af + ((size_t)s * nch * 8) * 64 + lane;
+  const uint4 *ft = Ff + (size_t)(s >> 2) * nch * FV_CHUNK;  // (s/4, chunk 0) tile
+  auto stage = [&](int c, int buf) {
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      __builtin_amdgcn_global_load_lds((const void *)(pa + ((size_t)c * 8 + k) * 64), (lds_void *)&Al[buf][w][k * 64],
+                                       16, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int j = w * 8 + q;
+      __builtin_amdgcn_global_load_lds((const void *)(ft + (size_t)c * FV_CHUNK + j * 64 + fl_pi(j, lane)),
+                                       (lds_void *)&Fl[buf][j * 64], 16, 0, 0);
+    }
+  };
+  // this lane's F operand positions: piece (rh, k, s_lo = w) sits in KiB j = rh >> 1
+  const int rh = 2 * (lane & 31) + (lane >> 5), fj = rh >> 1;
+  int fpos[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) fpos[k] = fj * 64 + fl_pi(fj, (rh & 1) * 32 + k * 4 + w);
+  // per chunk: wait for this wave's copies, barrier (everyone's copies landed,
+  // everyone done reading the other buffer), read both operands into
+  // registers, start the next chunk's copies, then the 64 products -- so the
+  // copies overlap the MFMAs and no wait sits between a copy and its issue
+  stage(c0, 0);
+  for (int c = c0; c < c1; c++) {
+    const int cur = (c - c0) & 1;
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
     v4i a[8], b[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-      uint4 x = pa[((size_t)c0 * 8 + k) * 64], y = pf[(size_t)c0 * FV_CHUNK + 4 * k];
+      const uint4 x = Al[cur][w][k * 64 + lane];
       a[k] = (v4i){(int)x.x, (int)x.y, (int)x.z, (int)x.w};
+      const uint4 y = Fl[cur][fpos[k]];
       b[k] = (v4i){(int)y.x, (int)y.y, (int)y.z, (int)y.w};
     }
-    for (int c = c0; c < c1; c++) {
-      v4i an[8], bn[8];
-      const int cn = c + 1 < c1 ? c + 1 : c;
+    if (c + 1 < c1) stage(c + 1, cur ^ 1);
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        uint4 x = pa[((size_t)cn * 8 + k) * 64], y = pf[(size_t)cn * FV_CHUNK + 4 * k];
-        an[k] = (v4i){(int)x.x, (int)x.y, (int)x.z, (int)x.w};
-        bn[k] = (v4i){(int)y.x, (int)y.y, (int)y.z, (int)y.w};
-      }
+    for (int kb = 0; kb < 8; kb++)
 #pragma unroll
       for (int ka = 0; ka < 8; ka++)
-#pragma unroll
-        for (int kb = 0; kb < 8; kb++)
-          acc[ka + kb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ka], b[kb], acc[ka + kb], 0, 0, 0);
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        a[k] = an[k];
-        b[k] = bn[k];
-      }
-    }
+        acc[ka + kb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ka], b[kb], acc[ka + kb], 0, 0, 0);
   }
   // fold the weights: value = sum_t 2^(8t) acc_t  (mod p); D reg i of lane l is
   // row (i & 3) + 8 (i >> 2) + 4 (l >> 5), column (vector) l & 31
+  // Exactly in int64 by quarters: S_j = sum_{t in 4j..4j+3} acc_t 2^(8(t-4j)),
+  // |S_j| < 2^57; value = S0 + S1 2^32 + S2 2^64 + S3 2^96
+  //                   == (S0 - S2 - S3) + (S1 + S2) 2^32   (2^64 == 2^32 - 1, 2^96 == -1)
   const int v = lane & 31, h = lane >> 5;
+  auto fe = [](int64_t x) { return x < 0 ? (uint64_t)x + gl::P : (uint64_t)x; };  // |x| < 2^63 - p
 #pragma unroll
   for (int i = 0; i < 16; i++) {
-    uint64_t r = 0;
+    int32_t x[15];
 #pragma unroll
-    for (int t = 0; t < 15; t++) {
-      const int32_t x = acc[t][i];
-      const uint64_t fx = x < 0 ? gl::P - (uint64_t)(-(int64_t)x) : (uint64_t)x;
-      r = gl::add(r, gl::mul_pow2(fx, 8 * t));
-    }
+    for (int t = 0; t < 15; t++) x[t] = acc[t][i];
+    // one output's 15 words at a time (the flush must not pull all 240 into VGPRs)
+    asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
+                 "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]));
+    int64_t S[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < 15; t++) S[t >> 2] += (int64_t)x[t] << (8 * (t & 3));
+    const uint64_t r = gl::add(fe(S[0] - S[2] - S[3]), gl::mul_pow2(fe(S[1] + S[2]), 32));
     const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
     if (v < nvec && row < kappa)
       partial[(((size_t)js * nvec + v) * kappa + row) * d + s] = r;
@@ -186,7 +219,7 @@ hipError_t to_frag(const VecPtrs &rows, int nrows, int row0, const FragGeom &g, 
 hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, const VecPtrs &fv, int nvec,
                       bool f_ready, uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st, hipEvent_t ev0,
                       hipEvent_t ev1) {
-  if (kappa > 32 || nvec < 1 || nvec > 32) return hipErrorInvalidValue;
+  if (kappa > 32 || nvec < 1 || nvec > 32 || d % 4) return hipErrorInvalidValue;
   if (!f_ready) {
     hipError_t e = to_frag(fv, nvec, 0, g, d, true, Ff, st);
     if (e != hipSuccess) return e;
