@@ -260,8 +260,13 @@ __global__ void __launch_bounds__(256, 1) k_decompose_n32(const uint64_t *f_coef
 #pragma unroll
           for (int i = 0; i < 32; i++) of[32 * n32::brv5(i)] = v[i];
         }
+        if (lb == 15) {  // GoldiLocksDP B = 2^15: a shift instead of a product
 #pragma unroll
-        for (int i = 0; i < 32; i++) acc[i] = gl::add(gl::mul(acc[i], b_pow), v[i]);
+          for (int i = 0; i < 32; i++) acc[i] = gl::add(gl::shl96(acc[i], 15), v[i]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 32; i++) acc[i] = gl::add(gl::mul(acc[i], b_pow), v[i]);
+        }
       }
       if (ok) {
         uint64_t *ow = w_ccs_k + ((size_t)kb * W + g) * D + x.r;
@@ -361,8 +366,13 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg,
 #pragma unroll
           for (int i = 0; i < 32; i++) of[32 * n32::brv5(i)] = v[i];
         }
+        if (lb == 15) {  // GoldiLocksDP B = 2^15: a shift instead of a product
 #pragma unroll
-        for (int i = 0; i < 32; i++) acc[i] = gl::add(gl::mul(acc[i], b_pow), v[i]);
+          for (int i = 0; i < 32; i++) acc[i] = gl::add(gl::shl96(acc[i], 15), v[i]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 32; i++) acc[i] = gl::add(gl::mul(acc[i], b_pow), v[i]);
+        }
         if (frag && kb > 0) {
           __syncthreads();  // every wave is past its transpose: S may overwrite T
 #pragma unroll

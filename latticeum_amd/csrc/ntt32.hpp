@@ -49,9 +49,11 @@ __device__ __forceinline__ void neg_ct32(uint64_t *a) {
       const int k = (1 << lv) + blk, st = 2 * ln * blk;
 #pragma unroll
       for (int j = st; j < st + ln; j++) {
-        const uint64_t t = gl::mul_pow2(a[j + ln], zexp(k, false));
-        a[j + ln] = gl::sub(a[j], t);
-        a[j] = gl::add(a[j], t);
+        const int e = zexp(k, false);  // 2^e = -2^(e-96) for e >= 96: swap the add and the sub
+        const uint64_t t = gl::shl96(a[j + ln], e % 96);
+        const uint64_t lo = gl::sub(a[j], t), hi = gl::add(a[j], t);
+        a[j + ln] = e < 96 ? lo : hi;
+        a[j] = e < 96 ? hi : lo;
       }
     }
   }
@@ -68,8 +70,9 @@ __device__ __forceinline__ void neg_gs32_inv(uint64_t *a) {
 #pragma unroll
       for (int j = st; j < st + ln; j++) {
         const uint64_t u = a[j], v = a[j + ln];
+        const int e = zexp(k, true);
         a[j] = gl::add(u, v);
-        a[j + ln] = gl::mul_pow2(gl::sub(u, v), zexp(k, true));
+        a[j + ln] = gl::shl96(e < 96 ? gl::sub(u, v) : gl::sub(v, u), e % 96);
       }
     }
   }
@@ -88,7 +91,7 @@ __device__ __forceinline__ void cyc_dif32(uint64_t *a) {
         const uint64_t u = a[st + j], v = a[st + j + ln];
         a[st + j] = gl::add(u, v);
         const int e = wexp(j * (16 / ln), INV);
-        a[st + j + ln] = e ? gl::mul_pow2(gl::sub(u, v), e) : gl::sub(u, v);
+        a[st + j + ln] = gl::shl96(e < 96 ? gl::sub(u, v) : gl::sub(v, u), e % 96);
       }
   }
 }
