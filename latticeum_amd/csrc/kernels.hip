@@ -525,15 +525,23 @@ __global__ void k_commit_y0(const uint64_t *cm, uint64_t *y, size_t n, int lbs, 
 // ============================================================ linear fold
 // LF/nifs/folding.rs:258-268 (f_0) and folding/utils.rs:470-476 (cm_0):
 //   out[j] = sum_i rho_i (.) x_i[j]
+// two adjacent slots per thread (16-B streaming loads; d is even)
 __global__ void __launch_bounds__(256) k_fold_nega(const uint64_t *rho, VecPtrs x, int nwit, size_t n,
                                                   int d, uint64_t *out) {
-  size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  const size_t c = 2 * (blockIdx.x * (size_t)blockDim.x + threadIdx.x);
   if (c >= n * (size_t)d) return;
   const int s = c % d;
-  Acc a;
-  gl::acc_zero(a);
-  for (int i = 0; i < nwit; i++) gl::acc_mad(a, rho[i * d + s], x.p[i][c]);
-  out[c] = gl::acc_reduce(a);
+  gl::CAcc a0, a1;
+  gl::cacc_zero(a0);
+  gl::cacc_zero(a1);
+  for (int i = 0; i < nwit; i++) {
+    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+    const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(x.p[i] + c));
+    const ulonglong2 r = *reinterpret_cast<const ulonglong2 *>(rho + i * d + s);
+    gl::cacc_mad(a0, r.x, v.x);
+    gl::cacc_mad(a1, r.y, v.y);
+  }
+  *reinterpret_cast<ulonglong2 *>(out + c) = make_ulonglong2(gl::cacc_reduce(a0), gl::cacc_reduce(a1));
 }
 __global__ void __launch_bounds__(256) k_fold_phi72(const uint64_t *rho, VecPtrs x, int nwit, size_t n,
                                                    uint64_t *out) {
@@ -860,7 +868,7 @@ hipError_t fold(const uint64_t *rho, const VecPtrs &x, int nwit, size_t n, int d
   if (d == 24)
     hipLaunchKernelGGL(k_fold_phi72, dim3(blocks(n * 8, 256)), dim3(256), 0, st, rho, x, nwit, n, out);
   else
-    hipLaunchKernelGGL(k_fold_nega, dim3(blocks(n * d, 256)), dim3(256), 0, st, rho, x, nwit, n, d, out);
+    hipLaunchKernelGGL(k_fold_nega, dim3(blocks(n * d / 2, 256)), dim3(256), 0, st, rho, x, nwit, n, d, out);
   return hipGetLastError();
 }
 
