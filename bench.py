@@ -51,15 +51,41 @@ def parse():
 
 
 def algorithmic_bytes(d, W, kappa, L=5, K=15):
-    """SURVEY.md §8d bytes/step and the batched-Ajtai launch bytes."""
+    """SURVEY.md §8d bytes/step and the algorithmic bytes of one launch of each
+    step phase (inputs read once + outputs written once)."""
     E, N = 8 * d, W * L
     step = (E * (W + 3 * N + kappa * N + kappa) + 2 * E * (N + K * (2 * N + W))
             + E * (kappa * N + 2 * (K - 1) * N + 2 * (K - 1) * kappa) + E * (2 * K * N + N)
             + E * (2 * N + W))
     nvec = 2 * (K - 1) + 1  # commit(z)'s A.f rides in the decomposition-commitment pass
-    ajtai_batched = E * (kappa * N + nvec * N + nvec * kappa)
-    ajtai_single = E * (kappa * N + N + kappa)
-    return step, ajtai_batched, ajtai_single
+    phases = {
+        # f_coeff in; f_k_coeff, f_k (K N each), w_ccs_k (K W), K-1 planes as i8-MFMA operand rows out
+        "decompose": E * (N + 2 * K * N + K * W + (K - 1) * N),
+        # A and the 29 vectors, both as 8 signed bytes per element, and the 29 kappa-element results
+        "ajtai": E * (kappa * N + nvec * N + nvec * kappa),
+        "fold": E * (2 * K * N + N),
+        "from_w_ccs": E * (W + 2 * N),
+        "from_f": E * (2 * N + W),
+        "to_frag": E * 2 * N,
+    }
+    return step, phases
+
+
+def load_traffic(d, W, kappa):
+    """PMC-measured HBM bytes per launch (profiles/pmc_traffic.json, written by
+    tools/prof_summary.py traffic from separate FETCH_SIZE / WRITE_SIZE passes of
+    this same configuration); {} when absent or for another configuration."""
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    try:
+        doc = json.loads(f.read_text())
+    except (OSError, ValueError):
+        return {}
+    if doc.get("config") != {"d": d, "W": W, "kappa": kappa}:
+        return {}
+    t = {k: v["hbm_bytes_per_launch"] for k, v in doc.get("kernels", {}).items()}
+    if "k_decompose_fused" in t and "k_pack_sm" in t:  # the decompose phase launches both
+        t["k_decompose_fused"] += t["k_pack_sm"]
+    return t
 
 
 def cpu_baseline(d, W_full, kappa, cpu_w, threads):
@@ -165,7 +191,7 @@ def main():
     ctx.sync()
     reducer = LD.AccumulatorReducer(ctx, world, [keep["cm0"], keep["f0"]]) if world > 1 else None
 
-    ctx.kernel_timing(True)
+    ctx.kernel_timing(True)  # HIP events on the stream around every phase (lf_ctx_phase_stats)
     LD.barrier(pg)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -180,12 +206,27 @@ def main():
     dt_max = LD.max_over_ranks(pg, dt)
     nvec = 2 * (K - 1) + 1
     ms_b, n_b = ctx.kernel_stats(nvec)
-    ms_1, n_1 = ctx.kernel_stats(1)
+    timed = {"ajtai": (ms_b, n_b)}
+    for ph in ("from_w_ccs", "decompose", "to_frag", "fold", "from_f"):
+        timed[ph] = ctx.phase_stats(ph)
     ctx.kernel_timing(False)
 
-    step_bytes, aj_bytes, aj1_bytes = algorithmic_bytes(d, W, kappa, L, K)
-    avg_ms = ms_b / max(n_b, 1)
-    achieved = aj_bytes / (avg_ms * 1e-3) / 1e9 if n_b else 0.0
+    step_bytes, ph_bytes = algorithmic_bytes(d, W, kappa, L, K)
+    kernel_of = {"decompose": "k_decompose_fused", "ajtai": "k_ajtai_mfma" if sch.layout == 1 else "k_ajtai_nega",
+                 "fold": "k_fold_nega", "from_w_ccs": "k_from_w_ccs_n32", "from_f": "k_from_f_n32",
+                 "to_frag": "k_to_frag<true>"}
+    traffic = load_traffic(d, W, kappa)
+    phases = {}
+    for ph, (ms, cnt) in timed.items():
+        if not cnt:
+            continue
+        avg = ms / cnt
+        gbs = ph_bytes[ph] / (avg * 1e-3) / 1e9
+        phases[ph] = {"kernel": kernel_of[ph], "avg_launch_ms": avg, "launches_per_step": cnt / args.steps,
+                      "ms_per_step": ms / args.steps, "algorithmic_bytes_per_launch": ph_bytes[ph],
+                      "achieved_gbs": gbs, "frac_hbm": gbs / HBM_PEAK_GBS,
+                      "traffic_bytes_per_launch": traffic.get(kernel_of[ph])}
+    dom = max(phases, key=lambda k: phases[k]["ms_per_step"]) if phases else None
     out = None
     if rank == 0:
         cpu = None
@@ -205,13 +246,15 @@ def main():
                        "d": d, "W": W, "N": N, "kappa": kappa,
                        "parallelism": f"{world} independent step streams (weak)"},
             "hbm_gbs_step_algorithmic": step_bytes * value / world / 1e9,
-            "roofline": {"kernel": ("k_ajtai_mfma (i8 MFMA, 29 vectors)" if sch.layout == 1 else
-                                    "k_ajtai_nega (VALU, 29 vectors)") if d != 24 else "k_ajtai_phi72",
-                         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "avg_launch_ms": avg_ms, "launches": n_b,
-                         "bytes_per_launch": aj_bytes,
-                         "single_commit_avg_ms": ms_1 / max(n_1, 1)},
+            # the dominant phase by device time per step; every phase below (HIP events
+            # on the launch stream, inside the timed region)
+            "roofline": None if dom is None else {
+                "kernel": phases[dom]["kernel"], "phase": dom, "bound": "hbm",
+                "achieved": phases[dom]["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": phases[dom]["frac_hbm"], "traffic": phases[dom]["traffic_bytes_per_launch"],
+                "avg_launch_ms": phases[dom]["avg_launch_ms"],
+                "bytes_per_launch": phases[dom]["algorithmic_bytes_per_launch"]},
+            "phases": phases,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -104,6 +104,16 @@ int lf_ctx_kernel_timing(lf_ctx *ctx, int enable);
 /* device ms summed over, and number of, timed Ajtai launches with nvec
  * vectors (nvec = 0: all) since timing was enabled; synchronises the stream */
 int lf_ctx_kernel_stats(lf_ctx *ctx, int nvec, double *total_ms, long *count);
+/* the same for the phases of lf_dev_fold_step (events on the stream around each) */
+enum {
+  LF_PHASE_FROM_W_CCS = 0, /* commit(z): Witness::from_w_ccs */
+  LF_PHASE_DECOMPOSE = 1,  /* decompose_witness, one record per side (fused: + MFMA operand rows) */
+  LF_PHASE_TO_FRAG = 2,    /* commit(z)'s f into MFMA operand order (fused path) */
+  LF_PHASE_FOLD = 3,       /* f_0 = sum rho_i f_i */
+  LF_PHASE_FROM_F = 4,     /* Witness::from_f(f_0) */
+  LF_PHASE_COUNT = 5
+};
+int lf_ctx_phase_stats(lf_ctx *ctx, int phase, double *total_ms, long *count);
 
 /* ------------------------------------------------------------ host-buffer API (synchronous) */
 int lf_crt(lf_ctx *ctx, uint64_t *elems, size_t n, int d, int repr);

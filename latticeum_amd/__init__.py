@@ -96,6 +96,13 @@ class Context:
         self.check(self.lib.lf_ctx_kernel_stats(self.h, nvec, C.byref(ms), C.byref(cnt)))
         return ms.value, cnt.value
 
+    PHASES = ("from_w_ccs", "decompose", "to_frag", "fold", "from_f")  # lf.h LF_PHASE_*
+
+    def phase_stats(self, phase: str):
+        ms, cnt = C.c_double(), C.c_long()
+        self.check(self.lib.lf_ctx_phase_stats(self.h, self.PHASES.index(phase), C.byref(ms), C.byref(cnt)))
+        return ms.value, cnt.value
+
     # ---------------------------------------------------------------- host-buffer API
     def crt(self, elems, d: int, repr: int = REPR_CANONICAL) -> np.ndarray:
         x = _u64(elems).copy()

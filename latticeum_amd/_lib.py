@@ -43,6 +43,7 @@ SIGNATURES = {
     "lf_ctx_reserve": (I, [VP, SZ, SZ, I, I]),
     "lf_ctx_kernel_timing": (I, [VP, I]),
     "lf_ctx_kernel_stats": (I, [VP, I, C.POINTER(C.c_double), C.POINTER(C.c_long)]),
+    "lf_ctx_phase_stats": (I, [VP, I, C.POINTER(C.c_double), C.POINTER(C.c_long)]),
     "lf_crt": (I, [VP, VP, SZ, I, I]),
     "lf_icrt": (I, [VP, VP, SZ, I, I]),
     "lf_ring_mul": (I, [VP, VP, VP, VP, SZ, I, I]),

@@ -25,7 +25,7 @@ struct Tables {
 
 struct TimedLaunch {
   hipEvent_t a, b;
-  int nvec;
+  int nvec;  // Ajtai launches: vectors per launch; phases: -1 - LF_PHASE_*
 };
 
 }  // namespace
@@ -251,7 +251,7 @@ int drain_timing(lf_ctx *c) {
   for (auto &t : c->pending) {
     float ms = 0;
     LF_HIP(c, hipEventElapsedTime(&ms, t.a, t.b));
-    auto &s = c->stats[t.nvec];
+    auto &s = c->stats[t.nvec];  // nvec < 0: a phase
     s.first += ms;
     s.second += 1;
     (void)hipEventDestroy(t.a);
@@ -265,6 +265,23 @@ int drain_timing(lf_ctx *c) {
 // given (the fused device step), commit(z)'s A.f rides in the same pass over A
 // as the 2(K-1) decomposition commitments (29 vectors, one read of A) and its
 // result lands in `commit_cm`, which is then cm_i.
+// events around one step phase (lf_ctx_phase_stats); no-op unless timing is on
+struct PhaseTimer {
+  lf_ctx *c;
+  int phase;
+  hipEvent_t a = nullptr;
+  PhaseTimer(lf_ctx *ctx, int ph) : c(ctx), phase(ph) {
+    if (c->timing && hipEventCreate(&a) == hipSuccess) (void)hipEventRecord(a, c->cur);
+  }
+  ~PhaseTimer() {
+    hipEvent_t b = nullptr;
+    if (a && hipEventCreate(&b) == hipSuccess) {
+      (void)hipEventRecord(b, c->cur);
+      c->pending.push_back({a, b, -1 - phase});
+    }
+  }
+};
+
 int fold_core(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lbs, size_t W,
               const lf_fold_step_bufs *b, const uint64_t *cm_i, const uint64_t *wi_f_coeff,
               const uint64_t *commit_f = nullptr, uint64_t *commit_cm = nullptr) {
@@ -288,11 +305,14 @@ int fold_core(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lb
   if (fused) {
     LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->geom, d)));
     LF_TRY(grow(c, c->smg, c->smg_elems, N * 512));
-    for (int s = 0; s < 2; s++)
+    for (int s = 0; s < 2; s++) {
+      PhaseTimer pt(c, LF_PHASE_DECOMPOSE);
       LF_HIP(c, lfk::decompose_fused(fc_side[s], N, lb, L, K, c->smg, b->fk_coeff[s], b->fk[s], b->wk[s], t->fwd,
                                      c->frag, aj->geom.nch, extra + s * (K - 1), c->d_err, c->cur));
+    }
     lfk::VecPtrs vp{};
     if (commit_f) {
+      PhaseTimer pt(c, LF_PHASE_TO_FRAG);
       vp.p[0] = commit_f;
       LF_HIP(c, lfk::to_frag(vp, 1, 0, aj->geom, d, true, c->frag, c->cur));
     }
@@ -305,9 +325,11 @@ int fold_core(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lb
     LF_HIP(c, lfk::ajtai_mfma(aj->Af, kappa, aj->geom, d, vp, nvec, true, c->frag, c->scratch, ycat, c->cur, ea, eb));
     if (c->timing) c->pending.push_back({ea, eb, nvec});
   } else {
-    for (int s = 0; s < 2; s++)
+    for (int s = 0; s < 2; s++) {
+      PhaseTimer pt(c, LF_PHASE_DECOMPOSE);
       LF_HIP(c, lfk::decompose_witness(fc_side[s], N, d, lb, L, lbs, K, b->fk_coeff[s], b->fk[s], b->wk[s],
                                        t->fwd, c->d_err, c->cur));
+    }
     // commit_witnesses: 2(K-1) commitments sharing one pass over A (decomposition.rs:185-188)
     std::vector<const uint64_t *> vecs;
     if (commit_f) vecs.push_back(commit_f);
@@ -330,9 +352,13 @@ int fold_core(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lb
       fx.p[s * K + k] = b->fk[s] + (size_t)k * N * d;
       yx.p[s * K + k] = b->y[s] + (size_t)k * kd;
     }
-  LF_HIP(c, lfk::fold(b->rho, fx, 2 * K, N, d, b->f0, c->cur));
+  {
+    PhaseTimer pt(c, LF_PHASE_FOLD);
+    LF_HIP(c, lfk::fold(b->rho, fx, 2 * K, N, d, b->f0, c->cur));
+  }
   LF_HIP(c, lfk::fold(b->rho, yx, 2 * K, kappa, d, b->cm0, c->cur));
   // Witness::from_f(f_0) (arith.rs:299-313)
+  PhaseTimer pt(c, LF_PHASE_FROM_F);
   LF_HIP(c, lfk::from_f(b->f0, N, d, lb, L, b->f0_coeff, b->w_ccs0, t->inv, c->cur));
   return LF_OK;
 }
@@ -452,13 +478,22 @@ int lf_ctx_kernel_timing(lf_ctx *c, int enable) {
   return LF_OK;
 }
 
+int lf_ctx_phase_stats(lf_ctx *c, int phase, double *ms, long *count) {
+  if (!c || !ms || !count || phase < 0 || phase >= LF_PHASE_COUNT) return LF_ERR_INVALID_ARG;
+  LF_TRY(drain_timing(c));
+  auto it = c->stats.find(-1 - phase);
+  *ms = it == c->stats.end() ? 0.0 : it->second.first;
+  *count = it == c->stats.end() ? 0 : it->second.second;
+  return LF_OK;
+}
+
 int lf_ctx_kernel_stats(lf_ctx *c, int nvec, double *ms, long *count) {
   if (!c || !ms || !count) return LF_ERR_INVALID_ARG;
   LF_TRY(drain_timing(c));
   *ms = 0;
   *count = 0;
   for (auto &kv : c->stats)
-    if (nvec == 0 || kv.first == nvec) {
+    if (kv.first > 0 && (nvec == 0 || kv.first == nvec)) {
       *ms += kv.second.first;
       *count += kv.second.second;
     }
@@ -812,7 +847,10 @@ int lf_dev_fold_step(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t 
   if (W * (size_t)pr->L != aj->ncols) return fail(c, LF_ERR_WRONG_WITNESS_LENGTH, "W*L != Ajtai width");
   // commit(z) (zkvm main.rs:348-367): Witness::from_w_ccs; its A f is batched
   // with the decomposition commitments of fold() in a single pass over A
-  LF_TRY(lf_dev_witness_from_w_ccs(c, pr, b->w_ccs, W, b->f_coeff, b->f));
+  {
+    PhaseTimer pt(c, LF_PHASE_FROM_W_CCS);
+    LF_TRY(lf_dev_witness_from_w_ccs(c, pr, b->w_ccs, W, b->f_coeff, b->f));
+  }
   return fold_core(c, aj, pr, lb, lbs, W, b, b->cm, b->f_coeff, b->f, b->cm);
 }
 

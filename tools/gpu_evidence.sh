@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round evidence on the GPU box: parity tests, PMC traffic passes (FETCH_SIZE /
+# WRITE_SIZE separately, MI355X_MICROARCH.md §HBM), the bench line (which reads
+# the traffic file), and a rocprofv3 kernel-trace --stats run of the same bench.
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+TAG=${1:-evidence}
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/pytest_$TAG.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
+ARGS="--steps 3 --warmup 1 --no-cpu-baseline"
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_$TAG -o run --output-format csv -- \
+  python bench.py $ARGS > gpurun_out/pmc_fetch_$TAG.log 2>&1
+rc=$?; echo "fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$TAG -o run --output-format csv -- \
+  python bench.py $ARGS > gpurun_out/pmc_write_$TAG.log 2>&1
+rc=$?; echo "write rc=$rc"; [ $rc -eq 0 ] || exit $rc
+python tools/prof_summary.py traffic gpurun_out/pmc_fetch_$TAG gpurun_out/pmc_write_$TAG \
+  gpurun_out/pmc_traffic_$TAG.json 1024 16384 32 > /dev/null && cp gpurun_out/pmc_traffic_$TAG.json profiles/pmc_traffic.json
+timeout -k 10 400 python bench.py > gpurun_out/bench_$TAG.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench_$TAG.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- \
+  python bench.py --no-cpu-baseline > gpurun_out/benchprof_$TAG.log 2>&1
+echo "prof rc=$?"

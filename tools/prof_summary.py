@@ -2,7 +2,7 @@
 
 usage:
   python tools/prof_summary.py stats  <prof_dir> <out.md>
-  python tools/prof_summary.py traffic <fetch_dir> <write_dir> <out.json> [--kernel k_ajtai_nega]
+  python tools/prof_summary.py traffic <fetch_dir> <write_dir> <out.json> [d W kappa]
 
 `traffic` follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE come from
 separate --pmc passes (TCC slot limits); both are in KiB; on gfx950 FETCH_SIZE
@@ -56,40 +56,47 @@ def stats(prof_dir, out_md):
     print("\n".join(lines))
 
 
-def counter_per_dispatch(d, counter, kernel):
+def counter_per_dispatch(d, counter):
     f = find(d, "counter_collection.csv")
     out = defaultdict(float)
-    grids = {}
+    meta = {}
     for r in csv.DictReader(open(f)):
-        if kernel not in r["Kernel_Name"] or r["Counter_Name"] != counter:
+        if r["Counter_Name"] != counter:
             continue
         did = r["Dispatch_Id"]
         out[did] += float(r["Counter_Value"])
-        grids[did] = grid(r)
-    return out, grids
+        meta[did] = (short(r["Kernel_Name"]).replace("lfk::", ""), grid(r))
+    return out, meta
 
 
-def traffic(fetch_dir, write_dir, out_json, kernel):
-    fetch, grids = counter_per_dispatch(fetch_dir, "FETCH_SIZE", kernel)
-    write, grids_w = counter_per_dispatch(write_dir, "WRITE_SIZE", kernel)
-    res = defaultdict(lambda: {"fetch_kib": [], "write_kib": []})
+def traffic(fetch_dir, write_dir, out_json, config):
+    """Per kernel (the grid that moves the most bytes, e.g. the f-fold rather
+    than the cm-fold): HBM bytes per launch = (2 FETCH_SIZE + WRITE_SIZE) KiB."""
+    fetch, mf = counter_per_dispatch(fetch_dir, "FETCH_SIZE")
+    write, mw = counter_per_dispatch(write_dir, "WRITE_SIZE")
+    acc = defaultdict(lambda: {"fetch_kib": [], "write_kib": []})
     for did, v in fetch.items():
-        res[grids[did]]["fetch_kib"].append(v)
+        acc[mf[did]]["fetch_kib"].append(v)
     for did, v in write.items():
-        res[grids_w[did]]["write_kib"].append(v)
-    summary = {}
-    for g, r in res.items():
-        fk = sum(r["fetch_kib"]) / max(len(r["fetch_kib"]), 1)
-        wk = sum(r["write_kib"]) / max(len(r["write_kib"]), 1)
-        summary[g] = {"launches": len(r["fetch_kib"]), "fetch_kib_raw": fk, "write_kib": wk,
-                      "hbm_bytes_per_launch": (2 * fk + wk) * 1024}
+        acc[mw[did]]["write_kib"].append(v)
+    kernels = {}
+    for (name, g), r in acc.items():
+        if not r["fetch_kib"] or not r["write_kib"]:
+            continue
+        fk = sum(r["fetch_kib"]) / len(r["fetch_kib"])
+        wk = sum(r["write_kib"]) / len(r["write_kib"])
+        e = {"grid": g, "launches": len(r["fetch_kib"]), "fetch_kib_raw": fk, "write_kib": wk,
+             "hbm_bytes_per_launch": (2 * fk + wk) * 1024}
+        if name not in kernels or e["hbm_bytes_per_launch"] > kernels[name]["hbm_bytes_per_launch"]:
+            kernels[name] = e
     try:
         rev = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
     except Exception:
         rev = "?"
-    doc = {"kernel": kernel, "by_grid": summary, "git": rev,
-           "method": "separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes; bytes = (2*FETCH_SIZE + "
-                     "WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE counts 1/2 of wide streaming reads)"}
+    doc = {"config": config, "kernels": kernels, "git": rev,
+           "method": "separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py; bytes = "
+                     "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE counts 1/2 of wide streaming "
+                     "reads, MI355X_MICROARCH.md §HBM)"}
     json.dump(doc, open(out_json, "w"), indent=1)
     print(json.dumps(doc, indent=1))
 
@@ -98,5 +105,5 @@ if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], sys.argv[3])
     elif sys.argv[1] == "traffic":
-        k = sys.argv[sys.argv.index("--kernel") + 1] if "--kernel" in sys.argv else "k_ajtai"
-        traffic(sys.argv[2], sys.argv[3], sys.argv[4], k)
+        d, W, kappa = (int(x) for x in sys.argv[5:8]) if len(sys.argv) >= 8 else (1024, 16384, 32)
+        traffic(sys.argv[2], sys.argv[3], sys.argv[4], {"d": d, "W": W, "kappa": kappa})
