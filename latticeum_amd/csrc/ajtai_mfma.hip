@@ -119,8 +119,8 @@ __device__ __forceinline__ int fl_pi(int j, int i) { return i ^ (((j & 7) << 1) 
 
 __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const uint4 *Ff, int d, int nch,
                                                       int nvec, int kappa, uint64_t *partial) {
-  __shared__ uint4 Al[2][4][8 * 64];
-  __shared__ uint4 Fl[2][32 * 64];
+  __shared__ uint4 Al[2][4][8 * 64];  // 64 KiB: A copies one chunk ahead
+  __shared__ uint4 Fl[3][32 * 64];    // 96 KiB: F copies two chunks ahead
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int gw = blockIdx.x * 4 + w;
   const int s = gw % d, js = gw / d;  // d % 4 == 0: one split per block, slots 4i .. 4i + 3
@@ -131,11 +131,13 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const ui
   for (int t = 0; t < 15; t++) acc[t] = (v16i){0};
   const uint4 *pa = Af + ((size_t)s * nch * 8) * 64 + lane;
   const uint4 *ft = Ff + (size_t)(s >> 2) * nch * FV_CHUNK;  // (s/4, chunk 0) tile
-  auto stage = [&](int c, int buf) {
+  auto stage_a = [&](int c, int buf) {
 #pragma unroll
     for (int k = 0; k < 8; k++)
       __builtin_amdgcn_global_load_lds((const void *)(pa + ((size_t)c * 8 + k) * 64), (lds_void *)&Al[buf][w][k * 64],
                                        16, 0, 0);
+  };
+  auto stage_f = [&](int c, int buf) {
 #pragma unroll
     for (int q = 0; q < 8; q++) {
       const int j = w * 8 + q;
@@ -148,24 +150,38 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const ui
   int fpos[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) fpos[k] = fj * 64 + fl_pi(fj, (rh & 1) * 32 + k * 4 + w);
-  // per chunk: wait for this wave's copies, barrier (everyone's copies landed,
-  // everyone done reading the other buffer), read both operands into
-  // registers, start the next chunk's copies, then the 64 products -- so the
-  // copies overlap the MFMAs and no wait sits between a copy and its issue
-  stage(c0, 0);
+  // per chunk: wait until this wave's copies of chunk c have landed (the
+  // eight F copies of chunk c + 1 issued last iteration may stay in flight:
+  // vmcnt <= 8), barrier (everyone's copies landed, everyone done reading the
+  // buffers about to be refilled), read both operands into registers, issue
+  // A(c + 1) and F(c + 2), then the 64 products.
+  constexpr int VM8 = (8 & 0xF) | (0x7 << 4) | (0xF << 8);  // s_waitcnt vmcnt(8), other counters free
+  stage_a(c0, 0);
+  stage_f(c0, 0);
+  if (c0 + 1 < c1) stage_f(c0 + 1, 1);
+  int fb = 0;  // F buffer of chunk c (c - c0 mod 3)
   for (int c = c0; c < c1; c++) {
     const int cur = (c - c0) & 1;
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
+    if (c + 1 < c1)
+      __builtin_amdgcn_s_waitcnt(VM8);
+    else
+      __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_s_barrier();  // no fence: the waitcnt above is the only ordering needed
+    // operand reads as inline ds_read_b128: the compiler treats any LDS read
+    // after an LDS-DMA copy as dependent on all of them and would wait for the
+    // F(c + 1) copies that must stay in flight; the one lgkmcnt wait is ours
     v4i a[8], b[8];
+    const uint32_t abase = (uint32_t)(uintptr_t)&Al[cur][w][lane];
+    const uint32_t fbase = (uint32_t)(uintptr_t)&Fl[fb][0];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-      const uint4 x = Al[cur][w][k * 64 + lane];
-      a[k] = (v4i){(int)x.x, (int)x.y, (int)x.z, (int)x.w};
-      const uint4 y = Fl[cur][fpos[k]];
-      b[k] = (v4i){(int)y.x, (int)y.y, (int)y.z, (int)y.w};
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(a[k]) : "v"(abase), "i"(k * 1024));
+      asm volatile("ds_read_b128 %0, %1" : "=v"(b[k]) : "v"(fbase + 16u * fpos[k]));
     }
-    if (c + 1 < c1) stage(c + 1, cur ^ 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (c + 1 < c1) stage_a(c + 1, cur ^ 1);
+    if (c + 2 < c1) stage_f(c + 2, fb == 0 ? 2 : fb - 1);
+    fb = fb == 2 ? 0 : fb + 1;
 #pragma unroll
     for (int kb = 0; kb < 8; kb++)
 #pragma unroll
