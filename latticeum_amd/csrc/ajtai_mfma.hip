@@ -137,12 +137,16 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const ui
       __builtin_amdgcn_global_load_lds((const void *)(pa + ((size_t)c * 8 + k) * 64), (lds_void *)&Al[buf][w][k * 64],
                                        16, 0, 0);
   };
+  // KiB j of an F chunk holds operand row j; wave w copies rows w, w + 4, ..
+  // and skips rows >= nvec (their products only reach discarded outputs)
+  const int nf = (nvec - w + 3) >> 2 < 8 ? (nvec - w + 3) >> 2 : 8;
   auto stage_f = [&](int c, int buf) {
 #pragma unroll
     for (int q = 0; q < 8; q++) {
-      const int j = w * 8 + q;
-      __builtin_amdgcn_global_load_lds((const void *)(ft + (size_t)c * FV_CHUNK + j * 64 + fl_pi(j, lane)),
-                                       (lds_void *)&Fl[buf][j * 64], 16, 0, 0);
+      const int j = 4 * q + w;
+      if (q < nf)
+        __builtin_amdgcn_global_load_lds((const void *)(ft + (size_t)c * FV_CHUNK + j * 64 + fl_pi(j, lane)),
+                                         (lds_void *)&Fl[buf][j * 64], 16, 0, 0);
     }
   };
   // this lane's F operand positions: piece (rh, k, s_lo = w) sits in KiB j = rh >> 1
@@ -150,12 +154,24 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const ui
   int fpos[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) fpos[k] = fj * 64 + fl_pi(fj, (rh & 1) * 32 + k * 4 + w);
-  // per chunk: wait until this wave's copies of chunk c have landed (the
-  // eight F copies of chunk c + 1 issued last iteration may stay in flight:
-  // vmcnt <= 8), barrier (everyone's copies landed, everyone done reading the
+  // per chunk: wait until this wave's copies of chunk c have landed (the nf
+  // F copies of chunk c + 1 issued last iteration may stay in flight:
+  // vmcnt <= nf), barrier (everyone's copies landed, everyone done reading the
   // buffers about to be refilled), read both operands into registers, issue
   // A(c + 1) and F(c + 2), then the 64 products.
-  constexpr int VM8 = (8 & 0xF) | (0x7 << 4) | (0xF << 8);  // s_waitcnt vmcnt(8), other counters free
+  auto wait_vm_nf = [&]() {  // s_waitcnt takes an immediate: one per wave-uniform nf
+    switch (nf) {
+      case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+      case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+      case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+      case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+      case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+      case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+      case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+      case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+  };
   stage_a(c0, 0);
   stage_f(c0, 0);
   if (c0 + 1 < c1) stage_f(c0 + 1, 1);
@@ -163,7 +179,7 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const ui
   for (int c = c0; c < c1; c++) {
     const int cur = (c - c0) & 1;
     if (c + 1 < c1)
-      __builtin_amdgcn_s_waitcnt(VM8);
+      wait_vm_nf();
     else
       __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_s_barrier();  // no fence: the waitcnt above is the only ordering needed
