@@ -325,14 +325,19 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg,
   uint64_t *S = lds_all;
   const size_t W = N / L, nblk = (W + 15) / 16;
   const uint64_t b_pow = gl::mul_pow2(1, lb);  // B = 2^lb
-  for (size_t B = blockIdx.x; B < nblk; B += gridDim.x) {
+  // a task is one digit plane of one block of 16 groups (planes are
+  // independent: small W still fills the chip); consecutive blocks take the
+  // planes of the same groups, so the packed words are shared through L2
+  for (size_t task = blockIdx.x; task < nblk * K; task += gridDim.x) {
+    const size_t B = task / K;
+    const int kb = (int)(task % K);
     const size_t g = 16 * B + hw;
     const bool ok = g < W;
     const size_t gg = ok ? g : 0;
-    uint32_t wn[16];  // next plane's packed words
+    uint32_t wn[16];  // next limb's packed words
 #pragma unroll
     for (int q = 0; q < 16; q++) wn[q] = smg[((gg * L + L - 1) * 16 + q) * 32 + r];
-    for (int kb = 0; kb < K; kb++) {
+    {
       uint64_t acc[32];
 #pragma unroll
       for (int i = 0; i < 32; i++) acc[i] = 0;
@@ -348,7 +353,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg,
             dg[2 * q + t] = (hwd & 0x8000) ? -bit : bit;
           }
         }
-        {  // words for the next (kb, l): limb l - 1, or limb L - 1 of the next plane
+        {  // words for the next limb (at l = 0 a harmless reload of limb L - 1)
           const int ln = l > 0 ? l - 1 : L - 1;
 #pragma unroll
           for (int q = 0; q < 16; q++) wn[q] = smg[((gg * L + ln) * 16 + q) * 32 + r];
@@ -412,8 +417,15 @@ hipError_t decompose_fused(const uint64_t *f_coeff, size_t N, int lb, int L, int
   if (K > 15 || !fwd.mid) return hipErrorInvalidValue;
   const size_t words = N * 512;
   hipLaunchKernelGGL(k_pack_sm, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st, f_coeff, N, K, smg, err);
-  const size_t nblk = (N / L + 15) / 16;
-  const unsigned grid = (unsigned)(nblk < 2048 ? nblk : 2048);
+  // one 8-wave block per CU (LDS-bound); ntask = nblk K tasks spread evenly
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
+      ncu = 256;
+  }
+  const size_t ntask = (N / L + 15) / 16 * (size_t)K;
+  const unsigned grid = (unsigned)(ntask < (size_t)ncu ? ntask : (size_t)ncu);
   hipLaunchKernelGGL(k_decompose_fused, dim3(grid), dim3(512), 0, st, smg, N, L, lb, K, f_coeff_k, f_k, w_ccs_k,
                      fwd.mid, frag, nch, row0);
   return hipGetLastError();
