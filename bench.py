@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--d", type=int, default=1024)
     ap.add_argument("--w", type=int, default=1 << 14, help="w_ccs length W (ring elements)")
     ap.add_argument("--kappa", type=int, default=32)
+    ap.add_argument("--streams", type=int, default=1, help="concurrent step streams per GPU")
+    ap.add_argument("--no-small-shape", dest="small", action="store_false", default=True,
+                    help="skip the W=464 multi-stream measurement reported beside the default workload")
     ap.add_argument("--cpu-baseline", dest="cpu", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu", action="store_false")
     ap.add_argument("--cpu-w", type=int, default=0, help="W of the CPU baseline sample (0 = auto)")
@@ -60,7 +63,7 @@ def algorithmic_bytes(d, W, kappa, L=5, K=15):
     nvec = 2 * (K - 1) + 1  # commit(z)'s A.f rides in the decomposition-commitment pass
     phases = {
         # f_coeff in; f_k_coeff, f_k (K N each), w_ccs_k (K W), K-1 planes as i8-MFMA operand rows out
-        "decompose": E * (N + 2 * K * N + K * W + (K - 1) * N),
+        "decompose": 2 * E * (N + 2 * K * N + K * W + (K - 1) * N),  # both sides in one launch
         # A and the 29 vectors, both as 8 signed bytes per element, and the 29 kappa-element results
         "ajtai": E * (kappa * N + nvec * N + nvec * kappa),
         "fold": E * (2 * K * N + N),
@@ -122,6 +125,115 @@ def cpu_baseline(d, W_full, kappa, cpu_w, threads):
                       f"{dt:.2f} s on {threads} threads; scaled linearly in W"}
 
 
+class Workload:
+    """One fold-step workload resident in HBM: the Ajtai scheme, the accumulator
+    side and rho (shared, read-only), and `streams` independent step streams,
+    each an lf context on its own HIP stream with its own w_ccs and outputs."""
+
+    def __init__(self, LA, torch, local, rank, d, W, kappa, streams):
+        self.LA, self.torch = LA, torch
+        self.d, self.W, self.kappa = d, W, kappa
+        self.pr = pr = LA.goldilocks_dp(d)
+        K, L = pr.K, pr.L
+        self.N = N = W * L
+        i64 = dict(dtype=torch.int64, device=f"cuda:{local}")
+        z = lambda n: torch.empty(n, **i64)
+        ctx = LA.Context(local)
+        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+        A = z(kappa * N * d)
+        ctx.dev_fill_uniform(A, SEED_A)
+        self.sch = sch = LA.AjtaiCommitmentScheme(ctx, device_tensor=A, kappa=kappa, ncols=N, d=d)
+        if sch.layout == 1:  # the scheme keeps A in MFMA fragment order; drop the AoS copy
+            del A
+            torch.cuda.empty_cache()
+        # accumulator side: a previous witness built the reference way (from_w_ccs + commit)
+        acc_w = z(W * d)
+        ctx.dev_fill_uniform(acc_w, SEED_ACC)
+        acc_fc, acc_f, acc_cm = z(N * d), z(N * d), z(kappa * d)
+        ctx.check(ctx.lib.lf_dev_witness_from_w_ccs(ctx.h, LA._lib.C.byref(pr), acc_w.data_ptr(), W,
+                                                    acc_fc.data_ptr(), acc_f.data_ptr()))
+        ctx.dev_ajtai_commit(sch, [acc_f], acc_cm)
+        del acc_w, acc_f
+        # rho: 29 short challenges from seeded bytes (CR/rings/goldilocks.rs:41-67) + ONE, NTT form
+        rng = np.random.default_rng(SEED_RHO)
+        rc = [LA.short_challenge(rng.integers(0, 256, 3 * d // 4, dtype=np.uint8).tobytes(), d)
+              for _ in range(2 * K - 1)]
+        one = np.zeros(d, np.uint64)
+        one[0] = 1
+        rho = torch.from_numpy(np.concatenate(rc + [one]).view(np.int64)).to(f"cuda:{local}")
+        ctx.dev_crt(rho, d)
+        self.ctxs, self.keeps, self.bufs, self.streams = [], [], [], []
+        for i in range(streams):
+            c = ctx if i == 0 else LA.Context(local)
+            if i > 0:
+                st = torch.cuda.Stream()
+                c.set_stream(st.cuda_stream)
+                self.streams.append(st)
+            w_ccs = z(W * d)
+            c.dev_fill_uniform(w_ccs, SEED_W + 7919 * rank + 104729 * i)
+            keep = {
+                "w_ccs": w_ccs, "acc_cm": acc_cm, "acc_f_coeff": acc_fc, "rho": rho,
+                "f_coeff": z(N * d), "f": z(N * d), "cm": z(kappa * d),
+                "fk_coeff": [z(K * N * d) for _ in range(2)], "fk": [z(K * N * d) for _ in range(2)],
+                "wk": [z(K * W * d) for _ in range(2)], "y": [z(K * kappa * d) for _ in range(2)],
+                "f0": z(N * d), "f0_coeff": z(N * d), "w_ccs0": z(W * d), "cm0": z(kappa * d),
+            }
+            bufs = LA.LfFoldStepBufs()
+            for k, v in keep.items():
+                if isinstance(v, list):
+                    for s in range(2):
+                        getattr(bufs, k)[s] = v[s].data_ptr()
+                else:
+                    setattr(bufs, k, v.data_ptr())
+            c.reserve(kappa, N, d, 2 * (K - 1) + 1)
+            self.ctxs.append(c)
+            self.keeps.append(keep)
+            self.bufs.append(bufs)
+        torch.cuda.synchronize()
+
+    def run(self, steps):
+        """`steps` fold steps, round-robin over the step streams (asynchronous)"""
+        S = len(self.ctxs)
+        for i in range(steps):
+            self.ctxs[i % S].dev_fold_step(self.sch, self.pr, self.W, self.bufs[i % S])
+
+    def sync(self):
+        for c in self.ctxs:
+            c.sync()  # surfaces any decomposition overflow
+
+    def close(self):
+        self.sync()
+        self.sch = None
+        self.keeps, self.bufs = [], []
+        for c in self.ctxs:
+            c.close()
+        self.ctxs = []
+
+
+def small_shape(LA, torch, LD, pg, local, rank, world, d, kappa):
+    """SURVEY.md §8d's byte-equivalent real-zkvm shape (W = 464) with concurrent
+    step streams: the per-GPU rate the north-star target (1e4 steps/s on 8 GPUs)
+    is about. Reported beside the default workload, not as `value`."""
+    W, S, steps, warmup = 464, 4, 256, 16
+    wl = Workload(LA, torch, local, rank, d, W, kappa, S)
+    wl.run(warmup)
+    torch.cuda.synchronize()
+    LD.barrier(pg)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    wl.run(steps)
+    torch.cuda.synchronize()
+    LD.barrier(pg)
+    dt = LD.max_over_ranks(pg, time.perf_counter() - t0)
+    wl.close()
+    value = world * steps / dt
+    step_bytes, _ = algorithmic_bytes(d, W, kappa)
+    return {"workload": f"commit+fold step, X^{d}+1 ring, w_ccs W={W} (byte-equivalent to the real zkvm step), "
+                        f"kappa={kappa}, {S} concurrent step streams per GPU",
+            "W": W, "streams": S, "value": value, "unit": "fold-steps/s", "n_gpus": world, "steps": steps,
+            "ms_per_step_per_gpu": dt / steps * 1e3, "hbm_gbs_step_algorithmic": step_bytes * value / world / 1e9}
+
+
 def main():
     args = parse()
     import torch
@@ -135,68 +247,20 @@ def main():
     pg = LD.init(world)
 
     d, W, kappa = args.d, args.w, args.kappa
-    pr = LA.goldilocks_dp(d)
-    K, L = pr.K, pr.L
-    N = W * L
-    ctx = LA.Context(local)
-    stream = torch.cuda.current_stream()
-    ctx.set_stream(stream.cuda_stream)
+    wl = Workload(LA, torch, local, rank, d, W, kappa, args.streams)
+    pr, sch = wl.pr, wl.sch
+    K, L, N = pr.K, pr.L, wl.N
+    ctx, keep, bufs = wl.ctxs[0], wl.keeps[0], wl.bufs[0]
 
-    i64 = dict(dtype=torch.int64, device=f"cuda:{local}")
-    z = lambda n: torch.empty(n, **i64)
-    A = z(kappa * N * d)
-    ctx.dev_fill_uniform(A, SEED_A)
-    sch = LA.AjtaiCommitmentScheme(ctx, device_tensor=A, kappa=kappa, ncols=N, d=d)
-    if sch.layout == 1:  # the scheme keeps A in MFMA fragment order; drop the AoS copy
-        del A
-        torch.cuda.empty_cache()
-    w_ccs = z(W * d)
-    ctx.dev_fill_uniform(w_ccs, SEED_W + 7919 * rank)
-    # accumulator side: a previous witness built the reference way (from_w_ccs + commit)
-    acc_w = z(W * d)
-    ctx.dev_fill_uniform(acc_w, SEED_ACC)
-    acc_fc, acc_f, acc_cm = z(N * d), z(N * d), z(kappa * d)
-    ctx.check(ctx.lib.lf_dev_witness_from_w_ccs(ctx.h, LA._lib.C.byref(pr), acc_w.data_ptr(), W,
-                                                acc_fc.data_ptr(), acc_f.data_ptr()))
-    ctx.dev_ajtai_commit(sch, [acc_f], acc_cm)
-    del acc_w, acc_f
-    # rho: 29 short challenges from seeded bytes (CR/rings/goldilocks.rs:41-67) + ONE, NTT form
-    rng = np.random.default_rng(SEED_RHO)
-    rc = [LA.short_challenge(rng.integers(0, 256, 3 * d // 4, dtype=np.uint8).tobytes(), d)
-          for _ in range(2 * K - 1)]
-    one = np.zeros(d, np.uint64)
-    one[0] = 1
-    rho = torch.from_numpy(np.concatenate(rc + [one]).view(np.int64)).to(f"cuda:{local}")
-    ctx.dev_crt(rho, d)
-
-    keep = {
-        "w_ccs": w_ccs, "acc_cm": acc_cm, "acc_f_coeff": acc_fc, "rho": rho,
-        "f_coeff": z(N * d), "f": z(N * d), "cm": z(kappa * d),
-        "fk_coeff": [z(K * N * d) for _ in range(2)], "fk": [z(K * N * d) for _ in range(2)],
-        "wk": [z(K * W * d) for _ in range(2)], "y": [z(K * kappa * d) for _ in range(2)],
-        "f0": z(N * d), "f0_coeff": z(N * d), "w_ccs0": z(W * d), "cm0": z(kappa * d),
-    }
-    bufs = LA.LfFoldStepBufs()
-    for k, v in keep.items():
-        if isinstance(v, list):
-            for s in range(2):
-                getattr(bufs, k)[s] = v[s].data_ptr()
-        else:
-            setattr(bufs, k, v.data_ptr())
-    ctx.reserve(kappa, N, d, 2 * (K - 1) + 1)
-    ctx.sync()
-
-    for _ in range(args.warmup):
-        ctx.dev_fold_step(sch, pr, W, bufs)
-    ctx.sync()
+    wl.run(args.warmup)
+    wl.sync()
     reducer = LD.AccumulatorReducer(ctx, world, [keep["cm0"], keep["f0"]]) if world > 1 else None
 
     ctx.kernel_timing(True)  # HIP events on the stream around every phase (lf_ctx_phase_stats)
     LD.barrier(pg)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ctx.dev_fold_step(sch, pr, W, bufs)
+    wl.run(args.steps)
     if reducer is not None:
         reducer.reduce()  # RCCL reduce of the folded accumulators (once per timed batch)
     torch.cuda.synchronize()
@@ -257,8 +321,16 @@ def main():
             "phases": phases,
             "cpu_baseline": cpu,
         }
+    del ctx, keep, bufs, reducer, sch
+    wl.close()
+    del wl
+    torch.cuda.empty_cache()
+    if args.small and args.d == 1024:
+        small = small_shape(LA, torch, LD, pg, local, rank, world, args.d, args.kappa)
+        if out is not None:
+            out["small_shape"] = small
+    if out is not None:
         print(json.dumps(out), flush=True)
-    ctx.close()
     LD.finalize(pg)
     return out
 

@@ -72,11 +72,17 @@ hipError_t from_f_n32(const uint64_t *f, size_t W, int lb, int L, uint64_t *f_co
 hipError_t decompose_n32(const uint64_t *f_coeff, size_t N, int lb, int L, int K, uint64_t *f_coeff_k,
                          uint64_t *f_k, uint64_t *w_ccs_k, const ring::NegaTables &fwd, int *err,
                          hipStream_t st);
-// b_small = 2, d = 1024: decomposition that also writes digit planes 1..K-1 as
-// i8-MFMA operand rows row0 .. row0 + K - 2 (vector-major, Lp = L order);
-// smg: N * 512 u32 scratch for the packed coefficients
-hipError_t decompose_fused(const uint64_t *f_coeff, size_t N, int lb, int L, int K, uint32_t *smg,
-                           uint64_t *f_coeff_k, uint64_t *f_k, uint64_t *w_ccs_k, const ring::NegaTables &fwd,
-                           uint4 *frag, int nch, int row0, int *err, hipStream_t st);
+// b_small = 2, d = 1024: decomposition of nside (<= 2) witnesses in one launch
+// that also writes digit planes 1..K-1 of side s as i8-MFMA operand rows
+// row0[s] .. row0[s] + K - 2 (vector-major, Lp = L order); smg: nside N 512 u32
+// scratch for the packed coefficients
+struct FusedSides {
+  const uint64_t *f_coeff[2];
+  uint64_t *f_coeff_k[2], *f_k[2], *w_ccs_k[2];
+  int row0[2];
+  int nside;
+};
+hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K, uint32_t *smg,
+                           const ring::NegaTables &fwd, uint4 *frag, int nch, int *err, hipStream_t st);
 
 }  // namespace lfk

@@ -20,13 +20,14 @@ struct Half {
   size_t stride;   // units per grid-stride step
   uint64_t *lds;   // this half's transpose tile
 };
+template <int NW = WPB>
 __device__ __forceinline__ Half half_ctx(uint64_t *lds_all) {
   Half x;
   const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
   x.r = lane & 31;
   x.h = lane >> 5;
-  x.unit = ((size_t)blockIdx.x * WPB + wib) * 2 + x.h;
-  x.stride = (size_t)gridDim.x * WPB * 2;
+  x.unit = ((size_t)blockIdx.x * NW + wib) * 2 + x.h;
+  x.stride = (size_t)gridDim.x * NW * 2;
   x.lds = lds_all + wib * n32::WAVE_U64 + x.h * n32::HALF_U64;
   return x;
 }
@@ -185,6 +186,109 @@ __global__ void __launch_bounds__(256) k_from_f_n32(const uint64_t *f, size_t W,
   }
 }
 
+// ---------------------------------------------------------------- small-W variants
+// When W half-waves cannot fill the chip, from_w_ccs and from_f run one
+// half-wave per (element, limb): W L units. Both halves of a wave take the same
+// limb of two adjacent elements (unit pair p: limb p % L, elements 2 (p / L) + h).
+constexpr int SPLIT_WPB = 8;  // 8 waves: the LDS of one block per CU (T tiles + tables) either way
+__device__ __forceinline__ void split_unit(size_t u, int L, size_t &j, int &l) {
+  const size_t p = u >> 1;
+  l = (int)(p % L);
+  j = 2 * (p / L) + (u & 1);
+}
+// from_w_ccs: each unit redoes its element's inverse transform (2 transforms per
+// unit instead of 1 + 1/L), then its own limb's digits (the carries of limbs
+// 0..l recomputed) and the forward transform
+__global__ void __launch_bounds__(512) k_from_w_ccs_split(const uint64_t *w_ccs, size_t W, int lb, int L,
+                                                         uint64_t *f_coeff, uint64_t *f, const uint64_t *mid_fg,
+                                                         const uint64_t *mid_ig, int *err) {
+  __shared__ uint64_t lds_all[SPLIT_WPB * n32::WAVE_U64];
+  __shared__ uint64_t mid_f[n32::MID_U64], mid_i[n32::MID_U64];
+  n32::stage_mid(mid_f, mid_fg);
+  n32::stage_mid(mid_i, mid_ig);
+  __syncthreads();
+  Half x = half_ctx<SPLIT_WPB>(lds_all);
+  const size_t units = ((W + 1) & ~(size_t)1) * L;
+  for (size_t u = x.unit; u < units; u += x.stride) {
+    size_t j;
+    int l;
+    split_unit(u, L, j, l);
+    const bool ok = j < W;
+    if (!ok) j = 0;
+    uint64_t v[32];
+    load_row32(w_ccs + j * D + x.r, v);
+    n32::inverse(v, mid_i, x.lds, x.r);
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < 32; k++) {
+      int64_t cur = signed_rep(v[k]), dg = 0;
+      for (int t = 0; t <= l; t++) dg = bal_digit(cur, lb);
+      bad |= l == L - 1 && cur != 0;
+      v[k] = from_signed(dg);
+    }
+    const size_t e = j * L + l;
+    if (ok) {
+      uint64_t *oc = f_coeff + e * D + x.r;
+#pragma unroll
+      for (int k = 0; k < 32; k++) oc[32 * k] = v[k];
+    }
+    n32::forward(v, mid_f, x.lds, x.r);
+    if (ok) {
+      uint64_t *of = f + e * D + x.r;
+#pragma unroll
+      for (int i = 0; i < 32; i++) of[32 * n32::brv5(i)] = v[i];
+    }
+    if (ok && bad) raise(err, 1);
+  }
+}
+// from_f: each unit inverts its own element; the limb-0 units also recompose
+// w_ccs = sum_l B^l f[jL + l] in slot form (Horner from the top limb)
+__global__ void __launch_bounds__(512) k_from_f_split(const uint64_t *f, size_t W, int lb, int L,
+                                                     uint64_t *f_coeff, uint64_t *w_ccs, const uint64_t *mid_ig) {
+  __shared__ uint64_t lds_all[SPLIT_WPB * n32::WAVE_U64];
+  __shared__ uint64_t mid_i[n32::MID_U64];
+  n32::stage_mid(mid_i, mid_ig);
+  __syncthreads();
+  Half x = half_ctx<SPLIT_WPB>(lds_all);
+  const uint64_t b_pow = gl::mul_pow2(1, lb);  // B = 2^lb
+  const size_t units = ((W + 1) & ~(size_t)1) * L;
+  for (size_t u = x.unit; u < units; u += x.stride) {
+    size_t j;
+    int l;
+    split_unit(u, L, j, l);
+    const bool ok = j < W;
+    if (!ok) j = 0;
+    const size_t e = j * L + l;
+    uint64_t v[32];
+    load_row32(f + e * D + x.r, v);
+    if (l == 0) {  // wave-uniform: both halves hold limb 0
+      uint64_t acc[32];
+      load_row32(f + (j * L + L - 1) * D + x.r, acc);
+      for (int l2 = L - 2; l2 >= 0; l2--) {
+        uint64_t t[32];
+        if (l2 > 0)
+          load_row32(f + (j * L + l2) * D + x.r, t);
+        else
+#pragma unroll
+          for (int k = 0; k < 32; k++) t[k] = v[k];
+#pragma unroll
+        for (int k = 0; k < 32; k++) acc[k] = gl::add(gl::mul(acc[k], b_pow), t[k]);
+      }
+      if (ok) {
+        uint64_t *ow = w_ccs + j * D + x.r;
+#pragma unroll
+        for (int k = 0; k < 32; k++) ow[32 * k] = acc[k];
+      }
+    }
+    n32::inverse(v, mid_i, x.lds, x.r);
+    if (ok) {
+      uint64_t *oc = f_coeff + e * D + x.r;
+#pragma unroll
+      for (int k = 0; k < 32; k++) oc[32 * k] = v[k];
+    }
+  }
+}
+
 // ---------------------------------------------------------------- decompose_witness
 // LF/nifs/decomposition.rs:162-167, decomposition/utils.rs:45-49, arith.rs:324-338,
 // specialised to b_small = 2 (GoldiLocksDP): the balanced base-2 digits of v are
@@ -297,10 +401,12 @@ constexpr int FD_T_U64 = FD_WAVES * n32::WAVE_U64;
 constexpr int FD_S_U64 = D * FD_SROW;
 constexpr int FD_LDS_U64 = FD_T_U64 > FD_S_U64 ? FD_T_U64 : FD_S_U64;
 
-__global__ void k_pack_sm(const uint64_t *f_coeff, size_t N, int K, uint32_t *smg, int *err) {
-  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // (col, q, r)
-  if (t >= N * 512) return;
-  const size_t col = t >> 9;
+__global__ void k_pack_sm(FusedSides sd, size_t N, int K, uint32_t *smg, int *err) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // (side, col, q, r)
+  if (t >= sd.nside * N * 512) return;
+  const int side = t >= N * 512;
+  const uint64_t *f_coeff = sd.f_coeff[side];
+  const size_t col = (t >> 9) - side * N;  // smg itself is indexed across sides
   const int q = (t >> 5) & 15, r = t & 31;
   const uint64_t *x = f_coeff + col * D + r + 64 * q;
   const int64_t a = signed_rep(x[0]), c = signed_rep(x[32]);
@@ -311,10 +417,9 @@ __global__ void k_pack_sm(const uint64_t *f_coeff, size_t N, int K, uint32_t *sm
   smg[t] = ea | (ec << 16);
 }
 
-__global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg, size_t N, int L, int lb, int K,
-                                                           uint64_t *f_coeff_k, uint64_t *f_k, uint64_t *w_ccs_k,
-                                                           const uint64_t *mid_fg, uint4 *frag, int nch,
-                                                           int row0) {
+__global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_all, size_t N, int L, int lb,
+                                                           int K, FusedSides sd, const uint64_t *mid_fg,
+                                                           uint4 *frag, int nch) {
   __shared__ uint64_t lds_all[FD_LDS_U64];
   __shared__ uint64_t mid_f[n32::MID_U64];
   n32::stage_mid(mid_f, mid_fg);
@@ -325,12 +430,16 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg,
   uint64_t *S = lds_all;
   const size_t W = N / L, nblk = (W + 15) / 16;
   const uint64_t b_pow = gl::mul_pow2(1, lb);  // B = 2^lb
-  // a task is one digit plane of one block of 16 groups (planes are
-  // independent: small W still fills the chip); consecutive blocks take the
-  // planes of the same groups, so the packed words are shared through L2
-  for (size_t task = blockIdx.x; task < nblk * K; task += gridDim.x) {
-    const size_t B = task / K;
+  // a task is one digit plane of one block of 16 groups of one side (planes
+  // are independent: small W still fills the chip); consecutive blocks take
+  // the planes of the same groups, so the packed words are shared through L2
+  for (size_t task = blockIdx.x; task < sd.nside * nblk * K; task += gridDim.x) {
+    const int side = task >= nblk * K;
+    const size_t B = task / K - side * nblk;
     const int kb = (int)(task % K);
+    const uint32_t *smg = smg_all + side * N * 512;
+    uint64_t *f_coeff_k = sd.f_coeff_k[side], *f_k = sd.f_k[side], *w_ccs_k = sd.w_ccs_k[side];
+    const int row0 = sd.row0[side];
     const size_t g = 16 * B + hw;
     const bool ok = g < W;
     const size_t gg = ok ? g : 0;
@@ -371,7 +480,10 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg,
 #pragma unroll
           for (int i = 0; i < 32; i++) of[32 * n32::brv5(i)] = v[i];
         }
-        if (lb == 15) {  // GoldiLocksDP B = 2^15: a shift instead of a product
+        if (l == L - 1) {  // Horner's first term
+#pragma unroll
+          for (int i = 0; i < 32; i++) acc[i] = v[i];
+        } else if (lb == 15) {  // GoldiLocksDP B = 2^15: a shift instead of a product
 #pragma unroll
           for (int i = 0; i < 32; i++) acc[i] = gl::add(gl::shl96(acc[i], 15), v[i]);
         } else {
@@ -411,12 +523,11 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg,
 }
 
 // ---------------------------------------------------------------- launchers
-hipError_t decompose_fused(const uint64_t *f_coeff, size_t N, int lb, int L, int K, uint32_t *smg,
-                           uint64_t *f_coeff_k, uint64_t *f_k, uint64_t *w_ccs_k, const ring::NegaTables &fwd,
-                           uint4 *frag, int nch, int row0, int *err, hipStream_t st) {
-  if (K > 15 || !fwd.mid) return hipErrorInvalidValue;
-  const size_t words = N * 512;
-  hipLaunchKernelGGL(k_pack_sm, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st, f_coeff, N, K, smg, err);
+hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K, uint32_t *smg,
+                           const ring::NegaTables &fwd, uint4 *frag, int nch, int *err, hipStream_t st) {
+  if (K > 15 || !fwd.mid || sd.nside < 1 || sd.nside > 2) return hipErrorInvalidValue;
+  const size_t words = sd.nside * N * 512;
+  hipLaunchKernelGGL(k_pack_sm, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st, sd, N, K, smg, err);
   // one 8-wave block per CU (LDS-bound); ntask = nblk K tasks spread evenly
   static int ncu = 0;
   if (!ncu) {
@@ -424,10 +535,9 @@ hipError_t decompose_fused(const uint64_t *f_coeff, size_t N, int lb, int L, int
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
       ncu = 256;
   }
-  const size_t ntask = (N / L + 15) / 16 * (size_t)K;
+  const size_t ntask = (N / L + 15) / 16 * (size_t)K * sd.nside;
   const unsigned grid = (unsigned)(ntask < (size_t)ncu ? ntask : (size_t)ncu);
-  hipLaunchKernelGGL(k_decompose_fused, dim3(grid), dim3(512), 0, st, smg, N, L, lb, K, f_coeff_k, f_k, w_ccs_k,
-                     fwd.mid, frag, nch, row0);
+  hipLaunchKernelGGL(k_decompose_fused, dim3(grid), dim3(512), 0, st, smg, N, L, lb, K, sd, fwd.mid, frag, nch);
   return hipGetLastError();
 }
 static unsigned half_blocks(size_t units, unsigned cap) {
@@ -443,14 +553,30 @@ hipError_t transform_n32(uint64_t *data, size_t n, bool fwd, const ring::NegaTab
     hipLaunchKernelGGL(k_xform_n32<false>, dim3(half_blocks(n, 4096)), dim3(256), 0, st, data, n, tb.mid);
   return hipGetLastError();
 }
+// below this W the one-half-wave-per-element kernels leave CUs idle
+constexpr size_t SPLIT_W = 4096;
 hipError_t from_w_ccs_n32(const uint64_t *w_ccs, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *f,
                           const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err, hipStream_t st) {
+  if (W < SPLIT_W) {
+    const size_t units = ((W + 1) & ~(size_t)1) * L;
+    hipLaunchKernelGGL(k_from_w_ccs_split, dim3((unsigned)((units + 2 * SPLIT_WPB - 1) / (2 * SPLIT_WPB))),
+                       dim3(64 * SPLIT_WPB), 0, st, w_ccs, W, lb, L,
+                       f_coeff, f, fwd.mid, inv.mid, err);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_from_w_ccs_n32, dim3(half_blocks(W, 4096)), dim3(256), 0, st, w_ccs, W, lb, L, f_coeff,
                      f, fwd.mid, inv.mid, err);
   return hipGetLastError();
 }
 hipError_t from_f_n32(const uint64_t *f, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *w_ccs,
                       const ring::NegaTables &inv, hipStream_t st) {
+  if (W < SPLIT_W) {
+    const size_t units = ((W + 1) & ~(size_t)1) * L;
+    hipLaunchKernelGGL(k_from_f_split, dim3((unsigned)((units + 2 * SPLIT_WPB - 1) / (2 * SPLIT_WPB))),
+                       dim3(64 * SPLIT_WPB), 0, st, f, W, lb, L, f_coeff,
+                       w_ccs, inv.mid);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_from_f_n32, dim3(half_blocks(W, 4096)), dim3(256), 0, st, f, W, lb, L, f_coeff, w_ccs,
                      inv.mid);
   return hipGetLastError();

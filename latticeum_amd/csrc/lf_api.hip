@@ -304,11 +304,19 @@ int fold_core(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lb
   const bool fused = aj->Af && aj->geom.Lp == L && d == 1024 && lbs == 1 && K <= 15 && t->fwd.mid;
   if (fused) {
     LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->geom, d)));
-    LF_TRY(grow(c, c->smg, c->smg_elems, N * 512));
+    LF_TRY(grow(c, c->smg, c->smg_elems, 2 * N * 512));
+    lfk::FusedSides sd{};
+    sd.nside = 2;
     for (int s = 0; s < 2; s++) {
+      sd.f_coeff[s] = fc_side[s];
+      sd.f_coeff_k[s] = b->fk_coeff[s];
+      sd.f_k[s] = b->fk[s];
+      sd.w_ccs_k[s] = b->wk[s];
+      sd.row0[s] = extra + s * (K - 1);
+    }
+    {  // both sides in one launch
       PhaseTimer pt(c, LF_PHASE_DECOMPOSE);
-      LF_HIP(c, lfk::decompose_fused(fc_side[s], N, lb, L, K, c->smg, b->fk_coeff[s], b->fk[s], b->wk[s], t->fwd,
-                                     c->frag, aj->geom.nch, extra + s * (K - 1), c->d_err, c->cur));
+      LF_HIP(c, lfk::decompose_fused(sd, N, lb, L, K, c->smg, t->fwd, c->frag, aj->geom.nch, c->d_err, c->cur));
     }
     lfk::VecPtrs vp{};
     if (commit_f) {

@@ -114,6 +114,27 @@ def test_witness_from_f(ctx, d):
     assert np.array_equal(fc, ofc) and np.array_equal(w, ow)
 
 
+@pytest.mark.parametrize("W", [4095, 4096, 4101])
+def test_from_w_ccs_and_from_f_both_kernels_sampled(ctx, W):
+    """d = 1024 runs a one-half-wave-per-(element, limb) kernel below W = 4096
+    and one half-wave per element above: both, checked on sampled elements
+    (every element's output depends on that element alone)"""
+    d = 1024
+    pr = params(d)
+    L = pr.L
+    w = rand(W * d, 900 + W)
+    fc, f = ctx.witness_from_w_ccs(w, pr)
+    f_in = rand(W * L * d, 950 + W)
+    fc2, w2 = ctx.witness_from_f(f_in, pr)
+    for j in (0, 1, W // 2, W - 2, W - 1):
+        ofc, of = O.witness_from_w_ccs(w[j * d:(j + 1) * d], d, pr.B, L)
+        assert np.array_equal(fc[j * L * d:(j + 1) * L * d], ofc)
+        assert np.array_equal(f[j * L * d:(j + 1) * L * d], of)
+        ofc2, ow2 = O.witness_from_f(f_in[j * L * d:(j + 1) * L * d], d, pr.B, L)
+        assert np.array_equal(fc2[j * L * d:(j + 1) * L * d], ofc2)
+        assert np.array_equal(w2[j * d:(j + 1) * d], ow2)
+
+
 @pytest.mark.parametrize("d", ALL_D)
 @pytest.mark.parametrize("W", [1, 9, 40])
 def test_decompose_witness(ctx, d, W):
