@@ -118,7 +118,8 @@ typedef __attribute__((address_space(3))) void lds_void;
 __device__ __forceinline__ int fl_pi(int j, int i) { return i ^ (((j & 7) << 1) | ((i >> 5) & 1)); }
 
 __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const uint4 *Ff, int d, int nch,
-                                                      int nvec, int kappa, uint64_t *partial) {
+                                                      int nvec, int kappa, uint64_t *partial, OutPtrs dst,
+                                                      int direct) {
   __shared__ uint4 Al[2][4][8 * 64];  // 64 KiB: A copies one chunk ahead
   __shared__ uint4 Fl[3][32 * 64];    // 96 KiB: F copies two chunks ahead
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -224,8 +225,12 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const ui
     for (int t = 0; t < 15; t++) S[t >> 2] += (int64_t)x[t] << (8 * (t & 3));
     const uint64_t r = gl::add(fe(S[0] - S[2] - S[3]), gl::mul_pow2(fe(S[1] + S[2]), 32));
     const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
-    if (v < nvec && row < kappa)
-      partial[(((size_t)js * nvec + v) * kappa + row) * d + s] = r;
+    if (v < nvec && row < kappa) {
+      if (direct)  // one column split: the result itself
+        dst.p[v][(size_t)row * d + s] = r;
+      else
+        partial[(((size_t)js * nvec + v) * kappa + row) * d + s] = r;
+    }
   }
 }
 
@@ -250,8 +255,10 @@ hipError_t to_frag(const VecPtrs &rows, int nrows, int row0, const FragGeom &g, 
 
 hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, const VecPtrs &fv, int nvec,
                       bool f_ready, uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st, hipEvent_t ev0,
-                      hipEvent_t ev1) {
-  if (kappa > 32 || nvec < 1 || nvec > 32 || d % 4) return hipErrorInvalidValue;
+                      hipEvent_t ev1, const OutPtrs *dst) {
+  if (kappa > 32 || nvec < 1 || nvec > 32 || d % 4 || (!cm && !dst)) return hipErrorInvalidValue;
+  OutPtrs out{};
+  for (int v = 0; v < nvec; v++) out.p[v] = cm ? cm + (size_t)v * kappa * d : dst->p[v];
   if (!f_ready) {
     hipError_t e = to_frag(fv, nvec, 0, g, d, true, Ff, st);
     if (e != hipSuccess) return e;
@@ -260,11 +267,12 @@ hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, c
   if (ev0) (void)hipEventRecord(ev0, st);
   const size_t waves = (size_t)d * nsplit;
   hipLaunchKernelGGL(k_ajtai_mfma, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, Af, Ff, d, g.nch, nvec,
-                     (int)kappa, partial);
+                     (int)kappa, partial, out, nsplit == 1 ? 1 : 0);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (ev1) (void)hipEventRecord(ev1, st);
-  return sum_planes(partial, nsplit, (size_t)nvec * kappa * d, cm, st);
+  if (nsplit == 1) return hipSuccess;
+  return sum_planes_to(partial, nsplit, kappa * (size_t)d, nvec, out, st);
 }
 
 }  // namespace lfk

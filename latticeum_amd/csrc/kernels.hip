@@ -512,6 +512,15 @@ __global__ void k_sum_planes(const uint64_t *partial, int nsplit, size_t len, ui
   out[v * out_stride_vec + r] = gl::acc_reduce(a);
 }
 
+__global__ void k_sum_planes_to(const uint64_t *partial, int nsplit, size_t len, int nvec, OutPtrs out) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= len * nvec) return;
+  Acc a;
+  gl::acc_zero(a);
+  for (int s = 0; s < nsplit; s++) gl::acc_add(a, partial[(size_t)s * len * nvec + i]);
+  out.p[i / len][i % len] = gl::acc_reduce(a);
+}
+
 // ============================================================ commit_witnesses y_0
 // LF/nifs/decomposition.rs:183-200: y_0 = cm - sum_{k>=1} b^k y_k (scalar b)
 __global__ void k_commit_y0(const uint64_t *cm, uint64_t *y, size_t n, int lbs, int K) {
@@ -520,6 +529,30 @@ __global__ void k_commit_y0(const uint64_t *cm, uint64_t *y, size_t n, int lbs, 
   uint64_t acc = 0;
   for (int k = K - 1; k >= 1; k--) acc = gl::mul_pow2(gl::add(acc, y[(size_t)k * n + c]), lbs);
   y[c] = gl::sub(cm[c], acc);
+}
+
+// both sides' y_0 and the folded commitment in one pass (see kernels.hpp y0_cm0)
+__global__ void k_y0_cm0(const uint64_t *cm0s, const uint64_t *cm1s, uint64_t *y0, uint64_t *y1,
+                         const uint64_t *rho, size_t n, int d, int lbs, int K, uint64_t *cm0) {
+  const size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  const int s = c % d;
+  gl::CAcc a;
+  gl::cacc_zero(a);
+  for (int side = 0; side < 2; side++) {
+    uint64_t *y = side ? y1 : y0;
+    const uint64_t *rs = rho + (size_t)side * K * d + s;
+    uint64_t acc = 0;
+    for (int k = K - 1; k >= 1; k--) {
+      const uint64_t v = y[(size_t)k * n + c];
+      gl::cacc_mad(a, rs[(size_t)k * d], v);
+      acc = gl::mul_pow2(gl::add(acc, v), lbs);
+    }
+    const uint64_t v0 = gl::sub((side ? cm1s : cm0s)[c], acc);
+    y[c] = v0;
+    gl::cacc_mad(a, rs[0], v0);
+  }
+  cm0[c] = gl::cacc_reduce(a);
 }
 
 // ============================================================ linear fold
@@ -850,6 +883,23 @@ hipError_t ajtai_commit(const uint64_t *A, size_t kappa, size_t ncols, int d, co
 hipError_t sum_planes(const uint64_t *partial, int nsplit, size_t len, uint64_t *out, hipStream_t st) {
   if (len == 0) return hipSuccess;
   hipLaunchKernelGGL(k_sum_planes, dim3(blocks(len, 256)), dim3(256), 0, st, partial, nsplit, len, out, len, len);
+  return hipGetLastError();
+}
+
+hipError_t sum_planes_to(const uint64_t *partial, int nsplit, size_t len, int nvec, const OutPtrs &out,
+                         hipStream_t st) {
+  if (len == 0 || nvec < 1) return hipSuccess;
+  hipLaunchKernelGGL(k_sum_planes_to, dim3(blocks(len * nvec, 256)), dim3(256), 0, st, partial, nsplit, len, nvec,
+                     out);
+  return hipGetLastError();
+}
+
+hipError_t y0_cm0(const uint64_t *cm0s, const uint64_t *cm1s, uint64_t *y0, uint64_t *y1, const uint64_t *rho,
+                  size_t kappa, int d, int lbs, int K, uint64_t *cm0, hipStream_t st) {
+  const size_t n = kappa * (size_t)d;
+  if (n == 0) return hipSuccess;
+  if (d == 24 || K < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_y0_cm0, dim3(blocks(n, 256)), dim3(256), 0, st, cm0s, cm1s, y0, y1, rho, n, d, lbs, K, cm0);
   return hipGetLastError();
 }
 

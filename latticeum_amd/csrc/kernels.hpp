@@ -14,6 +14,10 @@ namespace lfk {
 struct VecPtrs {
   const uint64_t *p[LF_MAX_VECS];
 };
+// destinations of up to LF_MAX_VECS output vectors
+struct OutPtrs {
+  uint64_t *p[LF_MAX_VECS];
+};
 
 hipError_t transform(uint64_t *data, size_t n, int d, bool fwd, const ring::NegaTables &tb,
                      hipStream_t st);
@@ -45,6 +49,14 @@ hipError_t limb_split(const uint64_t *x, size_t n, uint64_t *lo, uint64_t *hi, h
 hipError_t limb_join(const uint64_t *lo, const uint64_t *hi, size_t n, uint64_t *out, hipStream_t st);
 
 hipError_t sum_planes(const uint64_t *partial, int nsplit, size_t len, uint64_t *out, hipStream_t st);
+// out.p[v][r] = sum_s partial[s][v][r] for nvec vectors of len u64
+hipError_t sum_planes_to(const uint64_t *partial, int nsplit, size_t len, int nvec, const OutPtrs &out,
+                         hipStream_t st);
+// the fold step's epilogue over the kappa d commitment slots, both sides:
+// y_s[0] = cm_s - sum_{k>=1} 2^(k lbs) y_s[k] (decomposition.rs:183-200), then
+// cm0 = sum_{s,k} rho_{sK+k} (.) y_s[k] (folding/utils.rs:470-476); X^d + 1 rings
+hipError_t y0_cm0(const uint64_t *cm0s, const uint64_t *cm1s, uint64_t *y0, uint64_t *y1, const uint64_t *rho,
+                  size_t kappa, int d, int lbs, int K, uint64_t *cm0, hipStream_t st);
 
 // i8-MFMA Ajtai (ajtai_mfma.hip): negacyclic rings, kappa <= 32, nvec <= 32.
 // Column (contraction) order: 16-column units u = (u / Lp, u % Lp) = limb l of
@@ -59,9 +71,10 @@ size_t frag_elems(const FragGeom &g, int d);  // uint4 per fragment buffer
 int mfma_nsplit(const FragGeom &g);
 hipError_t to_frag(const VecPtrs &rows, int nrows, int row0, const FragGeom &g, int d, bool vmajor, uint4 *frag,
                    hipStream_t st);
+// cm: contiguous [nvec][kappa d] results, or (cm == nullptr) per-vector destinations dst
 hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, const VecPtrs &fv, int nvec,
                       bool f_ready, uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st,
-                      hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+                      hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, const OutPtrs *dst = nullptr);
 
 // d = 1024 kernels on the register-resident 32 x 32 NTT (kernels_n32.hip)
 hipError_t transform_n32(uint64_t *data, size_t n, bool fwd, const ring::NegaTables &tb, hipStream_t st);

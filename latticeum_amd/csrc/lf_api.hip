@@ -330,7 +330,13 @@ int fold_core(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lb
       LF_HIP(c, hipEventCreate(&ea));
       LF_HIP(c, hipEventCreate(&eb));
     }
-    LF_HIP(c, lfk::ajtai_mfma(aj->Af, kappa, aj->geom, d, vp, nvec, true, c->frag, c->scratch, ycat, c->cur, ea, eb));
+    // results straight to their places: commit(z)'s cm, then y_s[1..K-1]
+    lfk::OutPtrs dst{};
+    if (commit_f) dst.p[0] = commit_cm;
+    for (int s = 0; s < 2; s++)
+      for (int k = 1; k < K; k++) dst.p[extra + s * (K - 1) + k - 1] = b->y[s] + (size_t)k * kd;
+    LF_HIP(c, lfk::ajtai_mfma(aj->Af, kappa, aj->geom, d, vp, nvec, true, c->frag, c->scratch, nullptr, c->cur, ea,
+                              eb, &dst));
     if (c->timing) c->pending.push_back({ea, eb, nvec});
   } else {
     for (int s = 0; s < 2; s++) {
@@ -346,12 +352,17 @@ int fold_core(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lb
     LF_TRY(ajtai_launch(c, aj, vecs.data(), (int)vecs.size(), ycat));
   }
   if (commit_f) cm_i = commit_cm;
-  if (commit_f) LF_HIP(c, hipMemcpyAsync(commit_cm, ycat, kd * 8, hipMemcpyDeviceToDevice, c->cur));
   const uint64_t *cm_side[2] = {b->acc_cm, cm_i};
-  for (int s = 0; s < 2; s++) {
-    LF_HIP(c, hipMemcpyAsync(b->y[s] + kd, ycat + (extra + (size_t)s * (K - 1)) * kd, (size_t)(K - 1) * kd * 8,
-                             hipMemcpyDeviceToDevice, c->cur));
-    LF_HIP(c, lfk::commit_y0(cm_side[s], b->y[s], kappa, d, lbs, K, c->cur));
+  if (fused) {
+    // y_0 of both sides and cm_0 = sum rho_i y_i in one pass (the y_s[k >= 1] are in place)
+    LF_HIP(c, lfk::y0_cm0(cm_side[0], cm_side[1], b->y[0], b->y[1], b->rho, kappa, d, lbs, K, b->cm0, c->cur));
+  } else {
+    if (commit_f) LF_HIP(c, hipMemcpyAsync(commit_cm, ycat, kd * 8, hipMemcpyDeviceToDevice, c->cur));
+    for (int s = 0; s < 2; s++) {
+      LF_HIP(c, hipMemcpyAsync(b->y[s] + kd, ycat + (extra + (size_t)s * (K - 1)) * kd, (size_t)(K - 1) * kd * 8,
+                               hipMemcpyDeviceToDevice, c->cur));
+      LF_HIP(c, lfk::commit_y0(cm_side[s], b->y[s], kappa, d, lbs, K, c->cur));
+    }
   }
   // f_0 = sum rho_i f_i, cm_0 = sum rho_i y_i   (folding.rs:258-268, folding/utils.rs:470-476)
   lfk::VecPtrs fx{}, yx{};
@@ -364,7 +375,7 @@ int fold_core(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lb
     PhaseTimer pt(c, LF_PHASE_FOLD);
     LF_HIP(c, lfk::fold(b->rho, fx, 2 * K, N, d, b->f0, c->cur));
   }
-  LF_HIP(c, lfk::fold(b->rho, yx, 2 * K, kappa, d, b->cm0, c->cur));
+  if (!fused) LF_HIP(c, lfk::fold(b->rho, yx, 2 * K, kappa, d, b->cm0, c->cur));
   // Witness::from_f(f_0) (arith.rs:299-313)
   PhaseTimer pt(c, LF_PHASE_FROM_F);
   LF_HIP(c, lfk::from_f(b->f0, N, d, lb, L, b->f0_coeff, b->w_ccs0, t->inv, c->cur));
