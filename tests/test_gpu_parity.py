@@ -270,6 +270,10 @@ def test_commit_then_fold_hot(ctx, d, W, kappa):
 
 @pytest.mark.parametrize("d,W,kappa", [(24, 10, 4), (1024, 2, 2)])
 def test_dev_fold_step_matches_oracle(ctx, d, W, kappa):
+    check_dev_fold_step(ctx, d, W, kappa)
+
+
+def check_dev_fold_step(ctx, d, W, kappa):
     import torch
     pr = params(d)
     K, L = pr.K, pr.L

@@ -4,7 +4,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 TAG=${1:-iter}
-timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/pytest_$TAG.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_$TAG.log
 [ $rc -eq 0 ] || exit $rc
