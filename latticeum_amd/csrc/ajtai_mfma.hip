@@ -27,11 +27,25 @@
 // one unit is one limb of 16 consecutive groups, which is what a block of the
 // fused decomposition holds at once; Lp = 1 is the natural column order. A and
 // F use the same order, so the contraction is unchanged.
+//
+// Phi_72 (d = 24, the reference ring): a slot is an Fq3 = Fq[u]/(u^3 - 2^40)
+// element, and a slot product is a product of degree-2 polynomials reduced mod
+// u^3 - 2^40. Toom-3 turns the slot's 9 component products into 5 same-position
+// products: both operands are evaluated at u in {0, 1, -1, 2, inf} when they are
+// written in fragment order (5 "virtual slots" per slot, 40 per element), the
+// contraction runs unchanged over the 40 virtual slots (each an independent GEMM
+// over Z_p), and k_phi72_interp interpolates the sums
+//   D(u) = sum_j a_j(u) b_j(u),  deg D = 4
+// back to D's coefficients d0..d4 and reduces: c = (d0 + 2^40 d3, d1 + 2^40 d4, d2)
+// (goldilocks/mod.rs:34-54 Fq3 multiplication, summed over the columns as
+// matrix.rs:168-178 does).
 #include "frag.hpp"
 #include "kernels.hpp"
 
 namespace lfk {
 
+// virtual slots per element of the contraction: d for X^d + 1, 40 for Phi_72
+int mfma_dim(int d) { return d == 24 ? 40 : d; }
 
 // ---------------------------------------------------------------- to fragment order
 FragGeom frag_geom(size_t ncols, int Lp) {
@@ -53,10 +67,12 @@ __device__ __forceinline__ size_t frag_column(int c, int t, int Lp, size_t Wp, b
 // [row][slot][column] of D8 words, rows padded to 34 words so the 16-B
 // column reads of the emit phase are aligned. Rows >= nrows are never
 // written: they only feed MFMA output columns (or rows) that are discarded.
+// PHI72: d = 24, the element's 40 virtual slots (Toom-3 evaluations) are
+// produced on the fly; dv = virtual slots per element (d, or 40 for PHI72).
 constexpr int TF_S = 16, TF_R = 8, TF_J = 34;
-template <bool VMAJOR>
-__global__ void __launch_bounds__(256) k_to_frag(VecPtrs rows, int rlo, int rhi, int d, int nch, int Lp, size_t Wp,
-                                                 uint4 *frag) {
+template <bool VMAJOR, bool PHI72>
+__global__ void __launch_bounds__(256) k_to_frag(VecPtrs rows, int rlo, int rhi, int d, int dv, int nch, int Lp,
+                                                 size_t Wp, uint4 *frag) {
   __shared__ uint64_t tile[TF_R * TF_S * TF_J];
   const int sb = blockIdx.x, c = blockIdx.y, r0 = (rlo & ~(TF_R - 1)) + blockIdx.z * TF_R, tid = threadIdx.x;
   // load: 8 rows x 32 columns x (16 slots = 128 B = 8 pieces of 16 B)
@@ -67,8 +83,16 @@ __global__ void __launch_bounds__(256) k_to_frag(VecPtrs rows, int rlo, int rhi,
     bool ok;
     const size_t col = frag_column(c, j, Lp, Wp, ok);
     ulonglong2 v = make_ulonglong2(0, 0);
-    if (r0 + r >= rlo && r0 + r < rhi && ok)
-      v = *reinterpret_cast<const ulonglong2 *>(rows.p[r0 + r] + col * d + (size_t)sb * TF_S + 2 * q);
+    if (r0 + r >= rlo && r0 + r < rhi && ok) {
+      const uint64_t *e = rows.p[r0 + r] + col * d;
+      const int vs = sb * TF_S + 2 * q;
+      if (PHI72) {
+        if (vs < dv) v.x = ring::phi72_eval(e, vs);
+        if (vs + 1 < dv) v.y = ring::phi72_eval(e, vs + 1);
+      } else {
+        v = *reinterpret_cast<const ulonglong2 *>(e + vs);
+      }
+    }
     uint64_t *t = tile + (r * TF_S + 2 * q) * TF_J + j;
     t[0] = d8(v.x);
     t[TF_J] = d8(v.y);
@@ -77,7 +101,7 @@ __global__ void __launch_bounds__(256) k_to_frag(VecPtrs rows, int rlo, int rhi,
   // emit: thread = (slot sl, half h, row r); lane (r, h) of the MFMA operand
   // holds columns 16h..16h+15 of one slot as 16 bytes per digit
   const int r = tid & 7, h = (tid >> 3) & 1, sl = tid >> 4;
-  if (r0 + r < rlo || r0 + r >= rhi) return;
+  if (r0 + r < rlo || r0 + r >= rhi || sb * TF_S + sl >= dv) return;
   const ulonglong2 *src = reinterpret_cast<const ulonglong2 *>(tile + (r * TF_S + sl) * TF_J + 16 * h);
   uint64_t x[16];
 #pragma unroll
@@ -104,7 +128,7 @@ __global__ void __launch_bounds__(256) k_to_frag(VecPtrs rows, int rlo, int rhi,
 // one wave = one slot x one column split; one wave per SIMD (15 i32 32x32
 // accumulators = 240 registers). Fragments of chunk c+1 load while chunk c's
 // 64 MFMAs run. A is row-interleaved, F vector-major (see the top of the file).
-constexpr int AJ_CPS = 320;  // chunks per split (i32 bound: < 512)
+constexpr int AJ_CPS = 320;  // most chunks per split (i32 bound: < 512)
 // The 4 waves of a block take 4 consecutive slots (same split). Both operands
 // stream into LDS with global_load_lds_dwordx4 (no staging registers):
 //  * A: each wave copies its 8 KiB (8 one-KiB tiles, lane order) per chunk;
@@ -119,14 +143,14 @@ __device__ __forceinline__ int fl_pi(int j, int i) { return i ^ (((j & 7) << 1) 
 
 __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const uint4 *Ff, int d, int nch,
                                                       int nvec, int kappa, uint64_t *partial, OutPtrs dst,
-                                                      int direct) {
+                                                      int direct, int cps) {
   __shared__ uint4 Al[2][4][8 * 64];  // 64 KiB: A copies one chunk ahead
   __shared__ uint4 Fl[3][32 * 64];    // 96 KiB: F copies two chunks ahead
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int gw = blockIdx.x * 4 + w;
   const int s = gw % d, js = gw / d;  // d % 4 == 0: one split per block, slots 4i .. 4i + 3
-  if (js >= (nch + AJ_CPS - 1) / AJ_CPS) return;  // uniform over the block
-  const int c0 = js * AJ_CPS, c1 = min(nch, c0 + AJ_CPS);
+  if (js >= (nch + cps - 1) / cps) return;  // uniform over the block
+  const int c0 = js * cps, c1 = min(nch, c0 + cps);
   v16i acc[15];
 #pragma unroll
   for (int t = 0; t < 15; t++) acc[t] = (v16i){0};
@@ -234,45 +258,108 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const ui
   }
 }
 
+// Phi_72 epilogue: virtual-slot sums [nvec][kappa][40] -> Fq3 slots [kappa][24] per vector
+__global__ void k_phi72_interp(const uint64_t *virt, int nvec, size_t kappa, OutPtrs out) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // (v, row, slot)
+  if (i >= (size_t)nvec * kappa * 8) return;
+  const int slot = (int)(i & 7);
+  const size_t vr = i >> 3, v = vr / kappa, row = vr - v * kappa;
+  const uint64_t *P = virt + vr * 40 + 5 * slot;
+  constexpr uint64_t INV2 = 0x7FFFFFFF80000001ull, INV3 = 0xAAAAAAAA00000001ull;
+  const uint64_t d0 = P[0], d4 = P[4];
+  const uint64_t d2 = gl::sub(gl::sub(gl::mul(gl::add(P[1], P[2]), INV2), d0), d4);
+  const uint64_t s1 = gl::mul(gl::sub(P[1], P[2]), INV2);  // d1 + d3
+  const uint64_t u =  // d1 + 4 d3
+      gl::mul(gl::sub(gl::sub(gl::sub(P[3], d0), gl::mul_pow2(d2, 2)), gl::mul_pow2(d4, 4)), INV2);
+  const uint64_t d3 = gl::mul(gl::sub(u, s1), INV3), d1 = gl::sub(s1, d3);
+  uint64_t *o = out.p[v] + row * 24 + 3 * slot;
+  o[0] = gl::add(d0, gl::mul_pow2(d3, 40));
+  o[1] = gl::add(d1, gl::mul_pow2(d4, 40));
+  o[2] = d2;
+}
+
 // ---------------------------------------------------------------- launchers
-size_t frag_elems(const FragGeom &g, int d) { return (size_t)d * g.nch * 8 * 64; }  // uint4 per buffer
-int mfma_nsplit(const FragGeom &g) { return (g.nch + AJ_CPS - 1) / AJ_CPS; }
+size_t frag_elems(const FragGeom &g, int d) { return (size_t)mfma_dim(d) * g.nch * 8 * 64; }  // uint4 per buffer
+// chunks per column split: AJ_CPS for wide rings; for few virtual slots (Phi_72)
+// enough splits that about 2048 waves run
+int mfma_cps(const FragGeom &g, int d) {
+  const int dv = mfma_dim(d);
+  if (dv >= 256) return AJ_CPS;
+  const int want = 2048 / dv > 1 ? 2048 / dv : 1;
+  const int cps = (g.nch + want - 1) / want;
+  return cps < 1 ? 1 : (cps > AJ_CPS ? AJ_CPS : cps);
+}
+int mfma_nsplit(const FragGeom &g, int d) {
+  const int cps = mfma_cps(g, d);
+  return (g.nch + cps - 1) / cps;
+}
+size_t mfma_scratch_elems(const FragGeom &g, int d, size_t kappa, int nvec) {
+  const size_t dv = mfma_dim(d), nsplit = mfma_nsplit(g, d);
+  return (nsplit > 1 ? nsplit : 0) * nvec * kappa * dv + (d == 24 ? (size_t)nvec * kappa * dv : 0);
+}
 
 // operand rows row0 .. row0 + nrows - 1 <- rows.p[0 .. nrows - 1]
 hipError_t to_frag(const VecPtrs &rows, int nrows, int row0, const FragGeom &g, int d, bool vmajor, uint4 *frag,
                    hipStream_t st) {
-  if (nrows < 1 || row0 < 0 || row0 + nrows > 32 || d % TF_S) return hipErrorInvalidValue;
+  const int dv = mfma_dim(d);
+  if (nrows < 1 || row0 < 0 || row0 + nrows > 32 || (d != 24 && d % TF_S)) return hipErrorInvalidValue;
   VecPtrs abs{};
   for (int i = 0; i < nrows; i++) abs.p[row0 + i] = rows.p[i];
   const int rhi = row0 + nrows, ztiles = (rhi + TF_R - 1) / TF_R - row0 / TF_R;
-  const dim3 grid(d / TF_S, g.nch, ztiles);
-  if (vmajor)
-    hipLaunchKernelGGL(k_to_frag<true>, grid, dim3(256), 0, st, abs, row0, rhi, d, g.nch, g.Lp, g.Wp, frag);
-  else
-    hipLaunchKernelGGL(k_to_frag<false>, grid, dim3(256), 0, st, abs, row0, rhi, d, g.nch, g.Lp, g.Wp, frag);
+  const dim3 grid((dv + TF_S - 1) / TF_S, g.nch, ztiles);
+#define LF_TF(VM, PH) \
+  hipLaunchKernelGGL((k_to_frag<VM, PH>), grid, dim3(256), 0, st, abs, row0, rhi, d, dv, g.nch, g.Lp, g.Wp, frag)
+  if (d == 24) {
+    if (vmajor)
+      LF_TF(true, true);
+    else
+      LF_TF(false, true);
+  } else if (vmajor) {
+    LF_TF(true, false);
+  } else {
+    LF_TF(false, false);
+  }
+#undef LF_TF
   return hipGetLastError();
 }
 
+// partial: mfma_scratch_elems() u64 (split partial sums, then Phi_72's virtual-slot results)
 hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, const VecPtrs &fv, int nvec,
                       bool f_ready, uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st, hipEvent_t ev0,
                       hipEvent_t ev1, const OutPtrs *dst) {
-  if (kappa > 32 || nvec < 1 || nvec > 32 || d % 4 || (!cm && !dst)) return hipErrorInvalidValue;
+  const int dv = mfma_dim(d);
+  if (kappa > 32 || nvec < 1 || nvec > 32 || dv % 4 || (!cm && !dst)) return hipErrorInvalidValue;
   OutPtrs out{};
   for (int v = 0; v < nvec; v++) out.p[v] = cm ? cm + (size_t)v * kappa * d : dst->p[v];
   if (!f_ready) {
     hipError_t e = to_frag(fv, nvec, 0, g, d, true, Ff, st);
     if (e != hipSuccess) return e;
   }
-  const int nsplit = mfma_nsplit(g);
+  const int nsplit = mfma_nsplit(g, d), cps = mfma_cps(g, d);
+  // the contraction's own outputs: the results (X^d + 1), or Phi_72's virtual-slot sums
+  OutPtrs kout = out;
+  uint64_t *virt = nullptr;
+  if (d == 24) {
+    virt = partial + (nsplit > 1 ? (size_t)nsplit * nvec * kappa * dv : 0);
+    for (int v = 0; v < nvec; v++) kout.p[v] = virt + (size_t)v * kappa * dv;
+  }
   if (ev0) (void)hipEventRecord(ev0, st);
-  const size_t waves = (size_t)d * nsplit;
-  hipLaunchKernelGGL(k_ajtai_mfma, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, Af, Ff, d, g.nch, nvec,
-                     (int)kappa, partial, out, nsplit == 1 ? 1 : 0);
+  const size_t waves = (size_t)dv * nsplit;
+  hipLaunchKernelGGL(k_ajtai_mfma, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, Af, Ff, dv, g.nch, nvec,
+                     (int)kappa, partial, kout, nsplit == 1 ? 1 : 0, cps);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (ev1) (void)hipEventRecord(ev1, st);
-  if (nsplit == 1) return hipSuccess;
-  return sum_planes_to(partial, nsplit, kappa * (size_t)d, nvec, out, st);
+  if (nsplit > 1) {
+    e = sum_planes_to(partial, nsplit, kappa * (size_t)dv, nvec, kout, st);
+    if (e != hipSuccess) return e;
+  }
+  if (d == 24) {
+    const size_t n = (size_t)nvec * kappa * 8;
+    hipLaunchKernelGGL(k_phi72_interp, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, virt, nvec, kappa, out);
+    e = hipGetLastError();
+  }
+  return e;
 }
 
 }  // namespace lfk

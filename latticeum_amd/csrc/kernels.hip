@@ -4,6 +4,7 @@
 // (stark-rings crt.rs:53-77), d = 4^k for the negacyclic rings), canonical
 // values. Every launcher returns hipError_t and takes the stream explicitly.
 #include "digits.hpp"
+#include "frag.hpp"
 #include "kernels.hpp"
 #include "ring.hpp"
 
@@ -230,10 +231,16 @@ __global__ void __launch_bounds__(NT<D>::T) k_from_f_nega(const uint64_t *f, siz
 // Phi_72: one thread per element, 64 groups of L elements per block; the
 // recompose across the L elements of a group goes through LDS.
 constexpr int DEC_GROUPS = 32;
+constexpr int DEC_SROW = 41;  // operand staging row (40 virtual slots + pad) of the fused d = 24 decomposition
+// With frag != nullptr, planes k >= 1 are also written as i8-MFMA operand rows
+// row0 + k - 1 (ajtai_mfma.hip, vector-major, Lp = L column order): the block's
+// 32 groups are the 16-group units (G, l), G = 2 blockIdx.x + {0, 1}, and each
+// (unit, virtual slot) piece is assembled from the plane's NTT values in LDS.
 __global__ void __launch_bounds__(256) k_decompose_phi72(const uint64_t *f_coeff, size_t N, int lb,
                                                         int L, int lbs, int K, uint64_t *f_coeff_k,
-                                                        uint64_t *f_k, uint64_t *w_ccs_k, int *err) {
-  extern __shared__ uint64_t lds[];  // [DEC_GROUPS * L][25]
+                                                        uint64_t *f_k, uint64_t *w_ccs_k, int *err,
+                                                        uint4 *frag, int nch, int row0) {
+  extern __shared__ uint64_t lds[];  // [DEC_GROUPS * L][25] (with frag: [..][DEC_SROW])
   const int t = threadIdx.x;
   const size_t W = N / L;
   const size_t j = (size_t)blockIdx.x * DEC_GROUPS * L + t;  // element index
@@ -249,8 +256,8 @@ __global__ void __launch_bounds__(256) k_decompose_phi72(const uint64_t *f_coeff
     }
   }
   for (int k = 0; k < K; k++) {
+    uint64_t c[24];
     if (act) {
-      uint64_t c[24];
 #pragma unroll
       for (int i = 0; i < 24; i++) c[i] = from_signed(bal_digit(cur[i], lbs));
       ulonglong2 *dc = reinterpret_cast<ulonglong2 *>(f_coeff_k + ((size_t)k * N + j) * 24);
@@ -272,6 +279,33 @@ __global__ void __launch_bounds__(256) k_decompose_phi72(const uint64_t *f_coeff
         uint64_t a = lds[(g * L + L - 1) * 25 + i];
         for (int l = L - 2; l >= 0; l--) a = gl::add(gl::mul_pow2(a, lb), lds[(g * L + l) * 25 + i]);
         w_ccs_k[((size_t)k * W + wj) * 24 + i] = a;
+      }
+    }
+    if (frag && k > 0) {
+      // each element's 40 virtual slots (Toom-3 evaluations, ring::phi72_eval) as
+      // D8 words into LDS rows of DEC_SROW, then one thread per (unit, virtual
+      // slot) gathers the unit's 16 columns into the 8 operand pieces
+      __syncthreads();  // the recompose reads of lds are done
+      if (act) {
+#pragma unroll
+        for (int vs = 0; vs < 40; vs++) lds[t * DEC_SROW + vs] = d8(ring::phi72_eval(c, vs));
+      }
+      __syncthreads();
+      for (int tk = t; tk < 2 * L * 40; tk += blockDim.x) {
+        const int vs = tk % 40, ul = tk / 40, gh = ul / L, l = ul - gh * L;
+        const size_t u = ((size_t)blockIdx.x * 2 + gh) * L + l;  // contraction unit
+        if (u >= 2 * (size_t)nch) continue;
+        uint64_t x[16];
+#pragma unroll
+        for (int jj = 0; jj < 16; jj++) {
+          const int g = gh * 16 + jj;
+          x[jj] = (size_t)blockIdx.x * DEC_GROUPS + g < W ? lds[(g * L + l) * DEC_SROW + vs] : 0;
+        }
+        uint4 pu[8];
+        d8_transpose16(x, pu);
+        uint4 *out = frag + fv_index(vs, nch, (int)(u >> 1), row0 + k - 1, (int)(u & 1));
+#pragma unroll
+        for (int b = 0; b < 8; b++) out[4 * b] = pu[b];
       }
     }
     __syncthreads();
@@ -804,7 +838,8 @@ hipError_t from_f(const uint64_t *f, size_t N, int d, int lb, int L, uint64_t *f
 
 hipError_t decompose_witness(const uint64_t *f_coeff, size_t N, int d, int lb, int L, int lbs, int K,
                              uint64_t *f_coeff_k, uint64_t *f_k, uint64_t *w_ccs_k,
-                             const ring::NegaTables &fwd, int *err, hipStream_t st) {
+                             const ring::NegaTables &fwd, int *err, hipStream_t st, uint4 *frag, int nch,
+                             int row0) {
   const size_t W = N / L;
   if (W == 0) return hipSuccess;
   if (d == 1024 && fwd.mid && lbs == 1 && K <= 15 && L <= 5)
@@ -812,8 +847,10 @@ hipError_t decompose_witness(const uint64_t *f_coeff, size_t N, int d, int lb, i
   if (d == 24) {
     if (DEC_GROUPS * L > 256) return hipErrorInvalidValue;
     size_t lds = (size_t)DEC_GROUPS * L * 25 * sizeof(uint64_t);
+    if (frag && (L > 5 || row0 < 0 || row0 + K - 1 > 32)) return hipErrorInvalidValue;
+    if (frag) lds = (size_t)DEC_GROUPS * L * DEC_SROW * sizeof(uint64_t);
     hipLaunchKernelGGL(k_decompose_phi72, dim3(blocks(W, DEC_GROUPS)), dim3(256), lds, st, f_coeff, N,
-                       lb, L, lbs, K, f_coeff_k, f_k, w_ccs_k, err);
+                       lb, L, lbs, K, f_coeff_k, f_k, w_ccs_k, err, frag, nch, row0);
     return hipGetLastError();
   }
   if (L > 8) return hipErrorInvalidValue;

@@ -29,9 +29,11 @@ hipError_t from_w_ccs(const uint64_t *w_ccs, size_t W, int d, int lb, int L, uin
                       hipStream_t st);
 hipError_t from_f(const uint64_t *f, size_t N, int d, int lb, int L, uint64_t *f_coeff,
                   uint64_t *w_ccs, const ring::NegaTables &inv, hipStream_t st);
+// d = 24 with frag: planes 1..K-1 also written as i8-MFMA operand rows row0.. (Lp = L order, nch chunks)
 hipError_t decompose_witness(const uint64_t *f_coeff, size_t N, int d, int lb, int L, int lbs, int K,
                              uint64_t *f_coeff_k, uint64_t *f_k, uint64_t *w_ccs_k,
-                             const ring::NegaTables &fwd, int *err, hipStream_t st);
+                             const ring::NegaTables &fwd, int *err, hipStream_t st, uint4 *frag = nullptr,
+                             int nch = 0, int row0 = 0);
 int ajtai_nsplit(size_t ncols, int d, int nvec);
 size_t ajtai_partial_elems(size_t kappa, size_t ncols, int d, int nvec);
 hipError_t ajtai_commit(const uint64_t *A, size_t kappa, size_t ncols, int d, const VecPtrs &fv,
@@ -67,8 +69,12 @@ struct FragGeom {
   int nch;
 };
 FragGeom frag_geom(size_t ncols, int Lp);
+// d = 24 (Phi_72) contracts 40 virtual slots per element (Toom-3, ajtai_mfma.hip)
+int mfma_dim(int d);
 size_t frag_elems(const FragGeom &g, int d);  // uint4 per fragment buffer
-int mfma_nsplit(const FragGeom &g);
+int mfma_nsplit(const FragGeom &g, int d);
+// u64 of scratch ajtai_mfma needs (split partial sums, Phi_72 virtual-slot results)
+size_t mfma_scratch_elems(const FragGeom &g, int d, size_t kappa, int nvec);
 hipError_t to_frag(const VecPtrs &rows, int nrows, int row0, const FragGeom &g, int d, bool vmajor, uint4 *frag,
                    hipStream_t st);
 // cm: contiguous [nvec][kappa d] results, or (cm == nullptr) per-vector destinations dst

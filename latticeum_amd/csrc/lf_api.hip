@@ -168,7 +168,7 @@ int reserve(lf_ctx *c, size_t elems) { return grow(c, c->scratch, c->scratch_ele
 
 bool use_mfma(int d, size_t kappa) {
   const char *sel = getenv("LATTICEUM_AMD_AJTAI");
-  return d != 24 && d % 16 == 0 && kappa <= 32 && !(sel && strcmp(sel, "valu") == 0);
+  return (d == 24 || d % 16 == 0) && kappa <= 32 && !(sel && strcmp(sel, "valu") == 0);
 }
 
 // RAII device buffer for the synchronous host API
@@ -207,7 +207,7 @@ int check_repr(lf_ctx *c, int repr) {
 lfk::FragGeom ajtai_geom(size_t ncols) { return lfk::frag_geom(ncols, ncols % 5 == 0 ? 5 : 1); }
 
 size_t partial_elems(const lf_ajtai *aj, int nvec) {
-  if (aj->Af) return (size_t)lfk::mfma_nsplit(aj->geom) * nvec * aj->kappa * aj->d;
+  if (aj->Af) return lfk::mfma_scratch_elems(aj->geom, aj->d, aj->kappa, nvec);
   return lfk::ajtai_partial_elems(aj->kappa, aj->ncols, aj->d, nvec);
 }
 
@@ -302,7 +302,35 @@ int fold_core(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lb
   // fused path (d = 1024, b_small = 2, fragment order grouped by this L): the
   // decomposition writes its digit planes straight into the MFMA operand buffer
   const bool fused = aj->Af && aj->geom.Lp == L && d == 1024 && lbs == 1 && K <= 15 && t->fwd.mid;
-  if (fused) {
+  // Phi_72 (d = 24): each side's decomposition writes its planes as operand rows (kernels.hip)
+  const bool fused24 = aj->Af && aj->geom.Lp == L && d == 24 && L <= 5;
+  if (fused24) {
+    LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->geom, d)));
+    for (int s = 0; s < 2; s++) {
+      PhaseTimer pt(c, LF_PHASE_DECOMPOSE);
+      LF_HIP(c, lfk::decompose_witness(fc_side[s], N, d, lb, L, lbs, K, b->fk_coeff[s], b->fk[s], b->wk[s], t->fwd,
+                                       c->d_err, c->cur, c->frag, aj->geom.nch, extra + s * (K - 1)));
+    }
+    lfk::VecPtrs vp{};
+    if (commit_f) {
+      PhaseTimer pt(c, LF_PHASE_TO_FRAG);
+      vp.p[0] = commit_f;
+      LF_HIP(c, lfk::to_frag(vp, 1, 0, aj->geom, d, true, c->frag, c->cur));
+    }
+    LF_TRY(reserve(c, partial_elems(aj, nvec)));
+    hipEvent_t ea = nullptr, eb = nullptr;
+    if (c->timing) {
+      LF_HIP(c, hipEventCreate(&ea));
+      LF_HIP(c, hipEventCreate(&eb));
+    }
+    lfk::OutPtrs dst{};
+    if (commit_f) dst.p[0] = commit_cm;
+    for (int s = 0; s < 2; s++)
+      for (int k = 1; k < K; k++) dst.p[extra + s * (K - 1) + k - 1] = b->y[s] + (size_t)k * kd;
+    LF_HIP(c, lfk::ajtai_mfma(aj->Af, kappa, aj->geom, d, vp, nvec, true, c->frag, c->scratch, nullptr, c->cur, ea,
+                              eb, &dst));
+    if (c->timing) c->pending.push_back({ea, eb, nvec});
+  } else if (fused) {
     LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->geom, d)));
     LF_TRY(grow(c, c->smg, c->smg_elems, 2 * N * 512));
     lfk::FusedSides sd{};
@@ -356,6 +384,8 @@ int fold_core(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lb
   if (fused) {
     // y_0 of both sides and cm_0 = sum rho_i y_i in one pass (the y_s[k >= 1] are in place)
     LF_HIP(c, lfk::y0_cm0(cm_side[0], cm_side[1], b->y[0], b->y[1], b->rho, kappa, d, lbs, K, b->cm0, c->cur));
+  } else if (fused24) {
+    for (int s = 0; s < 2; s++) LF_HIP(c, lfk::commit_y0(cm_side[s], b->y[s], kappa, d, lbs, K, c->cur));
   } else {
     if (commit_f) LF_HIP(c, hipMemcpyAsync(commit_cm, ycat, kd * 8, hipMemcpyDeviceToDevice, c->cur));
     for (int s = 0; s < 2; s++) {

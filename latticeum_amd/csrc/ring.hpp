@@ -125,6 +125,21 @@ __device__ __forceinline__ void phi72_icrt(uint64_t *c) {
   }
 }
 
+// Toom-3 evaluation for the i8-MFMA Ajtai (ajtai_mfma.hip): virtual slot
+// vs = 5 slot + t of a Phi_72 NTT element e (24 canonical u64, [s.c0, s.c1, s.c2]
+// per slot) is the slot's polynomial c0 + c1 u + c2 u^2 at u = 0, 1, -1, 2, inf
+__device__ __forceinline__ uint64_t phi72_eval(const uint64_t *e, int vs) {
+  const int slot = vs / 5, t = vs - 5 * slot;
+  const uint64_t a0 = e[3 * slot], a1 = e[3 * slot + 1], a2 = e[3 * slot + 2];
+  switch (t) {
+    case 0: return a0;
+    case 1: return gl::add(gl::add(a0, a1), a2);
+    case 2: return gl::add(gl::sub(a0, a1), a2);
+    case 3: return gl::add(gl::add(a0, gl::add(a1, a1)), gl::mul_pow2(a2, 2));
+    default: return a2;
+  }
+}
+
 // Fq3 slot multiply-accumulate into lazy accumulators:
 //   c0 = sum a0b0 + 2^40 * sum(a1b2 + a2b1)
 //   c1 = sum(a0b1 + a1b0) + 2^40 * sum a2b2

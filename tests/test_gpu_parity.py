@@ -268,7 +268,7 @@ def test_commit_then_fold_hot(ctx, d, W, kappa):
         assert [int(v) for v in acc] == [int(v) for v in c]
 
 
-@pytest.mark.parametrize("d,W,kappa", [(24, 10, 4), (1024, 2, 2)])
+@pytest.mark.parametrize("d,W,kappa", [(24, 10, 4), (24, 70, 3), (1024, 2, 2), (1024, 37, 2)])
 def test_dev_fold_step_matches_oracle(ctx, d, W, kappa):
     check_dev_fold_step(ctx, d, W, kappa)
 
@@ -370,7 +370,8 @@ def test_limb_transport_roundtrip(ctx):
 
 @pytest.mark.parametrize("layout", ["mfma", "valu"])
 @pytest.mark.parametrize("d,kappa,ncols,nvec", [(16, 3, 40, 5), (64, 32, 70, 29), (1024, 7, 33, 1),
-                                                (1024, 32, 96, 29), (256, 17, 64, 32)])
+                                                (1024, 32, 96, 29), (256, 17, 64, 32), (24, 3, 40, 5),
+                                                (24, 32, 700, 29), (24, 9, 33, 1)])
 def test_ajtai_layouts(ctx, monkeypatch, layout, d, kappa, ncols, nvec):
     # the i8-MFMA contraction (signed base-256 limbs) and the VALU path agree with the oracle
     import torch
@@ -405,3 +406,19 @@ def test_ajtai_mfma_extreme_digits(ctx):
     ctx.sync()
     # (p-1)^2 = 1 per column, so every entry is ncols mod p
     assert set(cm.cpu().numpy().view(np.uint64).tolist()) == {ncols}
+
+
+def test_ajtai_mfma_phi72_extreme_digits(ctx):
+    # Phi_72 through the Toom-3 virtual slots: all-(p-1) operands (every D8 digit
+    # -1, every evaluation at its largest) over many column splits, against the oracle
+    import torch
+    d, kappa, ncols, nvec = 24, 32, 2000, 8
+    A = np.full(kappa * ncols * d, P - 1, np.uint64).reshape(kappa, ncols, d)
+    F = np.full(nvec * ncols * d, P - 1, np.uint64)
+    sch = LA.AjtaiCommitmentScheme(ctx, A)
+    assert sch.layout == 1
+    Ft = torch.from_numpy(F.view(np.int64)).cuda()
+    cm = torch.zeros(nvec * kappa * d, dtype=torch.int64, device="cuda")
+    ctx.dev_ajtai_commit(sch, [Ft[v * ncols * d:(v + 1) * ncols * d] for v in range(nvec)], cm)
+    ctx.sync()
+    assert np.array_equal(cm.cpu().numpy().view(np.uint64), O.ajtai_commit(A, kappa, ncols, d, F, nvec))
