@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--kappa", type=int, default=32)
     ap.add_argument("--streams", type=int, default=1, help="concurrent step streams per GPU")
     ap.add_argument("--no-small-shape", dest="small", action="store_false", default=True,
-                    help="skip the W=464 multi-stream measurement reported beside the default workload")
+                    help="skip the W=464 / d=24 multi-stream measurements and the NTT / Poseidon2 timings "
+                         "reported beside the default workload")
     ap.add_argument("--cpu-baseline", dest="cpu", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu", action="store_false")
     ap.add_argument("--cpu-w", type=int, default=0, help="W of the CPU baseline sample (0 = auto)")
@@ -210,11 +211,12 @@ class Workload:
         self.ctxs = []
 
 
-def small_shape(LA, torch, LD, pg, local, rank, world, d, kappa):
-    """SURVEY.md §8d's byte-equivalent real-zkvm shape (W = 464) with concurrent
-    step streams: the per-GPU rate the north-star target (1e4 steps/s on 8 GPUs)
-    is about. Reported beside the default workload, not as `value`."""
-    W, S, steps, warmup = 464, 4, 256, 16
+def extra_shape(LA, torch, LD, pg, local, rank, world, d, W, kappa, S, steps, warmup, what):
+    """Another commit+fold workload with S concurrent step streams per GPU,
+    reported beside the default one (not as `value`): SURVEY.md §8d's
+    byte-equivalent shape (d = 1024, W = 464), whose per-GPU rate the north-star
+    target (1e4 steps/s on 8 GPUs) is about, and the reference's own ring at the
+    real zkvm shape (d = 24, W = 19 763; the bit-exact-vs-reference path)."""
     wl = Workload(LA, torch, local, rank, d, W, kappa, S)
     wl.run(warmup)
     torch.cuda.synchronize()
@@ -226,12 +228,51 @@ def small_shape(LA, torch, LD, pg, local, rank, world, d, kappa):
     LD.barrier(pg)
     dt = LD.max_over_ranks(pg, time.perf_counter() - t0)
     wl.close()
+    torch.cuda.empty_cache()
     value = world * steps / dt
     step_bytes, _ = algorithmic_bytes(d, W, kappa)
-    return {"workload": f"commit+fold step, X^{d}+1 ring, w_ccs W={W} (byte-equivalent to the real zkvm step), "
-                        f"kappa={kappa}, {S} concurrent step streams per GPU",
-            "W": W, "streams": S, "value": value, "unit": "fold-steps/s", "n_gpus": world, "steps": steps,
+    return {"workload": f"commit+fold step, {what}, w_ccs W={W}, kappa={kappa}, {S} concurrent step streams per GPU",
+            "d": d, "W": W, "streams": S, "value": value, "unit": "fold-steps/s", "n_gpus": world, "steps": steps,
             "ms_per_step_per_gpu": dt / steps * 1e3, "hbm_gbs_step_algorithmic": step_bytes * value / world / 1e9}
+
+
+def side_ops(LA, torch, local):
+    """BASELINE.json configs[1] (batched d = 1024 NTT/INTT of 2^16 polynomials)
+    and the Poseidon2 batch of configs[4] (2^20 states), device time per launch."""
+    ctx = LA.Context(local)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+
+    def ev_ms(fn, reps=10):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    out = {}
+    d, n = 1024, 1 << 16
+    x = torch.empty(n * d, dtype=torch.int64, device=f"cuda:{local}")
+    ctx.dev_fill_uniform(x, SEED_W - 2)
+    by = 2 * n * d * 8
+    for name, fn in (("fwd", lambda: ctx.dev_crt(x, d)), ("inv", lambda: ctx.dev_icrt(x, d))):
+        ms = ev_ms(fn)
+        out[f"ntt_{name}"] = {"npoly": n, "d": d, "ms": ms, "polys_per_s": n / ms * 1e3,
+                              "achieved_gbs": by / ms / 1e6, "frac_hbm": by / ms / 1e6 / HBM_PEAK_GBS}
+    del x
+    m = 1 << 20
+    st = torch.empty(16 * m, dtype=torch.int64, device=f"cuda:{local}")
+    ctx.dev_fill_uniform(st, 0x4C460007)
+    ms = ev_ms(lambda: ctx.dev_poseidon2_permute(st))
+    out["poseidon2_w16"] = {"states": m, "ms": ms, "perms_per_s": m / ms * 1e3}
+    del st
+    ctx.sync()
+    ctx.close()
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -326,9 +367,15 @@ def main():
     del wl
     torch.cuda.empty_cache()
     if args.small and args.d == 1024:
-        small = small_shape(LA, torch, LD, pg, local, rank, world, args.d, args.kappa)
+        small = extra_shape(LA, torch, LD, pg, local, rank, world, 1024, 464, args.kappa, 4, 256, 16,
+                            "X^1024+1 ring (byte-equivalent to the real zkvm step)")
+        ref = extra_shape(LA, torch, LD, pg, local, rank, world, 24, 19763, 32, 4, 128, 8,
+                          "the reference ring Phi_72 = X^24 - X^12 + 1 at the real zkvm shape")
+        ops = side_ops(LA, torch, local)
         if out is not None:
             out["small_shape"] = small
+            out["reference_ring"] = ref
+            out["side_ops"] = ops
     if out is not None:
         print(json.dumps(out), flush=True)
     LD.finalize(pg)
