@@ -601,8 +601,22 @@ __global__ void __launch_bounds__(256) k_fold_nega(const uint64_t *rho, VecPtrs 
   gl::CAcc a0, a1;
   gl::cacc_zero(a0);
   gl::cacc_zero(a1);
-  for (int i = 0; i < nwit; i++) {
-    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+  // witnesses in batches of FB: the batch's loads are all in flight before its MACs
+  constexpr int FB = 6;
+  int i = 0;
+  for (; i + FB <= nwit; i += FB) {
+    u64x2 v[FB];
+#pragma unroll
+    for (int q = 0; q < FB; q++) v[q] = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(x.p[i + q] + c));
+#pragma unroll
+    for (int q = 0; q < FB; q++) {
+      const ulonglong2 r = *reinterpret_cast<const ulonglong2 *>(rho + (i + q) * d + s);
+      gl::cacc_mad(a0, r.x, v[q].x);
+      gl::cacc_mad(a1, r.y, v[q].y);
+    }
+  }
+  for (; i < nwit; i++) {
     const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(x.p[i] + c));
     const ulonglong2 r = *reinterpret_cast<const ulonglong2 *>(rho + i * d + s);
     gl::cacc_mad(a0, r.x, v.x);
