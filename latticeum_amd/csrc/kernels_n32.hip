@@ -536,7 +536,10 @@ hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K,
       ncu = 256;
   }
   const size_t ntask = (N / L + 15) / 16 * (size_t)K * sd.nside;
-  const unsigned grid = (unsigned)(ntask < (size_t)ncu ? ntask : (size_t)ncu);
+  // every block takes the same number of tasks (no tail round on part of the
+  // chip); the CUs left over run other streams' kernels
+  const size_t per = (ntask + ncu - 1) / ncu;
+  const unsigned grid = (unsigned)((ntask + per - 1) / per);
   hipLaunchKernelGGL(k_decompose_fused, dim3(grid), dim3(512), 0, st, smg, N, L, lb, K, sd, fwd.mid, frag, nch);
   return hipGetLastError();
 }
