@@ -62,15 +62,19 @@ def algorithmic_bytes(d, W, kappa, L=5, K=15):
             + E * (kappa * N + 2 * (K - 1) * N + 2 * (K - 1) * kappa) + E * (2 * K * N + N)
             + E * (2 * N + W))
     nvec = 2 * (K - 1) + 1  # commit(z)'s A.f rides in the decomposition-commitment pass
+    # i8-MFMA operand bytes per element: 8 signed bytes per slot; d = 24 (Phi_72)
+    # contracts 40 virtual slots (Toom-3 evaluations of its 8 Fq3 slots)
+    F = 8 * (40 if d == 24 else d)
+    sides = 1 if d == 24 else 2  # the d = 1024 decomposition runs both sides in one launch
     phases = {
         # f_coeff in; f_k_coeff, f_k (K N each), w_ccs_k (K W), K-1 planes as i8-MFMA operand rows out
-        "decompose": 2 * E * (N + 2 * K * N + K * W + (K - 1) * N),  # both sides in one launch
-        # A and the 29 vectors, both as 8 signed bytes per element, and the 29 kappa-element results
-        "ajtai": E * (kappa * N + nvec * N + nvec * kappa),
+        "decompose": sides * (E * (N + 2 * K * N + K * W) + F * (K - 1) * N),
+        # A and the 29 vectors in operand form, and the 29 kappa-element results
+        "ajtai": F * (kappa * N + nvec * N) + E * nvec * kappa,
         "fold": E * (2 * K * N + N),
         "from_w_ccs": E * (W + 2 * N),
         "from_f": E * (2 * N + W),
-        "to_frag": E * 2 * N,
+        "to_frag": E * N + F * N,
     }
     return step, phases
 
@@ -317,9 +321,16 @@ def main():
     ctx.kernel_timing(False)
 
     step_bytes, ph_bytes = algorithmic_bytes(d, W, kappa, L, K)
-    kernel_of = {"decompose": "k_decompose_fused", "ajtai": "k_ajtai_mfma" if sch.layout == 1 else "k_ajtai_nega",
-                 "fold": "k_fold_nega", "from_w_ccs": "k_from_w_ccs_n32", "from_f": "k_from_f_n32",
-                 "to_frag": "k_to_frag<true>"}
+    if d == 24:
+        kernel_of = {"decompose": "k_decompose_phi72", "ajtai": "k_ajtai_mfma" if sch.layout == 1 else "k_ajtai_phi72",
+                     "fold": "k_fold_phi72", "from_w_ccs": "k_from_w_ccs_phi72", "from_f": "k_from_f_phi72",
+                     "to_frag": "k_to_frag<true, true>"}
+    else:
+        small = W < 4096  # kernels_n32.hip SPLIT_W: one half-wave per (element, limb)
+        kernel_of = {"decompose": "k_decompose_fused",
+                     "ajtai": "k_ajtai_mfma" if sch.layout == 1 else "k_ajtai_nega", "fold": "k_fold_nega",
+                     "from_w_ccs": "k_from_w_ccs_split" if small else "k_from_w_ccs_n32",
+                     "from_f": "k_from_f_split" if small else "k_from_f_n32", "to_frag": "k_to_frag<true, false>"}
     traffic = load_traffic(d, W, kappa)
     phases = {}
     for ph, (ms, cnt) in timed.items():
