@@ -419,7 +419,7 @@ __global__ void k_pack_sm(FusedSides sd, size_t N, int K, uint32_t *smg, int *er
 
 __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_all, size_t N, int L, int lb,
                                                            int K, FusedSides sd, const uint64_t *mid_fg,
-                                                           uint4 *frag, int nch) {
+                                                           uint4 *frag, int nch, uint64_t *sink) {
   __shared__ uint64_t lds_all[FD_LDS_U64];
   __shared__ uint64_t mid_f[n32::MID_U64];
   n32::stage_mid(mid_f, mid_fg);
@@ -446,6 +446,14 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_
     uint32_t wn[16];  // next limb's packed words
 #pragma unroll
     for (int q = 0; q < 16; q++) wn[q] = smg[((gg * L + L - 1) * 16 + q) * 32 + r];
+    // consume the first limb's words here, so that at the limb loop's head the
+    // only outstanding loads are the prefetch issued before the previous limb's
+    // 64-80 stores (the compiler then needs no vmcnt wait there, instead of
+    // draining every store of the previous limb)
+#pragma unroll
+    for (int q = 0; q < 16; q += 8)
+      asm volatile("" : "+v"(wn[q]), "+v"(wn[q + 1]), "+v"(wn[q + 2]), "+v"(wn[q + 3]), "+v"(wn[q + 4]),
+                   "+v"(wn[q + 5]), "+v"(wn[q + 6]), "+v"(wn[q + 7]));
     {
       uint64_t acc[32];
 #pragma unroll
@@ -467,16 +475,16 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_
 #pragma unroll
           for (int q = 0; q < 16; q++) wn[q] = smg[((gg * L + ln) * 16 + q) * 32 + r];
         }
-        if (ok) {
-          uint64_t *oc = f_coeff_k + e * D + r;
+        {  // groups past W store into `sink` (no branch around the stores: see above)
+          uint64_t *oc = (ok ? f_coeff_k + e * D : sink) + r;
 #pragma unroll
           for (int k = 0; k < 32; k++) oc[32 * k] = from_signed(dg[k]);
         }
         uint64_t v[32];
         n32::neg_ct32_digits(dg, v);
         n32::forward<false>(v, mid_f, T, r);
-        if (ok) {
-          uint64_t *of = f_k + e * D + r;
+        {
+          uint64_t *of = (ok ? f_k + e * D : sink) + r;
 #pragma unroll
           for (int i = 0; i < 32; i++) of[32 * n32::brv5(i)] = v[i];
         }
@@ -525,6 +533,9 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_
 // ---------------------------------------------------------------- launchers
 hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K, uint32_t *smg,
                            const ring::NegaTables &fwd, uint4 *frag, int nch, int *err, hipStream_t st) {
+  // 8 KiB target for the row stores of groups past W (one half-wave's 1024 u64)
+  static uint64_t *sink = nullptr;
+  if (!sink && hipMalloc(&sink, D * sizeof(uint64_t)) != hipSuccess) return hipErrorOutOfMemory;
   if (K > 15 || !fwd.mid || sd.nside < 1 || sd.nside > 2) return hipErrorInvalidValue;
   const size_t words = sd.nside * N * 512;
   hipLaunchKernelGGL(k_pack_sm, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st, sd, N, K, smg, err);
@@ -540,7 +551,8 @@ hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K,
   // chip); the CUs left over run other streams' kernels
   const size_t per = (ntask + ncu - 1) / ncu;
   const unsigned grid = (unsigned)((ntask + per - 1) / per);
-  hipLaunchKernelGGL(k_decompose_fused, dim3(grid), dim3(512), 0, st, smg, N, L, lb, K, sd, fwd.mid, frag, nch);
+  hipLaunchKernelGGL(k_decompose_fused, dim3(grid), dim3(512), 0, st, smg, N, L, lb, K, sd, fwd.mid, frag, nch,
+                     sink);
   return hipGetLastError();
 }
 static unsigned half_blocks(size_t units, unsigned cap) {
