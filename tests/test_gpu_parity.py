@@ -273,7 +273,13 @@ def test_dev_fold_step_matches_oracle(ctx, d, W, kappa):
     check_dev_fold_step(ctx, d, W, kappa)
 
 
-def check_dev_fold_step(ctx, d, W, kappa):
+def test_dev_fold_step_repeated_in_place(ctx):
+    # consecutive steps reuse every buffer (as bench.py and the proving loop do):
+    # the fused fold must see each step's own f_k rows, never the previous step's
+    check_dev_fold_step(ctx, 1024, 37, 2, steps=3)
+
+
+def check_dev_fold_step(ctx, d, W, kappa, steps=1):
     import torch
     pr = params(d)
     K, L = pr.K, pr.L
@@ -305,9 +311,18 @@ def check_dev_fold_step(ctx, d, W, kappa):
                 getattr(b, k)[s] = v[s].data_ptr()
         else:
             setattr(b, k, v.data_ptr())
-    ctx.dev_fold_step(sch, pr, W, b)
-    ctx.sync()
     h = lambda t: t.cpu().numpy().view(np.uint64)
+    for step in range(steps):
+        if step:
+            w_ccs = rand(W * d, 2000 + step)
+            keep["w_ccs"].copy_(dev(w_ccs))
+        ctx.dev_fold_step(sch, pr, W, b)
+        ctx.sync()
+        check_fold_outputs(h, keep, A, kappa, d, pr, W, w_ccs, acc_cm, acc_fc, rho)
+
+
+def check_fold_outputs(h, keep, A, kappa, d, pr, W, w_ccs, acc_cm, acc_fc, rho):
+    L, N = pr.L, W * pr.L
     ofc, of = O.witness_from_w_ccs(w_ccs, d, pr.B, L)
     ocm = O.ajtai_commit(A, kappa, N, d, of)
     assert np.array_equal(h(keep["f"]), of) and np.array_equal(h(keep["cm"]), ocm)
