@@ -230,11 +230,11 @@ __global__ void __launch_bounds__(NT<D>::T) k_from_f_nega(const uint64_t *f, siz
 // f_k = CRT(f_coeff_k), w_ccs_k = recompose(f_k, B, L).
 // Phi_72: one thread per element, 64 groups of L elements per block; the
 // recompose across the L elements of a group goes through LDS.
-constexpr int DEC_GROUPS = 32;
+constexpr int DEC_GROUPS = 48;  // 3 units of 16 groups: 240 of the 256 threads own an element
 constexpr int DEC_SROW = 41;  // operand staging row (40 virtual slots + pad) of the fused d = 24 decomposition
 // With frag != nullptr, planes k >= 1 are also written as i8-MFMA operand rows
 // row0 + k - 1 (ajtai_mfma.hip, vector-major, Lp = L column order): the block's
-// 32 groups are the 16-group units (G, l), G = 2 blockIdx.x + {0, 1}, and each
+// 48 groups are the 16-group units (G, l), G = 3 blockIdx.x + {0, 1, 2}, and each
 // (unit, virtual slot) piece is assembled from the plane's NTT values in LDS.
 __global__ void __launch_bounds__(256) k_decompose_phi72(const uint64_t *f_coeff, size_t N, int lb,
                                                         int L, int lbs, int K, uint64_t *f_coeff_k,
@@ -291,9 +291,9 @@ __global__ void __launch_bounds__(256) k_decompose_phi72(const uint64_t *f_coeff
         for (int vs = 0; vs < 40; vs++) lds[t * DEC_SROW + vs] = d8(ring::phi72_eval(c, vs));
       }
       __syncthreads();
-      for (int tk = t; tk < 2 * L * 40; tk += blockDim.x) {
+      for (int tk = t; tk < DEC_GROUPS / 16 * L * 40; tk += blockDim.x) {
         const int vs = tk % 40, ul = tk / 40, gh = ul / L, l = ul - gh * L;
-        const size_t u = ((size_t)blockIdx.x * 2 + gh) * L + l;  // contraction unit
+        const size_t u = ((size_t)blockIdx.x * (DEC_GROUPS / 16) + gh) * L + l;  // contraction unit
         if (u >= 2 * (size_t)nch) continue;
         uint64_t x[16];
 #pragma unroll
