@@ -39,9 +39,18 @@ LF_HD uint64_t add(uint64_t a, uint64_t b) {  // canonical in -> canonical out
 }
 
 LF_HD uint64_t sub(uint64_t a, uint64_t b) {  // canonical in -> canonical out
+#if defined(__HIP_DEVICE_COMPILE__)
+  // on a 32-bit borrow chain, so the borrow out is the chain's own (no compare)
+  unsigned int b1, b2;
+  const uint32_t dl = __builtin_subc((uint32_t)a, (uint32_t)b, 0u, &b1);
+  const uint32_t dh = __builtin_subc((uint32_t)(a >> 32), (uint32_t)(b >> 32), b1, &b2);
+  const uint64_t d = ((uint64_t)dh << 32) | dl;
+  return b2 ? d - EPS : d;
+#else
   uint64_t d;
   const bool br = subb64(a, b, d);
   return br ? d - EPS : d;  // borrow: d wrapped by +2^64 == +EPS, remove it
+#endif
 }
 
 LF_HD uint64_t neg(uint64_t a) { return a ? P - a : 0; }
@@ -107,7 +116,18 @@ LF_HD uint64_t shl96(uint64_t x, int s) {
   uint64_t r;
   bool br;
   if (s == 0) return x;  // x is canonical (a twiddle of 2^0 or 2^96 costs only the add/sub swap)
-  if (s < 32) return mul_pow2(x, s);  // (lo, hi < 2^32) fold: already short
+  if (s < 32) {
+    // x 2^s = lo + 2^64 hi == lo + hi EPS with hi < 2^s, and lo + hi EPS < 2p.
+    // t = lo + EPS (hi + 1) = (lo + hi EPS) + 2^64 - p: with a carry out, t mod
+    // 2^64 is the reduced value; without one, lo + hi EPS = t - EPS < p.
+    const uint64_t lo = x << s;
+    const uint64_t nq = (x >> (64 - s)) * EPS + EPS;  // one v_mad_u64_u32
+    unsigned int c1, c2;
+    const uint32_t tl = __builtin_addc((uint32_t)lo, (uint32_t)nq, 0u, &c1);
+    const uint32_t th = __builtin_addc((uint32_t)(lo >> 32), (uint32_t)(nq >> 32), c1, &c2);
+    const uint64_t t = ((uint64_t)th << 32) | tl;
+    return c2 ? t : t + P;  // t + P == t - EPS mod 2^64
+  }
   if (s < 64) {
     // y = x 2^(s-32); x 2^s = y 2^32 == (y0 + y1) 2^32 - (y1 + y2)
     const int u = s - 32;
@@ -122,20 +142,42 @@ LF_HD uint64_t shl96(uint64_t x, int s) {
     r = ((uint64_t)rh << 32) | rl;
     br = b2;
   } else {
-    // y = x 2^(s-64); x 2^s = y (2^32 - 1) == (y0 - y2) 2^32 - (y0 + y1)
-    const int u = s - 64;
-    const uint32_t y0 = u ? x0 << u : x0, y1 = u ? (uint32_t)(x >> (32 - u)) : x1, y2 = u ? x1 >> (32 - u) : 0;
-    // a borrow b of y0 - y2 is -2^64 == -(2^32 - 1): L = y0 + y1 + b (2^32 - 1) = lh 2^32 + ll
-    unsigned int b, c1, c2, b1, b2;
-    const uint32_t dl = __builtin_subc(y0, y2, 0u, &b);
-    const uint32_t s1 = __builtin_addc(y0, y1, 0u, &c1);
-    const uint32_t ll = __builtin_addc(s1, b ? 0xFFFFFFFFu : 0u, 0u, &c2);
-    const uint32_t rl = __builtin_subc(0u, ll, 0u, &b1);
-    const uint32_t rh = __builtin_subc(dl, c1 + c2, b1, &b2);
+    // a division: 2^s = 2^96 2^-k == -2^-k with k = 96 - s in (0, 32]. Splitting
+    // x = (x >> k) 2^k + xl, and 2^-k == -2^(96-k) == 2^(32-k) - 2^(64-k):
+    //   x 2^-k == (x >> k) + xl 2^(32-k) - xl 2^(64-k) = D - B,
+    // D = (x >> k) + C, C = xl 2^(32-k) = (u32)x << (32-k) < 2^32, B = C 2^32.
+    // So x 2^s == B - D = C (2^32 - 1) - (x >> k): one 32 x 32 multiply and a
+    // 64-bit subtraction. Without a borrow the result is <= C (2^32 - 1) < p;
+    // with one, x >> k < 2^63 < p and adding p lands in (0, p). Canonical for
+    // any u64 x.
+    const int k = 96 - s;
+    const uint32_t C = x0 << (32 - k);
+    const uint64_t m = (uint64_t)C * EPS, a = x >> k;
+    unsigned int b1, b2;
+    const uint32_t rl = __builtin_subc((uint32_t)m, (uint32_t)a, 0u, &b1);
+    const uint32_t rh = __builtin_subc((uint32_t)(m >> 32), (uint32_t)(a >> 32), b1, &b2);
     r = ((uint64_t)rh << 32) | rl;
     br = b2;
   }
   return br ? r + P : r;
+}
+
+// Weakly reduced Horner pieces: any u64 in, a u64 congruent mod p out (the
+// caller canonicalises once at the end).
+// x 2^s for 0 < s < 32: x 2^s = lo + 2^64 hi, hi < 2^s, and 2^64 == EPS. A
+// carry out of lo + hi EPS leaves t < hi EPS < 2^63, so t + EPS cannot wrap.
+LF_HD uint64_t shl_small_weak(uint64_t x, int s) {
+  const uint64_t lo = x << s;
+  const uint64_t hi = x >> (64 - s);
+  uint64_t t;
+  const bool c = addc64(lo, hi * EPS, t);
+  return c ? t + EPS : t;
+}
+// a (any u64) + b (canonical): after a carry t = a + b - 2^64 < b < p, so t + EPS cannot wrap
+LF_HD uint64_t add_weak(uint64_t a, uint64_t b) {
+  uint64_t t;
+  const bool c = addc64(a, b, t);
+  return c ? t + EPS : t;
 }
 
 LF_HD uint64_t pow(uint64_t a, uint64_t e) {

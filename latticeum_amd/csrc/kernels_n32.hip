@@ -366,7 +366,7 @@ __global__ void __launch_bounds__(256, 1) k_decompose_n32(const uint64_t *f_coef
         }
         if (lb == 15) {  // GoldiLocksDP B = 2^15: a shift instead of a product
 #pragma unroll
-          for (int i = 0; i < 32; i++) acc[i] = gl::add(gl::shl96(acc[i], 15), v[i]);
+          for (int i = 0; i < 32; i++) acc[i] = gl::add_weak(gl::shl_small_weak(acc[i], 15), v[i]);
         } else {
 #pragma unroll
           for (int i = 0; i < 32; i++) acc[i] = gl::add(gl::mul(acc[i], b_pow), v[i]);
@@ -375,7 +375,7 @@ __global__ void __launch_bounds__(256, 1) k_decompose_n32(const uint64_t *f_coef
       if (ok) {
         uint64_t *ow = w_ccs_k + ((size_t)kb * W + g) * D + x.r;
 #pragma unroll
-        for (int i = 0; i < 32; i++) ow[32 * n32::brv5(i)] = acc[i];
+        for (int i = 0; i < 32; i++) ow[32 * n32::brv5(i)] = gl::canon(acc[i]);
       }
     }
   }
@@ -493,7 +493,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_
           for (int i = 0; i < 32; i++) acc[i] = v[i];
         } else if (lb == 15) {  // GoldiLocksDP B = 2^15: a shift instead of a product
 #pragma unroll
-          for (int i = 0; i < 32; i++) acc[i] = gl::add(gl::shl96(acc[i], 15), v[i]);
+          for (int i = 0; i < 32; i++) acc[i] = gl::add_weak(gl::shl_small_weak(acc[i], 15), v[i]);
         } else {
 #pragma unroll
           for (int i = 0; i < 32; i++) acc[i] = gl::add(gl::mul(acc[i], b_pow), v[i]);
@@ -524,7 +524,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_
       if (ok) {
         uint64_t *ow = w_ccs_k + ((size_t)kb * W + g) * D + r;
 #pragma unroll
-        for (int i = 0; i < 32; i++) ow[32 * n32::brv5(i)] = acc[i];
+        for (int i = 0; i < 32; i++) ow[32 * n32::brv5(i)] = gl::canon(acc[i]);
       }
     }
   }
