@@ -91,6 +91,12 @@ def load_traffic(d, W, kappa):
     if doc.get("config") != {"d": d, "W": W, "kappa": kappa}:
         return {}
     t = {k: v["hbm_bytes_per_launch"] for k, v in doc.get("kernels", {}).items()}
+    # a kernel launched as one template instance (k_decompose_fused<true>,
+    # k_ajtai_mfma<2>) is looked up by its plain name too
+    for k in list(t):
+        base = k.split("<")[0]
+        if base != k and base not in t and sum(x.split("<")[0] == base for x in t) == 1:
+            t[base] = t[k]
     if "k_decompose_fused" in t and "k_pack_sm" in t:  # the decompose phase launches both
         t["k_decompose_fused"] += t["k_pack_sm"]
     return t

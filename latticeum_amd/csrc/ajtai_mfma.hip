@@ -141,6 +141,9 @@ constexpr int AJ_CPS = 320;  // most chunks per split (i32 bound: < 512)
 typedef __attribute__((address_space(3))) void lds_void;
 __device__ __forceinline__ int fl_pi(int j, int i) { return i ^ (((j & 7) << 1) | ((i >> 5) & 1)); }
 
+// CPOL: cache policy of the operand copies (2 = nt: streaming, for operands far
+// larger than the caches -- A and F are each read once per launch)
+template <int CPOL>
 __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const uint4 *Ff, int d, int nch,
                                                       int nvec, int kappa, uint64_t *partial, OutPtrs dst,
                                                       int direct, int cps) {
@@ -160,7 +163,7 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const ui
 #pragma unroll
     for (int k = 0; k < 8; k++)
       __builtin_amdgcn_global_load_lds((const void *)(pa + ((size_t)c * 8 + k) * 64), (lds_void *)&Al[buf][w][k * 64],
-                                       16, 0, 0);
+                                       16, 0, CPOL);
   };
   // KiB j of an F chunk holds operand row j; wave w copies rows w, w + 4, ..
   // and skips rows >= nvec (their products only reach discarded outputs)
@@ -171,7 +174,7 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const ui
       const int j = 4 * q + w;
       if (q < nf)
         __builtin_amdgcn_global_load_lds((const void *)(ft + (size_t)c * FV_CHUNK + j * 64 + fl_pi(j, lane)),
-                                         (lds_void *)&Fl[buf][j * 64], 16, 0, 0);
+                                         (lds_void *)&Fl[buf][j * 64], 16, 0, CPOL);
     }
   };
   // this lane's F operand positions: piece (rh, k, s_lo = w) sits in KiB j = rh >> 1
@@ -345,8 +348,14 @@ hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, c
   }
   if (ev0) (void)hipEventRecord(ev0, st);
   const size_t waves = (size_t)dv * nsplit;
-  hipLaunchKernelGGL(k_ajtai_mfma, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, Af, Ff, dv, g.nch, nvec,
-                     (int)kappa, partial, kout, nsplit == 1 ? 1 : 0, cps);
+  const dim3 grid((unsigned)((waves + 3) / 4));
+  // F is dv nch 8 KiB per launch (A is as large for kappa = 32)
+  if ((size_t)dv * g.nch * 8192 > STREAM_OUT_BYTES)
+    hipLaunchKernelGGL(k_ajtai_mfma<2>, grid, dim3(256), 0, st, Af, Ff, dv, g.nch, nvec, (int)kappa, partial, kout,
+                       nsplit == 1 ? 1 : 0, cps);
+  else
+    hipLaunchKernelGGL(k_ajtai_mfma<0>, grid, dim3(256), 0, st, Af, Ff, dv, g.nch, nvec, (int)kappa, partial, kout,
+                       nsplit == 1 ? 1 : 0, cps);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (ev1) (void)hipEventRecord(ev1, st);

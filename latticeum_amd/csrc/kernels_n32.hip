@@ -417,6 +417,7 @@ __global__ void k_pack_sm(FusedSides sd, size_t N, int K, uint32_t *smg, int *er
   smg[t] = ea | (ec << 16);
 }
 
+template <bool NT>
 __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_all, size_t N, int L, int lb,
                                                            int K, FusedSides sd, const uint64_t *mid_fg,
                                                            uint4 *frag, int nch, uint64_t *sink) {
@@ -478,7 +479,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_
         {  // groups past W store into `sink` (no branch around the stores: see above)
           uint64_t *oc = (ok ? f_coeff_k + e * D : sink) + r;
 #pragma unroll
-          for (int k = 0; k < 32; k++) oc[32 * k] = from_signed(dg[k]);
+          for (int k = 0; k < 32; k++) out_store<NT>(&oc[32 * k], from_signed(dg[k]));
         }
         uint64_t v[32];
         n32::neg_ct32_digits(dg, v);
@@ -486,7 +487,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_
         {
           uint64_t *of = (ok ? f_k + e * D : sink) + r;
 #pragma unroll
-          for (int i = 0; i < 32; i++) of[32 * n32::brv5(i)] = v[i];
+          for (int i = 0; i < 32; i++) out_store<NT>(&of[32 * n32::brv5(i)], v[i]);
         }
         if (l == L - 1) {  // Horner's first term
 #pragma unroll
@@ -516,7 +517,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_
             d8_transpose16(x, pu);
             uint4 *out = frag + fv_index(s, nch, c, row, uh);
 #pragma unroll
-            for (int b = 0; b < 8; b++) out[4 * b] = pu[b];
+            for (int b = 0; b < 8; b++) out_store<NT>(&out[4 * b], pu[b]);
           }
           __syncthreads();  // S consumed before the next transpose
         }
@@ -524,7 +525,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_
       if (ok) {
         uint64_t *ow = w_ccs_k + ((size_t)kb * W + g) * D + r;
 #pragma unroll
-        for (int i = 0; i < 32; i++) ow[32 * n32::brv5(i)] = gl::canon(acc[i]);
+        for (int i = 0; i < 32; i++) out_store<NT>(&ow[32 * n32::brv5(i)], gl::canon(acc[i]));
       }
     }
   }
@@ -551,8 +552,14 @@ hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K,
   // chip); the CUs left over run other streams' kernels
   const size_t per = (ntask + ncu - 1) / ncu;
   const unsigned grid = (unsigned)((ntask + per - 1) / per);
-  hipLaunchKernelGGL(k_decompose_fused, dim3(grid), dim3(512), 0, st, smg, N, L, lb, K, sd, fwd.mid, frag, nch,
-                     sink);
+  // outputs: f_coeff_k, f_k, frag (each K N D words per side) and w_ccs_k
+  const size_t out_bytes = sd.nside * (size_t)K * N * D * 8 * 3;
+  if (out_bytes > STREAM_OUT_BYTES)
+    hipLaunchKernelGGL(k_decompose_fused<true>, dim3(grid), dim3(512), 0, st, smg, N, L, lb, K, sd, fwd.mid, frag,
+                       nch, sink);
+  else
+    hipLaunchKernelGGL(k_decompose_fused<false>, dim3(grid), dim3(512), 0, st, smg, N, L, lb, K, sd, fwd.mid, frag,
+                       nch, sink);
   return hipGetLastError();
 }
 static unsigned half_blocks(size_t units, unsigned cap) {
