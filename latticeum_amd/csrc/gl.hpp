@@ -180,6 +180,10 @@ LF_HD uint64_t add_weak(uint64_t a, uint64_t b) {
   return c ? t + EPS : t;
 }
 
+// x 2^e for canonical x and a constant 0 <= e < 192 (2^96 == -1): the
+// shl96 forms plus a negation, against mul_pow2's generic 128-bit fold
+LF_HD uint64_t shl192(uint64_t x, int e) { return e < 96 ? shl96(x, e) : neg(shl96(x, e - 96)); }
+
 LF_HD uint64_t pow(uint64_t a, uint64_t e) {
   uint64_t r = 1;
   while (e) {

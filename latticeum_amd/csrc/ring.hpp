@@ -3,7 +3,7 @@
 //  * Phi_72 = X^24 - X^12 + 1 (the reference's Goldilocks ring, d = 24): CRT to
 //    8 slots of Fq3, restating stark-rings goldilocks/ntt.rs:135-346. Every
 //    root of unity in that file is a power of two (omega_24 = 2^40, 2^192 == 1),
-//    so all twiddle products are shifts + one 128->64 fold (gl::mul_pow2);
+//    so all twiddle products are shifts (gl::shl192);
 //    only the ICRT's KAPPA (ntt.rs:43) is a general product.
 //  * X^d + 1, d = 4^k (this project's negacyclic ring, no reference analogue):
 //    slot k = f(psi^(2k+1)), psi = 7^((p-1)/2d), natural order. Radix-4
@@ -17,7 +17,7 @@ namespace ring {
 __host__ __device__ constexpr int W(int k) { return (40 * k) % 192; }
 constexpr uint64_t KAPPA = 12297829382473034411ull;  // ntt.rs:43 literal (= 1/(2 w^4 - 1))
 
-__device__ __forceinline__ uint64_t mw(uint64_t x, int k) { return gl::mul_pow2(x, W(k)); }
+__device__ __forceinline__ uint64_t mw(uint64_t x, int k) { return gl::shl192(x, W(k)); }
 
 // goldilocks/ntt.rs:326-334
 __device__ __forceinline__ void phi72_homogenize(uint64_t *c) {
@@ -120,8 +120,8 @@ __device__ __forceinline__ void phi72_icrt(uint64_t *c) {
   for (int i = 0; i < 12; i++) {
     uint64_t a = c[i], b = c[12 + i];
     uint64_t kd = gl::mul(KAPPA, gl::sub(a, b));
-    c[i] = gl::mul_pow2(gl::sub(gl::add(a, b), kd), 189);  // * 1/8 = 2^-3 = 2^189
-    c[12 + i] = gl::mul_pow2(kd, 190);                       // * 1/4 = 2^190
+    c[i] = gl::shl192(gl::sub(gl::add(a, b), kd), 189);  // * 1/8 = 2^-3 = 2^189
+    c[12 + i] = gl::shl192(kd, 190);                         // * 1/4 = 2^190
   }
 }
 
@@ -135,7 +135,7 @@ __device__ __forceinline__ uint64_t phi72_eval(const uint64_t *e, int vs) {
     case 0: return a0;
     case 1: return gl::add(gl::add(a0, a1), a2);
     case 2: return gl::add(gl::sub(a0, a1), a2);
-    case 3: return gl::add(gl::add(a0, gl::add(a1, a1)), gl::mul_pow2(a2, 2));
+    case 3: return gl::add(gl::add(a0, gl::add(a1, a1)), gl::shl96(a2, 2));
     default: return a2;
   }
 }
@@ -167,8 +167,8 @@ __device__ __forceinline__ void fq3acc_mad(Fq3Acc &s, uint64_t a0, uint64_t a1, 
   gl::acc_mad(s.s2, a2, b0);
 }
 __device__ __forceinline__ void fq3acc_final(const Fq3Acc &s, uint64_t *c) {
-  c[0] = gl::add(gl::acc_reduce(s.s00), gl::mul_pow2(gl::acc_reduce(s.s0n), 40));
-  c[1] = gl::add(gl::acc_reduce(s.s1), gl::mul_pow2(gl::acc_reduce(s.s1n), 40));
+  c[0] = gl::add(gl::acc_reduce(s.s00), gl::shl96(gl::acc_reduce(s.s0n), 40));
+  c[1] = gl::add(gl::acc_reduce(s.s1), gl::shl96(gl::acc_reduce(s.s1n), 40));
   c[2] = gl::acc_reduce(s.s2);
 }
 
