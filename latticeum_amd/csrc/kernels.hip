@@ -255,11 +255,25 @@ __global__ void __launch_bounds__(256) k_decompose_phi72(const uint64_t *f_coeff
       cur[2 * i + 1] = signed_rep(v.y);
     }
   }
-  for (int k = 0; k < K; k++) {
+  // b = 2 (lbs = 1): the balanced digits are sign(v) bit_k(|v|) (bal_digit's
+  // remainder is never rounded), so the planes are independent and
+  // blockIdx.y takes a range of them; otherwise gridDim.y = 1 and the planes
+  // run in order on the residual
+  const int KP = (K + (int)gridDim.y - 1) / (int)gridDim.y;
+  const int k0 = (int)blockIdx.y * KP, k1 = k0 + KP < K ? k0 + KP : K;
+  for (int k = k0; k < k1; k++) {
     uint64_t c[24];
     if (act) {
+      if (lbs == 1) {
 #pragma unroll
-      for (int i = 0; i < 24; i++) c[i] = from_signed(bal_digit(cur[i], lbs));
+        for (int i = 0; i < 24; i++) {
+          const int64_t m = cur[i] < 0 ? -cur[i] : cur[i], bit = (m >> k) & 1;
+          c[i] = from_signed(cur[i] < 0 ? -bit : bit);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 24; i++) c[i] = from_signed(bal_digit(cur[i], lbs));
+      }
       ulonglong2 *dc = reinterpret_cast<ulonglong2 *>(f_coeff_k + ((size_t)k * N + j) * 24);
 #pragma unroll
       for (int i = 0; i < 12; i++) dc[i] = make_ulonglong2(c[2 * i], c[2 * i + 1]);
@@ -310,10 +324,10 @@ __global__ void __launch_bounds__(256) k_decompose_phi72(const uint64_t *f_coeff
     }
     __syncthreads();
   }
-  if (act) {
+  if (act && blockIdx.y == 0) {
     bool bad = false;
 #pragma unroll
-    for (int i = 0; i < 24; i++) bad |= cur[i] != 0;
+    for (int i = 0; i < 24; i++) bad |= lbs == 1 ? ((cur[i] < 0 ? -cur[i] : cur[i]) >> K) != 0 : cur[i] != 0;
     if (bad) raise(err, 1);
   }
 }
@@ -863,8 +877,14 @@ hipError_t decompose_witness(const uint64_t *f_coeff, size_t N, int d, int lb, i
     size_t lds = (size_t)DEC_GROUPS * L * 25 * sizeof(uint64_t);
     if (frag && (L > 5 || row0 < 0 || row0 + K - 1 > 32)) return hipErrorInvalidValue;
     if (frag) lds = (size_t)DEC_GROUPS * L * DEC_SROW * sizeof(uint64_t);
-    hipLaunchKernelGGL(k_decompose_phi72, dim3(blocks(W, DEC_GROUPS)), dim3(256), lds, st, f_coeff, N,
-                       lb, L, lbs, K, f_coeff_k, f_k, w_ccs_k, err, frag, nch, row0);
+    // with independent planes (b = 2), split them over blockIdx.y until about
+    // 1024 blocks run: the real zkvm shape (W = 19 763) has only 412 element blocks
+    const unsigned nb = blocks(W, DEC_GROUPS);
+    unsigned ys = lbs == 1 ? (1024 + nb - 1) / nb : 1;
+    if (ys > (unsigned)K) ys = K;
+    if (ys < 1) ys = 1;
+    hipLaunchKernelGGL(k_decompose_phi72, dim3(nb, ys), dim3(256), lds, st, f_coeff, N, lb, L, lbs, K,
+                       f_coeff_k, f_k, w_ccs_k, err, frag, nch, row0);
     return hipGetLastError();
   }
   if (L > 8) return hipErrorInvalidValue;
