@@ -159,6 +159,31 @@ def test_decompose_overflow_is_an_error(ctx, d):
     ctx.decompose_witness(np.zeros(pr.L * d, np.uint64), pr)  # flag was cleared
 
 
+@pytest.mark.parametrize("d", [24, 1024])
+def test_decompose_digit_boundary(ctx, d):
+    """|v| = 2^K - 1 (either sign) takes exactly K binary digits; |v| = 2^K does
+    not (balanced_decomposition/mod.rs:85-87 panics). Several elements, so the
+    plane-split launches (one digit plane per block at this size) all run."""
+    pr = params(d)
+    K = pr.K
+    P = (1 << 64) - (1 << 32) + 1
+    n = 3 * pr.L * d
+    for v in ((1 << K) - 1, P - ((1 << K) - 1)):
+        fc = np.zeros(n, np.uint64)
+        fc[5] = v
+        fc[n - 1] = v
+        got = ctx.decompose_witness(fc, pr)
+        want = O.decompose_witness(fc, d, pr.B, pr.L, pr.b_small, K)
+        for g, w_ in zip(got, want):
+            assert np.array_equal(g, w_)
+    for v in (1 << K, P - (1 << K)):
+        fc = np.zeros(n, np.uint64)
+        fc[n - 1] = v
+        with pytest.raises(LA.LfError) as e:
+            ctx.decompose_witness(fc, pr)
+        assert e.value.code == 6
+
+
 # ------------------------------------------------------------------ Ajtai
 @pytest.mark.parametrize("d", ALL_D)
 @pytest.mark.parametrize("kappa,ncols", [(1, 1), (3, 17), (9, 300)])
