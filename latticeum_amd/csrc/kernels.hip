@@ -87,12 +87,18 @@ __global__ void k_mont(uint64_t *x, size_t n, int to) {
 
 // ============================================================ Witness::from_w_ccs
 // LF/arith.rs:230-248: ICRT -> gadget_decompose(B, L) -> CRT.
-// Phi_72: one thread per w_ccs element, all 24 coefficients in registers.
+// Phi_72: one thread per (w_ccs element j, digit l), so a launch has W * L
+// threads (about 1,500 waves at the real zkvm shape instead of 310). Each
+// thread redoes the ICRT of its element and the digit steps up to l; the last
+// digit's thread checks that the carry ran out. Neighbouring threads write
+// neighbouring 192-B outputs.
 __global__ void __launch_bounds__(128) k_from_w_ccs_phi72(const uint64_t *w_ccs, size_t W, int lb,
                                                          int L, uint64_t *f_coeff, uint64_t *f,
                                                          int *err) {
-  size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (j >= W) return;
+  const size_t u = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (u >= W * (size_t)L) return;
+  const size_t j = u / L;
+  const int l = (int)(u - j * L);
   uint64_t c[24];
   const ulonglong2 *src = reinterpret_cast<const ulonglong2 *>(w_ccs + j * 24);
 #pragma unroll
@@ -102,24 +108,28 @@ __global__ void __launch_bounds__(128) k_from_w_ccs_phi72(const uint64_t *w_ccs,
     c[2 * i + 1] = v.y;
   }
   ring::phi72_icrt(c);
-  int64_t cur[24];
+  int64_t cur[24], dg[24];
 #pragma unroll
   for (int i = 0; i < 24; i++) cur[i] = signed_rep(c[i]);
-  for (int l = 0; l < L; l++) {
+  for (int s = 0; s <= l; s++) {
 #pragma unroll
-    for (int i = 0; i < 24; i++) c[i] = from_signed(bal_digit(cur[i], lb));
-    ulonglong2 *dc = reinterpret_cast<ulonglong2 *>(f_coeff + (j * L + l) * 24);
-#pragma unroll
-    for (int i = 0; i < 12; i++) dc[i] = make_ulonglong2(c[2 * i], c[2 * i + 1]);
-    ring::phi72_crt(c);
-    ulonglong2 *df = reinterpret_cast<ulonglong2 *>(f + (j * L + l) * 24);
-#pragma unroll
-    for (int i = 0; i < 12; i++) df[i] = make_ulonglong2(c[2 * i], c[2 * i + 1]);
+    for (int i = 0; i < 24; i++) dg[i] = bal_digit(cur[i], lb);
   }
-  bool bad = false;
 #pragma unroll
-  for (int i = 0; i < 24; i++) bad |= cur[i] != 0;
-  if (bad) raise(err, 1);
+  for (int i = 0; i < 24; i++) c[i] = from_signed(dg[i]);
+  ulonglong2 *dc = reinterpret_cast<ulonglong2 *>(f_coeff + u * 24);
+#pragma unroll
+  for (int i = 0; i < 12; i++) dc[i] = make_ulonglong2(c[2 * i], c[2 * i + 1]);
+  ring::phi72_crt(c);
+  ulonglong2 *df = reinterpret_cast<ulonglong2 *>(f + u * 24);
+#pragma unroll
+  for (int i = 0; i < 12; i++) df[i] = make_ulonglong2(c[2 * i], c[2 * i + 1]);
+  if (l == L - 1) {
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < 24; i++) bad |= cur[i] != 0;
+    if (bad) raise(err, 1);
+  }
 }
 
 // negacyclic: one workgroup per w_ccs element.
@@ -166,14 +176,19 @@ __global__ void __launch_bounds__(NT<D>::T) k_from_w_ccs_nega(const uint64_t *w_
 
 // ============================================================ Witness::from_f
 // LF/arith.rs:299-313: f_coeff = ICRT(f); w_ccs = gadget_recompose(f, B, L).
-__global__ void __launch_bounds__(128) k_from_f_phi72(const uint64_t *f, size_t W, int lb, int L,
+// Phi_72: one thread per f element (j, l); a block holds G = blockDim / L whole
+// groups. The raw elements go through LDS, where the block's threads run the
+// Horner recompose (balanced_decomposition/mod.rs:105-117) over the G * 24
+// w_ccs coefficients and store them contiguously.
+__global__ void __launch_bounds__(256) k_from_f_phi72(const uint64_t *f, size_t W, int lb, int L,
                                                      uint64_t *f_coeff, uint64_t *w_ccs) {
-  size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (j >= W) return;
-  uint64_t acc[24];
-  for (int l = L - 1; l >= 0; l--) {
+  extern __shared__ uint64_t lds[];  // [G * L][24]
+  const int G = blockDim.x / L, t = threadIdx.x;
+  const size_t j0 = (size_t)blockIdx.x * G;
+  const size_t u = j0 * L + t;
+  if (t < G * L && u < W * (size_t)L) {
     uint64_t c[24];
-    const ulonglong2 *src = reinterpret_cast<const ulonglong2 *>(f + (j * L + l) * 24);
+    const ulonglong2 *src = reinterpret_cast<const ulonglong2 *>(f + u * 24);
 #pragma unroll
     for (int i = 0; i < 12; i++) {
       ulonglong2 v = src[i];
@@ -181,16 +196,21 @@ __global__ void __launch_bounds__(128) k_from_f_phi72(const uint64_t *f, size_t 
       c[2 * i + 1] = v.y;
     }
 #pragma unroll
-    for (int i = 0; i < 24; i++)  // Horner: recompose() (balanced_decomposition/mod.rs:105-117)
-      acc[i] = (l == L - 1) ? c[i] : gl::add(gl::mul_pow2(acc[i], lb), c[i]);
+    for (int i = 0; i < 24; i++) lds[t * 24 + i] = c[i];
     ring::phi72_icrt(c);
-    ulonglong2 *dc = reinterpret_cast<ulonglong2 *>(f_coeff + (j * L + l) * 24);
+    ulonglong2 *dc = reinterpret_cast<ulonglong2 *>(f_coeff + u * 24);
 #pragma unroll
     for (int i = 0; i < 12; i++) dc[i] = make_ulonglong2(c[2 * i], c[2 * i + 1]);
   }
-  ulonglong2 *dw = reinterpret_cast<ulonglong2 *>(w_ccs + j * 24);
-#pragma unroll
-  for (int i = 0; i < 12; i++) dw[i] = make_ulonglong2(acc[2 * i], acc[2 * i + 1]);
+  __syncthreads();
+  const size_t ng = W - j0 < (size_t)G ? W - j0 : (size_t)G;
+  for (int o = t; o < (int)ng * 24; o += blockDim.x) {
+    const int g = o / 24, i = o - g * 24;
+    const uint64_t *row = lds + g * L * 24 + i;
+    uint64_t acc = row[(L - 1) * 24];
+    for (int l = L - 2; l >= 0; l--) acc = gl::add(gl::mul_pow2(acc, lb), row[l * 24]);
+    w_ccs[j0 * 24 + o] = acc;
+  }
 }
 
 template <int D>
@@ -826,8 +846,8 @@ hipError_t from_w_ccs(const uint64_t *w_ccs, size_t W, int d, int lb, int L, uin
   if (W == 0) return hipSuccess;
   if (d == 1024 && fwd.mid && inv.mid) return from_w_ccs_n32(w_ccs, W, lb, L, f_coeff, f, fwd, inv, err, st);
   if (d == 24) {
-    hipLaunchKernelGGL(k_from_w_ccs_phi72, dim3(blocks(W, 128)), dim3(128), 0, st, w_ccs, W, lb, L,
-                       f_coeff, f, err);
+    hipLaunchKernelGGL(k_from_w_ccs_phi72, dim3(blocks(W * L, 128)), dim3(128), 0, st, w_ccs, W, lb,
+                       L, f_coeff, f, err);
     return hipGetLastError();
   }
 #define LF_CASE(DD)                                                                                \
@@ -848,8 +868,10 @@ hipError_t from_f(const uint64_t *f, size_t N, int d, int lb, int L, uint64_t *f
   if (W == 0) return hipSuccess;
   if (d == 1024 && inv.mid) return from_f_n32(f, W, lb, L, f_coeff, w_ccs, inv, st);
   if (d == 24) {
-    hipLaunchKernelGGL(k_from_f_phi72, dim3(blocks(W, 128)), dim3(128), 0, st, f, W, lb, L, f_coeff,
-                       w_ccs);
+    if (L < 1 || L > 256) return hipErrorInvalidValue;
+    const int G = 256 / L;
+    hipLaunchKernelGGL(k_from_f_phi72, dim3(blocks(W, G)), dim3(G * L), (size_t)G * L * 24 * 8, st, f,
+                       W, lb, L, f_coeff, w_ccs);
     return hipGetLastError();
   }
 #define LF_CASE(DD)                                                                              \

@@ -114,6 +114,23 @@ def test_witness_from_f(ctx, d):
     assert np.array_equal(fc, ofc) and np.array_equal(w, ow)
 
 
+@pytest.mark.parametrize("W", [50, 51, 52, 205])
+def test_phi72_witness_block_edges(ctx, W):
+    """d = 24 from_w_ccs runs one thread per (element, digit) and from_f packs
+    51 whole groups of L = 5 elements per 255-thread block: W around and past
+    one block, with a ragged last block"""
+    d = 24
+    pr = params(d)
+    w = rand(W * d, 1300 + W)
+    fc, f = ctx.witness_from_w_ccs(w, pr)
+    ofc, of = O.witness_from_w_ccs(w, d, pr.B, pr.L)
+    assert np.array_equal(fc, ofc) and np.array_equal(f, of)
+    f_in = rand(W * pr.L * d, 1400 + W)
+    fc2, w2 = ctx.witness_from_f(f_in, pr)
+    ofc2, ow2 = O.witness_from_f(f_in, d, pr.B, pr.L)
+    assert np.array_equal(fc2, ofc2) and np.array_equal(w2, ow2)
+
+
 @pytest.mark.parametrize("W", [4095, 4096, 4101])
 def test_from_w_ccs_and_from_f_both_kernels_sampled(ctx, W):
     """d = 1024 runs a one-half-wave-per-(element, limb) kernel below W = 4096
