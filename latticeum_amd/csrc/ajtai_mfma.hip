@@ -69,22 +69,27 @@ __device__ __forceinline__ size_t frag_column(int c, int t, int Lp, size_t Wp, b
 // written: they only feed MFMA output columns (or rows) that are discarded.
 // PHI72: d = 24, the element's 40 virtual slots (Toom-3 evaluations) are
 // produced on the fly; dv = virtual slots per element (d, or 40 for PHI72).
+// ONEROW (a single operand row, the commit of one witness): the tile's 8 "rows"
+// are 8 consecutive chunks of that row instead, so no thread idles.
 constexpr int TF_S = 16, TF_R = 8, TF_J = 34;
-template <bool VMAJOR, bool PHI72>
+template <bool VMAJOR, bool PHI72, bool ONEROW>
 __global__ void __launch_bounds__(256) k_to_frag(VecPtrs rows, int rlo, int rhi, int d, int dv, int nch, int Lp,
                                                  size_t Wp, uint4 *frag) {
   __shared__ uint64_t tile[TF_R * TF_S * TF_J];
-  const int sb = blockIdx.x, c = blockIdx.y, r0 = (rlo & ~(TF_R - 1)) + blockIdx.z * TF_R, tid = threadIdx.x;
-  // load: 8 rows x 32 columns x (16 slots = 128 B = 8 pieces of 16 B)
+  const int sb = blockIdx.x, tid = threadIdx.x;
+  const int c0 = ONEROW ? blockIdx.y * TF_R : blockIdx.y;
+  const int r0 = ONEROW ? rlo : (rlo & ~(TF_R - 1)) + blockIdx.z * TF_R;
+  // load: 8 rows (or chunks) x 32 columns x (16 slots = 128 B = 8 pieces of 16 B)
 #pragma unroll
   for (int it = 0; it < TF_R * 32 * 8 / 256; it++) {
     const int p = it * 256 + tid;
     const int r = p >> 8, j = (p >> 3) & 31, q = p & 7;
+    const int c = ONEROW ? c0 + r : c0, row = ONEROW ? r0 : r0 + r;
     bool ok;
     const size_t col = frag_column(c, j, Lp, Wp, ok);
     ulonglong2 v = make_ulonglong2(0, 0);
-    if (r0 + r >= rlo && r0 + r < rhi && ok) {
-      const uint64_t *e = rows.p[r0 + r] + col * d;
+    if (row >= rlo && row < rhi && c < nch && ok) {
+      const uint64_t *e = rows.p[row] + col * d;
       const int vs = sb * TF_S + 2 * q;
       if (PHI72) {
         if (vs < dv) v.x = ring::phi72_eval(e, vs);
@@ -101,7 +106,8 @@ __global__ void __launch_bounds__(256) k_to_frag(VecPtrs rows, int rlo, int rhi,
   // emit: thread = (slot sl, half h, row r); lane (r, h) of the MFMA operand
   // holds columns 16h..16h+15 of one slot as 16 bytes per digit
   const int r = tid & 7, h = (tid >> 3) & 1, sl = tid >> 4;
-  if (r0 + r < rlo || r0 + r >= rhi || sb * TF_S + sl >= dv) return;
+  const int c = ONEROW ? c0 + r : c0, row = ONEROW ? r0 : r0 + r;
+  if (row < rlo || row >= rhi || c >= nch || sb * TF_S + sl >= dv) return;
   const ulonglong2 *src = reinterpret_cast<const ulonglong2 *>(tile + (r * TF_S + sl) * TF_J + 16 * h);
   uint64_t x[16];
 #pragma unroll
@@ -114,11 +120,11 @@ __global__ void __launch_bounds__(256) k_to_frag(VecPtrs rows, int rlo, int rhi,
   d8_transpose16(x, u);
   const size_t s = (size_t)sb * TF_S + sl;
   if (VMAJOR) {
-    uint4 *out = frag + fv_index(s, nch, c, r0 + r, h);
+    uint4 *out = frag + fv_index(s, nch, c, row, h);
 #pragma unroll
     for (int b = 0; b < 8; b++) out[4 * b] = u[b];
   } else {
-    uint4 *out = frag + ((s * nch + c) * 8) * 64 + r0 + r + 32 * h;
+    uint4 *out = frag + ((s * nch + c) * 8) * 64 + row + 32 * h;
 #pragma unroll
     for (int b = 0; b < 8; b++) out[b * 64] = u[b];
   }
@@ -311,7 +317,17 @@ hipError_t to_frag(const VecPtrs &rows, int nrows, int row0, const FragGeom &g, 
   const int rhi = row0 + nrows, ztiles = (rhi + TF_R - 1) / TF_R - row0 / TF_R;
   const dim3 grid((dv + TF_S - 1) / TF_S, g.nch, ztiles);
 #define LF_TF(VM, PH) \
-  hipLaunchKernelGGL((k_to_frag<VM, PH>), grid, dim3(256), 0, st, abs, row0, rhi, d, dv, g.nch, g.Lp, g.Wp, frag)
+  hipLaunchKernelGGL((k_to_frag<VM, PH, false>), grid, dim3(256), 0, st, abs, row0, rhi, d, dv, g.nch, g.Lp, g.Wp, frag)
+  if (nrows == 1 && vmajor) {
+    const dim3 grid1((dv + TF_S - 1) / TF_S, (g.nch + TF_R - 1) / TF_R, 1);
+    if (d == 24)
+      hipLaunchKernelGGL((k_to_frag<true, true, true>), grid1, dim3(256), 0, st, abs, row0, rhi, d, dv, g.nch, g.Lp,
+                         g.Wp, frag);
+    else
+      hipLaunchKernelGGL((k_to_frag<true, false, true>), grid1, dim3(256), 0, st, abs, row0, rhi, d, dv, g.nch, g.Lp,
+                         g.Wp, frag);
+    return hipGetLastError();
+  }
   if (d == 24) {
     if (vmajor)
       LF_TF(true, true);
