@@ -401,20 +401,31 @@ constexpr int FD_T_U64 = FD_WAVES * n32::WAVE_U64;
 constexpr int FD_S_U64 = D * FD_SROW;
 constexpr int FD_LDS_U64 = FD_T_U64 > FD_S_U64 ? FD_T_U64 : FD_S_U64;
 
+// four packed words per thread (t0 = 4 * thread): 2 x 32 contiguous bytes in,
+// one 16-B store out
+__device__ __forceinline__ uint32_t pack_sm1(uint64_t x, int K, bool &bad) {
+  const int64_t a = signed_rep(x);
+  const uint64_t m = a < 0 ? (uint64_t)(-a) : (uint64_t)a;
+  bad |= (m >> K) != 0;
+  return (uint32_t)(m & 0x7FFF) | (a < 0 ? 0x8000u : 0u);
+}
 __global__ void k_pack_sm(FusedSides sd, size_t N, int K, uint32_t *smg, int *err) {
-  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // (side, col, q, r)
-  if (t >= sd.nside * N * 512) return;
-  const int side = t >= N * 512;
+  const size_t t0 = 4 * (blockIdx.x * (size_t)blockDim.x + threadIdx.x);  // (side, col, q, r..r+3)
+  if (t0 >= sd.nside * N * 512) return;
+  const int side = t0 >= N * 512;
   const uint64_t *f_coeff = sd.f_coeff[side];
-  const size_t col = (t >> 9) - side * N;  // smg itself is indexed across sides
-  const int q = (t >> 5) & 15, r = t & 31;
-  const uint64_t *x = f_coeff + col * D + r + 64 * q;
-  const int64_t a = signed_rep(x[0]), c = signed_rep(x[32]);
-  const uint64_t ma = a < 0 ? (uint64_t)(-a) : (uint64_t)a, mc = c < 0 ? (uint64_t)(-c) : (uint64_t)c;
-  if ((ma >> K) != 0 || (mc >> K) != 0) raise(err, 1);
-  const uint32_t ea = (uint32_t)(ma & 0x7FFF) | (a < 0 ? 0x8000u : 0u);
-  const uint32_t ec = (uint32_t)(mc & 0x7FFF) | (c < 0 ? 0x8000u : 0u);
-  smg[t] = ea | (ec << 16);
+  const size_t col = (t0 >> 9) - side * N;  // smg itself is indexed across sides
+  const int q = (t0 >> 5) & 15, r = t0 & 31;
+  const ulonglong2 *x = reinterpret_cast<const ulonglong2 *>(f_coeff + col * D + r + 64 * q);
+  const ulonglong2 a0 = x[0], a1 = x[1], c0 = x[16], c1 = x[17];
+  bool bad = false;
+  uint4 o;
+  o.x = pack_sm1(a0.x, K, bad) | (pack_sm1(c0.x, K, bad) << 16);
+  o.y = pack_sm1(a0.y, K, bad) | (pack_sm1(c0.y, K, bad) << 16);
+  o.z = pack_sm1(a1.x, K, bad) | (pack_sm1(c1.x, K, bad) << 16);
+  o.w = pack_sm1(a1.y, K, bad) | (pack_sm1(c1.y, K, bad) << 16);
+  if (bad) raise(err, 1);
+  *reinterpret_cast<uint4 *>(smg + t0) = o;
 }
 
 template <bool NT>
@@ -539,7 +550,7 @@ hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K,
   if (!sink && hipMalloc(&sink, D * sizeof(uint64_t)) != hipSuccess) return hipErrorOutOfMemory;
   if (K > 15 || !fwd.mid || sd.nside < 1 || sd.nside > 2) return hipErrorInvalidValue;
   const size_t words = sd.nside * N * 512;
-  hipLaunchKernelGGL(k_pack_sm, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st, sd, N, K, smg, err);
+  hipLaunchKernelGGL(k_pack_sm, dim3((unsigned)((words / 4 + 255) / 256)), dim3(256), 0, st, sd, N, K, smg, err);
   // one 8-wave block per CU (LDS-bound); ntask = nblk K tasks spread evenly
   static int ncu = 0;
   if (!ncu) {
