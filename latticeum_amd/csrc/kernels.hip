@@ -580,13 +580,22 @@ __global__ void k_sum_planes(const uint64_t *partial, int nsplit, size_t len, ui
   out[v * out_stride_vec + r] = gl::acc_reduce(a);
 }
 
-__global__ void k_sum_planes_to(const uint64_t *partial, int nsplit, size_t len, int nvec, OutPtrs out) {
-  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (i >= len * nvec) return;
+// 64 outputs x 4 split groups per block: wave g sums splits g, g + 4, ... of
+// its 64 outputs (coalesced), and the 4 partial sums meet in LDS
+__global__ void __launch_bounds__(256) k_sum_planes_to(const uint64_t *partial, int nsplit, size_t len, int nvec,
+                                                      OutPtrs out) {
+  __shared__ uint64_t part[3][64];
+  const int o = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const size_t i = blockIdx.x * (size_t)64 + o;
+  const bool ok = i < len * nvec;
   Acc a;
   gl::acc_zero(a);
-  for (int s = 0; s < nsplit; s++) gl::acc_add(a, partial[(size_t)s * len * nvec + i]);
-  out.p[i / len][i % len] = gl::acc_reduce(a);
+  if (ok)
+    for (int s = g; s < nsplit; s += 4) gl::acc_add(a, partial[(size_t)s * len * nvec + i]);
+  const uint64_t v = gl::acc_reduce(a);
+  if (g > 0) part[g - 1][o] = v;
+  __syncthreads();
+  if (g == 0 && ok) out.p[i / len][i % len] = gl::add(gl::add(v, part[0][o]), gl::add(part[1][o], part[2][o]));
 }
 
 // ============================================================ commit_witnesses y_0
@@ -982,7 +991,7 @@ hipError_t sum_planes(const uint64_t *partial, int nsplit, size_t len, uint64_t 
 hipError_t sum_planes_to(const uint64_t *partial, int nsplit, size_t len, int nvec, const OutPtrs &out,
                          hipStream_t st) {
   if (len == 0 || nvec < 1) return hipSuccess;
-  hipLaunchKernelGGL(k_sum_planes_to, dim3(blocks(len * nvec, 256)), dim3(256), 0, st, partial, nsplit, len, nvec,
+  hipLaunchKernelGGL(k_sum_planes_to, dim3(blocks(len * nvec, 64)), dim3(256), 0, st, partial, nsplit, len, nvec,
                      out);
   return hipGetLastError();
 }
