@@ -632,6 +632,67 @@ __global__ void k_y0_cm0(const uint64_t *cm0s, const uint64_t *cm1s, uint64_t *y
   cm0[c] = gl::cacc_reduce(a);
 }
 
+// Phi_72: 16 slots x 16 k-lanes per block. Lane q of slot u takes the planes
+// k = q, q + 16, ... (k >= 1) of both sides: y_k 2^(k lbs) (the Horner sum of
+// y_0, unrolled) and rho_k (.) y_k (the Fq3 slot product of the fold); the
+// lanes' sums meet in LDS, and lane 0 forms y_0 = cm - sum and adds rho_0 (.) y_0
+__global__ void __launch_bounds__(256) k_y0_cm0_phi72(const uint64_t *cm0s, const uint64_t *cm1s, uint64_t *y0,
+                                                     uint64_t *y1, const uint64_t *rho, size_t nslots, int lbs,
+                                                     int K, uint64_t *cm0) {
+  __shared__ uint64_t part[16][16][9];
+  const int q = threadIdx.x & 15, ul = threadIdx.x >> 4;
+  const size_t u = blockIdx.x * (size_t)16 + ul;
+  const bool ok = u < nslots;
+  const size_t n = nslots * 3;
+  const int s = u % 8;
+  ring::Fq3Acc a;
+  ring::fq3acc_zero(a);
+  uint64_t hs[2][3] = {{0, 0, 0}, {0, 0, 0}};
+  if (ok)
+    for (int side = 0; side < 2; side++) {
+      const uint64_t *y = side ? y1 : y0;
+      for (int k = q > 0 ? q : 16; k < K; k += 16) {
+        const uint64_t *v = y + (size_t)k * n + 3 * u, *r = rho + ((size_t)side * K + k) * 24 + 3 * s;
+        ring::fq3acc_mad(a, r[0], r[1], r[2], v[0], v[1], v[2]);
+        const int e = (int)(((long long)k * lbs) % 192);
+#pragma unroll
+        for (int c = 0; c < 3; c++) hs[side][c] = gl::add(hs[side][c], gl::mul_pow2(v[c], e));
+      }
+    }
+  uint64_t cc[3];
+  ring::fq3acc_final(a, cc);
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    part[ul][q][c] = cc[c];
+    part[ul][q][3 + c] = hs[0][c];
+    part[ul][q][6 + c] = hs[1][c];
+  }
+  __syncthreads();
+  if (q != 0 || !ok) return;
+  uint64_t t[9];
+#pragma unroll
+  for (int c = 0; c < 9; c++) t[c] = part[ul][0][c];
+  for (int l = 1; l < 16; l++)
+#pragma unroll
+    for (int c = 0; c < 9; c++) t[c] = gl::add(t[c], part[ul][l][c]);
+  ring::Fq3Acc a0;
+  ring::fq3acc_zero(a0);
+  for (int side = 0; side < 2; side++) {
+    uint64_t *y = side ? y1 : y0;
+    const uint64_t *cm = (side ? cm1s : cm0s) + 3 * u, *r = rho + (size_t)side * K * 24 + 3 * s;
+    uint64_t v0[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      v0[c] = gl::sub(cm[c], t[3 + 3 * side + c]);
+      y[3 * u + c] = v0[c];
+    }
+    ring::fq3acc_mad(a0, r[0], r[1], r[2], v0[0], v0[1], v0[2]);
+  }
+  ring::fq3acc_final(a0, cc);
+#pragma unroll
+  for (int c = 0; c < 3; c++) cm0[3 * u + c] = gl::add(cc[c], t[c]);
+}
+
 // ============================================================ linear fold
 // LF/nifs/folding.rs:258-268 (f_0) and folding/utils.rs:470-476 (cm_0):
 //   out[j] = sum_i rho_i (.) x_i[j]
@@ -1000,7 +1061,12 @@ hipError_t y0_cm0(const uint64_t *cm0s, const uint64_t *cm1s, uint64_t *y0, uint
                   size_t kappa, int d, int lbs, int K, uint64_t *cm0, hipStream_t st) {
   const size_t n = kappa * (size_t)d;
   if (n == 0) return hipSuccess;
-  if (d == 24 || K < 1) return hipErrorInvalidValue;
+  if (K < 1) return hipErrorInvalidValue;
+  if (d == 24) {
+    hipLaunchKernelGGL(k_y0_cm0_phi72, dim3(blocks(kappa * 8, 16)), dim3(256), 0, st, cm0s, cm1s, y0, y1, rho,
+                       kappa * 8, lbs, K, cm0);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_y0_cm0, dim3(blocks(n, 256)), dim3(256), 0, st, cm0s, cm1s, y0, y1, rho, n, d, lbs, K, cm0);
   return hipGetLastError();
 }

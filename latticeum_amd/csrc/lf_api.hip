@@ -381,11 +381,9 @@ int fold_core(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lb
   }
   if (commit_f) cm_i = commit_cm;
   const uint64_t *cm_side[2] = {b->acc_cm, cm_i};
-  if (fused) {
+  if (fused || fused24) {
     // y_0 of both sides and cm_0 = sum rho_i y_i in one pass (the y_s[k >= 1] are in place)
     LF_HIP(c, lfk::y0_cm0(cm_side[0], cm_side[1], b->y[0], b->y[1], b->rho, kappa, d, lbs, K, b->cm0, c->cur));
-  } else if (fused24) {
-    for (int s = 0; s < 2; s++) LF_HIP(c, lfk::commit_y0(cm_side[s], b->y[s], kappa, d, lbs, K, c->cur));
   } else {
     if (commit_f) LF_HIP(c, hipMemcpyAsync(commit_cm, ycat, kd * 8, hipMemcpyDeviceToDevice, c->cur));
     for (int s = 0; s < 2; s++) {
@@ -405,7 +403,7 @@ int fold_core(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lb
     PhaseTimer pt(c, LF_PHASE_FOLD);
     LF_HIP(c, lfk::fold(b->rho, fx, 2 * K, N, d, b->f0, c->cur));
   }
-  if (!fused) LF_HIP(c, lfk::fold(b->rho, yx, 2 * K, kappa, d, b->cm0, c->cur));
+  if (!fused && !fused24) LF_HIP(c, lfk::fold(b->rho, yx, 2 * K, kappa, d, b->cm0, c->cur));
   // Witness::from_f(f_0) (arith.rs:299-313)
   PhaseTimer pt(c, LF_PHASE_FROM_F);
   LF_HIP(c, lfk::from_f(b->f0, N, d, lb, L, b->f0_coeff, b->w_ccs0, t->inv, c->cur));
