@@ -330,13 +330,13 @@ def main():
     if d == 24:
         kernel_of = {"decompose": "k_decompose_phi72", "ajtai": "k_ajtai_mfma" if sch.layout == 1 else "k_ajtai_phi72",
                      "fold": "k_fold_phi72", "from_w_ccs": "k_from_w_ccs_phi72", "from_f": "k_from_f_phi72",
-                     "to_frag": "k_to_frag<true, true>"}
+                     "to_frag": "k_to_frag<true, true, true>"}
     else:
         small = W < 4096  # kernels_n32.hip SPLIT_W: one half-wave per (element, limb)
         kernel_of = {"decompose": "k_decompose_fused",
                      "ajtai": "k_ajtai_mfma" if sch.layout == 1 else "k_ajtai_nega", "fold": "k_fold_nega",
                      "from_w_ccs": "k_from_w_ccs_split" if small else "k_from_w_ccs_n32",
-                     "from_f": "k_from_f_split" if small else "k_from_f_n32", "to_frag": "k_to_frag<true, false>"}
+                     "from_f": "k_from_f_split" if small else "k_from_f_n32", "to_frag": "k_to_frag<true, false, true>"}
     traffic = load_traffic(d, W, kappa)
     phases = {}
     for ph, (ms, cnt) in timed.items():
