@@ -72,6 +72,13 @@ __device__ __forceinline__ size_t frag_column(int c, int t, int Lp, size_t Wp, b
 // ONEROW (a single operand row, the commit of one witness): the tile's 8 "rows"
 // are 8 consecutive chunks of that row instead, so no thread idles.
 constexpr int TF_S = 16, TF_R = 8, TF_J = 34;
+// virtual slots 16 SB .. 16 SB + 15 (those below 40) of one Phi_72 element
+template <int SB>
+__device__ __forceinline__ void phi72_evals(const uint64_t *e, uint64_t *ev) {
+#pragma unroll
+  for (int i = 0; i < TF_S; i++)
+    if (SB * TF_S + i < 40) ev[i] = ring::phi72_eval(e, SB * TF_S + i);
+}
 template <bool VMAJOR, bool PHI72, bool ONEROW>
 __global__ void __launch_bounds__(256) k_to_frag(VecPtrs rows, int rlo, int rhi, int d, int dv, int nch, int Lp,
                                                  size_t Wp, uint4 *frag) {
@@ -79,28 +86,44 @@ __global__ void __launch_bounds__(256) k_to_frag(VecPtrs rows, int rlo, int rhi,
   const int sb = blockIdx.x, tid = threadIdx.x;
   const int c0 = ONEROW ? blockIdx.y * TF_R : blockIdx.y;
   const int r0 = ONEROW ? rlo : (rlo & ~(TF_R - 1)) + blockIdx.z * TF_R;
-  // load: 8 rows (or chunks) x 32 columns x (16 slots = 128 B = 8 pieces of 16 B)
-#pragma unroll
-  for (int it = 0; it < TF_R * 32 * 8 / 256; it++) {
-    const int p = it * 256 + tid;
-    const int r = p >> 8, j = (p >> 3) & 31, q = p & 7;
+  if (PHI72) {
+    // load: one thread per (row or chunk r, column j); the element's Fq3 slots
+    // behind virtual slots 16 sb .. 16 sb + 15 are read once and evaluated in
+    // registers (the slot block is uniform per launch block, so no divergence)
+    const int r = tid >> 5, j = tid & 31;
     const int c = ONEROW ? c0 + r : c0, row = ONEROW ? r0 : r0 + r;
     bool ok;
     const size_t col = frag_column(c, j, Lp, Wp, ok);
-    ulonglong2 v = make_ulonglong2(0, 0);
+    uint64_t ev[TF_S];
+#pragma unroll
+    for (int i = 0; i < TF_S; i++) ev[i] = 0;
     if (row >= rlo && row < rhi && c < nch && ok) {
       const uint64_t *e = rows.p[row] + col * d;
-      const int vs = sb * TF_S + 2 * q;
-      if (PHI72) {
-        if (vs < dv) v.x = ring::phi72_eval(e, vs);
-        if (vs + 1 < dv) v.y = ring::phi72_eval(e, vs + 1);
-      } else {
-        v = *reinterpret_cast<const ulonglong2 *>(e + vs);
-      }
+      if (sb == 0)
+        phi72_evals<0>(e, ev);
+      else if (sb == 1)
+        phi72_evals<1>(e, ev);
+      else
+        phi72_evals<2>(e, ev);
     }
-    uint64_t *t = tile + (r * TF_S + 2 * q) * TF_J + j;
-    t[0] = d8(v.x);
-    t[TF_J] = d8(v.y);
+#pragma unroll
+    for (int i = 0; i < TF_S; i++) tile[(r * TF_S + i) * TF_J + j] = d8(ev[i]);
+  } else {
+    // load: 8 rows (or chunks) x 32 columns x (16 slots = 128 B = 8 pieces of 16 B)
+#pragma unroll
+    for (int it = 0; it < TF_R * 32 * 8 / 256; it++) {
+      const int p = it * 256 + tid;
+      const int r = p >> 8, j = (p >> 3) & 31, q = p & 7;
+      const int c = ONEROW ? c0 + r : c0, row = ONEROW ? r0 : r0 + r;
+      bool ok;
+      const size_t col = frag_column(c, j, Lp, Wp, ok);
+      ulonglong2 v = make_ulonglong2(0, 0);
+      if (row >= rlo && row < rhi && c < nch && ok)
+        v = *reinterpret_cast<const ulonglong2 *>(rows.p[row] + col * d + sb * TF_S + 2 * q);
+      uint64_t *t = tile + (r * TF_S + 2 * q) * TF_J + j;
+      t[0] = d8(v.x);
+      t[TF_J] = d8(v.y);
+    }
   }
   __syncthreads();
   // emit: thread = (slot sl, half h, row r); lane (r, h) of the MFMA operand
