@@ -587,7 +587,10 @@ hipError_t transform_n32(uint64_t *data, size_t n, bool fwd, const ring::NegaTab
   return hipGetLastError();
 }
 // below this W the one-half-wave-per-element kernels leave CUs idle
-constexpr size_t SPLIT_W = 4096;
+#ifndef LF_SPLIT_W
+#define LF_SPLIT_W 4096
+#endif
+constexpr size_t SPLIT_W = LF_SPLIT_W;
 hipError_t from_w_ccs_n32(const uint64_t *w_ccs, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *f,
                           const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err, hipStream_t st) {
   if (W < SPLIT_W) {
