@@ -88,34 +88,31 @@ __global__ void __launch_bounds__(256) k_xform_n32(uint64_t *data, size_t n, con
 }
 
 // ---------------------------------------------------------------- Witness::from_w_ccs
-// LF/arith.rs:230-248: ICRT -> gadget_decompose(B = 2^lb, L) -> CRT; one half-wave per element
-__global__ void __launch_bounds__(256) k_from_w_ccs_n32(const uint64_t *w_ccs, size_t W, int lb, int L,
-                                                       uint64_t *f_coeff, uint64_t *f, const uint64_t *mid_fg,
-                                                       const uint64_t *mid_ig, int *err) {
+// LF/arith.rs:230-248: ICRT -> gadget_decompose(B = 2^lb, L) -> CRT; one half-wave per element.
+// The inverse middle factors read from global (L1-resident 8 KiB table),
+// no next-element prefetch, so two blocks (8 waves) fit a CU: 0.71 -> 0.52 ms at
+// W = 16 384 against the LDS-table, prefetching form (one block per CU)
+__global__ void __launch_bounds__(256, 2) k_from_w_ccs_n32(const uint64_t *w_ccs, size_t W, int lb, int L,
+                                                          uint64_t *f_coeff, uint64_t *f, const uint64_t *mid_fg,
+                                                          const uint64_t *mid_ig, int *err) {
   __shared__ uint64_t lds_all[WPB * n32::WAVE_U64];
-  __shared__ uint64_t mid_f[n32::MID_U64], mid_i[n32::MID_U64];
+  __shared__ uint64_t mid_f[n32::MID_U64];
   n32::stage_mid(mid_f, mid_fg);
-  n32::stage_mid(mid_i, mid_ig);
   __syncthreads();
   Half x = half_ctx(lds_all);
-  uint64_t nx[32];
-  {
-    const uint64_t *g = w_ccs + (x.unit < W ? x.unit : 0) * D + x.r;
-#pragma unroll
-    for (int k = 0; k < 32; k++) nx[k] = g[32 * k];
-  }
   for (size_t j = x.unit; j < pair_bound(W); j += x.stride) {
     const bool ok = j < W;
     uint64_t v[32];
+    {
+      const uint64_t *g = w_ccs + (ok ? j : 0) * D + x.r;
 #pragma unroll
-    for (int k = 0; k < 32; k++) v[k] = nx[k];
-    n32::inverse(v, mid_i, x.lds, x.r);
-    {  // next element's loads ahead of this element's stores
-      const size_t jn = j + x.stride;
-      const uint64_t *g = w_ccs + (jn < W ? jn : 0) * D + x.r;
-#pragma unroll
-      for (int k = 0; k < 32; k++) nx[k] = g[32 * k];
+      for (int k = 0; k < 32; k++) v[k] = g[32 * k];
     }
+    n32::cyc_dif32<true>(v);
+#pragma unroll
+    for (int i = 0; i < 32; i++) v[i] = gl::mul(v[i], mid_ig[x.r * 32 + i]);
+    n32::transpose_inv(v, x.lds, x.r);
+    n32::neg_gs32_inv(v);
     int64_t cur[32];
 #pragma unroll
     for (int k = 0; k < 32; k++) cur[k] = signed_rep(v[k]);
