@@ -10,9 +10,17 @@ Default workload (BASELINE.json configs[2], "Ajtai commit + single LatticeFold
 step on 2^14 synthetic CCS witnesses", at the metric's d=1024): ring
 Fq[X]/(X^1024+1), w_ccs = 2^14 ring elements, kappa = 32, B=2^15, L=5, K=15.
 
-Multi-GPU (torchrun, one rank per GPU): independent steps per rank (weak
-scaling); at the end of the timed batch the ranks' folded accumulators
-(cm_0, f_0) are reduced mod p over RCCL (latticeum_amd.dist).
+Multi-GPU (torchrun, one rank per GPU): `value` counts independent step
+streams per rank (the trace-batch shard of BASELINE configs[3]; weak scaling,
+no collective on the data path). At N > 1 the line also carries
+`sharded_fold`: one fold column-sharded over all ranks, with an RCCL
+all-reduce (mod p) of the partial commitments in every step, through the C
+ABI's communicator (lf_dev_fold_step_sharded; latticeum_amd.dist).
+
+Beside the headline the line reports (same run, each its own timed batch):
+the reference ring Phi_72 at the real zkvm shape (the path with reference
+parity), the byte-equivalent d=1024 shape W=464, configs[4]'s d=4096 ring with
+kappa=64, the configs[1] NTT batch and batched Poseidon2.
 """
 from __future__ import annotations
 
@@ -49,34 +57,56 @@ def parse():
                          "reported beside the default workload")
     ap.add_argument("--cpu-baseline", dest="cpu", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu", action="store_false")
-    ap.add_argument("--cpu-w", type=int, default=0, help="W of the CPU baseline sample (0 = auto)")
-    ap.add_argument("--cpu-threads", type=int, default=0)
     return ap.parse_args()
 
 
 def algorithmic_bytes(d, W, kappa, L=5, K=15):
-    """SURVEY.md §8d bytes/step and the algorithmic bytes of one launch of each
-    step phase (inputs read once + outputs written once)."""
+    """SURVEY.md 8(d)'s bytes/step (B1..B5) and the algorithmic bytes of one
+    launch of each step phase: its inputs read once and its outputs written
+    once in the Witness forms the reference materialises (u64 per residue).
+    `operand` is what a phase moves on top of that because the contraction
+    runs on the i8 matrix cores: the D8 operand rows the fused decompositions
+    write (F bytes per element; Phi_72 has 40 Toom-3 virtual slots, F = 320 B
+    against E = 192 B) and the larger operand form of A and the vectors."""
     E, N = 8 * d, W * L
     step = (E * (W + 3 * N + kappa * N + kappa) + 2 * E * (N + K * (2 * N + W))
             + E * (kappa * N + 2 * (K - 1) * N + 2 * (K - 1) * kappa) + E * (2 * K * N + N)
             + E * (2 * N + W))
     nvec = 2 * (K - 1) + 1  # commit(z)'s A.f rides in the decomposition-commitment pass
-    # i8-MFMA operand bytes per element: 8 signed bytes per slot; d = 24 (Phi_72)
-    # contracts 40 virtual slots (Toom-3 evaluations of its 8 Fq3 slots)
     F = 8 * (40 if d == 24 else d)
-    sides = 1 if d == 24 else 2  # the d = 1024 decomposition runs both sides in one launch
-    phases = {
-        # f_coeff in; f_k_coeff, f_k (K N each), w_ccs_k (K W), K-1 planes as i8-MFMA operand rows out
-        "decompose": sides * (E * (N + 2 * K * N + K * W) + F * (K - 1) * N),
-        # A and the 29 vectors in operand form, and the 29 kappa-element results
-        "ajtai": F * (kappa * N + nvec * N) + E * nvec * kappa,
-        "fold": E * (2 * K * N + N),
+    fused = d in (24, 1024)  # the decompositions write planes 1..K-1 as operand rows
+    sides = 2 if d == 1024 else 1  # the d = 1024 decomposition runs both sides in one launch
+    alg = {
+        # B2 (per launch): f_coeff in; f_k_coeff, f_k (K N each), w_ccs_k (K W) out
+        "decompose": sides * E * (N + 2 * K * N + K * W),
+        # B3 + commit(z)'s A f: A once, the 29 vectors, the 29 kappa-element results
+        "ajtai": E * (kappa * N + nvec * N + nvec * kappa),
+        "fold": E * (2 * K * N + N),  # B4
         "from_w_ccs": E * (W + 2 * N),
-        "from_f": E * (2 * N + W),
-        "to_frag": E * N + F * N,
+        "from_f": E * (2 * N + W),  # B5
+        "to_frag": E * N + F * N,  # commit(z)'s f into operand form (fused paths)
     }
-    return step, phases
+    operand = {
+        "decompose": sides * F * (K - 1) * N if fused else 0,
+        "ajtai": (F - E) * (kappa * N + nvec * N),
+    }
+    return step, alg, operand
+
+
+def kernel_names(LA, d, W, layout):
+    """the kernel each lf_dev_fold_step phase launches (for the rocprof / PMC joins)"""
+    if d == 24:
+        return {"decompose": "k_decompose_phi72", "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_phi72",
+                "fold": "k_fold_phi72", "from_w_ccs": "k_from_w_ccs_phi72", "from_f": "k_from_f_phi72",
+                "to_frag": "k_to_frag<true, true, true>"}
+    if d == 1024:
+        small = W < LA.witness_split_w()  # one half-wave per (element, limb) below this W
+        return {"decompose": "k_decompose_fused", "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_nega",
+                "fold": "k_fold_nega", "from_w_ccs": "k_from_w_ccs_split" if small else "k_from_w_ccs_n32",
+                "from_f": "k_from_f_split" if small else "k_from_f_n32", "to_frag": "k_to_frag<true, false, true>"}
+    return {"decompose": "k_decompose_nega", "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_nega",
+            "fold": "k_fold_nega", "from_w_ccs": "k_from_w_ccs_nega", "from_f": "k_from_f_nega",
+            "to_frag": "k_to_frag"}
 
 
 def load_traffic(d, W, kappa):
@@ -102,13 +132,22 @@ def load_traffic(d, W, kappa):
     return t
 
 
-def cpu_baseline(d, W_full, kappa, cpu_w, threads):
-    """Time the oracle's restatement of the same step on host cores (bounded sample)."""
-    sys.path.insert(0, str(ROOT / "oracle"))
-    import oracle as O
+def host_cores():
+    """CPUs this process may use: its affinity set, capped by a cgroup CPU quota
+    (the GPU box shows the whole machine in os.cpu_count())"""
+    n = len(os.sched_getaffinity(0))
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if quota != "max":
+            n = min(n, -(-int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
 
+
+def cpu_step_seconds(O, d, kappa, W, threads):
+    """one commit+fold step of the oracle's C restatement at w_ccs length W"""
     B, L, bs, K = 1 << 15, 5, 2, 15
-    W = cpu_w
     N = W * L
     A = O.fill_uniform(kappa * N * d, SEED_A)
     w_ccs = O.fill_uniform(W * d, SEED_W)
@@ -129,11 +168,30 @@ def cpu_baseline(d, W_full, kappa, cpu_w, threads):
     f0 = O.fold_f0(rho, np.concatenate([s[1] for s in sides]), 2 * K, N, d, threads)
     O.fold_cm0(rho, np.concatenate(ys), 2 * K, kappa, d)
     O.witness_from_f(f0, d, B, L, threads)
-    dt = time.perf_counter() - t0
-    steps_per_s = 1.0 / (dt * W_full / W)  # every stage is linear in W
-    return {"value": steps_per_s, "unit": "fold-steps/s", "cores": threads, "kind": "port",
-            "sample": f"1 full step at W={W} (1/{W_full // W} of W={W_full}), d={d}, kappa={kappa}, "
-                      f"{dt:.2f} s on {threads} threads; scaled linearly in W"}
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(d, W_full, kappa):
+    """The oracle's C restatement of the same step (kind "port": the Rust
+    reference cannot be built here), parallelised where the reference uses
+    rayon, timed on all host cores and on one core over bounded samples of the
+    workload and scaled linearly in W (every stage is linear in W). It is the
+    naive u128-% restatement, not a tuned rayon build, so it understates what
+    the reference's own CPU path would reach."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle as O
+
+    cores = host_cores()
+    w_all = max(1, min(W_full, 512 if d >= 1024 else 4096))
+    w_one = max(1, min(W_full, 64 if d >= 1024 else 512))
+    t_all = cpu_step_seconds(O, d, kappa, w_all, cores)
+    t_one = cpu_step_seconds(O, d, kappa, w_one, 1)
+    v_all = 1.0 / (t_all * W_full / w_all)
+    v_one = 1.0 / (t_one * W_full / w_one)
+    return {"value": v_all, "unit": "fold-steps/s", "cores": cores, "kind": "port",
+            "sample": f"1 step at W={w_all} on {cores} threads ({t_all:.2f} s) and at W={w_one} on 1 thread "
+                      f"({t_one:.2f} s), d={d}, kappa={kappa}; scaled linearly to W={W_full}",
+            "single_core": {"value": v_one, "cores": 1}}
 
 
 class Workload:
@@ -141,7 +199,7 @@ class Workload:
     side and rho (shared, read-only), and `streams` independent step streams,
     each an lf context on its own HIP stream with its own w_ccs and outputs."""
 
-    def __init__(self, LA, torch, local, rank, d, W, kappa, streams):
+    def __init__(self, LA, torch, local, rank, d, W, kappa, streams, seed_a=SEED_A):
         self.LA, self.torch = LA, torch
         self.d, self.W, self.kappa = d, W, kappa
         self.pr = pr = LA.goldilocks_dp(d)
@@ -152,7 +210,7 @@ class Workload:
         ctx = LA.Context(local)
         ctx.set_stream(torch.cuda.current_stream().cuda_stream)
         A = z(kappa * N * d)
-        ctx.dev_fill_uniform(A, SEED_A)
+        ctx.dev_fill_uniform(A, seed_a)
         self.sch = sch = LA.AjtaiCommitmentScheme(ctx, device_tensor=A, kappa=kappa, ncols=N, d=d)
         if sch.layout == 1:  # the scheme keeps A in MFMA fragment order; drop the AoS copy
             del A
@@ -202,11 +260,31 @@ class Workload:
             self.bufs.append(bufs)
         torch.cuda.synchronize()
 
-    def run(self, steps):
-        """`steps` fold steps, round-robin over the step streams (asynchronous)"""
+    def run(self, steps, comm=None):
+        """`steps` fold steps, round-robin over the step streams (asynchronous);
+        with `comm`, each step is this rank's column shard of one fold
+        (lf_dev_fold_step_sharded: RCCL all-reduce of the commitments)"""
         S = len(self.ctxs)
         for i in range(steps):
-            self.ctxs[i % S].dev_fold_step(self.sch, self.pr, self.W, self.bufs[i % S])
+            if comm is None:
+                self.ctxs[i % S].dev_fold_step(self.sch, self.pr, self.W, self.bufs[i % S])
+            else:
+                self.ctxs[i % S].dev_fold_step_sharded(self.sch, self.pr, self.W, self.bufs[i % S], comm)
+
+    def timing(self, on):
+        for c in self.ctxs:
+            c.kernel_timing(on)
+
+    def phase_totals(self):
+        """(device ms, launches) per phase, summed over every step stream"""
+        nvec = 2 * (self.pr.K - 1) + 1
+        tot = {}
+        for c in self.ctxs:
+            for ph, (ms, cnt) in [("ajtai", c.kernel_stats(nvec))] + [(p, c.phase_stats(p)) for p in c.PHASES]:
+                a = tot.setdefault(ph, [0.0, 0])
+                a[0] += ms
+                a[1] += cnt
+        return tot
 
     def sync(self):
         for c in self.ctxs:
@@ -221,29 +299,110 @@ class Workload:
         self.ctxs = []
 
 
-def extra_shape(LA, torch, LD, pg, local, rank, world, d, W, kappa, S, steps, warmup, what):
-    """Another commit+fold workload with S concurrent step streams per GPU,
-    reported beside the default one (not as `value`): SURVEY.md §8d's
-    byte-equivalent shape (d = 1024, W = 464), whose per-GPU rate the north-star
-    target (1e4 steps/s on 8 GPUs) is about, and the reference's own ring at the
-    real zkvm shape (d = 24, W = 19 763; the bit-exact-vs-reference path)."""
-    wl = Workload(LA, torch, local, rank, d, W, kappa, S)
-    wl.run(warmup)
-    torch.cuda.synchronize()
+def measure(LA, torch, LD, pg, world, wl, steps, warmup, comm=None):
+    """time `steps` fold steps of workload `wl` (after `warmup` untimed ones):
+    barrier + device sync on both sides, max over ranks; every phase timed
+    with HIP events on its launch stream inside the timed region"""
+    wl.run(warmup, comm)
+    wl.sync()
+    wl.timing(True)
     LD.barrier(pg)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    wl.run(steps)
+    wl.run(steps, comm)
     torch.cuda.synchronize()
     LD.barrier(pg)
-    dt = LD.max_over_ranks(pg, time.perf_counter() - t0)
+    dt = time.perf_counter() - t0
+    wl.sync()  # surfaces any decomposition overflow
+    dt_max = LD.max_over_ranks(pg, dt)
+    tot = wl.phase_totals()
+    wl.timing(False)
+    return dt_max, phase_report(LA, wl, tot, steps)
+
+
+def phase_report(LA, wl, tot, steps):
+    """per phase: average launch, launches and device ms per step, algorithmic
+    bytes, achieved GB/s and fraction of HBM peak; the dominant phase's roofline"""
+    d, W, kappa = wl.d, wl.W, wl.kappa
+    _, alg, operand = algorithmic_bytes(d, W, kappa, wl.pr.L, wl.pr.K)
+    kernel_of = kernel_names(LA, d, W, wl.sch.layout)
+    traffic = load_traffic(d, W, kappa)
+    phases = {}
+    for ph, (ms, cnt) in tot.items():
+        if not cnt:
+            continue
+        avg = ms / cnt
+        gbs = alg[ph] / (avg * 1e-3) / 1e9
+        extra = operand.get(ph, 0)
+        phases[ph] = {"kernel": kernel_of[ph], "avg_launch_ms": avg, "launches_per_step": cnt / steps,
+                      "ms_per_step": ms / steps, "algorithmic_bytes_per_launch": alg[ph],
+                      "achieved_gbs": gbs, "frac_hbm": gbs / HBM_PEAK_GBS,
+                      "operand_bytes_per_launch": extra,
+                      "achieved_gbs_incl_operands": (alg[ph] + extra) / (avg * 1e-3) / 1e9,
+                      "traffic_bytes_per_launch": traffic.get(kernel_of[ph])}
+    if not phases:
+        return phases, None
+    dom = max(phases, key=lambda k: phases[k]["ms_per_step"])
+    p = phases[dom]
+    roof = {"kernel": p["kernel"], "phase": dom, "bound": "hbm", "achieved": p["achieved_gbs"],
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": p["frac_hbm"], "traffic": p["traffic_bytes_per_launch"],
+            "avg_launch_ms": p["avg_launch_ms"], "bytes_per_launch": p["algorithmic_bytes_per_launch"],
+            "extra_bytes": p["operand_bytes_per_launch"]}
+    return phases, roof
+
+
+def extra_shape(LA, torch, LD, pg, local, rank, world, d, W, kappa, S, steps, warmup, what):
+    """Another commit+fold workload with S concurrent step streams per GPU,
+    reported beside the default one (not as `value`): the reference's own ring
+    at the real zkvm shape (d = 24, W = 19 763; the bit-exact-vs-reference
+    path), SURVEY.md 8(d)'s byte-equivalent shape (d = 1024, W = 464), whose
+    per-GPU rate the north-star target (1e4 steps/s on 8 GPUs) is about, and
+    BASELINE configs[4]'s ring (d = 4096, kappa = 64)."""
+    wl = Workload(LA, torch, local, rank, d, W, kappa, S)
+    dt, (phases, roof) = measure(LA, torch, LD, pg, world, wl, steps, warmup)
     wl.close()
+    del wl
     torch.cuda.empty_cache()
     value = world * steps / dt
-    step_bytes, _ = algorithmic_bytes(d, W, kappa)
+    step_bytes, _, _ = algorithmic_bytes(d, W, kappa)
     return {"workload": f"commit+fold step, {what}, w_ccs W={W}, kappa={kappa}, {S} concurrent step streams per GPU",
-            "d": d, "W": W, "streams": S, "value": value, "unit": "fold-steps/s", "n_gpus": world, "steps": steps,
-            "ms_per_step_per_gpu": dt / steps * 1e3, "hbm_gbs_step_algorithmic": step_bytes * value / world / 1e9}
+            "d": d, "W": W, "kappa": kappa, "streams": S, "value": value, "unit": "fold-steps/s", "n_gpus": world,
+            "steps": steps, "ms_per_step_per_gpu": dt / steps * 1e3,
+            "hbm_gbs_step_algorithmic": step_bytes * value / world / 1e9, "roofline": roof, "phases": phases}
+
+
+def sharded_fold(LA, torch, LD, pg, local, rank, world, d, W, kappa, steps, warmup):
+    """One fold sharded by columns over all ranks: rank r holds
+    W w_ccs groups (its shard of a world * W witness) and A's matching columns;
+    every step all-reduces the 29 partial commitments over RCCL (mod p, limb
+    transport) on the step's stream (lf_dev_fold_step_sharded)."""
+    wl = Workload(LA, torch, local, rank, d, W, kappa, 1, seed_a=SEED_A + 7919 * rank)
+    comm = LD.make_comm(wl.ctxs[0], pg, world, rank)
+    try:
+        dt, (phases, roof) = measure(LA, torch, LD, pg, world, wl, steps, warmup, comm)
+        # the accumulator exchange of independent step streams, for reference
+        keep = wl.keeps[0]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        LD.AccumulatorReducer(comm, [keep["cm0"], keep["f0"]]).reduce()
+        torch.cuda.synchronize()
+        t_red = LD.max_over_ranks(pg, time.perf_counter() - t0)
+    finally:
+        if comm is not None:
+            comm.close()
+        wl.close()
+        del wl
+        torch.cuda.empty_cache()
+    kd = 29 * kappa * d * 8
+    return {"workload": f"one commit+fold step of a w_ccs of W={world}x{W} ring elements, column-sharded "
+                        f"over {world} GPUs (W={W} per GPU), d={d}, kappa={kappa}; per step one RCCL all-reduce "
+                        f"of the 29 partial commitments ({kd / 1e6:.1f} MB as 2x32-bit limbs)",
+            "value": steps / dt, "unit": "sharded fold-steps/s", "shard_steps_per_s": world * steps / dt,
+            "n_gpus": world, "steps": steps, "ms_per_step": dt / steps * 1e3, "scaling": "weak",
+            "roofline": roof, "phases": phases,
+            "accumulator_reduce_ms": t_red * 1e3,
+            "accumulator_reduce": f"cm_0 + f_0 ({(kappa + W * 5) * d * 8 / 1e6:.0f} MB) summed over ranks mod p "
+                                  f"(lf_fold_reduce_allranks), timed once outside the steps"}
 
 
 def side_ops(LA, torch, local):
@@ -285,6 +444,10 @@ def side_ops(LA, torch, local):
     return out
 
 
+EXCLUDED = ("outside the timed step (other tiers): the Poseidon2 transcript and challenge derivation (rho is an "
+            "input), linearization, the sumcheck provers and the Mz matrix-vector products")
+
+
 def main():
     args = parse()
     import torch
@@ -299,63 +462,18 @@ def main():
 
     d, W, kappa = args.d, args.w, args.kappa
     wl = Workload(LA, torch, local, rank, d, W, kappa, args.streams)
-    pr, sch = wl.pr, wl.sch
-    K, L, N = pr.K, pr.L, wl.N
-    ctx, keep, bufs = wl.ctxs[0], wl.keeps[0], wl.bufs[0]
+    K, L, N = wl.pr.K, wl.pr.L, wl.N
+    dt_max, (phases, roof) = measure(LA, torch, LD, pg, world, wl, args.steps, args.warmup)
+    wl.close()
+    del wl
+    torch.cuda.empty_cache()
 
-    wl.run(args.warmup)
-    wl.sync()
-    reducer = LD.AccumulatorReducer(ctx, world, [keep["cm0"], keep["f0"]]) if world > 1 else None
-
-    ctx.kernel_timing(True)  # HIP events on the stream around every phase (lf_ctx_phase_stats)
-    LD.barrier(pg)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    wl.run(args.steps)
-    if reducer is not None:
-        reducer.reduce()  # RCCL reduce of the folded accumulators (once per timed batch)
-    torch.cuda.synchronize()
-    LD.barrier(pg)
-    dt = time.perf_counter() - t0
-    ctx.sync()  # surfaces any decomposition overflow
-    dt_max = LD.max_over_ranks(pg, dt)
-    nvec = 2 * (K - 1) + 1
-    ms_b, n_b = ctx.kernel_stats(nvec)
-    timed = {"ajtai": (ms_b, n_b)}
-    for ph in ("from_w_ccs", "decompose", "to_frag", "fold", "from_f"):
-        timed[ph] = ctx.phase_stats(ph)
-    ctx.kernel_timing(False)
-
-    step_bytes, ph_bytes = algorithmic_bytes(d, W, kappa, L, K)
-    if d == 24:
-        kernel_of = {"decompose": "k_decompose_phi72", "ajtai": "k_ajtai_mfma" if sch.layout == 1 else "k_ajtai_phi72",
-                     "fold": "k_fold_phi72", "from_w_ccs": "k_from_w_ccs_phi72", "from_f": "k_from_f_phi72",
-                     "to_frag": "k_to_frag<true, true, true>"}
-    else:
-        small = W < 4096  # kernels_n32.hip SPLIT_W: one half-wave per (element, limb)
-        kernel_of = {"decompose": "k_decompose_fused",
-                     "ajtai": "k_ajtai_mfma" if sch.layout == 1 else "k_ajtai_nega", "fold": "k_fold_nega",
-                     "from_w_ccs": "k_from_w_ccs_split" if small else "k_from_w_ccs_n32",
-                     "from_f": "k_from_f_split" if small else "k_from_f_n32", "to_frag": "k_to_frag<true, false, true>"}
-    traffic = load_traffic(d, W, kappa)
-    phases = {}
-    for ph, (ms, cnt) in timed.items():
-        if not cnt:
-            continue
-        avg = ms / cnt
-        gbs = ph_bytes[ph] / (avg * 1e-3) / 1e9
-        phases[ph] = {"kernel": kernel_of[ph], "avg_launch_ms": avg, "launches_per_step": cnt / args.steps,
-                      "ms_per_step": ms / args.steps, "algorithmic_bytes_per_launch": ph_bytes[ph],
-                      "achieved_gbs": gbs, "frac_hbm": gbs / HBM_PEAK_GBS,
-                      "traffic_bytes_per_launch": traffic.get(kernel_of[ph])}
-    dom = max(phases, key=lambda k: phases[k]["ms_per_step"]) if phases else None
+    step_bytes, _, _ = algorithmic_bytes(d, W, kappa, L, K)
     out = None
     if rank == 0:
         cpu = None
         if args.cpu and world == 1:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            cpu_w = args.cpu_w or max(1, min(W, 64 if d >= 1024 else 2048))
-            cpu = cpu_baseline(d, W, kappa, cpu_w, threads)
+            cpu = cpu_baseline(d, W, kappa)
         value = world * args.steps / dt_max
         out = {
             "metric": "fold-steps/sec (Ajtai commit+fold) at d=1024",
@@ -364,35 +482,37 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "u64 (Goldilocks mod-p integer)",
             "data": "synthetic (seeded SplitMix64 inputs, random Ajtai matrix)",
             "config": {"workload": f"commit+fold step, X^{d}+1 ring, w_ccs W={W}, N={N}, kappa={kappa}, "
-                                   f"B=2^15 L=5 K=15, 29 Ajtai products in one pass over A",
+                                   f"B=2^15 L=5 K=15, 29 Ajtai products in one pass over A; {EXCLUDED}",
                        "d": d, "W": W, "N": N, "kappa": kappa,
-                       "parallelism": f"{world} independent step streams (weak)"},
+                       "parallelism": f"{world} ranks x {args.streams} independent step streams (weak, "
+                                      f"no collective on the data path)"},
             "hbm_gbs_step_algorithmic": step_bytes * value / world / 1e9,
-            # the dominant phase by device time per step; every phase below (HIP events
-            # on the launch stream, inside the timed region)
-            "roofline": None if dom is None else {
-                "kernel": phases[dom]["kernel"], "phase": dom, "bound": "hbm",
-                "achieved": phases[dom]["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": phases[dom]["frac_hbm"], "traffic": phases[dom]["traffic_bytes_per_launch"],
-                "avg_launch_ms": phases[dom]["avg_launch_ms"],
-                "bytes_per_launch": phases[dom]["algorithmic_bytes_per_launch"]},
+            # the dominant phase by device time per step (HIP events on the launch
+            # stream, inside the timed region); bytes per SURVEY.md 8(d)
+            "roofline": roof,
             "phases": phases,
             "cpu_baseline": cpu,
         }
-    del ctx, keep, bufs, reducer, sch
-    wl.close()
-    del wl
-    torch.cuda.empty_cache()
     if args.small and args.d == 1024:
-        small = extra_shape(LA, torch, LD, pg, local, rank, world, 1024, 464, args.kappa, 4, 256, 16,
-                            "X^1024+1 ring (byte-equivalent to the real zkvm step)")
         ref = extra_shape(LA, torch, LD, pg, local, rank, world, 24, 19763, 32, 4, 128, 8,
                           "the reference ring Phi_72 = X^24 - X^12 + 1 at the real zkvm shape")
+        small = extra_shape(LA, torch, LD, pg, local, rank, world, 1024, 464, args.kappa, 4, 256, 16,
+                            "X^1024+1 ring (byte-equivalent to the real zkvm step)")
+        c4 = extra_shape(LA, torch, LD, pg, local, rank, world, 4096, 1024, 64, 1, 20, 3,
+                         "BASELINE configs[4]'s ring X^4096+1 with kappa=64")
         ops = side_ops(LA, torch, local)
         if out is not None:
-            out["small_shape"] = small
             out["reference_ring"] = ref
+            out["small_shape"] = small
+            out["configs4_d4096_kappa64"] = c4
             out["side_ops"] = ops
+    if world > 1:
+        try:
+            sh = sharded_fold(LA, torch, LD, pg, local, rank, world, d, W, kappa, 5, 2)
+        except Exception as e:  # reported, never fatal for the headline line
+            sh = {"error": f"{type(e).__name__}: {e}"}
+        if out is not None:
+            out["sharded_fold"] = sh
     if out is not None:
         print(json.dumps(out), flush=True)
     LD.finalize(pg)

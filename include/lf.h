@@ -28,6 +28,10 @@
  *   zkvm/src/main.rs:348-367  commit()                          -> lf_commit
  *   zkvm/src/main.rs:380-404  fold() (its commit+fold arithmetic) -> lf_fold_hot /
  *                                                                 lf_dev_fold_step
+ *   zkvm/src/main.rs:121-219  the proving loop, sharded over GPUs (SURVEY.md 8(b)
+ *       lf_fold_reduce_allranks; no reference analogue: rayon only)
+ *                                                              -> lf_comm_*, lf_dev_fold_step_sharded,
+ *                                                                 lf_fold_reduce_allranks
  *
  * Data: a ring element is d u64 (AoS). d = 24 is the reference's Goldilocks
  * ring Fq[X]/(X^24 - X^12 + 1); its NTT form is 8 Fq3 slots laid out
@@ -40,7 +44,9 @@
  * context stream; decomposition overflow is reported by lf_ctx_sync().
  *
  * Threading: a context is single-threaded (like the reference's &mut
- * transcript); distinct contexts may be used from distinct threads.
+ * transcript); distinct contexts may be used from distinct threads. Every
+ * call runs on its context's device and restores the calling thread's current
+ * device before it returns.
  */
 #ifndef LATTICEUM_AMD_LF_H
 #define LATTICEUM_AMD_LF_H
@@ -54,6 +60,7 @@ extern "C" {
 typedef struct lf_ctx lf_ctx;
 typedef struct lf_ajtai lf_ajtai;
 typedef struct lf_transcript lf_transcript;
+typedef struct lf_comm lf_comm;
 
 enum lf_status {
   LF_OK = 0,
@@ -66,7 +73,8 @@ enum lf_status {
   LF_ERR_INCORRECT_LENGTH = 7,        /* Decomposition/FoldingError::IncorrectLength (nifs/error.rs) */
   LF_ERR_CHALLENGE_BYTES = 8,         /* ChallengeSetError::TooFewBytes */
   LF_ERR_DEVICE = 9,                  /* HIP runtime error (see lf_ctx_last_error) */
-  LF_ERR_OUT_OF_MEMORY = 10
+  LF_ERR_OUT_OF_MEMORY = 10,
+  LF_ERR_COMM = 11                    /* RCCL error (see lf_ctx_last_error) */
 };
 enum lf_repr { LF_REPR_CANONICAL = 0, LF_REPR_MONTGOMERY = 1 };
 
@@ -114,6 +122,9 @@ enum {
   LF_PHASE_COUNT = 5
 };
 int lf_ctx_phase_stats(lf_ctx *ctx, int phase, double *total_ms, long *count);
+/* d = 1024: W below which Witness::from_w_ccs / from_f run one half-wave per
+ * (element, limb) instead of one per element (a build constant, LF_SPLIT_W) */
+size_t lf_witness_split_w(void);
 
 /* ------------------------------------------------------------ host-buffer API (synchronous) */
 int lf_crt(lf_ctx *ctx, uint64_t *elems, size_t n, int d, int repr);
@@ -130,7 +141,7 @@ void lf_ajtai_destroy(lf_ajtai *aj);
 size_t lf_ajtai_kappa(const lf_ajtai *aj);
 size_t lf_ajtai_width(const lf_ajtai *aj);
 int lf_ajtai_d(const lf_ajtai *aj);
-/* 1 when the scheme keeps A in i8-MFMA fragment order (X^d+1 rings, kappa <= 32;
+/* 1 when the scheme keeps A in i8-MFMA fragment order (X^d+1 and Phi_72 rings, kappa <= 128;
  * the AoS matrix given to lf_ajtai_create_device is then no longer read and may
  * be freed), 0 when commitments run on the VALU from the AoS matrix */
 int lf_ajtai_layout(const lf_ajtai *aj);
@@ -209,6 +220,48 @@ typedef struct {
 /* commit(z) followed by the commit+fold arithmetic of fold(), all on device */
 int lf_dev_fold_step(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, size_t W,
                      const lf_fold_step_bufs *b);
+
+/* A column-sharded step: rank r holds the columns of groups
+ * [g_r, g_r + W_r) of the witness -- its w_ccs / acc_f_coeff shards, an Ajtai
+ * scheme over A's matching columns, and shard-sized witness outputs -- plus the
+ * full acc_cm and rho. The commitments are sums over columns, so each rank's
+ * A_r f_r is a partial sum; after they are summed over ranks (mod p) every
+ * rank finishes the step with the full y / cm / cm_0 and its own shard of
+ * f_0, f_0 coefficients and w_ccs_0, bit-exact with the unsharded step.
+ *   lf_dev_fold_step_partial: commit(z) + decompositions + the 1 + 2(K-1)
+ *     partial commitments into partial[lf_fold_step_partial_len] (u64; order:
+ *     commit(z)'s cm, then y_s[k], s = 0, 1, k = 1 .. K-1)
+ *   lf_dev_fold_step_finish: given their sum over ranks, the rest of the step
+ *   lf_dev_fold_step_sharded: partial, RCCL all-reduce mod p over `comm`, finish
+ * Without an RCCL communicator (comm == NULL) the sharded step is lf_dev_fold_step. */
+size_t lf_fold_step_partial_len(const lf_ajtai *aj, const lf_params *pr);
+int lf_dev_fold_step_partial(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, size_t W,
+                             const lf_fold_step_bufs *b, uint64_t *partial);
+int lf_dev_fold_step_finish(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, size_t W,
+                            const lf_fold_step_bufs *b, const uint64_t *partial_sum);
+int lf_dev_fold_step_sharded(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, size_t W,
+                             const lf_fold_step_bufs *b, lf_comm *comm);
+
+/* ------------------------------------------------------------ communicators (RCCL over xGMI)
+ * RCCL is resolved at run time (the copy already loaded in the process, else
+ * librccl.so.1). A host creates one communicator per rank, either from a
+ * unique id that rank 0 makes and the host distributes (128 bytes), or by
+ * wrapping a caller-created ncclComm_t (not destroyed by lf_comm_destroy).
+ * lf_comm_init with id == NULL and nranks == 1 makes a communicator without
+ * RCCL (every exchange is then the identity). */
+int lf_comm_unique_id(uint8_t *id, size_t len);
+int lf_comm_init(lf_ctx *ctx, int nranks, int rank, const uint8_t *id, size_t len, lf_comm **out);
+int lf_comm_wrap(lf_ctx *ctx, void *nccl_comm, lf_comm **out);
+void lf_comm_destroy(lf_comm *comm);
+int lf_comm_size(const lf_comm *comm);
+int lf_comm_rank(const lf_comm *comm);
+/* x <- sum over ranks of x (mod p), in place, on the context stream (32-bit
+ * limbs over RCCL's u64 sum, joined mod p) */
+int lf_comm_allreduce_modp(lf_ctx *ctx, lf_comm *comm, uint64_t *x, size_t n);
+/* the accumulator exchange of independent per-rank step streams: cm_0 and f_0
+ * summed over ranks mod p, in place (SURVEY.md 8(b) lf_fold_reduce_allranks) */
+int lf_fold_reduce_allranks(lf_ctx *ctx, lf_comm *comm, uint64_t *cm0, size_t cm0_len, uint64_t *f0,
+                            size_t f0_len);
 
 int lf_dev_poseidon2_permute(lf_ctx *ctx, uint64_t *states, size_t n);
 /* synthetic inputs: element i = SplitMix64(seed, i) re-mixed until < p */

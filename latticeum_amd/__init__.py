@@ -203,11 +203,98 @@ class Context:
                       bufs: LfFoldStepBufs):
         self.check(self.lib.lf_dev_fold_step(self.h, scheme.h, C.byref(params), W, C.byref(bufs)))
 
+    def fold_step_partial_len(self, scheme: "AjtaiCommitmentScheme", params: LfParams) -> int:
+        return self.lib.lf_fold_step_partial_len(scheme.h, C.byref(params))
+
+    def dev_fold_step_partial(self, scheme, params: LfParams, W: int, bufs: LfFoldStepBufs, partial):
+        """column-sharded step, first half: partial commitments of this rank's columns (lf.h)"""
+        self.check(self.lib.lf_dev_fold_step_partial(self.h, scheme.h, C.byref(params), W, C.byref(bufs),
+                                                     _dptr(partial)))
+
+    def dev_fold_step_finish(self, scheme, params: LfParams, W: int, bufs: LfFoldStepBufs, partial_sum):
+        """column-sharded step, second half, given the partial commitments summed over ranks"""
+        self.check(self.lib.lf_dev_fold_step_finish(self.h, scheme.h, C.byref(params), W, C.byref(bufs),
+                                                    _dptr(partial_sum)))
+
+    def dev_fold_step_sharded(self, scheme, params: LfParams, W: int, bufs: LfFoldStepBufs,
+                              comm: "Communicator | None"):
+        self.check(self.lib.lf_dev_fold_step_sharded(self.h, scheme.h, C.byref(params), W, C.byref(bufs),
+                                                     comm.h if comm is not None else None))
+
+    def dev_limb_split(self, x, lo, hi):
+        self.check(self.lib.lf_dev_limb_split(self.h, _dptr(x), x.numel(), _dptr(lo), _dptr(hi)))
+
+    def dev_limb_join(self, lo, hi, out):
+        self.check(self.lib.lf_dev_limb_join(self.h, _dptr(lo), _dptr(hi), out.numel(), _dptr(out)))
+
     def dev_poseidon2_permute(self, t):
         self.check(self.lib.lf_dev_poseidon2_permute(self.h, _dptr(t), t.numel() // 16))
 
     def dev_modp_sum(self, inp, nparts: int, length: int, out):
         self.check(self.lib.lf_dev_modp_sum(self.h, _dptr(inp), nparts, length, _dptr(out)))
+
+
+class Communicator:
+    """lf_comm: an RCCL communicator of one rank, for the accumulator exchange
+    (lf.h lf_comm_*). Built from a 128-byte unique id that rank 0 creates
+    (``Communicator.unique_id()``) and the host distributes, or by wrapping a
+    caller-created ncclComm_t (``Communicator.wrap``)."""
+
+    ID_BYTES = 128
+
+    def __init__(self, ctx: Context, nranks: int, rank: int, uid: bytes | None = None, *, _handle=None):
+        self.ctx, self.lib = ctx, ctx.lib
+        if _handle is not None:
+            self.h = _handle
+        else:
+            h = C.c_void_p()
+            if uid is None:  # one rank without RCCL
+                ctx.check(self.lib.lf_comm_init(ctx.h, nranks, rank, None, 0, C.byref(h)))
+            else:
+                buf = np.frombuffer(bytes(uid), np.uint8).copy()
+                ctx.check(self.lib.lf_comm_init(ctx.h, nranks, rank, _ptr(buf), buf.size, C.byref(h)))
+            self.h = h
+        self.size = self.lib.lf_comm_size(self.h)
+        self.rank = self.lib.lf_comm_rank(self.h)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        lib = load()
+        buf = np.zeros(Communicator.ID_BYTES, np.uint8)
+        rc = lib.lf_comm_unique_id(_ptr(buf), buf.size)
+        if rc:
+            raise LfError(rc, "lf_comm_unique_id: " + lib.lf_status_string(rc).decode())
+        return buf.tobytes()
+
+    @classmethod
+    def wrap(cls, ctx: Context, nccl_comm: int) -> "Communicator":
+        h = C.c_void_p()
+        ctx.check(ctx.lib.lf_comm_wrap(ctx.h, nccl_comm, C.byref(h)))
+        return cls(ctx, 0, 0, _handle=h)
+
+    def allreduce_modp(self, t):
+        """t <- sum over ranks of t (mod p), in place on the context stream"""
+        self.ctx.check(self.lib.lf_comm_allreduce_modp(self.ctx.h, self.h, _dptr(t), t.numel()))
+
+    def fold_reduce_allranks(self, cm0, f0):
+        self.ctx.check(self.lib.lf_fold_reduce_allranks(self.ctx.h, self.h, _dptr(cm0), cm0.numel(),
+                                                        _dptr(f0), f0.numel()))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.lf_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def witness_split_w() -> int:
+    """W below which the d = 1024 witness kernels split elements by limb (lf.h)."""
+    return load().lf_witness_split_w()
 
 
 class AjtaiCommitmentScheme:
@@ -310,6 +397,7 @@ def hash_iter(vals) -> np.ndarray:
     return out
 
 
-__all__ = ["Context", "AjtaiCommitmentScheme", "Poseidon2Transcript", "LfParams", "LfFoldStepBufs",
+__all__ = ["Context", "AjtaiCommitmentScheme", "Communicator", "witness_split_w", "Poseidon2Transcript",
+           "LfParams", "LfFoldStepBufs",
            "LfError", "goldilocks_dp", "short_challenge", "hash_iter", "P", "REPR_CANONICAL",
            "REPR_MONTGOMERY", "load"]

@@ -88,6 +88,19 @@ SIGNATURES = {
     "lf_transcript_squeeze_bytes": (None, [VP, VP, SZ]),
     "lf_transcript_get_short_challenges": (I, [VP, I, SZ, VP]),
     "lf_hash_iter": (None, [VP, SZ, VP]),
+    "lf_witness_split_w": (SZ, []),
+    "lf_fold_step_partial_len": (SZ, [VP, C.POINTER(LfParams)]),
+    "lf_dev_fold_step_partial": (I, [VP, VP, C.POINTER(LfParams), SZ, C.POINTER(LfFoldStepBufs), VP]),
+    "lf_dev_fold_step_finish": (I, [VP, VP, C.POINTER(LfParams), SZ, C.POINTER(LfFoldStepBufs), VP]),
+    "lf_dev_fold_step_sharded": (I, [VP, VP, C.POINTER(LfParams), SZ, C.POINTER(LfFoldStepBufs), VP]),
+    "lf_comm_unique_id": (I, [VP, SZ]),
+    "lf_comm_init": (I, [VP, I, I, VP, SZ, C.POINTER(VP)]),
+    "lf_comm_wrap": (I, [VP, VP, C.POINTER(VP)]),
+    "lf_comm_destroy": (None, [VP]),
+    "lf_comm_size": (I, [VP]),
+    "lf_comm_rank": (I, [VP]),
+    "lf_comm_allreduce_modp": (I, [VP, VP, VP, SZ]),
+    "lf_fold_reduce_allranks": (I, [VP, VP, VP, SZ, VP, SZ]),
 }
 
 _lib = None

@@ -172,21 +172,29 @@ __device__ __forceinline__ int fl_pi(int j, int i) { return i ^ (((j & 7) << 1) 
 
 // CPOL: cache policy of the operand copies (2 = nt: streaming, for operands far
 // larger than the caches -- A and F are each read once per launch)
+// kappa > 32: A is stored as 32-row tiles (tile_u4 uint4 each), and one wave
+// contracts one tile; the tiles of one (slot quad, split) are the blocks
+// i + 8 t of a group of 8 ktiles blocks. Blocks are dealt round-robin over the
+// 8 XCDs, so those blocks run on the same XCD at about the same time and the
+// second tile's F copies hit that XCD's L2 instead of HBM.
 template <int CPOL>
 __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const uint4 *Ff, int d, int nch,
                                                       int nvec, int kappa, uint64_t *partial, OutPtrs dst,
-                                                      int direct, int cps) {
+                                                      int direct, int cps, int ktiles, int nbase, size_t tile_u4) {
   __shared__ uint4 Al[2][4][8 * 64];  // 64 KiB: A copies one chunk ahead
   __shared__ uint4 Fl[3][32 * 64];    // 96 KiB: F copies two chunks ahead
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int gw = blockIdx.x * 4 + w;
+  const int grp = blockIdx.x / (8 * ktiles), rem = blockIdx.x - grp * 8 * ktiles;
+  const int kt = rem >> 3, bi = grp * 8 + (rem & 7);
+  if (bi >= nbase) return;  // uniform over the block
+  const int gw = bi * 4 + w;
   const int s = gw % d, js = gw / d;  // d % 4 == 0: one split per block, slots 4i .. 4i + 3
   if (js >= (nch + cps - 1) / cps) return;  // uniform over the block
   const int c0 = js * cps, c1 = min(nch, c0 + cps);
   v16i acc[15];
 #pragma unroll
   for (int t = 0; t < 15; t++) acc[t] = (v16i){0};
-  const uint4 *pa = Af + ((size_t)s * nch * 8) * 64 + lane;
+  const uint4 *pa = Af + kt * tile_u4 + ((size_t)s * nch * 8) * 64 + lane;
   const uint4 *ft = Ff + (size_t)(s >> 2) * nch * FV_CHUNK;  // (s/4, chunk 0) tile
   auto stage_a = [&](int c, int buf) {
 #pragma unroll
@@ -280,7 +288,7 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const ui
 #pragma unroll
     for (int t = 0; t < 15; t++) S[t >> 2] += (int64_t)x[t] << (8 * (t & 3));
     const uint64_t r = gl::add(fe(S[0] - S[2] - S[3]), gl::mul_pow2(fe(S[1] + S[2]), 32));
-    const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+    const int row = 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * h;
     if (v < nvec && row < kappa) {
       if (direct)  // one column split: the result itself
         dst.p[v][(size_t)row * d + s] = r;
@@ -312,6 +320,7 @@ __global__ void k_phi72_interp(const uint64_t *virt, int nvec, size_t kappa, Out
 
 // ---------------------------------------------------------------- launchers
 size_t frag_elems(const FragGeom &g, int d) { return (size_t)mfma_dim(d) * g.nch * 8 * 64; }  // uint4 per buffer
+int mfma_ktiles(size_t kappa) { return (int)((kappa + 31) / 32); }
 // chunks per column split: AJ_CPS for wide rings; for few virtual slots (Phi_72)
 // enough splits that about 2048 waves run
 int mfma_cps(const FragGeom &g, int d) {
@@ -370,7 +379,9 @@ hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, c
                       bool f_ready, uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st, hipEvent_t ev0,
                       hipEvent_t ev1, const OutPtrs *dst) {
   const int dv = mfma_dim(d);
-  if (kappa > 32 || nvec < 1 || nvec > 32 || dv % 4 || (!cm && !dst)) return hipErrorInvalidValue;
+  const int ktiles = mfma_ktiles(kappa);
+  if (kappa < 1 || ktiles > LF_MAX_KTILES || nvec < 1 || nvec > 32 || dv % 4 || (!cm && !dst))
+    return hipErrorInvalidValue;
   OutPtrs out{};
   for (int v = 0; v < nvec; v++) out.p[v] = cm ? cm + (size_t)v * kappa * d : dst->p[v];
   if (!f_ready) {
@@ -387,14 +398,16 @@ hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, c
   }
   if (ev0) (void)hipEventRecord(ev0, st);
   const size_t waves = (size_t)dv * nsplit;
-  const dim3 grid((unsigned)((waves + 3) / 4));
+  const int nbase = (int)((waves + 3) / 4);
+  const dim3 grid((unsigned)((nbase + 7) / 8 * 8 * ktiles));
+  const size_t tile_u4 = frag_elems(g, d);
   // F is dv nch 8 KiB per launch (A is as large for kappa = 32)
   if ((size_t)dv * g.nch * 8192 > STREAM_OUT_BYTES)
     hipLaunchKernelGGL(k_ajtai_mfma<2>, grid, dim3(256), 0, st, Af, Ff, dv, g.nch, nvec, (int)kappa, partial, kout,
-                       nsplit == 1 ? 1 : 0, cps);
+                       nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4);
   else
     hipLaunchKernelGGL(k_ajtai_mfma<0>, grid, dim3(256), 0, st, Af, Ff, dv, g.nch, nvec, (int)kappa, partial, kout,
-                       nsplit == 1 ? 1 : 0, cps);
+                       nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (ev1) (void)hipEventRecord(ev1, st);

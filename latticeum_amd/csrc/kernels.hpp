@@ -7,6 +7,7 @@
 #include "ring.hpp"
 
 #define LF_MAX_VECS 32
+#define LF_MAX_KTILES 4
 
 namespace lfk {
 
@@ -60,7 +61,9 @@ hipError_t sum_planes_to(const uint64_t *partial, int nsplit, size_t len, int nv
 hipError_t y0_cm0(const uint64_t *cm0s, const uint64_t *cm1s, uint64_t *y0, uint64_t *y1, const uint64_t *rho,
                   size_t kappa, int d, int lbs, int K, uint64_t *cm0, hipStream_t st);
 
-// i8-MFMA Ajtai (ajtai_mfma.hip): negacyclic rings, kappa <= 32, nvec <= 32.
+// i8-MFMA Ajtai (ajtai_mfma.hip): negacyclic rings and Phi_72, nvec <= 32,
+// kappa <= 32 LF_MAX_KTILES: A is stored as mfma_ktiles(kappa) tiles of 32 rows,
+// frag_elems() uint4 each.
 // Column (contraction) order: 16-column units u = (u / Lp, u % Lp) = limb l of
 // groups 16G..16G+15; nch 32-column chunks.
 struct FragGeom {
@@ -71,7 +74,8 @@ struct FragGeom {
 FragGeom frag_geom(size_t ncols, int Lp);
 // d = 24 (Phi_72) contracts 40 virtual slots per element (Toom-3, ajtai_mfma.hip)
 int mfma_dim(int d);
-size_t frag_elems(const FragGeom &g, int d);  // uint4 per fragment buffer
+size_t frag_elems(const FragGeom &g, int d);  // uint4 per fragment buffer (32 operand rows)
+int mfma_ktiles(size_t kappa);
 int mfma_nsplit(const FragGeom &g, int d);
 // u64 of scratch ajtai_mfma needs (split partial sums, Phi_72 virtual-slot results)
 size_t mfma_scratch_elems(const FragGeom &g, int d, size_t kappa, int nvec);
@@ -83,6 +87,8 @@ hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, c
                       hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, const OutPtrs *dst = nullptr);
 
 // d = 1024 kernels on the register-resident 32 x 32 NTT (kernels_n32.hip)
+// W below which from_w_ccs / from_f run one half-wave per (element, limb)
+size_t witness_split_w();
 hipError_t transform_n32(uint64_t *data, size_t n, bool fwd, const ring::NegaTables &tb, hipStream_t st);
 hipError_t from_w_ccs_n32(const uint64_t *w_ccs, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *f,
                           const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err, hipStream_t st);
@@ -101,7 +107,9 @@ struct FusedSides {
   int row0[2];
   int nside;
 };
+// sink: an 8 KiB device scratch row (stores of groups past W); ncu: the device's CU count
 hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K, uint32_t *smg,
-                           const ring::NegaTables &fwd, uint4 *frag, int nch, int *err, hipStream_t st);
+                           const ring::NegaTables &fwd, uint4 *frag, int nch, int *err, uint64_t *sink, int ncu,
+                           hipStream_t st);
 
 }  // namespace lfk

@@ -541,20 +541,12 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_
 
 // ---------------------------------------------------------------- launchers
 hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K, uint32_t *smg,
-                           const ring::NegaTables &fwd, uint4 *frag, int nch, int *err, hipStream_t st) {
-  // 8 KiB target for the row stores of groups past W (one half-wave's 1024 u64)
-  static uint64_t *sink = nullptr;
-  if (!sink && hipMalloc(&sink, D * sizeof(uint64_t)) != hipSuccess) return hipErrorOutOfMemory;
-  if (K > 15 || !fwd.mid || sd.nside < 1 || sd.nside > 2) return hipErrorInvalidValue;
+                           const ring::NegaTables &fwd, uint4 *frag, int nch, int *err, uint64_t *sink, int ncu,
+                           hipStream_t st) {
+  if (K > 15 || !fwd.mid || !sink || ncu < 1 || sd.nside < 1 || sd.nside > 2) return hipErrorInvalidValue;
   const size_t words = sd.nside * N * 512;
   hipLaunchKernelGGL(k_pack_sm, dim3((unsigned)((words / 4 + 255) / 256)), dim3(256), 0, st, sd, N, K, smg, err);
   // one 8-wave block per CU (LDS-bound); ntask = nblk K tasks spread evenly
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
-      ncu = 256;
-  }
   const size_t ntask = (N / L + 15) / 16 * (size_t)K * sd.nside;
   // every block takes the same number of tasks (no tail round on part of the
   // chip); the CUs left over run other streams' kernels
@@ -588,6 +580,7 @@ hipError_t transform_n32(uint64_t *data, size_t n, bool fwd, const ring::NegaTab
 #define LF_SPLIT_W 4096
 #endif
 constexpr size_t SPLIT_W = LF_SPLIT_W;
+size_t witness_split_w() { return SPLIT_W; }
 hipError_t from_w_ccs_n32(const uint64_t *w_ccs, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *f,
                           const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err, hipStream_t st) {
   if (W < SPLIT_W) {

@@ -2,11 +2,14 @@
 // tables, host-buffer wrappers, the device-resident commit+fold step, and the
 // host-side transcript. No CPU compute fallback exists: every ring/commit/fold
 // operation runs on the GPU, and creating a context fails loudly without one.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types only: the RCCL entry points are resolved at run time (rccl())
 
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <memory>
 #include <string>
@@ -44,21 +47,51 @@ struct lf_ctx {
   size_t frag_elems = 0;
   uint32_t *smg = nullptr;      // packed coefficients for the fused decomposition
   size_t smg_elems = 0;
+  uint64_t *sink = nullptr;     // 8 KiB row the fused decomposition stores groups past W into
+  int ncu = 0;                  // compute units of `device`
+  uint64_t *stage = nullptr;    // sharded step: the partial commitments [nvec][kappa d]
+  size_t stage_elems = 0;
+  uint64_t *limb = nullptr;     // RCCL transport: [lo | hi] 32-bit limbs of a field vector
+  size_t limb_elems = 0;
   bool timing = false;
   std::vector<TimedLaunch> pending;
   std::map<int, std::pair<double, long>> stats;  // nvec -> (ms, count)
 };
 
 struct lf_ajtai {
+  int device = 0;
   const uint64_t *A = nullptr;
-  uint4 *Af = nullptr;  // A in i8-MFMA fragment order (negacyclic rings, kappa <= 32)
+  uint4 *Af = nullptr;  // A in i8-MFMA fragment order, mfma_ktiles(kappa) tiles of 32 rows
   lfk::FragGeom geom{};  // contraction order of the fragments (ajtai_mfma.hip)
   bool owned = false;
   size_t kappa = 0, ncols = 0;
   int d = 0;
 };
 
+// a communicator for the accumulator exchange (RCCL over xGMI)
+struct lf_comm {
+  ncclComm_t comm = nullptr;
+  bool owned = false;
+  int nranks = 1, rank = 0;
+};
+
 namespace {
+
+// Every entry point runs on its context's device and restores the caller's
+// current device afterwards, so contexts on different GPUs can be used from
+// one thread (lf.h threading contract).
+struct DevGuard {
+  int prev = -1;
+  explicit DevGuard(int dev) {
+    int cur = -1;
+    if (dev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess) prev = cur;
+  }
+  explicit DevGuard(const lf_ctx *c);
+  ~DevGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+DevGuard::DevGuard(const lf_ctx *c) : DevGuard(c ? c->device : -1) {}
 
 int fail(lf_ctx *c, int code, const std::string &msg) {
   if (c) c->last_error = msg;
@@ -168,7 +201,7 @@ int reserve(lf_ctx *c, size_t elems) { return grow(c, c->scratch, c->scratch_ele
 
 bool use_mfma(int d, size_t kappa) {
   const char *sel = getenv("LATTICEUM_AMD_AJTAI");
-  return (d == 24 || d % 16 == 0) && kappa <= 32 && !(sel && strcmp(sel, "valu") == 0);
+  return (d == 24 || d % 16 == 0) && lfk::mfma_ktiles(kappa) <= LF_MAX_KTILES && !(sel && strcmp(sel, "valu") == 0);
 }
 
 // RAII device buffer for the synchronous host API
@@ -232,15 +265,19 @@ int ajtai_launch(lf_ctx *c, const lf_ajtai *aj, const uint64_t *const *vecs, int
   return LF_OK;
 }
 
-// build the MFMA fragment copy of A (scheme creation)
+// build the MFMA fragment copy of A (scheme creation): 32-row tiles
 int ajtai_prepare(lf_ctx *c, lf_ajtai *aj) {
   if (!use_mfma(aj->d, aj->kappa)) return LF_OK;
   aj->geom = ajtai_geom(aj->ncols);
   const size_t n = lfk::frag_elems(aj->geom, aj->d);
-  LF_HIP(c, hipMalloc((void **)&aj->Af, n * sizeof(uint4)));
-  lfk::VecPtrs rows{};
-  for (size_t i = 0; i < aj->kappa; i++) rows.p[i] = aj->A + i * aj->ncols * aj->d;
-  LF_HIP(c, lfk::to_frag(rows, (int)aj->kappa, 0, aj->geom, aj->d, false, aj->Af, c->cur));
+  const int ktiles = lfk::mfma_ktiles(aj->kappa);
+  LF_HIP(c, hipMalloc((void **)&aj->Af, n * ktiles * sizeof(uint4)));
+  for (int t = 0; t < ktiles; t++) {
+    lfk::VecPtrs rows{};
+    const int r0 = 32 * t, nr = (int)std::min<size_t>(32, aj->kappa - r0);
+    for (int i = 0; i < nr; i++) rows.p[i] = aj->A + (size_t)(r0 + i) * aj->ncols * aj->d;
+    LF_HIP(c, lfk::to_frag(rows, nr, 0, aj->geom, aj->d, false, aj->Af + n * t, c->cur));
+  }
   LF_HIP(c, hipStreamSynchronize(c->cur));
   return LF_OK;
 }
@@ -282,131 +319,182 @@ struct PhaseTimer {
   }
 };
 
-int fold_core(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lbs, size_t W,
-              const lf_fold_step_bufs *b, const uint64_t *cm_i, const uint64_t *wi_f_coeff,
-              const uint64_t *commit_f = nullptr, uint64_t *commit_cm = nullptr) {
+// The commit+fold arithmetic of fold() on device buffers, in two halves so a
+// column-sharded step can all-reduce the commitments between them:
+//  fold_commit: decompose_witness of both sides (decomposition.rs:162-167) and
+//    the 2(K-1) commitments of commit_witnesses (:178-201), plus -- when
+//    `commit_f` is given (the device step) -- commit(z)'s A.f in the same pass
+//    over A (29 vectors, one read of A). Result v goes to dst[v]: commit(z)'s
+//    cm first, then y_s[k], s = 0, 1, k = 1 .. K-1.
+//  fold_finish: y_0 = cm - sum b^k y_k of both sides, cm_0 = sum rho_i y_i,
+//    f_0 = sum rho_i f_i (folding.rs:258-268, folding/utils.rs:470-476) and
+//    Witness::from_f(f_0) (arith.rs:299-313).
+int fold_nvec(const lf_params *pr, bool commit_f) { return (commit_f ? 1 : 0) + 2 * (pr->K - 1); }
+
+int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lbs, size_t W,
+                const lf_fold_step_bufs *b, const uint64_t *wi_f_coeff, const uint64_t *commit_f,
+                const lfk::OutPtrs &dst) {
   const int d = pr->d, L = pr->L, K = pr->K;
   const size_t N = W * (size_t)L, kappa = aj->kappa;
-  if (2 * K > LF_MAX_VECS || 2 * (K - 1) + (commit_f ? 1 : 0) > LF_MAX_VECS)
-    return fail(c, LF_ERR_INVALID_ARG, "2K must be <= 32");
+  const int extra = commit_f ? 1 : 0, nvec = fold_nvec(pr, commit_f != nullptr);
+  if (2 * K > LF_MAX_VECS || nvec > LF_MAX_VECS) return fail(c, LF_ERR_INVALID_ARG, "2K must be <= 32");
   if (aj->ncols != N) return fail(c, LF_ERR_WRONG_WITNESS_LENGTH, "witness length != Ajtai width");
   Tables *t;
   LF_TRY(get_tables(c, d, t));
-  // decompose_witness for both sides (decomposition.rs:162-167)
   const uint64_t *fc_side[2] = {b->acc_f_coeff, wi_f_coeff};
-  const int extra = commit_f ? 1 : 0;
-  const int nvec = extra + 2 * (K - 1);
   const size_t kd = kappa * (size_t)d;
-  LF_TRY(grow(c, c->ybuf, c->ybuf_elems, (size_t)nvec * kd));
-  uint64_t *ycat = c->ybuf;
   // fused path (d = 1024, b_small = 2, fragment order grouped by this L): the
   // decomposition writes its digit planes straight into the MFMA operand buffer
   const bool fused = aj->Af && aj->geom.Lp == L && d == 1024 && lbs == 1 && K <= 15 && t->fwd.mid;
   // Phi_72 (d = 24): each side's decomposition writes its planes as operand rows (kernels.hip)
   const bool fused24 = aj->Af && aj->geom.Lp == L && d == 24 && L <= 5;
-  if (fused24) {
-    LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->geom, d)));
-    for (int s = 0; s < 2; s++) {
-      PhaseTimer pt(c, LF_PHASE_DECOMPOSE);
-      LF_HIP(c, lfk::decompose_witness(fc_side[s], N, d, lb, L, lbs, K, b->fk_coeff[s], b->fk[s], b->wk[s], t->fwd,
-                                       c->d_err, c->cur, c->frag, aj->geom.nch, extra + s * (K - 1)));
-    }
-    lfk::VecPtrs vp{};
-    if (commit_f) {
-      PhaseTimer pt(c, LF_PHASE_TO_FRAG);
-      vp.p[0] = commit_f;
-      LF_HIP(c, lfk::to_frag(vp, 1, 0, aj->geom, d, true, c->frag, c->cur));
-    }
-    LF_TRY(reserve(c, partial_elems(aj, nvec)));
-    hipEvent_t ea = nullptr, eb = nullptr;
-    if (c->timing) {
-      LF_HIP(c, hipEventCreate(&ea));
-      LF_HIP(c, hipEventCreate(&eb));
-    }
-    lfk::OutPtrs dst{};
-    if (commit_f) dst.p[0] = commit_cm;
-    for (int s = 0; s < 2; s++)
-      for (int k = 1; k < K; k++) dst.p[extra + s * (K - 1) + k - 1] = b->y[s] + (size_t)k * kd;
-    LF_HIP(c, lfk::ajtai_mfma(aj->Af, kappa, aj->geom, d, vp, nvec, true, c->frag, c->scratch, nullptr, c->cur, ea,
-                              eb, &dst));
-    if (c->timing) c->pending.push_back({ea, eb, nvec});
-  } else if (fused) {
-    LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->geom, d)));
-    LF_TRY(grow(c, c->smg, c->smg_elems, 2 * N * 512));
-    lfk::FusedSides sd{};
-    sd.nside = 2;
-    for (int s = 0; s < 2; s++) {
-      sd.f_coeff[s] = fc_side[s];
-      sd.f_coeff_k[s] = b->fk_coeff[s];
-      sd.f_k[s] = b->fk[s];
-      sd.w_ccs_k[s] = b->wk[s];
-      sd.row0[s] = extra + s * (K - 1);
-    }
-    {  // both sides in one launch
-      PhaseTimer pt(c, LF_PHASE_DECOMPOSE);
-      LF_HIP(c, lfk::decompose_fused(sd, N, lb, L, K, c->smg, t->fwd, c->frag, aj->geom.nch, c->d_err, c->cur));
-    }
-    lfk::VecPtrs vp{};
-    if (commit_f) {
-      PhaseTimer pt(c, LF_PHASE_TO_FRAG);
-      vp.p[0] = commit_f;
-      LF_HIP(c, lfk::to_frag(vp, 1, 0, aj->geom, d, true, c->frag, c->cur));
-    }
-    LF_TRY(reserve(c, partial_elems(aj, nvec)));
-    hipEvent_t ea = nullptr, eb = nullptr;
-    if (c->timing) {
-      LF_HIP(c, hipEventCreate(&ea));
-      LF_HIP(c, hipEventCreate(&eb));
-    }
-    // results straight to their places: commit(z)'s cm, then y_s[1..K-1]
-    lfk::OutPtrs dst{};
-    if (commit_f) dst.p[0] = commit_cm;
-    for (int s = 0; s < 2; s++)
-      for (int k = 1; k < K; k++) dst.p[extra + s * (K - 1) + k - 1] = b->y[s] + (size_t)k * kd;
-    LF_HIP(c, lfk::ajtai_mfma(aj->Af, kappa, aj->geom, d, vp, nvec, true, c->frag, c->scratch, nullptr, c->cur, ea,
-                              eb, &dst));
-    if (c->timing) c->pending.push_back({ea, eb, nvec});
-  } else {
-    for (int s = 0; s < 2; s++) {
-      PhaseTimer pt(c, LF_PHASE_DECOMPOSE);
-      LF_HIP(c, lfk::decompose_witness(fc_side[s], N, d, lb, L, lbs, K, b->fk_coeff[s], b->fk[s], b->wk[s],
-                                       t->fwd, c->d_err, c->cur));
-    }
-    // commit_witnesses: 2(K-1) commitments sharing one pass over A (decomposition.rs:185-188)
-    std::vector<const uint64_t *> vecs;
-    if (commit_f) vecs.push_back(commit_f);
-    for (int s = 0; s < 2; s++)
-      for (int k = 1; k < K; k++) vecs.push_back(b->fk[s] + (size_t)k * N * d);
-    LF_TRY(ajtai_launch(c, aj, vecs.data(), (int)vecs.size(), ycat));
-  }
-  if (commit_f) cm_i = commit_cm;
-  const uint64_t *cm_side[2] = {b->acc_cm, cm_i};
   if (fused || fused24) {
-    // y_0 of both sides and cm_0 = sum rho_i y_i in one pass (the y_s[k >= 1] are in place)
-    LF_HIP(c, lfk::y0_cm0(cm_side[0], cm_side[1], b->y[0], b->y[1], b->rho, kappa, d, lbs, K, b->cm0, c->cur));
-  } else {
-    if (commit_f) LF_HIP(c, hipMemcpyAsync(commit_cm, ycat, kd * 8, hipMemcpyDeviceToDevice, c->cur));
-    for (int s = 0; s < 2; s++) {
-      LF_HIP(c, hipMemcpyAsync(b->y[s] + kd, ycat + (extra + (size_t)s * (K - 1)) * kd, (size_t)(K - 1) * kd * 8,
-                               hipMemcpyDeviceToDevice, c->cur));
-      LF_HIP(c, lfk::commit_y0(cm_side[s], b->y[s], kappa, d, lbs, K, c->cur));
+    LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->geom, d)));
+    if (fused) {
+      LF_TRY(grow(c, c->smg, c->smg_elems, 2 * N * 512));
+      lfk::FusedSides sd{};
+      sd.nside = 2;
+      for (int s = 0; s < 2; s++) {
+        sd.f_coeff[s] = fc_side[s];
+        sd.f_coeff_k[s] = b->fk_coeff[s];
+        sd.f_k[s] = b->fk[s];
+        sd.w_ccs_k[s] = b->wk[s];
+        sd.row0[s] = extra + s * (K - 1);
+      }
+      PhaseTimer pt(c, LF_PHASE_DECOMPOSE);  // both sides in one launch
+      LF_HIP(c, lfk::decompose_fused(sd, N, lb, L, K, c->smg, t->fwd, c->frag, aj->geom.nch, c->d_err, c->sink,
+                                     c->ncu, c->cur));
+    } else {
+      for (int s = 0; s < 2; s++) {
+        PhaseTimer pt(c, LF_PHASE_DECOMPOSE);
+        LF_HIP(c, lfk::decompose_witness(fc_side[s], N, d, lb, L, lbs, K, b->fk_coeff[s], b->fk[s], b->wk[s],
+                                         t->fwd, c->d_err, c->cur, c->frag, aj->geom.nch, extra + s * (K - 1)));
+      }
     }
+    lfk::VecPtrs vp{};
+    if (commit_f) {
+      PhaseTimer pt(c, LF_PHASE_TO_FRAG);
+      vp.p[0] = commit_f;
+      LF_HIP(c, lfk::to_frag(vp, 1, 0, aj->geom, d, true, c->frag, c->cur));
+    }
+    LF_TRY(reserve(c, partial_elems(aj, nvec)));
+    hipEvent_t ea = nullptr, eb = nullptr;
+    if (c->timing) {
+      LF_HIP(c, hipEventCreate(&ea));
+      LF_HIP(c, hipEventCreate(&eb));
+    }
+    LF_HIP(c, lfk::ajtai_mfma(aj->Af, kappa, aj->geom, d, vp, nvec, true, c->frag, c->scratch, nullptr, c->cur, ea,
+                              eb, &dst));
+    if (c->timing) c->pending.push_back({ea, eb, nvec});
+    return LF_OK;
   }
-  // f_0 = sum rho_i f_i, cm_0 = sum rho_i y_i   (folding.rs:258-268, folding/utils.rs:470-476)
-  lfk::VecPtrs fx{}, yx{};
+  for (int s = 0; s < 2; s++) {
+    PhaseTimer pt(c, LF_PHASE_DECOMPOSE);
+    LF_HIP(c, lfk::decompose_witness(fc_side[s], N, d, lb, L, lbs, K, b->fk_coeff[s], b->fk[s], b->wk[s], t->fwd,
+                                     c->d_err, c->cur));
+  }
+  // commit_witnesses: 2(K-1) commitments sharing one pass over A (decomposition.rs:185-188)
+  std::vector<const uint64_t *> vecs;
+  if (commit_f) vecs.push_back(commit_f);
   for (int s = 0; s < 2; s++)
-    for (int k = 0; k < K; k++) {
-      fx.p[s * K + k] = b->fk[s] + (size_t)k * N * d;
-      yx.p[s * K + k] = b->y[s] + (size_t)k * kd;
-    }
+    for (int k = 1; k < K; k++) vecs.push_back(b->fk[s] + (size_t)k * N * d);
+  LF_TRY(grow(c, c->ybuf, c->ybuf_elems, (size_t)nvec * kd));
+  LF_TRY(ajtai_launch(c, aj, vecs.data(), nvec, c->ybuf));
+  for (int v = 0; v < nvec; v++)
+    if (dst.p[v] != c->ybuf + v * kd)
+      LF_HIP(c, hipMemcpyAsync(dst.p[v], c->ybuf + v * kd, kd * 8, hipMemcpyDeviceToDevice, c->cur));
+  return LF_OK;
+}
+
+// destinations of fold_commit's results in the step buffers
+lfk::OutPtrs fold_dst(const lf_params *pr, const lf_fold_step_bufs *b, size_t kd, uint64_t *commit_cm) {
+  lfk::OutPtrs dst{};
+  const int extra = commit_cm ? 1 : 0;
+  if (commit_cm) dst.p[0] = commit_cm;
+  for (int s = 0; s < 2; s++)
+    for (int k = 1; k < pr->K; k++) dst.p[extra + s * (pr->K - 1) + k - 1] = b->y[s] + (size_t)k * kd;
+  return dst;
+}
+
+int fold_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lbs, size_t W,
+                const lf_fold_step_bufs *b, const uint64_t *cm_i) {
+  const int d = pr->d, L = pr->L, K = pr->K;
+  const size_t N = W * (size_t)L, kappa = aj->kappa;
+  Tables *t;
+  LF_TRY(get_tables(c, d, t));
+  // y_0 of both sides and cm_0 = sum rho_i y_i in one pass (the y_s[k >= 1] are in place)
+  LF_HIP(c, lfk::y0_cm0(b->acc_cm, cm_i, b->y[0], b->y[1], b->rho, kappa, d, lbs, K, b->cm0, c->cur));
+  lfk::VecPtrs fx{};
+  for (int s = 0; s < 2; s++)
+    for (int k = 0; k < K; k++) fx.p[s * K + k] = b->fk[s] + (size_t)k * N * d;
   {
     PhaseTimer pt(c, LF_PHASE_FOLD);
     LF_HIP(c, lfk::fold(b->rho, fx, 2 * K, N, d, b->f0, c->cur));
   }
-  if (!fused && !fused24) LF_HIP(c, lfk::fold(b->rho, yx, 2 * K, kappa, d, b->cm0, c->cur));
-  // Witness::from_f(f_0) (arith.rs:299-313)
   PhaseTimer pt(c, LF_PHASE_FROM_F);
   LF_HIP(c, lfk::from_f(b->f0, N, d, lb, L, b->f0_coeff, b->w_ccs0, t->inv, c->cur));
+  return LF_OK;
+}
+
+// ---------------------------------------------------------------- RCCL (resolved at run time)
+// The library does not link RCCL: the entry points are looked up in the RCCL
+// already loaded into the process (torch's, whose communicators a caller may
+// hand over through lf_comm_wrap) or else in librccl.so.1.
+struct Rccl {
+  bool ok = false;
+  std::string err;
+  ncclResult_t (*getUniqueId)(ncclUniqueId *) = nullptr;
+  ncclResult_t (*commInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*commCount)(const ncclComm_t, int *) = nullptr;
+  ncclResult_t (*commUserRank)(const ncclComm_t, int *) = nullptr;
+  ncclResult_t (*allReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                            hipStream_t) = nullptr;
+  const char *(*errorString)(ncclResult_t) = nullptr;
+};
+const Rccl &rccl() {
+  static const Rccl r = [] {
+    Rccl x;
+    void *h = nullptr;
+    for (const char *name : {"librccl.so.1", "librccl.so"})
+      if (!h) h = dlopen(name, RTLD_NOW | RTLD_NOLOAD);
+    for (const char *name : {"librccl.so.1", "librccl.so"})
+      if (!h) h = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+      x.err = "RCCL (librccl.so.1) not found";
+      return x;
+    }
+    x.getUniqueId = (decltype(x.getUniqueId))dlsym(h, "ncclGetUniqueId");
+    x.commInitRank = (decltype(x.commInitRank))dlsym(h, "ncclCommInitRank");
+    x.commDestroy = (decltype(x.commDestroy))dlsym(h, "ncclCommDestroy");
+    x.commCount = (decltype(x.commCount))dlsym(h, "ncclCommCount");
+    x.commUserRank = (decltype(x.commUserRank))dlsym(h, "ncclCommUserRank");
+    x.allReduce = (decltype(x.allReduce))dlsym(h, "ncclAllReduce");
+    x.errorString = (decltype(x.errorString))dlsym(h, "ncclGetErrorString");
+    x.ok = x.getUniqueId && x.commInitRank && x.commDestroy && x.commCount && x.commUserRank && x.allReduce &&
+           x.errorString;
+    if (!x.ok) x.err = "RCCL entry points missing";
+    return x;
+  }();
+  return r;
+}
+#define LF_NCCL(ctx, call)                                                                       \
+  do {                                                                                          \
+    ncclResult_t r_ = (call);                                                                    \
+    if (r_ != ncclSuccess)                                                                       \
+      return fail((ctx), LF_ERR_COMM, std::string(#call) + ": " + rccl().errorString(r_));       \
+  } while (0)
+
+// x <- sum over the communicator's ranks of x, mod p, on the context stream:
+// RCCL's integer sum is mod 2^64, so the vector travels as 32-bit limbs
+// (exact for < 2^32 ranks) and is folded back into the field afterwards
+int allreduce_modp(lf_ctx *c, lf_comm *cm, uint64_t *x, size_t n) {
+  if (!cm || !cm->comm || !n) return LF_OK;  // one rank without a communicator: the sum is x
+  if (!rccl().ok) return fail(c, LF_ERR_COMM, rccl().err);
+  LF_TRY(grow(c, c->limb, c->limb_elems, 2 * n));
+  LF_HIP(c, lfk::limb_split(x, n, c->limb, c->limb + n, c->cur));
+  LF_NCCL(c, rccl().allReduce(c->limb, c->limb, 2 * n, ncclUint64, ncclSum, cm->comm, c->cur));
+  LF_HIP(c, lfk::limb_join(c->limb, c->limb + n, n, x, c->cur));
   return LF_OK;
 }
 
@@ -437,6 +525,7 @@ const char *lf_status_string(int s) {
     case LF_ERR_CHALLENGE_BYTES: return "wrong number of challenge bytes";
     case LF_ERR_DEVICE: return "HIP device error";
     case LF_ERR_OUT_OF_MEMORY: return "out of device memory";
+    case LF_ERR_COMM: return "RCCL communicator error";
   }
   return "unknown status";
 }
@@ -451,18 +540,21 @@ int lf_ctx_create(int device, lf_ctx **out) {
   }
   auto c = std::make_unique<lf_ctx>();
   c->device = device;
-  if (hipSetDevice(device) != hipSuccess) return LF_ERR_DEVICE;
+  DevGuard g(device);
   if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) return LF_ERR_DEVICE;
   c->cur = c->own;
   if (hipMalloc(&c->d_err, sizeof(int)) != hipSuccess) return LF_ERR_OUT_OF_MEMORY;
   if (hipMemset(c->d_err, 0, sizeof(int)) != hipSuccess) return LF_ERR_DEVICE;
+  if (hipMalloc(&c->sink, 1024 * sizeof(uint64_t)) != hipSuccess) return LF_ERR_OUT_OF_MEMORY;
+  if (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c->ncu < 1)
+    return LF_ERR_DEVICE;
   *out = c.release();
   return LF_OK;
 }
 
 void lf_ctx_destroy(lf_ctx *c) {
   if (!c) return;
-  (void)hipSetDevice(c->device);
+  DevGuard g(c);
   (void)hipStreamSynchronize(c->cur);
   for (auto &t : c->pending) {
     (void)hipEventDestroy(t.a);
@@ -474,12 +566,17 @@ void lf_ctx_destroy(lf_ctx *c) {
   if (c->ybuf) (void)hipFree(c->ybuf);
   if (c->frag) (void)hipFree(c->frag);
   if (c->smg) (void)hipFree(c->smg);
+  if (c->sink) (void)hipFree(c->sink);
+  if (c->stage) (void)hipFree(c->stage);
+  if (c->limb) (void)hipFree(c->limb);
   if (c->d_err) (void)hipFree(c->d_err);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
 }
 
 const char *lf_ctx_last_error(const lf_ctx *c) { return c ? c->last_error.c_str() : ""; }
+
+size_t lf_witness_split_w(void) { return lfk::witness_split_w(); }
 
 int lf_ctx_set_stream(lf_ctx *c, void *s) {
   if (!c) return LF_ERR_INVALID_ARG;
@@ -489,6 +586,7 @@ int lf_ctx_set_stream(lf_ctx *c, void *s) {
 void *lf_ctx_get_stream(const lf_ctx *c) { return c ? (void *)c->cur : nullptr; }
 
 int lf_ctx_sync(lf_ctx *c) {
+  DevGuard g(c);
   if (!c) return LF_ERR_INVALID_ARG;
   LF_HIP(c, hipStreamSynchronize(c->cur));
   int e = 0;
@@ -501,6 +599,7 @@ int lf_ctx_sync(lf_ctx *c) {
 }
 
 int lf_ctx_reserve(lf_ctx *c, size_t kappa, size_t ncols, int d, int nvec) {
+  DevGuard g(c);
   if (!c || !ring_ok(d) || nvec < 1 || nvec > LF_MAX_VECS) return LF_ERR_INVALID_ARG;
   Tables *t;
   LF_TRY(get_tables(c, d, t));
@@ -518,6 +617,7 @@ int lf_ctx_reserve(lf_ctx *c, size_t kappa, size_t ncols, int d, int nvec) {
 }
 
 int lf_ctx_kernel_timing(lf_ctx *c, int enable) {
+  DevGuard g(c);
   if (!c) return LF_ERR_INVALID_ARG;
   LF_TRY(drain_timing(c));
   c->timing = enable != 0;
@@ -526,6 +626,7 @@ int lf_ctx_kernel_timing(lf_ctx *c, int enable) {
 }
 
 int lf_ctx_phase_stats(lf_ctx *c, int phase, double *ms, long *count) {
+  DevGuard g(c);
   if (!c || !ms || !count || phase < 0 || phase >= LF_PHASE_COUNT) return LF_ERR_INVALID_ARG;
   LF_TRY(drain_timing(c));
   auto it = c->stats.find(-1 - phase);
@@ -535,6 +636,7 @@ int lf_ctx_phase_stats(lf_ctx *c, int phase, double *ms, long *count) {
 }
 
 int lf_ctx_kernel_stats(lf_ctx *c, int nvec, double *ms, long *count) {
+  DevGuard g(c);
   if (!c || !ms || !count) return LF_ERR_INVALID_ARG;
   LF_TRY(drain_timing(c));
   *ms = 0;
@@ -549,6 +651,7 @@ int lf_ctx_kernel_stats(lf_ctx *c, int nvec, double *ms, long *count) {
 
 // ---------------------------------------------------------------- host-buffer API
 static int xform_host(lf_ctx *c, uint64_t *e, size_t n, int d, int repr, bool fwd) {
+  DevGuard g(c);
   if (!c || (!e && n)) return LF_ERR_INVALID_ARG;
   LF_TRY(check_repr(c, repr));
   if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
@@ -564,6 +667,7 @@ int lf_crt(lf_ctx *c, uint64_t *e, size_t n, int d, int repr) { return xform_hos
 int lf_icrt(lf_ctx *c, uint64_t *e, size_t n, int d, int repr) { return xform_host(c, e, n, d, repr, false); }
 
 int lf_ring_mul(lf_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t n, int d, int repr) {
+  DevGuard g(c);
   if (!c || ((!a || !b || !out) && n)) return LF_ERR_INVALID_ARG;
   LF_TRY(check_repr(c, repr));
   if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
@@ -578,6 +682,7 @@ int lf_ring_mul(lf_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, 
 
 int lf_ajtai_create(lf_ctx *c, const uint64_t *A, size_t kappa, size_t ncols, int d, int repr,
                     lf_ajtai **out) {
+  DevGuard g(c);
   if (!c || !A || !out || !kappa || !ncols) return LF_ERR_INVALID_ARG;
   LF_TRY(check_repr(c, repr));
   if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
@@ -585,6 +690,7 @@ int lf_ajtai_create(lf_ctx *c, const uint64_t *A, size_t kappa, size_t ncols, in
   LF_TRY(upload(c, b, A, kappa * ncols * d, repr));
   LF_TRY(lf_ctx_sync(c));
   auto *aj = new lf_ajtai;
+  aj->device = c->device;
   aj->A = b.p;
   b.p = nullptr;
   aj->owned = true;
@@ -602,9 +708,11 @@ int lf_ajtai_create(lf_ctx *c, const uint64_t *A, size_t kappa, size_t ncols, in
 
 int lf_ajtai_create_device(lf_ctx *c, const uint64_t *A_dev, size_t kappa, size_t ncols, int d,
                            lf_ajtai **out) {
+  DevGuard g(c);
   if (!c || !A_dev || !out || !kappa || !ncols) return LF_ERR_INVALID_ARG;
   if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
   auto *aj = new lf_ajtai;
+  aj->device = c->device;
   aj->A = A_dev;
   aj->kappa = kappa;
   aj->ncols = ncols;
@@ -620,6 +728,7 @@ int lf_ajtai_create_device(lf_ctx *c, const uint64_t *A_dev, size_t kappa, size_
 
 void lf_ajtai_destroy(lf_ajtai *aj) {
   if (!aj) return;
+  DevGuard g(aj->device);
   if (aj->owned) (void)hipFree((void *)aj->A);
   if (aj->Af) (void)hipFree(aj->Af);
   delete aj;
@@ -630,6 +739,7 @@ int lf_ajtai_d(const lf_ajtai *aj) { return aj ? aj->d : 0; }
 int lf_ajtai_layout(const lf_ajtai *aj) { return aj && aj->Af ? 1 : 0; }
 
 int lf_ajtai_commit(lf_ctx *c, const lf_ajtai *aj, const uint64_t *f, size_t f_len, uint64_t *cm, int repr) {
+  DevGuard g(c);
   if (!c || !aj || !f || !cm) return LF_ERR_INVALID_ARG;
   LF_TRY(check_repr(c, repr));
   if (f_len != aj->ncols)  // commitment_scheme.rs:38-43
@@ -645,6 +755,7 @@ int lf_ajtai_commit(lf_ctx *c, const lf_ajtai *aj, const uint64_t *f, size_t f_l
 
 int lf_witness_from_w_ccs(lf_ctx *c, const lf_params *pr, const uint64_t *w, size_t W, uint64_t *fc,
                           uint64_t *f, int repr) {
+  DevGuard g(c);
   if (!c || (!w && W) || !fc || !f) return LF_ERR_INVALID_ARG;
   LF_TRY(check_repr(c, repr));
   int lb, lbs;
@@ -663,6 +774,7 @@ int lf_witness_from_w_ccs(lf_ctx *c, const lf_params *pr, const uint64_t *w, siz
 
 int lf_witness_from_f(lf_ctx *c, const lf_params *pr, const uint64_t *f, size_t N, uint64_t *fc,
                       uint64_t *w, int repr) {
+  DevGuard g(c);
   if (!c || (!f && N) || !fc || !w) return LF_ERR_INVALID_ARG;
   LF_TRY(check_repr(c, repr));
   int lb, lbs;
@@ -681,6 +793,7 @@ int lf_witness_from_f(lf_ctx *c, const lf_params *pr, const uint64_t *f, size_t 
 
 int lf_decompose_witness(lf_ctx *c, const lf_params *pr, const uint64_t *fc, size_t N, uint64_t *fck,
                          uint64_t *fk, uint64_t *wk, int repr) {
+  DevGuard g(c);
   if (!c || (!fc && N) || !fck || !fk || !wk) return LF_ERR_INVALID_ARG;
   LF_TRY(check_repr(c, repr));
   int lb, lbs;
@@ -701,6 +814,7 @@ int lf_decompose_witness(lf_ctx *c, const lf_params *pr, const uint64_t *fc, siz
 
 int lf_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, const uint64_t *z, size_t z_len, size_t l,
               uint64_t *fc, uint64_t *f, uint64_t *cm, int repr) {
+  DevGuard g(c);
   if (!c || !aj || !z || !fc || !f || !cm) return LF_ERR_INVALID_ARG;
   LF_TRY(check_repr(c, repr));
   int lb, lbs;
@@ -728,6 +842,7 @@ int lf_fold_hot(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, const uint64
                 const uint64_t *acc_fc, const uint64_t *cm_i, const uint64_t *wi_fc, size_t N,
                 const uint64_t *rho, uint64_t *y, uint64_t *f0, uint64_t *f0c, uint64_t *w0, uint64_t *cm0,
                 int repr) {
+  DevGuard g(c);
   if (!c || !aj || !acc_cm || !acc_fc || !cm_i || !wi_fc || !rho || !y || !f0 || !f0c || !w0 || !cm0)
     return LF_ERR_INVALID_ARG;
   LF_TRY(check_repr(c, repr));
@@ -767,7 +882,8 @@ int lf_fold_hot(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, const uint64
   b.f0_coeff = df0c.p;
   b.w_ccs0 = dw0.p;
   b.cm0 = dcm0.p;
-  LF_TRY(fold_core(c, aj, pr, lb, lbs, W, &b, dcmi.p, dwfc.p));
+  LF_TRY(fold_commit(c, aj, pr, lb, lbs, W, &b, dwfc.p, nullptr, fold_dst(pr, &b, kd, nullptr)));
+  LF_TRY(fold_finish(c, aj, pr, lb, lbs, W, &b, dcmi.p));
   LF_TRY(download(c, y, dy, 2 * K * kd, repr));
   LF_TRY(download(c, f0, df0, N * d, repr));
   LF_TRY(download(c, f0c, df0c, N * d, repr));
@@ -792,6 +908,7 @@ int lf_short_challenge(const uint8_t *bs, size_t nbytes, int d, uint64_t *coeffs
 }
 
 int lf_poseidon2_permute(lf_ctx *c, uint64_t *states, size_t n) {
+  DevGuard g(c);
   if (!c || (!states && n)) return LF_ERR_INVALID_ARG;
   DevBuf b;
   LF_TRY(upload(c, b, states, 16 * n, LF_REPR_CANONICAL));
@@ -802,6 +919,7 @@ int lf_poseidon2_permute(lf_ctx *c, uint64_t *states, size_t n) {
 
 // ---------------------------------------------------------------- device API
 int lf_dev_crt(lf_ctx *c, uint64_t *e, size_t n, int d) {
+  DevGuard g(c);
   if (!c || (!e && n)) return LF_ERR_INVALID_ARG;
   if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
   Tables *t;
@@ -810,6 +928,7 @@ int lf_dev_crt(lf_ctx *c, uint64_t *e, size_t n, int d) {
   return LF_OK;
 }
 int lf_dev_icrt(lf_ctx *c, uint64_t *e, size_t n, int d) {
+  DevGuard g(c);
   if (!c || (!e && n)) return LF_ERR_INVALID_ARG;
   if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
   Tables *t;
@@ -818,23 +937,27 @@ int lf_dev_icrt(lf_ctx *c, uint64_t *e, size_t n, int d) {
   return LF_OK;
 }
 int lf_dev_ring_mul(lf_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t n, int d) {
+  DevGuard g(c);
   if (!c) return LF_ERR_INVALID_ARG;
   if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
   LF_HIP(c, lfk::slot_mul(a, b, out, n, d, c->cur));
   return LF_OK;
 }
 int lf_dev_to_montgomery(lf_ctx *c, uint64_t *x, size_t n) {
+  DevGuard g(c);
   if (!c) return LF_ERR_INVALID_ARG;
   LF_HIP(c, lfk::mont(x, n, true, c->cur));
   return LF_OK;
 }
 int lf_dev_from_montgomery(lf_ctx *c, uint64_t *x, size_t n) {
+  DevGuard g(c);
   if (!c) return LF_ERR_INVALID_ARG;
   LF_HIP(c, lfk::mont(x, n, false, c->cur));
   return LF_OK;
 }
 int lf_dev_witness_from_w_ccs(lf_ctx *c, const lf_params *pr, const uint64_t *w, size_t W, uint64_t *fc,
                               uint64_t *f) {
+  DevGuard g(c);
   if (!c) return LF_ERR_INVALID_ARG;
   int lb, lbs;
   LF_TRY(check_params(c, pr, lb, lbs));
@@ -845,6 +968,7 @@ int lf_dev_witness_from_w_ccs(lf_ctx *c, const lf_params *pr, const uint64_t *w,
 }
 int lf_dev_witness_from_f(lf_ctx *c, const lf_params *pr, const uint64_t *f, size_t N, uint64_t *fc,
                           uint64_t *w) {
+  DevGuard g(c);
   if (!c) return LF_ERR_INVALID_ARG;
   int lb, lbs;
   LF_TRY(check_params(c, pr, lb, lbs));
@@ -856,6 +980,7 @@ int lf_dev_witness_from_f(lf_ctx *c, const lf_params *pr, const uint64_t *f, siz
 }
 int lf_dev_decompose_witness(lf_ctx *c, const lf_params *pr, const uint64_t *fc, size_t N, uint64_t *fck,
                              uint64_t *fk, uint64_t *wk) {
+  DevGuard g(c);
   if (!c) return LF_ERR_INVALID_ARG;
   int lb, lbs;
   LF_TRY(check_params(c, pr, lb, lbs));
@@ -866,10 +991,12 @@ int lf_dev_decompose_witness(lf_ctx *c, const lf_params *pr, const uint64_t *fc,
   return LF_OK;
 }
 int lf_dev_ajtai_commit(lf_ctx *c, const lf_ajtai *aj, const uint64_t *const *vecs, int nvec, uint64_t *cm) {
+  DevGuard g(c);
   if (!c || !aj || !vecs || !cm) return LF_ERR_INVALID_ARG;
   return ajtai_launch(c, aj, vecs, nvec, cm);
 }
 int lf_dev_commit_y0(lf_ctx *c, const lf_params *pr, const uint64_t *cm, uint64_t *y, size_t kappa) {
+  DevGuard g(c);
   if (!c) return LF_ERR_INVALID_ARG;
   int lb, lbs;
   LF_TRY(check_params(c, pr, lb, lbs));
@@ -878,6 +1005,7 @@ int lf_dev_commit_y0(lf_ctx *c, const lf_params *pr, const uint64_t *cm, uint64_
 }
 int lf_dev_fold(lf_ctx *c, int d, const uint64_t *rho, const uint64_t *const *x, int nwit, size_t n,
                 uint64_t *out) {
+  DevGuard g(c);
   if (!c || !rho || !x || !out || nwit < 1 || nwit > LF_MAX_VECS) return LF_ERR_INVALID_ARG;
   if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
   lfk::VecPtrs vp{};
@@ -886,43 +1014,165 @@ int lf_dev_fold(lf_ctx *c, int d, const uint64_t *rho, const uint64_t *const *x,
   return LF_OK;
 }
 
-int lf_dev_fold_step(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t W, const lf_fold_step_bufs *b) {
+// commit(z) (zkvm main.rs:348-367): Witness::from_w_ccs; its A f is batched
+// with the decomposition commitments of fold() in a single pass over A
+static int step_check(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t W, const lf_fold_step_bufs *b,
+                      int &lb, int &lbs) {
   if (!c || !aj || !b) return LF_ERR_INVALID_ARG;
-  int lb, lbs;
   LF_TRY(check_params(c, pr, lb, lbs));
   if (pr->d != aj->d) return fail(c, LF_ERR_INVALID_ARG, "params ring != Ajtai ring");
   if (W * (size_t)pr->L != aj->ncols) return fail(c, LF_ERR_WRONG_WITNESS_LENGTH, "W*L != Ajtai width");
-  // commit(z) (zkvm main.rs:348-367): Witness::from_w_ccs; its A f is batched
-  // with the decomposition commitments of fold() in a single pass over A
+  return LF_OK;
+}
+static int step_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t W, const lf_fold_step_bufs *b,
+                       int lb, int lbs, const lfk::OutPtrs &dst) {
   {
     PhaseTimer pt(c, LF_PHASE_FROM_W_CCS);
     LF_TRY(lf_dev_witness_from_w_ccs(c, pr, b->w_ccs, W, b->f_coeff, b->f));
   }
-  return fold_core(c, aj, pr, lb, lbs, W, b, b->cm, b->f_coeff, b->f, b->cm);
+  return fold_commit(c, aj, pr, lb, lbs, W, b, b->f_coeff, b->f, dst);
+}
+
+int lf_dev_fold_step(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t W, const lf_fold_step_bufs *b) {
+  DevGuard g(c);
+  int lb, lbs;
+  LF_TRY(step_check(c, aj, pr, W, b, lb, lbs));
+  LF_TRY(step_commit(c, aj, pr, W, b, lb, lbs, fold_dst(pr, b, aj->kappa * (size_t)pr->d, b->cm)));
+  return fold_finish(c, aj, pr, lb, lbs, W, b, b->cm);
+}
+
+size_t lf_fold_step_partial_len(const lf_ajtai *aj, const lf_params *pr) {
+  return aj && pr ? (size_t)fold_nvec(pr, true) * aj->kappa * pr->d : 0;
+}
+
+int lf_dev_fold_step_partial(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t W,
+                             const lf_fold_step_bufs *b, uint64_t *partial) {
+  DevGuard g(c);
+  int lb, lbs;
+  LF_TRY(step_check(c, aj, pr, W, b, lb, lbs));
+  if (!partial) return fail(c, LF_ERR_INVALID_ARG, "null partial buffer");
+  const size_t kd = aj->kappa * (size_t)pr->d;
+  lfk::OutPtrs dst{};
+  for (int v = 0; v < fold_nvec(pr, true); v++) dst.p[v] = partial + v * kd;
+  return step_commit(c, aj, pr, W, b, lb, lbs, dst);
+}
+
+int lf_dev_fold_step_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t W,
+                            const lf_fold_step_bufs *b, const uint64_t *partial_sum) {
+  DevGuard g(c);
+  int lb, lbs;
+  LF_TRY(step_check(c, aj, pr, W, b, lb, lbs));
+  if (!partial_sum) return fail(c, LF_ERR_INVALID_ARG, "null partial sum");
+  const size_t kd = aj->kappa * (size_t)pr->d;
+  const lfk::OutPtrs dst = fold_dst(pr, b, kd, b->cm);
+  for (int v = 0; v < fold_nvec(pr, true); v++)
+    LF_HIP(c, hipMemcpyAsync(dst.p[v], partial_sum + v * kd, kd * 8, hipMemcpyDeviceToDevice, c->cur));
+  return fold_finish(c, aj, pr, lb, lbs, W, b, b->cm);
+}
+
+int lf_dev_fold_step_sharded(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t W,
+                             const lf_fold_step_bufs *b, lf_comm *cm) {
+  DevGuard g(c);
+  int lb, lbs;
+  LF_TRY(step_check(c, aj, pr, W, b, lb, lbs));
+  if (!cm || !cm->comm) return lf_dev_fold_step(c, aj, pr, W, b);
+  const size_t len = lf_fold_step_partial_len(aj, pr);
+  LF_TRY(grow(c, c->stage, c->stage_elems, len));
+  LF_TRY(lf_dev_fold_step_partial(c, aj, pr, W, b, c->stage));
+  LF_TRY(allreduce_modp(c, cm, c->stage, len));
+  return lf_dev_fold_step_finish(c, aj, pr, W, b, c->stage);
+}
+
+// ---------------------------------------------------------------- communicators
+int lf_comm_unique_id(uint8_t *id, size_t len) {
+  if (!id || len != NCCL_UNIQUE_ID_BYTES) return LF_ERR_INVALID_ARG;
+  if (!rccl().ok) return LF_ERR_COMM;
+  ncclUniqueId u;
+  if (rccl().getUniqueId(&u) != ncclSuccess) return LF_ERR_COMM;
+  memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+  return LF_OK;
+}
+
+int lf_comm_init(lf_ctx *c, int nranks, int rank, const uint8_t *id, size_t len, lf_comm **out) {
+  if (!c || !out || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !id) ||
+      (id && len != NCCL_UNIQUE_ID_BYTES))
+    return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  *out = nullptr;
+  auto cm = std::make_unique<lf_comm>();
+  cm->nranks = nranks;
+  cm->rank = rank;
+  if (id) {  // one rank with an id still makes a (trivial) RCCL communicator
+    if (!rccl().ok) return fail(c, LF_ERR_COMM, rccl().err);
+    ncclUniqueId u;
+    memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+    LF_NCCL(c, rccl().commInitRank(&cm->comm, nranks, u, rank));
+    cm->owned = true;
+  }
+  *out = cm.release();
+  return LF_OK;
+}
+
+int lf_comm_wrap(lf_ctx *c, void *nccl_comm, lf_comm **out) {
+  if (!c || !nccl_comm || !out) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  if (!rccl().ok) return fail(c, LF_ERR_COMM, rccl().err);
+  auto cm = std::make_unique<lf_comm>();
+  cm->comm = (ncclComm_t)nccl_comm;
+  LF_NCCL(c, rccl().commCount(cm->comm, &cm->nranks));
+  LF_NCCL(c, rccl().commUserRank(cm->comm, &cm->rank));
+  *out = cm.release();
+  return LF_OK;
+}
+
+void lf_comm_destroy(lf_comm *cm) {
+  if (!cm) return;
+  if (cm->owned && cm->comm && rccl().ok) (void)rccl().commDestroy(cm->comm);
+  delete cm;
+}
+int lf_comm_size(const lf_comm *cm) { return cm ? cm->nranks : 0; }
+int lf_comm_rank(const lf_comm *cm) { return cm ? cm->rank : -1; }
+
+int lf_comm_allreduce_modp(lf_ctx *c, lf_comm *cm, uint64_t *x, size_t n) {
+  if (!c || !cm || (!x && n)) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  return allreduce_modp(c, cm, x, n);
+}
+
+int lf_fold_reduce_allranks(lf_ctx *c, lf_comm *cm, uint64_t *cm0, size_t cm0_len, uint64_t *f0, size_t f0_len) {
+  if (!c || !cm) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  LF_TRY(allreduce_modp(c, cm, cm0, cm0_len));
+  return allreduce_modp(c, cm, f0, f0_len);
 }
 
 int lf_dev_poseidon2_permute(lf_ctx *c, uint64_t *states, size_t n) {
+  DevGuard g(c);
   if (!c) return LF_ERR_INVALID_ARG;
   LF_HIP(c, lfk::p2_permute(states, n, c->cur));
   return LF_OK;
 }
 int lf_dev_fill_uniform(lf_ctx *c, uint64_t *out, size_t n, uint64_t seed) {
+  DevGuard g(c);
   if (!c) return LF_ERR_INVALID_ARG;
   LF_HIP(c, lfk::fill_uniform(out, n, seed, c->cur));
   return LF_OK;
 }
 int lf_dev_modp_sum(lf_ctx *c, const uint64_t *in, int nparts, size_t len, uint64_t *out) {
+  DevGuard g(c);
   if (!c || nparts < 1) return LF_ERR_INVALID_ARG;
   LF_HIP(c, lfk::modp_sum(in, nparts, len, out, c->cur));
   return LF_OK;
 }
 
 int lf_dev_limb_split(lf_ctx *c, const uint64_t *x, size_t n, uint64_t *lo, uint64_t *hi) {
+  DevGuard g(c);
   if (!c) return LF_ERR_INVALID_ARG;
   LF_HIP(c, lfk::limb_split(x, n, lo, hi, c->cur));
   return LF_OK;
 }
 int lf_dev_limb_join(lf_ctx *c, const uint64_t *lo, const uint64_t *hi, size_t n, uint64_t *out) {
+  DevGuard g(c);
   if (!c) return LF_ERR_INVALID_ARG;
   LF_HIP(c, lfk::limb_join(lo, hi, n, out, c->cur));
   return LF_OK;

@@ -1,16 +1,25 @@
-"""Multi-GPU plumbing: one process per GPU, torch.distributed over RCCL (xGMI).
+"""Multi-GPU plumbing: one process per GPU, torch.distributed for rendezvous and
+timing, RCCL over xGMI (through the C ABI's lf_comm) for the field exchange.
 
-The commit+fold steps of different trace-step witnesses are independent, so
-ranks run their own step streams (weak scaling) with no collective in the
-data path. The one exchange step is the reduce of the ranks' folded
-accumulators (cm_0, f_0) -- BASELINE.json configs[3]. RCCL's integer SUM is
-mod 2^64, not mod p = 2^64 - 2^32 + 1, so field vectors travel as 32-bit limbs
-(all-reduced as int64, exact for <= 2^31 ranks) and are folded back into the
-field by a HIP kernel (lf_dev_limb_join).
+Two ways to spread the commit+fold path over the GPUs of a node:
+
+* independent step streams (BASELINE.json configs[3], the trace-batch shard):
+  every rank folds its own trace-step witnesses. Steps never exchange data,
+  so there is no collective on the data path (weak scaling); the ranks'
+  folded accumulators can be summed once with ``AccumulatorReducer``
+  (lf_fold_reduce_allranks).
+* one fold sharded by columns: rank r owns the witness
+  columns of groups ``shard_groups(W, r, world)`` and the matching columns of
+  the Ajtai matrix. The commitments are sums over columns, so each rank's are
+  partial sums; one RCCL all-reduce (mod p) of the 1 + 2(K-1) kappa-element
+  commitments per step completes them (lf_dev_fold_step_sharded). f_0 and
+  Witness::from_f(f_0) are column-local and stay sharded.
+
+RCCL's integer SUM is mod 2^64, not mod p = 2^64 - 2^32 + 1, so field vectors
+travel as 32-bit limbs and are folded back into the field by a HIP kernel; the
+whole exchange (split, all-reduce, join) is ordered on the context's stream.
 """
 from __future__ import annotations
-
-import ctypes as C
 
 import torch
 import torch.distributed as dist
@@ -44,45 +53,53 @@ def finalize(pg):
         dist.destroy_process_group()
 
 
-class HipLimbOps:
-    """limb split / join on the GPU through the C ABI (the product path)."""
+def make_comm(ctx, pg, world: int, rank: int):
+    """The lf communicator of this rank: rank 0 makes the RCCL unique id and
+    torch.distributed carries it to the others (a Rust host would use its own
+    channel). None for a single rank."""
+    if world <= 1:
+        return None
+    from . import Communicator
+    obj = [Communicator.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=pg)
+    return Communicator(ctx, world, rank, obj[0])
 
-    def __init__(self, ctx):
-        self.ctx = ctx
 
-    def split(self, x, lo, hi):
-        self.ctx.check(self.ctx.lib.lf_dev_limb_split(self.ctx.h, x.data_ptr(), x.numel(),
-                                                      lo.data_ptr(), hi.data_ptr()))
-
-    def join(self, lo, hi, out):
-        self.ctx.check(self.ctx.lib.lf_dev_limb_join(self.ctx.h, lo.data_ptr(), hi.data_ptr(),
-                                                     out.numel(), out.data_ptr()))
+def shard_groups(W: int, rank: int, world: int, align: int = 16):
+    """[g0, g1): the groups (of L witness columns) rank owns in a column-sharded
+    fold. Shards are contiguous and, except the last, multiples of `align`
+    groups (the fused decomposition's and the MFMA contraction's 16-group unit),
+    so every rank's operand layout is the unsharded one restricted to its
+    columns."""
+    units = (W + align - 1) // align
+    lo = units * rank // world
+    hi = units * (rank + 1) // world
+    return min(W, lo * align), min(W, hi * align)
 
 
 class AccumulatorReducer:
-    """In-place  t <- sum over ranks of t  (mod p)  for each field vector t."""
+    """In place, t <- sum over ranks of t (mod p) for each field vector t, over
+    the C ABI's RCCL communicator on the context stream (independent step
+    streams: the ranks' folded accumulators cm_0 and f_0)."""
 
-    def __init__(self, ops, world: int, tensors, group=None):
-        if not isinstance(ops, (HipLimbOps,)) and hasattr(ops, "check"):  # a Context
-            ops = HipLimbOps(ops)
-        self.ops, self.world, self.group = ops, world, group
+    def __init__(self, comm, tensors):
+        self.comm = comm
         self.tensors = list(tensors)
-        self.lo = [torch.empty_like(t) for t in self.tensors]
-        self.hi = [torch.empty_like(t) for t in self.tensors]
 
     def reduce(self):
-        if self.world <= 1:
+        if self.comm is None or self.comm.size <= 1:
             return
-        for t, lo, hi in zip(self.tensors, self.lo, self.hi):
-            self.ops.split(t, lo, hi)
-            dist.all_reduce(lo, op=dist.ReduceOp.SUM, group=self.group)
-            dist.all_reduce(hi, op=dist.ReduceOp.SUM, group=self.group)
-            self.ops.join(lo, hi, t)
+        if len(self.tensors) == 2:
+            self.comm.fold_reduce_allranks(*self.tensors)
+        else:
+            for t in self.tensors:
+                self.comm.allreduce_modp(t)
 
 
 def shard(n_units: int, rank: int, world: int):
-    """unit indices owned by `rank` (round-robin by step index, SURVEY.md §8e C4)."""
+    """unit indices owned by `rank` (round-robin by step index, SURVEY.md 8e C4)."""
     return list(range(rank, n_units, world))
 
 
-__all__ = ["init", "barrier", "max_over_ranks", "finalize", "HipLimbOps", "AccumulatorReducer", "shard", "C"]
+__all__ = ["init", "barrier", "max_over_ranks", "finalize", "make_comm", "shard_groups", "AccumulatorReducer",
+           "shard"]

@@ -669,3 +669,55 @@ void lfo_fill_uniform(uint64_t *out, size_t n, uint64_t seed) {
     out[i] = x;
   }
 }
+
+static uint64_t uniform_at(uint64_t seed, uint64_t i) { /* element i of lfo_fill_uniform(seed) */
+  const uint64_t G = 0x9e3779b97f4a7c15ull;
+  uint64_t x = mix64(seed + (i + 1) * G);
+  while (x >= P) x = mix64(x + G);
+  return x;
+}
+
+/* Ajtai rows of a matrix that exists only as lfo_fill_uniform(seed) of
+ * kappa x ncols x d (row-major, as bench.py / the device fill make it): the
+ * same product as lfo_ajtai_commit (LA/matrix.rs:168-178), with A generated on
+ * the fly, so rows of a 21.5 GB matrix can be checked without a host copy. */
+typedef struct {
+  uint64_t seed;
+  size_t ncols, nchunk;
+  int d;
+  const uint64_t *f;
+  const size_t *rows;
+  uint64_t *part; /* [nrows][nchunk][d] */
+} seeded_arg;
+static void seeded_range(void *p, size_t lo, size_t hi) {
+  seeded_arg *a = p;
+  const int d = a->d;
+  uint64_t *e = malloc(sizeof(uint64_t) * (size_t)d);
+  for (size_t job = lo; job < hi; job++) {
+    const size_t ri = job / a->nchunk, ch = job % a->nchunk, row = a->rows[ri];
+    const size_t j0 = a->ncols * ch / a->nchunk, j1 = a->ncols * (ch + 1) / a->nchunk;
+    uint64_t *acc = a->part + job * (size_t)d;
+    memset(acc, 0, sizeof(uint64_t) * (size_t)d);
+    for (size_t j = j0; j < j1; j++) {
+      const uint64_t base = ((uint64_t)row * a->ncols + j) * (uint64_t)d;
+      for (int c = 0; c < d; c++) e[c] = uniform_at(a->seed, base + c);
+      slot_mul_acc(e, a->f + j * (size_t)d, acc, d);
+    }
+  }
+  free(e);
+}
+void lfo_ajtai_rows_seeded(uint64_t seed, size_t ncols, int d, const uint64_t *f, const size_t *rows,
+                           size_t nrows, uint64_t *cm, int nthreads) {
+  pthread_once(&once, init_consts);
+  const size_t nchunk = (size_t)(nthreads > 0 ? nthreads : 1) * 4;
+  uint64_t *part = malloc(sizeof(uint64_t) * nrows * nchunk * (size_t)d);
+  seeded_arg a = {seed, ncols, nchunk, d, f, rows, part};
+  parallel_for(nrows * nchunk, nthreads, seeded_range, &a);
+  for (size_t r = 0; r < nrows; r++)
+    for (int c = 0; c < d; c++) {
+      uint64_t v = 0;
+      for (size_t ch = 0; ch < nchunk; ch++) v = lfo_add(v, part[(r * nchunk + ch) * (size_t)d + c]);
+      cm[r * (size_t)d + c] = v;
+    }
+  free(part);
+}

@@ -124,6 +124,10 @@ void lfo_tr_squeeze_bytes(lfo_transcript *t, uint8_t *out, size_t n);
 
 /* ---- seeded synthetic inputs: SplitMix64 stream, rejection to [0,p) ---- */
 void lfo_fill_uniform(uint64_t *out, size_t n, uint64_t seed);
+/* rows[0..nrows) of A f for A = lfo_fill_uniform(seed) as kappa x ncols x d
+ * (generated on the fly, never stored): cm [nrows][d] */
+void lfo_ajtai_rows_seeded(uint64_t seed, size_t ncols, int d, const uint64_t *f, const size_t *rows,
+                           size_t nrows, uint64_t *cm, int nthreads);
 
 #ifdef __cplusplus
 }

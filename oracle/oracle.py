@@ -73,6 +73,7 @@ def lib():
         "lfo_tr_get_challenge": (None, [C.POINTER(Transcript), u64p]),
         "lfo_tr_squeeze_bytes": (None, [C.POINTER(Transcript), u8p, SZ]),
         "lfo_fill_uniform": (None, [u64p, SZ, U64]),
+        "lfo_ajtai_rows_seeded": (None, [U64, SZ, I, u64p, u64p, SZ, u64p, I]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -87,7 +88,8 @@ def _u64(a) -> np.ndarray:
 
 
 def nthreads_default() -> int:
-    return int(os.environ.get("LF_ORACLE_THREADS", os.cpu_count() or 1))
+    # os.cpu_count() is the whole machine on the GPU box; its CPU share is 16
+    return int(os.environ.get("LF_ORACLE_THREADS", min(16, os.cpu_count() or 1)))
 
 
 # ---------------------------------------------------------------- ring ops
@@ -242,6 +244,14 @@ def new_transcript() -> Transcript:
 def fill_uniform(n: int, seed: int) -> np.ndarray:
     out = np.zeros(n, np.uint64)
     lib().lfo_fill_uniform(out, n, seed)
+    return out
+
+
+def ajtai_rows_seeded(seed: int, ncols: int, d: int, f, rows, nthreads: int | None = None) -> np.ndarray:
+    """rows of A f with A = fill_uniform(kappa * ncols * d, seed) generated on the fly"""
+    r = np.ascontiguousarray(np.asarray(rows, dtype=np.uint64))
+    out = np.zeros(r.size * d, np.uint64)
+    lib().lfo_ajtai_rows_seeded(seed, ncols, d, _u64(f), r, r.size, out, nthreads or nthreads_default())
     return out
 
 
