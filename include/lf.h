@@ -19,6 +19,9 @@
  *                                                                 lf_dev_commit_y0
  *   latticefold/src/nifs/folding.rs:258-268, folding/utils.rs:456-517
  *       compute_f_0 / cm_0                                     -> lf_dev_fold
+ *       compute_v0_u0_x0_cm_0: u_0, x_0, v_0                   -> lf_fold_lcccs / lf_dev_fold_lcccs
+ *   cyclotomic-rings/src/rotation.rs:84-101 rot_lin_combination -> lf_fold_lcccs (v_0)
+ *   latticefold/src/nifs/decomposition.rs:172-175 compute_x_s  -> lf_compute_x_s / lf_dev_compute_x_s
  *   cyclotomic-rings/src/rings/goldilocks.rs:41-67
  *       short_challenge_from_random_bytes                      -> lf_short_challenge
  *   zkvm/src/poseidon2.rs:100-235
@@ -173,6 +176,21 @@ int lf_fold_hot(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, const uint
                 const uint64_t *rho, uint64_t *y, uint64_t *f0, uint64_t *f0_coeff, uint64_t *w_ccs0,
                 uint64_t *cm0, int repr);
 
+/* The rest of the folded LCCCS (compute_v0_u0_x0_cm_0, folding/utils.rs:456-517),
+ * given the folding sumcheck's outputs (theta_s, eta_s) and rho:
+ *   u0 = sum_i rho_i (.) eta_i           (t NTT elements; eta: [nwit][t])
+ *   x0 = sum_i rho_i (.) (x_w || h)_i     (l1 = l + 1 elements; xwh: [nwit][l1])
+ *   v0 = rot_lin_combination(rho_coeff, theta): rho_coeff [nwit][d] coefficient
+ *        form, theta [nwit][tau] NTT elements, v0 tau elements (tau = 3 for
+ *        d = 24, whose base ring is Fq3; 1 for X^d + 1)
+ * t = 0 / l1 = 0 / theta = NULL skip that output. nwit <= 32. */
+int lf_fold_lcccs(lf_ctx *ctx, int d, int nwit, const uint64_t *rho, const uint64_t *rho_coeff, const uint64_t *eta,
+                  size_t t, const uint64_t *xwh, size_t l1, const uint64_t *theta, uint64_t *u0, uint64_t *x0,
+                  uint64_t *v0, int repr);
+/* compute_x_s: x = x_w || h (m NTT elements) -> x_s [K][m], the K decomposed
+ * statements (decompose_big_vec_into_k_vec_and_compose_back) */
+int lf_compute_x_s(lf_ctx *ctx, const lf_params *pr, const uint64_t *x, size_t m, uint64_t *x_s, int repr);
+
 /* short_challenge_from_random_bytes: 3d/4 bytes -> d coefficients in [-32, 32) */
 int lf_short_challenge(const uint8_t *bytes, size_t nbytes, int d, uint64_t *coeffs);
 /* width-16 Poseidon2 permutation of n independent states (16 canonical u64 each) */
@@ -262,6 +280,11 @@ int lf_comm_allreduce_modp(lf_ctx *ctx, lf_comm *comm, uint64_t *x, size_t n);
  * summed over ranks mod p, in place (SURVEY.md 8(b) lf_fold_reduce_allranks) */
 int lf_fold_reduce_allranks(lf_ctx *ctx, lf_comm *comm, uint64_t *cm0, size_t cm0_len, uint64_t *f0,
                             size_t f0_len);
+
+int lf_dev_fold_lcccs(lf_ctx *ctx, int d, int nwit, const uint64_t *rho, const uint64_t *rho_coeff,
+                      const uint64_t *eta, size_t t, const uint64_t *xwh, size_t l1, const uint64_t *theta,
+                      uint64_t *u0, uint64_t *x0, uint64_t *v0);
+int lf_dev_compute_x_s(lf_ctx *ctx, const lf_params *pr, const uint64_t *x, size_t m, uint64_t *x_s);
 
 int lf_dev_poseidon2_permute(lf_ctx *ctx, uint64_t *states, size_t n);
 /* synthetic inputs: element i = SplitMix64(seed, i) re-mixed until < p */

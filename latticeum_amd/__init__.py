@@ -180,6 +180,35 @@ class Context:
             _ptr(out["cm0"]), repr))
         return out
 
+    def fold_lcccs(self, d: int, rho, rho_coeff=None, eta=None, xwh=None, theta=None,
+                   repr: int = REPR_CANONICAL) -> dict:
+        """u_0, x_0, v_0 of the folded LCCCS (compute_v0_u0_x0_cm_0,
+        folding/utils.rs:456-517): rho [nwit][d]; eta [nwit][t]; xwh [nwit][l+1];
+        theta [nwit][tau] with its rho_coeff [nwit][d] (tau = 3 for d = 24, else 1)"""
+        r = _u64(rho)
+        nwit = r.size // d
+        tau = 3 if d == 24 else 1
+        e = _u64(eta) if eta is not None else None
+        x = _u64(xwh) if xwh is not None else None
+        th = _u64(theta) if theta is not None else None
+        rc = _u64(rho_coeff) if rho_coeff is not None else None
+        t = e.size // (nwit * d) if e is not None else 0
+        l1 = x.size // (nwit * d) if x is not None else 0
+        out = {"u0": np.empty(t * d, np.uint64), "x0": np.empty(l1 * d, np.uint64),
+               "v0": np.empty(tau * d if th is not None else 0, np.uint64)}
+        p = lambda a: _ptr(a) if a is not None else None
+        self.check(self.lib.lf_fold_lcccs(self.h, d, nwit, _ptr(r), p(rc), p(e), t, p(x), l1, p(th),
+                                          _ptr(out["u0"]), _ptr(out["x0"]), _ptr(out["v0"]), repr))
+        return out
+
+    def compute_x_s(self, x, params: LfParams, repr: int = REPR_CANONICAL) -> np.ndarray:
+        """compute_x_s (decomposition.rs:172-175): x_w || h -> [K][m] decomposed statements"""
+        xx = _u64(x)
+        m = xx.size // params.d
+        out = np.empty(params.K * m * params.d, np.uint64)
+        self.check(self.lib.lf_compute_x_s(self.h, C.byref(params), _ptr(xx), m, _ptr(out), repr))
+        return out
+
     def poseidon2_permute(self, states) -> np.ndarray:
         s = _u64(states).copy()
         self.check(self.lib.lf_poseidon2_permute(self.h, _ptr(s), s.size // 16))

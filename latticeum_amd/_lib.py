@@ -89,6 +89,10 @@ SIGNATURES = {
     "lf_transcript_get_short_challenges": (I, [VP, I, SZ, VP]),
     "lf_hash_iter": (None, [VP, SZ, VP]),
     "lf_witness_split_w": (SZ, []),
+    "lf_fold_lcccs": (I, [VP, I, I, VP, VP, VP, SZ, VP, SZ, VP, VP, VP, VP, I]),
+    "lf_dev_fold_lcccs": (I, [VP, I, I, VP, VP, VP, SZ, VP, SZ, VP, VP, VP, VP]),
+    "lf_compute_x_s": (I, [VP, C.POINTER(LfParams), VP, SZ, VP, I]),
+    "lf_dev_compute_x_s": (I, [VP, C.POINTER(LfParams), VP, SZ, VP]),
     "lf_fold_step_partial_len": (SZ, [VP, C.POINTER(LfParams)]),
     "lf_dev_fold_step_partial": (I, [VP, VP, C.POINTER(LfParams), SZ, C.POINTER(LfFoldStepBufs), VP]),
     "lf_dev_fold_step_finish": (I, [VP, VP, C.POINTER(LfParams), SZ, C.POINTER(LfFoldStepBufs), VP]),

@@ -838,6 +838,41 @@ __global__ void k_modp_sum(const uint64_t *in, int nparts, size_t len, uint64_t 
   out[c] = gl::acc_reduce(a);
 }
 
+// ============================================================ rot_lin_combination
+// v_0 of the folded LCCCS (CR/rotation.rs:84-101, rot_sum :45-63):
+//   v0[j][c] = sum_i sum_r theta_i[r][c] coeff_j(X^r rho_i)
+// theta_i flattened to d base-ring values of comp components (Fq3 for Phi_72).
+// coeff_j(X^r a) in closed form: X^d + 1: a_(j-r), or -a_(d+j-r) when r > j;
+// Phi_72: the terms a_k X^m, m = k + r < 48, folded back with X^24 = X^12 - 1
+// (m in [24, 36): +X^(m-12) - X^(m-24)) and X^36 = -1 (m >= 36: -X^(m-36)).
+__device__ __forceinline__ uint64_t rot_coeff(const uint64_t *a, int d, int j, int r) {
+  if (d != 24) return j >= r ? a[j - r] : gl::sub(0, a[d + j - r]);
+  uint64_t v = j >= r ? a[j - r] : 0;
+  if (j >= 12 && r > j - 12) v = gl::add(v, a[j + 12 - r]);
+  if (j < 12 && r > j) v = gl::sub(v, a[j + 24 - r]);
+  if (j < 12 && r > j + 12) v = gl::sub(v, a[j + 36 - r]);
+  return v;
+}
+// one block per output value (j, c); threads stride over (i, r)
+__global__ void __launch_bounds__(256) k_rot_lin(const uint64_t *rho_coeff, const uint64_t *theta, int n, int d,
+                                                int comp, uint64_t *v0) {
+  __shared__ uint64_t red[256];
+  const int j = blockIdx.x / comp, c = blockIdx.x % comp;
+  gl::CAcc a;
+  gl::cacc_zero(a);
+  for (int t = threadIdx.x; t < n * d; t += blockDim.x) {
+    const int i = t / d, r = t - i * d;
+    gl::cacc_mad(a, gl::canon(theta[((size_t)i * d + r) * comp + c]), rot_coeff(rho_coeff + (size_t)i * d, d, j, r));
+  }
+  red[threadIdx.x] = gl::cacc_reduce(a);
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] = gl::add(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) v0[(size_t)j * comp + c] = red[0];
+}
+
 // ============================================================ RCCL limb transport
 // RCCL sums u64 mod 2^64, not mod p: ship 32-bit limbs (sums of <= 2^8 ranks
 // stay < 2^40) and fold the limb sums back into the field afterwards.
@@ -1105,6 +1140,13 @@ hipError_t fill_uniform(uint64_t *out, size_t n, uint64_t seed, hipStream_t st) 
 hipError_t modp_sum(const uint64_t *in, int nparts, size_t len, uint64_t *out, hipStream_t st) {
   if (len == 0) return hipSuccess;
   hipLaunchKernelGGL(k_modp_sum, dim3(blocks(len, 256)), dim3(256), 0, st, in, nparts, len, out);
+  return hipGetLastError();
+}
+
+hipError_t rot_lin(const uint64_t *rho_coeff, const uint64_t *theta, int n, int d, uint64_t *v0, hipStream_t st) {
+  if (n < 1 || (d != 24 && (d < 2 || (d & (d - 1))))) return hipErrorInvalidValue;
+  const int comp = d == 24 ? 3 : 1;
+  hipLaunchKernelGGL(k_rot_lin, dim3((unsigned)(d * comp)), dim3(256), 0, st, rho_coeff, theta, n, d, comp, v0);
   return hipGetLastError();
 }
 

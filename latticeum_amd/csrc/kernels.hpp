@@ -48,6 +48,8 @@ hipError_t p2_permute(uint64_t *states, size_t n, hipStream_t st);
 hipError_t fill_uniform(uint64_t *out, size_t n, uint64_t seed, hipStream_t st);
 hipError_t modp_sum(const uint64_t *in, int nparts, size_t len, uint64_t *out, hipStream_t st);
 
+// rot_lin_combination: rho_coeff [n][d] (canonical), theta [n][tau d] (tau = 3 for d = 24, else 1) -> v0 [tau d]
+hipError_t rot_lin(const uint64_t *rho_coeff, const uint64_t *theta, int n, int d, uint64_t *v0, hipStream_t st);
 hipError_t limb_split(const uint64_t *x, size_t n, uint64_t *lo, uint64_t *hi, hipStream_t st);
 hipError_t limb_join(const uint64_t *lo, const uint64_t *hi, size_t n, uint64_t *out, hipStream_t st);
 

@@ -53,6 +53,8 @@ struct lf_ctx {
   size_t stage_elems = 0;
   uint64_t *limb = nullptr;     // RCCL transport: [lo | hi] 32-bit limbs of a field vector
   size_t limb_elems = 0;
+  uint64_t *tmp = nullptr;      // small intermediates (compute_x_s)
+  size_t tmp_elems = 0;
   bool timing = false;
   std::vector<TimedLaunch> pending;
   std::map<int, std::pair<double, long>> stats;  // nvec -> (ms, count)
@@ -569,6 +571,7 @@ void lf_ctx_destroy(lf_ctx *c) {
   if (c->sink) (void)hipFree(c->sink);
   if (c->stage) (void)hipFree(c->stage);
   if (c->limb) (void)hipFree(c->limb);
+  if (c->tmp) (void)hipFree(c->tmp);
   if (c->d_err) (void)hipFree(c->d_err);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
@@ -1031,6 +1034,89 @@ static int step_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_
     LF_TRY(lf_dev_witness_from_w_ccs(c, pr, b->w_ccs, W, b->f_coeff, b->f));
   }
   return fold_commit(c, aj, pr, lb, lbs, W, b, b->f_coeff, b->f, dst);
+}
+
+int lf_dev_fold_lcccs(lf_ctx *c, int d, int nwit, const uint64_t *rho, const uint64_t *rho_coeff, const uint64_t *eta,
+                      size_t t, const uint64_t *xwh, size_t l1, const uint64_t *theta, uint64_t *u0, uint64_t *x0,
+                      uint64_t *v0) {
+  if (!c || nwit < 1 || nwit > LF_MAX_VECS || !rho) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  if ((t && (!eta || !u0)) || (l1 && (!xwh || !x0)) || (!rho_coeff != !theta) || (theta && !v0))
+    return fail(c, LF_ERR_INVALID_ARG, "missing buffer");
+  lfk::VecPtrs ve{}, vx{};
+  for (int i = 0; i < nwit; i++) {
+    ve.p[i] = eta + (size_t)i * t * d;
+    vx.p[i] = xwh + (size_t)i * l1 * d;
+  }
+  // u_0 = sum rho_i eta_i (folding/utils.rs:478-496), x_0 = sum rho_i (x_w || h)_i (:498-514)
+  if (t) LF_HIP(c, lfk::fold(rho, ve, nwit, t, d, u0, c->cur));
+  if (l1) LF_HIP(c, lfk::fold(rho, vx, nwit, l1, d, x0, c->cur));
+  // v_0 = rot_lin_combination(rho_s_coeff, theta_s) (:466)
+  if (theta) LF_HIP(c, lfk::rot_lin(rho_coeff, theta, nwit, d, v0, c->cur));
+  return LF_OK;
+}
+
+int lf_fold_lcccs(lf_ctx *c, int d, int nwit, const uint64_t *rho, const uint64_t *rho_coeff, const uint64_t *eta,
+                  size_t t, const uint64_t *xwh, size_t l1, const uint64_t *theta, uint64_t *u0, uint64_t *x0,
+                  uint64_t *v0, int repr) {
+  if (!c || nwit < 1 || nwit > LF_MAX_VECS || !rho) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  LF_TRY(check_repr(c, repr));
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  const size_t tau = d == 24 ? 3 : 1, n = (size_t)nwit;
+  DevBuf drho, drc, deta, dx, dth, du, dx0, dv;
+  LF_TRY(upload(c, drho, rho, n * d, repr));
+  if (t) {
+    LF_TRY(upload(c, deta, eta, n * t * d, repr));
+    LF_TRY(dev_alloc(c, du, t * d));
+  }
+  if (l1) {
+    LF_TRY(upload(c, dx, xwh, n * l1 * d, repr));
+    LF_TRY(dev_alloc(c, dx0, l1 * d));
+  }
+  if (theta) {
+    LF_TRY(upload(c, drc, rho_coeff, n * d, repr));
+    LF_TRY(upload(c, dth, theta, n * tau * d, repr));
+    LF_TRY(dev_alloc(c, dv, tau * d));
+  }
+  LF_TRY(lf_dev_fold_lcccs(c, d, nwit, drho.p, drc.p, deta.p, t, dx.p, l1, dth.p, du.p, dx0.p, dv.p));
+  if (t) LF_TRY(download(c, u0, du, t * d, repr));
+  if (l1) LF_TRY(download(c, x0, dx0, l1 * d, repr));
+  if (theta) LF_TRY(download(c, v0, dv, tau * d, repr));
+  return lf_ctx_sync(c);
+}
+
+// compute_x_s = w_ccs_k of decompose_witness(Witness::from_w_ccs(x).f_coeff):
+// gadget_decompose(ICRT(x)), its b_small digit planes, each plane recomposed
+// over the L limbs with B and CRT'd -- decompose_big_vec_into_k_vec_and_compose_back
+// (decomposition/utils.rs:12-42), the same arithmetic (CRT is linear)
+int lf_dev_compute_x_s(lf_ctx *c, const lf_params *pr, const uint64_t *x, size_t m, uint64_t *x_s) {
+  if (!c || (!x && m) || (!x_s && m)) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  int lb, lbs;
+  LF_TRY(check_params(c, pr, lb, lbs));
+  if (!m) return LF_OK;
+  const int d = pr->d, L = pr->L, K = pr->K;
+  const size_t N = m * L;
+  LF_TRY(grow(c, c->tmp, c->tmp_elems, (2 + 2 * (size_t)K) * N * d));
+  uint64_t *fc = c->tmp, *f = fc + N * d, *fck = f + N * d, *fk = fck + (size_t)K * N * d;
+  LF_TRY(lf_dev_witness_from_w_ccs(c, pr, x, m, fc, f));
+  return lf_dev_decompose_witness(c, pr, fc, N, fck, fk, x_s);
+}
+
+int lf_compute_x_s(lf_ctx *c, const lf_params *pr, const uint64_t *x, size_t m, uint64_t *x_s, int repr) {
+  if (!c || (!x && m) || (!x_s && m)) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  LF_TRY(check_repr(c, repr));
+  int lb, lbs;
+  LF_TRY(check_params(c, pr, lb, lbs));
+  DevBuf dx, ds;
+  LF_TRY(upload(c, dx, x, m * pr->d, repr));
+  LF_TRY(dev_alloc(c, ds, (size_t)pr->K * m * pr->d));
+  LF_TRY(lf_dev_compute_x_s(c, pr, dx.p, m, ds.p));
+  LF_TRY(download(c, x_s, ds, (size_t)pr->K * m * pr->d, repr));
+  return lf_ctx_sync(c);
 }
 
 int lf_dev_fold_step(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t W, const lf_fold_step_bufs *b) {

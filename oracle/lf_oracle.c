@@ -549,6 +549,67 @@ void lfo_fold_cm0(const uint64_t *rho, const uint64_t *cm, size_t nwit, size_t k
   fold_range(&a, 0, kappa);
 }
 
+/* ---------------------------------------- the rest of the folded LCCCS
+ * rot (GL/mod.rs:138-149 for Phi_72; X^d = -1 for the negacyclic rings):
+ * multiply a coefficient vector by X in place */
+static void rot1(uint64_t *c, int d) {
+  const uint64_t last = c[d - 1];
+  for (int i = d - 1; i > 0; i--) c[i] = c[i - 1];
+  c[0] = neg(last);
+  if (d == 24) c[12] = lfo_add(c[12], last); /* X^24 = X^12 - 1 */
+}
+/* rot_lin_combination (CR/rotation.rs:84-101) with rot_sum (:45-63):
+ * v_0 = sum_i RotSum(rho_i, flatten(theta_i)); flatten reinterprets the tau
+ * NTT elements of theta_i as d base-ring values b_r (Phi_72: Fq3 triples, tau
+ * = 3; X^d + 1: Fq, tau = 1); RotSum(a, b)_j = sum_r b_r coeff_j(X^r a);
+ * the result is promoted back to tau NTT elements (the same u64 layout). */
+void lfo_rot_lin_combination(const uint64_t *rho_coeff, const uint64_t *theta, size_t n, int d,
+                             uint64_t *v0) {
+  const int comp = d == 24 ? 3 : 1; /* base-ring components per value */
+  uint64_t *x = malloc(sizeof(uint64_t) * (size_t)d);
+  memset(v0, 0, sizeof(uint64_t) * (size_t)d * comp);
+  for (size_t i = 0; i < n; i++) {
+    memcpy(x, rho_coeff + i * d, sizeof(uint64_t) * (size_t)d); /* X^0 rho first (traits.rs:72-84) */
+    const uint64_t *b = theta + i * (size_t)d * comp;
+    for (int r = 0; r < d; r++) {
+      for (int j = 0; j < d; j++)
+        for (int c = 0; c < comp; c++)
+          v0[j * comp + c] = lfo_add(v0[j * comp + c], lfo_mul(b[r * comp + c], x[j]));
+      rot1(x, d);
+    }
+  }
+  free(x);
+}
+
+/* compute_x_s (LF/nifs/decomposition.rs:172-175) ->
+ * decompose_big_vec_into_k_vec_and_compose_back (decomposition/utils.rs:12-42):
+ * ICRT, gadget_decompose(B, L), decompose_to_vec(b_small, K) and transpose,
+ * recompose each L-chunk with B, CRT. x: m NTT elements; x_s: [K][m] */
+int lfo_compute_x_s(const uint64_t *x, size_t m, int d, uint64_t B, int L, uint64_t b_small, int K,
+                    uint64_t *x_s) {
+  uint64_t *coeff = malloc(sizeof(uint64_t) * m * d);
+  uint64_t *gad = malloc(sizeof(uint64_t) * m * L * d);
+  uint64_t dig[64];
+  int rc = 0;
+  memcpy(coeff, x, sizeof(uint64_t) * m * d);
+  lfo_icrt(coeff, m, d);
+  if (lfo_gadget_decompose(coeff, m, d, B, L, gad)) rc = -1;
+  for (size_t j = 0; j < m && !rc; j++)
+    for (int c = 0; c < d; c++) {
+      uint64_t acc[64];
+      for (int k = 0; k < K; k++) acc[k] = 0;
+      for (int l = L - 1; l >= 0; l--) { /* recompose(chunk, B): Horner over the L digits */
+        if (lfo_decompose_balanced(gad[(j * L + l) * d + c], b_small, K, dig)) rc = -1;
+        for (int k = 0; k < K; k++) acc[k] = lfo_add(lfo_mul(acc[k], B % P), dig[k]);
+      }
+      for (int k = 0; k < K; k++) x_s[((size_t)k * m + j) * d + c] = acc[k];
+    }
+  if (!rc) lfo_crt(x_s, (size_t)K * m, d);
+  free(coeff);
+  free(gad);
+  return rc;
+}
+
 /* --------------------------------------------- Poseidon2-16 (ZK/poseidon2.rs) */
 #include "p2_consts.inc"
 static const uint64_t EXT_INIT[64] = LF_P2_EXT_INIT;

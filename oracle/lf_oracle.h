@@ -99,6 +99,15 @@ void lfo_fold_f0(const uint64_t *rho, const uint64_t *f, size_t nwit, size_t N, 
 void lfo_fold_cm0(const uint64_t *rho, const uint64_t *cm, size_t nwit, size_t kappa, int d,
                   uint64_t *cm0);
 
+/* rot_lin_combination (CR/rotation.rs:84-101): v_0 from rho_i (coefficient
+ * form, [n][d]) and theta_i ([n][tau d] u64, tau = 3 for d = 24, 1 otherwise);
+ * v0: tau d u64 */
+void lfo_rot_lin_combination(const uint64_t *rho_coeff, const uint64_t *theta, size_t n, int d,
+                             uint64_t *v0);
+/* compute_x_s (LF/nifs/decomposition.rs:172-175): x (m NTT elems) -> x_s [K][m] */
+int lfo_compute_x_s(const uint64_t *x, size_t m, int d, uint64_t B, int L, uint64_t b_small, int K,
+                    uint64_t *x_s);
+
 /* ---- Poseidon2 width 16 (ZK/poseidon2.rs:100-173, 243-268) ---- */
 void lfo_p2_mds16(uint64_t *s);
 void lfo_p2_permute(uint64_t *s);

@@ -74,6 +74,8 @@ def lib():
         "lfo_tr_squeeze_bytes": (None, [C.POINTER(Transcript), u8p, SZ]),
         "lfo_fill_uniform": (None, [u64p, SZ, U64]),
         "lfo_ajtai_rows_seeded": (None, [U64, SZ, I, u64p, u64p, SZ, u64p, I]),
+        "lfo_rot_lin_combination": (None, [u64p, u64p, SZ, I, u64p]),
+        "lfo_compute_x_s": (I, [u64p, SZ, I, U64, I, U64, I, u64p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -212,6 +214,28 @@ def fold_f0(rho, f, nwit: int, N: int, d: int, nthreads: int | None = None) -> n
 def fold_cm0(rho, cm, nwit: int, kappa: int, d: int) -> np.ndarray:
     out = np.zeros(kappa * d, np.uint64)
     lib().lfo_fold_cm0(_u64(rho), _u64(cm), nwit, kappa, d, out)
+    return out
+
+
+def tau(d: int) -> int:
+    """NTT elements per f_hat evaluation / theta_i: the base ring's degree over Fq"""
+    return 3 if d == 24 else 1
+
+
+def rot_lin_combination(rho_coeff, theta, d: int) -> np.ndarray:
+    r = _u64(rho_coeff)
+    n = r.size // d
+    out = np.zeros(tau(d) * d, np.uint64)
+    lib().lfo_rot_lin_combination(r, _u64(theta), n, d, out)
+    return out
+
+
+def compute_x_s(x, d: int, B: int, L: int, b_small: int, K: int) -> np.ndarray:
+    xx = _u64(x)
+    m = xx.size // d
+    out = np.zeros(K * m * d, np.uint64)
+    if lib().lfo_compute_x_s(xx, m, d, B, L, b_small, K, out):
+        raise ValueError("compute_x_s: decomposition overflow")
     return out
 
 

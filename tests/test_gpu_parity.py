@@ -675,3 +675,50 @@ def test_rccl_comm_one_rank(ctx):
     ctx.sync()
     assert_shards_match(pr, 1024, 21, 2, keep, shards)
     comm.close()
+
+
+# ------------------------------------------------------------------ the rest of the folded LCCCS
+@pytest.mark.parametrize("d", [24, 16, 1024, 4096])
+def test_fold_lcccs_matches_oracle(ctx, d):
+    """u_0 (t = 125 CCS matrices), x_0 (l + 1 = 5) and v_0 over the 2K = 30
+    decomposed instances (compute_v0_u0_x0_cm_0, folding/utils.rs:456-517)"""
+    pr = params(d)
+    nwit, t, l1 = 2 * pr.K, 125, 5
+    tau = 3 if d == 24 else 1
+    rng = np.random.default_rng(2200 + d)
+    rc = [O.short_challenge(rng.integers(0, 256, 3 * d // 4, dtype=np.uint8).tobytes(), d) for _ in range(nwit - 1)]
+    one = np.zeros(d, np.uint64)
+    one[0] = 1
+    rho_coeff = np.concatenate(rc + [one])
+    rho = O.crt(rho_coeff, d)
+    eta, xwh, theta = rand(nwit * t * d, 2201 + d), rand(nwit * l1 * d, 2202 + d), rand(nwit * tau * d, 2203 + d)
+    got = ctx.fold_lcccs(d, rho, rho_coeff, eta, xwh, theta)
+    assert np.array_equal(got["u0"], O.fold_cm0(rho, eta, nwit, t, d))
+    assert np.array_equal(got["x0"], O.fold_cm0(rho, xwh, nwit, l1, d))
+    assert np.array_equal(got["v0"], O.rot_lin_combination(rho_coeff, theta, d))
+
+
+def test_rot_lin_combination_kat_on_gpu(ctx):
+    k = KATS["rot_lin_combination"]
+    rc = np.array(k["rho_coeff"], np.uint64)
+    got = ctx.fold_lcccs(24, O.crt(rc.ravel(), 24), rc, theta=np.array(k["theta_ntt"], np.uint64))
+    assert [int(v) for v in got["v0"]] == k["expected_ntt"]
+
+
+@pytest.mark.parametrize("d", [24, 1024])
+def test_compute_x_s_matches_oracle(ctx, d):
+    pr = params(d)
+    x = rand(5 * d, 2300 + d)
+    assert np.array_equal(ctx.compute_x_s(x, pr), O.compute_x_s(x, d, pr.B, pr.L, pr.b_small, pr.K))
+    xm = ctx.compute_x_s(mont(x), pr, repr=LA.REPR_MONTGOMERY)
+    assert np.array_equal(unmont(xm), O.compute_x_s(x, d, pr.B, pr.L, pr.b_small, pr.K))
+
+
+def test_fold_lcccs_montgomery(ctx):
+    d, nwit = 24, 30
+    rho_coeff = rand(nwit * d, 2400)
+    rho = O.crt(rho_coeff, d)
+    eta, theta = rand(nwit * 7 * d, 2401), rand(nwit * 3 * d, 2402)
+    got = ctx.fold_lcccs(d, mont(rho), mont(rho_coeff), mont(eta), None, mont(theta), repr=LA.REPR_MONTGOMERY)
+    assert np.array_equal(unmont(got["u0"]), O.fold_cm0(rho, eta, nwit, 7, d))
+    assert np.array_equal(unmont(got["v0"]), O.rot_lin_combination(rho_coeff, theta, d))

@@ -173,3 +173,38 @@ def test_fill_uniform_deterministic():
     a = O.fill_uniform(1000, 0x4C460003)
     assert np.array_equal(a, O.fill_uniform(1000, 0x4C460003))
     assert int(a.max()) < P and len(set(a.tolist())) == 1000
+
+
+# ------------------------------------------------------------------ the rest of the folded LCCCS
+def test_rot_lin_combination_kat():
+    """cyclotomic-rings rotation.rs test_rot_lin_combination (v_0 of the folded LCCCS)"""
+    k = KATS["rot_lin_combination"]
+    v = O.rot_lin_combination(np.array(k["rho_coeff"], np.uint64), np.array(k["theta_ntt"], np.uint64), 24)
+    assert [int(x) for x in v] == k["expected_ntt"]
+
+
+@pytest.mark.parametrize("d", [24, 16, 64])
+def test_rot_sum_is_the_ring_product(d):
+    """rotation.rs test_rot_sum_with_coeffs: RotSum(a, coeff(b)) = coeff(a b); for
+    Phi_72 with b's coefficients in one Fq3 component (the others zero)"""
+    a, b = O.fill_uniform(d, 31 + d), O.fill_uniform(d, 32 + d)
+    comp = 3 if d == 24 else 1
+    for c in range(comp):
+        theta = np.zeros(d * comp, np.uint64)
+        theta[c::comp] = b
+        v = O.rot_lin_combination(a, theta, d).reshape(d, comp)
+        assert np.array_equal(v[:, c], O.poly_mul(a, b, d))
+        assert not np.any(np.delete(v, c, axis=1))
+
+
+@pytest.mark.parametrize("d", [24, 64])
+def test_compute_x_s_recomposes(d):
+    """the decomposition verifier's check (decomposition.rs:137-150): the K
+    decomposed statements recompose to x_w || h with b_small"""
+    B, L, bs, K = 1 << 15, 5, 2, 15
+    x = O.fill_uniform(5 * d, 40 + d)
+    xs = O.compute_x_s(x, d, B, L, bs, K).reshape(K, 5 * d).astype(object)
+    acc = np.zeros(5 * d, object)
+    for k in reversed(range(K)):
+        acc = (acc * bs + xs[k]) % P
+    assert [int(v) for v in acc] == [int(v) for v in x]

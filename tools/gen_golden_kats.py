@@ -27,7 +27,7 @@ def fn_body(src: str, name: str) -> str:
 def field_list(text: str):
     """Parse a Rust vec![...] of Fq::from(n) / Fq::zero() / Fq::one() / MontFp!("n")."""
     vals = []
-    for m in re.finditer(r'MontFp!\("(\d+)"\)|Fq::from\((-?\d+)\)|Fq::zero\(\)|Fq::one\(\)', text):
+    for m in re.finditer(r'MontFp!\("(\d+)"\)|Fq::from\((-?\d+)(?:u64)?\)|Fq::zero\(\)|Fq::one\(\)', text):
         if m.group(1) is not None:
             vals.append(int(m.group(1)) % P)
         elif m.group(2) is not None:
@@ -119,6 +119,24 @@ def poseidon_kats():
     }
 
 
+ROT = REF / "crates/cyclotomic-rings/src/rotation.rs"
+
+
+def rot_kat():
+    """test_rot_lin_combination: v_0 = sum_i RotSum(rho_i, flatten(theta_i)) over Phi_72"""
+    src = ROT.read_text()
+    body = fn_body(src, "test_rot_lin_combination")
+    rho_txt, rest = body.split("let theta_s")[0], body.split("let theta_s")[1]
+    theta_txt, exp_txt = rest.split("let res")[0], rest.split("let expected")[1]
+    rho, theta, exp = field_list(rho_txt), field_list(theta_txt), field_list(exp_txt)
+    n = len(rho) // 24
+    assert len(rho) == 24 * n and len(theta) == 72 * n and len(exp) == 72, (len(rho), len(theta), len(exp))
+    return {"source": f"CR/rotation.rs:{line_of(ROT, 'fn test_rot_lin_combination(')}",
+            "rho_coeff": [rho[24 * i:24 * i + 24] for i in range(n)],
+            "theta_ntt": [theta[72 * i:72 * i + 72] for i in range(n)],
+            "expected_ntt": exp}
+
+
 def main() -> int:
     kats = {
         "_comment": "Known-answer data extracted from the reference's own tests/sage logs by "
@@ -140,6 +158,7 @@ def main() -> int:
             "expected_mle_first_ntt_slots": [[[1, 2, 3, 0, 0, 0, 0, 0], [4, 5, 6, 1, 1, 1, 1, 1]],
                                              [[0] * 8, [1] * 8], [[0] * 8, [1] * 8]]},
         "poseidon2": poseidon_kats(),
+        "rot_lin_combination": rot_kat(),
     }
     OUT.parent.mkdir(parents=True, exist_ok=True)
     OUT.write_text(json.dumps(kats, indent=1))
