@@ -260,11 +260,11 @@ class Workload:
             self.bufs.append(bufs)
         torch.cuda.synchronize()
 
-    def run(self, steps, comm=None):
+    def run(self, steps, comm=None, streams=None):
         """`steps` fold steps, round-robin over the step streams (asynchronous);
         with `comm`, each step is this rank's column shard of one fold
         (lf_dev_fold_step_sharded: RCCL all-reduce of the commitments)"""
-        S = len(self.ctxs)
+        S = streams or len(self.ctxs)
         for i in range(steps):
             if comm is None:
                 self.ctxs[i % S].dev_fold_step(self.sch, self.pr, self.W, self.bufs[i % S])
@@ -302,10 +302,14 @@ class Workload:
 def measure(LA, torch, LD, pg, world, wl, steps, warmup, comm=None):
     """time `steps` fold steps of workload `wl` (after `warmup` untimed ones):
     barrier + device sync on both sides, max over ranks; every phase timed
-    with HIP events on its launch stream inside the timed region"""
+    with HIP events on its launch stream inside the timed region. With several
+    step streams the phases overlap, so their launch times would not be the
+    kernels' own: the phases are then timed in a second batch on one stream."""
+    S = len(wl.ctxs)
     wl.run(warmup, comm)
     wl.sync()
-    wl.timing(True)
+    if S == 1:
+        wl.timing(True)
     LD.barrier(pg)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -315,6 +319,13 @@ def measure(LA, torch, LD, pg, world, wl, steps, warmup, comm=None):
     dt = time.perf_counter() - t0
     wl.sync()  # surfaces any decomposition overflow
     dt_max = LD.max_over_ranks(pg, dt)
+    if S > 1:  # the phase pass: one stream
+        wl.ctxs[0].kernel_timing(True)
+        wl.run(steps // S, comm, streams=1)
+        wl.sync()
+        tot = wl.phase_totals()
+        wl.timing(False)
+        return dt_max, phase_report(LA, wl, tot, steps // S)
     tot = wl.phase_totals()
     wl.timing(False)
     return dt_max, phase_report(LA, wl, tot, steps)
