@@ -297,6 +297,46 @@ int lf_dev_modp_sum(lf_ctx *ctx, const uint64_t *in, int nparts, size_t len, uin
 int lf_dev_limb_split(lf_ctx *ctx, const uint64_t *x, size_t n, uint64_t *lo, uint64_t *hi);
 int lf_dev_limb_join(lf_ctx *ctx, const uint64_t *lo, const uint64_t *hi, size_t n, uint64_t *out);
 
+/* ------------------------------------------------------------ multilinear sumcheck
+ * latticefold/src/utils/sumcheck.rs:61-88 (prove_as_subprotocol),
+ * utils/sumcheck/prover.rs:62-168 (prove_round), utils/sumcheck/utils.rs:140-210
+ * (build_eq_x_r), poly/src/mle/dense.rs:107-199 (evaluate, fix_variables),
+ * nifs/folding/utils.rs:196-331 and nifs/linearization/utils.rs:63-104 (the
+ * two polynomials). MLEs are device buffers of 2^nv NTT ring elements each
+ * (zero-padded), nm of them contiguous [nm][2^nv][d] unless a stride is given.
+ * Challenges are base-ring elements (Fq3 for d = 24, Fq otherwise: 3 or 1
+ * words) broadcast into every NTT slot. */
+enum { LF_COMB_FOLDING = 0, LF_COMB_LINEARIZATION = 1 };
+typedef struct {
+  int kind;
+  /* folding: MLEs [eq_r0, g0, eq_r1, g1, eq_beta, f_hat (nk instances x tau)];
+   * mu: nk NTT elements on the device */
+  int nk, tau, bsmall;
+  const uint64_t *mu;
+  /* linearization: MLEs [M_mles[j] for each i with c_i != 0, j in S_i] + [eq_beta];
+   * c: q NTT elements on the device; S_off [q + 1], S_idx: host arrays. The
+   * combination reads MLE position j for matrix index j, as the reference does. */
+  int q;
+  const uint64_t *c;
+  const int *S_off;
+  const int *S_idx;
+} lf_comb;
+int lf_dev_eq_table(lf_ctx *ctx, int d, const uint64_t *r, int nv, uint64_t *out);
+/* out[m][b] = in[m][2b] + r (in[m][2b + 1] - in[m][2b]) for b < 2^(nv-1); r: base-ring words (host) */
+int lf_dev_mle_fix_first(lf_ctx *ctx, int d, const uint64_t *in, size_t in_stride, int nm, int nv,
+                         const uint64_t *r_base, uint64_t *out, size_t out_stride);
+/* out[m] = mle_m(point) (nm NTT elements); point: nv NTT elements on the device */
+int lf_dev_mle_evaluate(lf_ctx *ctx, int d, const uint64_t *mles, int nm, int nv, const uint64_t *point,
+                        uint64_t *out);
+/* one prover round's message: evals[e] = sum_b comb(mle(2b) + e (mle(2b+1) - mle(2b))),
+ * e <= degree (folding: degree = 2 bsmall) */
+int lf_dev_sumcheck_round(lf_ctx *ctx, const lf_comb *comb, const uint64_t *mles, size_t stride, int nm, int nv,
+                          int d, int degree, uint64_t *evals);
+/* the whole prover with the Poseidon2 transcript: proof [nv][degree + 1][d]
+ * and randomness [nv][1 or 3] in host memory; the MLEs are clobbered */
+int lf_sumcheck_prove(lf_ctx *ctx, lf_transcript *t, const lf_comb *comb, uint64_t *mles, int nm, int nv, int d,
+                      int degree, uint64_t *proof, uint64_t *randomness);
+
 /* ------------------------------------------------------------ host transcript (sequential) */
 lf_transcript *lf_transcript_new(void);
 void lf_transcript_free(lf_transcript *t);

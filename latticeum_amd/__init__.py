@@ -17,7 +17,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import LfFoldStepBufs, LfParams, load
+from ._lib import LfComb, LfFoldStepBufs, LfParams, load
 
 P = (1 << 64) - (1 << 32) + 1
 REPR_CANONICAL = 0
@@ -256,6 +256,33 @@ class Context:
     def dev_limb_join(self, lo, hi, out):
         self.check(self.lib.lf_dev_limb_join(self.h, _dptr(lo), _dptr(hi), out.numel(), _dptr(out)))
 
+    # ---------------------------------------------------------------- multilinear sumcheck
+    def dev_eq_table(self, d: int, r, nv: int, out):
+        self.check(self.lib.lf_dev_eq_table(self.h, d, _dptr(r), nv, _dptr(out)))
+
+    def dev_mle_evaluate(self, d: int, mles, nm: int, nv: int, point, out):
+        self.check(self.lib.lf_dev_mle_evaluate(self.h, d, _dptr(mles), nm, nv, _dptr(point), _dptr(out)))
+
+    def dev_mle_fix_first(self, d: int, src, src_stride: int, nm: int, nv: int, r_base, out, out_stride: int):
+        r = _u64(r_base)
+        self.check(self.lib.lf_dev_mle_fix_first(self.h, d, _dptr(src), src_stride, nm, nv, _ptr(r), _dptr(out),
+                                                 out_stride))
+
+    def dev_sumcheck_round(self, comb: "Comb", mles, stride: int, nm: int, nv: int, d: int, degree: int, evals):
+        self.check(self.lib.lf_dev_sumcheck_round(self.h, C.byref(comb.s), _dptr(mles), stride, nm, nv, d, degree,
+                                                  _dptr(evals)))
+
+    def sumcheck_prove(self, transcript: "Poseidon2Transcript", comb: "Comb", mles, nm: int, nv: int, d: int,
+                       degree: int):
+        """MLSumcheck::prove_as_subprotocol on the device (mles is clobbered):
+        returns (proof [nv][degree+1][d], randomness [nv][tau]) as numpy"""
+        tau = 3 if d == 24 else 1
+        proof = np.zeros(nv * (degree + 1) * d, np.uint64)
+        rnd = np.zeros(nv * tau, np.uint64)
+        self.check(self.lib.lf_sumcheck_prove(self.h, transcript.h, C.byref(comb.s), _dptr(mles), nm, nv, d,
+                                              degree, _ptr(proof), _ptr(rnd)))
+        return proof, rnd
+
     def dev_poseidon2_permute(self, t):
         self.check(self.lib.lf_dev_poseidon2_permute(self.h, _dptr(t), t.numel() // 16))
 
@@ -319,6 +346,27 @@ class Communicator:
             self.close()
         except Exception:
             pass
+
+
+class Comb:
+    """lf_comb: the combination function of a sumcheck polynomial (lf.h)."""
+
+    def __init__(self, s: LfComb, keep):
+        self.s, self._keep = s, keep
+
+    @classmethod
+    def folding(cls, mu_dev, nk: int, tau: int, bsmall: int = 2) -> "Comb":
+        """the folding polynomial (folding/utils.rs:196-331); mu: nk NTT elements on the device"""
+        return cls(LfComb(kind=0, nk=nk, tau=tau, bsmall=bsmall, mu=_dptr(mu_dev)), [mu_dev])
+
+    @classmethod
+    def linearization(cls, c_dev, S) -> "Comb":
+        """the linearization polynomial (linearization/utils.rs:63-104); c: q NTT
+        elements on the device; S: q lists of matrix indices"""
+        off = np.zeros(len(S) + 1, np.int32)
+        off[1:] = np.cumsum([len(x) for x in S])
+        idx = np.array([j for x in S for j in x] or [0], np.int32)
+        return cls(LfComb(kind=1, q=len(S), c=_dptr(c_dev), S_off=_ptr(off), S_idx=_ptr(idx)), [c_dev, off, idx])
 
 
 def witness_split_w() -> int:
@@ -426,7 +474,7 @@ def hash_iter(vals) -> np.ndarray:
     return out
 
 
-__all__ = ["Context", "AjtaiCommitmentScheme", "Communicator", "witness_split_w", "Poseidon2Transcript",
+__all__ = ["Context", "AjtaiCommitmentScheme", "Communicator", "Comb", "witness_split_w", "Poseidon2Transcript",
            "LfParams", "LfFoldStepBufs",
            "LfError", "goldilocks_dp", "short_challenge", "hash_iter", "P", "REPR_CANONICAL",
            "REPR_MONTGOMERY", "load"]

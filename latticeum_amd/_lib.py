@@ -30,6 +30,11 @@ class LfFoldStepBufs(C.Structure):
     ]
 
 
+class LfComb(C.Structure):
+    _fields_ = [("kind", I), ("nk", I), ("tau", I), ("bsmall", I), ("mu", VP), ("q", I), ("c", VP),
+                ("S_off", VP), ("S_idx", VP)]
+
+
 # every function exported by include/lf.h: name -> (restype, argtypes)
 SIGNATURES = {
     "lf_goldilocks_dp": (LfParams, [I]),
@@ -89,6 +94,11 @@ SIGNATURES = {
     "lf_transcript_get_short_challenges": (I, [VP, I, SZ, VP]),
     "lf_hash_iter": (None, [VP, SZ, VP]),
     "lf_witness_split_w": (SZ, []),
+    "lf_dev_eq_table": (I, [VP, I, VP, I, VP]),
+    "lf_dev_mle_fix_first": (I, [VP, I, VP, SZ, I, I, VP, VP, SZ]),
+    "lf_dev_mle_evaluate": (I, [VP, I, VP, I, I, VP, VP]),
+    "lf_dev_sumcheck_round": (I, [VP, C.POINTER(LfComb), VP, SZ, I, I, I, I, VP]),
+    "lf_sumcheck_prove": (I, [VP, VP, C.POINTER(LfComb), VP, I, I, I, I, VP, VP]),
     "lf_fold_lcccs": (I, [VP, I, I, VP, VP, VP, SZ, VP, SZ, VP, VP, VP, VP, I]),
     "lf_dev_fold_lcccs": (I, [VP, I, I, VP, VP, VP, SZ, VP, SZ, VP, VP, VP, VP]),
     "lf_compute_x_s": (I, [VP, C.POINTER(LfParams), VP, SZ, VP, I]),

@@ -114,4 +114,30 @@ hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K,
                            const ring::NegaTables &fwd, uint4 *frag, int nch, int *err, uint64_t *sink, int ncu,
                            hipStream_t st);
 
+// ---------------------------------------------------------------- sumcheck (sumcheck.hip)
+// the multisets S_i of a CCS (linearization polynomial), by value as a kernel argument
+constexpr int LF_MAX_MULTISETS = 64, LF_MAX_S = 512;
+struct CombS {
+  int q;
+  int off[LF_MAX_MULTISETS + 1];
+  short idx[LF_MAX_S];
+};
+int slot_words(int d);  // words of one NTT slot: 3 (Fq3, Phi_72) or 1
+hipError_t eq_table(const uint64_t *r, int nv, int d, uint64_t *out, hipStream_t st);
+// out[m][b] = in[m][2b] + r (in[m][2b+1] - in[m][2b]), b < half; r_base: slot_words(d) words
+hipError_t mle_fix_first(const uint64_t *in, size_t in_stride, int nm, size_t half, int d, const uint64_t *r_base,
+                         uint64_t *out, size_t out_stride, hipStream_t st);
+size_t round_partial_elems(int d, size_t half, int nevals);
+hipError_t fold_weights(const uint64_t *mu, int nk, int tau, int d, uint64_t *w, hipStream_t st);
+// evals [2 bsmall + 1][d]: the folding polynomial's round sums over `half` points;
+// mles: 5 + nf MLEs at stride u64 apart; w: nf Horner weights
+hipError_t round_folding(const uint64_t *mles, size_t stride, int nf, const uint64_t *w, int bsmall, size_t half, int d,
+                         uint64_t *partial, uint64_t *evals, hipStream_t st);
+hipError_t round_lin(const uint64_t *mles, size_t stride, int nm, const uint64_t *c, const CombS &cs, int degree,
+                     size_t half, int d, uint64_t *partial, uint64_t *evals, hipStream_t st);
+size_t mle_eval_partial_elems(int d, int nm);
+// out[m] = sum_x eq[x] (.) mles[m][x], x < n
+hipError_t mle_dot(const uint64_t *mles, size_t stride, int nm, const uint64_t *eq, size_t n, int d,
+                   uint64_t *partial, uint64_t *out, hipStream_t st);
+
 }  // namespace lfk

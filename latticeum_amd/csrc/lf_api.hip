@@ -55,6 +55,8 @@ struct lf_ctx {
   size_t limb_elems = 0;
   uint64_t *tmp = nullptr;      // small intermediates (compute_x_s)
   size_t tmp_elems = 0;
+  uint64_t *sc = nullptr;       // sumcheck: fixed MLEs of the next round, round partial sums, weights
+  size_t sc_elems = 0;
   bool timing = false;
   std::vector<TimedLaunch> pending;
   std::map<int, std::pair<double, long>> stats;  // nvec -> (ms, count)
@@ -572,6 +574,7 @@ void lf_ctx_destroy(lf_ctx *c) {
   if (c->stage) (void)hipFree(c->stage);
   if (c->limb) (void)hipFree(c->limb);
   if (c->tmp) (void)hipFree(c->tmp);
+  if (c->sc) (void)hipFree(c->sc);
   if (c->d_err) (void)hipFree(c->d_err);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
@@ -1117,6 +1120,135 @@ int lf_compute_x_s(lf_ctx *c, const lf_params *pr, const uint64_t *x, size_t m, 
   LF_TRY(lf_dev_compute_x_s(c, pr, dx.p, m, ds.p));
   LF_TRY(download(c, x_s, ds, (size_t)pr->K * m * pr->d, repr));
   return lf_ctx_sync(c);
+}
+
+// ---------------------------------------------------------------- multilinear sumcheck
+static int comb_check(lf_ctx *c, const lf_comb *cb, int nm, int d, int degree, lfk::CombS *cs) {
+  if (!cb) return fail(c, LF_ERR_INVALID_ARG, "null combination");
+  if (cb->kind == LF_COMB_FOLDING) {
+    if (!cb->mu || cb->nk < 1 || cb->tau < 1 || cb->bsmall < 1 || cb->bsmall > 4 || nm != 5 + cb->nk * cb->tau ||
+        (degree >= 0 && degree != 2 * cb->bsmall))
+      return fail(c, LF_ERR_INVALID_ARG, "folding sumcheck: 5 + nk tau MLEs, degree 2 B_SMALL, B_SMALL <= 4");
+    return LF_OK;
+  }
+  if (cb->kind != LF_COMB_LINEARIZATION || !cb->c || !cb->S_off || !cb->S_idx || cb->q < 1 ||
+      cb->q > lfk::LF_MAX_MULTISETS || degree < 1 || degree > 9)
+    return fail(c, LF_ERR_INVALID_ARG, "linearization sumcheck: 1 <= q <= 64 multisets, degree <= 9");
+  cs->q = cb->q;
+  for (int i = 0; i <= cb->q; i++) cs->off[i] = cb->S_off[i];
+  if (cs->off[0] != 0 || cs->off[cb->q] > lfk::LF_MAX_S)
+    return fail(c, LF_ERR_INVALID_ARG, "linearization sumcheck: at most 512 multiset entries");
+  for (int i = 0; i < cs->off[cb->q]; i++) {
+    if (cb->S_idx[i] < 0 || cb->S_idx[i] >= nm - 1) return fail(c, LF_ERR_INVALID_ARG, "multiset index out of range");
+    cs->idx[i] = (short)cb->S_idx[i];
+  }
+  return LF_OK;
+}
+static int comb_degree(const lf_comb *cb, int degree) { return cb->kind == LF_COMB_FOLDING ? 2 * cb->bsmall : degree; }
+
+int lf_dev_eq_table(lf_ctx *c, int d, const uint64_t *r, int nv, uint64_t *out) {
+  if (!c || !r || !out || nv < 1) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  LF_HIP(c, lfk::eq_table(r, nv, d, out, c->cur));
+  return LF_OK;
+}
+
+int lf_dev_mle_fix_first(lf_ctx *c, int d, const uint64_t *in, size_t in_stride, int nm, int nv,
+                         const uint64_t *r_base, uint64_t *out, size_t out_stride) {
+  if (!c || !in || !out || !r_base || nm < 1 || nv < 1) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  LF_HIP(c, lfk::mle_fix_first(in, in_stride, nm, (size_t)1 << (nv - 1), d, r_base, out, out_stride, c->cur));
+  return LF_OK;
+}
+
+int lf_dev_mle_evaluate(lf_ctx *c, int d, const uint64_t *mles, int nm, int nv, const uint64_t *point, uint64_t *out) {
+  if (!c || !mles || !point || !out || nm < 1 || nv < 1) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  const size_t n = (size_t)1 << nv;
+  LF_TRY(grow(c, c->sc, c->sc_elems, n * d + lfk::mle_eval_partial_elems(d, nm)));
+  LF_HIP(c, lfk::eq_table(point, nv, d, c->sc, c->cur));
+  LF_HIP(c, lfk::mle_dot(mles, n * d, nm, c->sc, n, d, c->sc + n * d, out, c->cur));
+  return LF_OK;
+}
+
+int lf_dev_sumcheck_round(lf_ctx *c, const lf_comb *cb, const uint64_t *mles, size_t stride, int nm, int nv, int d,
+                          int degree, uint64_t *evals) {
+  if (!c || !mles || !evals || nv < 1) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  lfk::CombS cs;
+  LF_TRY(comb_check(c, cb, nm, d, cb && cb->kind == LF_COMB_FOLDING ? -1 : degree, &cs));
+  const int deg = comb_degree(cb, degree);
+  const size_t half = (size_t)1 << (nv - 1);
+  const size_t part = lfk::round_partial_elems(d, half, deg + 1);
+  const size_t wlen = cb->kind == LF_COMB_FOLDING ? (size_t)cb->nk * cb->tau * d : 0;
+  LF_TRY(grow(c, c->sc, c->sc_elems, part + wlen));
+  if (cb->kind == LF_COMB_FOLDING) {
+    uint64_t *w = c->sc + part;
+    LF_HIP(c, lfk::fold_weights(cb->mu, cb->nk, cb->tau, d, w, c->cur));
+    LF_HIP(c, lfk::round_folding(mles, stride, cb->nk * cb->tau, w, cb->bsmall, half, d, c->sc, evals, c->cur));
+  } else {
+    LF_HIP(c, lfk::round_lin(mles, stride, nm, cb->c, cs, deg, half, d, c->sc, evals, c->cur));
+  }
+  return LF_OK;
+}
+
+int lf_sumcheck_prove(lf_ctx *c, lf_transcript *t, const lf_comb *cb, uint64_t *mles, int nm, int nv, int d,
+                      int degree, uint64_t *proof, uint64_t *randomness) {
+  if (!c || !t || !mles || !proof || !randomness || nv < 1 || nm < 1) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  lfk::CombS cs;
+  LF_TRY(comb_check(c, cb, nm, d, degree, &cs));
+  const int tb = lfk::slot_words(d), nev = degree + 1;
+  const size_t n = (size_t)1 << nv;
+  // scratch: the MLEs fixed by the first challenge (later rounds ping-pong with
+  // `mles` itself), the round's partial sums, the evaluations, the weights
+  const size_t fixed = (size_t)nm * (n / 2) * d, part = lfk::round_partial_elems(d, n / 2, nev);
+  const size_t wlen = cb->kind == LF_COMB_FOLDING ? (size_t)cb->nk * cb->tau * d : 0;
+  LF_TRY(grow(c, c->sc, c->sc_elems, fixed + part + (size_t)nev * d + wlen));
+  uint64_t *buf = c->sc, *partial = buf + fixed, *ev = partial + part, *w = ev + (size_t)nev * d;
+  if (wlen) LF_HIP(c, lfk::fold_weights(cb->mu, cb->nk, cb->tau, d, w, c->cur));
+  // MLSumcheck::prove_as_subprotocol (sumcheck.rs:61-88): absorb R::from(nvars), R::from(degree)
+  std::vector<uint64_t> scal(d, 0);
+  for (int i = 0; i < d; i += tb) scal[i] = (uint64_t)nv;
+  lf_transcript_absorb_ring(t, scal.data(), 1, d, LF_REPR_CANONICAL);
+  for (int i = 0; i < d; i += tb) scal[i] = (uint64_t)degree;
+  lf_transcript_absorb_ring(t, scal.data(), 1, d, LF_REPR_CANONICAL);
+  const uint64_t *cur = mles;
+  size_t stride = n * d;
+  for (int i = 0; i < nv; i++) {
+    const size_t half = n >> (i + 1);
+    uint64_t *msg = proof + (size_t)i * nev * d;
+    if (cb->kind == LF_COMB_FOLDING)
+      LF_HIP(c, lfk::round_folding(cur, stride, cb->nk * cb->tau, w, cb->bsmall, half, d, partial, ev, c->cur));
+    else
+      LF_HIP(c, lfk::round_lin(cur, stride, nm, cb->c, cs, degree, half, d, partial, ev, c->cur));
+    LF_HIP(c, hipMemcpyAsync(msg, ev, (size_t)nev * d * 8, hipMemcpyDeviceToHost, c->cur));
+    LF_HIP(c, hipStreamSynchronize(c->cur));
+    // prover message absorbed, challenge sampled (fiat_shamir.rs:69-86; one sample for Fq) and absorbed
+    lf_transcript_absorb_ring(t, msg, (size_t)nev, d, LF_REPR_CANONICAL);
+    uint64_t *ch = randomness + (size_t)i * tb;
+    if (tb == 3) {
+      lf_transcript_get_challenge(t, ch);
+    } else {
+      ch[0] = lf_transcript_sample(t);
+      lf_transcript_observe(t, ch[0]);
+    }
+    for (int k = 0; k < d; k++) scal[k] = ch[k % tb];
+    lf_transcript_absorb_ring(t, scal.data(), 1, d, LF_REPR_CANONICAL);
+    // fix_variables(r) of every MLE (prover.rs:75-78), into the other buffer
+    if (half >= 1 && i + 1 < nv) {
+      uint64_t *dst = (i % 2 == 0) ? buf : mles;
+      LF_HIP(c, lfk::mle_fix_first(cur, stride, nm, half, d, ch, dst, half * d, c->cur));
+      cur = dst;
+      stride = half * d;
+    }
+  }
+  return LF_OK;
 }
 
 int lf_dev_fold_step(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t W, const lf_fold_step_bufs *b) {

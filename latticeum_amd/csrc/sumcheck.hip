@@ -1,0 +1,474 @@
+// sumcheck.hip -- the multilinear sumcheck prover's device work (SURVEY.md
+// 8(f) rank 1): eq tables, fix_variables, the per-round sums of the folding and
+// linearization polynomials, and MLE evaluation.
+//
+// Reference: latticefold/src/utils/sumcheck/prover.rs:62-168 (prove_round),
+// utils/sumcheck/utils.rs:140-210 (build_eq_x_r), poly/src/mle/dense.rs:107-199
+// (evaluate, fix_variables), nifs/folding/utils.rs:196-331 (the folding
+// polynomial and its combination function), nifs/linearization/utils.rs:63-104.
+//
+// An MLE over nv variables is 2^nv ring elements in NTT form (d u64 each; the
+// reference's zero-truncated vectors read as zero-padded, dense.rs:397-418),
+// and a batch of nm MLEs is one contiguous [nm][2^nv][d] buffer. The
+// challenges are base-ring elements broadcast into every NTT slot, so every
+// slot runs its own sumcheck: a thread owns one (point, slot) pair, where a
+// slot is an Fq3 (Phi_72, TB = 3 words) or an Fq (X^d + 1, TB = 1).
+#include "gl.hpp"
+#include "kernels.hpp"
+#include "ring.hpp"
+
+namespace lfk {
+
+namespace {
+
+template <int TB>
+struct Sv {
+  uint64_t c[TB];
+};
+template <int TB>
+__device__ __forceinline__ Sv<TB> s_load(const uint64_t *p) {
+  Sv<TB> r;
+#pragma unroll
+  for (int i = 0; i < TB; i++) r.c[i] = p[i];
+  return r;
+}
+template <int TB>
+__device__ __forceinline__ void s_store(uint64_t *p, const Sv<TB> &v) {
+#pragma unroll
+  for (int i = 0; i < TB; i++) p[i] = v.c[i];
+}
+template <int TB>
+__device__ __forceinline__ Sv<TB> s_add(const Sv<TB> &a, const Sv<TB> &b) {
+  Sv<TB> r;
+#pragma unroll
+  for (int i = 0; i < TB; i++) r.c[i] = gl::add(a.c[i], b.c[i]);
+  return r;
+}
+template <int TB>
+__device__ __forceinline__ Sv<TB> s_sub(const Sv<TB> &a, const Sv<TB> &b) {
+  Sv<TB> r;
+#pragma unroll
+  for (int i = 0; i < TB; i++) r.c[i] = gl::sub(a.c[i], b.c[i]);
+  return r;
+}
+template <int TB>
+__device__ __forceinline__ Sv<TB> s_zero() {
+  Sv<TB> r;
+#pragma unroll
+  for (int i = 0; i < TB; i++) r.c[i] = 0;
+  return r;
+}
+template <int TB>
+__device__ __forceinline__ Sv<TB> s_one() {
+  Sv<TB> r = s_zero<TB>();
+  r.c[0] = 1;
+  return r;
+}
+// small scalar k as a slot value (k, 0, 0)
+template <int TB>
+__device__ __forceinline__ Sv<TB> s_scalar(uint64_t k) {
+  Sv<TB> r = s_zero<TB>();
+  r.c[0] = k;
+  return r;
+}
+// slot product: Fq, or Fq3 = Fq[u]/(u^3 - 2^40) (goldilocks/mod.rs:34-54) with
+// the carry-chain accumulators and one reduction per output word
+__device__ __forceinline__ Sv<1> s_mul(const Sv<1> &a, const Sv<1> &b) {
+  Sv<1> r;
+  r.c[0] = gl::mul(a.c[0], b.c[0]);
+  return r;
+}
+__device__ __forceinline__ Sv<3> s_mul(const Sv<3> &a, const Sv<3> &b) {
+  gl::CAcc x0, x0n, x1, x1n, x2;
+  gl::cacc_zero(x0);
+  gl::cacc_zero(x0n);
+  gl::cacc_zero(x1);
+  gl::cacc_zero(x1n);
+  gl::cacc_zero(x2);
+  gl::cacc_mad(x0, a.c[0], b.c[0]);
+  gl::cacc_mad(x0n, a.c[1], b.c[2]);
+  gl::cacc_mad(x0n, a.c[2], b.c[1]);
+  gl::cacc_mad(x1, a.c[0], b.c[1]);
+  gl::cacc_mad(x1, a.c[1], b.c[0]);
+  gl::cacc_mad(x1n, a.c[2], b.c[2]);
+  gl::cacc_mad(x2, a.c[0], b.c[2]);
+  gl::cacc_mad(x2, a.c[1], b.c[1]);
+  gl::cacc_mad(x2, a.c[2], b.c[0]);
+  Sv<3> r;
+  r.c[0] = gl::add(gl::cacc_reduce(x0), gl::shl96(gl::cacc_reduce(x0n), 40));
+  r.c[1] = gl::add(gl::cacc_reduce(x1), gl::shl96(gl::cacc_reduce(x1n), 40));
+  r.c[2] = gl::cacc_reduce(x2);
+  return r;
+}
+template <int TB>
+__device__ __forceinline__ bool s_is_zero(const Sv<TB> &a) {
+  uint64_t o = 0;
+#pragma unroll
+  for (int i = 0; i < TB; i++) o |= a.c[i];
+  return o == 0;
+}
+
+// ---------------------------------------------------------------- eq table
+// build_eq_x_r (sumcheck/utils.rs:140-210): eq[x] = prod_k (x_k ? r_k : 1 - r_k),
+// x_0 = the least significant bit. The reference builds it by doubling with
+// b - r b and r b; the product of the same factors is the same field element.
+template <int TB>
+__global__ void k_eq_table(const uint64_t *r, int nv, int d, uint64_t *out) {
+  const int ns = d / TB;
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= ((size_t)ns << nv)) return;
+  const size_t x = i / ns;
+  const int s = (int)(i - x * ns);
+  Sv<TB> acc = s_one<TB>();
+  for (int k = 0; k < nv; k++) {
+    const Sv<TB> rk = s_load<TB>(r + (size_t)k * d + s * TB);
+    acc = s_mul(acc, (x >> k) & 1 ? rk : s_sub(s_one<TB>(), rk));
+  }
+  s_store(out + x * d + s * TB, acc);
+}
+
+// ---------------------------------------------------------------- fix_variables
+// dense.rs:171-199 for one point: out[m][b] = in[m][2b] + r (in[m][2b+1] - in[m][2b]),
+// r a base-ring value in every slot; out-of-place (ping-pong buffers)
+template <int TB>
+__global__ void k_fix_first(const uint64_t *in, size_t in_stride, int nm, size_t half, int d, Sv<TB> r,
+                            uint64_t *out, size_t out_stride) {
+  const int ns = d / TB;
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // (m, b, slot)
+  if (i >= (size_t)nm * half * ns) return;
+  const size_t mb = i / ns;
+  const int s = (int)(i - mb * ns);
+  const size_t m = mb / half, b = mb - m * half;
+  const uint64_t *p = in + m * in_stride + 2 * b * d + s * TB;
+  const Sv<TB> left = s_load<TB>(p), right = s_load<TB>(p + d);
+  s_store(out + m * out_stride + b * d + s * TB, s_add(left, s_mul(r, s_sub(right, left))));
+}
+
+// ---------------------------------------------------------------- round sums
+// A block holds PPB points x SPB slots; a thread loops over points with a grid
+// stride, keeps its per-evaluation-point sums in registers, and the block
+// writes partial[blockIdx.x][e][slot] after an LDS reduction over its points.
+constexpr int RT = 256;
+constexpr int MAX_EVALS = 10;  // degree + 1 <= 10
+
+// dst: this block's sums, evaluation point e at dst + e d (slot words at slot TB)
+template <int TB, int NE>
+__device__ __forceinline__ void block_partial(const Sv<TB> (&acc)[NE], int spb, int ppb, int slot, int lane_p,
+                                              int d, uint64_t *dst) {
+  __shared__ uint64_t red[RT * TB];
+#pragma unroll
+  for (int e = 0; e < NE; e++) {
+    s_store(red + threadIdx.x * TB, acc[e]);
+    __syncthreads();
+    for (int w = ppb / 2; w > 0; w >>= 1) {
+      if (lane_p < w) {
+        const int o = threadIdx.x + w * spb;
+        s_store(red + threadIdx.x * TB, s_add(s_load<TB>(red + threadIdx.x * TB), s_load<TB>(red + o * TB)));
+      }
+      __syncthreads();
+    }
+    if (lane_p == 0) s_store(dst + (size_t)e * d + slot * TB, s_load<TB>(red + threadIdx.x * TB));
+    __syncthreads();
+  }
+}
+
+// The folding polynomial (folding/utils.rs:196-331), MLEs [eq_r0, g0, eq_r1, g1,
+// eq_beta, f_hat (nk x tau)]:
+//   comb = v0 v1 + v2 v3 + sum_k Horner_dd( v4 f (prod_{b<B_SMALL} (f^2 - b^2)) ) in mu_k
+// The Horner over dd = tau-1 .. 0 is sum_dd mu_k^(dd+1) e_dd, so with
+// w_(k,dd) = mu_k^(dd+1) (k_fold_weights) the per-point value is
+//   v0 v1 + v2 v3 + v4 S,  S = sum_(k,dd) w_(k,dd) g(f_(k,dd)),  g(f) = f prod (f^2 - b^2)
+// (the reference's zero short-cuts do not change values). S is a polynomial of
+// degree 2 B_SMALL - 1 in the evaluation point e, so it is computed at the
+// first `degree` points and extrapolated to e = degree by finite differences.
+template <int TB, int BS>
+__global__ void __launch_bounds__(RT) k_round_folding(const uint64_t *mles, size_t stride, int nf, const uint64_t *w,
+                                                      size_t half, int d, int spb, uint64_t *partial) {
+  const int slot_l = threadIdx.x % spb, lane_p = threadIdx.x / spb, ppb = RT / spb;
+  const int slot = blockIdx.y * spb + slot_l;
+  constexpr int degree = 2 * BS;
+  Sv<TB> acc[degree + 1];
+#pragma unroll
+  for (int e = 0; e <= degree; e++) acc[e] = s_zero<TB>();
+  for (size_t b = (size_t)blockIdx.x * ppb + lane_p; b < half; b += (size_t)gridDim.x * ppb) {
+    const uint64_t *pb = mles + 2 * b * d + slot * TB;
+    Sv<TB> S[degree + 1];
+#pragma unroll
+    for (int e = 0; e < degree; e++) S[e] = s_zero<TB>();
+    for (int f = 0; f < nf; f++) {
+      const uint64_t *p = pb + (size_t)(5 + f) * stride;
+      const Sv<TB> a = s_load<TB>(p), st = s_sub(s_load<TB>(p + d), a);
+      const Sv<TB> wf = s_load<TB>(w + (size_t)f * d + slot * TB);
+      Sv<TB> x = a;
+#pragma unroll
+      for (int e = 0; e < degree; e++) {
+        const Sv<TB> x2 = s_mul(x, x);
+        Sv<TB> g = x;
+#pragma unroll
+        for (int bb = 1; bb < BS; bb++) g = s_mul(g, s_sub(x2, s_scalar<TB>((uint64_t)bb * bb)));
+        S[e] = s_add(S[e], s_mul(wf, g));
+        x = s_add(x, st);
+      }
+    }
+    // S(degree) from S(0 .. degree-1): sum_j (-1)^(degree-1-j) C(degree, j) S(j)
+    {
+      Sv<TB> ext = s_zero<TB>();
+      uint64_t binom = 1;  // C(degree, j)
+#pragma unroll
+      for (int j = 0; j < degree; j++) {
+        Sv<TB> t = S[j];
+        Sv<TB> scaled = s_zero<TB>();
+#pragma unroll
+        for (int q = 0; q < TB; q++) scaled.c[q] = gl::mul(t.c[q], binom);
+        ext = ((degree - 1 - j) & 1) ? s_sub(ext, scaled) : s_add(ext, scaled);
+        binom = binom * (uint64_t)(degree - j) / (uint64_t)(j + 1);
+      }
+      S[degree] = ext;
+    }
+    Sv<TB> v[5], sv[5];
+#pragma unroll
+    for (int m = 0; m < 5; m++) {
+      const uint64_t *p = pb + (size_t)m * stride;
+      v[m] = s_load<TB>(p);
+      sv[m] = s_sub(s_load<TB>(p + d), v[m]);
+    }
+#pragma unroll
+    for (int e = 0; e <= degree; e++) {
+      acc[e] = s_add(acc[e], s_add(s_add(s_mul(v[0], v[1]), s_mul(v[2], v[3])), s_mul(v[4], S[e])));
+#pragma unroll
+      for (int m = 0; m < 5; m++) v[m] = s_add(v[m], sv[m]);
+    }
+  }
+  block_partial<TB, degree + 1>(acc, spb, ppb, slot, lane_p, d, partial + (size_t)blockIdx.x * (degree + 1) * d);
+}
+
+// w_(k,dd) = mu_k^(dd+1), the Horner weights of the folding combination
+template <int TB>
+__global__ void k_fold_weights(const uint64_t *mu, int nk, int tau, int d, uint64_t *w) {
+  const int ns = d / TB;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (k, slot)
+  if (i >= nk * ns) return;
+  const int k = i / ns, s = i - k * ns;
+  const Sv<TB> m = s_load<TB>(mu + (size_t)k * d + s * TB);
+  Sv<TB> p = m;
+  for (int dd = 0; dd < tau; dd++) {
+    s_store(w + ((size_t)k * tau + dd) * d + s * TB, p);
+    p = s_mul(p, m);
+  }
+}
+
+// The linearization polynomial (linearization/utils.rs:63-104):
+//   comb = v_last * sum_i c_i prod_(j in S_i) v_j
+// v_j indexes the MLE list by the matrix index j, as the reference does.
+template <int TB, int DEG>
+__global__ void __launch_bounds__(RT) k_round_lin(const uint64_t *mles, size_t stride, int nm, const uint64_t *c,
+                                                  CombS cs, size_t half, int d, int spb, uint64_t *partial) {
+  const int slot_l = threadIdx.x % spb, lane_p = threadIdx.x / spb, ppb = RT / spb;
+  const int slot = blockIdx.y * spb + slot_l;
+  constexpr int degree = DEG;
+  Sv<TB> acc[degree + 1];
+#pragma unroll
+  for (int e = 0; e <= degree; e++) acc[e] = s_zero<TB>();
+  for (size_t b = (size_t)blockIdx.x * ppb + lane_p; b < half; b += (size_t)gridDim.x * ppb) {
+    const uint64_t *pb = mles + 2 * b * d + slot * TB;
+    const uint64_t *pe = pb + (size_t)(nm - 1) * stride;
+    const Sv<TB> e0 = s_load<TB>(pe), es = s_sub(s_load<TB>(pe + d), e0);
+#pragma unroll
+    for (int e = 0; e <= degree; e++) {
+      Sv<TB> sum = s_zero<TB>();
+      for (int i = 0; i < cs.q; i++) {
+        Sv<TB> term = s_load<TB>(c + (size_t)i * d + slot * TB);
+        for (int s = cs.off[i]; s < cs.off[i + 1]; s++) {
+          const uint64_t *p = pb + (size_t)cs.idx[s] * stride;
+          const Sv<TB> a = s_load<TB>(p);
+          Sv<TB> x = a;
+          if (e) {
+            const Sv<TB> st = s_sub(s_load<TB>(p + d), a);
+            for (int q = 0; q < e; q++) x = s_add(x, st);
+          }
+          term = s_mul(term, x);
+        }
+        sum = s_add(sum, term);
+      }
+      Sv<TB> ev = e0;
+      for (int q = 0; q < e; q++) ev = s_add(ev, es);
+      acc[e] = s_add(acc[e], s_mul(sum, ev));
+    }
+  }
+  block_partial<TB, degree + 1>(acc, spb, ppb, slot, lane_p, d, partial + (size_t)blockIdx.x * (degree + 1) * d);
+}
+
+// out[e][.] = sum over blocks of partial[blk][e][.]
+__global__ void k_sum_partials(const uint64_t *partial, int nblk, size_t len, uint64_t *out) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= len) return;
+  uint64_t s = 0;
+  for (int b = 0; b < nblk; b++) s = gl::add(s, partial[(size_t)b * len + i]);
+  out[i] = s;
+}
+
+// ---------------------------------------------------------------- MLE evaluation
+// evaluate (dense.rs:107-113) = sum_x eq(point, x) mle(x): partial sums over x
+// ranges, out[m] from k_sum_partials over the ranges
+template <int TB>
+__global__ void __launch_bounds__(RT) k_mle_dot(const uint64_t *mles, size_t stride, const uint64_t *eq, size_t n,
+                                                int d, int spb, int nsplit, uint64_t *partial, int nm) {
+  const int slot_l = threadIdx.x % spb, lane_p = threadIdx.x / spb, ppb = RT / spb;
+  const int slot = blockIdx.y * spb + slot_l;
+  const int m = blockIdx.z;
+  Sv<TB> acc[1] = {s_zero<TB>()};
+  for (size_t x = (size_t)blockIdx.x * ppb + lane_p; x < n; x += (size_t)nsplit * ppb)
+    acc[0] = s_add(acc[0], s_mul(s_load<TB>(eq + x * d + slot * TB), s_load<TB>(mles + m * stride + x * d + slot * TB)));
+  block_partial<TB, 1>(acc, spb, ppb, slot, lane_p, d, partial + ((size_t)blockIdx.x * nm + m) * d);
+}
+
+unsigned blocks_of(size_t n, int t) { return (unsigned)((n + t - 1) / t); }
+
+template <int TB>
+hipError_t dispatch_eq(const uint64_t *r, int nv, int d, uint64_t *out, hipStream_t st) {
+  const size_t n = ((size_t)(d / TB)) << nv;
+  hipLaunchKernelGGL(k_eq_table<TB>, dim3(blocks_of(n, 256)), dim3(256), 0, st, r, nv, d, out);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+int slot_words(int d) { return d == 24 ? 3 : 1; }
+
+hipError_t eq_table(const uint64_t *r, int nv, int d, uint64_t *out, hipStream_t st) {
+  if (nv < 1 || nv > 40) return hipErrorInvalidValue;
+  return d == 24 ? dispatch_eq<3>(r, nv, d, out, st) : dispatch_eq<1>(r, nv, d, out, st);
+}
+
+hipError_t mle_fix_first(const uint64_t *in, size_t in_stride, int nm, size_t half, int d, const uint64_t *r_base,
+                         uint64_t *out, size_t out_stride, hipStream_t st) {
+  const int tb = slot_words(d);
+  const size_t n = (size_t)nm * half * (d / tb);
+  if (!n) return hipSuccess;
+  if (tb == 3) {
+    Sv<3> r;
+    for (int i = 0; i < 3; i++) r.c[i] = r_base[i];
+    hipLaunchKernelGGL(k_fix_first<3>, dim3(blocks_of(n, 256)), dim3(256), 0, st, in, in_stride, nm, half, d, r, out,
+                       out_stride);
+  } else {
+    Sv<1> r;
+    r.c[0] = r_base[0];
+    hipLaunchKernelGGL(k_fix_first<1>, dim3(blocks_of(n, 256)), dim3(256), 0, st, in, in_stride, nm, half, d, r, out,
+                       out_stride);
+  }
+  return hipGetLastError();
+}
+
+// the round-sum launch geometry: spb slots per block (all of a Phi_72
+// element's 8, or up to 256 of X^d + 1), enough blocks for the points
+static void round_geom(int d, size_t half, int &spb, dim3 &grid) {
+  const int ns = d / slot_words(d);
+  spb = ns < RT ? ns : RT;
+  const int ppb = RT / spb;
+  size_t bx = (half + ppb - 1) / ppb;
+  const size_t cap = 1024;  // partial sums: at most this many blocks along the points
+  if (bx > cap) bx = cap;
+  if (bx < 1) bx = 1;
+  grid = dim3((unsigned)bx, (unsigned)(ns / spb));
+}
+size_t round_partial_elems(int d, size_t half, int nevals) {
+  int spb;
+  dim3 g;
+  round_geom(d, half, spb, g);
+  return (size_t)g.x * nevals * d;
+}
+
+hipError_t fold_weights(const uint64_t *mu, int nk, int tau, int d, uint64_t *w, hipStream_t st) {
+  const int tb = slot_words(d), n = nk * (d / tb);
+  if (tb == 3)
+    hipLaunchKernelGGL(k_fold_weights<3>, dim3(blocks_of(n, 256)), dim3(256), 0, st, mu, nk, tau, d, w);
+  else
+    hipLaunchKernelGGL(k_fold_weights<1>, dim3(blocks_of(n, 256)), dim3(256), 0, st, mu, nk, tau, d, w);
+  return hipGetLastError();
+}
+
+hipError_t round_folding(const uint64_t *mles, size_t stride, int nf, const uint64_t *w, int bsmall, size_t half, int d,
+                         uint64_t *partial, uint64_t *evals, hipStream_t st) {
+  if (bsmall < 1 || bsmall > 4 || !half) return hipErrorInvalidValue;
+  int spb;
+  dim3 grid;
+  round_geom(d, half, spb, grid);
+#define LF_RF(TB, BS)                                                                                           \
+  hipLaunchKernelGGL((k_round_folding<TB, BS>), grid, dim3(RT), 0, st, mles, stride, nf, w, half, d, spb, partial)
+#define LF_RF_BS(TB)          \
+  switch (bsmall) {           \
+    case 1: LF_RF(TB, 1); break; \
+    case 2: LF_RF(TB, 2); break; \
+    case 3: LF_RF(TB, 3); break; \
+    default: LF_RF(TB, 4); break; \
+  }
+  if (slot_words(d) == 3) {
+    LF_RF_BS(3)
+  } else {
+    LF_RF_BS(1)
+  }
+#undef LF_RF_BS
+#undef LF_RF
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const size_t len = (size_t)(2 * bsmall + 1) * d;
+  hipLaunchKernelGGL(k_sum_partials, dim3(blocks_of(len, 256)), dim3(256), 0, st, partial, (int)grid.x, len, evals);
+  return hipGetLastError();
+}
+
+hipError_t round_lin(const uint64_t *mles, size_t stride, int nm, const uint64_t *c, const CombS &cs, int degree,
+                     size_t half, int d, uint64_t *partial, uint64_t *evals, hipStream_t st) {
+  if (degree + 1 > MAX_EVALS || degree < 1 || !half) return hipErrorInvalidValue;
+  int spb;
+  dim3 grid;
+  round_geom(d, half, spb, grid);
+#define LF_RL(TB, DG) \
+  hipLaunchKernelGGL((k_round_lin<TB, DG>), grid, dim3(RT), 0, st, mles, stride, nm, c, cs, half, d, spb, partial)
+#define LF_RL_DEG(TB)                          \
+  switch (degree) {                            \
+    case 1: LF_RL(TB, 1); break;               \
+    case 2: LF_RL(TB, 2); break;               \
+    case 3: LF_RL(TB, 3); break;               \
+    case 4: LF_RL(TB, 4); break;               \
+    case 5: LF_RL(TB, 5); break;               \
+    case 6: LF_RL(TB, 6); break;               \
+    case 7: LF_RL(TB, 7); break;               \
+    case 8: LF_RL(TB, 8); break;               \
+    default: LF_RL(TB, 9); break;              \
+  }
+  if (slot_words(d) == 3) {
+    LF_RL_DEG(3)
+  } else {
+    LF_RL_DEG(1)
+  }
+#undef LF_RL_DEG
+#undef LF_RL
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const size_t len = (size_t)(degree + 1) * d;
+  hipLaunchKernelGGL(k_sum_partials, dim3(blocks_of(len, 256)), dim3(256), 0, st, partial, (int)grid.x, len, evals);
+  return hipGetLastError();
+}
+
+size_t mle_eval_partial_elems(int d, int nm) { return (size_t)64 * nm * d; }
+
+hipError_t mle_dot(const uint64_t *mles, size_t stride, int nm, const uint64_t *eq, size_t n, int d,
+                   uint64_t *partial, uint64_t *out, hipStream_t st) {
+  if (!nm || !n) return hipSuccess;
+  const int tb = slot_words(d), ns = d / tb;
+  const int spb = ns < RT ? ns : RT, ppb = RT / spb;
+  size_t sx = (n + ppb - 1) / ppb;
+  const int nsplit = (int)(sx < 64 ? sx : 64);
+  const dim3 grid((unsigned)nsplit, (unsigned)(ns / spb), (unsigned)nm);
+  if (tb == 3)
+    hipLaunchKernelGGL(k_mle_dot<3>, grid, dim3(RT), 0, st, mles, stride, eq, n, d, spb, nsplit, partial, nm);
+  else
+    hipLaunchKernelGGL(k_mle_dot<1>, grid, dim3(RT), 0, st, mles, stride, eq, n, d, spb, nsplit, partial, nm);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const size_t len = (size_t)nm * d;
+  hipLaunchKernelGGL(k_sum_partials, dim3(blocks_of(len, 256)), dim3(256), 0, st, partial, nsplit, len, out);
+  return hipGetLastError();
+}
+
+}  // namespace lfk

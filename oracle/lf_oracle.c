@@ -782,3 +782,291 @@ void lfo_ajtai_rows_seeded(uint64_t seed, size_t ncols, int d, const uint64_t *f
     }
   free(part);
 }
+
+/* ================================================ multilinear sumcheck (8(f) rank 1)
+ * Ring elements in NTT form (d u64: Phi_72's 8 Fq3 slots, or d Fq slots);
+ * an MLE over nv variables is 2^nv ring elements, zero-padded (the reference's
+ * DenseMultilinearExtension reads missing trailing entries as zero:
+ * PL/mle/dense.rs:397-418). Challenges are base-ring elements (Fq3 for
+ * Phi_72, Fq otherwise) broadcast into every slot (ntt_form.rs:689-692). */
+static int base_deg(int d) { return d == 24 ? 3 : 1; }
+static void ring_add(const uint64_t *a, const uint64_t *b, uint64_t *c, int d) {
+  for (int i = 0; i < d; i++) c[i] = lfo_add(a[i], b[i]);
+}
+static void ring_sub(const uint64_t *a, const uint64_t *b, uint64_t *c, int d) {
+  for (int i = 0; i < d; i++) c[i] = lfo_sub(a[i], b[i]);
+}
+static int ring_is_zero(const uint64_t *a, int d) {
+  for (int i = 0; i < d; i++)
+    if (a[i]) return 0;
+  return 1;
+}
+/* scalar (a base-ring element of base_deg(d) components) into every slot */
+static void ring_from_base(const uint64_t *v, int d, uint64_t *out) {
+  const int t = base_deg(d);
+  for (int i = 0; i < d; i++) out[i] = v[i % t];
+}
+
+/* build_eq_x_r (LF/utils/sumcheck/utils.rs:140-210): eq[x] = prod_k (x_k ? r_k : 1 - r_k),
+ * x_0 the least significant bit; built from r[nv-1] down as the reference's recursion */
+void lfo_eq_table(const uint64_t *r, int nv, int d, uint64_t *out) {
+  size_t len = 2;
+  uint64_t *tmp = malloc(sizeof(uint64_t) * (size_t)d);
+  uint64_t *buf = malloc(sizeof(uint64_t) * ((size_t)d << nv));
+  const uint64_t *rl = r + (size_t)(nv - 1) * d;
+  for (int i = 0; i < d; i++) buf[i] = lfo_sub((d == 24 && i % 3) ? 0 : 1, rl[i]); /* ONE - r */
+  memcpy(buf + d, rl, sizeof(uint64_t) * (size_t)d);
+  for (int k = nv - 2; k >= 0; k--) {
+    const uint64_t *rk = r + (size_t)k * d;
+    for (size_t i = len; i-- > 0;) { /* res[2i] = b_i - r_k b_i, res[2i+1] = r_k b_i */
+      uint64_t *bi = buf + i * d;
+      lfo_slot_mul(rk, bi, tmp, d);
+      ring_sub(bi, tmp, buf + 2 * i * d, d);
+      memcpy(buf + (2 * i + 1) * d, tmp, sizeof(uint64_t) * (size_t)d);
+    }
+    len *= 2;
+  }
+  memcpy(out, buf, sizeof(uint64_t) * ((size_t)d << nv));
+  free(buf);
+  free(tmp);
+}
+
+/* fix_variables with one point (PL/mle/dense.rs:171-199): mle[b] = left + r (right - left),
+ * b < half; the zero short-cut is value-neutral */
+void lfo_mle_fix_first(uint64_t *mle, size_t half, int d, const uint64_t *r) {
+  uint64_t *a = malloc(sizeof(uint64_t) * (size_t)d), *t = malloc(sizeof(uint64_t) * (size_t)d);
+  for (size_t b = 0; b < half; b++) {
+    const uint64_t *left = mle + 2 * b * d, *right = mle + (2 * b + 1) * d;
+    ring_sub(right, left, a, d);
+    if (!ring_is_zero(a, d)) {
+      lfo_slot_mul(r, a, t, d);
+      ring_add(left, t, mle + b * d, d);
+    } else {
+      memmove(mle + b * d, left, sizeof(uint64_t) * (size_t)d);
+    }
+  }
+  free(a);
+  free(t);
+}
+
+/* DenseMultilinearExtension::evaluate (dense.rs:107-113): fix every variable */
+void lfo_mle_evaluate(const uint64_t *mle, int nv, int d, const uint64_t *point, uint64_t *out) {
+  uint64_t *m = malloc(sizeof(uint64_t) * ((size_t)d << nv));
+  memcpy(m, mle, sizeof(uint64_t) * ((size_t)d << nv));
+  for (int i = 0; i < nv; i++) lfo_mle_fix_first(m, (size_t)1 << (nv - 1 - i), d, point + (size_t)i * d);
+  memcpy(out, m, sizeof(uint64_t) * (size_t)d);
+  free(m);
+}
+
+/* the sumcheck polynomials' combination functions (lfo_comb, lf_oracle.h):
+ * kind 0: folding (folding/utils.rs:278-331): 2K instances of tau f_hat MLEs, B_SMALL, mu [nk][d];
+ * kind 1: linearization (linearization/utils.rs:86-104): q multisets, c [q][d], S_off [q+1], S_idx */
+
+static void comb_eval(const lfo_comb *cb, const uint64_t *vals, int d, uint64_t *out) {
+  uint64_t *t0 = malloc(sizeof(uint64_t) * (size_t)d), *t1 = malloc(sizeof(uint64_t) * (size_t)d);
+  uint64_t *t2 = malloc(sizeof(uint64_t) * (size_t)d), *inter = malloc(sizeof(uint64_t) * (size_t)d);
+  if (cb->kind == 0) {
+    /* result = v0 v1 + v2 v3 (eq_r * (g1 + g3) of both halves) */
+    lfo_slot_mul(vals, vals + d, out, d);
+    lfo_slot_mul(vals + 2 * d, vals + 3 * d, t0, d);
+    ring_add(out, t0, out, d);
+    for (int k = 0; k < cb->nk; k++) {
+      const uint64_t *mu = cb->mu + (size_t)k * d;
+      memset(inter, 0, sizeof(uint64_t) * (size_t)d);
+      for (int dd = cb->tau - 1; dd >= 0; dd--) {
+        const uint64_t *f = vals + (size_t)(5 + k * cb->tau + dd) * d;
+        if (ring_is_zero(f, d)) {
+          if (!ring_is_zero(inter, d)) {
+            lfo_slot_mul(inter, mu, t0, d);
+            memcpy(inter, t0, sizeof(uint64_t) * (size_t)d);
+          }
+          continue;
+        }
+        memcpy(t1, vals + 4 * d, sizeof(uint64_t) * (size_t)d); /* eval = eq_beta */
+        lfo_slot_mul(f, f, t2, d);                                /* f^2 */
+        for (int b = 1; b < cb->bsmall; b++) {
+          uint64_t m[4096];
+          const uint64_t bb = (uint64_t)b * (uint64_t)b;
+          for (int i = 0; i < d; i++) m[i] = lfo_sub(t2[i], (d == 24 && i % 3) ? 0 : bb); /* f^2 - b^2 */
+          if (ring_is_zero(m, d)) {
+            memset(t1, 0, sizeof(uint64_t) * (size_t)d);
+            break;
+          }
+          lfo_slot_mul(t1, m, t0, d);
+          memcpy(t1, t0, sizeof(uint64_t) * (size_t)d);
+        }
+        lfo_slot_mul(t1, f, t0, d); /* eval *= f_i */
+        ring_add(inter, t0, inter, d);
+        lfo_slot_mul(inter, mu, t0, d);
+        memcpy(inter, t0, sizeof(uint64_t) * (size_t)d);
+      }
+      ring_add(out, inter, out, d);
+    }
+  } else {
+    memset(out, 0, sizeof(uint64_t) * (size_t)d);
+    for (int i = 0; i < cb->q; i++) {
+      const uint64_t *c = cb->c + (size_t)i * d;
+      if (ring_is_zero(c, d)) continue;
+      memcpy(t1, c, sizeof(uint64_t) * (size_t)d);
+      int skip = 0;
+      for (int s = cb->S_off[i]; s < cb->S_off[i + 1]; s++) {
+        const uint64_t *v = vals + (size_t)cb->S_idx[s] * d; /* vals[j], j the matrix index */
+        if (ring_is_zero(v, d)) {
+          skip = 1;
+          break;
+        }
+        lfo_slot_mul(t1, v, t0, d);
+        memcpy(t1, t0, sizeof(uint64_t) * (size_t)d);
+      }
+      if (!skip) ring_add(out, t1, out, d);
+    }
+    (void)t2;
+  }
+  free(t0);
+  free(t1);
+  free(t2);
+  free(inter);
+}
+/* the combination function at one point of the sumcheck domain: vals [nm][d] -> out */
+void lfo_comb_eval(const lfo_comb *cb, const uint64_t *vals, int nm, int d, uint64_t *out) {
+  if (cb->kind == 1) { /* eq is the last MLE: result * vals[last] */
+    uint64_t *t = malloc(sizeof(uint64_t) * (size_t)d);
+    comb_eval(cb, vals, d, t);
+    lfo_slot_mul(t, vals + (size_t)(nm - 1) * d, out, d);
+    free(t);
+  } else {
+    comb_eval(cb, vals, d, out);
+  }
+}
+
+/* IPForMLSumcheck::prove_round's sum (LF/utils/sumcheck/prover.rs:93-167):
+ * evals[e] = sum_b comb(v_b(e)), v_b(e) = mle[2b] + e (mle[2b+1] - mle[2b]), e <= degree;
+ * mles [nm][2^nv][d] */
+void lfo_sumcheck_round(const lfo_comb *cb, const uint64_t *mles, int nm, int nv, int d, int degree,
+                        uint64_t *evals) {
+  const size_t n = (size_t)1 << nv, half = n / 2;
+  uint64_t *v0 = malloc(sizeof(uint64_t) * (size_t)nm * d), *v1 = malloc(sizeof(uint64_t) * (size_t)nm * d);
+  uint64_t *st = malloc(sizeof(uint64_t) * (size_t)nm * d), *v = malloc(sizeof(uint64_t) * (size_t)nm * d);
+  uint64_t *le = malloc(sizeof(uint64_t) * (size_t)d);
+  memset(evals, 0, sizeof(uint64_t) * (size_t)(degree + 1) * d);
+  for (size_t b = 0; b < half; b++) {
+    for (int m = 0; m < nm; m++) {
+      memcpy(v0 + (size_t)m * d, mles + ((size_t)m * n + 2 * b) * d, sizeof(uint64_t) * (size_t)d);
+      memcpy(v1 + (size_t)m * d, mles + ((size_t)m * n + 2 * b + 1) * d, sizeof(uint64_t) * (size_t)d);
+    }
+    lfo_comb_eval(cb, v0, nm, d, le);
+    ring_add(evals, le, evals, d);
+    lfo_comb_eval(cb, v1, nm, d, le);
+    ring_add(evals + d, le, evals + d, d);
+    for (int m = 0; m < nm; m++) ring_sub(v1 + (size_t)m * d, v0 + (size_t)m * d, st + (size_t)m * d, d);
+    memcpy(v, v1, sizeof(uint64_t) * (size_t)nm * d);
+    for (int e = 2; e <= degree; e++) {
+      for (int m = 0; m < nm; m++) ring_add(v + (size_t)m * d, st + (size_t)m * d, v + (size_t)m * d, d);
+      lfo_comb_eval(cb, v, nm, d, le);
+      ring_add(evals + (size_t)e * d, le, evals + (size_t)e * d, d);
+    }
+  }
+  free(v0);
+  free(v1);
+  free(st);
+  free(v);
+  free(le);
+}
+
+/* MLSumcheck::prove_as_subprotocol (LF/utils/sumcheck.rs:61-88) with the
+ * Poseidon2 transcript: absorb nvars, degree; per round the prover message
+ * (degree + 1 ring elements) is absorbed, the challenge (a base-ring element:
+ * fiat_shamir.rs:69-86 for Fq3; one sample for Fq) sampled and absorbed as a
+ * broadcast ring element, and every MLE's first variable fixed to it.
+ * mles are consumed (fixed in place). proof [nv][degree+1][d], randomness [nv][tau]. */
+void lfo_sumcheck_prove(lfo_transcript *t, const lfo_comb *cb, uint64_t *mles, int nm, int nv, int d, int degree,
+                        uint64_t *proof, uint64_t *randomness) {
+  const int tb = base_deg(d);
+  uint64_t *scal = calloc((size_t)d, sizeof(uint64_t)), *rr = malloc(sizeof(uint64_t) * (size_t)d);
+  uint64_t *work = malloc(sizeof(uint64_t) * (size_t)nm * ((size_t)d << nv));
+  memcpy(work, mles, sizeof(uint64_t) * (size_t)nm * ((size_t)d << nv));
+  uint64_t sv[3] = {(uint64_t)nv, 0, 0};
+  ring_from_base(sv, d, scal); /* R::from(nvars as u128) */
+  lfo_tr_absorb_ring(t, scal, 1, d);
+  sv[0] = (uint64_t)degree;
+  ring_from_base(sv, d, scal);
+  lfo_tr_absorb_ring(t, scal, 1, d);
+  for (int i = 0; i < nv; i++) {
+    const int cur = nv - i; /* variables left */
+    const size_t n = (size_t)1 << cur;
+    /* the MLEs of this round are the first 2^cur entries of each (stride 2^nv) */
+    uint64_t *tmp = malloc(sizeof(uint64_t) * (size_t)nm * n * d);
+    for (int m = 0; m < nm; m++)
+      memcpy(tmp + (size_t)m * n * d, work + (size_t)m * ((size_t)d << nv), sizeof(uint64_t) * n * d);
+    uint64_t *msg = proof + (size_t)i * (degree + 1) * d;
+    lfo_sumcheck_round(cb, tmp, nm, cur, d, degree, msg);
+    free(tmp);
+    lfo_tr_absorb_ring(t, msg, (size_t)degree + 1, d);
+    uint64_t *ch = randomness + (size_t)i * tb;
+    if (tb == 3) {
+      lfo_tr_get_challenge(t, ch);
+    } else {
+      ch[0] = lfo_tr_sample(t);
+      lfo_tr_observe(t, ch[0]);
+    }
+    ring_from_base(ch, d, rr);
+    lfo_tr_absorb_ring(t, rr, 1, d);
+    for (int m = 0; m < nm; m++) lfo_mle_fix_first(work + (size_t)m * ((size_t)d << nv), n / 2, d, rr);
+  }
+  memcpy(mles, work, sizeof(uint64_t) * (size_t)nm * ((size_t)d << nv));
+  free(work);
+  free(scal);
+  free(rr);
+}
+
+/* the verifier's check (LF/utils/sumcheck/verifier.rs:100-129) with
+ * interpolate_uni_poly (:143-222) as plain Lagrange interpolation at 0..degree:
+ * p(0) + p(1) = expected each round, expected <- p(r). Returns 0 and the final
+ * expected evaluation, or -1 - round when a round's sum is wrong. */
+int lfo_sumcheck_check(const uint64_t *proof, const uint64_t *randomness, int nv, int d, int degree,
+                       const uint64_t *asserted_sum, uint64_t *expected_out) {
+  const int tb = base_deg(d);
+  uint64_t *exp = malloc(sizeof(uint64_t) * (size_t)d), *s = malloc(sizeof(uint64_t) * (size_t)d);
+  uint64_t *rr = malloc(sizeof(uint64_t) * (size_t)d), *acc = malloc(sizeof(uint64_t) * (size_t)d);
+  uint64_t *w = malloc(sizeof(uint64_t) * (size_t)d), *t = malloc(sizeof(uint64_t) * (size_t)d);
+  memcpy(exp, asserted_sum, sizeof(uint64_t) * (size_t)d);
+  int rc = 0;
+  for (int i = 0; i < nv && !rc; i++) {
+    const uint64_t *ev = proof + (size_t)i * (degree + 1) * d;
+    ring_add(ev, ev + d, s, d);
+    if (memcmp(s, exp, sizeof(uint64_t) * (size_t)d)) {
+      rc = -1 - i;
+      break;
+    }
+    ring_from_base(randomness + (size_t)i * tb, d, rr);
+    memset(acc, 0, sizeof(uint64_t) * (size_t)d);
+    for (int k = 0; k <= degree; k++) { /* L_k(r) = prod_{j != k} (r - j) / (k - j) */
+      uint64_t num[4096];
+      uint64_t one[3] = {1, 0, 0};
+      ring_from_base(one, d, num);
+      uint64_t den = 1;
+      for (int j = 0; j <= degree; j++) {
+        if (j == k) continue;
+        uint64_t jj[3] = {(uint64_t)j, 0, 0}, tmp[4096];
+        ring_from_base(jj, d, tmp);
+        ring_sub(rr, tmp, tmp, d);
+        lfo_slot_mul(num, tmp, w, d);
+        memcpy(num, w, sizeof(uint64_t) * (size_t)d);
+        den = lfo_mul(den, k > j ? (uint64_t)(k - j) : P - (uint64_t)(j - k));
+      }
+      const uint64_t dinv = lfo_inv(den);
+      for (int c = 0; c < d; c++) num[c] = lfo_mul(num[c], dinv);
+      lfo_slot_mul(num, ev + (size_t)k * d, t, d);
+      ring_add(acc, t, acc, d);
+    }
+    memcpy(exp, acc, sizeof(uint64_t) * (size_t)d);
+  }
+  memcpy(expected_out, exp, sizeof(uint64_t) * (size_t)d);
+  free(exp);
+  free(s);
+  free(rr);
+  free(acc);
+  free(w);
+  free(t);
+  return rc;
+}

@@ -131,6 +131,28 @@ void lfo_tr_absorb_ring(lfo_transcript *t, const uint64_t *elems, size_t n, int 
 void lfo_tr_get_challenge(lfo_transcript *t, uint64_t out[3]);
 void lfo_tr_squeeze_bytes(lfo_transcript *t, uint8_t *out, size_t n);
 
+/* ---- multilinear sumcheck (8(f) rank 1): LF/utils/sumcheck*, PL/mle/dense.rs ----
+ * ring elements in NTT form (d u64); MLEs over nv variables: 2^nv elements */
+void lfo_eq_table(const uint64_t *r, int nv, int d, uint64_t *out);
+void lfo_mle_fix_first(uint64_t *mle, size_t half, int d, const uint64_t *r);
+void lfo_mle_evaluate(const uint64_t *mle, int nv, int d, const uint64_t *point, uint64_t *out);
+typedef struct {
+  int kind; /* 0 folding, 1 linearization */
+  int nk, tau, bsmall;
+  const uint64_t *mu;
+  int q;
+  const uint64_t *c;
+  const int *S_off;
+  const int *S_idx;
+} lfo_comb;
+void lfo_comb_eval(const lfo_comb *cb, const uint64_t *vals, int nm, int d, uint64_t *out);
+void lfo_sumcheck_round(const lfo_comb *cb, const uint64_t *mles, int nm, int nv, int d, int degree,
+                        uint64_t *evals);
+void lfo_sumcheck_prove(lfo_transcript *t, const lfo_comb *cb, uint64_t *mles, int nm, int nv, int d, int degree,
+                        uint64_t *proof, uint64_t *randomness);
+int lfo_sumcheck_check(const uint64_t *proof, const uint64_t *randomness, int nv, int d, int degree,
+                       const uint64_t *asserted_sum, uint64_t *expected_out);
+
 /* ---- seeded synthetic inputs: SplitMix64 stream, rejection to [0,p) ---- */
 void lfo_fill_uniform(uint64_t *out, size_t n, uint64_t seed);
 /* rows[0..nrows) of A f for A = lfo_fill_uniform(seed) as kappa x ncols x d

@@ -36,6 +36,11 @@ class Transcript(C.Structure):
                 ("outbuf", U64 * 12), ("nout", I)]
 
 
+class Comb(C.Structure):
+    _fields_ = [("kind", I), ("nk", I), ("tau", I), ("bsmall", I), ("mu", C.c_void_p), ("q", I),
+                ("c", C.c_void_p), ("S_off", C.c_void_p), ("S_idx", C.c_void_p)]
+
+
 def lib():
     global _lib
     if _lib is not None:
@@ -75,6 +80,13 @@ def lib():
         "lfo_fill_uniform": (None, [u64p, SZ, U64]),
         "lfo_ajtai_rows_seeded": (None, [U64, SZ, I, u64p, u64p, SZ, u64p, I]),
         "lfo_rot_lin_combination": (None, [u64p, u64p, SZ, I, u64p]),
+        "lfo_eq_table": (None, [u64p, I, I, u64p]),
+        "lfo_mle_fix_first": (None, [u64p, SZ, I, u64p]),
+        "lfo_mle_evaluate": (None, [u64p, I, I, u64p, u64p]),
+        "lfo_comb_eval": (None, [C.POINTER(Comb), u64p, I, I, u64p]),
+        "lfo_sumcheck_round": (None, [C.POINTER(Comb), u64p, I, I, I, I, u64p]),
+        "lfo_sumcheck_prove": (None, [C.POINTER(Transcript), C.POINTER(Comb), u64p, I, I, I, I, u64p, u64p]),
+        "lfo_sumcheck_check": (I, [u64p, u64p, I, I, I, u64p, u64p]),
         "lfo_compute_x_s": (I, [u64p, SZ, I, U64, I, U64, I, u64p]),
     }
     for name, (res, args) in sig.items():
@@ -237,6 +249,81 @@ def compute_x_s(x, d: int, B: int, L: int, b_small: int, K: int) -> np.ndarray:
     if lib().lfo_compute_x_s(xx, m, d, B, L, b_small, K, out):
         raise ValueError("compute_x_s: decomposition overflow")
     return out
+
+
+# ---------------------------------------------------------------- multilinear sumcheck
+class SumcheckComb:
+    """the combination function (lfo_comb): keeps its arrays alive"""
+
+    def __init__(self, kind, nk=0, tau=0, bsmall=2, mu=None, c=None, S=None):
+        self.keep = []
+        mu_p = c_p = off_p = idx_p = None
+        if mu is not None:
+            mu = _u64(mu)
+            self.keep.append(mu)
+            mu_p = mu.ctypes.data
+        q = 0
+        if S is not None:
+            c = _u64(c)
+            off = np.zeros(len(S) + 1, np.int32)
+            off[1:] = np.cumsum([len(x) for x in S])
+            idx = np.array([j for x in S for j in x] or [0], np.int32)
+            self.keep += [c, off, idx]
+            c_p, off_p, idx_p, q = c.ctypes.data, off.ctypes.data, idx.ctypes.data, len(S)
+        self.s = Comb(kind, nk, tau, bsmall, mu_p, q, c_p, off_p, idx_p)
+
+    @classmethod
+    def folding(cls, mu, nk, tau, bsmall=2):
+        return cls(0, nk=nk, tau=tau, bsmall=bsmall, mu=mu)
+
+    @classmethod
+    def linearization(cls, c, S):
+        return cls(1, c=c, S=S)
+
+
+def eq_table(r, nv: int, d: int) -> np.ndarray:
+    out = np.zeros((d << nv), np.uint64)
+    lib().lfo_eq_table(_u64(r), nv, d, out)
+    return out
+
+
+def mle_evaluate(mle, nv: int, d: int, point) -> np.ndarray:
+    out = np.zeros(d, np.uint64)
+    lib().lfo_mle_evaluate(_u64(mle), nv, d, _u64(point), out)
+    return out
+
+
+def comb_eval(comb: SumcheckComb, vals, nm: int, d: int) -> np.ndarray:
+    out = np.zeros(d, np.uint64)
+    lib().lfo_comb_eval(C.byref(comb.s), _u64(vals), nm, d, out)
+    return out
+
+
+def sumcheck_round(comb: SumcheckComb, mles, nm: int, nv: int, d: int, degree: int) -> np.ndarray:
+    out = np.zeros((degree + 1) * d, np.uint64)
+    lib().lfo_sumcheck_round(C.byref(comb.s), _u64(mles), nm, nv, d, degree, out)
+    return out
+
+
+def sumcheck_prove(t: Transcript, comb: SumcheckComb, mles, nm: int, nv: int, d: int, degree: int):
+    m = _u64(mles).copy()
+    tau = 3 if d == 24 else 1
+    proof = np.zeros(nv * (degree + 1) * d, np.uint64)
+    rnd = np.zeros(nv * tau, np.uint64)
+    lib().lfo_sumcheck_prove(C.byref(t), C.byref(comb.s), m, nm, nv, d, degree, proof, rnd)
+    return proof, rnd
+
+
+def sumcheck_check(proof, randomness, nv: int, d: int, degree: int, asserted_sum):
+    out = np.zeros(d, np.uint64)
+    rc = lib().lfo_sumcheck_check(_u64(proof), _u64(randomness), nv, d, degree, _u64(asserted_sum), out)
+    return rc, out
+
+
+def broadcast(base, d: int) -> np.ndarray:
+    """a base-ring element (tau words) in every NTT slot"""
+    b = _u64(base)
+    return np.tile(b, d // b.size)
 
 
 # ---------------------------------------------------------------- Poseidon2

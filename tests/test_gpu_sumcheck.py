@@ -1,0 +1,151 @@
+"""GPU parity of the multilinear sumcheck prover
+against the oracle's restatement: eq tables, fix_variables, MLE evaluation,
+single round sums of the folding and linearization polynomials, and whole
+proofs through the Poseidon2 transcript (bit-identical messages and
+challenges). At the reference's real shape (Phi_72, 17 variables, the 95 MLEs
+of the folding polynomial) the device proof is checked with the oracle's
+verifier (round sums, interpolation) and its final claim against the MLEs
+evaluated at the challenge point."""
+import numpy as np
+import pytest
+
+import latticeum_amd as LA
+import oracle as O
+from test_sumcheck_oracle import final_claim, folding_case
+
+pytestmark = pytest.mark.gpu
+P = LA.P
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+    c = LA.Context(0)
+    c.set_stream(torch.cuda.current_stream().cuda_stream)
+    yield c
+    c.close()
+
+
+def dev(x=None, n=None):
+    import torch
+    if x is not None:
+        return torch.from_numpy(np.ascontiguousarray(x).view(np.int64)).cuda()
+    return torch.zeros(n, dtype=torch.int64, device="cuda")
+
+
+def host(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+def rand(n, seed):
+    return O.fill_uniform(n, seed)
+
+
+@pytest.mark.parametrize("d,nv", [(24, 6), (16, 5), (1024, 3)])
+def test_eq_table_fix_evaluate(ctx, d, nv):
+    n = 1 << nv
+    r = rand(nv * d, 10 + d)
+    eq = dev(n=n * d)
+    ctx.dev_eq_table(d, dev(r), nv, eq)
+    ctx.sync()
+    assert np.array_equal(host(eq), O.eq_table(r, nv, d))
+    nm = 3
+    mles = rand(nm * n * d, 11 + d)
+    out = dev(n=nm * d)
+    ctx.dev_mle_evaluate(d, dev(mles), nm, nv, dev(r), out)
+    ctx.sync()
+    want = np.concatenate([O.mle_evaluate(mles[m * n * d:(m + 1) * n * d], nv, d, r) for m in range(nm)])
+    assert np.array_equal(host(out), want)
+    tau = 3 if d == 24 else 1
+    rb = rand(tau, 12 + d)
+    fixed = dev(n=nm * (n // 2) * d)
+    ctx.dev_mle_fix_first(d, dev(mles), n * d, nm, nv, rb, fixed, (n // 2) * d)
+    ctx.sync()
+    for m in range(nm):
+        ref = mles[m * n * d:(m + 1) * n * d].copy()
+        O.lib().lfo_mle_fix_first(ref, n // 2, d, O.broadcast(rb, d))
+        assert np.array_equal(host(fixed)[m * (n // 2) * d:(m + 1) * (n // 2) * d], ref[:(n // 2) * d])
+
+
+@pytest.mark.parametrize("d,nv,nk,tau", [(24, 6, 30, 3), (16, 5, 4, 1), (1024, 2, 3, 1), (24, 1, 2, 3)])
+def test_folding_round_matches_oracle(ctx, d, nv, nk, tau):
+    mles, mu, nm = folding_case(d, nv, nk, tau, 500 + d + nv)
+    comb = O.SumcheckComb.folding(mu, nk, tau, 2)
+    want = O.sumcheck_round(comb, mles, nm, nv, d, 4)
+    ev = dev(n=5 * d)
+    ctx.dev_sumcheck_round(LA.Comb.folding(dev(mu), nk, tau, 2), dev(mles), (1 << nv) * d, nm, nv, d, 4, ev)
+    ctx.sync()
+    assert np.array_equal(host(ev), want)
+
+
+def lin_case(d, nv, seed):
+    """a CCS with degree-3 and degree-1 multisets and a zero coefficient: c = [3, 0, -1, 5],
+    S = [[0, 1, 2], [1], [3], [0, 3]]; the MLE list as prepare_lin_sumcheck_polynomial builds it"""
+    n = 1 << nv
+    one = np.zeros(d, np.uint64)
+    one[::3 if d == 24 else 1] = 1
+    c = np.concatenate([one * np.uint64(3), np.zeros(d, np.uint64), np.where(one == 1, np.uint64(P - 1), np.uint64(0)),
+                        rand(d, seed)])
+    S = [[0, 1, 2], [1], [3], [0, 3]]
+    mz = [rand(n * d, seed + 1 + j) for j in range(4)]
+    beta = rand(nv * d, seed + 9)
+    lst = [mz[j] for i, s_ in enumerate(S) if i != 1 for j in s_]
+    mles = np.concatenate(lst + [O.eq_table(beta, nv, d)])
+    return c, S, mles, len(lst) + 1
+
+
+@pytest.mark.parametrize("d,nv", [(24, 5), (64, 4)])
+def test_linearization_round_matches_oracle(ctx, d, nv):
+    c, S, mles, nm = lin_case(d, nv, 600 + d)
+    want = O.sumcheck_round(O.SumcheckComb.linearization(c, S), mles, nm, nv, d, 4)
+    ev = dev(n=5 * d)
+    ctx.dev_sumcheck_round(LA.Comb.linearization(dev(c), S), dev(mles), (1 << nv) * d, nm, nv, d, 4, ev)
+    ctx.sync()
+    assert np.array_equal(host(ev), want)
+
+
+@pytest.mark.parametrize("d,nv,nk,tau", [(24, 7, 30, 3), (16, 6, 5, 1)])
+def test_folding_prove_matches_oracle(ctx, d, nv, nk, tau):
+    mles, mu, nm = folding_case(d, nv, nk, tau, 700 + d)
+    want_p, want_r = O.sumcheck_prove(O.new_transcript(), O.SumcheckComb.folding(mu, nk, tau, 2), mles, nm, nv, d, 4)
+    t = LA.Poseidon2Transcript()
+    proof, rnd = ctx.sumcheck_prove(t, LA.Comb.folding(dev(mu), nk, tau, 2), dev(mles), nm, nv, d, 4)
+    assert np.array_equal(proof, want_p) and np.array_equal(rnd, want_r)
+
+
+def test_linearization_prove_matches_oracle(ctx):
+    d, nv = 24, 6
+    c, S, mles, nm = lin_case(d, nv, 800)
+    want_p, want_r = O.sumcheck_prove(O.new_transcript(), O.SumcheckComb.linearization(c, S), mles, nm, nv, d, 4)
+    proof, rnd = ctx.sumcheck_prove(LA.Poseidon2Transcript(), LA.Comb.linearization(dev(c), S), dev(mles), nm, nv,
+                                    d, 4)
+    assert np.array_equal(proof, want_p) and np.array_equal(rnd, want_r)
+
+
+def test_folding_sumcheck_real_shape(ctx):
+    """the zkvm's folding sumcheck: Phi_72, log m = 17, 2K = 30 instances of
+    tau = 3 f_hat MLEs (95 MLEs, 2.4 GB): the device proof passes the oracle's
+    verifier and its final claim is the combination at the evaluated MLEs"""
+    import torch
+    d, nv, nk, tau = 24, 17, 30, 3
+    n = 1 << nv
+    nm = 5 + nk * tau
+    m = dev(n=nm * n * d)
+    ctx.dev_fill_uniform(m, 900)
+    r = dev(rand(3 * nv * d, 901))
+    for i, k in enumerate((0, 2, 4)):  # the eq MLEs
+        ctx.dev_eq_table(d, r[i * nv * d:(i + 1) * nv * d], nv, m[k * n * d:(k + 1) * n * d])
+    mu = rand(nk * d, 902)
+    keep = m.clone()
+    proof, rnd = ctx.sumcheck_prove(LA.Poseidon2Transcript(), LA.Comb.folding(dev(mu), nk, tau, 2), m, nm, nv, d, 4)
+    asserted = np.array([(int(a) + int(b)) % P for a, b in zip(proof[:d], proof[d:2 * d])], np.uint64)
+    rc, expected = O.sumcheck_check(proof, rnd, nv, d, 4, asserted)
+    assert rc == 0
+    point = np.concatenate([O.broadcast(rnd[i * tau:(i + 1) * tau], d) for i in range(nv)])
+    vals = dev(n=nm * d)
+    ctx.dev_mle_evaluate(d, keep, nm, nv, dev(point), vals)
+    ctx.sync()
+    comb = O.SumcheckComb.folding(mu, nk, tau, 2)
+    assert np.array_equal(expected, O.comb_eval(comb, host(vals), nm, d))
+    del keep, m
+    torch.cuda.empty_cache()
