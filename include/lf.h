@@ -64,6 +64,7 @@ typedef struct lf_ctx lf_ctx;
 typedef struct lf_ajtai lf_ajtai;
 typedef struct lf_transcript lf_transcript;
 typedef struct lf_comm lf_comm;
+typedef struct lf_ccs lf_ccs;
 
 enum lf_status {
   LF_OK = 0,
@@ -336,6 +337,27 @@ int lf_dev_sumcheck_round(lf_ctx *ctx, const lf_comb *comb, const uint64_t *mles
  * and randomness [nv][1 or 3] in host memory; the MLEs are clobbered */
 int lf_sumcheck_prove(lf_ctx *ctx, lf_transcript *t, const lf_comb *comb, uint64_t *mles, int nm, int nv, int d,
                       int degree, uint64_t *proof, uint64_t *randomness);
+
+/* ------------------------------------------------------------ sparse Mz products
+ * CCS.M (latticefold/src/arith.rs:51-74): t matrices m x n of ring elements,
+ * given as one CSR: row_ptr [t][m + 1] absolute offsets into col / val
+ * (matrix j's entries follow matrix j-1's), col, val [nnz][d] (NTT form).
+ *   lf_dev_mz_mles: calculate_Mz_mles / compute_mz_mles (mle_helpers.rs:137-146,
+ *     nifs/decomposition.rs:229-256): out [nz][t][2^nv] = MLE(M_j z_i), mat_vec_mul
+ *     (arith/utils.rs:52-65) zero-padded to 2^nv (to_mles_err)
+ *   lf_dev_mz_challenged: calculate_challenged_mz_mle (nifs/folding.rs:208-234):
+ *     out [2^nv] = sum_i sum_j zeta_i^(j+1) MLE(M_j z_i); zeta: nz NTT elements
+ *   lf_dev_mz_evaluate: evaluate_mles of every MLE(M_j z_i) at point (compute_u_s,
+ *     get_etas, compute_u): out [nz][t]; point: nv NTT elements
+ * z: nz vectors [nz][n] (decomposed statement || w_ccs); all device buffers. */
+int lf_ccs_create(lf_ctx *ctx, int d, int t, size_t m, size_t n, const uint64_t *row_ptr, const uint32_t *col,
+                  const uint64_t *val, int repr, lf_ccs **out);
+void lf_ccs_destroy(lf_ccs *M);
+int lf_dev_mz_mles(lf_ctx *ctx, const lf_ccs *M, const uint64_t *z, int nz, int nv, uint64_t *out);
+int lf_dev_mz_challenged(lf_ctx *ctx, const lf_ccs *M, const uint64_t *z, const uint64_t *zeta, int nz, int nv,
+                         uint64_t *out);
+int lf_dev_mz_evaluate(lf_ctx *ctx, const lf_ccs *M, const uint64_t *z, int nz, int nv, const uint64_t *point,
+                       uint64_t *out);
 
 /* ------------------------------------------------------------ host transcript (sequential) */
 lf_transcript *lf_transcript_new(void);

@@ -369,6 +369,45 @@ class Comb:
         return cls(LfComb(kind=1, q=len(S), c=_dptr(c_dev), S_off=_ptr(off), S_idx=_ptr(idx)), [c_dev, off, idx])
 
 
+class CCSMatrices:
+    """CCS.M on the device (lf_ccs): t sparse m x n matrices of ring elements,
+    given as (row_ptr, col, val) per matrix (row_ptr relative to that matrix)."""
+
+    def __init__(self, ctx: Context, d: int, m: int, n: int, mats, repr: int = REPR_CANONICAL):
+        self.ctx, self.lib = ctx, ctx.lib
+        rps, cols, vals, base = [], [], [], 0
+        for rp, col, val in mats:
+            rp = np.asarray(rp, np.uint64)
+            rps.append(rp + np.uint64(base))
+            base += int(rp[-1])
+            cols.append(np.asarray(col, np.uint32))
+            vals.append(_u64(val))
+        row_ptr = np.ascontiguousarray(np.concatenate(rps))
+        col = np.ascontiguousarray(np.concatenate(cols)) if base else np.zeros(1, np.uint32)
+        val = np.ascontiguousarray(np.concatenate(vals)) if base else np.zeros(d, np.uint64)
+        h = C.c_void_p()
+        ctx.check(self.lib.lf_ccs_create(ctx.h, d, len(mats), m, n, _ptr(row_ptr), _ptr(col), _ptr(val), repr,
+                                         C.byref(h)))
+        self.h, self.d, self.t, self.m, self.n = h, d, len(mats), m, n
+
+    def mz_mles(self, z, nz: int, nv: int, out):
+        self.ctx.check(self.lib.lf_dev_mz_mles(self.ctx.h, self.h, _dptr(z), nz, nv, _dptr(out)))
+
+    def mz_challenged(self, z, zeta, nz: int, nv: int, out):
+        self.ctx.check(self.lib.lf_dev_mz_challenged(self.ctx.h, self.h, _dptr(z), _dptr(zeta), nz, nv, _dptr(out)))
+
+    def mz_evaluate(self, z, nz: int, nv: int, point, out):
+        self.ctx.check(self.lib.lf_dev_mz_evaluate(self.ctx.h, self.h, _dptr(z), nz, nv, _dptr(point), _dptr(out)))
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.lib.lf_ccs_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
 def witness_split_w() -> int:
     """W below which the d = 1024 witness kernels split elements by limb (lf.h)."""
     return load().lf_witness_split_w()
@@ -474,7 +513,7 @@ def hash_iter(vals) -> np.ndarray:
     return out
 
 
-__all__ = ["Context", "AjtaiCommitmentScheme", "Communicator", "Comb", "witness_split_w", "Poseidon2Transcript",
+__all__ = ["Context", "AjtaiCommitmentScheme", "Communicator", "Comb", "CCSMatrices", "witness_split_w", "Poseidon2Transcript",
            "LfParams", "LfFoldStepBufs",
            "LfError", "goldilocks_dp", "short_challenge", "hash_iter", "P", "REPR_CANONICAL",
            "REPR_MONTGOMERY", "load"]

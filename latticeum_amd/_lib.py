@@ -95,6 +95,11 @@ SIGNATURES = {
     "lf_hash_iter": (None, [VP, SZ, VP]),
     "lf_witness_split_w": (SZ, []),
     "lf_dev_eq_table": (I, [VP, I, VP, I, VP]),
+    "lf_ccs_create": (I, [VP, I, I, SZ, SZ, VP, VP, VP, I, C.POINTER(VP)]),
+    "lf_ccs_destroy": (None, [VP]),
+    "lf_dev_mz_mles": (I, [VP, VP, VP, I, I, VP]),
+    "lf_dev_mz_challenged": (I, [VP, VP, VP, VP, I, I, VP]),
+    "lf_dev_mz_evaluate": (I, [VP, VP, VP, I, I, VP, VP]),
     "lf_dev_mle_fix_first": (I, [VP, I, VP, SZ, I, I, VP, VP, SZ]),
     "lf_dev_mle_evaluate": (I, [VP, I, VP, I, I, VP, VP]),
     "lf_dev_sumcheck_round": (I, [VP, C.POINTER(LfComb), VP, SZ, I, I, I, I, VP]),

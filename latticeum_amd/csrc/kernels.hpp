@@ -140,4 +140,31 @@ size_t mle_eval_partial_elems(int d, int nm);
 hipError_t mle_dot(const uint64_t *mles, size_t stride, int nm, const uint64_t *eq, size_t n, int d,
                    uint64_t *partial, uint64_t *out, hipStream_t st);
 
+// ---------------------------------------------------------------- sparse Mz products (mz.hip)
+// the t CCS matrices (m x n, ring-element CSR) on the device, with the
+// row-merged [M_0 | .. | M_(t-1)] and the per-matrix transposes as index arrays
+// into the one value array
+struct CcsDev {
+  int d, t;
+  size_t m, n;
+  const uint64_t *rp;  // [t][m + 1], absolute offsets into col / val
+  const uint32_t *col;
+  const uint64_t *val;  // [nnz][d]
+  const uint64_t *hrp;  // [m + 1]
+  const uint32_t *hcol;  // j n + col
+  const uint32_t *hidx;  // value index
+  const uint64_t *crp;  // [t][n + 1]
+  const uint32_t *crow;
+  const uint32_t *cidx;
+};
+size_t mz_scratch_elems(const CcsDev &M, int nz, int nv);
+// out [nz][t][2^nv][d] = MLE(M_j z_i), zero-padded; z [nz][n][d]
+hipError_t mz_mles(const CcsDev &M, const uint64_t *z, int nz, int nv, uint64_t *out, hipStream_t st);
+// out [2^nv][d] = sum_i sum_j zeta_i^(j+1) MLE(M_j z_i)
+hipError_t mz_challenged(const CcsDev &M, const uint64_t *z, const uint64_t *zeta, int nz, int nv, uint64_t *out,
+                         uint64_t *scratch, hipStream_t st);
+// out [nz][t][d] = MLE(M_j z_i)(point)
+hipError_t mz_evaluate(const CcsDev &M, const uint64_t *z, int nz, int nv, const uint64_t *point, uint64_t *out,
+                       uint64_t *scratch, hipStream_t st);
+
 }  // namespace lfk

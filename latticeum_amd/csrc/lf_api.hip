@@ -72,6 +72,13 @@ struct lf_ajtai {
   int d = 0;
 };
 
+// the CCS matrices on the device (lf_ccs_create)
+struct lf_ccs {
+  int device = 0;
+  lfk::CcsDev dev{};
+  std::vector<void *> bufs;
+};
+
 // a communicator for the accumulator exchange (RCCL over xGMI)
 struct lf_comm {
   ncclComm_t comm = nullptr;
@@ -1248,6 +1255,133 @@ int lf_sumcheck_prove(lf_ctx *c, lf_transcript *t, const lf_comb *cb, uint64_t *
       stride = half * d;
     }
   }
+  return LF_OK;
+}
+
+// ---------------------------------------------------------------- sparse Mz products
+void lf_ccs_destroy(lf_ccs *M) {
+  if (!M) return;
+  DevGuard g(M->device);
+  for (void *p : M->bufs) (void)hipFree(p);
+  delete M;
+}
+
+int lf_ccs_create(lf_ctx *c, int d, int t, size_t m, size_t n, const uint64_t *row_ptr, const uint32_t *col,
+                  const uint64_t *val, int repr, lf_ccs **out) {
+  if (!c || !out || t < 1 || !m || !n || !row_ptr) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  LF_TRY(check_repr(c, repr));
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  *out = nullptr;
+  const size_t nnz = row_ptr[(size_t)t * (m + 1) - 1];
+  if (nnz >= (1ull << 32) || (nnz && (!col || !val)) || (size_t)t * n >= (1ull << 32))
+    return fail(c, LF_ERR_INVALID_ARG, "CCS: nnz and t n must fit 32-bit indices");
+  for (int j = 0; j < t; j++) {
+    const uint64_t *rp = row_ptr + (size_t)j * (m + 1);
+    for (size_t r = 0; r < m; r++)
+      if (rp[r] > rp[r + 1]) return fail(c, LF_ERR_INVALID_ARG, "CCS: row offsets must not decrease");
+    if (j && rp[0] != row_ptr[(size_t)j * (m + 1) - 1]) return fail(c, LF_ERR_INVALID_ARG, "CCS: matrices must be contiguous");
+  }
+  for (size_t k = 0; k < nnz; k++)
+    if (col[k] >= n) return fail(c, LF_ERR_INVALID_ARG, "CCS: column index out of range");
+  // the row-merged matrix (SparseMatrix::hconcat) and the per-matrix transposes
+  std::vector<uint64_t> hrp(m + 1, 0), crp((size_t)t * (n + 1), 0);
+  std::vector<uint32_t> hcol(nnz), hidx(nnz), crow(nnz), cidx(nnz);
+  for (int j = 0; j < t; j++)
+    for (size_t r = 0; r < m; r++) hrp[r + 1] += row_ptr[(size_t)j * (m + 1) + r + 1] - row_ptr[(size_t)j * (m + 1) + r];
+  for (size_t r = 0; r < m; r++) hrp[r + 1] += hrp[r];
+  {
+    std::vector<uint64_t> fill(hrp.begin(), hrp.end() - 1);
+    for (size_t r = 0; r < m; r++)
+      for (int j = 0; j < t; j++)
+        for (uint64_t k = row_ptr[(size_t)j * (m + 1) + r]; k < row_ptr[(size_t)j * (m + 1) + r + 1]; k++) {
+          hcol[fill[r]] = (uint32_t)(j * n + col[k]);
+          hidx[fill[r]++] = (uint32_t)k;
+        }
+  }
+  for (int j = 0; j < t; j++) {
+    uint64_t *cp = crp.data() + (size_t)j * (n + 1);
+    const uint64_t *rp = row_ptr + (size_t)j * (m + 1);
+    for (uint64_t k = rp[0]; k < rp[m]; k++) cp[col[k] + 1]++;
+    cp[0] = rp[0];
+    for (size_t q = 0; q < n; q++) cp[q + 1] += cp[q];
+    std::vector<uint64_t> fill(cp, cp + n);
+    for (size_t r = 0; r < m; r++)
+      for (uint64_t k = rp[r]; k < rp[r + 1]; k++) {
+        crow[fill[col[k]]] = (uint32_t)r;
+        cidx[fill[col[k]]++] = (uint32_t)k;
+      }
+  }
+  auto M = std::make_unique<lf_ccs>();
+  M->device = c->device;
+  auto put = [&](const void *h, size_t bytes, void **dst) -> int {
+    LF_HIP(c, hipMalloc(dst, bytes ? bytes : 8));
+    M->bufs.push_back(*dst);
+    if (bytes) LF_HIP(c, hipMemcpyAsync(*dst, h, bytes, hipMemcpyHostToDevice, c->cur));
+    return LF_OK;
+  };
+  void *p;
+  lfk::CcsDev &D = M->dev;
+  D.d = d;
+  D.t = t;
+  D.m = m;
+  D.n = n;
+  LF_TRY(put(row_ptr, (size_t)t * (m + 1) * 8, &p));
+  D.rp = (const uint64_t *)p;
+  LF_TRY(put(col, nnz * 4, &p));
+  D.col = (const uint32_t *)p;
+  LF_TRY(put(val, nnz * d * 8, &p));
+  D.val = (const uint64_t *)p;
+  if (repr == LF_REPR_MONTGOMERY && nnz) LF_HIP(c, lfk::mont((uint64_t *)p, nnz * d, false, c->cur));
+  LF_TRY(put(hrp.data(), hrp.size() * 8, &p));
+  D.hrp = (const uint64_t *)p;
+  LF_TRY(put(hcol.data(), nnz * 4, &p));
+  D.hcol = (const uint32_t *)p;
+  LF_TRY(put(hidx.data(), nnz * 4, &p));
+  D.hidx = (const uint32_t *)p;
+  LF_TRY(put(crp.data(), crp.size() * 8, &p));
+  D.crp = (const uint64_t *)p;
+  LF_TRY(put(crow.data(), nnz * 4, &p));
+  D.crow = (const uint32_t *)p;
+  LF_TRY(put(cidx.data(), nnz * 4, &p));
+  D.cidx = (const uint32_t *)p;
+  LF_HIP(c, hipStreamSynchronize(c->cur));  // the host vectors go out of scope
+  *out = M.release();
+  return LF_OK;
+}
+
+static int mz_check(lf_ctx *c, const lf_ccs *M, int nz, int nv) {
+  if (!M || nz < 1 || nv < 1) return fail(c, LF_ERR_INVALID_ARG, "CCS products: null matrices or no vectors");
+  if (M->device != c->device) return fail(c, LF_ERR_INVALID_ARG, "CCS matrices live on another device");
+  if (M->dev.m > ((size_t)1 << nv)) return fail(c, LF_ERR_INVALID_ARG, "MLE too short for m rows (to_mles_err)");
+  return LF_OK;
+}
+
+int lf_dev_mz_mles(lf_ctx *c, const lf_ccs *M, const uint64_t *z, int nz, int nv, uint64_t *out) {
+  if (!c || !z || !out) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  LF_TRY(mz_check(c, M, nz, nv));
+  LF_HIP(c, lfk::mz_mles(M->dev, z, nz, nv, out, c->cur));
+  return LF_OK;
+}
+
+int lf_dev_mz_challenged(lf_ctx *c, const lf_ccs *M, const uint64_t *z, const uint64_t *zeta, int nz, int nv,
+                         uint64_t *out) {
+  if (!c || !z || !zeta || !out) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  LF_TRY(mz_check(c, M, nz, nv));
+  LF_TRY(grow(c, c->tmp, c->tmp_elems, lfk::mz_scratch_elems(M->dev, nz, nv)));
+  LF_HIP(c, lfk::mz_challenged(M->dev, z, zeta, nz, nv, out, c->tmp, c->cur));
+  return LF_OK;
+}
+
+int lf_dev_mz_evaluate(lf_ctx *c, const lf_ccs *M, const uint64_t *z, int nz, int nv, const uint64_t *point,
+                       uint64_t *out) {
+  if (!c || !z || !point || !out) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  LF_TRY(mz_check(c, M, nz, nv));
+  LF_TRY(grow(c, c->tmp, c->tmp_elems, lfk::mz_scratch_elems(M->dev, nz, nv)));
+  LF_HIP(c, lfk::mz_evaluate(M->dev, z, nz, nv, point, out, c->tmp, c->cur));
   return LF_OK;
 }
 

@@ -1,0 +1,174 @@
+// mz.hip -- the sparse CCS products of the decomposition and folding provers
+// (SURVEY.md 8(f) rank 2): M_j z MLEs (calculate_Mz_mles, mle_helpers.rs:137-146;
+// compute_mz_mles, nifs/decomposition.rs:229-256), their zeta-challenged
+// combination (calculate_challenged_mz_mle, nifs/folding.rs:208-234) and their
+// evaluations at a point (compute_u_s, decomposition.rs:214-227; get_etas,
+// folding.rs:247-256; compute_u, linearization/utils.rs:24-29).
+//
+// The matrices are CSR of ring elements (SparseMatrix rows of (value, col),
+// linear_algebra/src/sparse_matrix.rs:18-22). mat_vec_mul (arith/utils.rs:52-65)
+// is one thread per (row, NTT slot) summing value (.) z[col] over the row.
+// The challenged combination sum_i sum_j zeta_i^(j+1) M_j z_i is linear, so it
+// runs as y_j = sum_i zeta_i^(j+1) z_i and one product with the row-merged
+// matrix [M_0 | .. | M_(t-1)] (SparseMatrix::hconcat, sparse_matrix.rs:42-70);
+// the evaluations MLE(M_j z_i)(r) = sum_x eq(r, x) (M_j z_i)[x] run as
+// w_j = M_j^T eq(r) and dot products w_j . z_i -- the same field elements
+// without materialising the t x nz MLEs of 2^s ring elements each.
+#include "kernels.hpp"
+#include "slot.hpp"
+
+namespace lfk {
+
+namespace {
+
+constexpr int MT = 256;
+
+// out[task][r] = sum_k val[vidx ? vidx[k] : k] (.) z[col[k]], k in [rp[r], rp[r+1]);
+// task = (a, b) = (task % na, task / na) selects rp + a rp_stride and z + b z_stride
+template <int TB>
+__global__ void __launch_bounds__(MT) k_csr(const uint64_t *rp, size_t rp_stride, int na, const uint32_t *col,
+                                           const uint32_t *vidx, const uint64_t *val, size_t nrows, int d,
+                                           const uint64_t *z, size_t z_stride, uint64_t *out, size_t out_stride,
+                                           int spb) {
+  const int slot_l = threadIdx.x % spb, lane_r = threadIdx.x / spb, rpb = MT / spb;
+  const int slot = blockIdx.z * spb + slot_l;
+  const size_t r = (size_t)blockIdx.x * rpb + lane_r;
+  if (r >= nrows) return;
+  const int task = blockIdx.y, a = task % na, b = task / na;
+  const uint64_t *rpa = rp + a * rp_stride;
+  const uint64_t *zb = z + b * z_stride + slot * TB;
+  Sv<TB> acc = s_zero<TB>();
+  for (uint64_t k = rpa[r], e = rpa[r + 1]; k < e; k++) {
+    const uint64_t vi = vidx ? vidx[k] : k;
+    acc = s_add(acc, s_mul(s_load<TB>(val + vi * d + slot * TB), s_load<TB>(zb + (size_t)col[k] * d)));
+  }
+  s_store(out + task * out_stride + r * d + slot * TB, acc);
+}
+
+// pw[j][i] = zeta_i^(j+1)
+template <int TB>
+__global__ void k_zeta_pows(const uint64_t *zeta, int nz, int t, int d, uint64_t *pw) {
+  const int ns = d / TB;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (instance, slot)
+  if (i >= nz * ns) return;
+  const int zi = i / ns, s = i - zi * ns;
+  const Sv<TB> zt = s_load<TB>(zeta + (size_t)zi * d + s * TB);
+  Sv<TB> p = zt;
+  for (int j = 0; j < t; j++) {
+    s_store(pw + ((size_t)j * nz + zi) * d + s * TB, p);
+    p = s_mul(p, zt);
+  }
+}
+
+// y[j][c] = sum_i pw[j][i] (.) z_i[c]
+template <int TB>
+__global__ void k_zcomb(const uint64_t *pw, const uint64_t *z, int nz, int t, size_t n, int d, uint64_t *y) {
+  const int ns = d / TB;
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // (j, c, slot)
+  if (i >= (size_t)t * n * ns) return;
+  const size_t jc = i / ns;
+  const int s = (int)(i - jc * ns);
+  const size_t j = jc / n, c = jc - j * n;
+  Sv<TB> acc = s_zero<TB>();
+  for (int zi = 0; zi < nz; zi++)
+    acc = s_add(acc, s_mul(s_load<TB>(pw + (j * nz + zi) * d + s * TB), s_load<TB>(z + (zi * n + c) * d + s * TB)));
+  s_store(y + jc * d + s * TB, acc);
+}
+
+// out[i][j] = sum_c w[j][c] (.) z_i[c]: one block per (i, j, slot chunk)
+template <int TB>
+__global__ void __launch_bounds__(MT) k_dots(const uint64_t *w, const uint64_t *z, int t, size_t n, int d, int spb,
+                                            uint64_t *out) {
+  __shared__ uint64_t red[MT * TB];
+  const int slot_l = threadIdx.x % spb, lane_c = threadIdx.x / spb, cpb = MT / spb;
+  const int slot = blockIdx.z * spb + slot_l;
+  const int i = blockIdx.y, j = blockIdx.x;
+  const uint64_t *wj = w + (size_t)j * n * d + slot * TB, *zi = z + (size_t)i * n * d + slot * TB;
+  Sv<TB> acc = s_zero<TB>();
+  for (size_t c = lane_c; c < n; c += cpb) acc = s_add(acc, s_mul(s_load<TB>(wj + c * d), s_load<TB>(zi + c * d)));
+  s_store(red + threadIdx.x * TB, acc);
+  __syncthreads();
+  for (int h = cpb / 2; h > 0; h >>= 1) {
+    if (lane_c < h)
+      s_store(red + threadIdx.x * TB, s_add(s_load<TB>(red + threadIdx.x * TB), s_load<TB>(red + (threadIdx.x + h * spb) * TB)));
+    __syncthreads();
+  }
+  if (lane_c == 0) s_store(out + ((size_t)i * t + j) * d + slot * TB, s_load<TB>(red + threadIdx.x * TB));
+}
+
+unsigned nblk(size_t n, int t) { return (unsigned)((n + t - 1) / t); }
+
+hipError_t csr(const uint64_t *rp, size_t rp_stride, int na, const uint32_t *col, const uint32_t *vidx,
+               const uint64_t *val, size_t nrows, int d, const uint64_t *z, size_t z_stride, uint64_t *out,
+               size_t out_stride, int ntask, hipStream_t st) {
+  if (!nrows || !ntask) return hipSuccess;
+  const int tb = slot_words(d), ns = d / tb, spb = ns < MT ? ns : MT;
+  const dim3 grid(nblk(nrows, MT / spb), (unsigned)ntask, (unsigned)(ns / spb));
+  if (tb == 3)
+    hipLaunchKernelGGL(k_csr<3>, grid, dim3(MT), 0, st, rp, rp_stride, na, col, vidx, val, nrows, d, z, z_stride, out,
+                       out_stride, spb);
+  else
+    hipLaunchKernelGGL(k_csr<1>, grid, dim3(MT), 0, st, rp, rp_stride, na, col, vidx, val, nrows, d, z, z_stride, out,
+                       out_stride, spb);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+size_t mz_scratch_elems(const CcsDev &M, int nz, int nv) {
+  const size_t e = ((size_t)1 << nv) * M.d, tn = (size_t)M.t * M.n * M.d;
+  const size_t chall = (size_t)M.t * nz * M.d + tn, eval = e + tn;
+  return chall > eval ? chall : eval;
+}
+
+hipError_t mz_mles(const CcsDev &M, const uint64_t *z, int nz, int nv, uint64_t *out, hipStream_t st) {
+  const size_t len = ((size_t)1 << nv) * M.d;
+  if (M.m > ((size_t)1 << nv)) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(out, 0, (size_t)nz * M.t * len * 8, st);  // the MLEs' zero padding
+  if (e != hipSuccess) return e;
+  return csr(M.rp, M.m + 1, M.t, M.col, nullptr, M.val, M.m, M.d, z, M.n * M.d, out, len, nz * M.t, st);
+}
+
+hipError_t mz_challenged(const CcsDev &M, const uint64_t *z, const uint64_t *zeta, int nz, int nv, uint64_t *out,
+                         uint64_t *scratch, hipStream_t st) {
+  const size_t len = ((size_t)1 << nv) * M.d;
+  if (M.m > ((size_t)1 << nv)) return hipErrorInvalidValue;
+  const int tb = slot_words(M.d), ns = M.d / tb;
+  uint64_t *pw = scratch, *y = scratch + (size_t)M.t * nz * M.d;
+  if (tb == 3)
+    hipLaunchKernelGGL(k_zeta_pows<3>, dim3(nblk((size_t)nz * ns, 256)), dim3(256), 0, st, zeta, nz, M.t, M.d, pw);
+  else
+    hipLaunchKernelGGL(k_zeta_pows<1>, dim3(nblk((size_t)nz * ns, 256)), dim3(256), 0, st, zeta, nz, M.t, M.d, pw);
+  const size_t ny = (size_t)M.t * M.n * ns;
+  if (tb == 3)
+    hipLaunchKernelGGL(k_zcomb<3>, dim3(nblk(ny, 256)), dim3(256), 0, st, pw, z, nz, M.t, M.n, M.d, y);
+  else
+    hipLaunchKernelGGL(k_zcomb<1>, dim3(nblk(ny, 256)), dim3(256), 0, st, pw, z, nz, M.t, M.n, M.d, y);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (len > M.m * M.d) {
+    e = hipMemsetAsync(out + M.m * M.d, 0, (len - M.m * M.d) * 8, st);
+    if (e != hipSuccess) return e;
+  }
+  return csr(M.hrp, 0, 1, M.hcol, M.hidx, M.val, M.m, M.d, y, 0, out, 0, 1, st);
+}
+
+hipError_t mz_evaluate(const CcsDev &M, const uint64_t *z, int nz, int nv, const uint64_t *point, uint64_t *out,
+                       uint64_t *scratch, hipStream_t st) {
+  if (M.m > ((size_t)1 << nv)) return hipErrorInvalidValue;
+  uint64_t *eq = scratch, *w = scratch + ((size_t)1 << nv) * M.d;
+  hipError_t e = eq_table(point, nv, M.d, eq, st);
+  if (e != hipSuccess) return e;
+  // w_j[c] = sum over column c of M_j of value (.) eq[row]
+  e = csr(M.crp, M.n + 1, M.t, M.crow, M.cidx, M.val, M.n, M.d, eq, 0, w, M.n * M.d, M.t, st);
+  if (e != hipSuccess) return e;
+  const int tb = slot_words(M.d), ns = M.d / tb, spb = ns < MT ? ns : MT;
+  const dim3 grid((unsigned)M.t, (unsigned)nz, (unsigned)(ns / spb));
+  if (tb == 3)
+    hipLaunchKernelGGL(k_dots<3>, grid, dim3(MT), 0, st, w, z, M.t, M.n, M.d, spb, out);
+  else
+    hipLaunchKernelGGL(k_dots<1>, grid, dim3(MT), 0, st, w, z, M.t, M.n, M.d, spb, out);
+  return hipGetLastError();
+}
+
+}  // namespace lfk

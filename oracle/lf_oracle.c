@@ -1070,3 +1070,16 @@ int lfo_sumcheck_check(const uint64_t *proof, const uint64_t *randomness, int nv
   free(t);
   return rc;
 }
+
+/* ================================================ sparse Mz products (8(f) rank 2)
+ * mat_vec_mul (LF/arith/utils.rs:52-65): y[r] = sum over row r's (value, col)
+ * of value (.) z[col]; CSR: row_ptr [nrows + 1], col, val [nnz][d] */
+void lfo_spmv(const uint64_t *row_ptr, const uint32_t *col, const uint64_t *val, size_t nrows, int d,
+              const uint64_t *z, uint64_t *y) {
+  for (size_t r = 0; r < nrows; r++) {
+    uint64_t *acc = y + r * (size_t)d;
+    memset(acc, 0, sizeof(uint64_t) * (size_t)d);
+    for (uint64_t k = row_ptr[r]; k < row_ptr[r + 1]; k++)
+      slot_mul_acc(val + k * (size_t)d, z + (size_t)col[k] * d, acc, d);
+  }
+}

@@ -153,6 +153,10 @@ void lfo_sumcheck_prove(lfo_transcript *t, const lfo_comb *cb, uint64_t *mles, i
 int lfo_sumcheck_check(const uint64_t *proof, const uint64_t *randomness, int nv, int d, int degree,
                        const uint64_t *asserted_sum, uint64_t *expected_out);
 
+/* ---- sparse Mz products: mat_vec_mul (LF/arith/utils.rs:52-65) over a CSR matrix of ring elements */
+void lfo_spmv(const uint64_t *row_ptr, const uint32_t *col, const uint64_t *val, size_t nrows, int d,
+              const uint64_t *z, uint64_t *y);
+
 /* ---- seeded synthetic inputs: SplitMix64 stream, rejection to [0,p) ---- */
 void lfo_fill_uniform(uint64_t *out, size_t n, uint64_t seed);
 /* rows[0..nrows) of A f for A = lfo_fill_uniform(seed) as kappa x ncols x d

@@ -81,6 +81,8 @@ def lib():
         "lfo_ajtai_rows_seeded": (None, [U64, SZ, I, u64p, u64p, SZ, u64p, I]),
         "lfo_rot_lin_combination": (None, [u64p, u64p, SZ, I, u64p]),
         "lfo_eq_table": (None, [u64p, I, I, u64p]),
+        "lfo_spmv": (None, [u64p, np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS"), u64p, SZ, I,
+                            u64p, u64p]),
         "lfo_mle_fix_first": (None, [u64p, SZ, I, u64p]),
         "lfo_mle_evaluate": (None, [u64p, I, I, u64p, u64p]),
         "lfo_comb_eval": (None, [C.POINTER(Comb), u64p, I, I, u64p]),
@@ -318,6 +320,42 @@ def sumcheck_check(proof, randomness, nv: int, d: int, degree: int, asserted_sum
     out = np.zeros(d, np.uint64)
     rc = lib().lfo_sumcheck_check(_u64(proof), _u64(randomness), nv, d, degree, _u64(asserted_sum), out)
     return rc, out
+
+
+# ---------------------------------------------------------------- sparse Mz products
+def spmv(row_ptr, col, val, d: int, z) -> np.ndarray:
+    """mat_vec_mul (LF/arith/utils.rs:52-65)"""
+    rp = _u64(row_ptr)
+    out = np.zeros((rp.size - 1) * d, np.uint64)
+    lib().lfo_spmv(rp, np.ascontiguousarray(col, np.uint32), _u64(val), rp.size - 1, d, _u64(z), out)
+    return out
+
+
+def mz_mles(mats, z, nv: int, d: int) -> np.ndarray:
+    """calculate_Mz_mles / compute_mz_mles (mle_helpers.rs:137-146): MLE(M_j z)
+    for every matrix, zero-padded to 2^nv; mats: [(row_ptr, col, val)]"""
+    out = []
+    for rp, col, val in mats:
+        y = spmv(rp, col, val, d, z)
+        pad = np.zeros((1 << nv) * d, np.uint64)
+        pad[:y.size] = y
+        out.append(pad)
+    return np.concatenate(out)
+
+
+def mz_challenged(mats, zs, zetas, nv: int, d: int) -> np.ndarray:
+    """calculate_challenged_mz_mle (folding.rs:208-234): for each instance i, Horner
+    over the matrices in reverse (mle += M_j z_i; mle *= zeta_i), summed over i"""
+    n = 1 << nv
+    total = np.zeros(n * d, np.uint64)
+    for z, zeta in zip(zs, zetas):
+        ms = mz_mles(mats, z, nv, d).reshape(len(mats), n * d)
+        mle = np.zeros(n * d, np.uint64)
+        for j in reversed(range(len(mats))):
+            mle = np.array([(int(a) + int(b)) % P for a, b in zip(mle, ms[j])], np.uint64)
+            mle = np.concatenate([slot_mul(mle[x * d:(x + 1) * d], zeta, d) for x in range(n)])
+        total = np.array([(int(a) + int(b)) % P for a, b in zip(total, mle)], np.uint64)
+    return total
 
 
 def broadcast(base, d: int) -> np.ndarray:

@@ -1,0 +1,120 @@
+"""GPU parity of the sparse CCS products against the
+oracle's mat_vec_mul restatement: the Mz MLEs of compute_mz_mles, the
+zeta-challenged combination of the folding prover, and the MLE evaluations
+(u_s, eta_s) -- including empty rows, repeated columns in a row and an empty
+matrix -- and, at the zkvm's CCS dimensions (m = 2^17 rows, n = 19 768
+columns, t = 125 matrices), the evaluation route (M_j^T eq(r)) . z against
+evaluating the materialised MLEs."""
+import numpy as np
+import pytest
+
+import latticeum_amd as LA
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+P = LA.P
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+    c = LA.Context(0)
+    c.set_stream(torch.cuda.current_stream().cuda_stream)
+    yield c
+    c.close()
+
+
+def dev(x=None, n=None):
+    import torch
+    if x is not None:
+        return torch.from_numpy(np.ascontiguousarray(x).view(np.int64)).cuda()
+    return torch.zeros(n, dtype=torch.int64, device="cuda")
+
+
+def host(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+def random_ccs(t, m, n, d, seed, max_per_row=3):
+    rng = np.random.default_rng(seed)
+    mats = []
+    for j in range(t):
+        if j == 1:  # an empty matrix
+            mats.append((np.zeros(m + 1, np.uint64), np.zeros(0, np.uint32), np.zeros(0, np.uint64)))
+            continue
+        cnt = rng.integers(0, max_per_row + 1, m)
+        rp = np.concatenate([[0], np.cumsum(cnt)]).astype(np.uint64)
+        col = rng.integers(0, n, int(rp[-1])).astype(np.uint32)
+        if col.size > 1:
+            col[1] = col[0]  # a repeated column
+        val = O.fill_uniform(int(rp[-1]) * d, seed + 7 * j)
+        mats.append((rp, col, val))
+    return mats
+
+
+@pytest.mark.parametrize("d", [24, 16, 1024])
+def test_mz_products_match_oracle(ctx, d):
+    t, m, n, nz, nv = 5, 100, 37, 3, 7
+    mats = random_ccs(t, m, n, d, 40 + d)
+    M = LA.CCSMatrices(ctx, d, m, n, mats)
+    zs = [O.fill_uniform(n * d, 50 + d + i) for i in range(nz)]
+    zd = dev(np.concatenate(zs))
+    out = dev(n=nz * t * (1 << nv) * d)
+    M.mz_mles(zd, nz, nv, out)
+    ctx.sync()
+    want = np.concatenate([O.mz_mles(mats, z, nv, d) for z in zs])
+    assert np.array_equal(host(out), want)
+    zeta = O.fill_uniform(nz * d, 60 + d)
+    ch = dev(n=(1 << nv) * d)
+    M.mz_challenged(zd, dev(zeta), nz, nv, ch)
+    ctx.sync()
+    assert np.array_equal(host(ch), O.mz_challenged(mats, zs, [zeta[i * d:(i + 1) * d] for i in range(nz)], nv, d))
+    point = O.fill_uniform(nv * d, 70 + d)
+    ev = dev(n=nz * t * d)
+    M.mz_evaluate(zd, nz, nv, dev(point), ev)
+    ctx.sync()
+    w = want.reshape(nz * t, (1 << nv) * d)
+    assert np.array_equal(host(ev), np.concatenate([O.mle_evaluate(w[k], nv, d, point) for k in range(nz * t)]))
+
+
+def test_mz_zkvm_dimensions(ctx):
+    """m = 2^17, n = 19 768, t = 125 (zkvm ccs.rs:43-67) with ~2 entries per row
+    per matrix: sampled rows of the materialised products against the oracle,
+    and the transposed evaluation route against evaluating the materialised MLEs"""
+    import torch
+    d, t, m, n, nz, nv = 24, 125, 1 << 17, 19768, 2, 17
+    rng = np.random.default_rng(5)
+    mats = []
+    for j in range(t):
+        cnt = rng.integers(0, 5, m)
+        rp = np.concatenate([[0], np.cumsum(cnt)]).astype(np.uint64)
+        col = rng.integers(0, n, int(rp[-1])).astype(np.uint32)
+        mats.append((rp, col, None))
+    nnz = sum(int(x[0][-1]) for x in mats)
+    vals = O.fill_uniform(nnz * d, 6)
+    off = 0
+    full = []
+    for rp, col, _ in mats:
+        k = int(rp[-1])
+        full.append((rp, col, vals[off * d:(off + k) * d]))
+        off += k
+    M = LA.CCSMatrices(ctx, d, m, n, full)
+    zs = O.fill_uniform(nz * n * d, 7)
+    zd = dev(zs)
+    out = dev(n=nz * t * (1 << nv) * d)
+    M.mz_mles(zd, nz, nv, out)
+    ctx.sync()
+    for i, j, r in ((0, 0, 0), (1, 124, m - 1), (0, 63, 77777), (1, 5, 4096)):
+        rp, col, val = full[j]
+        a, b = int(rp[r]), int(rp[r + 1])
+        want = O.spmv(np.array([0, b - a], np.uint64), col[a:b], val[a * d:b * d], d, zs[i * n * d:(i + 1) * n * d])
+        got = host(out[((i * t + j) * (1 << nv) + r) * d:((i * t + j) * (1 << nv) + r + 1) * d])
+        assert np.array_equal(got, want), (i, j, r)
+    point = dev(O.fill_uniform(nv * d, 8))
+    ev, ev2 = dev(n=nz * t * d), dev(n=nz * t * d)
+    M.mz_evaluate(zd, nz, nv, point, ev)
+    ctx.dev_mle_evaluate(d, out, nz * t, nv, point, ev2)
+    ctx.sync()
+    assert torch.equal(ev, ev2)
+    del out
+    torch.cuda.empty_cache()

@@ -100,3 +100,26 @@ def test_linearization_sumcheck_prove_verify(d):
     rc, expected = O.sumcheck_check(proof, rnd, nv, d, 3, asserted)
     assert rc == 0
     assert np.array_equal(expected, final_claim(comb, mles, 4, nv, d, rnd))
+
+
+def test_mz_oracle_identities():
+    """mat_vec_mul row by row, zero-padded MLEs, and the challenged Horner
+    (folding.rs:208-234) = sum_j zeta^(j+1) M_j z"""
+    d, m, n, nv = 24, 6, 5, 3
+    rp = np.array([0, 2, 2, 5, 6, 6, 8], np.uint64)
+    col = np.array([0, 4, 1, 1, 3, 2, 0, 4], np.uint32)
+    val = O.fill_uniform(8 * d, 3)
+    z = O.fill_uniform(n * d, 4)
+    y = O.spmv(rp, col, val, d, z).reshape(m, d)
+    for r in range(m):
+        acc = np.zeros(d, object)
+        for k in range(int(rp[r]), int(rp[r + 1])):
+            acc = (acc + O.slot_mul(val[k * d:(k + 1) * d], z[col[k] * d:(col[k] + 1) * d], d).astype(object)) % P
+        assert np.array_equal(y[r], acc.astype(np.uint64))
+    mats = [(rp, col, val), (rp, col[::-1].copy(), val[::-1].copy())]
+    ml = O.mz_mles(mats, z, nv, d).reshape(2, 1 << nv, d)
+    assert not ml[:, m:].any()
+    zeta = O.fill_uniform(d, 5)
+    z2 = O.slot_mul(zeta, zeta, d)
+    want = O.fold_cm0(np.concatenate([zeta, z2]), ml.ravel(), 2, 1 << nv, d)
+    assert np.array_equal(O.mz_challenged(mats, [z], [zeta], nv, d), want)
