@@ -455,6 +455,109 @@ def side_ops(LA, torch, local):
     return out
 
 
+def next_rows(LA, torch, local, cpu):
+    """SURVEY.md 8(f) rows 1 and 2 at the zkvm's shapes on the reference ring
+    (Phi_72, log m = 17): the folding sumcheck prover (95 MLEs, degree 4, 17
+    rounds through the Poseidon2 transcript; folding/utils.rs:196-331) and the
+    sparse CCS products of one fold (t = 125 matrices 2^17 x 19 768, ~1 entry
+    per row per matrix; the zeta-challenged Mz MLE of K = 15 instances and the
+    15 x 125 evaluations eta_s). Device time with the host transcript in the loop."""
+    ctx = LA.Context(local)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    out = {}
+    d, nv, nk, tau = 24, 17, 30, 3
+    n = 1 << nv
+    nm = 5 + nk * tau
+    i64 = dict(dtype=torch.int64, device=f"cuda:{local}")
+    m = torch.empty(nm * n * d, **i64)
+    mu = torch.empty(nk * d, **i64)
+    ctx.dev_fill_uniform(mu, 0x4C460010)
+    comb = LA.Comb.folding(mu, nk, tau, 2)
+    times = []
+    for rep_ in range(4):
+        ctx.dev_fill_uniform(m, 0x4C460011 + rep_)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ctx.sumcheck_prove(LA.Poseidon2Transcript(), comb, m, nm, nv, d, 4)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    ms = min(times[1:]) * 1e3
+    mle_bytes = nm * n * d * 8
+    out["folding_sumcheck"] = {
+        "workload": f"folding sumcheck prover: Phi_72, {nm} MLEs of 2^{nv} ring elements ({mle_bytes / 1e9:.2f} GB), "
+                    f"degree 4, {nv} rounds with the Poseidon2 transcript on the host",
+        "ms_per_prove": ms, "rounds": nv,
+        "hbm_gbs_min_traffic": 2.5 * mle_bytes / (ms * 1e-3) / 1e9,
+        "note": "VALU-bound: four Fq3 products and four lazy multiply-accumulates per MLE value per point (B_SMALL = 2 cubic form)"}
+    del m
+    torch.cuda.empty_cache()
+    if cpu is not None:
+        # the oracle's prover over the same comb at log m = 9, scaled by 2^(17-9)
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import oracle as O
+        nvs = 9
+        mles = O.fill_uniform(nm * (1 << nvs) * d, 5)
+        mu_h = O.fill_uniform(nk * d, 6)
+        t0 = time.perf_counter()
+        O.sumcheck_prove(O.new_transcript(), O.SumcheckComb.folding(mu_h, nk, tau, 2), mles, nm, nvs, d, 4)
+        dt = time.perf_counter() - t0
+        out["folding_sumcheck"]["cpu_baseline"] = {
+            "ms_per_prove": dt * (1 << (nv - nvs)) * 1e3, "cores": 1, "kind": "port",
+            "sample": f"the oracle's prover at log m = {nvs} ({dt:.2f} s, 1 thread), scaled by 2^{nv - nvs}"}
+    # sparse CCS products at the zkvm's dimensions
+    t, mm, nn, K = 125, 1 << 17, 19768, 15
+    rng = np.random.default_rng(0x4C460012)
+    mats, nnz = [], 0
+    for j in range(t):
+        cnt = rng.integers(0, 3, mm)
+        rp = np.concatenate([[0], np.cumsum(cnt)]).astype(np.uint64)
+        mats.append([rp, rng.integers(0, nn, int(rp[-1])).astype(np.uint32), None])
+        nnz += int(rp[-1])
+    vals = torch.empty(nnz * d, **i64)
+    ctx.dev_fill_uniform(vals, 0x4C460013)
+    hv = vals.cpu().numpy().view(np.uint64)
+    del vals
+    off = 0
+    for mt in mats:
+        k = int(mt[0][-1])
+        mt[2] = hv[off * d:(off + k) * d]
+        off += k
+    M = LA.CCSMatrices(ctx, d, mm, nn, mats)
+    del hv, mats
+    z = torch.empty(K * nn * d, **i64)
+    ctx.dev_fill_uniform(z, 0x4C460014)
+    zeta = torch.empty(K * d, **i64)
+    ctx.dev_fill_uniform(zeta, 0x4C460015)
+    point = torch.empty(nv * d, **i64)
+    ctx.dev_fill_uniform(point, 0x4C460016)
+    ch = torch.empty(mm * d, **i64)
+    ev = torch.empty(K * t * d, **i64)
+
+    def ev_ms(fn, reps=5):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    ms_ch = ev_ms(lambda: M.mz_challenged(z, zeta, K, nv, ch))
+    ms_ev = ev_ms(lambda: M.mz_evaluate(z, K, nv, point, ev))
+    val_bytes = nnz * d * 8
+    out["mz_products"] = {
+        "workload": f"CCS t={t} matrices {mm} x {nn} ({nnz} ring-element entries, {val_bytes / 1e9:.2f} GB), "
+                    f"K={K} decomposed vectors",
+        "challenged_mle_ms": ms_ch, "etas_ms": ms_ev,
+        "challenged_gbs_values": val_bytes / (ms_ch * 1e-3) / 1e9}
+    del M, z, ch, ev
+    ctx.close()
+    torch.cuda.empty_cache()
+    return out
+
+
 EXCLUDED = ("outside the timed step (other tiers): the Poseidon2 transcript and challenge derivation (rho is an "
             "input), linearization, the sumcheck provers and the Mz matrix-vector products")
 
@@ -512,7 +615,9 @@ def main():
         c4 = extra_shape(LA, torch, LD, pg, local, rank, world, 4096, 1024, 64, 1, 20, 3,
                          "BASELINE configs[4]'s ring X^4096+1 with kappa=64")
         ops = side_ops(LA, torch, local)
+        nxt = next_rows(LA, torch, local, out.get("cpu_baseline") if out is not None else None)
         if out is not None:
+            out["next_rows"] = nxt
             out["reference_ring"] = ref
             out["small_shape"] = small
             out["configs4_d4096_kappa64"] = c4

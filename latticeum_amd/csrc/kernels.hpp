@@ -127,7 +127,8 @@ hipError_t eq_table(const uint64_t *r, int nv, int d, uint64_t *out, hipStream_t
 // out[m][b] = in[m][2b] + r (in[m][2b+1] - in[m][2b]), b < half; r_base: slot_words(d) words
 hipError_t mle_fix_first(const uint64_t *in, size_t in_stride, int nm, size_t half, int d, const uint64_t *r_base,
                          uint64_t *out, size_t out_stride, hipStream_t st);
-size_t round_partial_elems(int d, size_t half, int nevals);
+// nf: the f_hat MLEs the folding round may split over chunks (1 for linearization)
+size_t round_partial_elems(int d, size_t half, int nevals, int nf);
 hipError_t fold_weights(const uint64_t *mu, int nk, int tau, int d, uint64_t *w, hipStream_t st);
 // evals [2 bsmall + 1][d]: the folding polynomial's round sums over `half` points;
 // mles: 5 + nf MLEs at stride u64 apart; w: nf Horner weights

@@ -37,12 +37,13 @@ __global__ void __launch_bounds__(MT) k_csr(const uint64_t *rp, size_t rp_stride
   const int task = blockIdx.y, a = task % na, b = task / na;
   const uint64_t *rpa = rp + a * rp_stride;
   const uint64_t *zb = z + b * z_stride + slot * TB;
-  Sv<TB> acc = s_zero<TB>();
+  SAcc<TB> acc;
+  sacc_zero(acc);
   for (uint64_t k = rpa[r], e = rpa[r + 1]; k < e; k++) {
     const uint64_t vi = vidx ? vidx[k] : k;
-    acc = s_add(acc, s_mul(s_load<TB>(val + vi * d + slot * TB), s_load<TB>(zb + (size_t)col[k] * d)));
+    sacc_mad(acc, s_load<TB>(val + vi * d + slot * TB), s_load<TB>(zb + (size_t)col[k] * d));
   }
-  s_store(out + task * out_stride + r * d + slot * TB, acc);
+  s_store(out + task * out_stride + r * d + slot * TB, sacc_final(acc));
 }
 
 // pw[j][i] = zeta_i^(j+1)
@@ -69,10 +70,11 @@ __global__ void k_zcomb(const uint64_t *pw, const uint64_t *z, int nz, int t, si
   const size_t jc = i / ns;
   const int s = (int)(i - jc * ns);
   const size_t j = jc / n, c = jc - j * n;
-  Sv<TB> acc = s_zero<TB>();
+  SAcc<TB> acc;
+  sacc_zero(acc);
   for (int zi = 0; zi < nz; zi++)
-    acc = s_add(acc, s_mul(s_load<TB>(pw + (j * nz + zi) * d + s * TB), s_load<TB>(z + (zi * n + c) * d + s * TB)));
-  s_store(y + jc * d + s * TB, acc);
+    sacc_mad(acc, s_load<TB>(pw + (j * nz + zi) * d + s * TB), s_load<TB>(z + (zi * n + c) * d + s * TB));
+  s_store(y + jc * d + s * TB, sacc_final(acc));
 }
 
 // out[i][j] = sum_c w[j][c] (.) z_i[c]: one block per (i, j, slot chunk)
@@ -84,9 +86,10 @@ __global__ void __launch_bounds__(MT) k_dots(const uint64_t *w, const uint64_t *
   const int slot = blockIdx.z * spb + slot_l;
   const int i = blockIdx.y, j = blockIdx.x;
   const uint64_t *wj = w + (size_t)j * n * d + slot * TB, *zi = z + (size_t)i * n * d + slot * TB;
-  Sv<TB> acc = s_zero<TB>();
-  for (size_t c = lane_c; c < n; c += cpb) acc = s_add(acc, s_mul(s_load<TB>(wj + c * d), s_load<TB>(zi + c * d)));
-  s_store(red + threadIdx.x * TB, acc);
+  SAcc<TB> la;
+  sacc_zero(la);
+  for (size_t c = lane_c; c < n; c += cpb) sacc_mad(la, s_load<TB>(wj + c * d), s_load<TB>(zi + c * d));
+  s_store(red + threadIdx.x * TB, sacc_final(la));
   __syncthreads();
   for (int h = cpb / 2; h > 0; h >>= 1) {
     if (lane_c < h)

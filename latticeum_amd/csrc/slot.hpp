@@ -64,25 +64,27 @@ __device__ __forceinline__ Sv<1> s_mul(const Sv<1> &a, const Sv<1> &b) {
   r.c[0] = gl::mul(a.c[0], b.c[0]);
   return r;
 }
+// c0 = a0 b0 + a1 (2^40 b2) + a2 (2^40 b1), c1 = a0 b1 + a1 b0 + a2 (2^40 b2),
+// c2 = a0 b2 + a1 b1 + a2 b0: the nonresidue folded into the operands (two
+// shifts) so each output word is one carry-chain accumulator and one reduction
 __device__ __forceinline__ Sv<3> s_mul(const Sv<3> &a, const Sv<3> &b) {
-  gl::CAcc x0, x0n, x1, x1n, x2;
+  const uint64_t b1n = gl::shl96(b.c[1], 40), b2n = gl::shl96(b.c[2], 40);
+  gl::CAcc x0, x1, x2;
   gl::cacc_zero(x0);
-  gl::cacc_zero(x0n);
   gl::cacc_zero(x1);
-  gl::cacc_zero(x1n);
   gl::cacc_zero(x2);
   gl::cacc_mad(x0, a.c[0], b.c[0]);
-  gl::cacc_mad(x0n, a.c[1], b.c[2]);
-  gl::cacc_mad(x0n, a.c[2], b.c[1]);
+  gl::cacc_mad(x0, a.c[1], b2n);
+  gl::cacc_mad(x0, a.c[2], b1n);
   gl::cacc_mad(x1, a.c[0], b.c[1]);
   gl::cacc_mad(x1, a.c[1], b.c[0]);
-  gl::cacc_mad(x1n, a.c[2], b.c[2]);
+  gl::cacc_mad(x1, a.c[2], b2n);
   gl::cacc_mad(x2, a.c[0], b.c[2]);
   gl::cacc_mad(x2, a.c[1], b.c[1]);
   gl::cacc_mad(x2, a.c[2], b.c[0]);
   Sv<3> r;
-  r.c[0] = gl::add(gl::cacc_reduce(x0), gl::shl96(gl::cacc_reduce(x0n), 40));
-  r.c[1] = gl::add(gl::cacc_reduce(x1), gl::shl96(gl::cacc_reduce(x1n), 40));
+  r.c[0] = gl::cacc_reduce(x0);
+  r.c[1] = gl::cacc_reduce(x1);
   r.c[2] = gl::cacc_reduce(x2);
   return r;
 }
@@ -94,5 +96,58 @@ __device__ __forceinline__ bool s_is_zero(const Sv<TB> &a) {
   return o == 0;
 }
 
+
+// lazy multiply-accumulate of slot products: sum_i a_i b_i with one reduction
+// per output word at the end (carry-chain accumulators, gl::CAcc: 8 VALU per
+// 64 x 64 product instead of a full product and reduction each)
+template <int TB>
+struct SAcc;
+template <>
+struct SAcc<1> {
+  gl::CAcc x;
+};
+template <>
+struct SAcc<3> {
+  gl::CAcc x0, x1, x2;  // the three output words (nonresidue folded into the operands)
+};
+__device__ __forceinline__ void sacc_zero(SAcc<1> &a) { gl::cacc_zero(a.x); }
+__device__ __forceinline__ void sacc_zero(SAcc<3> &a) {
+  gl::cacc_zero(a.x0);
+  gl::cacc_zero(a.x1);
+  gl::cacc_zero(a.x2);
+}
+__device__ __forceinline__ void sacc_mad(SAcc<1> &a, const Sv<1> &x, const Sv<1> &y) { gl::cacc_mad(a.x, x.c[0], y.c[0]); }
+__device__ __forceinline__ void sacc_mad(SAcc<3> &a, const Sv<3> &x, const Sv<3> &y) {
+  const uint64_t y1n = gl::shl96(y.c[1], 40), y2n = gl::shl96(y.c[2], 40);
+  gl::cacc_mad(a.x0, x.c[0], y.c[0]);
+  gl::cacc_mad(a.x0, x.c[1], y2n);
+  gl::cacc_mad(a.x0, x.c[2], y1n);
+  gl::cacc_mad(a.x1, x.c[0], y.c[1]);
+  gl::cacc_mad(a.x1, x.c[1], y.c[0]);
+  gl::cacc_mad(a.x1, x.c[2], y2n);
+  gl::cacc_mad(a.x2, x.c[0], y.c[2]);
+  gl::cacc_mad(a.x2, x.c[1], y.c[1]);
+  gl::cacc_mad(a.x2, x.c[2], y.c[0]);
+}
+__device__ __forceinline__ Sv<1> sacc_final(const SAcc<1> &a) {
+  Sv<1> r;
+  r.c[0] = gl::cacc_reduce(a.x);
+  return r;
+}
+__device__ __forceinline__ Sv<3> sacc_final(const SAcc<3> &a) {
+  Sv<3> r;
+  r.c[0] = gl::cacc_reduce(a.x0);
+  r.c[1] = gl::cacc_reduce(a.x1);
+  r.c[2] = gl::cacc_reduce(a.x2);
+  return r;
+}
+// k v for a small integer k (the finite-difference and cubic-evaluation weights)
+template <int TB>
+__device__ __forceinline__ Sv<TB> s_smul(const Sv<TB> &v, uint64_t k) {
+  Sv<TB> r;
+#pragma unroll
+  for (int i = 0; i < TB; i++) r.c[i] = gl::mul(v.c[i], k);
+  return r;
+}
 
 }  // namespace lfk

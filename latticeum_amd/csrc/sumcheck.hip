@@ -92,14 +92,23 @@ __device__ __forceinline__ void block_partial(const Sv<TB> (&acc)[NE], int spb, 
 // The Horner over dd = tau-1 .. 0 is sum_dd mu_k^(dd+1) e_dd, so with
 // w_(k,dd) = mu_k^(dd+1) (k_fold_weights) the per-point value is
 //   v0 v1 + v2 v3 + v4 S,  S = sum_(k,dd) w_(k,dd) g(f_(k,dd)),  g(f) = f prod (f^2 - b^2)
-// (the reference's zero short-cuts do not change values). S is a polynomial of
-// degree 2 B_SMALL - 1 in the evaluation point e, so it is computed at the
-// first `degree` points and extrapolated to e = degree by finite differences.
+// (the reference's zero short-cuts do not change values). S is linear in the
+// f_hat MLEs, so a launch may split them over blockIdx.z chunks: every chunk
+// adds v4 S_chunk and chunk 0 also v0 v1 + v2 v3; the block sums meet in
+// k_sum_partials. On the point line f(e) = a + e s:
+//  * B_SMALL = 2 (GoldiLocksDP): g = f^3 - f, and w g(f(e)) is the cubic
+//    C0 + C1 e + C2 e^2 + C3 e^3 with C3 = (w s^2) s, C2 = 3 (w s^2) a,
+//    C1 = (w s)(3 a^2 - 1), C0 = (w a)(a^2 - 1): four products and four lazy
+//    multiply-accumulates per MLE value, and S(e) from the summed coefficients;
+//  * otherwise S is evaluated at e < degree and extrapolated to e = degree by
+//    finite differences (S has degree 2 B_SMALL - 1).
 template <int TB, int BS>
 __global__ void __launch_bounds__(RT) k_round_folding(const uint64_t *mles, size_t stride, int nf, const uint64_t *w,
                                                       size_t half, int d, int spb, uint64_t *partial) {
   const int slot_l = threadIdx.x % spb, lane_p = threadIdx.x / spb, ppb = RT / spb;
   const int slot = blockIdx.y * spb + slot_l;
+  const int chunk = blockIdx.z, nchunk = gridDim.z;
+  const int f0 = (int)((long)nf * chunk / nchunk), f1 = (int)((long)nf * (chunk + 1) / nchunk);
   constexpr int degree = 2 * BS;
   Sv<TB> acc[degree + 1];
 #pragma unroll
@@ -107,33 +116,50 @@ __global__ void __launch_bounds__(RT) k_round_folding(const uint64_t *mles, size
   for (size_t b = (size_t)blockIdx.x * ppb + lane_p; b < half; b += (size_t)gridDim.x * ppb) {
     const uint64_t *pb = mles + 2 * b * d + slot * TB;
     Sv<TB> S[degree + 1];
-#pragma unroll
-    for (int e = 0; e < degree; e++) S[e] = s_zero<TB>();
-    for (int f = 0; f < nf; f++) {
-      const uint64_t *p = pb + (size_t)(5 + f) * stride;
-      const Sv<TB> a = s_load<TB>(p), st = s_sub(s_load<TB>(p + d), a);
-      const Sv<TB> wf = s_load<TB>(w + (size_t)f * d + slot * TB);
-      Sv<TB> x = a;
-#pragma unroll
-      for (int e = 0; e < degree; e++) {
-        const Sv<TB> x2 = s_mul(x, x);
-        Sv<TB> g = x;
-#pragma unroll
-        for (int bb = 1; bb < BS; bb++) g = s_mul(g, s_sub(x2, s_scalar<TB>((uint64_t)bb * bb)));
-        S[e] = s_add(S[e], s_mul(wf, g));
-        x = s_add(x, st);
+    if (BS == 2) {
+      SAcc<TB> c0, c1, c2, c3;
+      sacc_zero(c0);
+      sacc_zero(c1);
+      sacc_zero(c2);
+      sacc_zero(c3);
+      for (int f = f0; f < f1; f++) {
+        const uint64_t *p = pb + (size_t)(5 + f) * stride;
+        const Sv<TB> a = s_load<TB>(p), st = s_sub(s_load<TB>(p + d), a);
+        const Sv<TB> wf = s_load<TB>(w + (size_t)f * d + slot * TB);
+        const Sv<TB> ws = s_mul(wf, st), ws2 = s_mul(ws, st), a2 = s_mul(a, a), wa = s_mul(wf, a);
+        sacc_mad(c3, ws2, st);
+        sacc_mad(c2, ws2, a);
+        sacc_mad(c1, ws, s_sub(s_smul(a2, 3), s_one<TB>()));
+        sacc_mad(c0, wa, s_sub(a2, s_one<TB>()));
       }
-    }
-    // S(degree) from S(0 .. degree-1): sum_j (-1)^(degree-1-j) C(degree, j) S(j)
-    {
+      const Sv<TB> C0 = sacc_final(c0), C1 = sacc_final(c1), C2 = s_smul(sacc_final(c2), 3), C3 = sacc_final(c3);
+#pragma unroll
+      for (int e = 0; e <= degree; e++)
+        S[e] = s_add(s_add(C0, s_smul(C1, e)), s_add(s_smul(C2, e * e), s_smul(C3, e * e * e)));
+    } else {
+#pragma unroll
+      for (int e = 0; e < degree; e++) S[e] = s_zero<TB>();
+      for (int f = f0; f < f1; f++) {
+        const uint64_t *p = pb + (size_t)(5 + f) * stride;
+        const Sv<TB> a = s_load<TB>(p), st = s_sub(s_load<TB>(p + d), a);
+        const Sv<TB> wf = s_load<TB>(w + (size_t)f * d + slot * TB);
+        Sv<TB> x = a;
+#pragma unroll
+        for (int e = 0; e < degree; e++) {
+          const Sv<TB> x2 = s_mul(x, x);
+          Sv<TB> g = x;
+#pragma unroll
+          for (int bb = 1; bb < BS; bb++) g = s_mul(g, s_sub(x2, s_scalar<TB>((uint64_t)bb * bb)));
+          S[e] = s_add(S[e], s_mul(wf, g));
+          x = s_add(x, st);
+        }
+      }
+      // S(degree) from S(0 .. degree-1): sum_j (-1)^(degree-1-j) C(degree, j) S(j)
       Sv<TB> ext = s_zero<TB>();
       uint64_t binom = 1;  // C(degree, j)
 #pragma unroll
       for (int j = 0; j < degree; j++) {
-        Sv<TB> t = S[j];
-        Sv<TB> scaled = s_zero<TB>();
-#pragma unroll
-        for (int q = 0; q < TB; q++) scaled.c[q] = gl::mul(t.c[q], binom);
+        const Sv<TB> scaled = s_smul(S[j], binom);
         ext = ((degree - 1 - j) & 1) ? s_sub(ext, scaled) : s_add(ext, scaled);
         binom = binom * (uint64_t)(degree - j) / (uint64_t)(j + 1);
       }
@@ -148,12 +174,15 @@ __global__ void __launch_bounds__(RT) k_round_folding(const uint64_t *mles, size
     }
 #pragma unroll
     for (int e = 0; e <= degree; e++) {
-      acc[e] = s_add(acc[e], s_add(s_add(s_mul(v[0], v[1]), s_mul(v[2], v[3])), s_mul(v[4], S[e])));
+      Sv<TB> t = s_mul(v[4], S[e]);
+      if (chunk == 0) t = s_add(t, s_add(s_mul(v[0], v[1]), s_mul(v[2], v[3])));
+      acc[e] = s_add(acc[e], t);
 #pragma unroll
       for (int m = 0; m < 5; m++) v[m] = s_add(v[m], sv[m]);
     }
   }
-  block_partial<TB, degree + 1>(acc, spb, ppb, slot, lane_p, d, partial + (size_t)blockIdx.x * (degree + 1) * d);
+  block_partial<TB, degree + 1>(acc, spb, ppb, slot, lane_p, d,
+                                partial + ((size_t)chunk * gridDim.x + blockIdx.x) * (degree + 1) * d);
 }
 
 // w_(k,dd) = mu_k^(dd+1), the Horner weights of the folding combination
@@ -212,13 +241,20 @@ __global__ void __launch_bounds__(RT) k_round_lin(const uint64_t *mles, size_t s
   block_partial<TB, degree + 1>(acc, spb, ppb, slot, lane_p, d, partial + (size_t)blockIdx.x * (degree + 1) * d);
 }
 
-// out[e][.] = sum over blocks of partial[blk][e][.]
-__global__ void k_sum_partials(const uint64_t *partial, int nblk, size_t len, uint64_t *out) {
-  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (i >= len) return;
+// out[i] = sum over blocks of partial[blk][i]: one block per output word,
+// its threads striding over the blocks, then an LDS tree
+__global__ void __launch_bounds__(256) k_sum_partials(const uint64_t *partial, int nblk, size_t len, uint64_t *out) {
+  __shared__ uint64_t red[256];
+  const size_t i = blockIdx.x;
   uint64_t s = 0;
-  for (int b = 0; b < nblk; b++) s = gl::add(s, partial[(size_t)b * len + i]);
-  out[i] = s;
+  for (int b = threadIdx.x; b < nblk; b += 256) s = gl::add(s, partial[(size_t)b * len + i]);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) red[threadIdx.x] = gl::add(red[threadIdx.x], red[threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[i] = red[0];
 }
 
 // ---------------------------------------------------------------- MLE evaluation
@@ -230,9 +266,11 @@ __global__ void __launch_bounds__(RT) k_mle_dot(const uint64_t *mles, size_t str
   const int slot_l = threadIdx.x % spb, lane_p = threadIdx.x / spb, ppb = RT / spb;
   const int slot = blockIdx.y * spb + slot_l;
   const int m = blockIdx.z;
-  Sv<TB> acc[1] = {s_zero<TB>()};
+  SAcc<TB> la;
+  sacc_zero(la);
   for (size_t x = (size_t)blockIdx.x * ppb + lane_p; x < n; x += (size_t)nsplit * ppb)
-    acc[0] = s_add(acc[0], s_mul(s_load<TB>(eq + x * d + slot * TB), s_load<TB>(mles + m * stride + x * d + slot * TB)));
+    sacc_mad(la, s_load<TB>(eq + x * d + slot * TB), s_load<TB>(mles + m * stride + x * d + slot * TB));
+  const Sv<TB> acc[1] = {sacc_final(la)};
   block_partial<TB, 1>(acc, spb, ppb, slot, lane_p, d, partial + ((size_t)blockIdx.x * nm + m) * d);
 }
 
@@ -274,8 +312,11 @@ hipError_t mle_fix_first(const uint64_t *in, size_t in_stride, int nm, size_t ha
 }
 
 // the round-sum launch geometry: spb slots per block (all of a Phi_72
-// element's 8, or up to 256 of X^d + 1), enough blocks for the points
-static void round_geom(int d, size_t half, int &spb, dim3 &grid) {
+// element's 8, or up to 256 of X^d + 1), enough blocks for the points, and --
+// when the points are too few to fill the chip (late rounds) -- the f_hat
+// MLEs split over up to `nf` chunks (grid.z)
+constexpr size_t FILL_THREADS = (size_t)1 << 18;
+static void round_geom(int d, size_t half, int nf, int &spb, dim3 &grid) {
   const int ns = d / slot_words(d);
   spb = ns < RT ? ns : RT;
   const int ppb = RT / spb;
@@ -283,13 +324,19 @@ static void round_geom(int d, size_t half, int &spb, dim3 &grid) {
   const size_t cap = 1024;  // partial sums: at most this many blocks along the points
   if (bx > cap) bx = cap;
   if (bx < 1) bx = 1;
-  grid = dim3((unsigned)bx, (unsigned)(ns / spb));
+  size_t nchunk = 1;
+  const size_t threads = half * (size_t)ns;
+  if (nf > 1 && threads < FILL_THREADS) {
+    nchunk = (FILL_THREADS + threads - 1) / threads;
+    if (nchunk > (size_t)nf) nchunk = nf;
+  }
+  grid = dim3((unsigned)bx, (unsigned)(ns / spb), (unsigned)nchunk);
 }
-size_t round_partial_elems(int d, size_t half, int nevals) {
+size_t round_partial_elems(int d, size_t half, int nevals, int nf) {
   int spb;
   dim3 g;
-  round_geom(d, half, spb, g);
-  return (size_t)g.x * nevals * d;
+  round_geom(d, half, nf, spb, g);
+  return (size_t)g.x * g.z * nevals * d;
 }
 
 hipError_t fold_weights(const uint64_t *mu, int nk, int tau, int d, uint64_t *w, hipStream_t st) {
@@ -306,7 +353,7 @@ hipError_t round_folding(const uint64_t *mles, size_t stride, int nf, const uint
   if (bsmall < 1 || bsmall > 4 || !half) return hipErrorInvalidValue;
   int spb;
   dim3 grid;
-  round_geom(d, half, spb, grid);
+  round_geom(d, half, nf, spb, grid);
 #define LF_RF(TB, BS)                                                                                           \
   hipLaunchKernelGGL((k_round_folding<TB, BS>), grid, dim3(RT), 0, st, mles, stride, nf, w, half, d, spb, partial)
 #define LF_RF_BS(TB)          \
@@ -326,7 +373,8 @@ hipError_t round_folding(const uint64_t *mles, size_t stride, int nf, const uint
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t len = (size_t)(2 * bsmall + 1) * d;
-  hipLaunchKernelGGL(k_sum_partials, dim3(blocks_of(len, 256)), dim3(256), 0, st, partial, (int)grid.x, len, evals);
+  hipLaunchKernelGGL(k_sum_partials, dim3((unsigned)len), dim3(256), 0, st, partial, (int)(grid.x * grid.z), len,
+                     evals);
   return hipGetLastError();
 }
 
@@ -335,7 +383,7 @@ hipError_t round_lin(const uint64_t *mles, size_t stride, int nm, const uint64_t
   if (degree + 1 > MAX_EVALS || degree < 1 || !half) return hipErrorInvalidValue;
   int spb;
   dim3 grid;
-  round_geom(d, half, spb, grid);
+  round_geom(d, half, 1, spb, grid);
 #define LF_RL(TB, DG) \
   hipLaunchKernelGGL((k_round_lin<TB, DG>), grid, dim3(RT), 0, st, mles, stride, nm, c, cs, half, d, spb, partial)
 #define LF_RL_DEG(TB)                          \
@@ -360,7 +408,7 @@ hipError_t round_lin(const uint64_t *mles, size_t stride, int nm, const uint64_t
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t len = (size_t)(degree + 1) * d;
-  hipLaunchKernelGGL(k_sum_partials, dim3(blocks_of(len, 256)), dim3(256), 0, st, partial, (int)grid.x, len, evals);
+  hipLaunchKernelGGL(k_sum_partials, dim3((unsigned)len), dim3(256), 0, st, partial, (int)grid.x, len, evals);
   return hipGetLastError();
 }
 
@@ -381,7 +429,7 @@ hipError_t mle_dot(const uint64_t *mles, size_t stride, int nm, const uint64_t *
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t len = (size_t)nm * d;
-  hipLaunchKernelGGL(k_sum_partials, dim3(blocks_of(len, 256)), dim3(256), 0, st, partial, nsplit, len, out);
+  hipLaunchKernelGGL(k_sum_partials, dim3((unsigned)len), dim3(256), 0, st, partial, nsplit, len, out);
   return hipGetLastError();
 }
 
