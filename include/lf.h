@@ -31,6 +31,8 @@
  *   zkvm/src/main.rs:348-367  commit()                          -> lf_commit
  *   zkvm/src/main.rs:380-404  fold() (its commit+fold arithmetic) -> lf_fold_hot /
  *                                                                 lf_dev_fold_step
+ *   latticefold/src/nifs.rs:28-34 LFProof (ark CanonicalSerialize) -> lf_lfproof_serialize,
+ *       zkvm/src/main.rs:231-234 (serialized_size)                lf_lcccs_(de)serialize
  *   zkvm/src/main.rs:121-219  the proving loop, sharded over GPUs (SURVEY.md 8(b)
  *       lf_fold_reduce_allranks; no reference analogue: rayon only)
  *                                                              -> lf_comm_*, lf_dev_fold_step_sharded,
@@ -358,6 +360,44 @@ int lf_dev_mz_challenged(lf_ctx *ctx, const lf_ccs *M, const uint64_t *z, const 
                          uint64_t *out);
 int lf_dev_mz_evaluate(lf_ctx *ctx, const lf_ccs *M, const uint64_t *z, int nz, int nv, const uint64_t *point,
                        uint64_t *out);
+
+/* ------------------------------------------------------------ wire format
+ * ark-serialize 0.5 CanonicalSerialize as derived on the reference's types
+ * (compressed = uncompressed here): Fq = 8 bytes LE canonical; an NTT ring
+ * element = its d slot words, no length; Vec<T> = u64 LE length + items;
+ * structs = fields in declaration order. repr describes the caller's words.
+ * out == NULL (or too small: LF_ERR_INCORRECT_LENGTH) still returns the size. */
+typedef struct {
+  const uint64_t *elems; /* n ring elements (d words each) */
+  size_t n;
+} lf_ring_slice;
+/* LCCCS { r, v, cm, u, x_w, h } (latticefold/src/arith.rs:192-206) */
+typedef struct {
+  int d;
+  lf_ring_slice r, v, cm, u, x_w;
+  const uint64_t *h; /* one ring element */
+} lf_lcccs;
+/* LFProof (latticefold/src/nifs.rs:28-34) */
+typedef struct {
+  const lf_ring_slice *u_s, *v_s, *x_s, *y_s; /* Vec<Vec<R>> and Vec<Commitment> */
+  size_t n_u, n_v, n_x, n_y;
+} lf_decomposition_proof;
+typedef struct {
+  int d;
+  const uint64_t *lin_sumcheck; /* [lin_rounds][lin_evals] ring elements */
+  size_t lin_rounds, lin_evals;
+  lf_ring_slice lin_v, lin_u;
+  lf_decomposition_proof dec[2]; /* decomposition_proof_l, decomposition_proof_r */
+  const uint64_t *fold_sumcheck; /* [fold_rounds][fold_evals] */
+  size_t fold_rounds, fold_evals;
+  const lf_ring_slice *theta_s, *eta_s;
+  size_t n_theta, n_eta;
+} lf_lfproof;
+int lf_lcccs_serialize(const lf_lcccs *acc, int repr, uint8_t *out, size_t cap, size_t *len);
+/* parses into `buf` (buf_elems u64); `out` points into it */
+int lf_lcccs_deserialize(const uint8_t *in, size_t len, int d, int repr, uint64_t *buf, size_t buf_elems,
+                         lf_lcccs *out);
+int lf_lfproof_serialize(const lf_lfproof *proof, int repr, uint8_t *out, size_t cap, size_t *len);
 
 /* ------------------------------------------------------------ host transcript (sequential) */
 lf_transcript *lf_transcript_new(void);

@@ -30,6 +30,27 @@ class LfFoldStepBufs(C.Structure):
     ]
 
 
+class LfRingSlice(C.Structure):
+    _fields_ = [("elems", VP), ("n", SZ)]
+
+
+class LfLcccs(C.Structure):
+    _fields_ = [("d", I), ("r", LfRingSlice), ("v", LfRingSlice), ("cm", LfRingSlice), ("u", LfRingSlice),
+                ("x_w", LfRingSlice), ("h", VP)]
+
+
+class LfDecompositionProof(C.Structure):
+    _fields_ = [("u_s", VP), ("v_s", VP), ("x_s", VP), ("y_s", VP), ("n_u", SZ), ("n_v", SZ), ("n_x", SZ),
+                ("n_y", SZ)]
+
+
+class LfLfproof(C.Structure):
+    _fields_ = [("d", I), ("lin_sumcheck", VP), ("lin_rounds", SZ), ("lin_evals", SZ), ("lin_v", LfRingSlice),
+                ("lin_u", LfRingSlice), ("dec", LfDecompositionProof * 2), ("fold_sumcheck", VP),
+                ("fold_rounds", SZ), ("fold_evals", SZ), ("theta_s", VP), ("eta_s", VP), ("n_theta", SZ),
+                ("n_eta", SZ)]
+
+
 class LfComb(C.Structure):
     _fields_ = [("kind", I), ("nk", I), ("tau", I), ("bsmall", I), ("mu", VP), ("q", I), ("c", VP),
                 ("S_off", VP), ("S_idx", VP)]
@@ -94,6 +115,9 @@ SIGNATURES = {
     "lf_transcript_get_short_challenges": (I, [VP, I, SZ, VP]),
     "lf_hash_iter": (None, [VP, SZ, VP]),
     "lf_witness_split_w": (SZ, []),
+    "lf_lcccs_serialize": (I, [C.POINTER(LfLcccs), I, VP, SZ, C.POINTER(SZ)]),
+    "lf_lcccs_deserialize": (I, [VP, SZ, I, I, VP, SZ, C.POINTER(LfLcccs)]),
+    "lf_lfproof_serialize": (I, [C.POINTER(LfLfproof), I, VP, SZ, C.POINTER(SZ)]),
     "lf_dev_eq_table": (I, [VP, I, VP, I, VP]),
     "lf_ccs_create": (I, [VP, I, I, SZ, SZ, VP, VP, VP, I, C.POINTER(VP)]),
     "lf_ccs_destroy": (None, [VP]),
