@@ -31,6 +31,7 @@
  *   zkvm/src/main.rs:348-367  commit()                          -> lf_commit
  *   zkvm/src/main.rs:380-404  fold() (its commit+fold arithmetic) -> lf_fold_hot /
  *                                                                 lf_dev_fold_step
+ *   zkvm/src/commitments.rs:192-262 memory Merkle trees     -> lf_dev_merkle_tree, lf_merkle_open
  *   latticefold/src/nifs.rs:28-34 LFProof (ark CanonicalSerialize) -> lf_lfproof_serialize,
  *       zkvm/src/main.rs:231-234 (serialized_size)                lf_lcccs_(de)serialize
  *   zkvm/src/main.rs:121-219  the proving loop, sharded over GPUs (SURVEY.md 8(b)
@@ -360,6 +361,18 @@ int lf_dev_mz_challenged(lf_ctx *ctx, const lf_ccs *M, const uint64_t *z, const 
                          uint64_t *out);
 int lf_dev_mz_evaluate(lf_ctx *ctx, const lf_ccs *M, const uint64_t *z, int nz, int nv, const uint64_t *point,
                        uint64_t *out);
+
+/* ------------------------------------------------------------ width-8 Poseidon2 Merkle trees
+ * zkvm/src/commitments.rs:192-262 (vm_mem_comm / _with_opening): Poseidon2Goldilocks<8>
+ * (poseidon2.rs:31-49; external constants crypto_consts.rs:9-96; internal
+ * diagonal = Plonky3 MATRIX_DIAG_8_GOLDILOCKS, not in the reference: parity
+ * unpinned). A leaf is PaddingFreeSponge<8, rate 4, out 4> of one row, a parent
+ * is TruncatedPermutation<2, 4, 8> of its children.
+ *   nodes: (2 nrows - 1) x 4 words on the device, leaves first, root last
+ *   path: log2(nrows) sibling digests (4 words each, host), leaves first */
+int lf_dev_poseidon2_w8_permute(lf_ctx *ctx, uint64_t *states, size_t n);
+int lf_dev_merkle_tree(lf_ctx *ctx, const uint64_t *rows, size_t nrows, size_t width, uint64_t *nodes);
+int lf_merkle_open(lf_ctx *ctx, const uint64_t *nodes, size_t nrows, size_t index, uint64_t *path);
 
 /* ------------------------------------------------------------ wire format
  * ark-serialize 0.5 CanonicalSerialize as derived on the reference's types

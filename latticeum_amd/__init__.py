@@ -283,6 +283,19 @@ class Context:
                                               degree, _ptr(proof), _ptr(rnd)))
         return proof, rnd
 
+    # ---------------------------------------------------------------- width-8 Merkle trees
+    def dev_poseidon2_w8_permute(self, t):
+        self.check(self.lib.lf_dev_poseidon2_w8_permute(self.h, _dptr(t), t.numel() // 8))
+
+    def dev_merkle_tree(self, rows, nrows: int, width: int, nodes):
+        """memory matrix [nrows][width] -> (2 nrows - 1) x 4 digests, root last"""
+        self.check(self.lib.lf_dev_merkle_tree(self.h, _dptr(rows), nrows, width, _dptr(nodes)))
+
+    def merkle_open(self, nodes, nrows: int, index: int) -> np.ndarray:
+        path = np.zeros(4 * max(1, nrows.bit_length() - 1), np.uint64)
+        self.check(self.lib.lf_merkle_open(self.h, _dptr(nodes), nrows, index, _ptr(path)))
+        return path
+
     def dev_poseidon2_permute(self, t):
         self.check(self.lib.lf_dev_poseidon2_permute(self.h, _dptr(t), t.numel() // 16))
 

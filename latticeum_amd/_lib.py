@@ -115,6 +115,9 @@ SIGNATURES = {
     "lf_transcript_get_short_challenges": (I, [VP, I, SZ, VP]),
     "lf_hash_iter": (None, [VP, SZ, VP]),
     "lf_witness_split_w": (SZ, []),
+    "lf_dev_poseidon2_w8_permute": (I, [VP, VP, SZ]),
+    "lf_dev_merkle_tree": (I, [VP, VP, SZ, SZ, VP]),
+    "lf_merkle_open": (I, [VP, VP, SZ, SZ, VP]),
     "lf_lcccs_serialize": (I, [C.POINTER(LfLcccs), I, VP, SZ, C.POINTER(SZ)]),
     "lf_lcccs_deserialize": (I, [VP, SZ, I, I, VP, SZ, C.POINTER(LfLcccs)]),
     "lf_lfproof_serialize": (I, [C.POINTER(LfLfproof), I, VP, SZ, C.POINTER(SZ)]),

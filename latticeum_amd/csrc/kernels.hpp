@@ -141,6 +141,11 @@ size_t mle_eval_partial_elems(int d, int nm);
 hipError_t mle_dot(const uint64_t *mles, size_t stride, int nm, const uint64_t *eq, size_t n, int d,
                    uint64_t *partial, uint64_t *out, hipStream_t st);
 
+// ---------------------------------------------------------------- width-8 Poseidon2 Merkle trees (merkle.hip)
+hipError_t p2w8_permute(uint64_t *states, size_t n, hipStream_t st);
+// nodes: (2 nrows - 1) x 4 digests, leaves first, each level after the one below, root last
+hipError_t merkle_tree(const uint64_t *rows, size_t nrows, size_t width, uint64_t *nodes, hipStream_t st);
+
 // ---------------------------------------------------------------- sparse Mz products (mz.hip)
 // the t CCS matrices (m x n, ring-element CSR) on the device, with the
 // row-merged [M_0 | .. | M_(t-1)] and the per-matrix transposes as index arrays

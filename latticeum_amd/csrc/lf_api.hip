@@ -1389,6 +1389,39 @@ int lf_dev_mz_evaluate(lf_ctx *c, const lf_ccs *M, const uint64_t *z, int nz, in
   return LF_OK;
 }
 
+// ---------------------------------------------------------------- width-8 Poseidon2 Merkle trees
+int lf_dev_poseidon2_w8_permute(lf_ctx *c, uint64_t *states, size_t n) {
+  if (!c || (!states && n)) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  LF_HIP(c, lfk::p2w8_permute(states, n, c->cur));
+  return LF_OK;
+}
+
+int lf_dev_merkle_tree(lf_ctx *c, const uint64_t *rows, size_t nrows, size_t width, uint64_t *nodes) {
+  if (!c || !rows || !nodes || !width || !nrows || (nrows & (nrows - 1)))
+    return c ? fail(c, LF_ERR_INVALID_ARG, "Merkle tree: a power-of-two number of rows of width >= 1")
+             : LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  LF_HIP(c, lfk::merkle_tree(rows, nrows, width, nodes, c->cur));
+  return LF_OK;
+}
+
+int lf_merkle_open(lf_ctx *c, const uint64_t *nodes, size_t nrows, size_t index, uint64_t *path) {
+  if (!c || !nodes || !path || !nrows || (nrows & (nrows - 1)) || index >= nrows) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  // the sibling of the node on the path at every level, leaves first (open_batch's opening_proof)
+  size_t off = 0, n = nrows, i = index, k = 0;
+  while (n > 1) {
+    LF_HIP(c, hipMemcpyAsync(path + 4 * k, nodes + 4 * (off + (i ^ 1)), 32, hipMemcpyDeviceToHost, c->cur));
+    off += n;
+    n /= 2;
+    i /= 2;
+    k++;
+  }
+  LF_HIP(c, hipStreamSynchronize(c->cur));
+  return LF_OK;
+}
+
 int lf_dev_fold_step(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t W, const lf_fold_step_bufs *b) {
   DevGuard g(c);
   int lb, lbs;

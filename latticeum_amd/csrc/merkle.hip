@@ -1,0 +1,139 @@
+// merkle.hip -- width-8 Poseidon2 Merkle trees of VM memory (SURVEY.md 8(f)
+// rank 3): the zkvm's ZkVmCommitter hashes every memory page (a row of the
+// memory matrix) with PaddingFreeSponge<Poseidon2Goldilocks<8>, 8, 4, 4> and
+// joins digests with TruncatedPermutation<.., 2, 4, 8> up to the root
+// (zkvm/src/commitments.rs:192-262, poseidon2.rs:31-49). Every page hash is an
+// independent sponge chain (one thread each); every tree level is one launch
+// of independent compressions.
+//
+// Constants: the width-8 external rounds from the reference
+// (crypto_consts.rs:9-96), the 22 internal constants shared with width 16;
+// the internal diagonal is Plonky3's MATRIX_DIAG_8_GOLDILOCKS, which the
+// reference does not vendor (restated; parity unpinned).
+#include "gl.hpp"
+#include "kernels.hpp"
+#include "p2_consts.inc"
+
+namespace lfk {
+
+namespace {
+
+__constant__ uint64_t W8_EXT_INIT[32] = LF_P2W8_EXT_INIT;
+__constant__ uint64_t W8_EXT_TERM[32] = LF_P2W8_EXT_TERM;
+__constant__ uint64_t W8_INTERNAL[22] = LF_P2_INTERNAL;
+__constant__ uint64_t W8_DIAG_M1[8] = LF_P2W8_DIAG_M1;
+
+__device__ __forceinline__ uint64_t sbox7(uint64_t x) {
+  const uint64_t x2 = gl::mul(x, x), x4 = gl::mul(x2, x2);
+  return gl::mul(gl::mul(x4, x2), x);
+}
+// MDS light (poseidon2.rs:243-268 at width 8): MDSMat4 on each 4-chunk, then
+// each word plus the sum of its column over the chunks
+__device__ __forceinline__ void mds8(uint64_t *s) {
+#pragma unroll
+  for (int c = 0; c < 8; c += 4) {
+    const uint64_t x0 = s[c], x1 = s[c + 1], x2 = s[c + 2], x3 = s[c + 3];
+    const uint64_t t = gl::add(gl::add(x0, x1), gl::add(x2, x3));
+    s[c + 0] = gl::add(t, gl::add(x0, gl::add(x1, x1)));
+    s[c + 1] = gl::add(t, gl::add(x1, gl::add(x2, x2)));
+    s[c + 2] = gl::add(t, gl::add(x2, gl::add(x3, x3)));
+    s[c + 3] = gl::add(t, gl::add(x3, gl::add(x0, x0)));
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint64_t sum = gl::add(s[k], s[4 + k]);
+    s[k] = gl::add(s[k], sum);
+    s[4 + k] = gl::add(s[4 + k], sum);
+  }
+}
+__device__ void permute8(uint64_t *s) {
+  mds8(s);
+#pragma unroll 1
+  for (int r = 0; r < 4; r++) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) s[i] = sbox7(gl::add(s[i], W8_EXT_INIT[8 * r + i]));
+    mds8(s);
+  }
+#pragma unroll 1
+  for (int r = 0; r < 22; r++) {
+    s[0] = sbox7(gl::add(s[0], W8_INTERNAL[r]));
+    uint64_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) sum = gl::add(sum, s[i]);
+#pragma unroll
+    for (int i = 0; i < 8; i++) s[i] = gl::add(gl::mul(s[i], W8_DIAG_M1[i]), sum);
+  }
+#pragma unroll 1
+  for (int r = 0; r < 4; r++) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) s[i] = sbox7(gl::add(s[i], W8_EXT_TERM[8 * r + i]));
+    mds8(s);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_p2w8_permute(uint64_t *states, size_t n) {
+  const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  uint64_t s[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = gl::canon(states[e * 8 + i]);
+  permute8(s);
+#pragma unroll
+  for (int i = 0; i < 8; i++) states[e * 8 + i] = s[i];
+}
+
+// leaf i = PaddingFreeSponge hash of row i: overwrite state[0..4) with the next
+// four words, permute; a partial last block is permuted too; no padding
+__global__ void __launch_bounds__(256) k_merkle_leaves(const uint64_t *rows, size_t nrows, size_t width,
+                                                      uint64_t *leaves) {
+  const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (e >= nrows) return;
+  const uint64_t *row = rows + e * width;
+  uint64_t s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  size_t pos = 0;
+  while (pos < width) {
+    const size_t take = width - pos < 4 ? width - pos : 4;
+    for (size_t i = 0; i < take; i++) s[i] = gl::canon(row[pos + i]);
+    pos += take;
+    permute8(s);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) leaves[e * 4 + i] = s[i];
+}
+
+// parent i = permute(child 2i || child 2i + 1)[0..4)
+__global__ void __launch_bounds__(256) k_merkle_level(const uint64_t *children, size_t nparents, uint64_t *parents) {
+  const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (e >= nparents) return;
+  uint64_t s[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = children[e * 8 + i];
+  permute8(s);
+#pragma unroll
+  for (int i = 0; i < 4; i++) parents[e * 4 + i] = s[i];
+}
+
+unsigned nb(size_t n) { return (unsigned)((n + 255) / 256); }
+
+}  // namespace
+
+hipError_t p2w8_permute(uint64_t *states, size_t n, hipStream_t st) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_p2w8_permute, dim3(nb(n)), dim3(256), 0, st, states, n);
+  return hipGetLastError();
+}
+
+hipError_t merkle_tree(const uint64_t *rows, size_t nrows, size_t width, uint64_t *nodes, hipStream_t st) {
+  if (!nrows || (nrows & (nrows - 1)) || !width) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_merkle_leaves, dim3(nb(nrows)), dim3(256), 0, st, rows, nrows, width, nodes);
+  size_t off = 0, n = nrows;
+  while (n > 1) {
+    hipLaunchKernelGGL(k_merkle_level, dim3(nb(n / 2)), dim3(256), 0, st, nodes + 4 * off, n / 2,
+                       nodes + 4 * (off + n));
+    off += n;
+    n /= 2;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace lfk

@@ -1083,3 +1083,87 @@ void lfo_spmv(const uint64_t *row_ptr, const uint32_t *col, const uint64_t *val,
       slot_mul_acc(val + k * (size_t)d, z + (size_t)col[k] * d, acc, d);
   }
 }
+
+/* ================================================ width-8 Poseidon2 Merkle trees (8(f) rank 3)
+ * Poseidon2Goldilocks<8> (zkvm/src/poseidon2.rs:31-49, Plonky3 p3-poseidon2 at
+ * git 33e58c7, not vendored): the width-16 round structure above with the
+ * width-8 external constants (crypto_consts.rs:9-96), the same 22 internal
+ * constants, MDS light on two 4-chunks, and Plonky3's MATRIX_DIAG_8_GOLDILOCKS
+ * (restated; parity unpinned: no reference vector exists) */
+static const uint64_t EXT8_INIT[32] = LF_P2W8_EXT_INIT;
+static const uint64_t EXT8_TERM[32] = LF_P2W8_EXT_TERM;
+static const uint64_t DIAG8_M1[8] = LF_P2W8_DIAG_M1;
+static void mds8(uint64_t *s) {
+  for (int c = 0; c < 8; c += 4) {
+    uint64_t x0 = s[c], x1 = s[c + 1], x2 = s[c + 2], x3 = s[c + 3];
+    uint64_t t = lfo_add(lfo_add(x0, x1), lfo_add(x2, x3));
+    s[c + 0] = lfo_add(t, lfo_add(x0, lfo_add(x1, x1)));
+    s[c + 1] = lfo_add(t, lfo_add(x1, lfo_add(x2, x2)));
+    s[c + 2] = lfo_add(t, lfo_add(x2, lfo_add(x3, x3)));
+    s[c + 3] = lfo_add(t, lfo_add(x3, lfo_add(x0, x0)));
+  }
+  for (int k = 0; k < 4; k++) {
+    uint64_t sum = lfo_add(s[k], s[4 + k]);
+    s[k] = lfo_add(s[k], sum);
+    s[4 + k] = lfo_add(s[4 + k], sum);
+  }
+}
+void lfo_p2w8_permute(uint64_t *s) {
+  mds8(s);
+  for (int r = 0; r < 4; r++) {
+    for (int i = 0; i < 8; i++) s[i] = sbox(s[i], EXT8_INIT[8 * r + i]);
+    mds8(s);
+  }
+  for (int r = 0; r < 22; r++) {
+    s[0] = sbox(s[0], INTERNAL[r]);
+    uint64_t sum = 0;
+    for (int i = 0; i < 8; i++) sum = lfo_add(sum, s[i]);
+    for (int i = 0; i < 8; i++) s[i] = lfo_add(lfo_mul(s[i], DIAG8_M1[i]), sum);
+  }
+  for (int r = 0; r < 4; r++) {
+    for (int i = 0; i < 8; i++) s[i] = sbox(s[i], EXT8_TERM[8 * r + i]);
+    mds8(s);
+  }
+}
+/* PaddingFreeSponge<perm, 8, rate 4, out 4>::hash_iter: overwrite mode, permute
+ * on a partial final block, no padding (the structure of poseidon2.rs:210-234) */
+void lfo_p2w8_hash(const uint64_t *in, size_t n, uint64_t out[4]) {
+  uint64_t s[8] = {0};
+  size_t pos = 0;
+  for (;;) {
+    int i;
+    for (i = 0; i < 4; i++) {
+      if (pos < n) {
+        s[i] = in[pos++];
+      } else {
+        if (i != 0) lfo_p2w8_permute(s);
+        goto done;
+      }
+    }
+    lfo_p2w8_permute(s);
+  }
+done:
+  memcpy(out, s, 4 * sizeof(uint64_t));
+}
+/* TruncatedPermutation<perm, 2, 4, 8>::compress: permute(a || b)[0..4] */
+void lfo_p2w8_compress(const uint64_t a[4], const uint64_t b[4], uint64_t out[4]) {
+  uint64_t s[8];
+  memcpy(s, a, 32);
+  memcpy(s + 4, b, 32);
+  lfo_p2w8_permute(s);
+  memcpy(out, s, 32);
+}
+/* MerkleTreeMmcs::commit of one RowMajorMatrix of nrows (a power of two) rows
+ * (commitments.rs:192-262): leaf = hash(row), parent = compress(left, right).
+ * nodes: every level's digests concatenated, leaves first, root last
+ * ((2 nrows - 1) x 4 words) */
+void lfo_merkle_tree(const uint64_t *rows, size_t nrows, size_t width, uint64_t *nodes) {
+  for (size_t i = 0; i < nrows; i++) lfo_p2w8_hash(rows + i * width, width, nodes + 4 * i);
+  size_t off = 0, n = nrows;
+  while (n > 1) {
+    for (size_t i = 0; i < n / 2; i++)
+      lfo_p2w8_compress(nodes + 4 * (off + 2 * i), nodes + 4 * (off + 2 * i + 1), nodes + 4 * (off + n + i));
+    off += n;
+    n /= 2;
+  }
+}

@@ -115,6 +115,12 @@ void lfo_p2_permute_batch(uint64_t *states, size_t n, int nthreads);
 /* hash_iter (ZK/poseidon2.rs:206-235): overwrite sponge, rate 12, out state[0..4] */
 void lfo_p2_hash_iter(const uint64_t *in, size_t n, uint64_t out[4]);
 
+/* ---- width-8 Poseidon2 and Merkle trees (zkvm commitments.rs; parity unpinned: Plonky3 diag) ---- */
+void lfo_p2w8_permute(uint64_t *s);
+void lfo_p2w8_hash(const uint64_t *in, size_t n, uint64_t out[4]);
+void lfo_p2w8_compress(const uint64_t a[4], const uint64_t b[4], uint64_t out[4]);
+void lfo_merkle_tree(const uint64_t *rows, size_t nrows, size_t width, uint64_t *nodes);
+
 /* ---- transcript (ZK/fiat_shamir.rs) over DuplexChallenger<16,12> ---- */
 typedef struct {
   uint64_t state[16];

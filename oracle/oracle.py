@@ -81,6 +81,10 @@ def lib():
         "lfo_ajtai_rows_seeded": (None, [U64, SZ, I, u64p, u64p, SZ, u64p, I]),
         "lfo_rot_lin_combination": (None, [u64p, u64p, SZ, I, u64p]),
         "lfo_eq_table": (None, [u64p, I, I, u64p]),
+        "lfo_p2w8_permute": (None, [u64p]),
+        "lfo_p2w8_hash": (None, [u64p, SZ, u64p]),
+        "lfo_p2w8_compress": (None, [u64p, u64p, u64p]),
+        "lfo_merkle_tree": (None, [u64p, SZ, SZ, u64p]),
         "lfo_spmv": (None, [u64p, np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS"), u64p, SZ, I,
                             u64p, u64p]),
         "lfo_mle_fix_first": (None, [u64p, SZ, I, u64p]),
@@ -356,6 +360,32 @@ def mz_challenged(mats, zs, zetas, nv: int, d: int) -> np.ndarray:
             mle = np.concatenate([slot_mul(mle[x * d:(x + 1) * d], zeta, d) for x in range(n)])
         total = np.array([(int(a) + int(b)) % P for a, b in zip(total, mle)], np.uint64)
     return total
+
+
+# ---------------------------------------------------------------- width-8 Poseidon2 Merkle trees
+def p2w8_permute(state) -> np.ndarray:
+    s = _u64(state).copy()
+    lib().lfo_p2w8_permute(s)
+    return s
+
+
+def p2w8_hash(vals) -> np.ndarray:
+    out = np.zeros(4, np.uint64)
+    v = _u64(vals) if len(vals) else np.zeros(1, np.uint64)
+    lib().lfo_p2w8_hash(v, len(vals), out)
+    return out
+
+
+def p2w8_compress(a, b) -> np.ndarray:
+    out = np.zeros(4, np.uint64)
+    lib().lfo_p2w8_compress(_u64(a), _u64(b), out)
+    return out
+
+
+def merkle_tree(rows, nrows: int, width: int) -> np.ndarray:
+    out = np.zeros((2 * nrows - 1) * 4, np.uint64)
+    lib().lfo_merkle_tree(_u64(rows), nrows, width, out)
+    return out
 
 
 def broadcast(base, d: int) -> np.ndarray:
