@@ -553,6 +553,19 @@ def next_rows(LA, torch, local, cpu):
         "challenged_mle_ms": ms_ch, "etas_ms": ms_ev,
         "challenged_gbs_values": val_bytes / (ms_ch * 1e-3) / 1e9}
     del M, z, ch, ev
+    # the memory Merkle tree of the zkvm's 8 MB VM (8192 pages of 256 words,
+    # vm.rs:106-124; commitments.rs:192-262): 8192 sponge chains of 64 width-8
+    # permutations, then 13 levels of compressions
+    pages, words = 8192, 256
+    mem = torch.empty(pages * words, **i64)
+    ctx.dev_fill_uniform(mem, 0x4C460017)
+    mem.remainder_(1 << 32)  # u32 memory words
+    nodes = torch.empty((2 * pages - 1) * 4, **i64)
+    ms_mk = ev_ms(lambda: ctx.dev_merkle_tree(mem, pages, words, nodes))
+    out["merkle_memory"] = {"workload": f"Merkle tree of the 8 MB VM memory: {pages} pages x {words} words, "
+                                        "width-8 Poseidon2 sponge leaves + compressions",
+                            "ms_per_tree": ms_mk, "permutations": pages * words // 4 + pages - 1}
+    del mem, nodes
     ctx.close()
     torch.cuda.empty_cache()
     return out
