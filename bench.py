@@ -74,8 +74,8 @@ def algorithmic_bytes(d, W, kappa, L=5, K=15):
             + E * (2 * N + W))
     nvec = 2 * (K - 1) + 1  # commit(z)'s A.f rides in the decomposition-commitment pass
     F = 8 * (40 if d == 24 else d)
-    fused = d in (24, 1024)  # the decompositions write planes 1..K-1 as operand rows
-    sides = 2 if d == 1024 else 1  # the d = 1024 decomposition runs both sides in one launch
+    fused = d in (24, 1024, 4096)  # the decompositions write planes 1..K-1 as operand rows
+    sides = 2 if d in (1024, 4096) else 1  # these decompositions run both sides in one launch
     alg = {
         # B2 (per launch): f_coeff in; f_k_coeff, f_k (K N each), w_ccs_k (K W) out
         "decompose": sides * E * (N + 2 * K * N + K * W),
@@ -104,6 +104,11 @@ def kernel_names(LA, d, W, layout):
         return {"decompose": "k_decompose_fused", "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_nega",
                 "fold": "k_fold_nega", "from_w_ccs": "k_from_w_ccs_split" if small else "k_from_w_ccs_n32",
                 "from_f": "k_from_f_split" if small else "k_from_f_n32", "to_frag": "k_to_frag<true, false, true>"}
+    if d == 4096:
+        return {"decompose": "k_decompose_n4k_fused" if layout == 1 else "k_decompose_n4k",
+                "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_nega",
+                "fold": "k_fold_nega", "from_w_ccs": "k_from_w_ccs_nega", "from_f": "k_from_f_nega",
+                "to_frag": "k_to_frag<true, false, true>"}
     return {"decompose": "k_decompose_nega", "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_nega",
             "fold": "k_fold_nega", "from_w_ccs": "k_from_w_ccs_nega", "from_f": "k_from_f_nega",
             "to_frag": "k_to_frag"}
@@ -127,8 +132,10 @@ def load_traffic(d, W, kappa):
         base = k.split("<")[0]
         if base != k and base not in t and sum(x.split("<")[0] == base for x in t) == 1:
             t[base] = t[k]
-    if "k_decompose_fused" in t and "k_pack_sm" in t:  # the decompose phase launches both
-        t["k_decompose_fused"] += t["k_pack_sm"]
+    for dec, pack in (("k_decompose_fused", "k_pack_sm"), ("k_decompose_n4k_fused", "k_pack_sm4"),
+                      ("k_decompose_n4k", "k_pack_sm4")):
+        if dec in t and pack in t:  # the decompose phase launches both
+            t[dec] += t[pack]
     return t
 
 

@@ -79,9 +79,11 @@ __device__ __forceinline__ void phi72_evals(const uint64_t *e, uint64_t *ev) {
   for (int i = 0; i < TF_S; i++)
     if (SB * TF_S + i < 40) ev[i] = ring::phi72_eval(e, SB * TF_S + i);
 }
+// qd > 0: operand slot of slot s is (s % 4) qd + s / 4 (FragGeom::qperm, qd = d / 4)
+__host__ __device__ __forceinline__ size_t op_slot(size_t s, int qd) { return qd ? (s & 3) * qd + (s >> 2) : s; }
 template <bool VMAJOR, bool PHI72, bool ONEROW>
 __global__ void __launch_bounds__(256) k_to_frag(VecPtrs rows, int rlo, int rhi, int d, int dv, int nch, int Lp,
-                                                 size_t Wp, uint4 *frag) {
+                                                 size_t Wp, uint4 *frag, int qd) {
   __shared__ uint64_t tile[TF_R * TF_S * TF_J];
   const int sb = blockIdx.x, tid = threadIdx.x;
   const int c0 = ONEROW ? blockIdx.y * TF_R : blockIdx.y;
@@ -141,7 +143,7 @@ __global__ void __launch_bounds__(256) k_to_frag(VecPtrs rows, int rlo, int rhi,
   }
   uint4 u[8];
   d8_transpose16(x, u);
-  const size_t s = (size_t)sb * TF_S + sl;
+  const size_t s = op_slot((size_t)sb * TF_S + sl, qd);
   if (VMAJOR) {
     uint4 *out = frag + fv_index(s, nch, c, row, h);
 #pragma unroll
@@ -180,7 +182,8 @@ __device__ __forceinline__ int fl_pi(int j, int i) { return i ^ (((j & 7) << 1) 
 template <int CPOL>
 __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const uint4 *Ff, int d, int nch,
                                                       int nvec, int kappa, uint64_t *partial, OutPtrs dst,
-                                                      int direct, int cps, int ktiles, int nbase, size_t tile_u4) {
+                                                      int direct, int cps, int ktiles, int nbase, size_t tile_u4,
+                                                      int qd) {
   __shared__ uint4 Al[2][4][8 * 64];  // 64 KiB: A copies one chunk ahead
   __shared__ uint4 Fl[3][32 * 64];    // 96 KiB: F copies two chunks ahead
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -289,11 +292,12 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const ui
     for (int t = 0; t < 15; t++) S[t >> 2] += (int64_t)x[t] << (8 * (t & 3));
     const uint64_t r = gl::add(fe(S[0] - S[2] - S[3]), gl::mul_pow2(fe(S[1] + S[2]), 32));
     const int row = 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * h;
+    const int so = qd ? (s % qd) * 4 + s / qd : s;  // the ring slot of operand slot s
     if (v < nvec && row < kappa) {
       if (direct)  // one column split: the result itself
-        dst.p[v][(size_t)row * d + s] = r;
+        dst.p[v][(size_t)row * d + so] = r;
       else
-        partial[(((size_t)js * nvec + v) * kappa + row) * d + s] = r;
+        partial[(((size_t)js * nvec + v) * kappa + row) * d + so] = r;
     }
   }
 }
@@ -346,18 +350,20 @@ hipError_t to_frag(const VecPtrs &rows, int nrows, int row0, const FragGeom &g, 
   if (nrows < 1 || row0 < 0 || row0 + nrows > 32 || (d != 24 && d % TF_S)) return hipErrorInvalidValue;
   VecPtrs abs{};
   for (int i = 0; i < nrows; i++) abs.p[row0 + i] = rows.p[i];
+  const int qd = g.qperm ? d / 4 : 0;
   const int rhi = row0 + nrows, ztiles = (rhi + TF_R - 1) / TF_R - row0 / TF_R;
   const dim3 grid((dv + TF_S - 1) / TF_S, g.nch, ztiles);
 #define LF_TF(VM, PH) \
-  hipLaunchKernelGGL((k_to_frag<VM, PH, false>), grid, dim3(256), 0, st, abs, row0, rhi, d, dv, g.nch, g.Lp, g.Wp, frag)
+  hipLaunchKernelGGL((k_to_frag<VM, PH, false>), grid, dim3(256), 0, st, abs, row0, rhi, d, dv, g.nch, g.Lp, g.Wp, frag, \
+                     qd)
   if (nrows == 1 && vmajor) {
     const dim3 grid1((dv + TF_S - 1) / TF_S, (g.nch + TF_R - 1) / TF_R, 1);
     if (d == 24)
       hipLaunchKernelGGL((k_to_frag<true, true, true>), grid1, dim3(256), 0, st, abs, row0, rhi, d, dv, g.nch, g.Lp,
-                         g.Wp, frag);
+                         g.Wp, frag, qd);
     else
       hipLaunchKernelGGL((k_to_frag<true, false, true>), grid1, dim3(256), 0, st, abs, row0, rhi, d, dv, g.nch, g.Lp,
-                         g.Wp, frag);
+                         g.Wp, frag, qd);
     return hipGetLastError();
   }
   if (d == 24) {
@@ -404,10 +410,10 @@ hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, c
   // F is dv nch 8 KiB per launch (A is as large for kappa = 32)
   if ((size_t)dv * g.nch * 8192 > STREAM_OUT_BYTES)
     hipLaunchKernelGGL(k_ajtai_mfma<2>, grid, dim3(256), 0, st, Af, Ff, dv, g.nch, nvec, (int)kappa, partial, kout,
-                       nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4);
+                       nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4, g.qperm ? d / 4 : 0);
   else
     hipLaunchKernelGGL(k_ajtai_mfma<0>, grid, dim3(256), 0, st, Af, Ff, dv, g.nch, nvec, (int)kappa, partial, kout,
-                       nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4);
+                       nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4, g.qperm ? d / 4 : 0);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (ev1) (void)hipEventRecord(ev1, st);

@@ -72,6 +72,9 @@ struct FragGeom {
   int Lp;
   size_t Wp;
   int nch;
+  // d = 4096: operand slot sigma(s) = (s % 4) d/4 + s / 4 (quarter-major, the
+  // order kernels_n4k.hip produces slots in); the contraction maps it back
+  int qperm = 0;
 };
 FragGeom frag_geom(size_t ncols, int Lp);
 // d = 24 (Phi_72) contracts 40 virtual slots per element (Toom-3, ajtai_mfma.hip)
@@ -113,6 +116,13 @@ struct FusedSides {
 hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K, uint32_t *smg,
                            const ring::NegaTables &fwd, uint4 *frag, int nch, int *err, uint64_t *sink, int ncu,
                            hipStream_t st);
+
+// d = 4096, b_small = 2 (kernels_n4k.hip): sm4 holds nside N 1024 packed words; sink 4096 words.
+// With frag (a scheme whose geometry has Lp = L and qperm), planes k >= 1 are also
+// written as operand rows row0[side] + k - 1, as decompose_fused does for d = 1024.
+hipError_t decompose_n4k(const FusedSides &sd, size_t N, int lb, int L, int K, uint64_t *sm4,
+                         const ring::NegaTables &fwd, int *err, uint64_t *sink, int ncu, hipStream_t st,
+                         uint4 *frag = nullptr, int nch = 0);
 
 // ---------------------------------------------------------------- sumcheck (sumcheck.hip)
 // the multisets S_i of a CCS (linearization polynomial), by value as a kernel argument

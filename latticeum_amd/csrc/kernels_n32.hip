@@ -31,16 +31,7 @@ __device__ __forceinline__ Half half_ctx(uint64_t *lds_all) {
   x.lds = lds_all + wib * n32::WAVE_U64 + x.h * n32::HALF_U64;
   return x;
 }
-// issue 32 row loads before the first use: the asm consumes the values in
-// groups of 8, so the scheduler cannot interleave load -> wait -> use per value
-__device__ __forceinline__ void load_row32(const uint64_t *p, uint64_t *v) {
-#pragma unroll
-  for (int k = 0; k < 32; k++) v[k] = p[32 * k];
-#pragma unroll
-  for (int k = 0; k < 32; k += 8)
-    asm volatile("" : "+v"(v[k]), "+v"(v[k + 1]), "+v"(v[k + 2]), "+v"(v[k + 3]), "+v"(v[k + 4]), "+v"(v[k + 5]),
-                 "+v"(v[k + 6]), "+v"(v[k + 7]));
-}
+using n32::load_row32;
 // the loop bound every lane of a wave agrees on (both halves iterate together)
 __device__ __forceinline__ size_t pair_bound(size_t n) { return (n + 1) & ~(size_t)1; }
 }  // namespace

@@ -1,0 +1,333 @@
+// kernels_n4k.hip -- the X^4096 + 1 ring (BASELINE configs[4]) on the
+// register-resident 1024-point transform of ntt32.hpp. With j = a + 1024 b and
+// m = m0 + 4 m1 (a, m1 < 1024; b, m0 < 4), tools/ntt4096_model.py:
+//   X[m0 + 4 m1] = NTT1024_{psi^4}(y_m0)[m1]
+//   y_m0[a]      = psi^((2 m0 - 3) a) * sum_b x[a + 1024 b] w8^(b (2 m0 + 1)),  w8 = psi^1024 = 2^120
+// psi^4 is the X^1024 + 1 root, so the sub-transform is n32::forward with the
+// d = 1024 middle factors. Each quarter m0 is independent: a wave owns one m0
+// (wave-uniform) and its two halves two different work items, so no wave waits
+// for another and there is no s_barrier in the loop. The four waves of one
+// work item share a block (one CU, one L2), so their interleaved slot stores
+// (stride 4) merge into whole lines before they reach HBM.
+#include "digits.hpp"
+#include "frag.hpp"
+#include "kernels.hpp"
+#include "ntt32.hpp"
+
+namespace lfk {
+
+namespace {
+constexpr int D4 = 4096, Q4 = 1024;
+constexpr int WPB4 = 8;  // two work-item pairs x four quarters; one block per CU (LDS)
+
+// bit t of a 16-bit value -> bit 4 t (Morton spread for four interleaved values)
+__device__ __forceinline__ uint64_t spread4(uint32_t v) {
+  uint64_t x = v & 0xFFFFu;
+  x = (x | (x << 24)) & 0x000000FF000000FFull;
+  x = (x | (x << 12)) & 0x000F000F000F000Full;
+  x = (x | (x << 6)) & 0x0303030303030303ull;
+  x = (x | (x << 3)) & 0x1111111111111111ull;
+  return x;
+}
+__device__ __forceinline__ uint32_t sign_mag16(uint64_t x, int K, bool &bad) {
+  const int64_t a = signed_rep(x);
+  const uint64_t m = a < 0 ? (uint64_t)(-a) : (uint64_t)a;
+  bad |= (m >> K) != 0;
+  return (uint32_t)(m & 0x7FFF) | (a < 0 ? 0x8000u : 0u);
+}
+}  // namespace
+
+// ---------------------------------------------------------------- decompose_witness, d = 4096
+// The coefficients of element e at a, a + 1024, a + 2048, a + 3072 as one word:
+// magnitude bit t of quarter b at bit 4 t + b, the sign of quarter b at bit 60 + b
+// (K <= 15), so digit plane k of all four is the nibble at 4 k and one shift.
+__global__ void k_pack_sm4(FusedSides sd, size_t N, int K, uint64_t *sm4, int *err) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // (side, element, a)
+  if (t >= sd.nside * N * Q4) return;
+  const int side = t >= N * Q4;
+  const size_t ea = t - side * N * Q4;
+  const uint64_t *x = sd.f_coeff[side] + (ea >> 10) * D4 + (ea & (Q4 - 1));
+  bool bad = false;
+  uint64_t w = 0;
+#pragma unroll
+  for (int b = 0; b < 4; b++) w |= spread4(sign_mag16(x[b * Q4], K, bad)) << b;
+  if (bad) raise(err, 1);
+  sm4[t] = w;
+}
+
+// One quarter m0 of digit plane kb of one element, from the element's packed
+// words (lane r: words of a = r + 32 k): this quarter's digits (b = m0) to oc[32 k],
+// y_m0 (the radix-4 butterfly of the four digits is a table lookup: 81 values
+// per m0, zt[nibble | signs << 4]; then the twist), and its 1024-point transform:
+// v[i] = slot m0 + 4 (r + 32 brv5(i)).
+template <bool NT>
+__device__ __forceinline__ void quarter_ntt(const uint64_t *words, int kb, int m0, const uint64_t *zt,
+                                            const uint64_t *tw, uint64_t *oc, const uint64_t *mid, uint64_t *T, int r,
+                                            uint64_t *v) {
+  n32::load_row32(words, v);
+#pragma unroll
+  for (int k = 0; k < 32; k++) {
+    const uint64_t w = v[k];
+    const uint32_t nib = (uint32_t)(w >> (4 * kb)) & 15u, sg = (uint32_t)(w >> 60);
+    const uint32_t bit = (nib >> m0) & 1u, neg = (sg >> m0) & 1u;
+    // this quarter's digit: 0, 1 or p - 1 = 0xFFFFFFFF00000000
+    const uint64_t own = ((uint64_t)(bit & neg) * 0xFFFFFFFF00000000ull) | (uint64_t)(bit & (neg ^ 1u));
+    out_store<NT>(&oc[32 * k], own);
+    v[k] = zt[nib | (sg << 4)];
+  }
+#pragma unroll
+  for (int k0 = 0; k0 < 32; k0 += 8) {
+    uint64_t t8[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) t8[k] = tw[32 * (k0 + k)];
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k0 + k] = gl::mul(v[k0 + k], t8[k]);
+  }
+  n32::forward(v, mid, T, r);
+}
+// w_ccs_k's Horner step (B = 2^lb) over the limbs, from the top one
+__device__ __forceinline__ void horner_step(uint64_t *acc, const uint64_t *v, bool first, int lb, uint64_t b_pow) {
+  if (first) {
+#pragma unroll
+    for (int i = 0; i < 32; i++) acc[i] = v[i];
+  } else if (lb == 15) {  // GoldiLocksDP B = 2^15: a shift instead of a product
+#pragma unroll
+    for (int i = 0; i < 32; i++) acc[i] = gl::add_weak(gl::shl_small_weak(acc[i], 15), v[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 32; i++) acc[i] = gl::add(gl::mul(acc[i], b_pow), v[i]);
+  }
+}
+
+// LF/nifs/decomposition.rs:162-167, decomposition/utils.rs:45-49, arith.rs:324-338
+// for b_small = 2 (digit = sign(v) bit_k(|v|)). A work item is (side, group g,
+// plane k); per limb l the wave's quarter m0 writes f_coeff_k's quarter b = m0
+// and slots m0 + 4 m1 of f_k; w_ccs_k = sum_l B^l f_k[gL + l] accumulates in
+// the same registers.
+__global__ void __launch_bounds__(512, 1) k_decompose_n4k(const uint64_t *sm4_all, size_t N, int L, int lb, int K,
+                                                         FusedSides sd, const uint64_t *mid_fg, const uint64_t *tw_g,
+                                                         const uint64_t *ztab_g, uint64_t *sink) {
+  __shared__ uint64_t lds_all[WPB4 * n32::WAVE_U64];
+  __shared__ uint64_t mid_f[n32::MID_U64];
+  __shared__ uint64_t ztab[4 * 256];
+  n32::stage_mid(mid_f, mid_fg);
+  for (int q = threadIdx.x; q < 4 * 256; q += blockDim.x) ztab[q] = ztab_g[q];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5, m0 = wib & 3;
+  uint64_t *T = lds_all + wib * n32::WAVE_U64 + h * n32::HALF_U64;
+  const uint64_t *zt = ztab + m0 * 256;
+  const uint64_t *tw = tw_g + m0 * Q4 + r;
+  const size_t W = N / L, ntask = sd.nside * W * K, npair = (ntask + 1) / 2;
+  const uint64_t b_pow = gl::mul_pow2(1, lb);  // B = 2^lb
+  for (size_t tp = (size_t)blockIdx.x * 2 + (wib >> 2); tp < npair; tp += (size_t)gridDim.x * 2) {
+    // the two halves: consecutive planes of (mostly) one group, so both read the same words
+    const size_t t = 2 * tp + h;
+    const bool ok = t < ntask;
+    const size_t tt = ok ? t : 0;
+    const int kb = (int)(tt % K);
+    const size_t gt = tt / K;
+    const int side = gt >= W;
+    const size_t g = gt - side * W;
+    const uint64_t *sm4 = sm4_all + side * N * Q4;
+    uint64_t acc[32];
+    for (int l = L - 1; l >= 0; l--) {
+      const size_t e = (size_t)kb * N + g * L + l;
+      uint64_t v[32];
+      quarter_ntt<false>(sm4 + (g * L + l) * Q4 + r, kb, m0, zt, tw,
+                         (ok ? sd.f_coeff_k[side] + e * D4 + m0 * Q4 : sink) + r, mid_f, T, r, v);
+      uint64_t *of = (ok ? sd.f_k[side] + e * D4 : sink) + m0 + 4 * r;
+#pragma unroll
+      for (int i = 0; i < 32; i++) of[128 * n32::brv5(i)] = v[i];
+      horner_step(acc, v, l == L - 1, lb, b_pow);
+    }
+    uint64_t *ow = (ok ? sd.w_ccs_k[side] + ((size_t)kb * W + g) * D4 : sink) + m0 + 4 * r;
+#pragma unroll
+    for (int i = 0; i < 32; i++) ow[128 * n32::brv5(i)] = gl::canon(acc[i]);
+  }
+}
+
+// ---------------------------------------------------------------- fused with the Ajtai operands
+// As decompose_fused (kernels_n32.hip) for d = 1024: a block of 8 waves owns 16
+// consecutive groups (one per half-wave) at one digit plane and one quarter m0,
+// so for each limb l it holds one 16-column unit of the contraction order
+// (Lp = L) and writes the plane (k >= 1) straight into the vector-major operand
+// buffer. The operand slots are quarter-major (FragGeom::qperm): one quarter's
+// 1024 slots are 256 whole slot quads, so the pieces of a quad (4 neighbouring
+// threads) form whole 64-B segments. The blocks of the four quarters of a unit
+// are b, b + 8, b + 16, b + 24: the same XCD (blocks are dealt round-robin over
+// the 8), so the interleaved f_k slot stores of the four meet in one L2.
+//
+// The digits come as one byte per coefficient quad and plane (k_pack_sm8:
+// nibble | signs << 4, the index of the butterfly table), 32 bytes per lane per
+// limb, prefetched one limb ahead (issued before the limb's stores, so waiting
+// for them does not drain those stores). The quarter's twists, the table and
+// the middle factors stay in LDS.
+constexpr int FQ_WAVES = 8;
+constexpr int FQ_SROW = 17;  // staging row stride in u64 (16 groups + pad: conflict-free)
+constexpr int FQ_T_U64 = FQ_WAVES * n32::WAVE_U64;
+constexpr int FQ_S_U64 = Q4 * FQ_SROW;
+constexpr int FQ_LDS_U64 = FQ_T_U64 > FQ_S_U64 ? FQ_T_U64 : FQ_S_U64;
+
+// byte (element e, plane kb, lane r, k) at ((e K + kb) 32 + r) 32 + k; one
+// thread per (side, e, r, j) packs k = 4 j .. 4 j + 3 (one word per plane)
+__global__ void k_pack_sm8(FusedSides sd, size_t N, int K, uint32_t *sm8, int *err) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // (side, element, r, j)
+  if (t >= sd.nside * N * 256) return;
+  const int side = t >= N * 256;
+  const size_t erj = t - side * N * 256, e = erj >> 8;
+  const int r = (int)((erj >> 3) & 31), j = (int)(erj & 7);
+  const uint64_t *x = sd.f_coeff[side] + e * D4 + r + 128 * j;
+  uint64_t w[4];
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    w[k] = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) w[k] |= spread4(sign_mag16(x[32 * k + b * Q4], K, bad)) << b;
+  }
+  if (bad) raise(err, 1);
+  uint32_t *o = sm8 + ((side * N + e) * K * 32 + r) * 8 + j;
+  for (int kb = 0; kb < K; kb++) {
+    uint32_t q = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      q |= (((uint32_t)(w[k] >> (4 * kb)) & 15u) | ((uint32_t)(w[k] >> 60) << 4)) << (8 * k);
+    o[kb * 256] = q;
+  }
+}
+
+template <bool NT>
+__global__ void __launch_bounds__(512, 1) k_decompose_n4k_fused(const uint32_t *sm8, size_t N, int L, int lb, int K,
+                                                               FusedSides sd, const uint64_t *mid_fg,
+                                                               const uint64_t *tw_g, const uint64_t *ztab_g,
+                                                               uint4 *frag, int nch, uint64_t *sink) {
+  __shared__ uint64_t lds_all[FQ_LDS_U64];
+  __shared__ uint64_t mid_f[n32::MID_U64];
+  __shared__ uint64_t twl[Q4];
+  __shared__ uint64_t zt[256];
+  const int m0 = (blockIdx.x >> 3) & 3;
+  n32::stage_mid(mid_f, mid_fg);
+  for (int q = threadIdx.x; q < Q4; q += blockDim.x) twl[q] = tw_g[m0 * Q4 + q];
+  for (int q = threadIdx.x; q < 256; q += blockDim.x) zt[q] = ztab_g[m0 * 256 + q];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5, hw = 2 * wib + h;  // hw: this half's group within the block
+  uint64_t *T = lds_all + wib * n32::WAVE_U64 + h * n32::HALF_U64;
+  uint64_t *S = lds_all;
+  const size_t W = N / L, nblk = (W + 15) / 16, nunit = sd.nside * nblk * K;
+  const uint64_t b_pow = gl::mul_pow2(1, lb);  // B = 2^lb
+  const size_t ustride = 8 * (size_t)(gridDim.x >> 5);
+  for (size_t unit = (blockIdx.x & 7) + 8 * (size_t)(blockIdx.x >> 5); unit < nunit; unit += ustride) {
+    const int side = unit >= nblk * K;
+    const size_t B = unit / K - side * nblk;
+    const int kb = (int)(unit % K);
+    const size_t g = 16 * B + hw;
+    const bool ok = g < W;
+    const size_t gg = ok ? g : 0;
+    // this lane's 32 bytes of limb l: 8 words
+    auto bytes_of = [&](int l) { return sm8 + (((side * N + gg * L + l) * K + kb) * 32 + r) * 8; };
+    uint32_t wn[8];
+    {
+      const uint4 *p = reinterpret_cast<const uint4 *>(bytes_of(L - 1));
+      const uint4 a = p[0], c = p[1];
+      wn[0] = a.x, wn[1] = a.y, wn[2] = a.z, wn[3] = a.w, wn[4] = c.x, wn[5] = c.y, wn[6] = c.z, wn[7] = c.w;
+    }
+    asm volatile("" : "+v"(wn[0]), "+v"(wn[1]), "+v"(wn[2]), "+v"(wn[3]), "+v"(wn[4]), "+v"(wn[5]), "+v"(wn[6]),
+                 "+v"(wn[7]));
+    uint64_t acc[32];
+    for (int l = L - 1; l >= 0; l--) {
+      const size_t e = (size_t)kb * N + gg * L + l;
+      uint64_t v[32], own[32];
+#pragma unroll
+      for (int k = 0; k < 32; k++) {
+        const uint32_t byte = (wn[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+        const uint32_t bit = (byte >> m0) & 1u, neg = (byte >> (4 + m0)) & 1u;
+        // this quarter's digit: 0, 1 or p - 1 = 0xFFFFFFFF00000000
+        own[k] = ((uint64_t)(bit & neg) * 0xFFFFFFFF00000000ull) | (uint64_t)(bit & (neg ^ 1u));
+        v[k] = zt[byte];
+      }
+      {  // the next limb's bytes (at l = 0 a harmless reload of limb L - 1)
+        const uint4 *p = reinterpret_cast<const uint4 *>(bytes_of(l > 0 ? l - 1 : L - 1));
+        const uint4 a = p[0], c = p[1];
+        wn[0] = a.x, wn[1] = a.y, wn[2] = a.z, wn[3] = a.w, wn[4] = c.x, wn[5] = c.y, wn[6] = c.z, wn[7] = c.w;
+      }
+      {
+        uint64_t *oc = (ok ? sd.f_coeff_k[side] + e * D4 + m0 * Q4 : sink) + r;
+#pragma unroll
+        for (int k = 0; k < 32; k++) out_store<NT>(&oc[32 * k], own[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < 32; k++) v[k] = gl::mul(v[k], twl[r + 32 * k]);
+      n32::forward(v, mid_f, T, r);
+      {
+        uint64_t *of = (ok ? sd.f_k[side] + e * D4 : sink) + m0 + 4 * r;
+#pragma unroll
+        for (int i = 0; i < 32; i++) of[128 * n32::brv5(i)] = v[i];
+      }
+      horner_step(acc, v, l == L - 1, lb, b_pow);
+      if (kb > 0) {
+        __syncthreads();  // every wave is past its transpose: S may overwrite T
+#pragma unroll
+        for (int i = 0; i < 32; i++) S[(r + 32 * n32::brv5(i)) * FQ_SROW + hw] = d8(v[i]);
+        __syncthreads();
+        const size_t u = B * L + l;  // contraction unit of these 16 columns
+        const int c = (int)(u >> 1), uh = (int)(u & 1), row = sd.row0[side] + kb - 1;
+#pragma unroll
+        for (int rep = 0; rep < 2; rep++) {
+          const int m1 = threadIdx.x + 512 * rep;
+          const uint64_t *src = S + m1 * FQ_SROW;
+          uint64_t x[16];
+#pragma unroll
+          for (int j = 0; j < 16; j++) x[j] = src[j];
+          uint4 pu[8];
+          d8_transpose16(x, pu);
+          uint4 *out = frag + fv_index((size_t)m0 * Q4 + m1, nch, c, row, uh);
+#pragma unroll
+          for (int b = 0; b < 8; b++) out_store<NT>(&out[4 * b], pu[b]);
+        }
+        __syncthreads();  // S consumed before the next transpose
+      }
+    }
+    uint64_t *ow = (ok ? sd.w_ccs_k[side] + ((size_t)kb * W + g) * D4 : sink) + m0 + 4 * r;
+#pragma unroll
+    for (int i = 0; i < 32; i++) ow[128 * n32::brv5(i)] = gl::canon(acc[i]);
+  }
+}
+
+hipError_t decompose_n4k(const FusedSides &sd, size_t N, int lb, int L, int K, uint64_t *sm4,
+                         const ring::NegaTables &fwd, int *err, uint64_t *sink, int ncu, hipStream_t st, uint4 *frag,
+                         int nch) {
+  if (K > 15 || !fwd.mid || !fwd.tw4 || !fwd.ztab || !sink || ncu < 1 || sd.nside < 1 || sd.nside > 2 || N % L)
+    return hipErrorInvalidValue;
+  if (N == 0) return hipSuccess;
+  if (frag) {
+    for (int s = 0; s < sd.nside; s++)
+      if (sd.row0[s] < 0 || sd.row0[s] + K - 1 > 32) return hipErrorInvalidValue;
+    if (ncu < 32) return hipErrorInvalidValue;
+    uint32_t *sm8 = reinterpret_cast<uint32_t *>(sm4);  // nside N K 256 words
+    const size_t threads = sd.nside * N * 256;
+    hipLaunchKernelGGL(k_pack_sm8, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, sd, N, K, sm8, err);
+    // 32 blocks per group of 8 units (8 XCDs x 4 quarters), one block per CU
+    const unsigned grid = (unsigned)(ncu / 32 * 32);
+    // outputs: f_coeff_k, f_k, the operand rows (each K N d words per side) and w_ccs_k
+    if (sd.nside * (size_t)K * N * D4 * 8 * 3 > STREAM_OUT_BYTES)
+      hipLaunchKernelGGL(k_decompose_n4k_fused<true>, dim3(grid), dim3(512), 0, st, sm8, N, L, lb, K, sd, fwd.mid,
+                         fwd.tw4, fwd.ztab, frag, nch, sink);
+    else
+      hipLaunchKernelGGL(k_decompose_n4k_fused<false>, dim3(grid), dim3(512), 0, st, sm8, N, L, lb, K, sd, fwd.mid,
+                         fwd.tw4, fwd.ztab, frag, nch, sink);
+    return hipGetLastError();
+  }
+  const size_t words = sd.nside * N * Q4;
+  hipLaunchKernelGGL(k_pack_sm4, dim3((unsigned)((words + 255) / 256)), dim3(256), 0, st, sd, N, K, sm4, err);
+  const size_t npair = (sd.nside * (N / L) * K + 1) / 2;
+  // one block per CU, each taking the same number of work-item pairs
+  const size_t per = (npair + 2 * ncu - 1) / (2 * ncu);
+  const unsigned grid = (unsigned)((npair + 2 * per - 1) / (2 * per));
+  hipLaunchKernelGGL(k_decompose_n4k, dim3(grid), dim3(64 * WPB4), 0, st, sm4, N, L, lb, K, sd, fwd.mid, fwd.tw4,
+                     fwd.ztab, sink);
+  return hipGetLastError();
+}
+
+}  // namespace lfk

@@ -47,7 +47,7 @@ struct lf_ctx {
   size_t frag_elems = 0;
   uint32_t *smg = nullptr;      // packed coefficients for the fused decomposition
   size_t smg_elems = 0;
-  uint64_t *sink = nullptr;     // 8 KiB row the fused decomposition stores groups past W into
+  uint64_t *sink = nullptr;     // 32 KiB row the fused decompositions store work past the end into
   int ncu = 0;                  // compute units of `device`
   uint64_t *stage = nullptr;    // sharded step: the partial commitments [nvec][kappa d]
   size_t stage_elems = 0;
@@ -151,7 +151,10 @@ int get_tables(lf_ctx *c, int d, Tables *&out) {
   }
   Tables t;
   if (d != 24) {
-    const size_t extra = d == 1024 ? 2048 : 0;  // 32 x 32 NTT middle factors (fwd, inv)
+    // d = 1024: the 32 x 32 NTT middle factors (fwd, inv); d = 4096: those of its
+    // 1024-point sub-transforms, then the radix-4 twists (fwd, inv) and the digit
+    // butterfly table (kernels_n4k.hip)
+    const size_t extra = d == 1024 ? 2048 : d == 4096 ? 2048 + 2 * 4096 + 1024 : 0;
     std::vector<uint64_t> h(4 * (size_t)d + extra);
     const uint64_t psi = gl::pow(7, (gl::P - 1) / (2 * (uint64_t)d));
     const uint64_t psi_inv = gl::inv(psi), w = gl::mul(psi, psi), w_inv = gl::mul(psi_inv, psi_inv);
@@ -171,16 +174,44 @@ int get_tables(lf_ctx *c, int d, Tables *&out) {
     if (h[d + d / 4] != gl::mul_pow2(1, 48) || h[3 * d + d / 4] != gl::mul_pow2(1, 144))
       return fail(c, LF_ERR_DEVICE, "unexpected 4th root of unity");
     if (extra) {
-      // ntt32.hpp relies on psi^32 = 2^39 and psi^64 = 2^78 (shift-only 32-point stages)
-      if (gl::pow(psi, 32) != gl::mul_pow2(1, 39) || gl::pow(psi, 64) != gl::mul_pow2(1, 78))
+      // the 1024-point transform's root: psi itself (d = 1024) or psi^4 (d = 4096)
+      const uint64_t p1 = d == 1024 ? psi : gl::pow(psi, 4), p1_inv = gl::inv(p1), q1inv = gl::inv(1024);
+      // ntt32.hpp relies on p1^32 = 2^39 and p1^64 = 2^78 (shift-only 32-point stages)
+      if (gl::pow(p1, 32) != gl::mul_pow2(1, 39) || gl::pow(p1, 64) != gl::mul_pow2(1, 78))
         return fail(c, LF_ERR_DEVICE, "unexpected root of unity for the 32 x 32 NTT");
       auto brv5 = [](int i) { return ((i & 1) << 4) | ((i & 2) << 2) | (i & 4) | ((i & 8) >> 2) | ((i & 16) >> 4); };
       for (int r = 0; r < 32; r++)
         for (int i = 0; i < 32; i++) {
-          // forward: psi^((2 brv5(i) + 1) r);  inverse: d^-1 psi^-((2r + 1) brv5(i))
-          h[4 * d + r * 32 + i] = gl::pow(psi, (uint64_t)(2 * brv5(i) + 1) * r);
-          h[4 * d + 1024 + r * 32 + i] = gl::mul(dinv, gl::pow(psi_inv, (uint64_t)(2 * r + 1) * brv5(i)));
+          // forward: p1^((2 brv5(i) + 1) r);  inverse: 1024^-1 p1^-((2r + 1) brv5(i))
+          h[4 * d + r * 32 + i] = gl::pow(p1, (uint64_t)(2 * brv5(i) + 1) * r);
+          h[4 * d + 1024 + r * 32 + i] = gl::mul(q1inv, gl::pow(p1_inv, (uint64_t)(2 * r + 1) * brv5(i)));
         }
+      if (d == 4096) {
+        // kernels_n4k.hip relies on psi^1024 = 2^120 (the radix-4 butterflies are shifts)
+        if (gl::pow(psi, 1024) != gl::mul_pow2(1, 120)) return fail(c, LF_ERR_DEVICE, "unexpected 8th root of unity");
+        uint64_t *tf = h.data() + 4 * d + 2048, *ti = tf + 4096, *zt = ti + 4096;
+        const uint64_t inv4 = gl::inv(4);
+        for (int m0 = 0; m0 < 4; m0++) {
+          const uint64_t s = gl::pow(psi, (uint64_t)((2 * m0 - 3 + 8192) % 8192));  // psi^(2 m0 - 3)
+          const uint64_t s_inv = gl::inv(s);
+          uint64_t f = 1, g = inv4;
+          for (int ai = 0; ai < 1024; ai++) {
+            tf[m0 * 1024 + ai] = f;  // psi^((2 m0 - 3) a)
+            ti[m0 * 1024 + ai] = g;  // 4^-1 psi^-((2 m0 - 3) a)
+            f = gl::mul(f, s);
+            g = gl::mul(g, s_inv);
+          }
+          for (int idx = 0; idx < 256; idx++) {  // sum_b d_b 2^(120 b (2 m0 + 1)), d_b = +-bit_b
+            uint64_t z = 0;
+            for (int bb = 0; bb < 4; bb++) {
+              if (!((idx >> bb) & 1)) continue;
+              const uint64_t cb = gl::mul_pow2(1, (120 * bb * (2 * m0 + 1)) % 192);
+              z = (idx >> (4 + bb)) & 1 ? gl::sub(z, cb) : gl::add(z, cb);
+            }
+            zt[m0 * 256 + idx] = z;
+          }
+        }
+      }
     }
     LF_HIP(c, hipMalloc(&t.mem, h.size() * 8));
     LF_HIP(c, hipMemcpy(t.mem, h.data(), h.size() * 8, hipMemcpyHostToDevice));
@@ -190,6 +221,11 @@ int get_tables(lf_ctx *c, int d, Tables *&out) {
     const bool n32 = extra && !(sel && strcmp(sel, "stockham") == 0);
     t.fwd = {t.mem, t.mem + d, n32 ? t.mem + 4 * d : nullptr};
     t.inv = {t.mem + 2 * d, t.mem + 3 * d, n32 ? t.mem + 4 * d + 1024 : nullptr};
+    if (n32 && d == 4096) {
+      t.fwd.tw4 = t.mem + 4 * d + 2048;
+      t.inv.tw4 = t.fwd.tw4 + 4096;
+      t.fwd.ztab = t.inv.tw4 + 4096;
+    }
   }
   out = &(c->tables[d] = t);
   return LF_OK;
@@ -280,6 +316,7 @@ int ajtai_launch(lf_ctx *c, const lf_ajtai *aj, const uint64_t *const *vecs, int
 int ajtai_prepare(lf_ctx *c, lf_ajtai *aj) {
   if (!use_mfma(aj->d, aj->kappa)) return LF_OK;
   aj->geom = ajtai_geom(aj->ncols);
+  aj->geom.qperm = aj->d == 4096;  // the slot order kernels_n4k.hip produces
   const size_t n = lfk::frag_elems(aj->geom, aj->d);
   const int ktiles = lfk::mfma_ktiles(aj->kappa);
   LF_HIP(c, hipMalloc((void **)&aj->Af, n * ktiles * sizeof(uint4)));
@@ -340,6 +377,28 @@ struct PhaseTimer {
 //  fold_finish: y_0 = cm - sum b^k y_k of both sides, cm_0 = sum rho_i y_i,
 //    f_0 = sum rho_i f_i (folding.rs:258-268, folding/utils.rs:470-476) and
 //    Witness::from_f(f_0) (arith.rs:299-313).
+// d = 4096 with b_small = 2: the register-transform decomposition (kernels_n4k.hip),
+// all sides in one launch; the packed coefficients go to the smg scratch
+bool n4k_ok(const Tables *t, int d, int lbs, int K) { return d == 4096 && lbs == 1 && K <= 15 && t->fwd.tw4; }
+int decompose_n4k_sides(lf_ctx *c, const Tables *t, int nside, const uint64_t *const *fc, uint64_t *const *fck,
+                        uint64_t *const *fk, uint64_t *const *wk, size_t N, int lb, int L, int K,
+                        uint4 *frag = nullptr, int nch = 0, const int *row0 = nullptr) {
+  // packed digits: one u64 per 4 coefficients, or (fused) one byte per 4 coefficients and plane
+  LF_TRY(grow(c, c->smg, c->smg_elems, (size_t)nside * N * (frag ? (size_t)K * 256 : 2048)));
+  lfk::FusedSides sd{};
+  sd.nside = nside;
+  for (int s = 0; s < nside; s++) {
+    sd.f_coeff[s] = fc[s];
+    sd.f_coeff_k[s] = fck[s];
+    sd.f_k[s] = fk[s];
+    sd.w_ccs_k[s] = wk[s];
+    sd.row0[s] = row0 ? row0[s] : 0;
+  }
+  LF_HIP(c, lfk::decompose_n4k(sd, N, lb, L, K, reinterpret_cast<uint64_t *>(c->smg), t->fwd, c->d_err, c->sink,
+                               c->ncu, c->cur, frag, nch));
+  return LF_OK;
+}
+
 int fold_nvec(const lf_params *pr, bool commit_f) { return (commit_f ? 1 : 0) + 2 * (pr->K - 1); }
 
 int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lbs, size_t W,
@@ -359,9 +418,16 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
   const bool fused = aj->Af && aj->geom.Lp == L && d == 1024 && lbs == 1 && K <= 15 && t->fwd.mid;
   // Phi_72 (d = 24): each side's decomposition writes its planes as operand rows (kernels.hip)
   const bool fused24 = aj->Af && aj->geom.Lp == L && d == 24 && L <= 5;
-  if (fused || fused24) {
+  // d = 4096 (kernels_n4k.hip): the same, with the quarter-major operand slots
+  const bool fused4k = aj->Af && aj->geom.Lp == L && aj->geom.qperm && n4k_ok(t, d, lbs, K);
+  if (fused || fused24 || fused4k) {
     LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->geom, d)));
-    if (fused) {
+    if (fused4k) {
+      const int row0[2] = {extra, extra + K - 1};
+      PhaseTimer pt(c, LF_PHASE_DECOMPOSE);  // both sides in one launch
+      LF_TRY(decompose_n4k_sides(c, t, 2, fc_side, b->fk_coeff, b->fk, b->wk, N, lb, L, K, c->frag, aj->geom.nch,
+                                 row0));
+    } else if (fused) {
       LF_TRY(grow(c, c->smg, c->smg_elems, 2 * N * 512));
       lfk::FusedSides sd{};
       sd.nside = 2;
@@ -399,10 +465,15 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
     if (c->timing) c->pending.push_back({ea, eb, nvec});
     return LF_OK;
   }
-  for (int s = 0; s < 2; s++) {
-    PhaseTimer pt(c, LF_PHASE_DECOMPOSE);
-    LF_HIP(c, lfk::decompose_witness(fc_side[s], N, d, lb, L, lbs, K, b->fk_coeff[s], b->fk[s], b->wk[s], t->fwd,
-                                     c->d_err, c->cur));
+  if (n4k_ok(t, d, lbs, K)) {
+    PhaseTimer pt(c, LF_PHASE_DECOMPOSE);  // both sides in one launch
+    LF_TRY(decompose_n4k_sides(c, t, 2, fc_side, b->fk_coeff, b->fk, b->wk, N, lb, L, K));
+  } else {
+    for (int s = 0; s < 2; s++) {
+      PhaseTimer pt(c, LF_PHASE_DECOMPOSE);
+      LF_HIP(c, lfk::decompose_witness(fc_side[s], N, d, lb, L, lbs, K, b->fk_coeff[s], b->fk[s], b->wk[s], t->fwd,
+                                       c->d_err, c->cur));
+    }
   }
   // commit_witnesses: 2(K-1) commitments sharing one pass over A (decomposition.rs:185-188)
   std::vector<const uint64_t *> vecs;
@@ -556,7 +627,7 @@ int lf_ctx_create(int device, lf_ctx **out) {
   c->cur = c->own;
   if (hipMalloc(&c->d_err, sizeof(int)) != hipSuccess) return LF_ERR_OUT_OF_MEMORY;
   if (hipMemset(c->d_err, 0, sizeof(int)) != hipSuccess) return LF_ERR_DEVICE;
-  if (hipMalloc(&c->sink, 1024 * sizeof(uint64_t)) != hipSuccess) return LF_ERR_OUT_OF_MEMORY;
+  if (hipMalloc(&c->sink, 4096 * sizeof(uint64_t)) != hipSuccess) return LF_ERR_OUT_OF_MEMORY;
   if (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c->ncu < 1)
     return LF_ERR_DEVICE;
   *out = c.release();
@@ -1000,6 +1071,8 @@ int lf_dev_decompose_witness(lf_ctx *c, const lf_params *pr, const uint64_t *fc,
   if (N % pr->L) return fail(c, LF_ERR_INCORRECT_LENGTH, "N must be a multiple of L");
   Tables *t;
   LF_TRY(get_tables(c, pr->d, t));
+  if (n4k_ok(t, pr->d, lbs, pr->K) && N % pr->L == 0)
+    return decompose_n4k_sides(c, t, 1, &fc, &fck, &fk, &wk, N, lb, pr->L, pr->K);
   LF_HIP(c, lfk::decompose_witness(fc, N, pr->d, lb, pr->L, lbs, pr->K, fck, fk, wk, t->fwd, c->d_err, c->cur));
   return LF_OK;
 }

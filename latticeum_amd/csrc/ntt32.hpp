@@ -36,6 +36,16 @@ __host__ __device__ constexpr int brv5(int i) {
 __host__ __device__ constexpr int zexp(int k, bool inv) { return ((inv ? 153 : 39) * brv5(k)) % 192; }
 __host__ __device__ constexpr int wexp(int e, bool inv) { return ((inv ? 114 : 78) * e) % 192; }
 
+// issue 32 row loads before the first use: the asm consumes the values in
+// groups of 8, so the scheduler cannot interleave load -> wait -> use per value
+__device__ __forceinline__ void load_row32(const uint64_t *p, uint64_t *v) {
+#pragma unroll
+  for (int k = 0; k < 32; k++) v[k] = p[32 * k];
+#pragma unroll
+  for (int k = 0; k < 32; k += 8)
+    asm volatile("" : "+v"(v[k]), "+v"(v[k + 1]), "+v"(v[k + 2]), "+v"(v[k + 3]), "+v"(v[k + 4]), "+v"(v[k + 5]),
+                 "+v"(v[k + 6]), "+v"(v[k + 7]));
+}
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // forward merged CT network for X^32 + 1, levels [LV0, 5): natural in, bit-reversed out

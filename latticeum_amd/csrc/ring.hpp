@@ -177,6 +177,9 @@ struct NegaTables {
   const uint64_t *twist;      // fwd: psi^j ; inv: d^-1 psi^-j
   const uint64_t *roots;      // fwd: omega^e ; inv: omega^-e   (omega = psi^2), e < d
   const uint64_t *mid;        // d = 1024 only: 32 x 32 middle factors of the four-step NTT (ntt32.hpp)
+                              // (d = 4096: those of its 1024-point sub-transforms, kernels_n4k.hip)
+  const uint64_t *tw4 = nullptr;   // d = 4096: radix-4 twists [m0][a] (fwd psi^((2m0-3)a), inv 4^-1 psi^-((2m0-3)a))
+  const uint64_t *ztab = nullptr;  // d = 4096 fwd: butterflies of four balanced bits [m0][nibble | signs << 4]
 };
 
 // Radix-4 Stockham DFT of size D over LDS buffers x -> y (ping-pong), T threads.

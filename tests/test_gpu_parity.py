@@ -166,7 +166,7 @@ def test_decompose_witness(ctx, d, W):
         assert np.array_equal(g, w_)
 
 
-@pytest.mark.parametrize("d", [24, 1024])
+@pytest.mark.parametrize("d", [24, 1024, 4096])
 def test_decompose_overflow_is_an_error(ctx, d):
     pr = params(d)
     fc = np.zeros(pr.L * d, np.uint64)
@@ -177,7 +177,7 @@ def test_decompose_overflow_is_an_error(ctx, d):
     ctx.decompose_witness(np.zeros(pr.L * d, np.uint64), pr)  # flag was cleared
 
 
-@pytest.mark.parametrize("d", [24, 1024])
+@pytest.mark.parametrize("d", [24, 1024, 4096])
 def test_decompose_digit_boundary(ctx, d):
     """|v| = 2^K - 1 (either sign) takes exactly K binary digits; |v| = 2^K does
     not (balanced_decomposition/mod.rs:85-87 panics). Several elements, so the
