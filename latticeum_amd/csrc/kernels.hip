@@ -256,24 +256,32 @@ constexpr int DEC_SROW = 41;  // operand staging row (40 virtual slots + pad) of
 // row0 + k - 1 (ajtai_mfma.hip, vector-major, Lp = L column order): the block's
 // 48 groups are the 16-group units (G, l), G = 3 blockIdx.x + {0, 1, 2}, and each
 // (unit, virtual slot) piece is assembled from the plane's NTT values in LDS.
+// Every HBM access of the block is a run of whole 16-B pieces over contiguous
+// rows: f_coeff comes in and f_coeff_k / f_k go out through LDS (the element
+// rows [e][SROW] and a byte copy of the digits), not as one 192-B row per thread.
 __global__ void __launch_bounds__(256) k_decompose_phi72(const uint64_t *f_coeff, size_t N, int lb,
                                                         int L, int lbs, int K, uint64_t *f_coeff_k,
                                                         uint64_t *f_k, uint64_t *w_ccs_k, int *err,
-                                                        uint4 *frag, int nch, int row0) {
-  extern __shared__ uint64_t lds[];  // [DEC_GROUPS * L][25] (with frag: [..][DEC_SROW])
-  const int t = threadIdx.x;
+                                                        uint4 *frag, int nch, int row0, int srow) {
+  extern __shared__ uint64_t lds[];  // [DEC_GROUPS * L][srow] u64; a row's words 25..27 hold the digit bytes
+  const int t = threadIdx.x, ne = DEC_GROUPS * L;
+  int8_t *dgl = reinterpret_cast<int8_t *>(lds + 25);  // element e's digits at dgl[e * 8 srow + i]
   const size_t W = N / L;
-  const size_t j = (size_t)blockIdx.x * DEC_GROUPS * L + t;  // element index
-  const bool act = t < DEC_GROUPS * L && j < N;
+  const size_t j0 = (size_t)blockIdx.x * ne, j = j0 + t;  // element index
+  const int nv = (int)(N - j0 < (size_t)ne ? N - j0 : (size_t)ne);  // valid elements of the block
+  const bool act = t < nv;
+  // the block's f_coeff rows, 16 B per thread per step
+  for (int q = t; q < nv * 12; q += blockDim.x) {
+    const int e = q / 12, pr = q - 12 * e;
+    const ulonglong2 v = reinterpret_cast<const ulonglong2 *>(f_coeff + j0 * 24)[q];
+    lds[e * srow + 2 * pr] = v.x;
+    lds[e * srow + 2 * pr + 1] = v.y;
+  }
+  __syncthreads();
   int64_t cur[24];
   if (act) {
-    const ulonglong2 *src = reinterpret_cast<const ulonglong2 *>(f_coeff + j * 24);
 #pragma unroll
-    for (int i = 0; i < 12; i++) {
-      ulonglong2 v = src[i];
-      cur[2 * i] = signed_rep(v.x);
-      cur[2 * i + 1] = signed_rep(v.y);
-    }
+    for (int i = 0; i < 24; i++) cur[i] = signed_rep(lds[t * srow + i]);
   }
   // b = 2 (lbs = 1): the balanced digits are sign(v) bit_k(|v|) (bal_digit's
   // remainder is never rounded), so the planes are independent and
@@ -284,45 +292,60 @@ __global__ void __launch_bounds__(256) k_decompose_phi72(const uint64_t *f_coeff
   for (int k = k0; k < k1; k++) {
     uint64_t c[24];
     if (act) {
-      if (lbs == 1) {
 #pragma unroll
-        for (int i = 0; i < 24; i++) {
+      for (int i = 0; i < 24; i++) {
+        int64_t dg;
+        if (lbs == 1) {
           const int64_t m = cur[i] < 0 ? -cur[i] : cur[i], bit = (m >> k) & 1;
-          c[i] = from_signed(cur[i] < 0 ? -bit : bit);
+          dg = cur[i] < 0 ? -bit : bit;
+        } else {
+          dg = bal_digit(cur[i], lbs);
         }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 24; i++) c[i] = from_signed(bal_digit(cur[i], lbs));
+        c[i] = from_signed(dg);
+        // |digit| <= b/2 fits a byte for b_small <= 2^8; larger b_small keeps the u64 path below
+        if (lbs <= 8) dgl[t * 8 * srow + i] = (int8_t)dg;
       }
-      ulonglong2 *dc = reinterpret_cast<ulonglong2 *>(f_coeff_k + ((size_t)k * N + j) * 24);
+      if (lbs > 8) {
+        ulonglong2 *dc = reinterpret_cast<ulonglong2 *>(f_coeff_k + ((size_t)k * N + j) * 24);
 #pragma unroll
-      for (int i = 0; i < 12; i++) dc[i] = make_ulonglong2(c[2 * i], c[2 * i + 1]);
+        for (int i = 0; i < 12; i++) dc[i] = make_ulonglong2(c[2 * i], c[2 * i + 1]);
+      }
       ring::phi72_crt(c);
-      ulonglong2 *df = reinterpret_cast<ulonglong2 *>(f_k + ((size_t)k * N + j) * 24);
+    }
+    __syncthreads();  // the f_coeff rows (first plane) or the previous plane's rows are consumed
+    if (act) {
 #pragma unroll
-      for (int i = 0; i < 12; i++) df[i] = make_ulonglong2(c[2 * i], c[2 * i + 1]);
-#pragma unroll
-      for (int i = 0; i < 24; i++) lds[t * 25 + i] = c[i];
+      for (int i = 0; i < 24; i++) lds[t * srow + i] = c[i];
     }
     __syncthreads();
-    // recompose: one thread per (group, coefficient)
+    // f_coeff_k and f_k rows of the block, and the recompose: one thread per (group, coefficient)
+    {
+      uint64_t *fck = f_coeff_k + ((size_t)k * N + j0) * 24, *fk = f_k + ((size_t)k * N + j0) * 24;
+      for (int q = t; q < nv * 12; q += blockDim.x) {
+        const int e = q / 12, pr = q - 12 * e;
+        if (lbs <= 8)
+          reinterpret_cast<ulonglong2 *>(fck)[q] =
+              make_ulonglong2(from_signed(dgl[e * 8 * srow + 2 * pr]), from_signed(dgl[e * 8 * srow + 2 * pr + 1]));
+        reinterpret_cast<ulonglong2 *>(fk)[q] = make_ulonglong2(lds[e * srow + 2 * pr], lds[e * srow + 2 * pr + 1]);
+      }
+    }
     for (int u = t; u < DEC_GROUPS * 24; u += blockDim.x) {
       const int g = u / 24, i = u % 24;
       const size_t wj = (size_t)blockIdx.x * DEC_GROUPS + g;
       if (wj < W) {
-        uint64_t a = lds[(g * L + L - 1) * 25 + i];
-        for (int l = L - 2; l >= 0; l--) a = gl::add(gl::mul_pow2(a, lb), lds[(g * L + l) * 25 + i]);
+        uint64_t a = lds[(g * L + L - 1) * srow + i];
+        for (int l = L - 2; l >= 0; l--) a = gl::add(gl::mul_pow2(a, lb), lds[(g * L + l) * srow + i]);
         w_ccs_k[((size_t)k * W + wj) * 24 + i] = a;
       }
     }
     if (frag && k > 0) {
       // each element's 40 virtual slots (Toom-3 evaluations, ring::phi72_eval) as
-      // D8 words into LDS rows of DEC_SROW, then one thread per (unit, virtual
+      // D8 words into LDS rows of srow, then one thread per (unit, virtual
       // slot) gathers the unit's 16 columns into the 8 operand pieces
-      __syncthreads();  // the recompose reads of lds are done
+      __syncthreads();  // the copy-out and recompose reads of lds are done
       if (act) {
 #pragma unroll
-        for (int vs = 0; vs < 40; vs++) lds[t * DEC_SROW + vs] = d8(ring::phi72_eval(c, vs));
+        for (int vs = 0; vs < 40; vs++) lds[t * srow + vs] = d8(ring::phi72_eval(c, vs));
       }
       __syncthreads();
       for (int tk = t; tk < DEC_GROUPS / 16 * L * 40; tk += blockDim.x) {
@@ -333,7 +356,7 @@ __global__ void __launch_bounds__(256) k_decompose_phi72(const uint64_t *f_coeff
 #pragma unroll
         for (int jj = 0; jj < 16; jj++) {
           const int g = gh * 16 + jj;
-          x[jj] = (size_t)blockIdx.x * DEC_GROUPS + g < W ? lds[(g * L + l) * DEC_SROW + vs] : 0;
+          x[jj] = (size_t)blockIdx.x * DEC_GROUPS + g < W ? lds[(g * L + l) * srow + vs] : 0;
         }
         uint4 pu[8];
         d8_transpose16(x, pu);
@@ -342,7 +365,7 @@ __global__ void __launch_bounds__(256) k_decompose_phi72(const uint64_t *f_coeff
         for (int b = 0; b < 8; b++) out[4 * b] = pu[b];
       }
     }
-    __syncthreads();
+    if (k + 1 < k1) __syncthreads();  // this plane's reads of the digit bytes and rows are done
   }
   if (act && blockIdx.y == 0) {
     bool bad = false;
@@ -1001,17 +1024,18 @@ hipError_t decompose_witness(const uint64_t *f_coeff, size_t N, int d, int lb, i
     return decompose_n32(f_coeff, N, lb, L, K, f_coeff_k, f_k, w_ccs_k, fwd, err, st);
   if (d == 24) {
     if (DEC_GROUPS * L > 256) return hipErrorInvalidValue;
-    size_t lds = (size_t)DEC_GROUPS * L * 25 * sizeof(uint64_t);
     if (frag && (L > 5 || row0 < 0 || row0 + K - 1 > 32)) return hipErrorInvalidValue;
-    if (frag) lds = (size_t)DEC_GROUPS * L * DEC_SROW * sizeof(uint64_t);
+    const int srow = frag ? DEC_SROW : 28;
+    const size_t lds = (size_t)DEC_GROUPS * L * srow * sizeof(uint64_t);
     // with independent planes (b = 2), split them over blockIdx.y until about
-    // 1024 blocks run: the real zkvm shape (W = 19 763) has only 412 element blocks
+    // 1024 blocks run: the real zkvm shape (W = 19 763) has only 412 element
+    // blocks (one plane per block is no faster there: 0.30 against 0.29 ms)
     const unsigned nb = blocks(W, DEC_GROUPS);
     unsigned ys = lbs == 1 ? (1024 + nb - 1) / nb : 1;
     if (ys > (unsigned)K) ys = K;
     if (ys < 1) ys = 1;
     hipLaunchKernelGGL(k_decompose_phi72, dim3(nb, ys), dim3(256), lds, st, f_coeff, N, lb, L, lbs, K,
-                       f_coeff_k, f_k, w_ccs_k, err, frag, nch, row0);
+                       f_coeff_k, f_k, w_ccs_k, err, frag, nch, row0, srow);
     return hipGetLastError();
   }
   if (L > 8) return hipErrorInvalidValue;
