@@ -3,8 +3,8 @@
 TAG=${1:?tag}; R=${2:-r01}
 cd "$(dirname "$0")/.." || exit 1
 cp gpurun_out/pmc_traffic_$TAG.json profiles/pmc_traffic.json
-grep "^{" gpurun_out/bench_$TAG.log | tail -1 > profiles/${R}_bench.json
-for name in d1024_W16384 d1024_W464 d24_W19763; do
+grep "^{" gpurun_out/bench_${BENCH_TAG:-$TAG}.log | tail -1 > profiles/${R}_bench.json
+for name in d1024_W16384 d1024_W464 d24_W19763 d4096_W1024; do
   cp gpurun_out/stats_${TAG}_$name.md profiles/${R}_rocprof_stats_$name.md
   grep "^{" gpurun_out/benchprof_${TAG}_$name.log | tail -1 > profiles/${R}_benchprof_$name.json
 done

@@ -8,8 +8,10 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 TAG=${1:-evidence}
 mkdir -p gpurun_out
+if [ -z "$SKIP_TESTS" ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
+fi
 ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-small-shape"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_$TAG -o run --output-format csv -- \
   python bench.py $ARGS > gpurun_out/pmc_fetch_$TAG.log 2>&1
@@ -19,9 +21,12 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$TAG -o run
 rc=$?; echo "write rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python tools/prof_summary.py traffic gpurun_out/pmc_fetch_$TAG gpurun_out/pmc_write_$TAG \
   gpurun_out/pmc_traffic_$TAG.json 1024 16384 32 > /dev/null && cp gpurun_out/pmc_traffic_$TAG.json profiles/pmc_traffic.json
+if [ -z "$SKIP_BENCH" ]; then
 timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -c 300 gpurun_out/bench_$TAG.log; [ $rc -eq 0 ] || exit $rc
-for cfg in "d1024_W16384:" "d1024_W464:--w 464 --steps 64 --warmup 8" "d24_W19763:--d 24 --w 19763 --steps 32 --warmup 4"; do
+fi
+for cfg in "d1024_W16384:" "d1024_W464:--w 464 --steps 64 --warmup 8" "d24_W19763:--d 24 --w 19763 --steps 32 --warmup 4" \
+           "d4096_W1024:--d 4096 --w 1024 --kappa 64 --steps 10 --warmup 2"; do
   name=${cfg%%:*}; args=${cfg#*:}
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_$name -o run --output-format csv -- \
     python bench.py --no-cpu-baseline --no-small-shape $args > gpurun_out/benchprof_${TAG}_$name.log 2>&1
