@@ -326,6 +326,11 @@ typedef struct {
   const int *S_idx;
 } lf_comb;
 int lf_dev_eq_table(lf_ctx *ctx, int d, const uint64_t *r, int nv, uint64_t *out);
+/* Witness::get_fhat (latticefold/src/arith.rs:273-297): the f_hat MLEs of a
+ * witness from its f_coeff [N][d] (N <= 2^nv): out [tau][2^nv][d], tau = 3 for
+ * Phi_72 (slot s of MLE j is (f_coeff[i][8 j + s], 0, 0)), 1 for X^d + 1; the
+ * points past N are zero (the reference truncates them; the MLE reads zero). */
+int lf_dev_get_fhat(lf_ctx *ctx, int d, const uint64_t *f_coeff, size_t N, int nv, uint64_t *out);
 /* out[m][b] = in[m][2b] + r (in[m][2b + 1] - in[m][2b]) for b < 2^(nv-1); r: base-ring words (host) */
 int lf_dev_mle_fix_first(lf_ctx *ctx, int d, const uint64_t *in, size_t in_stride, int nm, int nv,
                          const uint64_t *r_base, uint64_t *out, size_t out_stride);

@@ -260,6 +260,10 @@ class Context:
     def dev_eq_table(self, d: int, r, nv: int, out):
         self.check(self.lib.lf_dev_eq_table(self.h, d, _dptr(r), nv, _dptr(out)))
 
+    def dev_get_fhat(self, d, f_coeff, N, nv, out):
+        """Witness::get_fhat on the device: out [tau][2^nv][d] from f_coeff [N][d]"""
+        self.check(self.lib.lf_dev_get_fhat(self.h, d, _dptr(f_coeff), N, nv, _dptr(out)))
+
     def dev_mle_evaluate(self, d: int, mles, nm: int, nv: int, point, out):
         self.check(self.lib.lf_dev_mle_evaluate(self.h, d, _dptr(mles), nm, nv, _dptr(point), _dptr(out)))
 

@@ -122,6 +122,7 @@ SIGNATURES = {
     "lf_lcccs_deserialize": (I, [VP, SZ, I, I, VP, SZ, C.POINTER(LfLcccs)]),
     "lf_lfproof_serialize": (I, [C.POINTER(LfLfproof), I, VP, SZ, C.POINTER(SZ)]),
     "lf_dev_eq_table": (I, [VP, I, VP, I, VP]),
+    "lf_dev_get_fhat": (I, [VP, I, VP, SZ, I, VP]),
     "lf_ccs_create": (I, [VP, I, I, SZ, SZ, VP, VP, VP, I, C.POINTER(VP)]),
     "lf_ccs_destroy": (None, [VP]),
     "lf_dev_mz_mles": (I, [VP, VP, VP, I, I, VP]),

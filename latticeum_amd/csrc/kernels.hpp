@@ -134,6 +134,8 @@ struct CombS {
 };
 int slot_words(int d);  // words of one NTT slot: 3 (Fq3, Phi_72) or 1
 hipError_t eq_table(const uint64_t *r, int nv, int d, uint64_t *out, hipStream_t st);
+// Witness::get_fhat: tau = d / slots MLEs of 2^nv points from N <= 2^nv coefficient elements
+hipError_t get_fhat(const uint64_t *f_coeff, size_t N, int d, int nv, uint64_t *out, hipStream_t st);
 // out[m][b] = in[m][2b] + r (in[m][2b+1] - in[m][2b]), b < half; r_base: slot_words(d) words
 hipError_t mle_fix_first(const uint64_t *in, size_t in_stride, int nm, size_t half, int d, const uint64_t *r_base,
                          uint64_t *out, size_t out_stride, hipStream_t st);

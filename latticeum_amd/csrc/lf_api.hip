@@ -1234,6 +1234,15 @@ int lf_dev_eq_table(lf_ctx *c, int d, const uint64_t *r, int nv, uint64_t *out) 
   return LF_OK;
 }
 
+int lf_dev_get_fhat(lf_ctx *c, int d, const uint64_t *f_coeff, size_t N, int nv, uint64_t *out) {
+  if (!c || !out || (N && !f_coeff) || nv < 0 || nv > 40) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  if (N > ((size_t)1 << nv)) return fail(c, LF_ERR_INCORRECT_LENGTH, "N exceeds 2^nv");
+  LF_HIP(c, lfk::get_fhat(f_coeff, N, d, nv, out, c->cur));
+  return LF_OK;
+}
+
 int lf_dev_mle_fix_first(lf_ctx *c, int d, const uint64_t *in, size_t in_stride, int nm, int nv,
                          const uint64_t *r_base, uint64_t *out, size_t out_stride) {
   if (!c || !in || !out || !r_base || nm < 1 || nv < 1) return LF_ERR_INVALID_ARG;

@@ -433,4 +433,35 @@ hipError_t mle_dot(const uint64_t *mles, size_t stride, int nm, const uint64_t *
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- f_hat
+// Witness::get_fhat (LF/arith.rs:273-297): MLE j of a witness holds, at point
+// i < N, the NTT element whose slot s is coefficient j D + s of f_coeff[i] as a
+// base-ring value (Phi_72: (c, 0, 0) in an Fq3 slot, D = 8 slots; X^d + 1:
+// tau = 1, the coefficients themselves); points N .. 2^nv - 1 are zero (the
+// reference's truncated MLE read as zero padding). One thread per output word.
+__global__ void k_get_fhat(const uint64_t *f_coeff, size_t N, int d, size_t npts, uint64_t *out) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  const int tau = d == 24 ? 3 : 1;
+  if (t >= (size_t)tau * npts * d) return;
+  const size_t w = t % d, ji = t / d, i = ji % npts;
+  const int j = (int)(ji / npts);
+  uint64_t v = 0;
+  if (i < N) {
+    if (d == 24)
+      v = w % 3 == 0 ? f_coeff[i * 24 + 8 * j + w / 3] : 0;
+    else
+      v = f_coeff[i * d + w];
+  }
+  out[t] = v;
+}
+
+hipError_t get_fhat(const uint64_t *f_coeff, size_t N, int d, int nv, uint64_t *out, hipStream_t st) {
+  const size_t npts = (size_t)1 << nv;
+  if (N > npts) return hipErrorInvalidValue;
+  const size_t n = (size_t)(d == 24 ? 3 : 1) * npts * d;
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_get_fhat, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, f_coeff, N, d, npts, out);
+  return hipGetLastError();
+}
+
 }  // namespace lfk

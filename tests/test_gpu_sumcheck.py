@@ -149,3 +149,19 @@ def test_folding_sumcheck_real_shape(ctx):
     assert np.array_equal(expected, O.comb_eval(comb, host(vals), nm, d))
     del keep, m
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("d,N,nv", [(24, 13, 4), (24, 16, 4), (1024, 5, 3), (16, 1, 0)])
+def test_get_fhat_matches_oracle(ctx, d, N, nv):
+    """Witness::get_fhat (arith.rs:273-297): Phi_72 against the oracle's
+    restatement, X^d + 1 as the coefficients themselves; zero past N"""
+    fc = rand(N * d, 40 + d + N)
+    tau = 3 if d == 24 else 1
+    n = 1 << nv
+    out = dev(n=tau * n * d)
+    ctx.dev_get_fhat(d, dev(fc), N, nv, out)
+    ctx.sync()
+    got = host(out).reshape(tau, n, d)
+    want = O.get_fhat_phi72(fc).reshape(tau, N, d) if d == 24 else fc.reshape(1, N, d)
+    assert np.array_equal(got[:, :N], want)
+    assert not got[:, N:].any()
