@@ -107,7 +107,7 @@ def kernel_names(LA, d, W, layout):
     if d == 4096:
         return {"decompose": "k_decompose_n4k_fused" if layout == 1 else "k_decompose_n4k",
                 "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_nega",
-                "fold": "k_fold_nega", "from_w_ccs": "k_from_w_ccs_nega", "from_f": "k_from_f_nega",
+                "fold": "k_fold_nega", "from_w_ccs": "k_from_w_ccs_n4k", "from_f": "k_from_f_n4k",
                 "to_frag": "k_to_frag<true, false, true>"}
     return {"decompose": "k_decompose_nega", "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_nega",
             "fold": "k_fold_nega", "from_w_ccs": "k_from_w_ccs_nega", "from_f": "k_from_f_nega",

@@ -973,6 +973,7 @@ hipError_t from_w_ccs(const uint64_t *w_ccs, size_t W, int d, int lb, int L, uin
                       hipStream_t st) {
   if (W == 0) return hipSuccess;
   if (d == 1024 && fwd.mid && inv.mid) return from_w_ccs_n32(w_ccs, W, lb, L, f_coeff, f, fwd, inv, err, st);
+  if (d == 4096 && fwd.tw4 && inv.tw4) return from_w_ccs_n4k(w_ccs, W, lb, L, f_coeff, f, fwd, inv, err, st);
   if (d == 24) {
     hipLaunchKernelGGL(k_from_w_ccs_phi72, dim3(blocks(W * L, 128)), dim3(128), 0, st, w_ccs, W, lb,
                        L, f_coeff, f, err);
@@ -995,6 +996,7 @@ hipError_t from_f(const uint64_t *f, size_t N, int d, int lb, int L, uint64_t *f
   const size_t W = N / L;
   if (W == 0) return hipSuccess;
   if (d == 1024 && inv.mid) return from_f_n32(f, W, lb, L, f_coeff, w_ccs, inv, st);
+  if (d == 4096 && inv.tw4) return from_f_n4k(f, W, lb, L, f_coeff, w_ccs, inv, st);
   if (d == 24) {
     if (L < 1 || L > 256) return hipErrorInvalidValue;
     const int G = 256 / L;

@@ -124,6 +124,12 @@ hipError_t decompose_n4k(const FusedSides &sd, size_t N, int lb, int L, int K, u
                          const ring::NegaTables &fwd, int *err, uint64_t *sink, int ncu, hipStream_t st,
                          uint4 *frag = nullptr, int nch = 0);
 
+// d = 4096 Witness::from_f / from_w_ccs on the quarter transforms (kernels_n4k.hip)
+hipError_t from_f_n4k(const uint64_t *f, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *w_ccs,
+                      const ring::NegaTables &inv, hipStream_t st);
+hipError_t from_w_ccs_n4k(const uint64_t *w_ccs, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *f,
+                          const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err, hipStream_t st);
+
 // ---------------------------------------------------------------- sumcheck (sumcheck.hip)
 // the multisets S_i of a CCS (linearization polynomial), by value as a kernel argument
 constexpr int LF_MAX_MULTISETS = 64, LF_MAX_S = 512;

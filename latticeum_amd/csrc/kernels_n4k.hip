@@ -295,6 +295,222 @@ __global__ void __launch_bounds__(512, 1) k_decompose_n4k_fused(const uint32_t *
   }
 }
 
+// ---------------------------------------------------------------- Witness::from_f / from_w_ccs, d = 4096
+// The inverse: x[a + 1024 b] = 1/4 sum_m0 w8^(-b (2 m0 + 1)) psi^(-(2 m0 - 3) a) INTT1024(X[m0 + 4 .])[a]
+// (tools/ntt4096_model.py). A block of 8 waves holds four elements at a time,
+// each on the four half-waves of two waves (one per quarter m0); after its
+// quarter's INTT and twist (4^-1 folded into the table) a half-wave leaves
+// z_m0 in LDS over its two waves' transpose tiles (E, 4 x 1024 words), and
+// half-wave q then combines a in [256 q, 256 q + 256) for all four b:
+// sum_m0 w8^(-b (2 m0 + 1)) z_m0 = w8^-b DFT4_{w4^-1}(z)_b, w4 = w8^2 = 2^48, all shifts.
+// The forward direction of from_w_ccs runs the same exchange backwards.
+namespace {
+constexpr int FW_WAVES = 8;
+// a quarter's slots in the transform's input order: v[m2] = p[128 m2] (all loads issued first)
+__device__ __forceinline__ void load_quarter(const uint64_t *p, uint64_t *v) {
+#pragma unroll
+  for (int k = 0; k < 32; k++) v[k] = p[128 * k];
+#pragma unroll
+  for (int k = 0; k < 32; k += 8)
+    asm volatile("" : "+v"(v[k]), "+v"(v[k + 1]), "+v"(v[k + 2]), "+v"(v[k + 3]), "+v"(v[k + 4]), "+v"(v[k + 5]),
+                 "+v"(v[k + 6]), "+v"(v[k + 7]));
+}
+__device__ __forceinline__ void dft4_inv(uint64_t z0, uint64_t z1, uint64_t z2, uint64_t z3, uint64_t *x) {
+  // X_b = sum_m z_m w^(bm), w = w4^-1 = 2^144 = -2^48; then x_b = w8^-b X_b (w8^-1 = 2^72)
+  const uint64_t t0 = gl::add(z0, z2), t1 = gl::sub(z0, z2), t2 = gl::add(z1, z3);
+  const uint64_t t3 = gl::shl96(gl::sub(z3, z1), 48);  // (z1 - z3) 2^144
+  x[0] = gl::add(t0, t2);
+  x[1] = gl::shl96(gl::add(t1, t3), 72);
+  x[2] = gl::shl96(gl::sub(t2, t0), 48);  // (t0 - t2) 2^144
+  x[3] = gl::shl96(gl::sub(t1, t3), 24);  // w8^-3 = 2^-360 = 2^24
+}
+__device__ __forceinline__ void dft4_fwd(uint64_t d0, uint64_t d1, uint64_t d2, uint64_t d3, uint64_t *z) {
+  // z_m = sum_b d_b w8^(b (2m + 1)) = sum_b (w8^b d_b) w4^(bm), w8 = 2^120 = -2^24, w4 = 2^48
+  const uint64_t e1 = gl::neg(gl::shl96(d1, 24)), e2 = gl::shl96(d2, 48), e3 = gl::shl96(d3, 72);  // 2^240 = 2^48, 2^360 = 2^168 = -2^72
+  const uint64_t f3 = gl::neg(e3);
+  const uint64_t t0 = gl::add(d0, e2), t1 = gl::sub(d0, e2), t2 = gl::add(e1, f3);
+  const uint64_t t3 = gl::shl96(gl::sub(e1, f3), 48);  // (e1 - f3) w4
+  z[0] = gl::add(t0, t2);
+  z[1] = gl::add(t1, t3);
+  z[2] = gl::sub(t0, t2);
+  z[3] = gl::sub(t1, t3);
+}
+}  // namespace
+
+// LF/arith.rs:299-313: f_coeff = ICRT(f), w_ccs = recompose(f) in slot form (Horner over the limbs)
+__global__ void __launch_bounds__(512, 1) k_from_f_n4k(const uint64_t *f, size_t W, int lb, int L, uint64_t *f_coeff,
+                                                      uint64_t *w_ccs, const uint64_t *mid_ig, const uint64_t *twi) {
+  __shared__ uint64_t lds_all[FW_WAVES * n32::WAVE_U64];
+  __shared__ uint64_t mid_i[n32::MID_U64];
+  n32::stage_mid(mid_i, mid_ig);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5, G = wib >> 1, q = 2 * (wib & 1) + h;
+  uint64_t *T = lds_all + wib * n32::WAVE_U64 + h * n32::HALF_U64;
+  uint64_t *E = lds_all + 2 * G * n32::WAVE_U64;
+  const uint64_t b_pow = gl::mul_pow2(1, lb);
+  const uint64_t *tw = twi + q * Q4 + r;
+  for (size_t g0 = (size_t)blockIdx.x * 4; g0 < W; g0 += (size_t)gridDim.x * 4) {
+    const size_t g = g0 + G;
+    const bool ok = g < W;
+    const size_t gg = ok ? g : 0;
+    uint64_t acc[32];
+    for (int l = L - 1; l >= 0; l--) {
+      const size_t e = gg * L + l;
+      uint64_t v[32];
+      load_quarter(f + e * D4 + q + 4 * r, v);  // v[m2] = X[q + 4 (r + 32 m2)]
+      horner_step(acc, v, l == L - 1, lb, b_pow);
+      n32::inverse(v, mid_i, T, r);
+#pragma unroll
+      for (int k0 = 0; k0 < 32; k0 += 8) {
+        uint64_t t8[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) t8[k] = tw[32 * (k0 + k)];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k0 + k] = gl::mul(v[k0 + k], t8[k]);
+      }
+      __syncthreads();  // the group's transposes are done: E may overwrite its tiles
+#pragma unroll
+      for (int k = 0; k < 32; k++) E[q * Q4 + r + 32 * k] = v[k];
+      __syncthreads();
+      uint64_t *oc = f_coeff + e * D4 + 256 * q + r;
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const int a = 256 * q + r + 32 * i;
+        uint64_t x[4];
+        dft4_inv(E[a], E[Q4 + a], E[2 * Q4 + a], E[3 * Q4 + a], x);
+        if (ok)
+#pragma unroll
+          for (int b = 0; b < 4; b++) oc[32 * i + b * Q4] = x[b];
+      }
+      __syncthreads();  // E read before the next transposes
+    }
+    if (ok) {
+      uint64_t *ow = w_ccs + g * D4 + q + 4 * r;
+#pragma unroll
+      for (int k = 0; k < 32; k++) ow[128 * k] = gl::canon(acc[k]);
+    }
+  }
+}
+
+// LF/arith.rs:230-248: ICRT -> gadget_decompose(B = 2^lb, L) -> CRT, one element per four half-waves
+__global__ void __launch_bounds__(512, 1) k_from_w_ccs_n4k(const uint64_t *w_ccs, size_t W, int lb, int L,
+                                                          uint64_t *f_coeff, uint64_t *f, const uint64_t *mid_fg,
+                                                          const uint64_t *mid_ig, const uint64_t *twf,
+                                                          const uint64_t *twi, int *err) {
+  __shared__ uint64_t lds_all[FW_WAVES * n32::WAVE_U64];
+  __shared__ uint64_t mid_f[n32::MID_U64];
+  n32::stage_mid(mid_f, mid_fg);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5, G = wib >> 1, q = 2 * (wib & 1) + h;
+  uint64_t *T = lds_all + wib * n32::WAVE_U64 + h * n32::HALF_U64;
+  uint64_t *E = lds_all + 2 * G * n32::WAVE_U64;
+  for (size_t j0 = (size_t)blockIdx.x * 4; j0 < W; j0 += (size_t)gridDim.x * 4) {
+    const size_t j = j0 + G;
+    const bool ok = j < W;
+    const size_t jj = ok ? j : 0;
+    int64_t cur[32];  // coefficient a + 1024 b, a = 256 q + r + 32 i, at cur[4 i + b]
+    {
+      uint64_t v[32];
+      load_quarter(w_ccs + jj * D4 + q + 4 * r, v);
+      // the inverse middle factors from global (an L1-resident 8 KiB table), as k_from_w_ccs_n32 does
+      n32::cyc_dif32<true>(v);
+#pragma unroll
+      for (int i0 = 0; i0 < 32; i0 += 8) {
+        uint64_t t8[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) t8[i] = mid_ig[r * 32 + i0 + i];
+#pragma unroll
+        for (int i = 0; i < 8; i++) v[i0 + i] = gl::mul(v[i0 + i], t8[i]);
+      }
+      n32::transpose_inv(v, T, r);
+      n32::neg_gs32_inv(v);
+#pragma unroll
+      for (int k0 = 0; k0 < 32; k0 += 8) {
+        uint64_t t8[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) t8[k] = twi[q * Q4 + r + 32 * (k0 + k)];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k0 + k] = gl::mul(v[k0 + k], t8[k]);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 32; k++) E[q * Q4 + r + 32 * k] = v[k];
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const int a = 256 * q + r + 32 * i;
+        uint64_t x[4];
+        dft4_inv(E[a], E[Q4 + a], E[2 * Q4 + a], E[3 * Q4 + a], x);
+#pragma unroll
+        for (int b = 0; b < 4; b++) cur[4 * i + b] = signed_rep(x[b]);
+      }
+      __syncthreads();
+    }
+    for (int l = 0; l < L; l++) {
+      const size_t e = jj * L + l;
+      uint64_t *oc = f_coeff + e * D4 + 256 * q + r;
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        uint64_t dg[4], z[4];
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          dg[b] = from_signed(bal_digit(cur[4 * i + b], lb));
+          if (ok) oc[32 * i + b * Q4] = dg[b];
+        }
+        dft4_fwd(dg[0], dg[1], dg[2], dg[3], z);
+        const int a = 256 * q + r + 32 * i;
+#pragma unroll
+        for (int m = 0; m < 4; m++) E[m * Q4 + a] = z[m];
+      }
+      __syncthreads();
+      uint64_t v[32];
+#pragma unroll
+      for (int k0 = 0; k0 < 32; k0 += 8) {
+        uint64_t t8[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) t8[k] = twf[q * Q4 + r + 32 * (k0 + k)];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k0 + k] = gl::mul(E[q * Q4 + r + 32 * (k0 + k)], t8[k]);
+      }
+      __syncthreads();  // E read before the transposes overwrite it
+      n32::forward(v, mid_f, T, r);
+      if (ok) {
+        uint64_t *of = f + e * D4 + q + 4 * r;
+#pragma unroll
+        for (int i = 0; i < 32; i++) of[128 * n32::brv5(i)] = v[i];
+      }
+      __syncthreads();  // transposes done before the next limb's E writes
+    }
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < 32; k++) bad |= cur[k] != 0;
+    if (ok && bad) raise(err, 1);
+  }
+}
+
+// grids: one block per 4 elements, capped (the kernels loop)
+constexpr size_t FW_GRID_CAP = 4096;
+hipError_t from_f_n4k(const uint64_t *f, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *w_ccs,
+                      const ring::NegaTables &inv, hipStream_t st) {
+  if (!inv.mid || !inv.tw4) return hipErrorInvalidValue;
+  if (!W) return hipSuccess;
+  const size_t nb = (W + 3) / 4;
+  hipLaunchKernelGGL(k_from_f_n4k, dim3((unsigned)(nb < FW_GRID_CAP ? nb : FW_GRID_CAP)), dim3(512), 0, st,
+                     f, W, lb, L, f_coeff, w_ccs, inv.mid, inv.tw4);
+  return hipGetLastError();
+}
+hipError_t from_w_ccs_n4k(const uint64_t *w_ccs, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *f,
+                          const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err, hipStream_t st) {
+  if (!fwd.mid || !fwd.tw4 || !inv.mid || !inv.tw4) return hipErrorInvalidValue;
+  if (!W) return hipSuccess;
+  const size_t nb = (W + 3) / 4;
+  hipLaunchKernelGGL(k_from_w_ccs_n4k, dim3((unsigned)(nb < FW_GRID_CAP ? nb : FW_GRID_CAP)), dim3(512), 0,
+                     st, w_ccs, W, lb, L, f_coeff, f, fwd.mid, inv.mid, fwd.tw4, inv.tw4, err);
+  return hipGetLastError();
+}
+
 hipError_t decompose_n4k(const FusedSides &sd, size_t N, int lb, int L, int K, uint64_t *sm4,
                          const ring::NegaTables &fwd, int *err, uint64_t *sink, int ncu, hipStream_t st, uint4 *frag,
                          int nch) {
