@@ -39,6 +39,9 @@
 // back to D's coefficients d0..d4 and reduces: c = (d0 + 2^40 d3, d1 + 2^40 d4, d2)
 // (goldilocks/mod.rs:34-54 Fq3 multiplication, summed over the columns as
 // matrix.rs:168-178 does).
+#include <cstdlib>
+#include <cstring>
+
 #include "frag.hpp"
 #include "kernels.hpp"
 
@@ -172,6 +175,38 @@ constexpr int AJ_CPS = 320;  // most chunks per split (i32 bound: < 512)
 typedef __attribute__((address_space(3))) void lds_void;
 __device__ __forceinline__ int fl_pi(int j, int i) { return i ^ (((j & 7) << 1) | ((i >> 5) & 1)); }
 
+// fold the weights: value = sum_t 2^(8t) acc_t  (mod p); D reg i of lane l is
+// row (i & 3) + 8 (i >> 2) + 4 (l >> 5), column (vector) l & 31
+// Exactly in int64 by quarters: S_j = sum_{t in 4j..4j+3} acc_t 2^(8(t-4j)),
+// |S_j| < 2^57; value = S0 + S1 2^32 + S2 2^64 + S3 2^96
+//                   == (S0 - S2 - S3) + (S1 + S2) 2^32   (2^64 == 2^32 - 1, 2^96 == -1)
+// so: the ring slot the wave's results belong to
+__device__ __forceinline__ void mfma_epilogue(const v16i *acc, int lane, int kt, int kappa, int nvec, int d, int so,
+                                              int js, int direct, const OutPtrs &dst, uint64_t *partial) {
+  const int v = lane & 31, h = lane >> 5;
+  auto fe = [](int64_t x) { return x < 0 ? (uint64_t)x + gl::P : (uint64_t)x; };  // |x| < 2^63 - p
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    int32_t x[15];
+#pragma unroll
+    for (int t = 0; t < 15; t++) x[t] = acc[t][i];
+    // one output's 15 words at a time (the flush must not pull all 240 into VGPRs)
+    asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
+                 "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]));
+    int64_t S[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < 15; t++) S[t >> 2] += (int64_t)x[t] << (8 * (t & 3));
+    const uint64_t r = gl::add(fe(S[0] - S[2] - S[3]), gl::mul_pow2(fe(S[1] + S[2]), 32));
+    const int row = 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * h;
+    if (v < nvec && row < kappa) {
+      if (direct)  // one column split: the result itself
+        dst.p[v][(size_t)row * d + so] = r;
+      else
+        partial[(((size_t)js * nvec + v) * kappa + row) * d + so] = r;
+    }
+  }
+}
+
 // CPOL: cache policy of the operand copies (2 = nt: streaming, for operands far
 // larger than the caches -- A and F are each read once per launch)
 // kappa > 32: A is stored as 32-row tiles (tile_u4 uint4 each), and one wave
@@ -272,34 +307,165 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const ui
       for (int ka = 0; ka < 8; ka++)
         acc[ka + kb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ka], b[kb], acc[ka + kb], 0, 0, 0);
   }
-  // fold the weights: value = sum_t 2^(8t) acc_t  (mod p); D reg i of lane l is
-  // row (i & 3) + 8 (i >> 2) + 4 (l >> 5), column (vector) l & 31
-  // Exactly in int64 by quarters: S_j = sum_{t in 4j..4j+3} acc_t 2^(8(t-4j)),
-  // |S_j| < 2^57; value = S0 + S1 2^32 + S2 2^64 + S3 2^96
-  //                   == (S0 - S2 - S3) + (S1 + S2) 2^32   (2^64 == 2^32 - 1, 2^96 == -1)
-  const int v = lane & 31, h = lane >> 5;
-  auto fe = [](int64_t x) { return x < 0 ? (uint64_t)x + gl::P : (uint64_t)x; };  // |x| < 2^63 - p
+  const int so = qd ? (s % qd) * 4 + s / qd : s;  // the ring slot of operand slot s
+  mfma_epilogue(acc, lane, kt, kappa, nvec, d, so, js, direct, dst, partial);
+}
+
+// ---------------------------------------------------------------- F straight from the vectors
+// X^d + 1 in plain slot order: the block's F tile (nvec vectors x 32 columns x
+// its 4 slots) is gathered from the vectors themselves -- 32 contiguous bytes
+// (4 slots) per (vector, column) -- converted to D8 and byte-transposed in
+// registers, and written to LDS in the layout the DMA path leaves there. So
+// the decomposition writes no operand rows and commit(z)'s f needs no
+// k_to_frag. A thread owns (vector pv, column quad jq): per slot it
+// transposes 4 columns x 8 digits (v_perm) into 8 words, one ds_write_b32 per
+// (slot, digit). The global loads of chunk c + 2 are in flight while chunk c
+// multiplies; the LDS writes of chunk c + 1 follow the barrier of chunk c.
+// The four blocks that read the same 128-B line of an element (16 slots) are
+// blocks bi + 8 t (one XCD under the round-robin placement), so the line is
+// fetched into that L2 once.
+template <int CPOL>
+__global__ void __launch_bounds__(256, 1) k_ajtai_mfma_fv(const uint4 *Af, VecPtrs fv, int d, int nch, int nvec,
+                                                         int kappa, uint64_t *partial, OutPtrs dst, int direct,
+                                                         int cps, int ktiles, int nbase, size_t tile_u4, int Lp,
+                                                         size_t Wp) {
+  __shared__ uint4 Al[2][4][8 * 64];  // 64 KiB: A copies one chunk ahead
+  __shared__ uint4 Fl[2][32 * 64];    // 64 KiB: F tiles (chunk c, chunk c + 1)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int grp = blockIdx.x / (8 * ktiles), rem = blockIdx.x - grp * 8 * ktiles;
+  const int kt = rem >> 3, bi = grp * 8 + (rem & 7);
+  if (bi >= nbase) return;  // uniform over the block
+  const int nq = d >> 2, js = bi / nq, bq = bi - js * nq;
+  const int quad = nq % 32 ? bq : (bq & ~31) + 4 * (bq & 7) + ((bq >> 3) & 3);
+  const int s = 4 * quad + w;
+  if (js >= (nch + cps - 1) / cps) return;  // uniform over the block
+  const int c0 = js * cps, c1 = min(nch, c0 + cps);
+  v16i acc[15];
 #pragma unroll
-  for (int i = 0; i < 16; i++) {
-    int32_t x[15];
+  for (int t = 0; t < 15; t++) acc[t] = (v16i){0};
+  const uint4 *pa = Af + kt * tile_u4 + ((size_t)s * nch * 8) * 64 + lane;
+  auto stage_a = [&](int c, int buf) {
 #pragma unroll
-    for (int t = 0; t < 15; t++) x[t] = acc[t][i];
-    // one output's 15 words at a time (the flush must not pull all 240 into VGPRs)
-    asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
-                 "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]));
-    int64_t S[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int t = 0; t < 15; t++) S[t >> 2] += (int64_t)x[t] << (8 * (t & 3));
-    const uint64_t r = gl::add(fe(S[0] - S[2] - S[3]), gl::mul_pow2(fe(S[1] + S[2]), 32));
-    const int row = 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * h;
-    const int so = qd ? (s % qd) * 4 + s / qd : s;  // the ring slot of operand slot s
-    if (v < nvec && row < kappa) {
-      if (direct)  // one column split: the result itself
-        dst.p[v][(size_t)row * d + so] = r;
-      else
-        partial[(((size_t)js * nvec + v) * kappa + row) * d + so] = r;
-    }
+    for (int k = 0; k < 8; k++)
+      __builtin_amdgcn_global_load_lds((const void *)(pa + ((size_t)c * 8 + k) * 64), (lds_void *)&Al[buf][w][k * 64],
+                                       16, 0, CPOL);
+  };
+  // producer role: vector pv, columns 4 jq .. 4 jq + 3 of the chunk (half ph, bytes pb .. pb + 3 of a piece)
+  const int pv = tid >> 3, jq = tid & 7, ph = jq >> 2, pb = 4 * (jq & 3);
+  // rows >= nvec only reach discarded outputs: they copy vector 0 (no divergent path)
+  const uint64_t *fvp = fv.p[pv < nvec ? pv : 0] + 4 * quad;
+  ulonglong2 fr[8];
+  // this thread's unit u = 2 c + ph = G Lp + l, advanced by 2 per chunk (no division in the loop)
+  int uG, ul;
+  {
+    const int u = 2 * c0 + ph;
+    uG = u / Lp;
+    ul = u - uG * Lp;
   }
+  auto load_f = [&]() {  // the next chunk's columns (the unit advances afterwards)
+    const size_t g0 = 16 * (size_t)uG + pb;  // groups g0 .. g0 + 3
+    const size_t col0 = g0 * Lp + ul;
+#pragma unroll
+    for (int cc = 0; cc < 4; cc++) {
+      // columns past the matrix meet zero columns of A: any valid row will do
+      const size_t col = g0 + cc < Wp ? col0 + (size_t)cc * Lp : 0;
+      const ulonglong2 *p = reinterpret_cast<const ulonglong2 *>(fvp + col * d);
+      fr[2 * cc] = p[0];
+      fr[2 * cc + 1] = p[1];
+    }
+    ul += 2;  // ul < Lp before, so at most two subtractions (Lp >= 1)
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      const bool wrap = ul >= Lp;
+      ul -= wrap ? Lp : 0;
+      uG += wrap ? 1 : 0;
+    }
+  };
+  // piece (pv, ph, k, sl) of the tile sits at LDS uint4 pv 64 + fl_pi(pv, 32 ph + 4 k + sl)
+  const uint32_t fl0 = (uint32_t)(uintptr_t)&Fl[0][0], fl1 = (uint32_t)(uintptr_t)&Fl[1][0];
+  auto store_f = [&](int buf) {
+    const uint32_t base = (buf ? fl1 : fl0) + (uint32_t)(pv * 64 * 16 + pb);
+#pragma unroll
+    for (int sl = 0; sl < 4; sl++) {
+      uint32_t lo[4], hi[4];
+#pragma unroll
+      for (int cc = 0; cc < 4; cc++) {
+        const uint64_t x = d8((sl & 1) ? fr[2 * cc + (sl >> 1)].y : fr[2 * cc + (sl >> 1)].x);
+        lo[cc] = (uint32_t)x;
+        hi[cc] = (uint32_t)(x >> 32);
+      }
+      uint32_t wk[8];  // digit k of the 4 columns, column cc in byte cc
+#pragma unroll
+      for (int half = 0; half < 2; half++) {
+        const uint32_t *q = half ? hi : lo;
+#pragma unroll
+        for (int bb = 0; bb < 4; bb += 2) {
+          const uint32_t sel = (uint32_t)bb | ((uint32_t)(4 + bb) << 8) | ((uint32_t)(bb + 1) << 16) |
+                               ((uint32_t)(5 + bb) << 24);
+          const uint32_t t01 = __builtin_amdgcn_perm(q[1], q[0], sel);
+          const uint32_t t23 = __builtin_amdgcn_perm(q[3], q[2], sel);
+          wk[4 * half + bb] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
+          wk[4 * half + bb + 1] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t addr = base + 16u * (uint32_t)fl_pi(pv, 32 * ph + 4 * k + sl);
+        asm volatile("ds_write_b32 %0, %1" ::"v"(addr), "v"(wk[k]) : "memory");
+      }
+    }
+  };
+  // this lane's F operand positions: piece (rh, k, s_lo = w) sits in KiB j = rh >> 1
+  const int rh = 2 * (lane & 31) + (lane >> 5), fj = rh >> 1;
+  int fpos[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) fpos[k] = fj * 64 + fl_pi(fj, (rh & 1) * 32 + k * 4 + w);
+  stage_a(c0, 0);
+  load_f();
+  store_f(0);
+  asm volatile("" ::: "memory");
+  load_f();
+  // every iteration runs the same copies (the last two re-copy chunk c1 - 1 /
+  // load columns past the split: harmless), so the compiler's wait analysis
+  // sees one path and waits only for what each use needs
+  for (int c = c0; c < c1; c++) {
+    const int cur = (c - c0) & 1;
+    // A(c) landed (the 8 F loads of chunk c + 1 issued after it stay in
+    // flight), this thread's F writes of chunk c done; then the barrier
+    asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    v4i a[8], b[8];
+    const uint32_t abase = (uint32_t)(uintptr_t)&Al[cur][w][lane];
+    const uint32_t fbase = cur ? fl1 : fl0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(a[k]) : "v"(abase), "i"(k * 1024));
+      asm volatile("ds_read_b128 %0, %1" : "=v"(b[k]) : "v"(fbase + 16u * fpos[k]));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // the F values may not be touched above this point (the compiler would
+    // otherwise convert them early and wait for every copy in flight)
+#pragma unroll
+    for (int i = 0; i < 8; i += 2)
+      asm volatile("" : "+v"(fr[i].x), "+v"(fr[i].y), "+v"(fr[i + 1].x), "+v"(fr[i + 1].y));
+    // chunk c + 1's F values (loaded an iteration ago: the only vector-memory
+    // operations outstanding here) into the buffer everyone is past reading,
+    // then the copies of A(c + 1) and the loads of F(c + 2) behind the products
+    store_f(cur ^ 1);
+    stage_a(c + 1 < c1 ? c + 1 : c1 - 1, cur ^ 1);
+    // every A copy is issued before any F load: the vmcnt(8) at the loop head
+    // then means "A(c + 1) landed" wherever the compiler places the loads
+    asm volatile("" ::: "memory");
+    load_f();
+    asm volatile("" ::: "memory");  // all of them issued before the products
+#pragma unroll
+    for (int kb = 0; kb < 8; kb++)
+#pragma unroll
+      for (int ka = 0; ka < 8; ka++)
+        acc[ka + kb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ka], b[kb], acc[ka + kb], 0, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no copy into LDS outlives the block
+  mfma_epilogue(acc, lane, kt, kappa, nvec, d, s, js, direct, dst, partial);
 }
 
 // Phi_72 epilogue: virtual-slot sums [nvec][kappa][40] -> Fq3 slots [kappa][24] per vector
@@ -323,6 +489,15 @@ __global__ void k_phi72_interp(const uint64_t *virt, int nvec, size_t kappa, Out
 }
 
 // ---------------------------------------------------------------- launchers
+// the F-from-vectors contraction (k_ajtai_mfma_fv) applies to X^d + 1 in plain
+// slot order. It is opt-in (LATTICEUM_AMD_AJTAI_FV=1): at d = 1024, W = 2^14 it
+// saves the decomposition its operand rows (13.8 -> 12.2 ms) but its 32-byte
+// gathers from element-major f_k run at about 1.5 TB/s, so the contraction takes
+// 12.8 ms instead of 6.9
+bool mfma_from_vectors(const FragGeom &g, int d) {
+  const char *e = getenv("LATTICEUM_AMD_AJTAI_FV");
+  return e && strcmp(e, "1") == 0 && d != 24 && d % 16 == 0 && !g.qperm;
+}
 size_t frag_elems(const FragGeom &g, int d) { return (size_t)mfma_dim(d) * g.nch * 8 * 64; }  // uint4 per buffer
 int mfma_ktiles(size_t kappa) { return (int)((kappa + 31) / 32); }
 // chunks per column split: AJ_CPS for wide rings; for few virtual slots (Phi_72)
@@ -390,7 +565,9 @@ hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, c
     return hipErrorInvalidValue;
   OutPtrs out{};
   for (int v = 0; v < nvec; v++) out.p[v] = cm ? cm + (size_t)v * kappa * d : dst->p[v];
-  if (!f_ready) {
+  // X^d + 1 in plain slot order: the contraction gathers F from the vectors itself
+  const bool from_vectors = !f_ready && mfma_from_vectors(g, d);
+  if (!f_ready && !from_vectors) {
     hipError_t e = to_frag(fv, nvec, 0, g, d, true, Ff, st);
     if (e != hipSuccess) return e;
   }
@@ -408,7 +585,14 @@ hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, c
   const dim3 grid((unsigned)((nbase + 7) / 8 * 8 * ktiles));
   const size_t tile_u4 = frag_elems(g, d);
   // F is dv nch 8 KiB per launch (A is as large for kappa = 32)
-  if ((size_t)dv * g.nch * 8192 > STREAM_OUT_BYTES)
+  if (from_vectors) {
+    if ((size_t)dv * g.nch * 8192 > STREAM_OUT_BYTES)
+      hipLaunchKernelGGL(k_ajtai_mfma_fv<2>, grid, dim3(256), 0, st, Af, fv, dv, g.nch, nvec, (int)kappa, partial,
+                         kout, nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4, g.Lp, g.Wp);
+    else
+      hipLaunchKernelGGL(k_ajtai_mfma_fv<0>, grid, dim3(256), 0, st, Af, fv, dv, g.nch, nvec, (int)kappa, partial,
+                         kout, nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4, g.Lp, g.Wp);
+  } else if ((size_t)dv * g.nch * 8192 > STREAM_OUT_BYTES)
     hipLaunchKernelGGL(k_ajtai_mfma<2>, grid, dim3(256), 0, st, Af, Ff, dv, g.nch, nvec, (int)kappa, partial, kout,
                        nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4, g.qperm ? d / 4 : 0);
   else

@@ -297,7 +297,8 @@ int ajtai_launch(lf_ctx *c, const lf_ajtai *aj, const uint64_t *const *vecs, int
   lfk::VecPtrs vp{};
   for (int v = 0; v < nvec; v++) vp.p[v] = vecs[v];
   LF_TRY(reserve(c, partial_elems(aj, nvec)));
-  if (aj->Af) LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->geom, aj->d)));
+  if (aj->Af && !lfk::mfma_from_vectors(aj->geom, aj->d))
+    LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->geom, aj->d)));
   hipEvent_t a = nullptr, b = nullptr;
   if (c->timing) {
     LF_HIP(c, hipEventCreate(&a));
@@ -416,12 +417,14 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
   // fused path (d = 1024, b_small = 2, fragment order grouped by this L): the
   // decomposition writes its digit planes straight into the MFMA operand buffer
   const bool fused = aj->Af && aj->geom.Lp == L && d == 1024 && lbs == 1 && K <= 15 && t->fwd.mid;
+  // the contraction gathers the planes from f_k itself (k_ajtai_mfma_fv): no operand rows, no k_to_frag
+  const bool fv = aj->Af && lfk::mfma_from_vectors(aj->geom, d);
   // Phi_72 (d = 24): each side's decomposition writes its planes as operand rows (kernels.hip)
   const bool fused24 = aj->Af && aj->geom.Lp == L && d == 24 && L <= 5;
   // d = 4096 (kernels_n4k.hip): the same, with the quarter-major operand slots
   const bool fused4k = aj->Af && aj->geom.Lp == L && aj->geom.qperm && n4k_ok(t, d, lbs, K);
   if (fused || fused24 || fused4k) {
-    LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->geom, d)));
+    if (!fv) LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->geom, d)));
     if (fused4k) {
       const int row0[2] = {extra, extra + K - 1};
       PhaseTimer pt(c, LF_PHASE_DECOMPOSE);  // both sides in one launch
@@ -439,8 +442,8 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
         sd.row0[s] = extra + s * (K - 1);
       }
       PhaseTimer pt(c, LF_PHASE_DECOMPOSE);  // both sides in one launch
-      LF_HIP(c, lfk::decompose_fused(sd, N, lb, L, K, c->smg, t->fwd, c->frag, aj->geom.nch, c->d_err, c->sink,
-                                     c->ncu, c->cur));
+      LF_HIP(c, lfk::decompose_fused(sd, N, lb, L, K, c->smg, t->fwd, fv ? nullptr : c->frag, aj->geom.nch, c->d_err,
+                                     c->sink, c->ncu, c->cur));
     } else {
       for (int s = 0; s < 2; s++) {
         PhaseTimer pt(c, LF_PHASE_DECOMPOSE);
@@ -449,7 +452,11 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       }
     }
     lfk::VecPtrs vp{};
-    if (commit_f) {
+    if (fv) {
+      if (commit_f) vp.p[0] = commit_f;
+      for (int s = 0; s < 2; s++)
+        for (int k = 1; k < K; k++) vp.p[extra + s * (K - 1) + k - 1] = b->fk[s] + (size_t)k * N * d;
+    } else if (commit_f) {
       PhaseTimer pt(c, LF_PHASE_TO_FRAG);
       vp.p[0] = commit_f;
       LF_HIP(c, lfk::to_frag(vp, 1, 0, aj->geom, d, true, c->frag, c->cur));
@@ -460,7 +467,7 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       LF_HIP(c, hipEventCreate(&ea));
       LF_HIP(c, hipEventCreate(&eb));
     }
-    LF_HIP(c, lfk::ajtai_mfma(aj->Af, kappa, aj->geom, d, vp, nvec, true, c->frag, c->scratch, nullptr, c->cur, ea,
+    LF_HIP(c, lfk::ajtai_mfma(aj->Af, kappa, aj->geom, d, vp, nvec, !fv, c->frag, c->scratch, nullptr, c->cur, ea,
                               eb, &dst));
     if (c->timing) c->pending.push_back({ea, eb, nvec});
     return LF_OK;
@@ -694,7 +701,8 @@ int lf_ctx_reserve(lf_ctx *c, size_t kappa, size_t ncols, int d, int nvec) {
   if (use_mfma(d, kappa)) {
     probe.Af = reinterpret_cast<uint4 *>(1);  // sizing only
     probe.geom = ajtai_geom(ncols);
-    LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(probe.geom, d)));
+    probe.geom.qperm = d == 4096;
+    if (!lfk::mfma_from_vectors(probe.geom, d)) LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(probe.geom, d)));
   }
   LF_TRY(reserve(c, partial_elems(&probe, nvec)));
   return grow(c, c->ybuf, c->ybuf_elems, (size_t)nvec * kappa * d);

@@ -314,6 +314,13 @@ def test_dev_fold_step_matches_oracle(ctx, d, W, kappa):
     check_dev_fold_step(ctx, d, W, kappa)
 
 
+def test_dev_fold_step_gathering_contraction(ctx, monkeypatch):
+    """LATTICEUM_AMD_AJTAI_FV=1: the decomposition writes no operand rows and the
+    contraction gathers the planes from f_k (k_ajtai_mfma_fv)"""
+    monkeypatch.setenv("LATTICEUM_AMD_AJTAI_FV", "1")
+    check_dev_fold_step(ctx, 1024, 37, 2)
+
+
 def test_dev_fold_step_repeated_in_place(ctx):
     # consecutive steps reuse every buffer (as bench.py and the proving loop do):
     # the fused fold must see each step's own f_k rows, never the previous step's
@@ -422,7 +429,7 @@ def test_limb_transport_roundtrip(ctx):
     assert [int(v) for v in out.cpu().numpy().view(np.uint64)] == [int(v) for v in want]
 
 
-@pytest.mark.parametrize("layout", ["mfma", "valu"])
+@pytest.mark.parametrize("layout", ["mfma", "valu", "fv"])
 @pytest.mark.parametrize("d,kappa,ncols,nvec", [(16, 3, 40, 5), (64, 32, 70, 29), (1024, 7, 33, 1),
                                                 (1024, 32, 96, 29), (256, 17, 64, 32), (24, 3, 40, 5),
                                                 (24, 32, 700, 29), (24, 9, 33, 1),
@@ -434,11 +441,13 @@ def test_ajtai_layouts(ctx, monkeypatch, layout, d, kappa, ncols, nvec):
     import torch
     if layout == "valu":
         monkeypatch.setenv("LATTICEUM_AMD_AJTAI", "valu")
+    if layout == "fv":  # the opt-in contraction that gathers F from the vectors itself
+        monkeypatch.setenv("LATTICEUM_AMD_AJTAI_FV", "1")
     A = rand(kappa * ncols * d, 21 + d + kappa).reshape(kappa, ncols, d)
     # edge values in A: 0, p-1 and the D8 digit boundaries
     A.reshape(-1)[:6] = [0, P - 1, 0x7F7F7F7F7F7F7F7F, 0x7F7F7F7F7F7F7F80, (P - 1) // 2, 1]
     sch = LA.AjtaiCommitmentScheme(ctx, A)
-    assert sch.layout == (1 if layout == "mfma" else 0)
+    assert sch.layout == (0 if layout == "valu" else 1)
     F = rand(nvec * ncols * d, 31 + d)
     F[:4] = [P - 1, 0x7F7F7F7F7F7F7F7F, 0x7F7F7F7F7F7F7F80, 0]
     Ft = torch.from_numpy(F.view(np.int64)).cuda()
