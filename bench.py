@@ -75,10 +75,10 @@ def algorithmic_bytes(d, W, kappa, L=5, K=15):
     nvec = 2 * (K - 1) + 1  # commit(z)'s A.f rides in the decomposition-commitment pass
     F = 8 * (40 if d == 24 else d)
     fused = d in (24, 1024, 4096)  # the decompositions write planes 1..K-1 as operand rows
-    sides = 2 if d in (1024, 4096) else 1  # these decompositions run both sides in one launch
     alg = {
-        # B2 (per launch): f_coeff in; f_k_coeff, f_k (K N each), w_ccs_k (K W) out
-        "decompose": sides * E * (N + 2 * K * N + K * W),
+        # B2 (per side; phase_report scales by the sides one launch covers):
+        # f_coeff in; f_k_coeff, f_k (K N each), w_ccs_k (K W) out
+        "decompose": E * (N + 2 * K * N + K * W),
         # B3 + commit(z)'s A f: A once, the 29 vectors, the 29 kappa-element results
         "ajtai": E * (kappa * N + nvec * N + nvec * kappa),
         "fold": E * (2 * K * N + N),  # B4
@@ -87,7 +87,7 @@ def algorithmic_bytes(d, W, kappa, L=5, K=15):
         "to_frag": E * N + F * N,  # commit(z)'s f into operand form (fused paths)
     }
     operand = {
-        "decompose": sides * F * (K - 1) * N if fused else 0,
+        "decompose": F * (K - 1) * N if fused else 0,
         "ajtai": (F - E) * (kappa * N + nvec * N),
     }
     return step, alg, operand
@@ -350,13 +350,16 @@ def phase_report(LA, wl, tot, steps):
         if not cnt:
             continue
         avg = ms / cnt
-        gbs = alg[ph] / (avg * 1e-3) / 1e9
-        extra = operand.get(ph, 0)
+        # the decomposition covers both sides of a step in one launch or one per launch
+        sides = max(1, round(2 * steps / cnt)) if ph == "decompose" else 1
+        a = alg[ph] * sides
+        gbs = a / (avg * 1e-3) / 1e9
+        extra = operand.get(ph, 0) * sides
         phases[ph] = {"kernel": kernel_of[ph], "avg_launch_ms": avg, "launches_per_step": cnt / steps,
-                      "ms_per_step": ms / steps, "algorithmic_bytes_per_launch": alg[ph],
+                      "ms_per_step": ms / steps, "algorithmic_bytes_per_launch": a,
                       "achieved_gbs": gbs, "frac_hbm": gbs / HBM_PEAK_GBS,
                       "operand_bytes_per_launch": extra,
-                      "achieved_gbs_incl_operands": (alg[ph] + extra) / (avg * 1e-3) / 1e9,
+                      "achieved_gbs_incl_operands": (a + extra) / (avg * 1e-3) / 1e9,
                       "traffic_bytes_per_launch": traffic.get(kernel_of[ph])}
     if not phases:
         return phases, None

@@ -259,11 +259,14 @@ constexpr int DEC_SROW = 41;  // operand staging row (40 virtual slots + pad) of
 // Every HBM access of the block is a run of whole 16-B pieces over contiguous
 // rows: f_coeff comes in and f_coeff_k / f_k go out through LDS (the element
 // rows [e][SROW] and a byte copy of the digits), not as one 192-B row per thread.
-__global__ void __launch_bounds__(256) k_decompose_phi72(const uint64_t *f_coeff, size_t N, int lb,
-                                                        int L, int lbs, int K, uint64_t *f_coeff_k,
-                                                        uint64_t *f_k, uint64_t *w_ccs_k, int *err,
-                                                        uint4 *frag, int nch, int row0, int srow) {
+// blockIdx.z selects the side (both sides of a fold step in one launch)
+__global__ void __launch_bounds__(256) k_decompose_phi72(FusedSides sd, size_t N, int lb, int L, int lbs, int K,
+                                                        int *err, uint4 *frag, int nch, int srow) {
   extern __shared__ uint64_t lds[];  // [DEC_GROUPS * L][srow] u64; a row's words 25..27 hold the digit bytes
+  const int side = blockIdx.z;
+  const uint64_t *f_coeff = sd.f_coeff[side];
+  uint64_t *f_coeff_k = sd.f_coeff_k[side], *f_k = sd.f_k[side], *w_ccs_k = sd.w_ccs_k[side];
+  const int row0 = sd.row0[side];
   const int t = threadIdx.x, ne = DEC_GROUPS * L;
   int8_t *dgl = reinterpret_cast<int8_t *>(lds + 25);  // element e's digits at dgl[e * 8 srow + i]
   const size_t W = N / L;
@@ -1016,6 +1019,30 @@ hipError_t from_f(const uint64_t *f, size_t N, int d, int lb, int L, uint64_t *f
   return hipGetLastError();
 }
 
+hipError_t decompose_phi72_sides(const FusedSides &sd, size_t N, int lb, int L, int lbs, int K, int *err,
+                                 uint4 *frag, int nch, hipStream_t st) {
+  const size_t W = N / L;
+  if (W == 0) return hipSuccess;
+  if (DEC_GROUPS * L > 256 || sd.nside < 1 || sd.nside > 2) return hipErrorInvalidValue;
+  if (frag) {
+    if (L > 5) return hipErrorInvalidValue;
+    for (int s = 0; s < sd.nside; s++)
+      if (sd.row0[s] < 0 || sd.row0[s] + K - 1 > 32) return hipErrorInvalidValue;
+  }
+  const int srow = frag ? DEC_SROW : 28;
+  const size_t lds = (size_t)DEC_GROUPS * L * srow * sizeof(uint64_t);
+  // with independent planes (b = 2), split them over blockIdx.y until about
+  // 1024 blocks run per side: the real zkvm shape (W = 19 763) has only 412
+  // element blocks (one plane per block is no faster there: 0.30 against 0.29 ms)
+  const unsigned nb = blocks(W, DEC_GROUPS);
+  unsigned ys = lbs == 1 ? (1024 + nb - 1) / nb : 1;
+  if (ys > (unsigned)K) ys = K;
+  if (ys < 1) ys = 1;
+  hipLaunchKernelGGL(k_decompose_phi72, dim3(nb, ys, (unsigned)sd.nside), dim3(256), lds, st, sd, N, lb, L, lbs, K,
+                     err, frag, nch, srow);
+  return hipGetLastError();
+}
+
 hipError_t decompose_witness(const uint64_t *f_coeff, size_t N, int d, int lb, int L, int lbs, int K,
                              uint64_t *f_coeff_k, uint64_t *f_k, uint64_t *w_ccs_k,
                              const ring::NegaTables &fwd, int *err, hipStream_t st, uint4 *frag, int nch,
@@ -1025,20 +1052,14 @@ hipError_t decompose_witness(const uint64_t *f_coeff, size_t N, int d, int lb, i
   if (d == 1024 && fwd.mid && lbs == 1 && K <= 15 && L <= 5)
     return decompose_n32(f_coeff, N, lb, L, K, f_coeff_k, f_k, w_ccs_k, fwd, err, st);
   if (d == 24) {
-    if (DEC_GROUPS * L > 256) return hipErrorInvalidValue;
-    if (frag && (L > 5 || row0 < 0 || row0 + K - 1 > 32)) return hipErrorInvalidValue;
-    const int srow = frag ? DEC_SROW : 28;
-    const size_t lds = (size_t)DEC_GROUPS * L * srow * sizeof(uint64_t);
-    // with independent planes (b = 2), split them over blockIdx.y until about
-    // 1024 blocks run: the real zkvm shape (W = 19 763) has only 412 element
-    // blocks (one plane per block is no faster there: 0.30 against 0.29 ms)
-    const unsigned nb = blocks(W, DEC_GROUPS);
-    unsigned ys = lbs == 1 ? (1024 + nb - 1) / nb : 1;
-    if (ys > (unsigned)K) ys = K;
-    if (ys < 1) ys = 1;
-    hipLaunchKernelGGL(k_decompose_phi72, dim3(nb, ys), dim3(256), lds, st, f_coeff, N, lb, L, lbs, K,
-                       f_coeff_k, f_k, w_ccs_k, err, frag, nch, row0, srow);
-    return hipGetLastError();
+    FusedSides sd{};
+    sd.nside = 1;
+    sd.f_coeff[0] = f_coeff;
+    sd.f_coeff_k[0] = f_coeff_k;
+    sd.f_k[0] = f_k;
+    sd.w_ccs_k[0] = w_ccs_k;
+    sd.row0[0] = row0;
+    return decompose_phi72_sides(sd, N, lb, L, lbs, K, err, frag, nch, st);
   }
   if (L > 8) return hipErrorInvalidValue;
 #define LF_CASE(DD)                                                                                  \

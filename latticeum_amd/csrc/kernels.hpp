@@ -119,6 +119,9 @@ hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K,
                            const ring::NegaTables &fwd, uint4 *frag, int nch, int *err, uint64_t *sink, int ncu,
                            hipStream_t st);
 
+// d = 24: both sides of a fold step in one launch (blockIdx.z = side); frag as decompose_witness
+hipError_t decompose_phi72_sides(const FusedSides &sd, size_t N, int lb, int L, int lbs, int K, int *err,
+                                 uint4 *frag, int nch, hipStream_t st);
 // d = 4096, b_small = 2 (kernels_n4k.hip): sm4 holds nside N 1024 packed words; sink 4096 words.
 // With frag (a scheme whose geometry has Lp = L and qperm), planes k >= 1 are also
 // written as operand rows row0[side] + k - 1, as decompose_fused does for d = 1024.

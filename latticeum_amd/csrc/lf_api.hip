@@ -445,11 +445,17 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       LF_HIP(c, lfk::decompose_fused(sd, N, lb, L, K, c->smg, t->fwd, fv ? nullptr : c->frag, aj->geom.nch, c->d_err,
                                      c->sink, c->ncu, c->cur));
     } else {
+      lfk::FusedSides sd{};
+      sd.nside = 2;
       for (int s = 0; s < 2; s++) {
-        PhaseTimer pt(c, LF_PHASE_DECOMPOSE);
-        LF_HIP(c, lfk::decompose_witness(fc_side[s], N, d, lb, L, lbs, K, b->fk_coeff[s], b->fk[s], b->wk[s],
-                                         t->fwd, c->d_err, c->cur, c->frag, aj->geom.nch, extra + s * (K - 1)));
+        sd.f_coeff[s] = fc_side[s];
+        sd.f_coeff_k[s] = b->fk_coeff[s];
+        sd.f_k[s] = b->fk[s];
+        sd.w_ccs_k[s] = b->wk[s];
+        sd.row0[s] = extra + s * (K - 1);
       }
+      PhaseTimer pt(c, LF_PHASE_DECOMPOSE);  // both sides in one launch
+      LF_HIP(c, lfk::decompose_phi72_sides(sd, N, lb, L, lbs, K, c->d_err, c->frag, aj->geom.nch, c->cur));
     }
     lfk::VecPtrs vp{};
     if (fv) {
