@@ -514,6 +514,32 @@ def next_rows(LA, torch, local, cpu):
         out["folding_sumcheck"]["cpu_baseline"] = {
             "ms_per_prove": dt * (1 << (nv - nvs)) * 1e3, "cores": 1, "kind": "port",
             "sample": f"the oracle's prover at log m = {nvs} ({dt:.2f} s, 1 thread), scaled by 2^{nv - nvs}"}
+    # the linearization sumcheck at the zkvm's CCS degree: 125 Mz MLEs + eq(beta),
+    # 52 multisets (16 of size 7, the Poseidon2 S-box, and 36 of size 1 or 2),
+    # degree 8 (LINEARIZATION_DEGREE - 1, zkvm/src/ccs.rs:55-67), 17 rounds
+    rng = np.random.default_rng(0x4C460014)
+    S = [list(rng.integers(0, 125, 7)) for _ in range(16)] + \
+        [list(rng.integers(0, 125, 1 + (i % 2))) for i in range(36)]
+    S = [[int(j) for j in x] for x in S]
+    nml = 126
+    m = torch.empty(nml * n * d, **i64)
+    cdev = torch.empty(len(S) * d, **i64)
+    ctx.dev_fill_uniform(cdev, 0x4C460015)
+    combl = LA.Comb.linearization(cdev, S)
+    times = []
+    for rep_ in range(3):
+        ctx.dev_fill_uniform(m, 0x4C460016 + rep_)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ctx.sumcheck_prove(LA.Poseidon2Transcript(), combl, m, nml, nv, d, 8)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    out["linearization_sumcheck"] = {
+        "workload": f"linearization sumcheck prover: Phi_72, {nml} MLEs of 2^{nv} ring elements "
+                    f"({nml * n * d * 8 / 1e9:.2f} GB), 52 multisets (16 of size 7), degree 8, {nv} rounds",
+        "ms_per_prove": min(times[1:]) * 1e3, "rounds": nv}
+    del m
+    torch.cuda.empty_cache()
     # sparse CCS products at the zkvm's dimensions
     t, mm, nn, K = 125, 1 << 17, 19768, 15
     rng = np.random.default_rng(0x4C460012)

@@ -1286,7 +1286,7 @@ int lf_dev_sumcheck_round(lf_ctx *c, const lf_comb *cb, const uint64_t *mles, si
   LF_TRY(comb_check(c, cb, nm, d, cb && cb->kind == LF_COMB_FOLDING ? -1 : degree, &cs));
   const int deg = comb_degree(cb, degree);
   const size_t half = (size_t)1 << (nv - 1);
-  const size_t part = lfk::round_partial_elems(d, half, deg + 1, cb->kind == LF_COMB_FOLDING ? cb->nk * cb->tau : 1);
+  const size_t part = lfk::round_partial_elems(d, half, deg + 1, cb->kind == LF_COMB_FOLDING ? cb->nk * cb->tau : cb->q);
   const size_t wlen = cb->kind == LF_COMB_FOLDING ? (size_t)cb->nk * cb->tau * d : 0;
   LF_TRY(grow(c, c->sc, c->sc_elems, part + wlen));
   if (cb->kind == LF_COMB_FOLDING) {
@@ -1311,7 +1311,7 @@ int lf_sumcheck_prove(lf_ctx *c, lf_transcript *t, const lf_comb *cb, uint64_t *
   // scratch: the MLEs fixed by the first challenge (later rounds ping-pong with
   // `mles` itself), the round's partial sums, the evaluations, the weights
   // the partial sums of every round fit the largest round's (chunks only split the small ones)
-  const int nfc = cb->kind == LF_COMB_FOLDING ? cb->nk * cb->tau : 1;
+  const int nfc = cb->kind == LF_COMB_FOLDING ? cb->nk * cb->tau : cb->q;  // the chunked sum (f_hat MLEs / multisets)
   size_t part = 0;
   for (size_t h = n / 2; h >= 1; h /= 2) part = std::max(part, lfk::round_partial_elems(d, h, nev, nfc));
   const size_t fixed = (size_t)nm * (n / 2) * d;

@@ -208,6 +208,9 @@ __global__ void __launch_bounds__(RT) k_round_lin(const uint64_t *mles, size_t s
                                                   CombS cs, size_t half, int d, int spb, uint64_t *partial) {
   const int slot_l = threadIdx.x % spb, lane_p = threadIdx.x / spb, ppb = RT / spb;
   const int slot = blockIdx.y * spb + slot_l;
+  // the sum over the multisets is split over blockIdx.z chunks when the points are few
+  const int chunk = blockIdx.z, nchunk = gridDim.z;
+  const int i0 = (int)((long)cs.q * chunk / nchunk), i1 = (int)((long)cs.q * (chunk + 1) / nchunk);
   constexpr int degree = DEG;
   Sv<TB> acc[degree + 1];
 #pragma unroll
@@ -215,30 +218,74 @@ __global__ void __launch_bounds__(RT) k_round_lin(const uint64_t *mles, size_t s
   for (size_t b = (size_t)blockIdx.x * ppb + lane_p; b < half; b += (size_t)gridDim.x * ppb) {
     const uint64_t *pb = mles + 2 * b * d + slot * TB;
     const uint64_t *pe = pb + (size_t)(nm - 1) * stride;
-    const Sv<TB> e0 = s_load<TB>(pe), es = s_sub(s_load<TB>(pe + d), e0);
+    // every MLE value of a multiset is loaded once and walked along the line
+    // x(e) = a + e (b - a) by additions, multiplied into all degree + 1 terms
+    Sv<TB> sum[degree + 1];
+#pragma unroll
+    for (int e = 0; e <= degree; e++) sum[e] = s_zero<TB>();
+    for (int i = i0; i < i1; i++) {
+      const Sv<TB> ci = s_load<TB>(c + (size_t)i * d + slot * TB);
+      if (s_is_zero(ci)) continue;  // the term vanishes in this slot
+      const int s0 = cs.off[i], s1 = cs.off[i + 1];
+      Sv<TB> term[degree + 1];
+      if (s1 == s0) {
+#pragma unroll
+        for (int e = 0; e <= degree; e++) term[e] = ci;
+      } else {
+        // c_i times the first one or two factors in coefficient form (2 or 6
+        // products instead of 9 or 18), then the values at e = 0 .. degree by
+        // forward differences (additions only)
+        const uint64_t *p = pb + (size_t)cs.idx[s0] * stride;
+        const Sv<TB> a = s_load<TB>(p);
+        const Sv<TB> u0 = s_mul(ci, a), u1 = s_mul(ci, s_sub(s_load<TB>(p + d), a));  // c_i x1(e) = u0 + u1 e
+        if (s1 - s0 == 1) {
+          Sv<TB> x = u0;
+#pragma unroll
+          for (int e = 0; e <= degree; e++) {
+            term[e] = x;
+            if (e < degree) x = s_add(x, u1);
+          }
+        } else {
+          const uint64_t *q = pb + (size_t)cs.idx[s0 + 1] * stride;
+          const Sv<TB> g0 = s_load<TB>(q), g1 = s_sub(s_load<TB>(q + d), g0);  // x2(e) = g0 + g1 e
+          // (u0 + u1 e)(g0 + g1 e) = k0 + k1 e + k2 e^2: f(0) = k0, delta_0 = k1 + k2, second difference 2 k2
+          const Sv<TB> k0 = s_mul(u0, g0), k2 = s_mul(u1, g1);
+          const Sv<TB> k1 = s_add(s_mul(u0, g1), s_mul(u1, g0));
+          Sv<TB> x = k0, dx = s_add(k1, k2);
+          const Sv<TB> d2 = s_add(k2, k2);
+#pragma unroll
+          for (int e = 0; e <= degree; e++) {
+            term[e] = x;
+            if (e < degree) {
+              x = s_add(x, dx);
+              dx = s_add(dx, d2);
+            }
+          }
+        }
+      }
+      for (int sx = s0 + 2 < s1 ? s0 + 2 : s1; sx < s1; sx++) {
+        const uint64_t *p = pb + (size_t)cs.idx[sx] * stride;
+        Sv<TB> x = s_load<TB>(p);
+        const Sv<TB> st = s_sub(s_load<TB>(p + d), x);
+#pragma unroll
+        for (int e = 0; e <= degree; e++) {
+          term[e] = s_mul(term[e], x);
+          if (e < degree) x = s_add(x, st);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e <= degree; e++) sum[e] = s_add(sum[e], term[e]);
+    }
+    Sv<TB> ev = s_load<TB>(pe);
+    const Sv<TB> es = s_sub(s_load<TB>(pe + d), ev);
 #pragma unroll
     for (int e = 0; e <= degree; e++) {
-      Sv<TB> sum = s_zero<TB>();
-      for (int i = 0; i < cs.q; i++) {
-        Sv<TB> term = s_load<TB>(c + (size_t)i * d + slot * TB);
-        for (int s = cs.off[i]; s < cs.off[i + 1]; s++) {
-          const uint64_t *p = pb + (size_t)cs.idx[s] * stride;
-          const Sv<TB> a = s_load<TB>(p);
-          Sv<TB> x = a;
-          if (e) {
-            const Sv<TB> st = s_sub(s_load<TB>(p + d), a);
-            for (int q = 0; q < e; q++) x = s_add(x, st);
-          }
-          term = s_mul(term, x);
-        }
-        sum = s_add(sum, term);
-      }
-      Sv<TB> ev = e0;
-      for (int q = 0; q < e; q++) ev = s_add(ev, es);
-      acc[e] = s_add(acc[e], s_mul(sum, ev));
+      acc[e] = s_add(acc[e], s_mul(sum[e], ev));
+      if (e < degree) ev = s_add(ev, es);
     }
   }
-  block_partial<TB, degree + 1>(acc, spb, ppb, slot, lane_p, d, partial + (size_t)blockIdx.x * (degree + 1) * d);
+  block_partial<TB, degree + 1>(acc, spb, ppb, slot, lane_p, d,
+                                partial + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * (degree + 1) * d);
 }
 
 // out[i] = sum over blocks of partial[blk][i]: one block per output word,
@@ -383,7 +430,7 @@ hipError_t round_lin(const uint64_t *mles, size_t stride, int nm, const uint64_t
   if (degree + 1 > MAX_EVALS || degree < 1 || !half) return hipErrorInvalidValue;
   int spb;
   dim3 grid;
-  round_geom(d, half, 1, spb, grid);
+  round_geom(d, half, cs.q, spb, grid);
 #define LF_RL(TB, DG) \
   hipLaunchKernelGGL((k_round_lin<TB, DG>), grid, dim3(RT), 0, st, mles, stride, nm, c, cs, half, d, spb, partial)
 #define LF_RL_DEG(TB)                          \
@@ -408,7 +455,8 @@ hipError_t round_lin(const uint64_t *mles, size_t stride, int nm, const uint64_t
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const size_t len = (size_t)(degree + 1) * d;
-  hipLaunchKernelGGL(k_sum_partials, dim3((unsigned)len), dim3(256), 0, st, partial, (int)grid.x, len, evals);
+  hipLaunchKernelGGL(k_sum_partials, dim3((unsigned)len), dim3(256), 0, st, partial, (int)(grid.x * grid.z), len,
+                     evals);
   return hipGetLastError();
 }
 
