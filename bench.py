@@ -93,7 +93,7 @@ def algorithmic_bytes(d, W, kappa, L=5, K=15):
     return step, alg, operand
 
 
-def kernel_names(LA, d, W, layout):
+def kernel_names(LA, d, W, layout, keep_fk=True):
     """the kernel each lf_dev_fold_step phase launches (for the rocprof / PMC joins)"""
     if d == 24:
         return {"decompose": "k_decompose_phi72", "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_phi72",
@@ -102,7 +102,8 @@ def kernel_names(LA, d, W, layout):
     if d == 1024:
         small = W < LA.witness_split_w()  # one half-wave per (element, limb) below this W
         return {"decompose": "k_decompose_fused", "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_nega",
-                "fold": "k_fold_nega", "from_w_ccs": "k_from_w_ccs_split" if small else "k_from_w_ccs_n32",
+                "fold": "k_fold_nega" if keep_fk else "k_fold_frag",
+                "from_w_ccs": "k_from_w_ccs_split" if small else "k_from_w_ccs_n32",
                 "from_f": "k_from_f_split" if small else "k_from_f_n32", "to_frag": "k_to_frag<true, false, true>"}
     if d == 4096:
         return {"decompose": "k_decompose_n4k_fused" if layout == 1 else "k_decompose_n4k",
@@ -206,7 +207,11 @@ class Workload:
     side and rho (shared, read-only), and `streams` independent step streams,
     each an lf context on its own HIP stream with its own w_ccs and outputs."""
 
-    def __init__(self, LA, torch, local, rank, d, W, kappa, streams, seed_a=SEED_A):
+    def __init__(self, LA, torch, local, rank, d, W, kappa, streams, seed_a=SEED_A, keep_fk=True):
+        # keep_fk=False (fused X^1024+1 path only): the decomposed planes live only
+        # as MFMA operand rows (lf.h: f_k buffers omitted) -- 20 GB less HBM at
+        # W = 2^14, but slower (DESIGN.md section 7), so the bench keeps f_k
+        self.keep_fk = keep_fk
         self.LA, self.torch = LA, torch
         self.d, self.W, self.kappa = d, W, kappa
         self.pr = pr = LA.goldilocks_dp(d)
@@ -250,7 +255,8 @@ class Workload:
             keep = {
                 "w_ccs": w_ccs, "acc_cm": acc_cm, "acc_f_coeff": acc_fc, "rho": rho,
                 "f_coeff": z(N * d), "f": z(N * d), "cm": z(kappa * d),
-                "fk_coeff": [z(K * N * d) for _ in range(2)], "fk": [z(K * N * d) for _ in range(2)],
+                "fk_coeff": [z(K * N * d) for _ in range(2)],
+                "fk": [z(K * N * d) for _ in range(2)] if keep_fk else [None, None],
                 "wk": [z(K * W * d) for _ in range(2)], "y": [z(K * kappa * d) for _ in range(2)],
                 "f0": z(N * d), "f0_coeff": z(N * d), "w_ccs0": z(W * d), "cm0": z(kappa * d),
             }
@@ -258,7 +264,7 @@ class Workload:
             for k, v in keep.items():
                 if isinstance(v, list):
                     for s in range(2):
-                        getattr(bufs, k)[s] = v[s].data_ptr()
+                        getattr(bufs, k)[s] = v[s].data_ptr() if v[s] is not None else None
                 else:
                     setattr(bufs, k, v.data_ptr())
             c.reserve(kappa, N, d, 2 * (K - 1) + 1)
@@ -343,7 +349,9 @@ def phase_report(LA, wl, tot, steps):
     bytes, achieved GB/s and fraction of HBM peak; the dominant phase's roofline"""
     d, W, kappa = wl.d, wl.W, wl.kappa
     _, alg, operand = algorithmic_bytes(d, W, kappa, wl.pr.L, wl.pr.K)
-    kernel_of = kernel_names(LA, d, W, wl.sch.layout)
+    if not wl.keep_fk:  # the planes are written once, as the operand rows: no bytes beyond B2
+        operand["decompose"] = 0
+    kernel_of = kernel_names(LA, d, W, wl.sch.layout, wl.keep_fk)
     traffic = load_traffic(d, W, kappa)
     phases = {}
     for ph, (ms, cnt) in tot.items():

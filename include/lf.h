@@ -232,7 +232,9 @@ typedef struct {
   uint64_t *f_coeff, *f;       /* N each: Witness::from_w_ccs(w_ccs) */
   uint64_t *cm;                /* kappa: CCCS.cm = A f */
   uint64_t *fk_coeff[2];       /* [K][N] per side (0 = accumulator, 1 = new instance) */
-  uint64_t *fk[2];             /* [K][N] */
+  uint64_t *fk[2];             /* [K][N]; both NULL on the fused X^1024+1 path: the decomposed planes then
+                                * live only in the context's MFMA operand rows, which the fold reads
+                                * (they are transient in the reference too: compute_f_0, folding.rs:258) */
   uint64_t *wk[2];             /* [K][W] */
   uint64_t *y[2];              /* [K][kappa] decomposition commitments */
   uint64_t *f0, *f0_coeff;     /* N each: folded witness */

@@ -138,6 +138,11 @@ class Context:
         self.check(self.lib.lf_witness_from_f(self.h, C.byref(params), _ptr(x), N, _ptr(fc), _ptr(w), repr))
         return fc, w
 
+    def dev_decompose_witness(self, params: LfParams, f_coeff, N: int, f_coeff_k, f_k, w_ccs_k):
+        """decompose_witness on device buffers: f_coeff [N] -> [K][N], [K][N], [K][N / L]"""
+        self.check(self.lib.lf_dev_decompose_witness(self.h, C.byref(params), _dptr(f_coeff), N, _dptr(f_coeff_k),
+                                                     _dptr(f_k), _dptr(w_ccs_k)))
+
     def decompose_witness(self, f_coeff, params: LfParams, repr: int = REPR_CANONICAL):
         x = _u64(f_coeff)
         d, L, K = params.d, params.L, params.K

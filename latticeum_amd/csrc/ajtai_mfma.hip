@@ -468,6 +468,59 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_fv(const uint4 *Af, VecPt
   mfma_epilogue(acc, lane, kt, kappa, nvec, d, s, js, direct, dst, partial);
 }
 
+// ---------------------------------------------------------------- f_0 from the operand rows
+// folding.rs:258-268 compute_f_0 when the step keeps the decomposed planes only
+// as D8 operand rows (the fused d = 1024 decomposition with f_k = null): a
+// block takes 16 slots (four slot quads, one 128-B line of every element) of
+// one 32-column chunk; thread (quad, slot, half, vector group) undoes the byte
+// transposition of its 16 columns for vectors v = vg, vg + 8, .. and
+// multiply-accumulates rho_v (.) f_v lazily; the 8 vector groups meet in LDS
+// and each output column's 16 slots go out as one 128-B run.
+__global__ void __launch_bounds__(256) k_fold_frag(const uint4 *frag, int nch, int Lp, size_t Wp, FoldRows fr,
+                                                  const uint64_t *rho, int d, size_t N, uint64_t *out) {
+  __shared__ uint64_t red[512 * 9];  // [output (column, slot)][vector group], rows padded to 9
+  const int tid = threadIdx.x, vg = tid & 7, h = (tid >> 3) & 1, sl = (tid >> 4) & 3, qq = tid >> 6;
+  const int ng = d >> 4, G = blockIdx.x % ng, c = blockIdx.x / ng;
+  const int s = 16 * G + 4 * qq + sl;
+  gl::CAcc acc[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) gl::cacc_zero(acc[j]);
+  for (int v = vg; v < fr.n; v += 8) {
+    const uint4 *pc = frag + fv_index(s, nch, c, fr.row[v], h);
+    uint4 u[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) u[k] = pc[4 * k];
+    const uint64_t rv = rho[(size_t)fr.rho[v] * d + s];
+    uint64_t x[16];
+    d8_untranspose16(u, x);
+#pragma unroll
+    for (int j = 0; j < 16; j++) gl::cacc_mad(acc[j], rv, x[j]);
+  }
+  // output o = column (32) x slot (16): o = (16 h + jj) 16 + 4 qq + sl
+#pragma unroll
+  for (int jj = 0; jj < 16; jj++) red[((16 * h + jj) * 16 + 4 * qq + sl) * 9 + vg] = gl::cacc_reduce(acc[jj]);
+  __syncthreads();
+#pragma unroll
+  for (int rep = 0; rep < 2; rep++) {
+    const int o = tid + 256 * rep, j = o >> 4, s16 = o & 15;
+    uint64_t t = red[o * 9];
+#pragma unroll
+    for (int g = 1; g < 8; g++) t = gl::add(t, red[o * 9 + g]);
+    bool ok;
+    const size_t col = frag_column(c, j, Lp, Wp, ok);
+    if (ok && col < N) out[col * d + 16 * G + s16] = t;
+  }
+}
+
+hipError_t fold_frag(const uint4 *frag, const FragGeom &g, const FoldRows &fr, const uint64_t *rho, int d, size_t N,
+                     uint64_t *out, hipStream_t st) {
+  if (d == 24 || d % 16 || g.qperm || fr.n < 1 || fr.n > LF_MAX_VECS) return hipErrorInvalidValue;
+  if (!N) return hipSuccess;
+  const size_t nb = (size_t)(d / 16) * g.nch;
+  hipLaunchKernelGGL(k_fold_frag, dim3((unsigned)nb), dim3(256), 0, st, frag, g.nch, g.Lp, g.Wp, fr, rho, d, N, out);
+  return hipGetLastError();
+}
+
 // Phi_72 epilogue: virtual-slot sums [nvec][kappa][40] -> Fq3 slots [kappa][24] per vector
 __global__ void k_phi72_interp(const uint64_t *virt, int nvec, size_t kappa, OutPtrs out) {
   const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // (v, row, slot)

@@ -47,6 +47,37 @@ __device__ __forceinline__ void d8_transpose16(const uint64_t *x, uint4 *u) {
   }
 }
 
+// 4 x 4 byte transpose: o[k] byte i = w[i] byte k
+__device__ __forceinline__ void byte_tr4(const uint32_t *w, uint32_t *o) {
+#pragma unroll
+  for (int bb = 0; bb < 4; bb += 2) {
+    const uint32_t sel =
+        (uint32_t)bb | ((uint32_t)(4 + bb) << 8) | ((uint32_t)(bb + 1) << 16) | ((uint32_t)(5 + bb) << 24);
+    const uint32_t t01 = __builtin_amdgcn_perm(w[1], w[0], sel);
+    const uint32_t t23 = __builtin_amdgcn_perm(w[3], w[2], sel);
+    o[bb] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
+    o[bb + 1] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
+  }
+}
+// the inverse of d8_transpose16 followed by the D8 decode: 8 operand pieces
+// (digit b of 16 columns) -> the 16 residues (canonical)
+__device__ __forceinline__ void d8_untranspose16(const uint4 *u, uint64_t *x) {
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    uint32_t w[8], lo[4], hi[4];
+#pragma unroll
+    for (int k = 0; k < 8; k++) w[k] = q == 0 ? u[k].x : q == 1 ? u[k].y : q == 2 ? u[k].z : u[k].w;
+    byte_tr4(w, lo);
+    byte_tr4(w + 4, hi);
+#pragma unroll
+    for (int cc = 0; cc < 4; cc++) {
+      const uint64_t wd = (uint64_t)lo[cc] | ((uint64_t)hi[cc] << 32);
+      const uint64_t t = (wd ^ 0x8080808080808080ull) - 0x8080808080808080ull;
+      x[4 * q + cc] = t <= 0x7F7F7F7F7F7F7F7Full ? t : t - 0xFFFFFFFFull;
+    }
+  }
+}
+
 // Streaming (nontemporal) stores for outputs written once and not re-read by
 // the writing launch. At W = 2^14 (61 GB of decomposition outputs per step)
 // they keep the outputs from cycling through the caches (15.5 -> 14.2 ms); at

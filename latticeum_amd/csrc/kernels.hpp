@@ -110,10 +110,19 @@ hipError_t decompose_n32(const uint64_t *f_coeff, size_t N, int lb, int L, int K
 // scratch for the packed coefficients
 struct FusedSides {
   const uint64_t *f_coeff[2];
-  uint64_t *f_coeff_k[2], *f_k[2], *w_ccs_k[2];
-  int row0[2];
+  uint64_t *f_coeff_k[2], *f_k[2], *w_ccs_k[2];  // f_k may be null (d = 1024: the planes stay in the operand rows)
+  int row0[2];                                   // operand row of plane 1 (planes 1 .. K-1 consecutive)
   int nside;
+  int row_p0[2] = {-1, -1};                      // operand row of plane 0, or -1 (not written)
 };
+// f_0 = sum_v rho_v f_v with every f_v read from the D8 operand rows (k_fold_frag)
+struct FoldRows {
+  int row[LF_MAX_VECS];   // operand row of vector v
+  int rho[LF_MAX_VECS];   // its rho index
+  int n;
+};
+hipError_t fold_frag(const uint4 *frag, const FragGeom &g, const FoldRows &fr, const uint64_t *rho, int d, size_t N,
+                     uint64_t *out, hipStream_t st);
 // sink: an 8 KiB device scratch row (stores of groups past W); ncu: the device's CU count
 hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K, uint32_t *smg,
                            const ring::NegaTables &fwd, uint4 *frag, int nch, int *err, uint64_t *sink, int ncu,

@@ -439,7 +439,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_
     const int kb = (int)(task % K);
     const uint32_t *smg = smg_all + side * N * 512;
     uint64_t *f_coeff_k = sd.f_coeff_k[side], *f_k = sd.f_k[side], *w_ccs_k = sd.w_ccs_k[side];
-    const int row0 = sd.row0[side];
+    const int row0 = sd.row0[side], row_p0 = sd.row_p0[side];
     const size_t g = 16 * B + hw;
     const bool ok = g < W;
     const size_t gg = ok ? g : 0;
@@ -483,7 +483,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_
         uint64_t v[32];
         n32::neg_ct32_digits(dg, v);
         n32::forward<false>(v, mid_f, T, r);
-        {
+        if (f_k) {  // uniform: without f_k the planes live only in the operand rows
           uint64_t *of = (ok ? f_k + e * D : sink) + r;
 #pragma unroll
           for (int i = 0; i < 32; i++) out_store<NT>(&of[32 * n32::brv5(i)], v[i]);
@@ -498,13 +498,13 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_
 #pragma unroll
           for (int i = 0; i < 32; i++) acc[i] = gl::add(gl::mul(acc[i], b_pow), v[i]);
         }
-        if (frag && kb > 0) {
+        if (frag && (kb > 0 || row_p0 >= 0)) {
           __syncthreads();  // every wave is past its transpose: S may overwrite T
 #pragma unroll
           for (int i = 0; i < 32; i++) S[(r + 32 * n32::brv5(i)) * FD_SROW + hw] = d8(v[i]);
           __syncthreads();
           const size_t u = B * L + l;  // contraction unit of these 16 columns
-          const int c = (int)(u >> 1), uh = (int)(u & 1), row = row0 + kb - 1;
+          const int c = (int)(u >> 1), uh = (int)(u & 1), row = kb > 0 ? row0 + kb - 1 : row_p0;
 #pragma unroll
           for (int rep = 0; rep < 2; rep++) {
             const int s = threadIdx.x + 512 * rep;

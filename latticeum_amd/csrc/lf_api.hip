@@ -57,6 +57,8 @@ struct lf_ctx {
   size_t tmp_elems = 0;
   uint64_t *sc = nullptr;       // sumcheck: fixed MLEs of the next round, round partial sums, weights
   size_t sc_elems = 0;
+  lfk::FoldRows fold_rows{};    // a step without f_k buffers: where its 2K planes sit in the operand rows
+  bool fold_from_frag = false;
   bool timing = false;
   std::vector<TimedLaunch> pending;
   std::map<int, std::pair<double, long>> stats;  // nvec -> (ms, count)
@@ -423,6 +425,25 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
   const bool fused24 = aj->Af && aj->geom.Lp == L && d == 24 && L <= 5;
   // d = 4096 (kernels_n4k.hip): the same, with the quarter-major operand slots
   const bool fused4k = aj->Af && aj->geom.Lp == L && aj->geom.qperm && n4k_ok(t, d, lbs, K);
+  // without f_k buffers the planes exist only as operand rows (planes 1..K-1
+  // of each side as usual, plane 0 in rows extra + 2(K-1) + s) and fold_finish
+  // reads f_0's inputs from there (k_fold_frag)
+  const bool no_fk = !b->fk[0] && !b->fk[1];
+  c->fold_from_frag = false;
+  if (no_fk) {
+    if (!fused || fv) return fail(c, LF_ERR_INVALID_ARG, "f_k buffers may be omitted only on the fused X^1024+1 path");
+    if (extra + 2 * (K - 1) + 2 > LF_MAX_VECS) return fail(c, LF_ERR_INVALID_ARG, "too many operand rows");
+    lfk::FoldRows &fr = c->fold_rows;
+    fr.n = 2 * K;
+    for (int s2 = 0; s2 < 2; s2++)
+      for (int k = 0; k < K; k++) {
+        fr.row[s2 * K + k] = k > 0 ? extra + s2 * (K - 1) + k - 1 : extra + 2 * (K - 1) + s2;
+        fr.rho[s2 * K + k] = s2 * K + k;
+      }
+    c->fold_from_frag = true;
+  } else if (!b->fk[0] || !b->fk[1]) {
+    return fail(c, LF_ERR_INVALID_ARG, "f_k: both sides or neither");
+  }
   if (fused || fused24 || fused4k) {
     if (!fv) LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->geom, d)));
     if (fused4k) {
@@ -440,6 +461,7 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
         sd.f_k[s] = b->fk[s];
         sd.w_ccs_k[s] = b->wk[s];
         sd.row0[s] = extra + s * (K - 1);
+        sd.row_p0[s] = no_fk ? extra + 2 * (K - 1) + s : -1;
       }
       PhaseTimer pt(c, LF_PHASE_DECOMPOSE);  // both sides in one launch
       LF_HIP(c, lfk::decompose_fused(sd, N, lb, L, K, c->smg, t->fwd, fv ? nullptr : c->frag, aj->geom.nch, c->d_err,
@@ -519,10 +541,13 @@ int fold_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
   LF_TRY(get_tables(c, d, t));
   // y_0 of both sides and cm_0 = sum rho_i y_i in one pass (the y_s[k >= 1] are in place)
   LF_HIP(c, lfk::y0_cm0(b->acc_cm, cm_i, b->y[0], b->y[1], b->rho, kappa, d, lbs, K, b->cm0, c->cur));
-  lfk::VecPtrs fx{};
-  for (int s = 0; s < 2; s++)
-    for (int k = 0; k < K; k++) fx.p[s * K + k] = b->fk[s] + (size_t)k * N * d;
-  {
+  if (c->fold_from_frag) {  // the planes are only in the operand rows (fold_commit)
+    PhaseTimer pt(c, LF_PHASE_FOLD);
+    LF_HIP(c, lfk::fold_frag(c->frag, aj->geom, c->fold_rows, b->rho, d, N, b->f0, c->cur));
+  } else {
+    lfk::VecPtrs fx{};
+    for (int s = 0; s < 2; s++)
+      for (int k = 0; k < K; k++) fx.p[s * K + k] = b->fk[s] + (size_t)k * N * d;
     PhaseTimer pt(c, LF_PHASE_FOLD);
     LF_HIP(c, lfk::fold(b->rho, fx, 2 * K, N, d, b->f0, c->cur));
   }

@@ -314,6 +314,20 @@ def test_dev_fold_step_matches_oracle(ctx, d, W, kappa):
     check_dev_fold_step(ctx, d, W, kappa)
 
 
+@pytest.mark.parametrize("W", [2, 37, 130])
+def test_dev_fold_step_without_fk(ctx, W):
+    """f_k buffers omitted (the fused X^1024+1 path): the planes exist only as
+    MFMA operand rows, plane 0 of each side in rows 29 and 30, and f_0 is folded
+    from them (k_fold_frag); every other output equals the oracle's"""
+    check_dev_fold_step(ctx, 1024, W, 2, keep_fk=False)
+    check_dev_fold_step(ctx, 1024, W, 2, steps=2, keep_fk=False)
+
+
+def test_dev_fold_step_without_fk_unfused_is_an_error(ctx):
+    with pytest.raises(LA.LfError):
+        check_dev_fold_step(ctx, 24, 10, 3, keep_fk=False)
+
+
 def test_dev_fold_step_gathering_contraction(ctx, monkeypatch):
     """LATTICEUM_AMD_AJTAI_FV=1: the decomposition writes no operand rows and the
     contraction gathers the planes from f_k (k_ajtai_mfma_fv)"""
@@ -327,7 +341,7 @@ def test_dev_fold_step_repeated_in_place(ctx):
     check_dev_fold_step(ctx, 1024, 37, 2, steps=3)
 
 
-def check_dev_fold_step(ctx, d, W, kappa, steps=1):
+def check_dev_fold_step(ctx, d, W, kappa, steps=1, keep_fk=True):
     import torch
     pr = params(d)
     K, L = pr.K, pr.L
@@ -348,7 +362,8 @@ def check_dev_fold_step(ctx, d, W, kappa, steps=1):
     keep = {
         "w_ccs": dev(w_ccs), "acc_cm": dev(acc_cm), "acc_f_coeff": dev(acc_fc), "rho": dev(rho),
         "f_coeff": dev(n=N * d), "f": dev(n=N * d), "cm": dev(n=kappa * d),
-        "fk_coeff": [dev(n=K * N * d) for _ in range(2)], "fk": [dev(n=K * N * d) for _ in range(2)],
+        "fk_coeff": [dev(n=K * N * d) for _ in range(2)],
+        "fk": [dev(n=K * N * d) for _ in range(2)] if keep_fk else [None, None],
         "wk": [dev(n=K * W * d) for _ in range(2)], "y": [dev(n=K * kappa * d) for _ in range(2)],
         "f0": dev(n=N * d), "f0_coeff": dev(n=N * d), "w_ccs0": dev(n=W * d), "cm0": dev(n=kappa * d),
     }
@@ -356,7 +371,7 @@ def check_dev_fold_step(ctx, d, W, kappa, steps=1):
     for k, v in keep.items():
         if isinstance(v, list):
             for s in range(2):
-                getattr(b, k)[s] = v[s].data_ptr()
+                getattr(b, k)[s] = v[s].data_ptr() if v[s] is not None else None
         else:
             setattr(b, k, v.data_ptr())
     h = lambda t: t.cpu().numpy().view(np.uint64)
@@ -380,7 +395,8 @@ def check_fold_outputs(h, keep, A, kappa, d, pr, W, w_ccs, acc_cm, acc_fc, rho):
         assert np.array_equal(h(keep[key]), want[key]), key
     for s in range(2):
         assert np.array_equal(h(keep["fk_coeff"][s]), sides[s][0])
-        assert np.array_equal(h(keep["fk"][s]), sides[s][1])
+        if keep["fk"][s] is not None:
+            assert np.array_equal(h(keep["fk"][s]), sides[s][1])
         assert np.array_equal(h(keep["wk"][s]), sides[s][2])
 
 

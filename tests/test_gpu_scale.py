@@ -75,8 +75,21 @@ def check_workload(wl, seed_w, picks, cm_rows, y_rows):
     assert np.array_equal(host(keep["rho"]), rho)
     # y rows of both sides: the decomposition's own operand rows through the contraction
     y = [host(t).reshape(K, kappa, d) for t in keep["y"]]
+    fk_dev = keep["fk"]
+    if fk_dev[0] is None:
+        # the step kept its planes only as operand rows: decompose both sides
+        # again through the standalone entry (parity-tested on its own)
+        fk_dev = []
+        for s, src in ((0, keep["acc_f_coeff"]), (1, keep["f_coeff"])):
+            fck, fk, wk = (torch.empty(n, dtype=torch.int64, device=src.device) for n in (K * N * d, K * N * d,
+                                                                                          K * W * d))
+            wl.ctxs[0].dev_decompose_witness(pr, src, N, fck, fk, wk)
+            wl.ctxs[0].sync()
+            assert torch.equal(fck, keep["fk_coeff"][s]) and torch.equal(wk, keep["wk"][s]), f"side {s}"
+            del fck, wk
+            fk_dev.append(fk)
     for s, k, row in y_rows:
-        fk = host(keep["fk"][s][k * N * d:(k + 1) * N * d])
+        fk = host(fk_dev[s][k * N * d:(k + 1) * N * d])
         got = O.ajtai_rows_seeded(bench.SEED_A, N, d, fk, [row])
         assert np.array_equal(y[s][k, row], got), f"y side {s} k {k} row {row}"
     # y_0 = cm - sum 2^k y_k and cm_0 = sum rho_i y_i, recomputed from the device's y
@@ -96,7 +109,7 @@ def check_workload(wl, seed_w, picks, cm_rows, y_rows):
         sub = fc.reshape(N, d)[cols].ravel()
         ofck, ofk, owk = O.decompose_witness(sub, d, pr.B, L, pr.b_small, K)
         ofck, ofk, owk = ofck.reshape(K, -1, d), ofk.reshape(K, -1, d), owk.reshape(K, ng, d)
-        for name, got_t, want, idx in (("f_coeff_k", keep["fk_coeff"][s], ofck, cols), ("f_k", keep["fk"][s], ofk, cols),
+        for name, got_t, want, idx in (("f_coeff_k", keep["fk_coeff"][s], ofck, cols), ("f_k", fk_dev[s], ofk, cols),
                                        ("w_ccs_k", keep["wk"][s], owk, groups)):
             n_per = N if name != "w_ccs_k" else W
             g = got_t.view(K, n_per, d)[:, torch.from_numpy(idx).to(got_t.device)]
