@@ -6,6 +6,9 @@
 // independent sponge chain (one thread each); every tree level is one launch
 // of independent compressions.
 //
+// One permutation state spreads over 8 lanes (permute8_lane) in the tree
+// kernels; the batched permutation keeps one state per thread.
+//
 // Constants: the width-8 external rounds from the reference
 // (crypto_consts.rs:9-96), the 22 internal constants shared with width 16;
 // the internal diagonal is Plonky3's MATRIX_DIAG_8_GOLDILOCKS, which the
@@ -82,35 +85,76 @@ __global__ void __launch_bounds__(256) k_p2w8_permute(uint64_t *states, size_t n
   for (int i = 0; i < 8; i++) states[e * 8 + i] = s[i];
 }
 
-// leaf i = PaddingFreeSponge hash of row i: overwrite state[0..4) with the next
-// four words, permute; a partial last block is permuted too; no padding
-__global__ void __launch_bounds__(256) k_merkle_leaves(const uint64_t *rows, size_t nrows, size_t width,
-                                                      uint64_t *leaves) {
-  const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (e >= nrows) return;
-  const uint64_t *row = rows + e * width;
-  uint64_t s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  size_t pos = 0;
-  while (pos < width) {
-    const size_t take = width - pos < 4 ? width - pos : 4;
-    for (size_t i = 0; i < take; i++) s[i] = gl::canon(row[pos + i]);
-    pos += take;
-    permute8(s);
+// ---------------------------------------------------------------- one state over 8 lanes
+// A sponge chain is sequential, so a tree over P pages has only P independent
+// chains (8 MB of memory: 8192, an eighth of the chip's SIMDs at one lane
+// each). Here lane i of an 8-lane group holds state word i: the s-boxes of a
+// full round run in parallel, the MDS mixing and the partial rounds' sum use
+// cross-lane reads (ds_swizzle / bpermute), and 8x as many waves run.
+__device__ __forceinline__ uint64_t shfl64(uint64_t x, int src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)x, src), hi = (uint32_t)__shfl((int)(uint32_t)(x >> 32), src);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ __forceinline__ uint64_t shfl64_xor(uint64_t x, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, m), hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), m);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+// mds8 with word i in lane i of the group (lane = the thread's lane in the wave)
+__device__ __forceinline__ uint64_t mds8_lane(uint64_t x, int lane) {
+  const uint64_t s1 = gl::add(x, shfl64_xor(x, 1));
+  const uint64_t t = gl::add(s1, shfl64_xor(s1, 2));                 // the 4-chunk's sum
+  const uint64_t xn = shfl64(x, (lane & ~3) | ((lane + 1) & 3));     // x_(i+1 mod 4) of the chunk
+  const uint64_t y = gl::add(t, gl::add(x, gl::add(xn, xn)));
+  return gl::add(y, gl::add(y, shfl64_xor(y, 4)));                   // + the column sum over the two chunks
+}
+__device__ uint64_t permute8_lane(uint64_t x, int lane) {
+  const int i = lane & 7;
+  x = mds8_lane(x, lane);
+#pragma unroll 1
+  for (int r = 0; r < 4; r++) x = mds8_lane(sbox7(gl::add(x, W8_EXT_INIT[8 * r + i])), lane);
+  const uint64_t dg = W8_DIAG_M1[i];
+#pragma unroll 1
+  for (int r = 0; r < 22; r++) {
+    if (i == 0) x = sbox7(gl::add(x, W8_INTERNAL[r]));
+    uint64_t sum = gl::add(x, shfl64_xor(x, 1));
+    sum = gl::add(sum, shfl64_xor(sum, 2));
+    sum = gl::add(sum, shfl64_xor(sum, 4));
+    x = gl::add(gl::mul(x, dg), sum);
   }
-#pragma unroll
-  for (int i = 0; i < 4; i++) leaves[e * 4 + i] = s[i];
+#pragma unroll 1
+  for (int r = 0; r < 4; r++) x = mds8_lane(sbox7(gl::add(x, W8_EXT_TERM[8 * r + i])), lane);
+  return x;
 }
 
-// parent i = permute(child 2i || child 2i + 1)[0..4)
+// leaf e = PaddingFreeSponge hash of row e: overwrite state[0..4) with the next
+// four words, permute; a partial last block is permuted too; no padding. One
+// 8-lane group per row (groups past nrows run on a clamped row, store nothing:
+// every lane of a wave takes part in the cross-lane reads)
+__global__ void __launch_bounds__(256) k_merkle_leaves(const uint64_t *rows, size_t nrows, size_t width,
+                                                      uint64_t *leaves) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63, i = lane & 7;
+  const size_t e = t >> 3;
+  const bool ok = e < nrows;
+  const uint64_t *row = rows + (ok ? e : 0) * width;
+  uint64_t x = 0;
+  for (size_t pos = 0; pos < width; pos += 4) {
+    const size_t take = width - pos < 4 ? width - pos : 4;
+    if ((size_t)i < take) x = gl::canon(row[pos + i]);
+    x = permute8_lane(x, lane);
+  }
+  if (ok && i < 4) leaves[e * 4 + i] = x;
+}
+
+// parent e = permute(child 2e || child 2e + 1)[0..4): the 8 words are contiguous
 __global__ void __launch_bounds__(256) k_merkle_level(const uint64_t *children, size_t nparents, uint64_t *parents) {
-  const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (e >= nparents) return;
-  uint64_t s[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) s[i] = children[e * 8 + i];
-  permute8(s);
-#pragma unroll
-  for (int i = 0; i < 4; i++) parents[e * 4 + i] = s[i];
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63, i = lane & 7;
+  const size_t e = t >> 3;
+  const bool ok = e < nparents;
+  uint64_t x = children[(ok ? e : 0) * 8 + i];
+  x = permute8_lane(x, lane);
+  if (ok && i < 4) parents[e * 4 + i] = x;
 }
 
 unsigned nb(size_t n) { return (unsigned)((n + 255) / 256); }
@@ -125,10 +169,10 @@ hipError_t p2w8_permute(uint64_t *states, size_t n, hipStream_t st) {
 
 hipError_t merkle_tree(const uint64_t *rows, size_t nrows, size_t width, uint64_t *nodes, hipStream_t st) {
   if (!nrows || (nrows & (nrows - 1)) || !width) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_merkle_leaves, dim3(nb(nrows)), dim3(256), 0, st, rows, nrows, width, nodes);
+  hipLaunchKernelGGL(k_merkle_leaves, dim3(nb(8 * nrows)), dim3(256), 0, st, rows, nrows, width, nodes);
   size_t off = 0, n = nrows;
   while (n > 1) {
-    hipLaunchKernelGGL(k_merkle_level, dim3(nb(n / 2)), dim3(256), 0, st, nodes + 4 * off, n / 2,
+    hipLaunchKernelGGL(k_merkle_level, dim3(nb(8 * (n / 2))), dim3(256), 0, st, nodes + 4 * off, n / 2,
                        nodes + 4 * (off + n));
     off += n;
     n /= 2;
