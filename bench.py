@@ -93,6 +93,15 @@ def algorithmic_bytes(d, W, kappa, L=5, K=15):
     return step, alg, operand
 
 
+I8_DENSE_TOPS = 5000.0  # MI355X dense i8 MFMA peak (2x the dense bf16 2.5 PFLOP/s)
+
+
+def coeff_fold(d, layout, keep_fk):
+    """whether lf_dev_fold_step folds f_0 in coefficient form on the i8 matrix
+    cores (fold_coeff.hip): X^1024+1 after the fused decomposition, f_k kept"""
+    return d == 1024 and layout == 1 and keep_fk and os.environ.get("LATTICEUM_AMD_FOLD") != "slot"
+
+
 def kernel_names(LA, d, W, layout, keep_fk=True):
     """the kernel each lf_dev_fold_step phase launches (for the rocprof / PMC joins)"""
     if d == 24:
@@ -101,10 +110,12 @@ def kernel_names(LA, d, W, layout, keep_fk=True):
                 "to_frag": "k_to_frag<true, true, true>"}
     if d == 1024:
         small = W < LA.witness_split_w()  # one half-wave per (element, limb) below this W
+        cf = coeff_fold(d, layout, keep_fk)
         return {"decompose": "k_decompose_fused", "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_nega",
-                "fold": "k_fold_nega" if keep_fk else "k_fold_frag",
+                "fold": "k_fold_coeff" if cf else "k_fold_nega" if keep_fk else "k_fold_frag",
                 "from_w_ccs": "k_from_w_ccs_split" if small else "k_from_w_ccs_n32",
-                "from_f": "k_from_f_split" if small else "k_from_f_n32", "to_frag": "k_to_frag<true, false, true>"}
+                "from_f": "k_from_fcoeff_n32" if cf else "k_from_f_split" if small else "k_from_f_n32",
+                "to_frag": "k_to_frag<true, false, true>"}
     if d == 4096:
         return {"decompose": "k_decompose_n4k_fused" if layout == 1 else "k_decompose_n4k",
                 "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_nega",
@@ -134,7 +145,7 @@ def load_traffic(d, W, kappa):
         if base != k and base not in t and sum(x.split("<")[0] == base for x in t) == 1:
             t[base] = t[k]
     for dec, pack in (("k_decompose_fused", "k_pack_sm"), ("k_decompose_n4k_fused", "k_pack_sm4"),
-                      ("k_decompose_n4k", "k_pack_sm4")):
+                      ("k_decompose_n4k", "k_pack_sm4"), ("k_fold_coeff", "k_pack_keys")):
         if dec in t and pack in t:  # the decompose phase launches both
             t[dec] += t[pack]
     return t
@@ -361,6 +372,9 @@ def phase_report(LA, wl, tot, steps):
         # the decomposition covers both sides of a step in one launch or one per launch
         sides = max(1, round(2 * steps / cnt)) if ph == "decompose" else 1
         a = alg[ph] * sides
+        cf = ph == "fold" and kernel_of[ph] == "k_fold_coeff"
+        if cf:  # the coefficient-form fold never reads the 2K NTT-form planes (B4): count what it moves
+            a = wl.N * (2 * 2048 + 2 * 2 * wl.pr.K * 256 + 8 * 1024)  # packed digits in, keys out + in, f0_coeff out
         gbs = a / (avg * 1e-3) / 1e9
         extra = operand.get(ph, 0) * sides
         phases[ph] = {"kernel": kernel_of[ph], "avg_launch_ms": avg, "launches_per_step": cnt / steps,
@@ -369,6 +383,16 @@ def phase_report(LA, wl, tot, steps):
                       "operand_bytes_per_launch": extra,
                       "achieved_gbs_incl_operands": (a + extra) / (avg * 1e-3) / 1e9,
                       "traffic_bytes_per_launch": traffic.get(kernel_of[ph])}
+        if cf:
+            # an exact i8 GEMM: 1024 coefficients x 2K 1024 digit rows x N elements
+            macs = 1024 * 2 * wl.pr.K * 1024 * wl.N
+            tops = 2 * macs / (avg * 1e-3) / 1e12
+            phases[ph]["coefficient_form"] = {
+                "bound": "mfma", "i8_macs": macs, "achieved_tops": tops, "peak_tops": I8_DENSE_TOPS,
+                "frac_mfma": tops / I8_DENSE_TOPS, "survey_b4_bytes": alg[ph],
+                "note": "f_0 = NTT(sum_i rho_i * D_i) from the digit planes D_i on the i8 matrix cores "
+                        "(fold_coeff.hip, with the digit-key packing in the same phase); "
+                        "algorithmic_bytes_per_launch is what it moves, SURVEY B4 would read the 2K NTT-form planes"}
     if not phases:
         return phases, None
     dom = max(phases, key=lambda k: phases[k]["ms_per_step"])

@@ -1,0 +1,267 @@
+// fold_coeff.hip -- f_0 = sum_i rho_i f_i (LF/nifs/folding.rs:258-268) for X^1024 + 1,
+// in coefficient form on the i8 matrix cores.
+//
+// The 2K folded witnesses are the balanced digit planes of the two decomposed
+// sides, f_i = NTT(D_i) with D_i in {-1, 0, 1}^1024 (b_small = 2), and the
+// folding challenges are short: rho_i has coefficients in [-32, 32)
+// (cyclotomic-rings rings/goldilocks.rs:41-67, get_rhos in folding/utils.rs:116-127).
+// The NTT is a ring isomorphism, so f_0 = NTT(sum_i rho_i * D_i), * the
+// negacyclic product, and
+//   f0_coeff[c][e] = sum_i sum_j R_i[c][j] D_i[j][e],
+//   R_i[c][j] = rho_i[c - j] (c >= j),  -rho_i[c - j + 1024] (c < j),
+// an exact integer GEMM of i8 operands (|f0_coeff| <= 2K 1024 32 < 2^31):
+// M = 1024 coefficients, N = elements, K = 2K x 1024. Canonicalised, it is
+// Witness::from_f's f_coeff itself; f_0 and w_ccs follow from one forward
+// transform per element (k_from_fcoeff_n32). Instead of the 2K NTT-form planes
+// (E 2K N = 20 GB at W = 2^14) the fold reads one key byte per coefficient quad
+// and plane (0.6 GB).
+//
+// R_i is Toeplitz: the 32 x 32 A tile of rows 32t.. and columns 32q.. depends
+// only on t - q. A wave owns 8 row tiles; stepping q by one shifts its 8 tiles
+// one diagonal, so it keeps them in an 8-slot register window and loads one new
+// tile per 32-column step (16 bytes at a lane-dependent byte offset of the
+// reversed table, assembled from 5 LDS dwords with v_alignbyte). The B operand
+// (16 digits of one element) comes from 4 key bytes through a 256-entry LDS
+// table: key = 4 magnitude bits | 4 sign bits -> the quad's 4 digit bytes.
+//
+// Used only when every rho_i has coefficients in [-127, 127] (k_rho_tab checks
+// on the device); otherwise the flag it raises makes these kernels return at
+// once and the NTT-form fold and Witness::from_f run instead (the same flag,
+// the other way round), with no host synchronisation.
+#include "digits.hpp"
+#include "frag.hpp"
+#include "kernels.hpp"
+
+namespace lfk {
+
+namespace {
+constexpr int FD = 1024;
+constexpr int FC_KEYROW = 64;  // u32 per (element, plane): 256 key bytes
+
+// bit b of x (b < 8) -> bit 4b
+__device__ __forceinline__ uint32_t spread8(uint32_t x) {
+  x &= 0xFFu;
+  x = (x | (x << 12)) & 0x000F000Fu;
+  x = (x | (x << 6)) & 0x03030303u;
+  x = (x | (x << 3)) & 0x11111111u;
+  return x;
+}
+
+// keys[(col K + k) 64 + h 32 + q] byte i = key of quad p = 8q + 4h + i (its
+// coefficients 4p .. 4p + 3) in plane k: bit m = bit k of |x_(4p+m)|, bit 4 + m
+// = its sign. From the fused decomposition's packed coefficients
+// (k_pack_sm: smg[(col 16 + qq) 32 + rr] = sm(x[rr + 64 qq]) | sm(x[rr + 64 qq + 32]) << 16,
+// sm = 15-bit magnitude | sign << 15). One thread per (col, h, 4 consecutive q):
+// 128 B in, one 16-B row piece per plane out.
+__global__ void __launch_bounds__(256) k_pack_keys(const uint32_t *smg, size_t ncol, int K, uint32_t *keys) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t >= ncol * 16) return;
+  const size_t col = t >> 4;
+  const int h = (int)(t >> 3) & 1, q0 = 4 * (int)(t & 7);
+  // coefficient j = 32 q + 16 h + 4 i + m sits in word (qq = q / 2, rr = 16 h + 4 i + m), half q & 1
+  uint32_t w[2][16];
+#pragma unroll
+  for (int a = 0; a < 2; a++) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(smg + col * 512 + (q0 / 2 + a) * 32 + 16 * h);
+#pragma unroll
+    for (int v = 0; v < 4; v++) {
+      const uint4 x = src[v];
+      w[a][4 * v] = x.x;
+      w[a][4 * v + 1] = x.y;
+      w[a][4 * v + 2] = x.z;
+      w[a][4 * v + 3] = x.w;
+    }
+  }
+  // per quad: planes 0..7 (lo) and 8..15 (hi, plane 15 = the sign) bit-sliced, bit 4 (k % 8) + m
+  uint32_t lo[16], hi[16];
+#pragma unroll
+  for (int qd = 0; qd < 4; qd++)
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      uint32_t L = 0, H = 0;
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        const uint32_t v = w[qd >> 1][4 * i + m] >> (16 * (qd & 1));
+        L |= spread8(v) << m;
+        H |= spread8(v >> 8) << m;
+      }
+      lo[4 * qd + i] = L;
+      hi[4 * qd + i] = H;
+    }
+  uint4 *dst = reinterpret_cast<uint4 *>(keys + col * K * FC_KEYROW + 32 * h + q0);
+  for (int k = 0; k < K; k++) {
+    uint32_t o[4];
+#pragma unroll
+    for (int qd = 0; qd < 4; qd++) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int u = 4 * qd + i;
+        const uint32_t nib = (k < 8 ? lo[u] >> (4 * k) : hi[u] >> (4 * (k - 8))) & 0xFu;
+        x |= (nib | ((hi[u] >> 28) << 4)) << (8 * i);
+      }
+      o[qd] = x;
+    }
+    dst[k * (FC_KEYROW / 4)] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// block i: the reversed table of rho_i (coefficient form, canonical) as bytes,
+// tab[i][u + 1024] = rho_i[-u] (-1023 <= u <= 0), -rho_i[1024 - u] (1 <= u <= 1023), else 0;
+// *bad = 1 if a coefficient is outside [-127, 127]
+__global__ void __launch_bounds__(256) k_rho_tab(const uint64_t *rc, uint8_t *tab, int *bad) {
+  const uint64_t *r = rc + (size_t)blockIdx.x * FD;
+  uint32_t *tb = reinterpret_cast<uint32_t *>(tab + (size_t)blockIdx.x * FOLD_RT);
+  for (int o4 = threadIdx.x; o4 < FOLD_RT / 4; o4 += blockDim.x) {
+    uint32_t wv = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const int u = 4 * o4 + b - 1024;
+      int64_t v = 0;
+      if (u <= 0 && u >= -1023)
+        v = signed_rep(r[-u]);
+      else if (u >= 1 && u <= 1023)
+        v = -signed_rep(r[1024 - u]);
+      wv |= (uint32_t)(uint8_t)(int8_t)v << (8 * b);
+    }
+    tb[o4] = wv;
+  }
+  bool out = false;
+  for (int j = threadIdx.x; j < FD; j += blockDim.x) {
+    const int64_t s = signed_rep(r[j]);
+    out |= s > 127 || s < -127;
+  }
+  if (out) raise(bad, 1);
+}
+
+// 16 bytes of a rho table at byte offset o (any alignment): 5 dwords, v_alignbyte
+__device__ __forceinline__ v4i tile_a(const uint8_t *ri, int o, int sh) {
+  const uint32_t *p = reinterpret_cast<const uint32_t *>(ri + (o & ~3));
+  const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], d4 = p[4];
+  v4i a;
+  a[0] = (int)__builtin_amdgcn_alignbyte(d1, d0, sh);
+  a[1] = (int)__builtin_amdgcn_alignbyte(d2, d1, sh);
+  a[2] = (int)__builtin_amdgcn_alignbyte(d3, d2, sh);
+  a[3] = (int)__builtin_amdgcn_alignbyte(d4, d3, sh);
+  return a;
+}
+
+constexpr int FC_MAXW = 30;  // 2K <= 30
+// A block (4 waves) owns 32 elements (MFMA columns) at a time; wave w the rows
+// 256 w .. 256 w + 255 (row tiles t = 8 w + tt). Grid-stride over element tiles.
+__global__ void __launch_bounds__(256, 2) k_fold_coeff(const uint32_t *keys, const uint8_t *tab_g, const int *bad,
+                                                      size_t N, int K, uint64_t *f0c) {
+  __shared__ __attribute__((aligned(16))) uint8_t rt[FC_MAXW * FOLD_RT];
+  __shared__ uint32_t lut[256];
+  if (*bad) return;  // rho not short: the NTT-form fold runs instead
+  const int nw = 2 * K, tid = threadIdx.x;
+  for (int x = tid; x < nw * FOLD_RT / 16; x += blockDim.x)
+    reinterpret_cast<uint4 *>(rt)[x] = reinterpret_cast<const uint4 *>(tab_g)[x];
+  {
+    const uint32_t m = tid & 15, s = tid >> 4;
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if ((m >> i) & 1) v |= ((s >> i) & 1 ? 0xFFu : 0x01u) << (8 * i);
+    lut[tid] = v;
+  }
+  __syncthreads();
+  const int lane = tid & 63, wv = tid >> 6, col = lane & 31, h = lane >> 5;
+  const int sh = (-col) & 3;
+  // A tile of diagonal dl = t - q for this lane: bytes o .. o + 15, o = obase - 32 dl
+  const int obase = 1024 + 16 * h - col;
+  const size_t ntile = (N + 31) / 32;
+  for (size_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+    const size_t e = tile * 32 + col, ee = e < N ? e : N - 1;
+    const uint32_t *kb0 = keys + ee * K * FC_KEYROW + 32 * h, *kb1 = keys + (N + ee) * K * FC_KEYROW + 32 * h;
+    v16i acc[8];
+#pragma unroll
+    for (int tt = 0; tt < 8; tt++)
+#pragma unroll
+      for (int i = 0; i < 16; i++) acc[tt][i] = 0;
+    v4i A[8];
+    // the key words of (plane i, q block qb): 8 dwords, one block ahead
+    auto kaddr = [&](int iq) {
+      const int i = iq >> 2, s = i >= K;
+      return (s ? kb1 : kb0) + (i - s * K) * FC_KEYROW + 8 * (iq & 3);
+    };
+    uint4 kn0, kn1;
+    {
+      const uint4 *p = reinterpret_cast<const uint4 *>(kaddr(0));
+      kn0 = p[0];
+      kn1 = p[1];
+    }
+    for (int iq = 0; iq < 4 * nw; iq++) {
+      const int i = iq >> 2;
+      const uint8_t *ri = rt + i * FOLD_RT;
+      if ((iq & 3) == 0) {  // a new plane: slots 1..7 take diagonals 8 w + 1 .. 8 w + 7
+#pragma unroll
+        for (int tt = 1; tt < 8; tt++) A[tt] = tile_a(ri, obase - 32 * (8 * wv + tt), sh);
+      }
+      const uint32_t kw[8] = {kn0.x, kn0.y, kn0.z, kn0.w, kn1.x, kn1.y, kn1.z, kn1.w};
+      {
+        const uint4 *p = reinterpret_cast<const uint4 *>(kaddr(iq + 1 < 4 * nw ? iq + 1 : iq));
+        kn0 = p[0];
+        kn1 = p[1];
+      }
+      const int q0 = 8 * (iq & 3);
+#pragma unroll
+      for (int qi = 0; qi < 8; qi++) {
+        // slot (tt - q) & 7 holds diagonal 8 w + tt - q; the new one (tt = 0) goes to slot (-q) & 7
+        A[(8 - qi) & 7] = tile_a(ri, obase - 32 * (8 * wv - (q0 + qi)), sh);
+        v4i b;
+        b[0] = (int)lut[kw[qi] & 0xFF];
+        b[1] = (int)lut[(kw[qi] >> 8) & 0xFF];
+        b[2] = (int)lut[(kw[qi] >> 16) & 0xFF];
+        b[3] = (int)lut[kw[qi] >> 24];
+#pragma unroll
+        for (int tt = 0; tt < 8; tt++)
+          acc[tt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[(tt - qi) & 7], b, acc[tt], 0, 0, 0);
+      }
+    }
+    if (e < N) {
+      // lane (col, h), acc[tt][4 g + r]: row 32 (8 w + tt) + 8 g + 4 h + r of element e
+      uint64_t *out = f0c + e * FD + 256 * wv + 4 * h;
+      auto fe = [](int x) { return x < 0 ? (uint64_t)(int64_t)x + gl::P : (uint64_t)x; };
+#pragma unroll
+      for (int tt = 0; tt < 8; tt++)
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+          ulonglong2 *o = reinterpret_cast<ulonglong2 *>(out + 32 * tt + 8 * g);
+          o[0] = make_ulonglong2(fe(acc[tt][4 * g]), fe(acc[tt][4 * g + 1]));
+          o[1] = make_ulonglong2(fe(acc[tt][4 * g + 2]), fe(acc[tt][4 * g + 3]));
+        }
+    }
+  }
+}
+}  // namespace
+
+hipError_t fold_keys(const uint32_t *smg, size_t ncol, int K, uint32_t *keys, hipStream_t st) {
+  if (K < 1 || K > 15) return hipErrorInvalidValue;
+  if (!ncol) return hipSuccess;
+  hipLaunchKernelGGL(k_pack_keys, dim3((unsigned)((ncol * 16 + 255) / 256)), dim3(256), 0, st, smg, ncol, K, keys);
+  return hipGetLastError();
+}
+
+hipError_t fold_rho_tables(const uint64_t *rho, int nw, uint64_t *rc, uint8_t *tab, int *bad,
+                           const ring::NegaTables &inv, hipStream_t st) {
+  if (nw < 1 || nw > FC_MAXW || !inv.mid) return hipErrorInvalidValue;
+  hipError_t e = hipMemcpyAsync(rc, rho, (size_t)nw * FD * 8, hipMemcpyDeviceToDevice, st);
+  if (e == hipSuccess) e = hipMemsetAsync(bad, 0, sizeof(int), st);
+  if (e == hipSuccess) e = transform_n32(rc, nw, false, inv, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_rho_tab, dim3(nw), dim3(256), 0, st, rc, tab, bad);
+  return hipGetLastError();
+}
+
+hipError_t fold_coeff(const uint32_t *keys, const uint8_t *tab, const int *bad, size_t N, int K, uint64_t *f0c,
+                      int ncu, hipStream_t st) {
+  if (K < 1 || 2 * K > FC_MAXW || ncu < 1) return hipErrorInvalidValue;
+  if (!N) return hipSuccess;
+  const size_t ntile = (N + 31) / 32, cap = 2 * (size_t)ncu;  // two blocks per CU (LDS 63 KB, 256 registers)
+  hipLaunchKernelGGL(k_fold_coeff, dim3((unsigned)(ntile < cap ? ntile : cap)), dim3(256), 0, st, keys, tab, bad, N,
+                     K, f0c);
+  return hipGetLastError();
+}
+
+}  // namespace lfk

@@ -723,10 +723,13 @@ __global__ void __launch_bounds__(256) k_y0_cm0_phi72(const uint64_t *cm0s, cons
 // LF/nifs/folding.rs:258-268 (f_0) and folding/utils.rs:470-476 (cm_0):
 //   out[j] = sum_i rho_i (.) x_i[j]
 // two adjacent slots per thread (16-B streaming loads; d is even)
+// run_if: when given, nothing to do unless *run_if != 0 (the fallback of the
+// coefficient-form fold, fold_coeff.hip; its launch is then grid-capped and strides)
 __global__ void __launch_bounds__(256) k_fold_nega(const uint64_t *rho, VecPtrs x, int nwit, size_t n,
-                                                  int d, uint64_t *out) {
-  const size_t c = 2 * (blockIdx.x * (size_t)blockDim.x + threadIdx.x);
-  if (c >= n * (size_t)d) return;
+                                                  int d, uint64_t *out, const int *run_if) {
+  if (run_if && !*run_if) return;
+  for (size_t c = 2 * (blockIdx.x * (size_t)blockDim.x + threadIdx.x); c < n * (size_t)d;
+       c += 2 * (size_t)gridDim.x * blockDim.x) {
   const int s = c % d;
   gl::CAcc a0, a1;
   gl::cacc_zero(a0);
@@ -753,6 +756,7 @@ __global__ void __launch_bounds__(256) k_fold_nega(const uint64_t *rho, VecPtrs 
     gl::cacc_mad(a1, r.y, v.y);
   }
   *reinterpret_cast<ulonglong2 *>(out + c) = make_ulonglong2(gl::cacc_reduce(a0), gl::cacc_reduce(a1));
+  }
 }
 __global__ void __launch_bounds__(256) k_fold_phi72(const uint64_t *rho, VecPtrs x, int nwit, size_t n,
                                                    uint64_t *out) {
@@ -995,10 +999,11 @@ hipError_t from_w_ccs(const uint64_t *w_ccs, size_t W, int d, int lb, int L, uin
 }
 
 hipError_t from_f(const uint64_t *f, size_t N, int d, int lb, int L, uint64_t *f_coeff,
-                  uint64_t *w_ccs, const ring::NegaTables &inv, hipStream_t st) {
+                  uint64_t *w_ccs, const ring::NegaTables &inv, hipStream_t st, const int *run_if) {
   const size_t W = N / L;
   if (W == 0) return hipSuccess;
-  if (d == 1024 && inv.mid) return from_f_n32(f, W, lb, L, f_coeff, w_ccs, inv, st);
+  if (d == 1024 && inv.mid) return from_f_n32(f, W, lb, L, f_coeff, w_ccs, inv, st, run_if);
+  if (run_if) return hipErrorInvalidValue;
   if (d == 4096 && inv.tw4) return from_f_n4k(f, W, lb, L, f_coeff, w_ccs, inv, st);
   if (d == 24) {
     if (L < 1 || L > 256) return hipErrorInvalidValue;
@@ -1162,13 +1167,16 @@ hipError_t commit_y0(const uint64_t *cm, uint64_t *y, size_t kappa, int d, int l
 }
 
 hipError_t fold(const uint64_t *rho, const VecPtrs &x, int nwit, size_t n, int d, uint64_t *out,
-                hipStream_t st) {
+                hipStream_t st, const int *run_if) {
   if (n == 0) return hipSuccess;
-  if (nwit <= 0 || nwit > LF_MAX_VECS) return hipErrorInvalidValue;
-  if (d == 24)
+  if (nwit <= 0 || nwit > LF_MAX_VECS || (run_if && d == 24)) return hipErrorInvalidValue;
+  if (d == 24) {
     hipLaunchKernelGGL(k_fold_phi72, dim3(blocks(n * 8, 256)), dim3(256), 0, st, rho, x, nwit, n, out);
-  else
-    hipLaunchKernelGGL(k_fold_nega, dim3(blocks(n * d / 2, 256)), dim3(256), 0, st, rho, x, nwit, n, d, out);
+  } else {
+    unsigned nb = blocks(n * d / 2, 256);
+    if (run_if && nb > 8192) nb = 8192;  // usually returns at once: do not launch a block per 512 slots
+    hipLaunchKernelGGL(k_fold_nega, dim3(nb), dim3(256), 0, st, rho, x, nwit, n, d, out, run_if);
+  }
   return hipGetLastError();
 }
 

@@ -28,8 +28,10 @@ hipError_t mont(uint64_t *x, size_t n, bool to, hipStream_t st);
 hipError_t from_w_ccs(const uint64_t *w_ccs, size_t W, int d, int lb, int L, uint64_t *f_coeff,
                       uint64_t *f, const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err,
                       hipStream_t st);
+// run_if (X^1024 + 1 only): when given, the kernels do nothing unless *run_if != 0
+// (the fallbacks of the coefficient-form fold, fold_coeff.hip)
 hipError_t from_f(const uint64_t *f, size_t N, int d, int lb, int L, uint64_t *f_coeff,
-                  uint64_t *w_ccs, const ring::NegaTables &inv, hipStream_t st);
+                  uint64_t *w_ccs, const ring::NegaTables &inv, hipStream_t st, const int *run_if = nullptr);
 // d = 24 with frag: planes 1..K-1 also written as i8-MFMA operand rows row0.. (Lp = L order, nch chunks)
 hipError_t decompose_witness(const uint64_t *f_coeff, size_t N, int d, int lb, int L, int lbs, int K,
                              uint64_t *f_coeff_k, uint64_t *f_k, uint64_t *w_ccs_k,
@@ -43,7 +45,7 @@ hipError_t ajtai_commit(const uint64_t *A, size_t kappa, size_t ncols, int d, co
 hipError_t commit_y0(const uint64_t *cm, uint64_t *y, size_t kappa, int d, int lbs, int K,
                      hipStream_t st);
 hipError_t fold(const uint64_t *rho, const VecPtrs &x, int nwit, size_t n, int d, uint64_t *out,
-                hipStream_t st);
+                hipStream_t st, const int *run_if = nullptr);
 hipError_t p2_permute(uint64_t *states, size_t n, hipStream_t st);
 hipError_t fill_uniform(uint64_t *out, size_t n, uint64_t seed, hipStream_t st);
 hipError_t modp_sum(const uint64_t *in, int nparts, size_t len, uint64_t *out, hipStream_t st);
@@ -100,7 +102,7 @@ hipError_t transform_n32(uint64_t *data, size_t n, bool fwd, const ring::NegaTab
 hipError_t from_w_ccs_n32(const uint64_t *w_ccs, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *f,
                           const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err, hipStream_t st);
 hipError_t from_f_n32(const uint64_t *f, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *w_ccs,
-                      const ring::NegaTables &inv, hipStream_t st);
+                      const ring::NegaTables &inv, hipStream_t st, const int *run_if = nullptr);
 hipError_t decompose_n32(const uint64_t *f_coeff, size_t N, int lb, int L, int K, uint64_t *f_coeff_k,
                          uint64_t *f_k, uint64_t *w_ccs_k, const ring::NegaTables &fwd, int *err,
                          hipStream_t st);
@@ -127,6 +129,21 @@ hipError_t fold_frag(const uint4 *frag, const FragGeom &g, const FoldRows &fr, c
 hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K, uint32_t *smg,
                            const ring::NegaTables &fwd, uint4 *frag, int nch, int *err, uint64_t *sink, int ncu,
                            hipStream_t st);
+
+// f_0 in coefficient form on the i8 matrix cores (fold_coeff.hip), X^1024 + 1, b_small = 2:
+// keys [ncol = nside N][K][64] u32 from decompose_fused's packed coefficients (smg);
+// rho (nw = 2K NTT elements) -> rc (nw 1024 u64 scratch, its coefficients) -> tab
+// [nw][FOLD_RT] bytes, *bad = 1 if a coefficient is outside [-127, 127];
+// fold_coeff writes f0c = the canonical coefficients of sum_i rho_i f_i unless *bad
+constexpr int FOLD_RT = 2080;
+hipError_t fold_keys(const uint32_t *smg, size_t ncol, int K, uint32_t *keys, hipStream_t st);
+hipError_t fold_rho_tables(const uint64_t *rho, int nw, uint64_t *rc, uint8_t *tab, int *bad,
+                           const ring::NegaTables &inv, hipStream_t st);
+hipError_t fold_coeff(const uint32_t *keys, const uint8_t *tab, const int *bad, size_t N, int K, uint64_t *f0c,
+                      int ncu, hipStream_t st);
+// Witness::from_f given f's coefficients: f = NTT(f_coeff), w_ccs = recompose(f); gate: as fold_coeff
+hipError_t from_fcoeff_n32(const uint64_t *f_coeff, size_t W, int lb, int L, uint64_t *f, uint64_t *w_ccs,
+                           const ring::NegaTables &fwd, const int *gate, hipStream_t st);
 
 // d = 24: both sides of a fold step in one launch (blockIdx.z = side); frag as decompose_witness
 hipError_t decompose_phi72_sides(const FusedSides &sd, size_t N, int lb, int L, int lbs, int K, int *err,

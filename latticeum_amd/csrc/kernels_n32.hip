@@ -131,7 +131,9 @@ __global__ void __launch_bounds__(256, 2) k_from_w_ccs_n32(const uint64_t *w_ccs
 // ---------------------------------------------------------------- Witness::from_f
 // LF/arith.rs:299-313: f_coeff = ICRT(f), w_ccs = recompose(f) in slot form; one half-wave per group
 __global__ void __launch_bounds__(256) k_from_f_n32(const uint64_t *f, size_t W, int lb, int L,
-                                                   uint64_t *f_coeff, uint64_t *w_ccs, const uint64_t *mid_ig) {
+                                                   uint64_t *f_coeff, uint64_t *w_ccs, const uint64_t *mid_ig,
+                                                   const int *run_if) {
+  if (run_if && !*run_if) return;  // uniform: the coefficient-form fold produced f_coeff
   __shared__ uint64_t lds_all[WPB * n32::WAVE_U64];
   __shared__ uint64_t mid_i[n32::MID_U64];
   n32::stage_mid(mid_i, mid_ig);
@@ -170,6 +172,52 @@ __global__ void __launch_bounds__(256) k_from_f_n32(const uint64_t *f, size_t W,
       uint64_t *ow = w_ccs + g * D + x.r;
 #pragma unroll
       for (int k = 0; k < 32; k++) ow[32 * k] = acc[k];
+    }
+  }
+}
+
+// Witness::from_f when f_0 was folded in coefficient form (fold_coeff.hip): the
+// coefficients are the input, f = NTT(f_coeff) and w_ccs = recompose(f) in slot
+// form; one half-wave per group. gate: nothing to do when *gate != 0 (rho was
+// not short, the NTT-form fold and from_f ran instead)
+__global__ void __launch_bounds__(256, 2) k_from_fcoeff_n32(const uint64_t *f_coeff, size_t W, int lb, int L,
+                                                        uint64_t *f, uint64_t *w_ccs, const uint64_t *mid_fg,
+                                                        const int *gate) {
+  if (gate && *gate) return;
+  __shared__ uint64_t lds_all[WPB * n32::WAVE_U64];
+  __shared__ uint64_t mid_f[n32::MID_U64];
+  n32::stage_mid(mid_f, mid_fg);
+  __syncthreads();
+  Half x = half_ctx(lds_all);
+  const uint64_t b_pow = gl::mul_pow2(1, lb);  // B = 2^lb
+  for (size_t g = x.unit; g < pair_bound(W); g += x.stride) {
+    const bool ok = g < W;
+    const size_t gg = ok ? g : 0;
+    uint64_t acc[32];
+    for (int l = L - 1; l >= 0; l--) {
+      uint64_t v[32];
+      load_row32(f_coeff + (gg * L + l) * D + x.r, v);
+      n32::forward(v, mid_f, x.lds, x.r);  // v[i] = X[r + 32 brv5(i)]
+      if (l == L - 1) {
+#pragma unroll
+        for (int i = 0; i < 32; i++) acc[i] = v[i];
+      } else if (lb == 15) {  // GoldiLocksDP B = 2^15: a shift instead of a product
+#pragma unroll
+        for (int i = 0; i < 32; i++) acc[i] = gl::add_weak(gl::shl_small_weak(acc[i], 15), v[i]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 32; i++) acc[i] = gl::add(gl::mul(acc[i], b_pow), v[i]);
+      }
+      if (ok) {
+        uint64_t *of = f + (g * L + l) * D + x.r;
+#pragma unroll
+        for (int i = 0; i < 32; i++) of[32 * n32::brv5(i)] = v[i];
+      }
+    }
+    if (ok) {
+      uint64_t *ow = w_ccs + g * D + x.r;
+#pragma unroll
+      for (int i = 0; i < 32; i++) ow[32 * n32::brv5(i)] = gl::canon(acc[i]);
     }
   }
 }
@@ -232,7 +280,9 @@ __global__ void __launch_bounds__(512) k_from_w_ccs_split(const uint64_t *w_ccs,
 // from_f: each unit inverts its own element; the limb-0 units also recompose
 // w_ccs = sum_l B^l f[jL + l] in slot form (Horner from the top limb)
 __global__ void __launch_bounds__(512) k_from_f_split(const uint64_t *f, size_t W, int lb, int L,
-                                                     uint64_t *f_coeff, uint64_t *w_ccs, const uint64_t *mid_ig) {
+                                                     uint64_t *f_coeff, uint64_t *w_ccs, const uint64_t *mid_ig,
+                                                     const int *run_if) {
+  if (run_if && !*run_if) return;  // uniform: the coefficient-form fold produced f_coeff
   __shared__ uint64_t lds_all[SPLIT_WPB * n32::WAVE_U64];
   __shared__ uint64_t mid_i[n32::MID_U64];
   n32::stage_mid(mid_i, mid_ig);
@@ -586,16 +636,24 @@ hipError_t from_w_ccs_n32(const uint64_t *w_ccs, size_t W, int lb, int L, uint64
   return hipGetLastError();
 }
 hipError_t from_f_n32(const uint64_t *f, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *w_ccs,
-                      const ring::NegaTables &inv, hipStream_t st) {
+                      const ring::NegaTables &inv, hipStream_t st, const int *run_if) {
   if (W < SPLIT_W) {
     const size_t units = ((W + 1) & ~(size_t)1) * L;
     hipLaunchKernelGGL(k_from_f_split, dim3((unsigned)((units + 2 * SPLIT_WPB - 1) / (2 * SPLIT_WPB))),
                        dim3(64 * SPLIT_WPB), 0, st, f, W, lb, L, f_coeff,
-                       w_ccs, inv.mid);
+                       w_ccs, inv.mid, run_if);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_from_f_n32, dim3(half_blocks(W, 4096)), dim3(256), 0, st, f, W, lb, L, f_coeff, w_ccs,
-                     inv.mid);
+                     inv.mid, run_if);
+  return hipGetLastError();
+}
+hipError_t from_fcoeff_n32(const uint64_t *f_coeff, size_t W, int lb, int L, uint64_t *f, uint64_t *w_ccs,
+                           const ring::NegaTables &fwd, const int *gate, hipStream_t st) {
+  if (!W) return hipSuccess;
+  if (!fwd.mid) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_from_fcoeff_n32, dim3(half_blocks(W, 4096)), dim3(256), 0, st, f_coeff, W, lb, L, f, w_ccs,
+                     fwd.mid, gate);
   return hipGetLastError();
 }
 hipError_t decompose_n32(const uint64_t *f_coeff, size_t N, int lb, int L, int K, uint64_t *f_coeff_k,

@@ -47,6 +47,11 @@ struct lf_ctx {
   size_t frag_elems = 0;
   uint32_t *smg = nullptr;      // packed coefficients for the fused decomposition
   size_t smg_elems = 0;
+  size_t smg_sides_n = 0;       // N when smg holds both sides of the last fused d = 1024 fold_commit, else 0
+  uint32_t *fkeys = nullptr;    // coefficient-form fold: digit keys [2 N][K][64] (fold_coeff.hip)
+  size_t fkeys_elems = 0;
+  uint64_t *faux = nullptr;     // coefficient-form fold: rho coefficients, byte tables, the not-short flag
+  size_t faux_elems = 0;
   uint64_t *sink = nullptr;     // 32 KiB row the fused decompositions store work past the end into
   int ncu = 0;                  // compute units of `device`
   uint64_t *stage = nullptr;    // sharded step: the partial commitments [nvec][kappa d]
@@ -388,6 +393,7 @@ int decompose_n4k_sides(lf_ctx *c, const Tables *t, int nside, const uint64_t *c
                         uint4 *frag = nullptr, int nch = 0, const int *row0 = nullptr) {
   // packed digits: one u64 per 4 coefficients, or (fused) one byte per 4 coefficients and plane
   LF_TRY(grow(c, c->smg, c->smg_elems, (size_t)nside * N * (frag ? (size_t)K * 256 : 2048)));
+  c->smg_sides_n = 0;
   lfk::FusedSides sd{};
   sd.nside = nside;
   for (int s = 0; s < nside; s++) {
@@ -466,6 +472,7 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       PhaseTimer pt(c, LF_PHASE_DECOMPOSE);  // both sides in one launch
       LF_HIP(c, lfk::decompose_fused(sd, N, lb, L, K, c->smg, t->fwd, fv ? nullptr : c->frag, aj->geom.nch, c->d_err,
                                      c->sink, c->ncu, c->cur));
+      c->smg_sides_n = N;  // fold_finish's coefficient-form fold reads the digits from here
     } else {
       lfk::FusedSides sd{};
       sd.nside = 2;
@@ -533,6 +540,12 @@ lfk::OutPtrs fold_dst(const lf_params *pr, const lf_fold_step_bufs *b, size_t kd
   return dst;
 }
 
+// LATTICEUM_AMD_FOLD=slot: always fold f_0 in NTT form (k_fold_nega), never in coefficient form
+bool coeff_fold_enabled() {
+  const char *e = getenv("LATTICEUM_AMD_FOLD");
+  return !(e && !strcmp(e, "slot"));
+}
+
 int fold_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lbs, size_t W,
                 const lf_fold_step_bufs *b, const uint64_t *cm_i) {
   const int d = pr->d, L = pr->L, K = pr->K;
@@ -541,6 +554,34 @@ int fold_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
   LF_TRY(get_tables(c, d, t));
   // y_0 of both sides and cm_0 = sum rho_i y_i in one pass (the y_s[k >= 1] are in place)
   LF_HIP(c, lfk::y0_cm0(b->acc_cm, cm_i, b->y[0], b->y[1], b->rho, kappa, d, lbs, K, b->cm0, c->cur));
+  // X^1024 + 1 after the fused decomposition: f_0 in coefficient form on the
+  // matrix cores from the digits (fold_coeff.hip), then f_0 and w_ccs by one
+  // forward transform per element. If a rho is not short the device flag `bad`
+  // turns those kernels off and the NTT-form fold and from_f on.
+  if (c->smg_sides_n == N && N && d == 1024 && lbs == 1 && K <= 15 && !c->fold_from_frag && t->fwd.mid &&
+      t->inv.mid && coeff_fold_enabled()) {
+    const int nw = 2 * K;
+    const size_t tab_u64 = ((size_t)nw * lfk::FOLD_RT + 7) / 8, aux = (size_t)nw * 1024 + tab_u64 + 1;
+    LF_TRY(grow(c, c->fkeys, c->fkeys_elems, 2 * N * (size_t)K * 64));
+    LF_TRY(grow(c, c->faux, c->faux_elems, aux));
+    uint64_t *rc = c->faux;
+    uint8_t *tab = reinterpret_cast<uint8_t *>(c->faux + (size_t)nw * 1024);
+    int *bad = reinterpret_cast<int *>(c->faux + aux - 1);
+    {
+      PhaseTimer pt(c, LF_PHASE_FOLD);
+      LF_HIP(c, lfk::fold_keys(c->smg, 2 * N, K, c->fkeys, c->cur));
+      LF_HIP(c, lfk::fold_rho_tables(b->rho, nw, rc, tab, bad, t->inv, c->cur));
+      LF_HIP(c, lfk::fold_coeff(c->fkeys, tab, bad, N, K, b->f0_coeff, c->ncu, c->cur));
+      lfk::VecPtrs fx{};
+      for (int s = 0; s < 2; s++)
+        for (int k = 0; k < K; k++) fx.p[s * K + k] = b->fk[s] + (size_t)k * N * d;
+      LF_HIP(c, lfk::fold(b->rho, fx, nw, N, d, b->f0, c->cur, bad));
+    }
+    PhaseTimer pt(c, LF_PHASE_FROM_F);
+    LF_HIP(c, lfk::from_fcoeff_n32(b->f0_coeff, W, lb, L, b->f0, b->w_ccs0, t->fwd, bad, c->cur));
+    LF_HIP(c, lfk::from_f(b->f0, N, d, lb, L, b->f0_coeff, b->w_ccs0, t->inv, c->cur, bad));
+    return LF_OK;
+  }
   if (c->fold_from_frag) {  // the planes are only in the operand rows (fold_commit)
     PhaseTimer pt(c, LF_PHASE_FOLD);
     LF_HIP(c, lfk::fold_frag(c->frag, aj->geom, c->fold_rows, b->rho, d, N, b->f0, c->cur));
@@ -686,6 +727,8 @@ void lf_ctx_destroy(lf_ctx *c) {
   if (c->ybuf) (void)hipFree(c->ybuf);
   if (c->frag) (void)hipFree(c->frag);
   if (c->smg) (void)hipFree(c->smg);
+  if (c->fkeys) (void)hipFree(c->fkeys);
+  if (c->faux) (void)hipFree(c->faux);
   if (c->sink) (void)hipFree(c->sink);
   if (c->stage) (void)hipFree(c->stage);
   if (c->limb) (void)hipFree(c->limb);

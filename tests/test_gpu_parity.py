@@ -335,13 +335,31 @@ def test_dev_fold_step_gathering_contraction(ctx, monkeypatch):
     check_dev_fold_step(ctx, 1024, 37, 2)
 
 
+def test_dev_fold_step_ntt_form_fold(ctx, monkeypatch):
+    """LATTICEUM_AMD_FOLD=slot: f_0 folded from the NTT-form planes (k_fold_nega)
+    instead of in coefficient form on the matrix cores (fold_coeff.hip)"""
+    monkeypatch.setenv("LATTICEUM_AMD_FOLD", "slot")
+    check_dev_fold_step(ctx, 1024, 37, 2)
+
+
+@pytest.mark.parametrize("W", [2, 7, 130])
+def test_dev_fold_step_rho_not_short(ctx, W):
+    """rho with full-size coefficients: the coefficient-form fold's device flag
+    turns it off and the NTT-form fold + from_f run instead (no host sync)"""
+    d, K = 1024, params(1024).K
+    rho = rand(2 * K * d, 4242 + W)
+    check_dev_fold_step(ctx, d, W, 2, rho=rho)
+    # and a short rho again on the same context: the flag is reset per step
+    check_dev_fold_step(ctx, d, W, 2)
+
+
 def test_dev_fold_step_repeated_in_place(ctx):
     # consecutive steps reuse every buffer (as bench.py and the proving loop do):
     # the fused fold must see each step's own f_k rows, never the previous step's
     check_dev_fold_step(ctx, 1024, 37, 2, steps=3)
 
 
-def check_dev_fold_step(ctx, d, W, kappa, steps=1, keep_fk=True):
+def check_dev_fold_step(ctx, d, W, kappa, steps=1, keep_fk=True, rho=None):
     import torch
     pr = params(d)
     K, L = pr.K, pr.L
@@ -352,7 +370,8 @@ def check_dev_fold_step(ctx, d, W, kappa, steps=1, keep_fk=True):
     w_ccs = rand(W * d, 1001 + d)
     acc_fc, acc_f = valid_f_coeff(d, W, 1002 + d)
     acc_cm = O.ajtai_commit(A, kappa, N, d, acc_f)
-    rho = make_rho(d, K, 1003 + d)
+    if rho is None:
+        rho = make_rho(d, K, 1003 + d)
 
     def dev(x=None, n=None):
         if x is not None:

@@ -31,7 +31,7 @@ def grid(r):
 
 
 def short(name):
-    n = name.split("(")[0]
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
     return n.replace("void ", "").strip()
 
 
