@@ -151,6 +151,23 @@ def load_traffic(d, W, kappa):
     return t
 
 
+def load_sq(d, W, kappa):
+    """PMC-measured VALU busy fraction per kernel (profiles/pmc_sq.json, written by
+    tools/prof_summary.py sq from one SQ pass of this configuration); {} otherwise."""
+    try:
+        doc = json.loads((ROOT / "profiles" / "pmc_sq.json").read_text())
+    except (OSError, ValueError):
+        return {}
+    if doc.get("config") != {"d": d, "W": W, "kappa": kappa}:
+        return {}
+    t = {k: v.get("valu_busy") for k, v in doc.get("kernels", {}).items()}
+    for k in list(t):
+        base = k.split("<")[0]
+        if base != k and base not in t and sum(x.split("<")[0] == base for x in t) == 1:
+            t[base] = t[k]
+    return t
+
+
 def host_cores():
     """CPUs this process may use: its affinity set, capped by a cgroup CPU quota
     (the GPU box shows the whole machine in os.cpu_count())"""
@@ -364,6 +381,7 @@ def phase_report(LA, wl, tot, steps):
         operand["decompose"] = 0
     kernel_of = kernel_names(LA, d, W, wl.sch.layout, wl.keep_fk)
     traffic = load_traffic(d, W, kappa)
+    valu = load_sq(d, W, kappa)
     phases = {}
     for ph, (ms, cnt) in tot.items():
         if not cnt:
@@ -382,7 +400,8 @@ def phase_report(LA, wl, tot, steps):
                       "achieved_gbs": gbs, "frac_hbm": gbs / HBM_PEAK_GBS,
                       "operand_bytes_per_launch": extra,
                       "achieved_gbs_incl_operands": (a + extra) / (avg * 1e-3) / 1e9,
-                      "traffic_bytes_per_launch": traffic.get(kernel_of[ph])}
+                      "traffic_bytes_per_launch": traffic.get(kernel_of[ph]),
+                      "valu_busy": valu.get(kernel_of[ph])}
         if cf:
             # an exact i8 GEMM: 1024 coefficients x 2K 1024 digit rows x N elements
             macs = 1024 * 2 * wl.pr.K * 1024 * wl.N
@@ -400,7 +419,7 @@ def phase_report(LA, wl, tot, steps):
     roof = {"kernel": p["kernel"], "phase": dom, "bound": "hbm", "achieved": p["achieved_gbs"],
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": p["frac_hbm"], "traffic": p["traffic_bytes_per_launch"],
             "avg_launch_ms": p["avg_launch_ms"], "bytes_per_launch": p["algorithmic_bytes_per_launch"],
-            "extra_bytes": p["operand_bytes_per_launch"]}
+            "extra_bytes": p["operand_bytes_per_launch"], "valu_busy": p["valu_busy"]}
     return phases, roof
 
 

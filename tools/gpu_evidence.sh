@@ -21,6 +21,12 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$TAG -o run
 rc=$?; echo "write rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python tools/prof_summary.py traffic gpurun_out/pmc_fetch_$TAG gpurun_out/pmc_write_$TAG \
   gpurun_out/pmc_traffic_$TAG.json 1024 16384 32 > /dev/null && cp gpurun_out/pmc_traffic_$TAG.json profiles/pmc_traffic.json
+timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+  SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_WAVES GRBM_GUI_ACTIVE -d gpurun_out/pmc_sq_$TAG -o run --output-format csv -- \
+  python bench.py $ARGS > gpurun_out/pmc_sq_$TAG.log 2>&1
+rc=$?; echo "sq rc=$rc"; [ $rc -eq 0 ] || exit $rc
+python tools/prof_summary.py sq gpurun_out/pmc_sq_$TAG gpurun_out/pmc_sq_$TAG.json 1024 16384 32 > /dev/null && \
+  cp gpurun_out/pmc_sq_$TAG.json profiles/pmc_sq.json
 if [ -z "$SKIP_BENCH" ]; then
 timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -c 300 gpurun_out/bench_$TAG.log; [ $rc -eq 0 ] || exit $rc

@@ -13,7 +13,7 @@ for d in sys.argv[1:]:
         names = {}
         for r in csv.DictReader(open(f)):
             per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
-            names[r["Dispatch_Id"]] = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            names[r["Dispatch_Id"]] = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
         for did, cs in per.items():
             for c, v in cs.items():
                 agg[names[did]][c].append(v)

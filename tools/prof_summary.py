@@ -101,9 +101,40 @@ def traffic(fetch_dir, write_dir, out_json, config):
     print(json.dumps(doc, indent=1))
 
 
+def sq(sq_dir, out_json, config, simds=1024, xcds=8):
+    """Per kernel: the VALU pipes' busy fraction from one SQ pass,
+    SQ_ACTIVE_INST_VALU (quad-cycles) x 4 / (SIMDs x GRBM_GUI_ACTIVE / XCDs)
+    (GRBM_GUI_ACTIVE is summed over the XCDs), averaged over launches."""
+    per = {}
+    for c in ("SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
+              "SQ_WAIT_INST_ANY"):
+        vals, meta = counter_per_dispatch(sq_dir, c)
+        for did, v in vals.items():
+            per.setdefault(did, {"name": meta[did][0]})[c] = v
+    acc = defaultdict(list)
+    for did, r in per.items():
+        if r.get("GRBM_GUI_ACTIVE") and "SQ_ACTIVE_INST_VALU" in r:
+            cyc = r["GRBM_GUI_ACTIVE"] / xcds
+            acc[r["name"]].append({"valu_busy": 4 * r["SQ_ACTIVE_INST_VALU"] / (simds * cyc),
+                                   "valu_insts_per_cu_cycle": r["SQ_INSTS_VALU"] / (simds / 4 * cyc),
+                                   "cycles": cyc,
+                                   "wait_issue_frac": r["SQ_WAIT_INST_ANY"] / max(r["SQ_WAVE_CYCLES"], 1),
+                                   "wait_cnt_frac": r["SQ_WAIT_ANY"] / max(r["SQ_WAVE_CYCLES"], 1)})
+    kernels = {k: {f: sum(x[f] for x in v) / len(v) for f in v[0]} | {"launches": len(v)} for k, v in acc.items()}
+    doc = {"config": config, "kernels": kernels,
+           "method": "one rocprofv3 --pmc pass (SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY "
+                     "SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_WAVES GRBM_GUI_ACTIVE) of bench.py; "
+                     "valu_busy = 4 SQ_ACTIVE_INST_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)"}
+    json.dump(doc, open(out_json, "w"), indent=1)
+    print(json.dumps(doc, indent=1))
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], sys.argv[3])
     elif sys.argv[1] == "traffic":
         d, W, kappa = (int(x) for x in sys.argv[5:8]) if len(sys.argv) >= 8 else (1024, 16384, 32)
         traffic(sys.argv[2], sys.argv[3], sys.argv[4], {"d": d, "W": W, "kappa": kappa})
+    elif sys.argv[1] == "sq":
+        d, W, kappa = (int(x) for x in sys.argv[4:7]) if len(sys.argv) >= 7 else (1024, 16384, 32)
+        sq(sys.argv[2], sys.argv[3], {"d": d, "W": W, "kappa": kappa})
