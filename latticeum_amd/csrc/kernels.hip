@@ -3,6 +3,9 @@
 // Phi_72 in the reference's in-place CRT layout [s0.c0, s0.c1, s0.c2, s1.c0, ..]
 // (stark-rings crt.rs:53-77), d = 4^k for the negacyclic rings), canonical
 // values. Every launcher returns hipError_t and takes the stream explicitly.
+#include <cstdlib>
+#include <cstring>
+
 #include "digits.hpp"
 #include "frag.hpp"
 #include "kernels.hpp"
@@ -376,6 +379,191 @@ __global__ void __launch_bounds__(256) k_decompose_phi72(FusedSides sd, size_t N
     for (int i = 0; i < 24; i++) bad |= lbs == 1 ? ((cur[i] < 0 ? -cur[i] : cur[i]) >> K) != 0 : cur[i] != 0;
     if (bad) raise(err, 1);
   }
+}
+
+// Phi_72 with b_small = 2, wave-local (the default d = 24 decomposition): a wave
+// owns 16 groups -- one 16-column contraction unit per limb -- at 4 digit
+// planes; lane 16 kq + gi owns group 16 G + gi at plane 4 pass + kq and walks
+// the group's L limbs. The plane's digits of a limb are kept as two bit masks,
+// so w_ccs_k = sum_l B^l f_k[gL + l] = CRT(sum_l B^l D_l) (linearity; an exact
+// integer for (L - 1) lb < 62) is one more CRT per group, not a 24-value
+// accumulator in registers. Every store instruction writes whole 192-B rows:
+// lane t stores piece t % 12 of row t / 12 (64 lanes = 5.3 rows), the rows
+// coming from the owning lane's masks (f_coeff_k, by ds_bpermute) or from a
+// wave-private LDS tile (f_k, w_ccs_k) -- one request per line instead of one
+// per 16-B piece, which is what bounds a store stream scattered over 192-B
+// rows. The operand pieces of a (unit, plane) are a byte transpose over the 16
+// lanes of a quarter, 8 virtual slots at a time through the same tile; each
+// lane then emits the 4 pieces of one (plane, virtual slot, digit half). The
+// waves of a block never synchronise with each other.
+constexpr int PW_VS = 8;     // virtual slots per staging round (4 kq x 8 vs x 2 halves = one task per lane)
+constexpr int PW_ROW = 17;   // u64 per operand staging row: 16 columns + pad
+constexpr int PW_RROW = 25;  // u64 per element row in the tile: 24 + pad
+constexpr int PW_WAVE_U64 = 64 * PW_RROW;  // 12.8 KB per wave (>= 4 PW_VS PW_ROW)
+template <int NT>
+__device__ __forceinline__ void st16(ulonglong2 *p, ulonglong2 v) {
+  if (NT)
+    nt_store(reinterpret_cast<uint4 *>(p), make_uint4((uint32_t)v.x, (uint32_t)(v.x >> 32), (uint32_t)v.y, (uint32_t)(v.y >> 32)));
+  else
+    *p = v;
+}
+__device__ __forceinline__ uint64_t pw_digit(uint32_t nz, uint32_t ng, int i) {
+  return (nz >> i & 1) ? ((ng >> i & 1) ? gl::P - 1 : 1) : 0;
+}
+template <int NTM>  // streaming stores: bit 0 f_coeff_k, bit 1 f_k, bit 2 operand pieces
+__global__ void __launch_bounds__(256) k_decompose_phi72_w(FusedSides sd, size_t N, int lb, int L, int K, int *err,
+                                                          uint4 *frag, int nch, size_t nblk) {
+  __shared__ uint64_t lds_all[4 * PW_WAVE_U64];
+  const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+  uint64_t *S = lds_all + wib * PW_WAVE_U64;
+  const int npass = (K + 3) / 4;
+  const size_t task = (size_t)blockIdx.x * 4 + wib;  // (side, G, pass), pass fastest
+  if (task >= (size_t)sd.nside * nblk * npass) return;  // wave-uniform; the kernel has no block barrier
+  const int pass = (int)(task % npass);
+  const size_t rest = task / npass;
+  const int side = rest >= nblk ? 1 : 0;
+  const size_t G = rest - side * nblk;
+  const int kq = lane >> 4, gi = lane & 15, k = 4 * pass + kq;
+  const bool kok = k < K;
+  const size_t W = N / L, g = 16 * G + gi;
+  const bool ok = g < W;
+  const uint64_t *f_coeff = sd.f_coeff[side];
+  uint64_t *f_coeff_k = sd.f_coeff_k[side], *f_k = sd.f_k[side], *w_ccs_k = sd.w_ccs_k[side];
+  const int row0 = sd.row0[side];
+  // this lane's operand task: plane kq_t, virtual slot PW_VS r + vl_t, digit half hf_t
+  const int kq_t = lane >> 4, vl_t = (lane & 3) | ((lane >> 3 & 1) << 2), hf_t = lane >> 2 & 1;
+  const int k_t = 4 * pass + kq_t;
+  const bool emit = frag && k_t >= 1 && k_t < K;
+  // this lane's row pieces: piece (64 it + lane) % 12 of the row of source lane
+  // (64 it + lane) / 12, it < 12. The lane index goes through an empty asm at
+  // each use, so these per-piece offsets are recomputed (a few integer
+  // operations) instead of being hoisted out of the limb loop into 100+ VGPRs
+  auto opaque_lane = [&]() {
+    int x = lane;
+    asm volatile("" : "+v"(x));
+    return x;
+  };
+  auto row_live = [&](int j) { return 16 * G + (j & 15) < W && 4 * pass + (j >> 4) < K; };
+  bool bad = false;
+  uint32_t nzm[8], ngm[8];
+  for (int l = L - 1; l >= 0; l--) {
+    uint32_t nz = 0, ng = 0;
+    if (ok) {
+      const ulonglong2 *src = reinterpret_cast<const ulonglong2 *>(f_coeff + (g * L + l) * 24);
+#pragma unroll
+      for (int i = 0; i < 12; i++) {
+        const ulonglong2 v2 = src[i];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          const int64_t v = signed_rep(h ? v2.y : v2.x);
+          const uint64_t m = v < 0 ? (uint64_t)(-v) : (uint64_t)v;
+          bad |= (m >> K) != 0;
+          const uint32_t bit = kok ? (uint32_t)(m >> k) & 1u : 0u;
+          nz |= bit << (2 * i + h);
+          ng |= (v < 0 ? bit : 0u) << (2 * i + h);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++)
+      if (q == l) {
+        nzm[q] = nz;
+        ngm[q] = ng;
+      }
+    // f_coeff_k rows from the owners' masks
+    const int ln0 = opaque_lane();
+#pragma unroll
+    for (int it = 0; it < 12; it++) {
+      const int j = (64 * it + ln0) / 12, pq = (64 * it + ln0) % 12;
+      const uint32_t nzj = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * j, (int)nz);
+      const uint32_t ngj = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * j, (int)ng);
+      if (row_live(j)) {
+        const size_t ej = (16 * G + (j & 15)) * L + l;
+        st16<NTM & 1>(reinterpret_cast<ulonglong2 *>(f_coeff_k + ((size_t)(4 * pass + (j >> 4)) * N + ej) * 24) + pq,
+                      make_ulonglong2(pw_digit(nzj, ngj, 2 * pq), pw_digit(nzj, ngj, 2 * pq + 1)));
+      }
+    }
+    uint64_t c[24];
+#pragma unroll
+    for (int i = 0; i < 24; i++) c[i] = pw_digit(nz, ng, i);
+    ring::phi72_crt(c);
+    // f_k rows through the tile
+#pragma unroll
+    for (int i = 0; i < 12; i++)
+      *reinterpret_cast<ulonglong2 *>(S + lane * PW_RROW + 2 * i) = make_ulonglong2(c[2 * i], c[2 * i + 1]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int ln1 = opaque_lane();
+#pragma unroll
+    for (int it = 0; it < 12; it++) {
+      const int j = (64 * it + ln1) / 12, pq = (64 * it + ln1) % 12;
+      const ulonglong2 v = *reinterpret_cast<const ulonglong2 *>(S + j * PW_RROW + 2 * pq);
+      if (row_live(j)) {
+        const size_t ej = (16 * G + (j & 15)) * L + l;
+        st16<NTM & 2>(reinterpret_cast<ulonglong2 *>(f_k + ((size_t)(4 * pass + (j >> 4)) * N + ej) * 24) + pq, v);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the tile is read before the operand rounds reuse it
+    if (frag) {
+      const size_t u = G * L + l;  // contraction unit of these 16 columns
+      const int ch = (int)(u >> 1), uh = (int)(u & 1);
+#pragma unroll
+      for (int r = 0; r < 40 / PW_VS; r++) {
+        // keep the rounds in order (the compiler would otherwise evaluate all
+        // 40 virtual slots up front)
+#pragma unroll
+        for (int i = 0; i < 24; i += 4) asm volatile("" : "+v"(c[i]), "+v"(c[i + 1]), "+v"(c[i + 2]), "+v"(c[i + 3]));
+#pragma unroll
+        for (int v = 0; v < PW_VS; v++) S[(kq * PW_VS + v) * PW_ROW + gi] = d8(ring::phi72_eval(c, PW_VS * r + v));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's tile writes landed
+        const uint32_t *row = reinterpret_cast<const uint32_t *>(S + (kq_t * PW_VS + vl_t) * PW_ROW) + hf_t;
+        uint32_t w[16];
+#pragma unroll
+        for (int jj = 0; jj < 16; jj++) w[jj] = row[2 * jj];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read before the next round overwrites the tile
+        if (emit) {
+          // 4 pieces: digit 4 hf_t + b of the 16 columns (byte jj = column jj)
+          uint32_t o[4][4];
+#pragma unroll
+          for (int q = 0; q < 4; q++) byte_tr4(w + 4 * q, o[q]);
+          const int vs = PW_VS * r + vl_t;
+          uint4 *out = frag + fv_index(vs, nch, ch, row0 + k_t - 1, uh) + 16 * hf_t;
+#pragma unroll
+          for (int b = 0; b < 4; b++) out_store<(NTM & 4) != 0>(&out[4 * b], make_uint4(o[0][b], o[1][b], o[2][b], o[3][b]));
+        }
+      }
+    }
+  }
+  {  // w_ccs_k = CRT(sum_l B^l D_l), rows w_ccs_k[k][16 G ..] through the tile
+    uint64_t c[24];
+#pragma unroll
+    for (int i = 0; i < 24; i++) {
+      int64_t a = 0;
+      for (int l = L - 1; l >= 0; l--) {
+        uint32_t nz = 0, ng = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+          if (q == l) {
+            nz = nzm[q];
+            ng = ngm[q];
+          }
+        a = a * ((int64_t)1 << lb) + ((nz >> i & 1) ? ((ng >> i & 1) ? -1 : 1) : 0);
+      }
+      c[i] = from_signed(a);
+    }
+    ring::phi72_crt(c);
+#pragma unroll
+    for (int i = 0; i < 12; i++)
+      *reinterpret_cast<ulonglong2 *>(S + lane * PW_RROW + 2 * i) = make_ulonglong2(c[2 * i], c[2 * i + 1]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int it = 0; it < 12; it++) {
+      const int j = (64 * it + lane) / 12, pq = (64 * it + lane) % 12;
+      const ulonglong2 v = *reinterpret_cast<const ulonglong2 *>(S + j * PW_RROW + 2 * pq);
+      if (row_live(j))
+        reinterpret_cast<ulonglong2 *>(w_ccs_k + ((size_t)(4 * pass + (j >> 4)) * W + 16 * G + (j & 15)) * 24)[pq] = v;
+    }
+  }
+  if (pass == 0 && kq == 0 && ok && bad) raise(err, 1);
 }
 
 // negacyclic: one workgroup per group of L elements; coefficients of the
@@ -1024,6 +1212,12 @@ hipError_t from_f(const uint64_t *f, size_t N, int d, int lb, int L, uint64_t *f
   return hipGetLastError();
 }
 
+// LATTICEUM_AMD_DEC24=block: the block-wide d = 24 decomposition (k_decompose_phi72) also for b_small = 2
+static bool dec24_block() {
+  const char *e = getenv("LATTICEUM_AMD_DEC24");
+  return e && !strcmp(e, "block");
+}
+
 hipError_t decompose_phi72_sides(const FusedSides &sd, size_t N, int lb, int L, int lbs, int K, int *err,
                                  uint4 *frag, int nch, hipStream_t st) {
   const size_t W = N / L;
@@ -1033,6 +1227,24 @@ hipError_t decompose_phi72_sides(const FusedSides &sd, size_t N, int lb, int L, 
     if (L > 5) return hipErrorInvalidValue;
     for (int s = 0; s < sd.nside; s++)
       if (sd.row0[s] < 0 || sd.row0[s] + K - 1 > 32) return hipErrorInvalidValue;
+  }
+  if (lbs == 1 && L <= 8 && (L - 1) * lb < 62 && !dec24_block()) {
+    const size_t nblk = (W + 15) / 16, waves = (size_t)sd.nside * nblk * ((K + 3) / 4);
+    // streaming stores for the f_coeff_k and f_k rows (mask 3): nothing in the
+    // step re-reads f_coeff_k, and the fold's one pass over f_k does not gain
+    // from them sitting in the caches (W = 19 763, 4 streams: 0.65 -> 0.53 ms per
+    // launch, 900 -> 1,045 steps/s; mask 7, the operand rows too, ties);
+    // LATTICEUM_AMD_DEC24_NT overrides the mask
+    const char *nte = getenv("LATTICEUM_AMD_DEC24_NT");
+    const int ntm = nte ? atoi(nte) : 3;
+    const dim3 grid((unsigned)((waves + 3) / 4));
+#define LF_PW(M)                                                                                          \
+  case M:                                                                                                \
+    hipLaunchKernelGGL(k_decompose_phi72_w<M>, grid, dim3(256), 0, st, sd, N, lb, L, K, err, frag, nch, nblk); \
+    break;
+    switch (ntm) { LF_PW(0) LF_PW(1) LF_PW(2) LF_PW(3) LF_PW(4) LF_PW(5) LF_PW(6) LF_PW(7) default: return hipErrorInvalidValue; }
+#undef LF_PW
+    return hipGetLastError();
   }
   const int srow = frag ? DEC_SROW : 28;
   const size_t lds = (size_t)DEC_GROUPS * L * srow * sizeof(uint64_t);
