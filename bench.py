@@ -105,7 +105,8 @@ def coeff_fold(d, layout, keep_fk):
 def kernel_names(LA, d, W, layout, keep_fk=True):
     """the kernel each lf_dev_fold_step phase launches (for the rocprof / PMC joins)"""
     if d == 24:
-        return {"decompose": "k_decompose_phi72", "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_phi72",
+        dec = "k_decompose_phi72" if os.environ.get("LATTICEUM_AMD_DEC24") == "block" else "k_decompose_phi72_w"
+        return {"decompose": dec, "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_phi72",
                 "fold": "k_fold_phi72", "from_w_ccs": "k_from_w_ccs_phi72", "from_f": "k_from_f_phi72",
                 "to_frag": "k_to_frag<true, true, true>"}
     if d == 1024:

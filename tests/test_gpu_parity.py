@@ -335,6 +335,20 @@ def test_dev_fold_step_gathering_contraction(ctx, monkeypatch):
     check_dev_fold_step(ctx, 1024, 37, 2)
 
 
+@pytest.mark.parametrize("variant", ["block", "nt0", "nt7"])
+@pytest.mark.parametrize("W", [10, 17, 70])
+def test_dev_fold_step_phi72_decomposition_variants(ctx, monkeypatch, variant, W):
+    """Phi_72: the block-wide decomposition (LATTICEUM_AMD_DEC24=block) and the
+    wave-local one with other streaming-store masks give the oracle's step too
+    (the default, wave-local with mask 3, is test_dev_fold_step_matches_oracle);
+    W = 17 leaves a 16-group unit with one live group"""
+    if variant == "block":
+        monkeypatch.setenv("LATTICEUM_AMD_DEC24", "block")
+    else:
+        monkeypatch.setenv("LATTICEUM_AMD_DEC24_NT", variant[2:])
+    check_dev_fold_step(ctx, 24, W, 3)
+
+
 def test_dev_fold_step_ntt_form_fold(ctx, monkeypatch):
     """LATTICEUM_AMD_FOLD=slot: f_0 folded from the NTT-form planes (k_fold_nega)
     instead of in coefficient form on the matrix cores (fold_coeff.hip)"""

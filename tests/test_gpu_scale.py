@@ -154,6 +154,23 @@ def test_fold_step_bench_shape_d1024():
         torch.cuda.empty_cache()
 
 
+def test_fold_step_reference_ring_zkvm_shape():
+    """the reference ring Phi_72 (d=24) at the real zkvm step shape, bench.py's
+    reference_ring workload: W = 19 763 (1 236 units of 16 groups, the last
+    with 3 live groups), kappa = 32, the wave-local decomposition"""
+    import torch
+    wl = run_workload(24, 19763, 32)
+    try:
+        assert wl.sch.layout == 1
+        nblk = (wl.W + 15) // 16
+        check_workload(wl, bench.SEED_W, [0, 1, nblk // 2, nblk - 1], [0, 1, 15, 16, 30, 31],
+                       [(0, 1, 0), (1, 14, 31), (1, 7, 16), (0, 14, 5)])
+    finally:
+        wl.close()
+        del wl
+        torch.cuda.empty_cache()
+
+
 def test_fold_step_configs4_d4096_kappa64():
     """BASELINE configs[4]'s ring: d=4096 with kappa=64 (two 32-row MFMA tiles)"""
     import torch
