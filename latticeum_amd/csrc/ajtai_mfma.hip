@@ -311,6 +311,123 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const ui
   mfma_epilogue(acc, lane, kt, kappa, nvec, d, so, js, direct, dst, partial);
 }
 
+// The same contraction with A in registers ("ra"): a wave's A operand is its
+// own (one slot per wave), so it needs no LDS. Each wave keeps DP chunks of A
+// in flight in VGPRs (32 per chunk, next to the 240 accumulator AGPRs), and the
+// 160 KiB of LDS hold DP chunks of F: per CU about 2 (DP - 1) x 32 KiB of
+// copies stay outstanding instead of 96 KiB. Per chunk c: wait for this wave's
+// A(c) and F(c) copies, barrier, issue F(c + DP - 1) into the buffer F(c - 1)
+// left, read F(c), 64 MFMAs, issue A(c + DP) into A(c)'s registers. Issue
+// order: A(c0) F(c0) A(c0+1) .. F(c0+DP-2) A(c0+DP-1), then per chunk F, A.
+// waits and loads as asm: the compiler's own waitcnt insertion cannot see that
+// A(c) has landed once F(c) has, and would wait for every copy in flight
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int DP>
+__device__ __forceinline__ void vm_wait_chunk(int nf) {
+  // ops issued after F(c): A(c+1) and DP - 2 (F, A) pairs
+  switch (nf) {
+    case 8: vm_wait<8 + (DP - 2) * 16>(); break;
+    case 7: vm_wait<8 + (DP - 2) * 15>(); break;
+    case 6: vm_wait<8 + (DP - 2) * 14>(); break;
+    case 5: vm_wait<8 + (DP - 2) * 13>(); break;
+    case 4: vm_wait<8 + (DP - 2) * 12>(); break;
+    case 3: vm_wait<8 + (DP - 2) * 11>(); break;
+    case 2: vm_wait<8 + (DP - 2) * 10>(); break;
+    case 1: vm_wait<8 + (DP - 2) * 9>(); break;
+    default: vm_wait<8 + (DP - 2) * 8>(); break;
+  }
+}
+template <int CPOL>
+__device__ __forceinline__ v4i gload16(const v4i *p) {
+  v4i r;
+  if (CPOL == 2)
+    asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(r) : "v"(p) : "memory");
+  else
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+template <int CPOL, int DP>
+__global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const uint4 *Ff, int d, int nch,
+                                                         int nvec, int kappa, uint64_t *partial, OutPtrs dst,
+                                                         int direct, int cps, int ktiles, int nbase, size_t tile_u4,
+                                                         int qd) {
+  static_assert(DP >= 3 && DP <= 5, "F buffers: DP x 32 KiB of LDS");
+  __shared__ uint4 Fl[DP][32 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int grp = blockIdx.x / (8 * ktiles), rem = blockIdx.x - grp * 8 * ktiles;
+  const int kt = rem >> 3, bi = grp * 8 + (rem & 7);
+  if (bi >= nbase) return;  // uniform over the block
+  const int gw = bi * 4 + w;
+  const int s = gw % d, js = gw / d;
+  if (js >= (nch + cps - 1) / cps) return;  // uniform over the block
+  const int c0 = js * cps, c1 = min(nch, c0 + cps);
+  v16i acc[15];
+#pragma unroll
+  for (int t = 0; t < 15; t++) acc[t] = (v16i){0};
+  const v4i *pa = reinterpret_cast<const v4i *>(Af + kt * tile_u4 + ((size_t)s * nch * 8) * 64 + lane);
+  const uint4 *ft = Ff + (size_t)(s >> 2) * nch * FV_CHUNK;
+  v4i ra[DP][8];
+  auto load_a = [&](int c, v4i *dstr) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      dstr[k] = gload16<CPOL>(pa + ((size_t)c * 8 + k) * 64);
+    }
+  };
+  const int nf = __builtin_amdgcn_readfirstlane((nvec - w + 3) >> 2 < 8 ? (nvec - w + 3) >> 2 : 8);  // wave-uniform
+  auto stage_f = [&](int c, int buf) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int j = 4 * q + w;
+      if (q < nf)
+        __builtin_amdgcn_global_load_lds((const void *)(ft + (size_t)c * FV_CHUNK + j * 64 + fl_pi(j, lane)),
+                                         (lds_void *)&Fl[buf][j * 64], 16, 0, CPOL);
+    }
+  };
+  const int rh = 2 * (lane & 31) + (lane >> 5), fj = rh >> 1;
+  int fpos[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) fpos[k] = fj * 64 + fl_pi(fj, (rh & 1) * 32 + k * 4 + w);
+#pragma unroll
+  for (int j = 0; j < DP; j++) {
+    if (c0 + j < c1) load_a(c0 + j, ra[j]);
+    if (j < DP - 1 && c0 + j < c1) stage_f(c0 + j, j);
+  }
+  for (int cb = c0; cb < c1; cb += DP) {
+#pragma unroll
+    for (int j = 0; j < DP; j++) {
+      const int c = cb + j;
+      if (c >= c1) continue;  // uniform (only in a split's last round)
+      if (c + DP - 1 < c1)
+        vm_wait_chunk<DP>(nf);
+      else
+        vm_wait<0>();
+      __builtin_amdgcn_s_barrier();  // every wave's F(c) landed; every wave is done reading F(c - 1)
+      if (c + DP - 1 < c1) stage_f(c + DP - 1, (j + DP - 1) % DP);
+      v4i b[8];
+      const uint32_t fbase = (uint32_t)(uintptr_t)&Fl[j][0];
+#pragma unroll
+      for (int k = 0; k < 8; k++) asm volatile("ds_read_b128 %0, %1" : "=v"(b[k]) : "v"(fbase + 16u * fpos[k]));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // the products read the operands only after the waits above
+#pragma unroll
+      for (int k = 0; k < 8; k++) asm volatile("" : "+v"(b[k]), "+v"(ra[j][k]));
+#pragma unroll
+      for (int kb = 0; kb < 8; kb++)
+#pragma unroll
+        for (int ka = 0; ka < 8; ka++)
+          acc[ka + kb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ra[j][ka], b[kb],
+                                                              acc[ka + kb], 0, 0, 0);
+      if (c + DP < c1) load_a(c + DP, ra[j]);
+    }
+  }
+  const int so = qd ? (s % qd) * 4 + s / qd : s;
+  mfma_epilogue(acc, lane, kt, kappa, nvec, d, so, js, direct, dst, partial);
+}
+
 // ---------------------------------------------------------------- F straight from the vectors
 // X^d + 1 in plain slot order: the block's F tile (nvec vectors x 32 columns x
 // its 4 slots) is gathered from the vectors themselves -- 32 contiguous bytes
@@ -608,6 +725,15 @@ hipError_t to_frag(const VecPtrs &rows, int nrows, int row0, const FragGeom &g, 
   return hipGetLastError();
 }
 
+// the contraction with A in registers and n chunks of each operand in flight
+// (k_ajtai_mfma_ra, n = 4 by default); LATTICEUM_AMD_AJTAI_RA=n (3..5) picks
+// n, 0 the LDS-staged A (k_ajtai_mfma). d = 1024, W = 2^14: 7.0 -> 6.7-6.9 ms
+static int ajtai_ra() {
+  const char *e = getenv("LATTICEUM_AMD_AJTAI_RA");
+  const int v = e ? atoi(e) : 4;
+  return v >= 3 && v <= 5 ? v : 0;
+}
+
 // partial: mfma_scratch_elems() u64 (split partial sums, then Phi_72's virtual-slot results)
 hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, const VecPtrs &fv, int nvec,
                       bool f_ready, uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st, hipEvent_t ev0,
@@ -645,6 +771,20 @@ hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, c
     else
       hipLaunchKernelGGL(k_ajtai_mfma_fv<0>, grid, dim3(256), 0, st, Af, fv, dv, g.nch, nvec, (int)kappa, partial,
                          kout, nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4, g.Lp, g.Wp);
+  } else if (ajtai_ra()) {
+    const bool nt = (size_t)dv * g.nch * 8192 > STREAM_OUT_BYTES;
+#define LF_RA(CP, DP)                                                                                        \
+  hipLaunchKernelGGL((k_ajtai_mfma_ra<CP, DP>), grid, dim3(256), 0, st, Af, Ff, dv, g.nch, nvec, (int)kappa, partial, \
+                     kout, nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4, g.qperm ? d / 4 : 0)
+    switch (ajtai_ra() * 2 + (nt ? 1 : 0)) {
+      case 6: LF_RA(0, 3); break;
+      case 7: LF_RA(2, 3); break;
+      case 8: LF_RA(0, 4); break;
+      case 9: LF_RA(2, 4); break;
+      case 10: LF_RA(0, 5); break;
+      default: LF_RA(2, 5); break;
+    }
+#undef LF_RA
   } else if ((size_t)dv * g.nch * 8192 > STREAM_OUT_BYTES)
     hipLaunchKernelGGL(k_ajtai_mfma<2>, grid, dim3(256), 0, st, Af, Ff, dv, g.nch, nvec, (int)kappa, partial, kout,
                        nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4, g.qperm ? d / 4 : 0);
