@@ -478,7 +478,7 @@ def test_limb_transport_roundtrip(ctx):
     assert [int(v) for v in out.cpu().numpy().view(np.uint64)] == [int(v) for v in want]
 
 
-@pytest.mark.parametrize("layout", ["mfma", "valu", "fv"])
+@pytest.mark.parametrize("layout", ["mfma", "mfma_lds", "mfma_ra3", "mfma_ra5", "valu", "fv"])
 @pytest.mark.parametrize("d,kappa,ncols,nvec", [(16, 3, 40, 5), (64, 32, 70, 29), (1024, 7, 33, 1),
                                                 (1024, 32, 96, 29), (256, 17, 64, 32), (24, 3, 40, 5),
                                                 (24, 32, 700, 29), (24, 9, 33, 1),
@@ -492,6 +492,8 @@ def test_ajtai_layouts(ctx, monkeypatch, layout, d, kappa, ncols, nvec):
         monkeypatch.setenv("LATTICEUM_AMD_AJTAI", "valu")
     if layout == "fv":  # the opt-in contraction that gathers F from the vectors itself
         monkeypatch.setenv("LATTICEUM_AMD_AJTAI_FV", "1")
+    if layout.startswith("mfma_"):  # A staged through LDS (0), or in registers n chunks ahead (default 4)
+        monkeypatch.setenv("LATTICEUM_AMD_AJTAI_RA", "0" if layout == "mfma_lds" else layout[-1])
     A = rand(kappa * ncols * d, 21 + d + kappa).reshape(kappa, ncols, d)
     # edge values in A: 0, p-1 and the D8 digit boundaries
     A.reshape(-1)[:6] = [0, P - 1, 0x7F7F7F7F7F7F7F7F, 0x7F7F7F7F7F7F7F80, (P - 1) // 2, 1]
@@ -507,10 +509,17 @@ def test_ajtai_layouts(ctx, monkeypatch, layout, d, kappa, ncols, nvec):
     assert np.array_equal(cm.cpu().numpy().view(np.uint64), want)
 
 
-def test_ajtai_mfma_extreme_digits(ctx):
-    # all-(-128) digit products stress the i32 weight accumulators over a full column split
+@pytest.mark.parametrize("ra", ["4", "0", "3", "5"])
+@pytest.mark.parametrize("nch", [320, 329])
+def test_ajtai_mfma_extreme_digits(ctx, monkeypatch, ra, nch):
+    # all-(-128) digit products stress the i32 weight accumulators over a full
+    # column split (d = 256: 320 chunks per split), and with 329 chunks a ragged
+    # second split of 9 chunks, for
+    # both contraction kernels (LATTICEUM_AMD_AJTAI_RA: A in registers n chunks
+    # ahead, 0: through LDS)
     import torch
-    d, kappa, ncols, nvec = 16, 32, 320 * 32, 32
+    monkeypatch.setenv("LATTICEUM_AMD_AJTAI_RA", ra)
+    d, kappa, ncols, nvec = 256, 32, nch * 32, 32
     A = np.full(kappa * ncols * d, P - 1, np.uint64).reshape(kappa, ncols, d)
     F = np.full(nvec * ncols * d, P - 1, np.uint64)
     sch = LA.AjtaiCommitmentScheme(ctx, A)
