@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--no-small-shape", dest="small", action="store_false", default=True,
                     help="skip the W=464 / d=24 multi-stream measurements and the NTT / Poseidon2 timings "
                          "reported beside the default workload")
+    ap.add_argument("--cu-partition", action="store_true", default=False,
+                    help="give each step stream its own contiguous block of CUs (lf_stream_create_cu_mask)")
     ap.add_argument("--cpu-baseline", dest="cpu", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu", action="store_false")
     return ap.parse_args()
@@ -251,7 +253,7 @@ class Workload:
     side and rho (shared, read-only), and `streams` independent step streams,
     each an lf context on its own HIP stream with its own w_ccs and outputs."""
 
-    def __init__(self, LA, torch, local, rank, d, W, kappa, streams, seed_a=SEED_A, keep_fk=True):
+    def __init__(self, LA, torch, local, rank, d, W, kappa, streams, seed_a=SEED_A, keep_fk=True, cu_partition=False):
         # keep_fk=False (fused X^1024+1 path only): the decomposed planes live only
         # as MFMA operand rows (lf.h: f_k buffers omitted) -- 20 GB less HBM at
         # W = 2^14, but slower (DESIGN.md section 7), so the bench keeps f_k
@@ -311,6 +313,9 @@ class Workload:
                         getattr(bufs, k)[s] = v[s].data_ptr() if v[s] is not None else None
                 else:
                     setattr(bufs, k, v.data_ptr())
+            if cu_partition and streams > 1:
+                ncu = torch.cuda.get_device_properties(local).multi_processor_count
+                c.use_cu_mask(range(i * ncu // streams, (i + 1) * ncu // streams))
             c.reserve(kappa, N, d, 2 * (K - 1) + 1)
             self.ctxs.append(c)
             self.keeps.append(keep)
@@ -691,7 +696,7 @@ def main():
     pg = LD.init(world)
 
     d, W, kappa = args.d, args.w, args.kappa
-    wl = Workload(LA, torch, local, rank, d, W, kappa, args.streams)
+    wl = Workload(LA, torch, local, rank, d, W, kappa, args.streams, cu_partition=args.cu_partition)
     K, L, N = wl.pr.K, wl.pr.L, wl.N
     dt_max, (phases, roof) = measure(LA, torch, LD, pg, world, wl, args.steps, args.warmup)
     wl.close()

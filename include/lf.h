@@ -108,6 +108,17 @@ const char *lf_ctx_last_error(const lf_ctx *ctx);
  * which is what torch's default current stream is. */
 int lf_ctx_set_stream(lf_ctx *ctx, void *hip_stream);
 void *lf_ctx_get_stream(const lf_ctx *ctx);
+/* a non-blocking HIP stream of `device` whose kernels run only on the compute
+ * units set in mask (nwords 32-bit words, bit i = CU i as the HIP runtime
+ * numbers them), for lf_ctx_set_stream: a host can give concurrent step
+ * streams disjoint parts of the chip. lf_stream_destroy releases it. */
+int lf_stream_create_cu_mask(int device, const uint32_t *mask, int nwords, void **stream);
+int lf_stream_destroy(void *stream);
+/* compute units this context's stream may use (default: the device's): the
+ * grid size of the persistent kernels (the fused decompositions, the
+ * coefficient-form fold), so a context on a CU-masked stream fills its part
+ * of the chip in one round */
+int lf_ctx_set_cu_count(lf_ctx *ctx, int ncu);
 /* wait for the stream; returns LF_ERR_DECOMPOSITION_OVERFLOW (and clears it)
  * if any device decomposition since the last sync ran out of digits */
 int lf_ctx_sync(lf_ctx *ctx);

@@ -64,8 +64,11 @@ class Context:
 
     def close(self):
         if getattr(self, "h", None):
-            self.lib.lf_ctx_destroy(self.h)
+            self.lib.lf_ctx_destroy(self.h)  # synchronises the current stream first
             self.h = None
+        for st in getattr(self, "_masked", []):
+            self.lib.lf_stream_destroy(st)
+        self._masked = []
 
     def __del__(self):
         try:
@@ -84,6 +87,23 @@ class Context:
 
     def sync(self):
         self.check(self.lib.lf_ctx_sync(self.h))
+
+    def use_cu_mask(self, cus):
+        """run this context's work on a stream of its own restricted to the
+        compute units `cus` (iterable of CU indices); lf_stream_create_cu_mask"""
+        cus = list(cus)
+        words = (max(cus) // 32 + 1) if cus else 1
+        mask = (C.c_uint32 * words)()
+        for i in cus:
+            mask[i // 32] |= 1 << (i % 32)
+        st = C.c_void_p()
+        rc = self.lib.lf_stream_create_cu_mask(self.device, mask, words, C.byref(st))
+        if rc != 0:
+            raise LfError(rc, "lf_stream_create_cu_mask")
+        self.set_stream(st.value)
+        self.check(self.lib.lf_ctx_set_cu_count(self.h, len(set(cus))))
+        self._masked = getattr(self, "_masked", []) + [st.value]
+        return st.value
 
     def reserve(self, kappa: int, ncols: int, d: int, nvec: int):
         self.check(self.lib.lf_ctx_reserve(self.h, kappa, ncols, d, nvec))

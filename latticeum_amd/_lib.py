@@ -65,6 +65,9 @@ SIGNATURES = {
     "lf_ctx_last_error": (C.c_char_p, [VP]),
     "lf_ctx_set_stream": (I, [VP, VP]),
     "lf_ctx_get_stream": (VP, [VP]),
+    "lf_stream_create_cu_mask": (I, [I, VP, I, VP]),
+    "lf_stream_destroy": (I, [VP]),
+    "lf_ctx_set_cu_count": (I, [VP, I]),
     "lf_ctx_sync": (I, [VP]),
     "lf_ctx_reserve": (I, [VP, SZ, SZ, I, I]),
     "lf_ctx_kernel_timing": (I, [VP, I]),

@@ -750,6 +750,25 @@ int lf_ctx_set_stream(lf_ctx *c, void *s) {
 }
 void *lf_ctx_get_stream(const lf_ctx *c) { return c ? (void *)c->cur : nullptr; }
 
+int lf_stream_create_cu_mask(int device, const uint32_t *mask, int nwords, void **stream) {
+  if (!mask || nwords < 1 || !stream) return LF_ERR_INVALID_ARG;
+  *stream = nullptr;
+  DevGuard g(device);
+  hipStream_t s = nullptr;
+  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, mask) != hipSuccess) return LF_ERR_DEVICE;
+  *stream = (void *)s;
+  return LF_OK;
+}
+int lf_ctx_set_cu_count(lf_ctx *c, int ncu) {
+  if (!c || ncu < 1) return LF_ERR_INVALID_ARG;
+  c->ncu = ncu;
+  return LF_OK;
+}
+int lf_stream_destroy(void *stream) {
+  if (!stream) return LF_ERR_INVALID_ARG;
+  return hipStreamDestroy((hipStream_t)stream) == hipSuccess ? LF_OK : LF_ERR_DEVICE;
+}
+
 int lf_ctx_sync(lf_ctx *c) {
   DevGuard g(c);
   if (!c) return LF_ERR_INVALID_ARG;

@@ -367,6 +367,18 @@ def test_dev_fold_step_rho_not_short(ctx, W):
     check_dev_fold_step(ctx, d, W, 2)
 
 
+def test_dev_fold_step_on_cu_masked_stream():
+    """a context on a stream restricted to a block of 64 CUs (and the persistent
+    grids sized to it, lf_ctx_set_cu_count) computes the same step"""
+    c = LA.Context(0)
+    try:
+        c.use_cu_mask(range(64, 128))
+        check_dev_fold_step(c, 1024, 37, 2)
+        check_dev_fold_step(c, 24, 17, 3)
+    finally:
+        c.close()
+
+
 def test_dev_fold_step_repeated_in_place(ctx):
     # consecutive steps reuse every buffer (as bench.py and the proving loop do):
     # the fused fold must see each step's own f_k rows, never the previous step's
@@ -412,6 +424,7 @@ def check_dev_fold_step(ctx, d, W, kappa, steps=1, keep_fk=True, rho=None):
         if step:
             w_ccs = rand(W * d, 2000 + step)
             keep["w_ccs"].copy_(dev(w_ccs))
+        torch.cuda.synchronize()  # the inputs torch wrote on its stream, before the context's stream reads them
         ctx.dev_fold_step(sch, pr, W, b)
         ctx.sync()
         check_fold_outputs(h, keep, A, kappa, d, pr, W, w_ccs, acc_cm, acc_fc, rho)
