@@ -106,6 +106,13 @@ def coeff_fold(d, layout, keep_fk):
 
 def kernel_names(LA, d, W, layout, keep_fk=True):
     """the kernel each lf_dev_fold_step phase launches (for the rocprof / PMC joins)"""
+    names = _kernel_names(LA, d, W, layout, keep_fk)
+    if names["ajtai"] == "k_ajtai_mfma" and os.environ.get("LATTICEUM_AMD_AJTAI_RA", "4") in ("3", "4", "5"):
+        names["ajtai"] = "k_ajtai_mfma_ra"  # A in registers (ajtai_mfma.hip), the default
+    return names
+
+
+def _kernel_names(LA, d, W, layout, keep_fk=True):
     if d == 24:
         dec = "k_decompose_phi72" if os.environ.get("LATTICEUM_AMD_DEC24") == "block" else "k_decompose_phi72_w"
         return {"decompose": dec, "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_phi72",
