@@ -114,9 +114,12 @@ def kernel_names(LA, d, W, layout, keep_fk=True):
 
 def _kernel_names(LA, d, W, layout, keep_fk=True):
     if d == 24:
-        dec = "k_decompose_phi72" if os.environ.get("LATTICEUM_AMD_DEC24") == "block" else "k_decompose_phi72_w"
-        return {"decompose": dec, "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_phi72",
-                "fold": "k_fold_phi72", "from_w_ccs": "k_from_w_ccs_phi72", "from_f": "k_from_f_phi72",
+        block = os.environ.get("LATTICEUM_AMD_DEC24") == "block"
+        cf24 = not block and keep_fk and os.environ.get("LATTICEUM_AMD_FOLD") != "slot"
+        return {"decompose": "k_decompose_phi72" if block else "k_decompose_phi72_w",
+                "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_phi72",
+                "fold": "k_fold_coeff_phi72" if cf24 else "k_fold_phi72", "from_w_ccs": "k_from_w_ccs_phi72",
+                "from_f": "k_from_f_phi72",
                 "to_frag": "k_to_frag<true, true, true>"}
     if d == 1024:
         small = W < LA.witness_split_w()  # one half-wave per (element, limb) below this W
@@ -419,8 +422,11 @@ def phase_report(LA, wl, tot, steps):
         sides = max(1, round(2 * steps / cnt)) if ph == "decompose" else 1
         a = alg[ph] * sides
         cf = ph == "fold" and kernel_of[ph] == "k_fold_coeff"
+        cf24 = ph == "fold" and kernel_of[ph] == "k_fold_coeff_phi72"
         if cf:  # the coefficient-form fold never reads the 2K NTT-form planes (B4): count what it moves
             a = wl.N * (2 * 2048 + 2 * 2 * wl.pr.K * 256 + 8 * 1024)  # packed digits in, keys out + in, f0_coeff out
+        if cf24:  # digit masks in (8 B per element and plane); f0_coeff, f0 (E each) and w_ccs0 out (from_f's outputs)
+            a = wl.N * (2 * wl.pr.K * 8 + 2 * 8 * d) + wl.W * 8 * d
         gbs = a / (avg * 1e-3) / 1e9
         extra = operand.get(ph, 0) * sides
         phases[ph] = {"kernel": kernel_of[ph], "avg_launch_ms": avg, "launches_per_step": cnt / steps,
@@ -440,6 +446,12 @@ def phase_report(LA, wl, tot, steps):
                 "note": "f_0 = NTT(sum_i rho_i * D_i) from the digit planes D_i on the i8 matrix cores "
                         "(fold_coeff.hip, with the digit-key packing in the same phase); "
                         "algorithmic_bytes_per_launch is what it moves, SURVEY B4 would read the 2K NTT-form planes"}
+        if cf24:
+            phases[ph]["coefficient_form"] = {
+                "survey_b4_bytes": alg[ph],
+                "note": "f_0 = CRT(sum_i rho_i * D_i) from the decomposition's digit masks, with Witness::from_f "
+                        "(f0_coeff, w_ccs0) in the same launch (k_fold_coeff_phi72); the from_f phase only "
+                        "launches the gated fallback"}
     if not phases:
         return phases, None
     dom = max(phases, key=lambda k: phases[k]["ms_per_step"])

@@ -58,23 +58,7 @@ LF_HD uint64_t neg(uint64_t a) { return a ? P - a : 0; }
 // 64x64 -> 128 from four 32x32 -> 64 multiply-adds (v_mad_u64_u32 each; no
 // intermediate sum overflows: (2^32-1)^2 + 2 (2^32-1) = 2^64 - 1)
 LF_HD void mul_wide(uint64_t a, uint64_t b, uint64_t &lo, uint64_t &hi) {
-#if defined(__HIP_DEVICE_COMPILE__) && defined(LF_MUL_LOHI)
-  // eight 32-bit multiplies and two carry chains: no 64-bit addends to
-  // assemble (v_mad_u64_u32 takes them as register pairs, which cost about 17
-  // v_mov per product in the NTT kernels)
-  const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
-  const uint32_t l0 = a0 * b0, h0 = __umulhi(a0, b0), l1 = a0 * b1, h1 = __umulhi(a0, b1);
-  const uint32_t l2 = a1 * b0, h2 = __umulhi(a1, b0), l3 = a1 * b1, h3 = __umulhi(a1, b1);
-  unsigned int c1, c2, c3, c4, c5, c6;
-  uint32_t w1 = __builtin_addc(h0, l1, 0u, &c1);
-  w1 = __builtin_addc(w1, l2, 0u, &c2);
-  uint32_t w2 = __builtin_addc(h1, h2, c1, &c3);
-  w2 = __builtin_addc(w2, l3, c2, &c4);
-  uint32_t w3 = __builtin_addc(h3, 0u, c3, &c5);
-  w3 = __builtin_addc(w3, 0u, c4, &c6);
-  lo = ((uint64_t)w1 << 32) | l0;
-  hi = ((uint64_t)w3 << 32) | w2;
-#elif defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
   const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
   const uint64_t p0 = (uint64_t)a0 * b0;
   const uint64_t t = (uint64_t)a0 * b1 + (p0 >> 32);

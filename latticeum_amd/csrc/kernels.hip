@@ -184,7 +184,8 @@ __global__ void __launch_bounds__(NT<D>::T) k_from_w_ccs_nega(const uint64_t *w_
 // Horner recompose (balanced_decomposition/mod.rs:105-117) over the G * 24
 // w_ccs coefficients and store them contiguously.
 __global__ void __launch_bounds__(256) k_from_f_phi72(const uint64_t *f, size_t W, int lb, int L,
-                                                     uint64_t *f_coeff, uint64_t *w_ccs) {
+                                                     uint64_t *f_coeff, uint64_t *w_ccs, const int *run_if) {
+  if (run_if && !*run_if) return;    // uniform: the coefficient-form fold produced f_coeff and w_ccs
   extern __shared__ uint64_t lds[];  // [G * L][24]
   const int G = blockDim.x / L, t = threadIdx.x;
   const size_t j0 = (size_t)blockIdx.x * G;
@@ -470,6 +471,7 @@ __global__ void __launch_bounds__(256) k_decompose_phi72_w(FusedSides sd, size_t
         nzm[q] = nz;
         ngm[q] = ng;
       }
+    if (sd.masks[side] && ok && kok) sd.masks[side][(size_t)k * N + g * L + l] = make_uint2(nz, ng);
     // f_coeff_k rows from the owners' masks
     const int ln0 = opaque_lane();
 #pragma unroll
@@ -947,10 +949,10 @@ __global__ void __launch_bounds__(256) k_fold_nega(const uint64_t *rho, VecPtrs 
   }
 }
 __global__ void __launch_bounds__(256) k_fold_phi72(const uint64_t *rho, VecPtrs x, int nwit, size_t n,
-                                                   uint64_t *out) {
-  size_t u = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // Fq3 slot index
-  if (u >= n * 8) return;
-  const int s = u % 8;
+                                                   uint64_t *out, const int *run_if) {
+  if (run_if && !*run_if) return;  // uniform: the coefficient-form fold produced f_0
+  for (size_t u = blockIdx.x * (size_t)blockDim.x + threadIdx.x; u < n * 8; u += (size_t)gridDim.x * blockDim.x) {
+  const int s = u % 8;  // Fq3 slot index u
   ring::Fq3Acc a;
   ring::fq3acc_zero(a);
   for (int i = 0; i < nwit; i++) {
@@ -962,6 +964,147 @@ __global__ void __launch_bounds__(256) k_fold_phi72(const uint64_t *rho, VecPtrs
   out[3 * u] = c[0];
   out[3 * u + 1] = c[1];
   out[3 * u + 2] = c[2];
+  }
+}
+
+// ============================================================ Phi_72 fold in coefficient form
+// The 2K folded witnesses are digit planes, f_i = CRT(D_i) with D_i in {-1, 0, 1}^24,
+// and get_rhos' challenges are short (coefficients in [-32, 31],
+// rings/goldilocks.rs:41-67). CRT is a ring isomorphism, so f_0 = CRT(f0_coeff)
+// with f0_coeff = sum_i rho_i * D_i, the product in Z[X]/(X^24 - X^12 + 1) of
+// small integers. Before the reduction every coefficient of the degree-46 sum is
+// at most 2K 24 32 = 23 040 in magnitude, so it runs on packed 16-bit lanes
+// (v_pk_mad_i16: two coefficients per instruction). It replaces reading the 2K
+// NTT-form planes (30 x 192 B per element) with 30 x 8 B of digit masks, and
+// Witness::from_f's ICRT with a CRT.
+constexpr int RHO24_BOUND = 32;
+constexpr int RHO24_WORDS = 25;  // per witness: 12 pairs (rho_2b, rho_2b+1), 13 pairs (rho_2b-1, rho_2b)
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack16(int lo, int hi) { return (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16); }
+__global__ void k_rho_phi72(const uint64_t *rho, int nw, uint32_t *rc, int *bad) {
+  const int i = threadIdx.x;  // one block of >= nw threads: it also clears / sets the flag
+  bool out = false;
+  if (i < nw) {
+  uint64_t c[24];
+#pragma unroll
+  for (int t = 0; t < 24; t++) c[t] = rho[(size_t)i * 24 + t];
+  ring::phi72_icrt(c);
+  int v[26];
+  v[0] = v[25] = 0;  // rho_-1, rho_24
+#pragma unroll
+  for (int t = 0; t < 24; t++) {
+    const int64_t x = signed_rep(c[t]);
+    out |= x > RHO24_BOUND || x < -RHO24_BOUND;
+    v[t + 1] = (int)(x > RHO24_BOUND ? 0 : x < -RHO24_BOUND ? 0 : x);
+  }
+#pragma unroll
+  for (int b = 0; b < 12; b++) rc[i * RHO24_WORDS + b] = pack16(v[2 * b + 1], v[2 * b + 2]);
+#pragma unroll
+  for (int b = 0; b < 13; b++) rc[i * RHO24_WORDS + 12 + b] = pack16(v[2 * b], v[2 * b + 1]);
+  }
+  out = __syncthreads_or(out);
+  if (i == 0) *bad = out ? 1 : 0;
+}
+
+// one thread per element (blocks of whole groups, G = blockDim / L); the f0
+// elements meet in LDS for w_ccs0 = sum_l B^l f0[gL + l], as in k_from_f_phi72.
+// acc2[q] holds coefficients (2q, 2q + 1) of the degree-46 sum: digit j = 2a
+// adds dg (rho_2b, rho_2b+1) to acc2[a + b], digit j = 2a + 1 adds
+// dg (rho_2b-1, rho_2b) to acc2[a + b]
+__global__ void __launch_bounds__(256) k_fold_coeff_phi72(const uint2 *masks0, const uint2 *masks1,
+                                                          const uint32_t *rc, const int *bad, size_t N, int K, int L,
+                                                          int lb, uint64_t *f0_coeff, uint64_t *f0,
+                                                          uint64_t *w_ccs0) {
+  if (*bad) return;  // uniform: a challenge is not short, the NTT-form fold runs instead
+  extern __shared__ uint64_t lds[];  // [G L][24] f0 elements, then the 2K x 25 packed rho words
+  const int G = blockDim.x / L, t = threadIdx.x, nw = 2 * K;
+  uint32_t *rl = reinterpret_cast<uint32_t *>(lds + (size_t)G * L * 24);
+  for (int q = t; q < nw * RHO24_WORDS; q += blockDim.x) rl[q] = rc[q];
+  __syncthreads();
+  const size_t W = N / L, j0 = (size_t)blockIdx.x * G;
+  const size_t e = j0 * L + t;
+  if (t < G * L && e < N) {
+    s16x2 acc2[24];
+#pragma unroll
+    for (int q = 0; q < 24; q++) acc2[q] = (s16x2){0, 0};
+    // the next witness's masks load while this one's products run
+    auto mask_of = [&](int i) { return (i < K ? masks0 : masks1)[(size_t)(i < K ? i : i - K) * N + e]; };
+    uint2 mn = mask_of(0);
+    for (int i = 0; i < nw; i++) {
+      const uint2 m = mn;
+      if (i + 1 < nw) mn = mask_of(i + 1);
+      s16x2 r[RHO24_WORDS];
+#pragma unroll
+      for (int u = 0; u < RHO24_WORDS; u++) r[u] = __builtin_bit_cast(s16x2, rl[i * RHO24_WORDS + u]);
+#pragma unroll
+      for (int jj = 0; jj < 24; jj++) {
+        const short dv = (m.x >> jj & 1) ? ((m.y >> jj & 1) ? (short)-1 : (short)1) : (short)0;
+        const s16x2 dg = {dv, dv};
+        const int a = jj >> 1;
+        if ((jj & 1) == 0) {
+#pragma unroll
+          for (int b2 = 0; b2 < 12; b2++) acc2[a + b2] += dg * r[b2];
+        } else {
+#pragma unroll
+          for (int b2 = 0; b2 < 13; b2++)
+            if (a + b2 < 24) acc2[a + b2] += dg * r[12 + b2];
+        }
+      }
+    }
+    int32_t acc[48];
+#pragma unroll
+    for (int q = 0; q < 24; q++) {
+      acc[2 * q] = acc2[q].x;
+      acc[2 * q + 1] = acc2[q].y;
+    }
+    // X^24 = X^12 - 1:  X^s = X^(s-12) - X^(s-24) for 24 <= s < 36, X^s = -X^(s-36) for s >= 36
+#pragma unroll
+    for (int s2 = 46; s2 >= 36; s2--) acc[s2 - 36] -= acc[s2];
+#pragma unroll
+    for (int s2 = 35; s2 >= 24; s2--) {
+      acc[s2 - 12] += acc[s2];
+      acc[s2 - 24] -= acc[s2];
+    }
+    uint64_t c[24];
+#pragma unroll
+    for (int u = 0; u < 24; u++) c[u] = from_signed(acc[u]);
+    ulonglong2 *dc = reinterpret_cast<ulonglong2 *>(f0_coeff + e * 24);
+#pragma unroll
+    for (int u = 0; u < 12; u++) dc[u] = make_ulonglong2(c[2 * u], c[2 * u + 1]);
+    ring::phi72_crt(c);
+    ulonglong2 *df = reinterpret_cast<ulonglong2 *>(f0 + e * 24);
+#pragma unroll
+    for (int u = 0; u < 12; u++) df[u] = make_ulonglong2(c[2 * u], c[2 * u + 1]);
+#pragma unroll
+    for (int u = 0; u < 24; u++) lds[t * 24 + u] = c[u];
+  }
+  __syncthreads();
+  const size_t ng = W - j0 < (size_t)G ? W - j0 : (size_t)G;
+  for (int o = t; o < (int)ng * 24; o += blockDim.x) {
+    const int g = o / 24, i = o - g * 24;
+    const uint64_t *row = lds + g * L * 24 + i;
+    uint64_t acc = row[(L - 1) * 24];
+    for (int l = L - 2; l >= 0; l--) acc = gl::add(gl::mul_pow2(acc, lb), row[l * 24]);
+    w_ccs0[j0 * 24 + o] = acc;
+  }
+}
+
+hipError_t fold_phi72_rho(const uint64_t *rho, int nw, uint32_t *rc, int *bad, hipStream_t st) {
+  if (nw < 1 || nw > 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_rho_phi72, dim3(1), dim3(64), 0, st, rho, nw, rc, bad);
+  return hipGetLastError();
+}
+
+hipError_t fold_phi72_coeff(const uint2 *masks0, const uint2 *masks1, const uint32_t *rc, const int *bad, size_t N,
+                            int K, int L, int lb, uint64_t *f0_coeff, uint64_t *f0, uint64_t *w_ccs0, hipStream_t st) {
+  const size_t W = N / L;
+  if (W == 0) return hipSuccess;
+  if (L < 1 || L > 256 || K < 1 || 2 * K > 64) return hipErrorInvalidValue;
+  const int G = 256 / L;
+  const size_t lds = (size_t)G * L * 24 * 8 + (size_t)2 * K * RHO24_WORDS * 4;
+  hipLaunchKernelGGL(k_fold_coeff_phi72, dim3((unsigned)((W + G - 1) / G)), dim3(G * L), lds, st, masks0, masks1, rc, bad, N, K,
+                     L, lb, f0_coeff, f0, w_ccs0);
+  return hipGetLastError();
 }
 
 // ============================================================ Poseidon2-16
@@ -1191,15 +1334,15 @@ hipError_t from_f(const uint64_t *f, size_t N, int d, int lb, int L, uint64_t *f
   const size_t W = N / L;
   if (W == 0) return hipSuccess;
   if (d == 1024 && inv.mid) return from_f_n32(f, W, lb, L, f_coeff, w_ccs, inv, st, run_if);
-  if (run_if) return hipErrorInvalidValue;
-  if (d == 4096 && inv.tw4) return from_f_n4k(f, W, lb, L, f_coeff, w_ccs, inv, st);
   if (d == 24) {
     if (L < 1 || L > 256) return hipErrorInvalidValue;
     const int G = 256 / L;
     hipLaunchKernelGGL(k_from_f_phi72, dim3(blocks(W, G)), dim3(G * L), (size_t)G * L * 24 * 8, st, f,
-                       W, lb, L, f_coeff, w_ccs);
+                       W, lb, L, f_coeff, w_ccs, run_if);
     return hipGetLastError();
   }
+  if (run_if) return hipErrorInvalidValue;
+  if (d == 4096 && inv.tw4) return from_f_n4k(f, W, lb, L, f_coeff, w_ccs, inv, st);
 #define LF_CASE(DD)                                                                              \
   case DD:                                                                                       \
     hipLaunchKernelGGL((k_from_f_nega<DD>), dim3(grid_cap(W)), dim3(NT<DD>::T), 0, st, f, W, lb, L, \
@@ -1219,8 +1362,9 @@ static bool dec24_block() {
 }
 
 hipError_t decompose_phi72_sides(const FusedSides &sd, size_t N, int lb, int L, int lbs, int K, int *err,
-                                 uint4 *frag, int nch, hipStream_t st) {
+                                 uint4 *frag, int nch, hipStream_t st, bool *masks_written) {
   const size_t W = N / L;
+  if (masks_written) *masks_written = false;
   if (W == 0) return hipSuccess;
   if (DEC_GROUPS * L > 256 || sd.nside < 1 || sd.nside > 2) return hipErrorInvalidValue;
   if (frag) {
@@ -1244,6 +1388,7 @@ hipError_t decompose_phi72_sides(const FusedSides &sd, size_t N, int lb, int L, 
     break;
     switch (ntm) { LF_PW(0) LF_PW(1) LF_PW(2) LF_PW(3) LF_PW(4) LF_PW(5) LF_PW(6) LF_PW(7) default: return hipErrorInvalidValue; }
 #undef LF_PW
+    if (masks_written) *masks_written = sd.masks[0] != nullptr && (sd.nside < 2 || sd.masks[1] != nullptr);
     return hipGetLastError();
   }
   const int srow = frag ? DEC_SROW : 28;
@@ -1381,9 +1526,11 @@ hipError_t commit_y0(const uint64_t *cm, uint64_t *y, size_t kappa, int d, int l
 hipError_t fold(const uint64_t *rho, const VecPtrs &x, int nwit, size_t n, int d, uint64_t *out,
                 hipStream_t st, const int *run_if) {
   if (n == 0) return hipSuccess;
-  if (nwit <= 0 || nwit > LF_MAX_VECS || (run_if && d == 24)) return hipErrorInvalidValue;
+  if (nwit <= 0 || nwit > LF_MAX_VECS) return hipErrorInvalidValue;
   if (d == 24) {
-    hipLaunchKernelGGL(k_fold_phi72, dim3(blocks(n * 8, 256)), dim3(256), 0, st, rho, x, nwit, n, out);
+    unsigned nb = blocks(n * 8, 256);
+    if (run_if && nb > 1024) nb = 1024;  // usually returns at once: do not launch a block per 256 slots
+    hipLaunchKernelGGL(k_fold_phi72, dim3(nb), dim3(256), 0, st, rho, x, nwit, n, out, run_if);
   } else {
     unsigned nb = blocks(n * d / 2, 256);
     if (run_if && nb > 8192) nb = 8192;  // usually returns at once: do not launch a block per 512 slots

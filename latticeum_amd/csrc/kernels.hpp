@@ -28,7 +28,7 @@ hipError_t mont(uint64_t *x, size_t n, bool to, hipStream_t st);
 hipError_t from_w_ccs(const uint64_t *w_ccs, size_t W, int d, int lb, int L, uint64_t *f_coeff,
                       uint64_t *f, const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err,
                       hipStream_t st);
-// run_if (X^1024 + 1 only): when given, the kernels do nothing unless *run_if != 0
+// run_if (X^1024 + 1 and Phi_72): when given, the kernels do nothing unless *run_if != 0
 // (the fallbacks of the coefficient-form fold, fold_coeff.hip)
 hipError_t from_f(const uint64_t *f, size_t N, int d, int lb, int L, uint64_t *f_coeff,
                   uint64_t *w_ccs, const ring::NegaTables &inv, hipStream_t st, const int *run_if = nullptr);
@@ -116,6 +116,7 @@ struct FusedSides {
   int row0[2];                                   // operand row of plane 1 (planes 1 .. K-1 consecutive)
   int nside;
   int row_p0[2] = {-1, -1};                      // operand row of plane 0, or -1 (not written)
+  uint2 *masks[2] = {nullptr, nullptr};          // d = 24, b_small = 2: digit masks [K][N] (nonzero, negative), or null
 };
 // f_0 = sum_v rho_v f_v with every f_v read from the D8 operand rows (k_fold_frag)
 struct FoldRows {
@@ -146,8 +147,16 @@ hipError_t from_fcoeff_n32(const uint64_t *f_coeff, size_t W, int lb, int L, uin
                            const ring::NegaTables &fwd, const int *gate, hipStream_t st);
 
 // d = 24: both sides of a fold step in one launch (blockIdx.z = side); frag as decompose_witness
+// *masks_written: whether the launch filled sd.masks (the wave-local kernel does)
 hipError_t decompose_phi72_sides(const FusedSides &sd, size_t N, int lb, int L, int lbs, int K, int *err,
-                                 uint4 *frag, int nch, hipStream_t st);
+                                 uint4 *frag, int nch, hipStream_t st, bool *masks_written = nullptr);
+// f_0 in coefficient form from the decomposition's digit masks (d = 24, b_small = 2):
+// rho (2K NTT elements) -> rc [2K][25] packed 16-bit coefficient pairs, *bad = 1 if
+// one is outside [-32, 32]; unless *bad: f0_coeff = sum_i rho_i * D_i, f0 = CRT(f0_coeff),
+// w_ccs0 = recompose(f0) (folding.rs:258-268 then Witness::from_f, arith.rs:299-313)
+hipError_t fold_phi72_rho(const uint64_t *rho, int nw, uint32_t *rc, int *bad, hipStream_t st);
+hipError_t fold_phi72_coeff(const uint2 *masks0, const uint2 *masks1, const uint32_t *rc, const int *bad, size_t N,
+                            int K, int L, int lb, uint64_t *f0_coeff, uint64_t *f0, uint64_t *w_ccs0, hipStream_t st);
 // d = 4096, b_small = 2 (kernels_n4k.hip): sm4 holds nside N 1024 packed words; sink 4096 words.
 // With frag (a scheme whose geometry has Lp = L and qperm), planes k >= 1 are also
 // written as operand rows row0[side] + k - 1, as decompose_fused does for d = 1024.

@@ -48,6 +48,7 @@ struct lf_ctx {
   uint32_t *smg = nullptr;      // packed coefficients for the fused decomposition
   size_t smg_elems = 0;
   size_t smg_sides_n = 0;       // N when smg holds both sides of the last fused d = 1024 fold_commit, else 0
+  size_t masks24_n = 0;         // N when fkeys holds both sides' Phi_72 digit masks of the last fold_commit, else 0
   uint32_t *fkeys = nullptr;    // coefficient-form fold: digit keys [2 N][K][64] (fold_coeff.hip)
   size_t fkeys_elems = 0;
   uint64_t *faux = nullptr;     // coefficient-form fold: rho coefficients, byte tables, the not-short flag
@@ -408,6 +409,12 @@ int decompose_n4k_sides(lf_ctx *c, const Tables *t, int nside, const uint64_t *c
   return LF_OK;
 }
 
+// LATTICEUM_AMD_FOLD=slot: always fold f_0 in NTT form (k_fold_nega, k_fold_phi72), never in coefficient form
+bool coeff_fold_enabled() {
+  const char *e = getenv("LATTICEUM_AMD_FOLD");
+  return !(e && !strcmp(e, "slot"));
+}
+
 int fold_nvec(const lf_params *pr, bool commit_f) { return (commit_f ? 1 : 0) + 2 * (pr->K - 1); }
 
 int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lbs, size_t W,
@@ -436,6 +443,7 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
   // reads f_0's inputs from there (k_fold_frag)
   const bool no_fk = !b->fk[0] && !b->fk[1];
   c->fold_from_frag = false;
+  c->masks24_n = 0;
   if (no_fk) {
     if (!fused || fv) return fail(c, LF_ERR_INVALID_ARG, "f_k buffers may be omitted only on the fused X^1024+1 path");
     if (extra + 2 * (K - 1) + 2 > LF_MAX_VECS) return fail(c, LF_ERR_INVALID_ARG, "too many operand rows");
@@ -476,15 +484,21 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
     } else {
       lfk::FusedSides sd{};
       sd.nside = 2;
+      // b_small = 2: the digit masks for fold_finish's coefficient-form fold
+      const bool want_masks = lbs == 1 && coeff_fold_enabled();
+      if (want_masks) LF_TRY(grow(c, c->fkeys, c->fkeys_elems, 2 * 2 * (size_t)K * N));
       for (int s = 0; s < 2; s++) {
         sd.f_coeff[s] = fc_side[s];
         sd.f_coeff_k[s] = b->fk_coeff[s];
         sd.f_k[s] = b->fk[s];
         sd.w_ccs_k[s] = b->wk[s];
         sd.row0[s] = extra + s * (K - 1);
+        if (want_masks) sd.masks[s] = reinterpret_cast<uint2 *>(c->fkeys) + (size_t)s * K * N;
       }
       PhaseTimer pt(c, LF_PHASE_DECOMPOSE);  // both sides in one launch
-      LF_HIP(c, lfk::decompose_phi72_sides(sd, N, lb, L, lbs, K, c->d_err, c->frag, aj->geom.nch, c->cur));
+      bool masks = false;
+      LF_HIP(c, lfk::decompose_phi72_sides(sd, N, lb, L, lbs, K, c->d_err, c->frag, aj->geom.nch, c->cur, &masks));
+      c->masks24_n = masks ? N : 0;
     }
     lfk::VecPtrs vp{};
     if (fv) {
@@ -540,11 +554,6 @@ lfk::OutPtrs fold_dst(const lf_params *pr, const lf_fold_step_bufs *b, size_t kd
   return dst;
 }
 
-// LATTICEUM_AMD_FOLD=slot: always fold f_0 in NTT form (k_fold_nega), never in coefficient form
-bool coeff_fold_enabled() {
-  const char *e = getenv("LATTICEUM_AMD_FOLD");
-  return !(e && !strcmp(e, "slot"));
-}
 
 int fold_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lbs, size_t W,
                 const lf_fold_step_bufs *b, const uint64_t *cm_i) {
@@ -579,6 +588,30 @@ int fold_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
     }
     PhaseTimer pt(c, LF_PHASE_FROM_F);
     LF_HIP(c, lfk::from_fcoeff_n32(b->f0_coeff, W, lb, L, b->f0, b->w_ccs0, t->fwd, bad, c->cur));
+    LF_HIP(c, lfk::from_f(b->f0, N, d, lb, L, b->f0_coeff, b->w_ccs0, t->inv, c->cur, bad));
+    return LF_OK;
+  }
+  // Phi_72 after the wave-local decomposition: f_0 in coefficient form from its
+  // digit masks, then f_0 = CRT and w_ccs_0 (kernels.hip k_fold_coeff_phi72); a
+  // rho that is not short raises `bad`, which turns that kernel off and the
+  // NTT-form fold and Witness::from_f on
+  if (c->masks24_n == N && N && d == 24 && lbs == 1 && !c->fold_from_frag && coeff_fold_enabled()) {
+    const int nw = 2 * K;
+    LF_TRY(grow(c, c->faux, c->faux_elems, (size_t)nw * 13 + 1));
+    uint32_t *rc = reinterpret_cast<uint32_t *>(c->faux);  // 25 packed words per witness
+    int *bad = reinterpret_cast<int *>(c->faux + (size_t)nw * 13);
+    const uint2 *m = reinterpret_cast<const uint2 *>(c->fkeys);
+    {
+      PhaseTimer pt(c, LF_PHASE_FOLD);
+      LF_HIP(c, lfk::fold_phi72_rho(b->rho, nw, rc, bad, c->cur));
+      LF_HIP(c, lfk::fold_phi72_coeff(m, m + (size_t)K * N, rc, bad, N, K, L, lb, b->f0_coeff, b->f0, b->w_ccs0,
+                                      c->cur));
+      lfk::VecPtrs fx{};
+      for (int s = 0; s < 2; s++)
+        for (int k = 0; k < K; k++) fx.p[s * K + k] = b->fk[s] + (size_t)k * N * d;
+      LF_HIP(c, lfk::fold(b->rho, fx, nw, N, d, b->f0, c->cur, bad));
+    }
+    PhaseTimer pt(c, LF_PHASE_FROM_F);
     LF_HIP(c, lfk::from_f(b->f0, N, d, lb, L, b->f0_coeff, b->w_ccs0, t->inv, c->cur, bad));
     return LF_OK;
   }

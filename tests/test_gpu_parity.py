@@ -335,7 +335,7 @@ def test_dev_fold_step_gathering_contraction(ctx, monkeypatch):
     check_dev_fold_step(ctx, 1024, 37, 2)
 
 
-@pytest.mark.parametrize("variant", ["block", "nt0", "nt7"])
+@pytest.mark.parametrize("variant", ["block", "nt0", "nt7", "slotfold"])
 @pytest.mark.parametrize("W", [10, 17, 70])
 def test_dev_fold_step_phi72_decomposition_variants(ctx, monkeypatch, variant, W):
     """Phi_72: the block-wide decomposition (LATTICEUM_AMD_DEC24=block) and the
@@ -344,6 +344,8 @@ def test_dev_fold_step_phi72_decomposition_variants(ctx, monkeypatch, variant, W
     W = 17 leaves a 16-group unit with one live group"""
     if variant == "block":
         monkeypatch.setenv("LATTICEUM_AMD_DEC24", "block")
+    elif variant == "slotfold":  # f_0 from the NTT-form planes (k_fold_phi72) instead of the digit masks
+        monkeypatch.setenv("LATTICEUM_AMD_FOLD", "slot")
     else:
         monkeypatch.setenv("LATTICEUM_AMD_DEC24_NT", variant[2:])
     check_dev_fold_step(ctx, 24, W, 3)
@@ -354,6 +356,16 @@ def test_dev_fold_step_ntt_form_fold(ctx, monkeypatch):
     instead of in coefficient form on the matrix cores (fold_coeff.hip)"""
     monkeypatch.setenv("LATTICEUM_AMD_FOLD", "slot")
     check_dev_fold_step(ctx, 1024, 37, 2)
+
+
+@pytest.mark.parametrize("W", [3, 17, 70])
+def test_dev_fold_step_phi72_rho_not_short(ctx, W):
+    """Phi_72: rho with full-size coefficients turns the coefficient-form fold
+    (k_fold_coeff_phi72) off through its device flag and the NTT-form fold and
+    Witness::from_f on; a short rho on the same context folds from the masks again"""
+    d, K = 24, params(24).K
+    check_dev_fold_step(ctx, d, W, 3, rho=rand(2 * K * d, 5151 + W))
+    check_dev_fold_step(ctx, d, W, 3)
 
 
 @pytest.mark.parametrize("W", [2, 7, 130])
