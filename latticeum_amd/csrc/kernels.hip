@@ -1017,22 +1017,29 @@ __global__ void __launch_bounds__(256) k_fold_coeff_phi72(const uint2 *masks0, c
                                                           uint64_t *w_ccs0) {
   if (*bad) return;  // uniform: a challenge is not short, the NTT-form fold runs instead
   extern __shared__ uint64_t lds[];  // [G L][24] f0 elements, then the 2K x 25 packed rho words
-  const int G = blockDim.x / L, t = threadIdx.x, nw = 2 * K;
+  // PW_SPLIT lanes per element (consecutive, one quad): lane h takes witnesses
+  // h, h + PW_SPLIT, ..; their partial sums meet by two xor-shuffles
+  constexpr int PW_SPLIT = 4;
+  const int G = blockDim.x / (PW_SPLIT * L), t = threadIdx.x, nw = 2 * K, h = t & (PW_SPLIT - 1);
   uint32_t *rl = reinterpret_cast<uint32_t *>(lds + (size_t)G * L * 24);
   for (int q = t; q < nw * RHO24_WORDS; q += blockDim.x) rl[q] = rc[q];
   __syncthreads();
   const size_t W = N / L, j0 = (size_t)blockIdx.x * G;
-  const size_t e = j0 * L + t;
-  if (t < G * L && e < N) {
+  const int el = t / PW_SPLIT;  // element within the block
+  const size_t e = j0 * L + el;
+  const bool live = el < G * L && e < N;
+  {
     s16x2 acc2[24];
 #pragma unroll
     for (int q = 0; q < 24; q++) acc2[q] = (s16x2){0, 0};
     // the next witness's masks load while this one's products run
-    auto mask_of = [&](int i) { return (i < K ? masks0 : masks1)[(size_t)(i < K ? i : i - K) * N + e]; };
-    uint2 mn = mask_of(0);
-    for (int i = 0; i < nw; i++) {
+    auto mask_of = [&](int i) {
+      return live ? (i < K ? masks0 : masks1)[(size_t)(i < K ? i : i - K) * N + e] : make_uint2(0u, 0u);
+    };
+    uint2 mn = mask_of(h);
+    for (int i = h; i < nw; i += PW_SPLIT) {
       const uint2 m = mn;
-      if (i + 1 < nw) mn = mask_of(i + 1);
+      if (i + PW_SPLIT < nw) mn = mask_of(i + PW_SPLIT);
       s16x2 r[RHO24_WORDS];
 #pragma unroll
       for (int u = 0; u < RHO24_WORDS; u++) r[u] = __builtin_bit_cast(s16x2, rl[i * RHO24_WORDS + u]);
@@ -1051,6 +1058,14 @@ __global__ void __launch_bounds__(256) k_fold_coeff_phi72(const uint2 *masks0, c
         }
       }
     }
+    // sum over the quad (exact in 16 bits: the total is the one bounded above)
+#pragma unroll
+    for (int q = 0; q < 24; q++) {
+      uint32_t v = __builtin_bit_cast(uint32_t, acc2[q]);
+      v = __builtin_bit_cast(uint32_t, acc2[q] + __builtin_bit_cast(s16x2, (uint32_t)__shfl_xor((int)v, 1)));
+      acc2[q] = __builtin_bit_cast(s16x2, v) + __builtin_bit_cast(s16x2, (uint32_t)__shfl_xor((int)v, 2));
+    }
+    if (live && h == 0) {
     int32_t acc[48];
 #pragma unroll
     for (int q = 0; q < 24; q++) {
@@ -1076,7 +1091,8 @@ __global__ void __launch_bounds__(256) k_fold_coeff_phi72(const uint2 *masks0, c
 #pragma unroll
     for (int u = 0; u < 12; u++) df[u] = make_ulonglong2(c[2 * u], c[2 * u + 1]);
 #pragma unroll
-    for (int u = 0; u < 24; u++) lds[t * 24 + u] = c[u];
+    for (int u = 0; u < 24; u++) lds[el * 24 + u] = c[u];
+    }
   }
   __syncthreads();
   const size_t ng = W - j0 < (size_t)G ? W - j0 : (size_t)G;
@@ -1099,11 +1115,12 @@ hipError_t fold_phi72_coeff(const uint2 *masks0, const uint2 *masks1, const uint
                             int K, int L, int lb, uint64_t *f0_coeff, uint64_t *f0, uint64_t *w_ccs0, hipStream_t st) {
   const size_t W = N / L;
   if (W == 0) return hipSuccess;
-  if (L < 1 || L > 256 || K < 1 || 2 * K > 64) return hipErrorInvalidValue;
-  const int G = 256 / L;
+  if (L < 1 || L > 64 || K < 1 || 2 * K > 64) return hipErrorInvalidValue;
+  const int G = 256 / (4 * L);  // 4 lanes per element (k_fold_coeff_phi72's PW_SPLIT)
+  if (G < 1) return hipErrorInvalidValue;
   const size_t lds = (size_t)G * L * 24 * 8 + (size_t)2 * K * RHO24_WORDS * 4;
-  hipLaunchKernelGGL(k_fold_coeff_phi72, dim3((unsigned)((W + G - 1) / G)), dim3(G * L), lds, st, masks0, masks1, rc, bad, N, K,
-                     L, lb, f0_coeff, f0, w_ccs0);
+  hipLaunchKernelGGL(k_fold_coeff_phi72, dim3((unsigned)((W + G - 1) / G)), dim3(4 * G * L), lds, st, masks0, masks1,
+                     rc, bad, N, K, L, lb, f0_coeff, f0, w_ccs0);
   return hipGetLastError();
 }
 
