@@ -671,11 +671,14 @@ bool mfma_from_vectors(const FragGeom &g, int d) {
 size_t frag_elems(const FragGeom &g, int d) { return (size_t)mfma_dim(d) * g.nch * 8 * 64; }  // uint4 per buffer
 int mfma_ktiles(size_t kappa) { return (int)((kappa + 31) / 32); }
 // chunks per column split: AJ_CPS for wide rings; for few virtual slots (Phi_72)
-// enough splits that about 2048 waves run
+// enough splits that about 1024 waves run
 int mfma_cps(const FragGeom &g, int d) {
   const int dv = mfma_dim(d);
   if (dv >= 256) return AJ_CPS;
-  const int want = 2048 / dv > 1 ? 2048 / dv : 1;
+  // about 1024 waves: Phi_72 at the zkvm shape, 4 streams, measured the same
+  // at 1024 and 2048 waves and worse at 4096 / 8192 (one stream: 0.41 ms at
+  // 1024 against 0.42, 0.44, 0.47; tools/gpu_p24w.sh)
+  const int want = 1024 / dv > 1 ? 1024 / dv : 1;
   const int cps = (g.nch + want - 1) / want;
   return cps < 1 ? 1 : (cps > AJ_CPS ? AJ_CPS : cps);
 }
