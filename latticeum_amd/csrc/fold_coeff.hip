@@ -149,8 +149,12 @@ __device__ __forceinline__ v4i tile_a(const uint8_t *ri, int o, int sh) {
 constexpr int FC_MAXW = 30;  // 2K <= 30
 // A block (4 waves) owns 32 elements (MFMA columns) at a time; wave w the rows
 // 256 w .. 256 w + 255 (row tiles t = 8 w + tt). Grid-stride over element tiles.
+// ks_n > 1 (few elements: fewer 32-element tiles than the chip has block
+// slots): task (tile, ks) sums only witnesses [ks nw / ks_n, (ks + 1) nw / ks_n)
+// and writes its exact int32 partials to part[ks][e][1024]; k_fold_coeff_sum
+// adds them up
 __global__ void __launch_bounds__(256, 2) k_fold_coeff(const uint32_t *keys, const uint8_t *tab_g, const int *bad,
-                                                      size_t N, int K, uint64_t *f0c) {
+                                                      size_t N, int K, uint64_t *f0c, int ks_n, int32_t *part) {
   __shared__ __attribute__((aligned(16))) uint8_t rt[FC_MAXW * FOLD_RT];
   __shared__ uint32_t lut[256];
   if (*bad) return;  // rho not short: the NTT-form fold runs instead
@@ -171,7 +175,9 @@ __global__ void __launch_bounds__(256, 2) k_fold_coeff(const uint32_t *keys, con
   // A tile of diagonal dl = t - q for this lane: bytes o .. o + 15, o = obase - 32 dl
   const int obase = 1024 + 16 * h - col;
   const size_t ntile = (N + 31) / 32;
-  for (size_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+  for (size_t task = blockIdx.x; task < ntile * ks_n; task += gridDim.x) {
+    const size_t tile = task / ks_n;
+    const int ks = (int)(task % ks_n), iq0 = 4 * (ks * nw / ks_n), iq1 = 4 * ((ks + 1) * nw / ks_n);
     const size_t e = tile * 32 + col, ee = e < N ? e : N - 1;
     const uint32_t *kb0 = keys + ee * K * FC_KEYROW + 32 * h, *kb1 = keys + (N + ee) * K * FC_KEYROW + 32 * h;
     v16i acc[8];
@@ -187,11 +193,11 @@ __global__ void __launch_bounds__(256, 2) k_fold_coeff(const uint32_t *keys, con
     };
     uint4 kn0, kn1;
     {
-      const uint4 *p = reinterpret_cast<const uint4 *>(kaddr(0));
+      const uint4 *p = reinterpret_cast<const uint4 *>(kaddr(iq0));
       kn0 = p[0];
       kn1 = p[1];
     }
-    for (int iq = 0; iq < 4 * nw; iq++) {
+    for (int iq = iq0; iq < iq1; iq++) {
       const int i = iq >> 2;
       const uint8_t *ri = rt + i * FOLD_RT;
       if ((iq & 3) == 0) {  // a new plane: slots 1..7 take diagonals 8 w + 1 .. 8 w + 7
@@ -200,7 +206,7 @@ __global__ void __launch_bounds__(256, 2) k_fold_coeff(const uint32_t *keys, con
       }
       const uint32_t kw[8] = {kn0.x, kn0.y, kn0.z, kn0.w, kn1.x, kn1.y, kn1.z, kn1.w};
       {
-        const uint4 *p = reinterpret_cast<const uint4 *>(kaddr(iq + 1 < 4 * nw ? iq + 1 : iq));
+        const uint4 *p = reinterpret_cast<const uint4 *>(kaddr(iq + 1 < iq1 ? iq + 1 : iq));
         kn0 = p[0];
         kn1 = p[1];
       }
@@ -219,7 +225,15 @@ __global__ void __launch_bounds__(256, 2) k_fold_coeff(const uint32_t *keys, con
           acc[tt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[(tt - qi) & 7], b, acc[tt], 0, 0, 0);
       }
     }
-    if (e < N) {
+    if (e < N && ks_n > 1) {
+      int32_t *out = part + ((size_t)ks * N + e) * FD + 256 * wv + 4 * h;
+#pragma unroll
+      for (int tt = 0; tt < 8; tt++)
+#pragma unroll
+        for (int g = 0; g < 4; g++)
+          *reinterpret_cast<v4i *>(out + 32 * tt + 8 * g) =
+              (v4i){acc[tt][4 * g], acc[tt][4 * g + 1], acc[tt][4 * g + 2], acc[tt][4 * g + 3]};
+    } else if (e < N) {
       // lane (col, h), acc[tt][4 g + r]: row 32 (8 w + tt) + 8 g + 4 h + r of element e
       uint64_t *out = f0c + e * FD + 256 * wv + 4 * h;
       auto fe = [](int x) { return x < 0 ? (uint64_t)(int64_t)x + gl::P : (uint64_t)x; };
@@ -234,7 +248,29 @@ __global__ void __launch_bounds__(256, 2) k_fold_coeff(const uint32_t *keys, con
     }
   }
 }
+// f0c[e][c] = sum_ks part[ks][e][c] (exact: the full sum is the bounded one), canonical
+__global__ void k_fold_coeff_sum(const int32_t *part, int ks_n, size_t n, const int *bad, uint64_t *f0c) {
+  if (*bad) return;
+  const size_t q = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // 4 coefficients
+  if (q >= n / 4) return;
+  v4i s = *reinterpret_cast<const v4i *>(part + 4 * q);
+  for (int k = 1; k < ks_n; k++) s += *reinterpret_cast<const v4i *>(part + (size_t)k * n + 4 * q);
+  auto fe = [](int x) { return x < 0 ? (uint64_t)(int64_t)x + gl::P : (uint64_t)x; };
+  ulonglong2 *o = reinterpret_cast<ulonglong2 *>(f0c + 4 * q);
+  o[0] = make_ulonglong2(fe(s[0]), fe(s[1]));
+  o[1] = make_ulonglong2(fe(s[2]), fe(s[3]));
+}
 }  // namespace
+
+// witness splits for N elements: enough (tile, split) tasks for two blocks per
+// CU, the splits dividing the 2K witnesses evenly (1 at the bench's W = 2^14)
+int fold_coeff_splits(size_t N, int K, int ncu) {
+  const size_t ntile = (N + 31) / 32, cap = 2 * (size_t)ncu;
+  int best = 1;
+  for (int ks = 2; ks <= 2 * K; ks++)
+    if ((2 * K) % ks == 0 && ntile * ks <= cap) best = ks;
+  return best;
+}
 
 hipError_t fold_keys(const uint32_t *smg, size_t ncol, int K, uint32_t *keys, hipStream_t st) {
   if (K < 1 || K > 15) return hipErrorInvalidValue;
@@ -255,12 +291,18 @@ hipError_t fold_rho_tables(const uint64_t *rho, int nw, uint64_t *rc, uint8_t *t
 }
 
 hipError_t fold_coeff(const uint32_t *keys, const uint8_t *tab, const int *bad, size_t N, int K, uint64_t *f0c,
-                      int ncu, hipStream_t st) {
+                      int ncu, hipStream_t st, int32_t *part) {
   if (K < 1 || 2 * K > FC_MAXW || ncu < 1) return hipErrorInvalidValue;
   if (!N) return hipSuccess;
-  const size_t ntile = (N + 31) / 32, cap = 2 * (size_t)ncu;  // two blocks per CU (LDS 63 KB, 256 registers)
-  hipLaunchKernelGGL(k_fold_coeff, dim3((unsigned)(ntile < cap ? ntile : cap)), dim3(256), 0, st, keys, tab, bad, N,
-                     K, f0c);
+  const int ks_n = part ? fold_coeff_splits(N, K, ncu) : 1;
+  const size_t ntask = (N + 31) / 32 * ks_n, cap = 2 * (size_t)ncu;  // two blocks per CU (LDS 63 KB, 256 registers)
+  hipLaunchKernelGGL(k_fold_coeff, dim3((unsigned)(ntask < cap ? ntask : cap)), dim3(256), 0, st, keys, tab, bad, N,
+                     K, f0c, ks_n, part);
+  if (ks_n > 1) {
+    const size_t n = N * FD;
+    hipLaunchKernelGGL(k_fold_coeff_sum, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, part, ks_n, n, bad,
+                       f0c);
+  }
   return hipGetLastError();
 }
 

@@ -140,8 +140,11 @@ constexpr int FOLD_RT = 2080;
 hipError_t fold_keys(const uint32_t *smg, size_t ncol, int K, uint32_t *keys, hipStream_t st);
 hipError_t fold_rho_tables(const uint64_t *rho, int nw, uint64_t *rc, uint8_t *tab, int *bad,
                            const ring::NegaTables &inv, hipStream_t st);
+// part: fold_coeff_splits() N 1024 int32 of scratch for the witness-split partial
+// sums when there are few elements (or null: no split)
+int fold_coeff_splits(size_t N, int K, int ncu);
 hipError_t fold_coeff(const uint32_t *keys, const uint8_t *tab, const int *bad, size_t N, int K, uint64_t *f0c,
-                      int ncu, hipStream_t st);
+                      int ncu, hipStream_t st, int32_t *part = nullptr);
 // Witness::from_f given f's coefficients: f = NTT(f_coeff), w_ccs = recompose(f); gate: as fold_coeff
 hipError_t from_fcoeff_n32(const uint64_t *f_coeff, size_t W, int lb, int L, uint64_t *f, uint64_t *w_ccs,
                            const ring::NegaTables &fwd, const int *gate, hipStream_t st);

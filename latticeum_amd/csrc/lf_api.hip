@@ -52,6 +52,8 @@ struct lf_ctx {
   uint32_t *fkeys = nullptr;    // coefficient-form fold: digit keys [2 N][K][64] (fold_coeff.hip)
   size_t fkeys_elems = 0;
   uint64_t *faux = nullptr;     // coefficient-form fold: rho coefficients, byte tables, the not-short flag
+  int32_t *fpart = nullptr;     // coefficient-form fold with few elements: per witness-split partial sums
+  size_t fpart_elems = 0;
   size_t faux_elems = 0;
   uint64_t *sink = nullptr;     // 32 KiB row the fused decompositions store work past the end into
   int ncu = 0;                  // compute units of `device`
@@ -580,7 +582,11 @@ int fold_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       PhaseTimer pt(c, LF_PHASE_FOLD);
       LF_HIP(c, lfk::fold_keys(c->smg, 2 * N, K, c->fkeys, c->cur));
       LF_HIP(c, lfk::fold_rho_tables(b->rho, nw, rc, tab, bad, t->inv, c->cur));
-      LF_HIP(c, lfk::fold_coeff(c->fkeys, tab, bad, N, K, b->f0_coeff, c->ncu, c->cur));
+      // LATTICEUM_AMD_FOLD_SPLIT=0: one task per 32-element tile even when there are few tiles
+      const char *fs = getenv("LATTICEUM_AMD_FOLD_SPLIT");
+      const int ks_n = fs && !strcmp(fs, "0") ? 1 : lfk::fold_coeff_splits(N, K, c->ncu);
+      if (ks_n > 1) LF_TRY(grow(c, c->fpart, c->fpart_elems, (size_t)ks_n * N * 1024));
+      LF_HIP(c, lfk::fold_coeff(c->fkeys, tab, bad, N, K, b->f0_coeff, c->ncu, c->cur, ks_n > 1 ? c->fpart : nullptr));
       lfk::VecPtrs fx{};
       for (int s = 0; s < 2; s++)
         for (int k = 0; k < K; k++) fx.p[s * K + k] = b->fk[s] + (size_t)k * N * d;
@@ -762,6 +768,7 @@ void lf_ctx_destroy(lf_ctx *c) {
   if (c->smg) (void)hipFree(c->smg);
   if (c->fkeys) (void)hipFree(c->fkeys);
   if (c->faux) (void)hipFree(c->faux);
+  if (c->fpart) (void)hipFree(c->fpart);
   if (c->sink) (void)hipFree(c->sink);
   if (c->stage) (void)hipFree(c->stage);
   if (c->limb) (void)hipFree(c->limb);
