@@ -143,12 +143,16 @@ def load_traffic(d, W, kappa):
     """PMC-measured HBM bytes per launch (profiles/pmc_traffic.json, written by
     tools/prof_summary.py traffic from separate FETCH_SIZE / WRITE_SIZE passes of
     this same configuration); {} when absent or for another configuration."""
-    f = ROOT / "profiles" / "pmc_traffic.json"
-    try:
-        doc = json.loads(f.read_text())
-    except (OSError, ValueError):
-        return {}
-    if doc.get("config") != {"d": d, "W": W, "kappa": kappa}:
+    doc = None
+    for name in ("pmc_traffic.json", f"pmc_traffic_d{d}.json"):  # the default workload's, then a side config's
+        try:
+            cand = json.loads((ROOT / "profiles" / name).read_text())
+        except (OSError, ValueError):
+            continue
+        if cand.get("config") == {"d": d, "W": W, "kappa": kappa}:
+            doc = cand
+            break
+    if doc is None:
         return {}
     t = {k: v["hbm_bytes_per_launch"] for k, v in doc.get("kernels", {}).items()}
     # a kernel launched as one template instance (k_decompose_fused<true>,

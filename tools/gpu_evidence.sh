@@ -21,6 +21,15 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$TAG -o run
 rc=$?; echo "write rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python tools/prof_summary.py traffic gpurun_out/pmc_fetch_$TAG gpurun_out/pmc_write_$TAG \
   gpurun_out/pmc_traffic_$TAG.json 1024 16384 32 > /dev/null && cp gpurun_out/pmc_traffic_$TAG.json profiles/pmc_traffic.json
+# the reference ring (d = 24 at the zkvm shape, one stream): its own traffic file
+A24="--d 24 --w 19763 --kappa 32 --steps 8 --warmup 2 --no-cpu-baseline --no-small-shape"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc24_fetch_$TAG -o run --output-format csv -- \
+  python bench.py $A24 > gpurun_out/pmc24_fetch_$TAG.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc24_write_$TAG -o run --output-format csv -- \
+  python bench.py $A24 > gpurun_out/pmc24_write_$TAG.log 2>&1 && \
+python tools/prof_summary.py traffic gpurun_out/pmc24_fetch_$TAG gpurun_out/pmc24_write_$TAG \
+  gpurun_out/pmc_traffic_d24_$TAG.json 24 19763 32 > /dev/null && cp gpurun_out/pmc_traffic_d24_$TAG.json profiles/pmc_traffic_d24.json
+rc=$?; echo "d24 traffic rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
   SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_WAVES GRBM_GUI_ACTIVE -d gpurun_out/pmc_sq_$TAG -o run --output-format csv -- \
   python bench.py $ARGS > gpurun_out/pmc_sq_$TAG.log 2>&1
