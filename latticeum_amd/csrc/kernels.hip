@@ -1391,13 +1391,15 @@ hipError_t decompose_phi72_sides(const FusedSides &sd, size_t N, int lb, int L, 
   }
   if (lbs == 1 && L <= 8 && (L - 1) * lb < 62 && !dec24_block()) {
     const size_t nblk = (W + 15) / 16, waves = (size_t)sd.nside * nblk * ((K + 3) / 4);
-    // streaming stores for the f_coeff_k and f_k rows (mask 3): nothing in the
-    // step re-reads f_coeff_k, and the fold's one pass over f_k does not gain
-    // from them sitting in the caches (W = 19 763, 4 streams: 0.65 -> 0.53 ms per
-    // launch, 900 -> 1,045 steps/s; mask 7, the operand rows too, ties);
+    // streaming stores for the f_coeff_k, f_k and operand rows (mask 7):
+    // nothing in the step re-reads f_coeff_k or f_k (the fold reads the digit
+    // masks), and the contraction's one pass over the operand rows does not gain
+    // from them sitting in the caches either (W = 19 763, 4 streams: cached 0.65
+    // ms per launch, 900 steps/s; mask 3 0.50-0.53 ms; mask 7 0.47-0.49 ms with
+    // the contraction 0.385 -> 0.36 ms, 1,133-1,138 -> 1,141-1,150 steps/s);
     // LATTICEUM_AMD_DEC24_NT overrides the mask
     const char *nte = getenv("LATTICEUM_AMD_DEC24_NT");
-    const int ntm = nte ? atoi(nte) : 3;
+    const int ntm = nte ? atoi(nte) : 7;
     const dim3 grid((unsigned)((waves + 3) / 4));
 #define LF_PW(M)                                                                                          \
   case M:                                                                                                \

@@ -335,12 +335,12 @@ def test_dev_fold_step_gathering_contraction(ctx, monkeypatch):
     check_dev_fold_step(ctx, 1024, 37, 2)
 
 
-@pytest.mark.parametrize("variant", ["block", "nt0", "nt7", "slotfold"])
+@pytest.mark.parametrize("variant", ["block", "nt0", "nt3", "slotfold"])
 @pytest.mark.parametrize("W", [10, 17, 70])
 def test_dev_fold_step_phi72_decomposition_variants(ctx, monkeypatch, variant, W):
     """Phi_72: the block-wide decomposition (LATTICEUM_AMD_DEC24=block) and the
     wave-local one with other streaming-store masks give the oracle's step too
-    (the default, wave-local with mask 3, is test_dev_fold_step_matches_oracle);
+    (the default, wave-local with mask 7, is test_dev_fold_step_matches_oracle);
     W = 17 leaves a 16-group unit with one live group"""
     if variant == "block":
         monkeypatch.setenv("LATTICEUM_AMD_DEC24", "block")
