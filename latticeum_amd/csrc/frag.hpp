@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace lfk {
 
@@ -98,6 +99,13 @@ __device__ __forceinline__ void out_store(T *p, T v) {
 }
 // outputs above this many bytes per launch are written with streaming stores
 constexpr size_t STREAM_OUT_BYTES = (size_t)4 << 30;
+// LATTICEUM_AMD_DEC_NT=1 / 0: the fused decompositions always / never use them
+inline bool dec_streaming(size_t out_bytes) {
+  const char *e = getenv("LATTICEUM_AMD_DEC_NT");
+  if (e && e[0] == '1') return true;
+  if (e && e[0] == '0') return false;
+  return out_bytes > STREAM_OUT_BYTES;
+}
 
 // vector-major operand layout (uint4 index of digit 0; digit k adds 4k, chunk c adds c FV_CHUNK)
 constexpr size_t FV_CHUNK = 32 * 2 * 8 * 4;
