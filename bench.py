@@ -115,7 +115,7 @@ def kernel_names(LA, d, W, layout, keep_fk=True):
 def _kernel_names(LA, d, W, layout, keep_fk=True):
     if d == 24:
         block = os.environ.get("LATTICEUM_AMD_DEC24") == "block"
-        cf24 = not block and keep_fk and os.environ.get("LATTICEUM_AMD_FOLD") != "slot"
+        cf24 = not block and os.environ.get("LATTICEUM_AMD_FOLD") != "slot"
         return {"decompose": "k_decompose_phi72" if block else "k_decompose_phi72_w",
                 "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_phi72",
                 "fold": "k_fold_coeff_phi72" if cf24 else "k_fold_phi72", "from_w_ccs": "k_from_w_ccs_phi72",
@@ -267,11 +267,16 @@ class Workload:
     side and rho (shared, read-only), and `streams` independent step streams,
     each an lf context on its own HIP stream with its own w_ccs and outputs."""
 
-    def __init__(self, LA, torch, local, rank, d, W, kappa, streams, seed_a=SEED_A, keep_fk=True, cu_partition=False):
+    def __init__(self, LA, torch, local, rank, d, W, kappa, streams, seed_a=SEED_A, keep_fk=True, cu_partition=False,
+                 packed=None):
         # keep_fk=False (fused X^1024+1 path only): the decomposed planes live only
         # as MFMA operand rows (lf.h: f_k buffers omitted) -- 20 GB less HBM at
-        # W = 2^14, but slower (DESIGN.md section 7), so the bench keeps f_k
-        self.keep_fk = keep_fk
+        # W = 2^14, but slower (DESIGN.md section 7), so the bench keeps f_k.
+        # packed (default for d = 24): the decomposed witnesses are kept as packed
+        # digit planes (lf_fold_step_bufs.planes, 8 B per element and plane) instead
+        # of u64 f_k / f_coeff_k rows (2 x 192 B); lf_dev_expand_planes makes the rows
+        self.packed = packed = (d == 24) if packed is None else packed
+        self.keep_fk = keep_fk and not packed
         self.LA, self.torch = LA, torch
         self.d, self.W, self.kappa = d, W, kappa
         self.pr = pr = LA.goldilocks_dp(d)
@@ -315,10 +320,11 @@ class Workload:
             keep = {
                 "w_ccs": w_ccs, "acc_cm": acc_cm, "acc_f_coeff": acc_fc, "rho": rho,
                 "f_coeff": z(N * d), "f": z(N * d), "cm": z(kappa * d),
-                "fk_coeff": [z(K * N * d) for _ in range(2)],
-                "fk": [z(K * N * d) for _ in range(2)] if keep_fk else [None, None],
+                "fk_coeff": [z(K * N * d) for _ in range(2)] if not packed else [None, None],
+                "fk": [z(K * N * d) for _ in range(2)] if self.keep_fk else [None, None],
                 "wk": [z(K * W * d) for _ in range(2)], "y": [z(K * kappa * d) for _ in range(2)],
                 "f0": z(N * d), "f0_coeff": z(N * d), "w_ccs0": z(W * d), "cm0": z(kappa * d),
+                "planes": [z(K * N) for _ in range(2)] if packed else [None, None],
             }
             bufs = LA.LfFoldStepBufs()
             for k, v in keep.items():
@@ -412,7 +418,7 @@ def phase_report(LA, wl, tot, steps):
     bytes, achieved GB/s and fraction of HBM peak; the dominant phase's roofline"""
     d, W, kappa = wl.d, wl.W, wl.kappa
     _, alg, operand = algorithmic_bytes(d, W, kappa, wl.pr.L, wl.pr.K)
-    if not wl.keep_fk:  # the planes are written once, as the operand rows: no bytes beyond B2
+    if not wl.keep_fk and not wl.packed:  # the planes are written once, as the operand rows: no bytes beyond B2
         operand["decompose"] = 0
     kernel_of = kernel_names(LA, d, W, wl.sch.layout, wl.keep_fk)
     traffic = load_traffic(d, W, kappa)
@@ -429,6 +435,14 @@ def phase_report(LA, wl, tot, steps):
         cf24 = ph == "fold" and kernel_of[ph] == "k_fold_coeff_phi72"
         if cf:  # the coefficient-form fold never reads the 2K NTT-form planes (B4): count what it moves
             a = wl.N * (2 * 2048 + 2 * 2 * wl.pr.K * 256 + 8 * 1024)  # packed digits in, keys out + in, f0_coeff out
+        if ph == "decompose" and wl.packed:
+            # B2 counts the u64 f_k / f_coeff_k rows the reference materialises; this
+            # launch writes them as packed planes (8 B per element and plane) instead
+            phases_note = {"packed_planes": True,
+                           "moved_bytes_per_launch": sides * (wl.N * 8 * d + wl.pr.K * wl.N * 8
+                                                                + wl.pr.K * W * 8 * d) + operand.get(ph, 0) * sides}
+        else:
+            phases_note = {}
         if cf24:  # digit masks in (8 B per element and plane); f0_coeff, f0 (E each) and w_ccs0 out (from_f's outputs)
             a = wl.N * (2 * wl.pr.K * 8 + 2 * 8 * d) + wl.W * 8 * d
         gbs = a / (avg * 1e-3) / 1e9
@@ -439,7 +453,7 @@ def phase_report(LA, wl, tot, steps):
                       "operand_bytes_per_launch": extra,
                       "achieved_gbs_incl_operands": (a + extra) / (avg * 1e-3) / 1e9,
                       "traffic_bytes_per_launch": traffic.get(kernel_of[ph]),
-                      "valu_busy": valu.get(kernel_of[ph])}
+                      "valu_busy": valu.get(kernel_of[ph]), **phases_note}
         if cf:
             # an exact i8 GEMM: 1024 coefficients x 2K 1024 digit rows x N elements
             macs = 1024 * 2 * wl.pr.K * 1024 * wl.N

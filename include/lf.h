@@ -31,7 +31,9 @@
  *   zkvm/src/main.rs:348-367  commit()                          -> lf_commit
  *   zkvm/src/main.rs:380-404  fold() (its commit+fold arithmetic) -> lf_fold_hot /
  *                                                                 lf_dev_fold_step
- *   zkvm/src/commitments.rs:192-262 memory Merkle trees     -> lf_dev_merkle_tree, lf_merkle_open
+ *   zkvm/src/commitments.rs:192-340 vm_mem_comm, vm_mem_comm_with_opening, vm_code_comm
+ *                                                              -> lf_vm_mem_comm, lf_dev_merkle_tree,
+ *                                                                 lf_merkle_open, lf_vm_code_comm
  *   latticefold/src/nifs.rs:28-34 LFProof (ark CanonicalSerialize) -> lf_lfproof_serialize,
  *       zkvm/src/main.rs:231-234 (serialized_size)                lf_lcccs_(de)serialize
  *   zkvm/src/main.rs:121-219  the proving loop, sharded over GPUs (SURVEY.md 8(b)
@@ -251,7 +253,18 @@ typedef struct {
   uint64_t *f0, *f0_coeff;     /* N each: folded witness */
   uint64_t *w_ccs0;            /* W */
   uint64_t *cm0;               /* kappa */
+  /* d = 24 with b_small = 2 (optional, both sides or neither): the decomposed
+   * witnesses as packed digit planes [K][N], one u64 per element and plane:
+   * bit i = coefficient i is nonzero, bit 32 + i = it is -1. With fk and
+   * fk_coeff all NULL they are the planes' only form (the u64 rows, 2 x 192 B
+   * per element and plane, are not written; lf_dev_expand_planes makes them). */
+  uint64_t *planes[2];
 } lf_fold_step_bufs;
+/* packed Phi_72 digit planes (lf_fold_step_bufs.planes; n elements) -> the
+ * Witness forms of decompose_witness's outputs (decomposition.rs:162-167,
+ * arith.rs:324-338): f_coeff (digits mod p) and / or f = CRT(f_coeff); either
+ * output may be NULL */
+int lf_dev_expand_planes(lf_ctx *ctx, int d, const uint64_t *planes, size_t n, uint64_t *f_coeff, uint64_t *f);
 /* commit(z) followed by the commit+fold arithmetic of fold(), all on device */
 int lf_dev_fold_step(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, size_t W,
                      const lf_fold_step_bufs *b);
@@ -380,17 +393,35 @@ int lf_dev_mz_challenged(lf_ctx *ctx, const lf_ccs *M, const uint64_t *z, const 
 int lf_dev_mz_evaluate(lf_ctx *ctx, const lf_ccs *M, const uint64_t *z, int nz, int nv, const uint64_t *point,
                        uint64_t *out);
 
-/* ------------------------------------------------------------ width-8 Poseidon2 Merkle trees
- * zkvm/src/commitments.rs:192-262 (vm_mem_comm / _with_opening): Poseidon2Goldilocks<8>
- * (poseidon2.rs:31-49; external constants crypto_consts.rs:9-96; internal
- * diagonal = Plonky3 MATRIX_DIAG_8_GOLDILOCKS, not in the reference: parity
- * unpinned). A leaf is PaddingFreeSponge<8, rate 4, out 4> of one row, a parent
- * is TruncatedPermutation<2, 4, 8> of its children.
- *   nodes: (2 nrows - 1) x 4 words on the device, leaves first, root last
- *   path: log2(nrows) sibling digests (4 words each, host), leaves first */
+/* ------------------------------------------------------------ width-8 Poseidon2 commitments
+ * zkvm/src/commitments.rs:192-340, over Poseidon2Goldilocks<8> (poseidon2.rs:31-49;
+ * external constants crypto_consts.rs:9-96; internal diagonal = Plonky3
+ * MATRIX_DIAG_8_GOLDILOCKS, not in the reference: parity unpinned). A row hash is
+ * PaddingFreeSponge<8, rate 4, out 4>, a parent TruncatedPermutation<2, 4, 8> of its
+ * children; trees follow Plonky3 MerkleTree::new over one matrix (git 33e58c7787f9,
+ * not vendored): every layer below the root is padded to an even length with the
+ * zero digest, so any height works.
+ *   lf_dev_merkle_tree: vm_mem_comm_with_opening (:222-268; PAGE_COUNT rows of
+ *     WORDS_PER_PAGE words) and vm_code_comm (:314-340; a width-1 matrix of the
+ *     code's half-words, any height). nodes: lf_merkle_nodes_len(nrows) x 4 words on
+ *     the device (2 nrows - 1 for a power of two), padded layers leaves first, root last
+ *   lf_merkle_open: the sibling digest in every layer below the root (4 words each,
+ *     host), leaves first: open_batch's opening_proof (log2(nrows) for a power of two)
+ *   lf_vm_code_comm: vm_code_comm of `len` code bytes (host buffer) -> root
+ *   lf_dev_hash_w8_rows: independent sponge hashes of nrows rows (the leaf layer)
+ *   lf_hash_w8 / lf_vm_mem_comm (host, sequential): vm_mem_comm (:192-217) gives
+ *     MerkleTree::new PAGE_COUNT one-row matrices, all of height 1, so its root is ONE
+ *     sponge over all pages' words in page order -- a strictly sequential chain of
+ *     nwords / 4 permutations that runs on the host (the device would run it on one
+ *     8-lane group) */
 int lf_dev_poseidon2_w8_permute(lf_ctx *ctx, uint64_t *states, size_t n);
+size_t lf_merkle_nodes_len(size_t nrows);
 int lf_dev_merkle_tree(lf_ctx *ctx, const uint64_t *rows, size_t nrows, size_t width, uint64_t *nodes);
 int lf_merkle_open(lf_ctx *ctx, const uint64_t *nodes, size_t nrows, size_t index, uint64_t *path);
+int lf_vm_code_comm(lf_ctx *ctx, const uint8_t *code, size_t len, uint64_t out4[4]);
+int lf_dev_hash_w8_rows(lf_ctx *ctx, const uint64_t *rows, size_t nrows, size_t width, uint64_t *out);
+void lf_hash_w8(const uint64_t *in, size_t n, uint64_t out4[4]);
+int lf_vm_mem_comm(const uint32_t *words, size_t nwords, uint64_t out4[4]);
 
 /* ------------------------------------------------------------ wire format
  * ark-serialize 0.5 CanonicalSerialize as derived on the reference's types

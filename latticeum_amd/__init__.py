@@ -285,6 +285,12 @@ class Context:
     def dev_eq_table(self, d: int, r, nv: int, out):
         self.check(self.lib.lf_dev_eq_table(self.h, d, _dptr(r), nv, _dptr(out)))
 
+    def dev_expand_planes(self, d, planes, n, f_coeff=None, f=None):
+        """packed Phi_72 digit planes (lf_fold_step_bufs.planes) -> f_coeff and / or f = CRT(f_coeff)"""
+        self.check(self.lib.lf_dev_expand_planes(self.h, d, _dptr(planes), n,
+                                                 _dptr(f_coeff) if f_coeff is not None else None,
+                                                 _dptr(f) if f is not None else None))
+
     def dev_get_fhat(self, d, f_coeff, N, nv, out):
         """Witness::get_fhat on the device: out [tau][2^nv][d] from f_coeff [N][d]"""
         self.check(self.lib.lf_dev_get_fhat(self.h, d, _dptr(f_coeff), N, nv, _dptr(out)))
@@ -317,13 +323,25 @@ class Context:
         self.check(self.lib.lf_dev_poseidon2_w8_permute(self.h, _dptr(t), t.numel() // 8))
 
     def dev_merkle_tree(self, rows, nrows: int, width: int, nodes):
-        """memory matrix [nrows][width] -> (2 nrows - 1) x 4 digests, root last"""
+        """matrix [nrows][width] -> merkle_nodes_len(nrows) x 4 digests (Plonky3's even-padded
+        layers), root last"""
         self.check(self.lib.lf_dev_merkle_tree(self.h, _dptr(rows), nrows, width, _dptr(nodes)))
 
     def merkle_open(self, nodes, nrows: int, index: int) -> np.ndarray:
-        path = np.zeros(4 * max(1, nrows.bit_length() - 1), np.uint64)
+        path = np.zeros(4 * max(1, merkle_depth(nrows)), np.uint64)
         self.check(self.lib.lf_merkle_open(self.h, _dptr(nodes), nrows, index, _ptr(path)))
-        return path
+        return path[:4 * merkle_depth(nrows)]
+
+    def dev_hash_w8_rows(self, rows, nrows: int, width: int, out):
+        """independent width-8 sponge hashes of nrows rows -> out [nrows][4]"""
+        self.check(self.lib.lf_dev_hash_w8_rows(self.h, _dptr(rows), nrows, width, _dptr(out)))
+
+    def vm_code_comm(self, code: bytes) -> np.ndarray:
+        """zkvm vm_code_comm (commitments.rs:314-340): Merkle root over the code's half-words"""
+        out = np.zeros(4, np.uint64)
+        buf = (C.c_uint8 * len(code)).from_buffer_copy(code)
+        self.check(self.lib.lf_vm_code_comm(self.h, buf, len(code), _ptr(out)))
+        return out
 
     def dev_poseidon2_permute(self, t):
         self.check(self.lib.lf_dev_poseidon2_permute(self.h, _dptr(t), t.numel() // 16))
@@ -555,7 +573,39 @@ def hash_iter(vals) -> np.ndarray:
     return out
 
 
+def merkle_nodes_len(nrows: int) -> int:
+    """digests in a tree over nrows rows (Plonky3's even-padded layers)"""
+    return load().lf_merkle_nodes_len(nrows)
+
+
+def merkle_depth(nrows: int) -> int:
+    """layers below the root (the length of an opening path)"""
+    n, k = (1 if nrows <= 1 else nrows + nrows % 2), 0
+    while n > 1:
+        n, k = (1 if n == 2 else (n // 2 + 1) & ~1), k + 1
+    return k
+
+
+def hash_w8(vals) -> np.ndarray:
+    """PaddingFreeSponge<Poseidon2Goldilocks<8>, 8, 4, 4>::hash_iter (host)"""
+    x = np.ascontiguousarray(np.asarray(vals, dtype=np.uint64)) if len(vals) else np.zeros(1, np.uint64)
+    out = np.zeros(4, np.uint64)
+    load().lf_hash_w8(_ptr(x), len(vals), _ptr(out))
+    return out
+
+
+def vm_mem_comm(words) -> np.ndarray:
+    """zkvm vm_mem_comm (commitments.rs:192-217): one width-8 sponge over every page's u32 words"""
+    w = np.ascontiguousarray(np.asarray(words, dtype=np.uint32))
+    out = np.zeros(4, np.uint64)
+    lib = load()
+    rc = lib.lf_vm_mem_comm(w.ctypes.data if w.size else None, w.size, _ptr(out))
+    if rc:
+        raise LfError(rc, lib.lf_status_string(rc).decode())
+    return out
+
+
 __all__ = ["Context", "AjtaiCommitmentScheme", "Communicator", "Comb", "CCSMatrices", "witness_split_w", "Poseidon2Transcript",
-           "LfParams", "LfFoldStepBufs",
+           "LfParams", "LfFoldStepBufs", "merkle_nodes_len", "merkle_depth", "hash_w8", "vm_mem_comm",
            "LfError", "goldilocks_dp", "short_challenge", "hash_iter", "P", "REPR_CANONICAL",
            "REPR_MONTGOMERY", "load"]

@@ -26,7 +26,7 @@ class LfFoldStepBufs(C.Structure):
         ("w_ccs", VP), ("acc_cm", VP), ("acc_f_coeff", VP), ("rho", VP),
         ("f_coeff", VP), ("f", VP), ("cm", VP),
         ("fk_coeff", VP * 2), ("fk", VP * 2), ("wk", VP * 2), ("y", VP * 2),
-        ("f0", VP), ("f0_coeff", VP), ("w_ccs0", VP), ("cm0", VP),
+        ("f0", VP), ("f0_coeff", VP), ("w_ccs0", VP), ("cm0", VP), ("planes", VP * 2),
     ]
 
 
@@ -121,11 +121,17 @@ SIGNATURES = {
     "lf_dev_poseidon2_w8_permute": (I, [VP, VP, SZ]),
     "lf_dev_merkle_tree": (I, [VP, VP, SZ, SZ, VP]),
     "lf_merkle_open": (I, [VP, VP, SZ, SZ, VP]),
+    "lf_merkle_nodes_len": (SZ, [SZ]),
+    "lf_dev_hash_w8_rows": (I, [VP, VP, SZ, SZ, VP]),
+    "lf_vm_code_comm": (I, [VP, VP, SZ, VP]),
+    "lf_hash_w8": (None, [VP, SZ, VP]),
+    "lf_vm_mem_comm": (I, [VP, SZ, VP]),
     "lf_lcccs_serialize": (I, [C.POINTER(LfLcccs), I, VP, SZ, C.POINTER(SZ)]),
     "lf_lcccs_deserialize": (I, [VP, SZ, I, I, VP, SZ, C.POINTER(LfLcccs)]),
     "lf_lfproof_serialize": (I, [C.POINTER(LfLfproof), I, VP, SZ, C.POINTER(SZ)]),
     "lf_dev_eq_table": (I, [VP, I, VP, I, VP]),
     "lf_dev_get_fhat": (I, [VP, I, VP, SZ, I, VP]),
+    "lf_dev_expand_planes": (I, [VP, I, VP, SZ, VP, VP]),
     "lf_ccs_create": (I, [VP, I, I, SZ, SZ, VP, VP, VP, I, C.POINTER(VP)]),
     "lf_ccs_destroy": (None, [VP]),
     "lf_dev_mz_mles": (I, [VP, VP, VP, I, I, VP]),

@@ -411,9 +411,13 @@ __device__ __forceinline__ void st16(ulonglong2 *p, ulonglong2 v) {
 __device__ __forceinline__ uint64_t pw_digit(uint32_t nz, uint32_t ng, int i) {
   return (nz >> i & 1) ? ((ng >> i & 1) ? gl::P - 1 : 1) : 0;
 }
-template <int NTM>  // streaming stores: bit 0 f_coeff_k, bit 1 f_k, bit 2 operand pieces
+// NTM: streaming stores, bit 0 f_coeff_k, bit 1 f_k, bit 2 operand pieces; bit 3:
+// packed planes only -- no u64 f_coeff_k / f_k rows, the decomposed witnesses
+// stay as the digit masks (lf_fold_step_bufs.planes, lf_dev_expand_planes)
+template <int NTM>
 __global__ void __launch_bounds__(256) k_decompose_phi72_w(FusedSides sd, size_t N, int lb, int L, int K, int *err,
                                                           uint4 *frag, int nch, size_t nblk) {
+  constexpr bool ROWS = !(NTM & 8);
   __shared__ uint64_t lds_all[4 * PW_WAVE_U64];
   const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
   uint64_t *S = lds_all + wib * PW_WAVE_U64;
@@ -473,6 +477,7 @@ __global__ void __launch_bounds__(256) k_decompose_phi72_w(FusedSides sd, size_t
       }
     if (sd.masks[side] && ok && kok) sd.masks[side][(size_t)k * N + g * L + l] = make_uint2(nz, ng);
     // f_coeff_k rows from the owners' masks
+    if constexpr (ROWS) {
     const int ln0 = opaque_lane();
 #pragma unroll
     for (int it = 0; it < 12; it++) {
@@ -485,11 +490,13 @@ __global__ void __launch_bounds__(256) k_decompose_phi72_w(FusedSides sd, size_t
                       make_ulonglong2(pw_digit(nzj, ngj, 2 * pq), pw_digit(nzj, ngj, 2 * pq + 1)));
       }
     }
+    }
     uint64_t c[24];
 #pragma unroll
     for (int i = 0; i < 24; i++) c[i] = pw_digit(nz, ng, i);
     ring::phi72_crt(c);
     // f_k rows through the tile
+    if constexpr (ROWS) {
 #pragma unroll
     for (int i = 0; i < 12; i++)
       *reinterpret_cast<ulonglong2 *>(S + lane * PW_RROW + 2 * i) = make_ulonglong2(c[2 * i], c[2 * i + 1]);
@@ -505,6 +512,7 @@ __global__ void __launch_bounds__(256) k_decompose_phi72_w(FusedSides sd, size_t
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the tile is read before the operand rounds reuse it
+    }
     if (frag) {
       const size_t u = G * L + l;  // contraction unit of these 16 columns
       const int ch = (int)(u >> 1), uh = (int)(u & 1);
@@ -967,6 +975,9 @@ __global__ void __launch_bounds__(256) k_fold_phi72(const uint64_t *rho, VecPtrs
   }
 }
 
+static inline unsigned blocks(size_t n, int t) { return (unsigned)((n + t - 1) / t); }
+static inline unsigned grid_cap(size_t n) { return (unsigned)(n < 65536 ? n : 65536); }
+
 // ============================================================ Phi_72 fold in coefficient form
 // The 2K folded witnesses are digit planes, f_i = CRT(D_i) with D_i in {-1, 0, 1}^24,
 // and get_rhos' challenges are short (coefficients in [-32, 31],
@@ -1124,6 +1135,96 @@ hipError_t fold_phi72_coeff(const uint2 *masks0, const uint2 *masks1, const uint
   return hipGetLastError();
 }
 
+// f_0 from the digit masks for any rho (the fallback of k_fold_coeff_phi72 when
+// the planes are kept packed, lf_fold_step_bufs.fk == NULL): the same ring
+// product in coefficient form, f0_coeff = sum_i ICRT(rho_i) * D_i mod p, one
+// thread per element, then f_0 = CRT(f0_coeff). Every block takes the 2K
+// inverse transforms of rho (and their negatives) into LDS itself.
+__global__ void __launch_bounds__(256) k_fold_phi72_masks(const uint2 *masks0, const uint2 *masks1, const uint64_t *rho,
+                                                          int K, size_t N, uint64_t *f0, const int *run_if) {
+  if (run_if && !*run_if) return;  // uniform: the short-challenge fold produced f_0
+  __shared__ uint64_t rc[2][64 * 24];  // [sign][witness][coefficient]
+  const int nw = 2 * K;
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) {
+    uint64_t c[24];
+#pragma unroll
+    for (int t = 0; t < 24; t++) c[t] = rho[(size_t)i * 24 + t];
+    ring::phi72_icrt(c);
+#pragma unroll
+    for (int t = 0; t < 24; t++) {
+      rc[0][i * 24 + t] = c[t];
+      rc[1][i * 24 + t] = gl::sub(0, c[t]);
+    }
+  }
+  __syncthreads();
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < N; e += (size_t)gridDim.x * blockDim.x) {
+    uint64_t acc[47];
+#pragma unroll
+    for (int t = 0; t < 47; t++) acc[t] = 0;
+    for (int i = 0; i < nw; i++) {
+      const uint2 m = (i < K ? masks0 : masks1)[(size_t)(i < K ? i : i - K) * N + e];
+#pragma unroll
+      for (int j = 0; j < 24; j++) {
+        if (!(m.x >> j & 1)) continue;
+        const uint64_t *r = rc[m.y >> j & 1] + i * 24;
+#pragma unroll
+        for (int t = 0; t < 24; t++) acc[j + t] = gl::add(acc[j + t], r[t]);
+      }
+    }
+    // X^24 = X^12 - 1 (as in k_fold_coeff_phi72)
+#pragma unroll
+    for (int s2 = 46; s2 >= 36; s2--) acc[s2 - 36] = gl::sub(acc[s2 - 36], acc[s2]);
+#pragma unroll
+    for (int s2 = 35; s2 >= 24; s2--) {
+      acc[s2 - 12] = gl::add(acc[s2 - 12], acc[s2]);
+      acc[s2 - 24] = gl::sub(acc[s2 - 24], acc[s2]);
+    }
+    ring::phi72_crt(acc);
+    ulonglong2 *df = reinterpret_cast<ulonglong2 *>(f0 + e * 24);
+#pragma unroll
+    for (int u = 0; u < 12; u++) df[u] = make_ulonglong2(acc[2 * u], acc[2 * u + 1]);
+  }
+}
+
+hipError_t fold_phi72_masks(const uint2 *masks0, const uint2 *masks1, const uint64_t *rho, int K, size_t N,
+                            uint64_t *f0, const int *run_if, hipStream_t st) {
+  if (N == 0) return hipSuccess;
+  if (K < 1 || 2 * K > 64) return hipErrorInvalidValue;
+  unsigned nb = blocks(N, 256);
+  if (run_if && nb > 1024) nb = 1024;  // usually returns at once
+  hipLaunchKernelGGL(k_fold_phi72_masks, dim3(nb), dim3(256), 0, st, masks0, masks1, rho, K, N, f0, run_if);
+  return hipGetLastError();
+}
+
+// packed Phi_72 digit planes (one u64 per element: bit i of the low word =
+// coefficient i is nonzero, of the high word = it is negative) -> the u64
+// witness forms f_coeff (the digits mod p) and f = CRT(f_coeff); either may be null
+__global__ void __launch_bounds__(256) k_expand_phi72(const uint2 *planes, size_t n, uint64_t *fc, uint64_t *f) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const uint2 m = planes[e];
+    uint64_t c[24];
+#pragma unroll
+    for (int i = 0; i < 24; i++) c[i] = pw_digit(m.x, m.y, i);
+    if (fc) {
+      ulonglong2 *o = reinterpret_cast<ulonglong2 *>(fc + e * 24);
+#pragma unroll
+      for (int u = 0; u < 12; u++) o[u] = make_ulonglong2(c[2 * u], c[2 * u + 1]);
+    }
+    if (f) {
+      ring::phi72_crt(c);
+      ulonglong2 *o = reinterpret_cast<ulonglong2 *>(f + e * 24);
+#pragma unroll
+      for (int u = 0; u < 12; u++) o[u] = make_ulonglong2(c[2 * u], c[2 * u + 1]);
+    }
+  }
+}
+
+hipError_t expand_phi72(const uint2 *planes, size_t n, uint64_t *fc, uint64_t *f, hipStream_t st) {
+  if (n == 0 || (!fc && !f)) return hipSuccess;
+  hipLaunchKernelGGL(k_expand_phi72, dim3(grid_cap(blocks(n, 256))), dim3(256), 0, st, planes, n, fc, f);
+  return hipGetLastError();
+}
+
 // ============================================================ Poseidon2-16
 // zkvm/src/poseidon2.rs:100-173 (+ Plonky3 add_rc_and_sbox_generic, matmul_internal)
 #include "p2_consts.inc"
@@ -1271,8 +1372,6 @@ __global__ void k_limb_join(const uint64_t *lo, const uint64_t *hi, size_t n, ui
 }
 
 // ============================================================ launchers
-static inline unsigned blocks(size_t n, int t) { return (unsigned)((n + t - 1) / t); }
-static inline unsigned grid_cap(size_t n) { return (unsigned)(n < 65536 ? n : 65536); }
 
 hipError_t transform(uint64_t *data, size_t n, int d, bool fwd, const ring::NegaTables &tb,
                      hipStream_t st) {
@@ -1399,13 +1498,27 @@ hipError_t decompose_phi72_sides(const FusedSides &sd, size_t N, int lb, int L, 
     // the contraction 0.385 -> 0.36 ms, 1,133-1,138 -> 1,141-1,150 steps/s);
     // LATTICEUM_AMD_DEC24_NT overrides the mask
     const char *nte = getenv("LATTICEUM_AMD_DEC24_NT");
-    const int ntm = nte ? atoi(nte) : 7;
+    int ntm = nte ? atoi(nte) : 7;
+    if (ntm < 0 || ntm > 7) return hipErrorInvalidValue;
+    // no f_coeff_k / f_k buffers: the planes stay packed (the masks must be kept)
+    bool rows = false, none = true;
+    for (int s = 0; s < sd.nside; s++) {
+      rows |= sd.f_k[s] != nullptr || sd.f_coeff_k[s] != nullptr;
+      none &= sd.f_k[s] == nullptr && sd.f_coeff_k[s] == nullptr;
+      if (!sd.f_k[s] != !sd.f_coeff_k[s]) return hipErrorInvalidValue;
+    }
+    if (rows && !none) return hipErrorInvalidValue;
+    if (none) {
+      for (int s = 0; s < sd.nside; s++)
+        if (!sd.masks[s]) return hipErrorInvalidValue;
+      ntm = 8 | (ntm & 4);
+    }
     const dim3 grid((unsigned)((waves + 3) / 4));
 #define LF_PW(M)                                                                                          \
   case M:                                                                                                \
     hipLaunchKernelGGL(k_decompose_phi72_w<M>, grid, dim3(256), 0, st, sd, N, lb, L, K, err, frag, nch, nblk); \
     break;
-    switch (ntm) { LF_PW(0) LF_PW(1) LF_PW(2) LF_PW(3) LF_PW(4) LF_PW(5) LF_PW(6) LF_PW(7) default: return hipErrorInvalidValue; }
+    switch (ntm) { LF_PW(0) LF_PW(1) LF_PW(2) LF_PW(3) LF_PW(4) LF_PW(5) LF_PW(6) LF_PW(7) LF_PW(8) LF_PW(12) default: return hipErrorInvalidValue; }
 #undef LF_PW
     if (masks_written) *masks_written = sd.masks[0] != nullptr && (sd.nside < 2 || sd.masks[1] != nullptr);
     return hipGetLastError();

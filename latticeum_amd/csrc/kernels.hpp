@@ -112,7 +112,9 @@ hipError_t decompose_n32(const uint64_t *f_coeff, size_t N, int lb, int L, int K
 // scratch for the packed coefficients
 struct FusedSides {
   const uint64_t *f_coeff[2];
-  uint64_t *f_coeff_k[2], *f_k[2], *w_ccs_k[2];  // f_k may be null (d = 1024: the planes stay in the operand rows)
+  // f_k may be null (d = 1024: the planes stay in the operand rows); d = 24: f_k and
+  // f_coeff_k both null keeps the planes packed (the masks below are then required)
+  uint64_t *f_coeff_k[2], *f_k[2], *w_ccs_k[2];
   int row0[2];                                   // operand row of plane 1 (planes 1 .. K-1 consecutive)
   int nside;
   int row_p0[2] = {-1, -1};                      // operand row of plane 0, or -1 (not written)
@@ -160,6 +162,11 @@ hipError_t decompose_phi72_sides(const FusedSides &sd, size_t N, int lb, int L, 
 hipError_t fold_phi72_rho(const uint64_t *rho, int nw, uint32_t *rc, int *bad, hipStream_t st);
 hipError_t fold_phi72_coeff(const uint2 *masks0, const uint2 *masks1, const uint32_t *rc, const int *bad, size_t N,
                             int K, int L, int lb, uint64_t *f0_coeff, uint64_t *f0, uint64_t *w_ccs0, hipStream_t st);
+// f_0 (NTT form) = CRT(sum_i ICRT(rho_i) * D_i) from the digit masks for any rho (run_if: only when *run_if != 0)
+hipError_t fold_phi72_masks(const uint2 *masks0, const uint2 *masks1, const uint64_t *rho, int K, size_t N,
+                            uint64_t *f0, const int *run_if, hipStream_t st);
+// packed Phi_72 planes (n elements) -> f_coeff (digits mod p) and / or f = CRT(f_coeff)
+hipError_t expand_phi72(const uint2 *planes, size_t n, uint64_t *fc, uint64_t *f, hipStream_t st);
 // d = 4096, b_small = 2 (kernels_n4k.hip): sm4 holds nside N 1024 packed words; sink 4096 words.
 // With frag (a scheme whose geometry has Lp = L and qperm), planes k >= 1 are also
 // written as operand rows row0[side] + k - 1, as decompose_fused does for d = 1024.
@@ -204,8 +211,11 @@ hipError_t mle_dot(const uint64_t *mles, size_t stride, int nm, const uint64_t *
 
 // ---------------------------------------------------------------- width-8 Poseidon2 Merkle trees (merkle.hip)
 hipError_t p2w8_permute(uint64_t *states, size_t n, hipStream_t st);
-// nodes: (2 nrows - 1) x 4 digests, leaves first, each level after the one below, root last
+// nodes: merkle_nodes(nrows) x 4 digests (Plonky3's even-padded layers; 2 nrows - 1 for a
+// power of two), leaves first, each level after the one below, root last
+size_t merkle_nodes(size_t nrows);
 hipError_t merkle_tree(const uint64_t *rows, size_t nrows, size_t width, uint64_t *nodes, hipStream_t st);
+hipError_t hash_w8_rows(const uint64_t *rows, size_t nrows, size_t width, uint64_t *out, hipStream_t st);
 
 // ---------------------------------------------------------------- sparse Mz products (mz.hip)
 // the t CCS matrices (m x n, ring-element CSR) on the device, with the

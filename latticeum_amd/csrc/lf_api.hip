@@ -48,7 +48,8 @@ struct lf_ctx {
   uint32_t *smg = nullptr;      // packed coefficients for the fused decomposition
   size_t smg_elems = 0;
   size_t smg_sides_n = 0;       // N when smg holds both sides of the last fused d = 1024 fold_commit, else 0
-  size_t masks24_n = 0;         // N when fkeys holds both sides' Phi_72 digit masks of the last fold_commit, else 0
+  size_t masks24_n = 0;         // N when masks24 hold both sides' Phi_72 digit masks of the last fold_commit, else 0
+  const uint2 *masks24[2] = {nullptr, nullptr};  // in fkeys or the caller's lf_fold_step_bufs.planes
   uint32_t *fkeys = nullptr;    // coefficient-form fold: digit keys [2 N][K][64] (fold_coeff.hip)
   size_t fkeys_elems = 0;
   uint64_t *faux = nullptr;     // coefficient-form fold: rho coefficients, byte tables, the not-short flag
@@ -446,7 +447,17 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
   const bool no_fk = !b->fk[0] && !b->fk[1];
   c->fold_from_frag = false;
   c->masks24_n = 0;
-  if (no_fk) {
+  if (b->planes[0] || b->planes[1]) {
+    if (!fused24 || lbs != 1 || !b->planes[0] || !b->planes[1])
+      return fail(c, LF_ERR_INVALID_ARG, "packed planes: d = 24 with b_small = 2, both sides");
+  }
+  // Phi_72 without f_k / f_coeff_k: the decomposed witnesses stay packed (digit masks)
+  const bool packed24 = no_fk && fused24;
+  if (packed24) {
+    if (lbs != 1) return fail(c, LF_ERR_INVALID_ARG, "packed Phi_72 planes need b_small = 2");
+    if (b->fk_coeff[0] || b->fk_coeff[1])
+      return fail(c, LF_ERR_INVALID_ARG, "Phi_72: f_k and f_coeff_k are both given or both NULL");
+  } else if (no_fk) {
     if (!fused || fv) return fail(c, LF_ERR_INVALID_ARG, "f_k buffers may be omitted only on the fused X^1024+1 path");
     if (extra + 2 * (K - 1) + 2 > LF_MAX_VECS) return fail(c, LF_ERR_INVALID_ARG, "too many operand rows");
     lfk::FoldRows &fr = c->fold_rows;
@@ -486,20 +497,25 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
     } else {
       lfk::FusedSides sd{};
       sd.nside = 2;
-      // b_small = 2: the digit masks for fold_finish's coefficient-form fold
-      const bool want_masks = lbs == 1 && coeff_fold_enabled();
-      if (want_masks) LF_TRY(grow(c, c->fkeys, c->fkeys_elems, 2 * 2 * (size_t)K * N));
+      // b_small = 2: the digit masks for fold_finish's coefficient-form fold,
+      // into the caller's planes if given, else the context's scratch
+      const bool want_masks = lbs == 1 && (coeff_fold_enabled() || packed24 || b->planes[0]);
+      if (want_masks && !b->planes[0]) LF_TRY(grow(c, c->fkeys, c->fkeys_elems, 2 * 2 * (size_t)K * N));
       for (int s = 0; s < 2; s++) {
         sd.f_coeff[s] = fc_side[s];
         sd.f_coeff_k[s] = b->fk_coeff[s];
         sd.f_k[s] = b->fk[s];
         sd.w_ccs_k[s] = b->wk[s];
         sd.row0[s] = extra + s * (K - 1);
-        if (want_masks) sd.masks[s] = reinterpret_cast<uint2 *>(c->fkeys) + (size_t)s * K * N;
+        if (want_masks)
+          sd.masks[s] = b->planes[s] ? reinterpret_cast<uint2 *>(b->planes[s])
+                                     : reinterpret_cast<uint2 *>(c->fkeys) + (size_t)s * K * N;
+        c->masks24[s] = sd.masks[s];
       }
       PhaseTimer pt(c, LF_PHASE_DECOMPOSE);  // both sides in one launch
       bool masks = false;
       LF_HIP(c, lfk::decompose_phi72_sides(sd, N, lb, L, lbs, K, c->d_err, c->frag, aj->geom.nch, c->cur, &masks));
+      if (packed24 && !masks) return fail(c, LF_ERR_INVALID_ARG, "packed Phi_72 planes need the wave-local decomposition");
       c->masks24_n = masks ? N : 0;
     }
     lfk::VecPtrs vp{};
@@ -601,17 +617,40 @@ int fold_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
   // digit masks, then f_0 = CRT and w_ccs_0 (kernels.hip k_fold_coeff_phi72); a
   // rho that is not short raises `bad`, which turns that kernel off and the
   // NTT-form fold and Witness::from_f on
-  if (c->masks24_n == N && N && d == 24 && lbs == 1 && !c->fold_from_frag && coeff_fold_enabled()) {
+  if (c->masks24_n == N && N && d == 24 && lbs == 1 && !c->fold_from_frag) {
+    const uint2 *m0 = c->masks24[0], *m1 = c->masks24[1];
+    if (!b->fk[0] || !coeff_fold_enabled()) {
+      // the planes are packed and rho is not known to be short (or LATTICEUM_AMD_FOLD=slot):
+      // f_0 from the masks in Z_p, then Witness::from_f
+      const bool cf = coeff_fold_enabled();
+      const int nw = 2 * K;
+      int *bad = nullptr;
+      uint32_t *rc = nullptr;
+      if (cf) {
+        LF_TRY(grow(c, c->faux, c->faux_elems, (size_t)nw * 13 + 1));
+        rc = reinterpret_cast<uint32_t *>(c->faux);
+        bad = reinterpret_cast<int *>(c->faux + (size_t)nw * 13);
+      }
+      {
+        PhaseTimer pt(c, LF_PHASE_FOLD);
+        if (cf) {
+          LF_HIP(c, lfk::fold_phi72_rho(b->rho, nw, rc, bad, c->cur));
+          LF_HIP(c, lfk::fold_phi72_coeff(m0, m1, rc, bad, N, K, L, lb, b->f0_coeff, b->f0, b->w_ccs0, c->cur));
+        }
+        LF_HIP(c, lfk::fold_phi72_masks(m0, m1, b->rho, K, N, b->f0, bad, c->cur));
+      }
+      PhaseTimer pt(c, LF_PHASE_FROM_F);
+      LF_HIP(c, lfk::from_f(b->f0, N, d, lb, L, b->f0_coeff, b->w_ccs0, t->inv, c->cur, bad));
+      return LF_OK;
+    }
     const int nw = 2 * K;
     LF_TRY(grow(c, c->faux, c->faux_elems, (size_t)nw * 13 + 1));
     uint32_t *rc = reinterpret_cast<uint32_t *>(c->faux);  // 25 packed words per witness
     int *bad = reinterpret_cast<int *>(c->faux + (size_t)nw * 13);
-    const uint2 *m = reinterpret_cast<const uint2 *>(c->fkeys);
     {
       PhaseTimer pt(c, LF_PHASE_FOLD);
       LF_HIP(c, lfk::fold_phi72_rho(b->rho, nw, rc, bad, c->cur));
-      LF_HIP(c, lfk::fold_phi72_coeff(m, m + (size_t)K * N, rc, bad, N, K, L, lb, b->f0_coeff, b->f0, b->w_ccs0,
-                                      c->cur));
+      LF_HIP(c, lfk::fold_phi72_coeff(m0, m1, rc, bad, N, K, L, lb, b->f0_coeff, b->f0, b->w_ccs0, c->cur));
       lfk::VecPtrs fx{};
       for (int s = 0; s < 2; s++)
         for (int k = 0; k < K; k++) fx.p[s * K + k] = b->fk[s] + (size_t)k * N * d;
@@ -1620,28 +1659,64 @@ int lf_dev_poseidon2_w8_permute(lf_ctx *c, uint64_t *states, size_t n) {
   return LF_OK;
 }
 
+size_t lf_merkle_nodes_len(size_t nrows) { return nrows ? lfk::merkle_nodes(nrows) : 0; }
+
 int lf_dev_merkle_tree(lf_ctx *c, const uint64_t *rows, size_t nrows, size_t width, uint64_t *nodes) {
-  if (!c || !rows || !nodes || !width || !nrows || (nrows & (nrows - 1)))
-    return c ? fail(c, LF_ERR_INVALID_ARG, "Merkle tree: a power-of-two number of rows of width >= 1")
-             : LF_ERR_INVALID_ARG;
+  if (!c || !rows || !nodes || !width || !nrows)
+    return c ? fail(c, LF_ERR_INVALID_ARG, "Merkle tree: at least one row of width >= 1") : LF_ERR_INVALID_ARG;
   DevGuard g(c);
   LF_HIP(c, lfk::merkle_tree(rows, nrows, width, nodes, c->cur));
   return LF_OK;
 }
 
-int lf_merkle_open(lf_ctx *c, const uint64_t *nodes, size_t nrows, size_t index, uint64_t *path) {
-  if (!c || !nodes || !path || !nrows || (nrows & (nrows - 1)) || index >= nrows) return LF_ERR_INVALID_ARG;
+int lf_dev_hash_w8_rows(lf_ctx *c, const uint64_t *rows, size_t nrows, size_t width, uint64_t *out) {
+  if (!c || (nrows && (!out || (width && !rows)))) return LF_ERR_INVALID_ARG;
   DevGuard g(c);
-  // the sibling of the node on the path at every level, leaves first (open_batch's opening_proof)
-  size_t off = 0, n = nrows, i = index, k = 0;
+  LF_HIP(c, lfk::hash_w8_rows(rows, nrows, width, out, c->cur));
+  return LF_OK;
+}
+
+int lf_merkle_open(lf_ctx *c, const uint64_t *nodes, size_t nrows, size_t index, uint64_t *path) {
+  if (!c || !nodes || !path || !nrows || index >= nrows) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  // the sibling of the node on the path in every padded layer below the root,
+  // leaves first (open_batch's opening_proof; a zero digest where the layer was padded)
+  size_t off = 0, n = nrows <= 1 ? 1 : nrows + nrows % 2, i = index, k = 0;
   while (n > 1) {
     LF_HIP(c, hipMemcpyAsync(path + 4 * k, nodes + 4 * (off + (i ^ 1)), 32, hipMemcpyDeviceToHost, c->cur));
     off += n;
-    n /= 2;
+    n = n == 2 ? 1 : ((n / 2 + 1) & ~(size_t)1);
     i /= 2;
     k++;
   }
   LF_HIP(c, hipStreamSynchronize(c->cur));
+  return LF_OK;
+}
+
+int lf_vm_code_comm(lf_ctx *c, const uint8_t *code, size_t len, uint64_t out4[4]) {
+  if (!c || !out4 || (len && !code)) return LF_ERR_INVALID_ARG;
+  if (!len) return fail(c, LF_ERR_INVALID_ARG, "vm_code_comm: empty code (the reference asserts)");
+  DevGuard g(c);
+  // little-endian 16-bit half-words, an odd last byte padded with zero (commitments.rs:316-328)
+  const size_t nh = (len + 1) / 2;
+  std::vector<uint64_t> hw(nh);
+  for (size_t i = 0; i < nh; i++) hw[i] = code[2 * i] | (2 * i + 1 < len ? (uint64_t)code[2 * i + 1] << 8 : 0);
+  DevBuf dr, dn;
+  LF_TRY(upload(c, dr, hw.data(), nh, LF_REPR_CANONICAL));
+  const size_t nn = lfk::merkle_nodes(nh);
+  LF_TRY(dev_alloc(c, dn, 4 * nn));
+  LF_HIP(c, lfk::merkle_tree(dr.p, nh, 1, dn.p, c->cur));
+  LF_HIP(c, hipMemcpyAsync(out4, dn.p + 4 * (nn - 1), 32, hipMemcpyDeviceToHost, c->cur));
+  LF_HIP(c, hipStreamSynchronize(c->cur));
+  return LF_OK;
+}
+
+int lf_dev_expand_planes(lf_ctx *c, int d, const uint64_t *planes, size_t n, uint64_t *fc, uint64_t *f) {
+  if (!c) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  if (d != 24) return fail(c, LF_ERR_UNSUPPORTED_RING, "packed planes: d = 24 only");
+  if (!planes && n) return fail(c, LF_ERR_INVALID_ARG, "planes is NULL");
+  LF_HIP(c, lfk::expand_phi72(reinterpret_cast<const uint2 *>(planes), n, fc, f, c->cur));
   return LF_OK;
 }
 

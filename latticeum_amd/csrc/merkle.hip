@@ -167,16 +167,44 @@ hipError_t p2w8_permute(uint64_t *states, size_t n, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t merkle_tree(const uint64_t *rows, size_t nrows, size_t width, uint64_t *nodes, hipStream_t st) {
-  if (!nrows || (nrows & (nrows - 1)) || !width) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_merkle_leaves, dim3(nb(8 * nrows)), dim3(256), 0, st, rows, nrows, width, nodes);
-  size_t off = 0, n = nrows;
+// Plonky3 MerkleTree::new over one matrix (p3-merkle-tree merkle_tree.rs at
+// git 33e58c7787f9; not vendored): every layer but the root is padded to an even
+// length with the zero digest (first_digest_layer: max_height + max_height % 2;
+// compress: prev == 2 ? 1 : (prev / 2 + 1) & ~1), so any number of rows works
+// (vm_code_comm, commitments.rs:314-340, commits a width-1 matrix of the code's
+// half-words). nodes: the padded layers, leaves first, root last.
+size_t merkle_nodes(size_t nrows) {
+  size_t n = nrows <= 1 ? 1 : nrows + nrows % 2, tot = n;
   while (n > 1) {
+    n = n == 2 ? 1 : ((n / 2 + 1) & ~(size_t)1);
+    tot += n;
+  }
+  return tot;
+}
+
+hipError_t merkle_tree(const uint64_t *rows, size_t nrows, size_t width, uint64_t *nodes, hipStream_t st) {
+  if (!nrows || !width) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_merkle_leaves, dim3(nb(8 * nrows)), dim3(256), 0, st, rows, nrows, width, nodes);
+  size_t off = 0, n = nrows <= 1 ? 1 : nrows + nrows % 2;
+  hipError_t e;
+  if (n > nrows && (e = hipMemsetAsync(nodes + 4 * nrows, 0, 32 * (n - nrows), st)) != hipSuccess) return e;
+  while (n > 1) {
+    const size_t nn = n == 2 ? 1 : ((n / 2 + 1) & ~(size_t)1);
     hipLaunchKernelGGL(k_merkle_level, dim3(nb(8 * (n / 2))), dim3(256), 0, st, nodes + 4 * off, n / 2,
                        nodes + 4 * (off + n));
+    if (nn > n / 2 && (e = hipMemsetAsync(nodes + 4 * (off + n + n / 2), 0, 32 * (nn - n / 2), st)) != hipSuccess)
+      return e;
     off += n;
-    n /= 2;
+    n = nn;
   }
+  return hipGetLastError();
+}
+
+// independent PaddingFreeSponge hashes of nrows rows (the leaf layer alone)
+hipError_t hash_w8_rows(const uint64_t *rows, size_t nrows, size_t width, uint64_t *out, hipStream_t st) {
+  if (!nrows) return hipSuccess;
+  if (!width) return hipMemsetAsync(out, 0, 32 * nrows, st);  // the empty input's digest is the zero state
+  hipLaunchKernelGGL(k_merkle_leaves, dim3(nb(8 * nrows)), dim3(256), 0, st, rows, nrows, width, out);
   return hipGetLastError();
 }
 

@@ -18,6 +18,9 @@ const uint64_t EXT_INIT[64] = LF_P2_EXT_INIT;
 const uint64_t EXT_TERM[64] = LF_P2_EXT_TERM;
 const uint64_t INTERNAL[22] = LF_P2_INTERNAL;
 const uint64_t DIAG_M1[16] = LF_P2_DIAG_M1;
+const uint64_t W8_EXT_INIT[32] = LF_P2W8_EXT_INIT;
+const uint64_t W8_EXT_TERM[32] = LF_P2W8_EXT_TERM;
+const uint64_t W8_DIAG_M1[8] = LF_P2W8_DIAG_M1;
 
 uint64_t sbox7(uint64_t x) {
   uint64_t x2 = gl::mul(x, x), x4 = gl::mul(x2, x2);
@@ -52,6 +55,61 @@ void permute(uint64_t *s) {
   for (int r = 0; r < 4; r++) {
     for (int i = 0; i < 16; i++) s[i] = sbox7(gl::add(s[i], EXT_TERM[16 * r + i]));
     mds16(s);
+  }
+}
+// Poseidon2Goldilocks<8> (poseidon2.rs:31-49): the same round structure at
+// width 8 (MDSMat4 on both 4-chunks, then the column sums), the reference's
+// width-8 external constants (crypto_consts.rs:9-96) and Plonky3's
+// MATRIX_DIAG_8_GOLDILOCKS (not vendored: restated, parity unpinned)
+void mds8(uint64_t *s) {
+  for (int c = 0; c < 8; c += 4) {
+    uint64_t x0 = s[c], x1 = s[c + 1], x2 = s[c + 2], x3 = s[c + 3];
+    uint64_t t = gl::add(gl::add(x0, x1), gl::add(x2, x3));
+    s[c] = gl::add(t, gl::add(x0, gl::add(x1, x1)));
+    s[c + 1] = gl::add(t, gl::add(x1, gl::add(x2, x2)));
+    s[c + 2] = gl::add(t, gl::add(x2, gl::add(x3, x3)));
+    s[c + 3] = gl::add(t, gl::add(x3, gl::add(x0, x0)));
+  }
+  for (int k = 0; k < 4; k++) {
+    uint64_t sum = gl::add(s[k], s[4 + k]);
+    s[k] = gl::add(s[k], sum);
+    s[4 + k] = gl::add(s[4 + k], sum);
+  }
+}
+void permute8(uint64_t *s) {
+  mds8(s);
+  for (int r = 0; r < 4; r++) {
+    for (int i = 0; i < 8; i++) s[i] = sbox7(gl::add(s[i], W8_EXT_INIT[8 * r + i]));
+    mds8(s);
+  }
+  for (int r = 0; r < 22; r++) {
+    s[0] = sbox7(gl::add(s[0], INTERNAL[r]));
+    uint64_t sum = 0;
+    for (int i = 0; i < 8; i++) sum = gl::add(sum, s[i]);
+    for (int i = 0; i < 8; i++) s[i] = gl::add(gl::mul(s[i], W8_DIAG_M1[i]), sum);
+  }
+  for (int r = 0; r < 4; r++) {
+    for (int i = 0; i < 8; i++) s[i] = sbox7(gl::add(s[i], W8_EXT_TERM[8 * r + i]));
+    mds8(s);
+  }
+}
+// PaddingFreeSponge<_, 8, 4, 4>::hash_iter: overwrite state[0..4), permute; a
+// partial last block is permuted; an empty input is the zero digest
+template <class Next>
+void sponge8(Next next, size_t n, uint64_t out4[4]) {
+  uint64_t s[8] = {0};
+  size_t pos = 0;
+  for (;;) {
+    for (int i = 0; i < 4; i++) {
+      if (pos < n) {
+        s[i] = next(pos++);
+      } else {
+        if (i != 0) permute8(s);
+        memcpy(out4, s, 4 * sizeof(uint64_t));
+        return;
+      }
+    }
+    permute8(s);
   }
 }
 }  // namespace
@@ -131,6 +189,19 @@ void lf_hash_iter(const uint64_t *in, size_t n, uint64_t out4[4]) {
     }
     permute(s);
   }
+}
+
+void lf_hash_w8(const uint64_t *in, size_t n, uint64_t out4[4]) {
+  sponge8([&](size_t i) { return gl::canon(in[i]); }, n, out4);
+}
+
+int lf_vm_mem_comm(const uint32_t *words, size_t nwords, uint64_t out4[4]) {
+  // vm_mem_comm (commitments.rs:192-217) hands MerkleTree::new PAGE_COUNT
+  // one-row matrices: all of height 1, so the first digest layer is the
+  // root, one sponge over every page's row in page order
+  if (!out4 || (nwords && !words)) return LF_ERR_INVALID_ARG;
+  sponge8([&](size_t i) { return (uint64_t)words[i]; }, nwords, out4);
+  return LF_OK;
 }
 
 }  // extern "C"

@@ -1157,13 +1157,32 @@ void lfo_p2w8_compress(const uint64_t a[4], const uint64_t b[4], uint64_t out[4]
  * (commitments.rs:192-262): leaf = hash(row), parent = compress(left, right).
  * nodes: every level's digests concatenated, leaves first, root last
  * ((2 nrows - 1) x 4 words) */
-void lfo_merkle_tree(const uint64_t *rows, size_t nrows, size_t width, uint64_t *nodes) {
-  for (size_t i = 0; i < nrows; i++) lfo_p2w8_hash(rows + i * width, width, nodes + 4 * i);
-  size_t off = 0, n = nrows;
+/* Plonky3 MerkleTree::new over one matrix (p3-merkle-tree merkle_tree.rs,
+ * git 33e58c7787f9, not vendored: restated): first_digest_layer hashes every
+ * row and pads the layer to an even length with the zero digest (a single row
+ * is the root); every next layer compresses pairs and pads to an even length
+ * again (compress: next_len_padded = prev == 2 ? 1 : (prev / 2 + 1) & ~1).
+ * Called with PAGE_COUNT rows by vm_mem_comm_with_opening
+ * (ZK/commitments.rs:222-240) and with the code half-words by vm_code_comm
+ * (:314-340). nodes: the padded layers, leaves first, root last. */
+size_t lfo_merkle_nodes(size_t nrows) {
+  size_t n = nrows <= 1 ? 1 : nrows + nrows % 2, tot = n;
   while (n > 1) {
+    n = n == 2 ? 1 : ((n / 2 + 1) & ~(size_t)1);
+    tot += n;
+  }
+  return tot;
+}
+void lfo_merkle_tree(const uint64_t *rows, size_t nrows, size_t width, uint64_t *nodes) {
+  size_t n = nrows <= 1 ? 1 : nrows + nrows % 2, off = 0;
+  for (size_t i = 0; i < nrows; i++) lfo_p2w8_hash(rows + i * width, width, nodes + 4 * i);
+  memset(nodes + 4 * nrows, 0, 32 * (n - nrows));
+  while (n > 1) {
+    const size_t nn = n == 2 ? 1 : ((n / 2 + 1) & ~(size_t)1);
     for (size_t i = 0; i < n / 2; i++)
       lfo_p2w8_compress(nodes + 4 * (off + 2 * i), nodes + 4 * (off + 2 * i + 1), nodes + 4 * (off + n + i));
+    memset(nodes + 4 * (off + n + n / 2), 0, 32 * (nn - n / 2));
     off += n;
-    n /= 2;
+    n = nn;
   }
 }

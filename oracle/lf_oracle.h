@@ -119,6 +119,7 @@ void lfo_p2_hash_iter(const uint64_t *in, size_t n, uint64_t out[4]);
 void lfo_p2w8_permute(uint64_t *s);
 void lfo_p2w8_hash(const uint64_t *in, size_t n, uint64_t out[4]);
 void lfo_p2w8_compress(const uint64_t a[4], const uint64_t b[4], uint64_t out[4]);
+size_t lfo_merkle_nodes(size_t nrows);
 void lfo_merkle_tree(const uint64_t *rows, size_t nrows, size_t width, uint64_t *nodes);
 
 /* ---- transcript (ZK/fiat_shamir.rs) over DuplexChallenger<16,12> ---- */

@@ -85,6 +85,7 @@ def lib():
         "lfo_p2w8_hash": (None, [u64p, SZ, u64p]),
         "lfo_p2w8_compress": (None, [u64p, u64p, u64p]),
         "lfo_merkle_tree": (None, [u64p, SZ, SZ, u64p]),
+        "lfo_merkle_nodes": (SZ, [SZ]),
         "lfo_spmv": (None, [u64p, np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS"), u64p, SZ, I,
                             u64p, u64p]),
         "lfo_mle_fix_first": (None, [u64p, SZ, I, u64p]),
@@ -382,8 +383,13 @@ def p2w8_compress(a, b) -> np.ndarray:
     return out
 
 
+def merkle_nodes(nrows: int) -> int:
+    """digests in the padded layers of a tree over nrows rows (2 nrows - 1 for a power of two)"""
+    return lib().lfo_merkle_nodes(nrows)
+
+
 def merkle_tree(rows, nrows: int, width: int) -> np.ndarray:
-    out = np.zeros((2 * nrows - 1) * 4, np.uint64)
+    out = np.zeros(merkle_nodes(nrows) * 4, np.uint64)
     lib().lfo_merkle_tree(_u64(rows), nrows, width, out)
     return out
 

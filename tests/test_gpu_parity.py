@@ -397,7 +397,29 @@ def test_dev_fold_step_repeated_in_place(ctx):
     check_dev_fold_step(ctx, 1024, 37, 2, steps=3)
 
 
-def check_dev_fold_step(ctx, d, W, kappa, steps=1, keep_fk=True, rho=None):
+@pytest.mark.parametrize("W", [3, 17, 70])
+@pytest.mark.parametrize("short", [True, False])
+def test_dev_fold_step_phi72_packed_planes(ctx, W, short):
+    """Phi_72 with the decomposed witnesses kept as packed digit planes
+    (lf_fold_step_bufs.planes, no u64 f_k / f_coeff_k rows): the step's outputs
+    and the planes expanded by lf_dev_expand_planes equal the oracle's
+    decompose_witness; a rho that is not short folds from the masks in Z_p"""
+    d, K = 24, params(24).K
+    check_dev_fold_step(ctx, d, W, 3, packed=True, rho=None if short else rand(2 * K * d, 6161 + W))
+
+
+def test_dev_fold_step_phi72_packed_planes_slot_fold(ctx, monkeypatch):
+    """LATTICEUM_AMD_FOLD=slot with packed planes: the Z_p fold from the masks runs ungated"""
+    monkeypatch.setenv("LATTICEUM_AMD_FOLD", "slot")
+    check_dev_fold_step(ctx, 24, 17, 3, packed=True)
+
+
+def test_dev_fold_step_phi72_planes_beside_rows(ctx):
+    """planes given together with the u64 rows: both are written"""
+    check_dev_fold_step(ctx, 24, 17, 3, packed="both")
+
+
+def check_dev_fold_step(ctx, d, W, kappa, steps=1, keep_fk=True, rho=None, packed=False):
     import torch
     pr = params(d)
     K, L = pr.K, pr.L
@@ -419,10 +441,11 @@ def check_dev_fold_step(ctx, d, W, kappa, steps=1, keep_fk=True, rho=None):
     keep = {
         "w_ccs": dev(w_ccs), "acc_cm": dev(acc_cm), "acc_f_coeff": dev(acc_fc), "rho": dev(rho),
         "f_coeff": dev(n=N * d), "f": dev(n=N * d), "cm": dev(n=kappa * d),
-        "fk_coeff": [dev(n=K * N * d) for _ in range(2)],
-        "fk": [dev(n=K * N * d) for _ in range(2)] if keep_fk else [None, None],
+        "fk_coeff": [dev(n=K * N * d) for _ in range(2)] if packed is not True else [None, None],
+        "fk": [dev(n=K * N * d) for _ in range(2)] if keep_fk and packed is not True else [None, None],
         "wk": [dev(n=K * W * d) for _ in range(2)], "y": [dev(n=K * kappa * d) for _ in range(2)],
         "f0": dev(n=N * d), "f0_coeff": dev(n=N * d), "w_ccs0": dev(n=W * d), "cm0": dev(n=kappa * d),
+        "planes": [dev(n=K * N) for _ in range(2)] if packed else [None, None],
     }
     b = LA.LfFoldStepBufs()
     for k, v in keep.items():
@@ -439,6 +462,14 @@ def check_dev_fold_step(ctx, d, W, kappa, steps=1, keep_fk=True, rho=None):
         torch.cuda.synchronize()  # the inputs torch wrote on its stream, before the context's stream reads them
         ctx.dev_fold_step(sch, pr, W, b)
         ctx.sync()
+        if packed:  # the rows as lf_dev_expand_planes makes them from the packed planes
+            for s in range(2):
+                fck, fk = dev(n=K * N * d), dev(n=K * N * d)
+                ctx.dev_expand_planes(d, keep["planes"][s], K * N, fck, fk)
+                ctx.sync()
+                if packed == "both":
+                    assert torch.equal(fck, keep["fk_coeff"][s]) and torch.equal(fk, keep["fk"][s])
+                keep["fk_coeff"][s], keep["fk"][s] = fck, fk
         check_fold_outputs(h, keep, A, kappa, d, pr, W, w_ccs, acc_cm, acc_fc, rho)
 
 

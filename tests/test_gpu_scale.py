@@ -75,8 +75,17 @@ def check_workload(wl, seed_w, picks, cm_rows, y_rows):
     assert np.array_equal(host(keep["rho"]), rho)
     # y rows of both sides: the decomposition's own operand rows through the contraction
     y = [host(t).reshape(K, kappa, d) for t in keep["y"]]
-    fk_dev = keep["fk"]
-    if fk_dev[0] is None:
+    fk_dev, fck_dev = keep["fk"], keep["fk_coeff"]
+    if keep.get("planes", [None])[0] is not None and fk_dev[0] is None:
+        # the step kept its planes packed (d = 24): the u64 rows as lf_dev_expand_planes makes them
+        fk_dev, fck_dev = [], []
+        for s in range(2):
+            fck, fk = (torch.empty(K * N * d, dtype=torch.int64, device=keep["f"].device) for _ in range(2))
+            wl.ctxs[0].dev_expand_planes(d, keep["planes"][s], K * N, fck, fk)
+            fk_dev.append(fk)
+            fck_dev.append(fck)
+        wl.ctxs[0].sync()
+    elif fk_dev[0] is None:
         # the step kept its planes only as operand rows: decompose both sides
         # again through the standalone entry (parity-tested on its own)
         fk_dev = []
@@ -109,7 +118,7 @@ def check_workload(wl, seed_w, picks, cm_rows, y_rows):
         sub = fc.reshape(N, d)[cols].ravel()
         ofck, ofk, owk = O.decompose_witness(sub, d, pr.B, L, pr.b_small, K)
         ofck, ofk, owk = ofck.reshape(K, -1, d), ofk.reshape(K, -1, d), owk.reshape(K, ng, d)
-        for name, got_t, want, idx in (("f_coeff_k", keep["fk_coeff"][s], ofck, cols), ("f_k", fk_dev[s], ofk, cols),
+        for name, got_t, want, idx in (("f_coeff_k", fck_dev[s], ofck, cols), ("f_k", fk_dev[s], ofk, cols),
                                        ("w_ccs_k", keep["wk"][s], owk, groups)):
             n_per = N if name != "w_ccs_k" else W
             g = got_t.view(K, n_per, d)[:, torch.from_numpy(idx).to(got_t.device)]
@@ -157,7 +166,8 @@ def test_fold_step_bench_shape_d1024():
 def test_fold_step_reference_ring_zkvm_shape():
     """the reference ring Phi_72 (d=24) at the real zkvm step shape, bench.py's
     reference_ring workload: W = 19 763 (1 236 units of 16 groups, the last
-    with 3 live groups), kappa = 32, the wave-local decomposition"""
+    with 3 live groups), kappa = 32, the wave-local decomposition with the
+    decomposed witnesses kept as packed digit planes (bench.Workload's d = 24 default)"""
     import torch
     wl = run_workload(24, 19763, 32)
     try:
