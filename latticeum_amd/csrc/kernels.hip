@@ -1501,13 +1501,12 @@ hipError_t decompose_phi72_sides(const FusedSides &sd, size_t N, int lb, int L, 
     int ntm = nte ? atoi(nte) : 7;
     if (ntm < 0 || ntm > 7) return hipErrorInvalidValue;
     // no f_coeff_k / f_k buffers: the planes stay packed (the masks must be kept)
-    bool rows = false, none = true;
+    bool all = true, none = true;  // every side has its u64 rows / no side has
     for (int s = 0; s < sd.nside; s++) {
-      rows |= sd.f_k[s] != nullptr || sd.f_coeff_k[s] != nullptr;
+      all &= sd.f_k[s] != nullptr && sd.f_coeff_k[s] != nullptr;
       none &= sd.f_k[s] == nullptr && sd.f_coeff_k[s] == nullptr;
-      if (!sd.f_k[s] != !sd.f_coeff_k[s]) return hipErrorInvalidValue;
     }
-    if (rows && !none) return hipErrorInvalidValue;
+    if (!all && !none) return hipErrorInvalidValue;
     if (none) {
       for (int s = 0; s < sd.nside; s++)
         if (!sd.masks[s]) return hipErrorInvalidValue;
