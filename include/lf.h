@@ -461,6 +461,72 @@ int lf_lcccs_deserialize(const uint8_t *in, size_t len, int d, int repr, uint64_
                          lf_lcccs *out);
 int lf_lfproof_serialize(const lf_lfproof *proof, int repr, uint8_t *out, size_t cap, size_t *len);
 
+/* ------------------------------------------------------------ fold() end to end
+ * zk_latticefold_prove (zkvm/src/zk_latticefold.rs:37-102), what fold()
+ * (zkvm/src/main.rs:369-404) runs with a fresh Poseidon2 transcript:
+ * absorb_public_input (:162-184), the linearization prover
+ * (latticefold/src/nifs/linearization.rs:153-197), the decomposition provers of
+ * (acc, w_acc) and of the linearized (cm_i, w_i) (nifs/decomposition.rs:33-88)
+ * and the folding prover (nifs/folding.rs:42-130), in the reference's transcript
+ * order. The witnesses stay in HBM; the LCCCS and the proof are host memory.
+ *   lf_ccs_set_structure: the CCS's l (= |x_ccs|), degree (ccs.d), c (q NTT
+ *     elements) and multisets S (S_off [q + 1], S_idx) -- CCS (arith.rs:51-74)
+ *   lf_prover_create: device scratch for one (scheme, params, CCS) shape;
+ *     the CCS must pass sanity_check (m = max((n - l - 1) L, m) rounded up to a
+ *     power of two) with N = (n - l - 1) L rounding up to m as well
+ *   lf_fold_prove: -> the folded LCCCS, its witness (caller-allocated device
+ *     buffers: f, f_coeff N elements, w_ccs W) and the LFProof (nifs.rs:28-34).
+ *     repr describes every host buffer (acc, cm_i, x_ccs, out, proof).
+ * Sizes: s = log2 m, tau = 3 (d = 24) or 1, t matrices, K = params K. */
+typedef struct lf_prover lf_prover;
+typedef struct {
+  uint64_t *w_ccs;   /* W NTT elements */
+  uint64_t *f;       /* N = W L NTT elements */
+  uint64_t *f_coeff; /* N coefficient-form elements */
+} lf_witness;
+typedef struct {
+  uint64_t *r;   /* s */
+  uint64_t *v;   /* tau */
+  uint64_t *cm;  /* kappa */
+  uint64_t *u;   /* t */
+  uint64_t *x_w; /* l */
+  uint64_t *h;   /* 1 */
+} lf_lcccs_mut;
+typedef struct {
+  uint64_t *lin_sumcheck;             /* [s][degree + 2] (linearization_sumcheck) */
+  uint64_t *lin_v, *lin_u;            /* tau, t */
+  uint64_t *u_s[2], *v_s[2];          /* [K][t], [K][tau]: decomposition_proof_l / _r */
+  uint64_t *x_s[2], *y_s[2];          /* [K][l + 1], [K][kappa] */
+  uint64_t *fold_sumcheck;            /* [s][2 b_small + 1] (pointshift_sumcheck_proof) */
+  uint64_t *theta_s, *eta_s;          /* [2K][tau], [2K][t] */
+} lf_lfproof_mut;
+int lf_ccs_set_structure(lf_ctx *ctx, lf_ccs *M, size_t l, int degree, int q, const uint64_t *c, const int *S_off,
+                         const int *S_idx, int repr);
+int lf_ccs_shape(const lf_ccs *M, int *t, size_t *m, size_t *n, size_t *l, int *q, int *degree);
+int lf_ccs_get_structure(const lf_ccs *M, uint64_t *c, int *S_off, int *S_idx);
+const uint64_t *lf_ccs_c_device(const lf_ccs *M);
+int lf_prover_create(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, const lf_ccs *ccs, lf_prover **out);
+void lf_prover_destroy(lf_prover *prover);
+const char *lf_prover_last_error(const lf_prover *prover);
+int lf_fold_prove(lf_prover *prover, const lf_lcccs *acc, const lf_witness *w_acc, const uint64_t *cm_i,
+                  const uint64_t *x_ccs, const lf_witness *w_i, lf_lcccs_mut *out, const lf_witness *w_out,
+                  lf_lfproof_mut *proof, int repr);
+/* the halves of the device fold step that fold() interleaves with its sumchecks:
+ *   lf_dev_decompose_commit: decompose_witness + commit_witnesses of both sides
+ *     (y_0 included), inputs acc_f_coeff, acc_cm, f_coeff and cm (the linearized instance)
+ *   lf_dev_fold_combine: given rho, cm_0 / f_0 / Witness::from_f(f_0) (same context and buffers) */
+int lf_dev_decompose_commit(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, size_t W,
+                            const lf_fold_step_bufs *b);
+int lf_dev_fold_combine(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, size_t W, const lf_fold_step_bufs *b);
+/* evaluate_mles of the f_hat MLEs of nw witnesses straight from their f_coeff rows
+ * (wstride u64 apart, 0 = N d): out [nw][tau] NTT elements; point: nv NTT elements */
+int lf_dev_fhat_evaluate(lf_ctx *ctx, int d, const uint64_t *f_coeff, size_t N, size_t wstride, int nw, int nv,
+                         const uint64_t *point, uint64_t *out);
+/* io[x] += sum_m coef[m] (.) mles[m][x] over 2^nv points (stride 0 = 2^nv d) */
+int lf_dev_mle_lincomb(lf_ctx *ctx, int d, const uint64_t *mles, size_t stride, int nm, int nv, const uint64_t *coef,
+                       uint64_t *io);
+int lf_ctx_device(const lf_ctx *ctx);
+
 /* ------------------------------------------------------------ host transcript (sequential) */
 lf_transcript *lf_transcript_new(void);
 void lf_transcript_free(lf_transcript *t);

@@ -468,6 +468,75 @@ class CCSMatrices:
             pass
 
 
+class Prover:
+    """fold() end to end (lf_fold_prove, zk_latticefold_prove): device scratch for one
+    (scheme, params, CCS) shape. The CCS gets its structure (l, degree, c, S) here."""
+
+    def __init__(self, ctx: Context, scheme: "AjtaiCommitmentScheme", params: LfParams, ccs: CCSMatrices, l: int,
+                 degree: int, c, S, repr: int = REPR_CANONICAL):
+        self.ctx, self.lib, self.pr, self.ccs, self.scheme = ctx, ctx.lib, params, ccs, scheme
+        c = _u64(c)
+        off = np.zeros(len(S) + 1, np.int32)
+        off[1:] = np.cumsum([len(x) for x in S])
+        idx = np.array([j for x in S for j in x] or [0], np.int32)
+        ctx.check(self.lib.lf_ccs_set_structure(ctx.h, ccs.h, l, degree, len(S), _ptr(c), _ptr(off), _ptr(idx), repr))
+        h = C.c_void_p()
+        rc = self.lib.lf_prover_create(ctx.h, scheme.h, C.byref(params), ccs.h, C.byref(h))
+        if rc:
+            raise LfError(rc, "lf_prover_create: " + self.lib.lf_status_string(rc).decode())
+        self.h = h
+        self.d, self.l, self.t, self.degree = params.d, l, ccs.t, degree
+        self.s = ccs.m.bit_length() - 1
+        self.tau = 3 if params.d == 24 else 1
+        self.kappa = scheme.kappa
+
+    def fold_prove(self, acc: dict, w_acc: dict, cm_i, x_ccs, w_i: dict, w_out: dict, repr: int = REPR_CANONICAL):
+        """acc: {r, v, cm, u, x_w, h} host arrays; w_*: {w_ccs, f, f_coeff} device tensors.
+        Returns (folded LCCCS dict, LFProof dict) as host arrays; w_out is filled."""
+        from ._lib import LfLcccs, LfLcccsMut, LfLfproofMut, LfRingSlice, LfWitness
+        d, s, tau, t, l, K, kappa = self.d, self.s, self.tau, self.t, self.l, self.pr.K, self.kappa
+        keep = {k: _u64(v) for k, v in acc.items()}
+        sl = lambda a: LfRingSlice(a.ctypes.data, a.size // d)
+        A = LfLcccs(d, sl(keep["r"]), sl(keep["v"]), sl(keep["cm"]), sl(keep["u"]), sl(keep["x_w"]),
+                    keep["h"].ctypes.data)
+        wit = lambda w: LfWitness(_dptr(w["w_ccs"]), _dptr(w["f"]), _dptr(w["f_coeff"]))
+        out = {"r": np.zeros(s * d, np.uint64), "v": np.zeros(tau * d, np.uint64),
+               "cm": np.zeros(kappa * d, np.uint64), "u": np.zeros(t * d, np.uint64),
+               "x_w": np.zeros(max(l, 1) * d, np.uint64), "h": np.zeros(d, np.uint64)}
+        pf = {"lin_sumcheck": np.zeros(s * (self.degree + 2) * d, np.uint64), "lin_v": np.zeros(tau * d, np.uint64),
+              "lin_u": np.zeros(t * d, np.uint64),
+              "u_s": [np.zeros(K * t * d, np.uint64) for _ in range(2)],
+              "v_s": [np.zeros(K * tau * d, np.uint64) for _ in range(2)],
+              "x_s": [np.zeros(K * (l + 1) * d, np.uint64) for _ in range(2)],
+              "y_s": [np.zeros(K * kappa * d, np.uint64) for _ in range(2)],
+              "fold_sumcheck": np.zeros(s * (2 * self.pr.b_small + 1) * d, np.uint64),
+              "theta_s": np.zeros(2 * K * tau * d, np.uint64), "eta_s": np.zeros(2 * K * t * d, np.uint64)}
+        O_ = LfLcccsMut(*[out[k].ctypes.data for k in ("r", "v", "cm", "u", "x_w", "h")])
+        PM = LfLfproofMut()
+        for k in ("lin_sumcheck", "lin_v", "lin_u", "fold_sumcheck", "theta_s", "eta_s"):
+            setattr(PM, k, pf[k].ctypes.data)
+        for k in ("u_s", "v_s", "x_s", "y_s"):
+            for side in range(2):
+                getattr(PM, k)[side] = pf[k][side].ctypes.data
+        cm = _u64(cm_i)
+        xc = _u64(x_ccs) if l else np.zeros(1, np.uint64)
+        wa, wi, wo = wit(w_acc), wit(w_i), wit(w_out)
+        rc = self.lib.lf_fold_prove(self.h, C.byref(A), C.byref(wa), cm.ctypes.data, xc.ctypes.data, C.byref(wi),
+                                    C.byref(O_), C.byref(wo), C.byref(PM), repr)
+        if rc:
+            raise LfError(rc, self.lib.lf_prover_last_error(self.h).decode() or self.lib.lf_status_string(rc).decode())
+        out["x_w"] = out["x_w"][:l * d]
+        return out, pf
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.lib.lf_prover_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
 def witness_split_w() -> int:
     """W below which the d = 1024 witness kernels split elements by limb (lf.h)."""
     return load().lf_witness_split_w()
@@ -605,7 +674,7 @@ def vm_mem_comm(words) -> np.ndarray:
     return out
 
 
-__all__ = ["Context", "AjtaiCommitmentScheme", "Communicator", "Comb", "CCSMatrices", "witness_split_w", "Poseidon2Transcript",
+__all__ = ["Context", "AjtaiCommitmentScheme", "Communicator", "Comb", "CCSMatrices", "Prover", "witness_split_w", "Poseidon2Transcript",
            "LfParams", "LfFoldStepBufs", "merkle_nodes_len", "merkle_depth", "hash_w8", "vm_mem_comm",
            "LfError", "goldilocks_dp", "short_challenge", "hash_iter", "P", "REPR_CANONICAL",
            "REPR_MONTGOMERY", "load"]

@@ -51,6 +51,19 @@ class LfLfproof(C.Structure):
                 ("n_eta", SZ)]
 
 
+class LfWitness(C.Structure):
+    _fields_ = [("w_ccs", VP), ("f", VP), ("f_coeff", VP)]
+
+
+class LfLcccsMut(C.Structure):
+    _fields_ = [("r", VP), ("v", VP), ("cm", VP), ("u", VP), ("x_w", VP), ("h", VP)]
+
+
+class LfLfproofMut(C.Structure):
+    _fields_ = [("lin_sumcheck", VP), ("lin_v", VP), ("lin_u", VP), ("u_s", VP * 2), ("v_s", VP * 2),
+                ("x_s", VP * 2), ("y_s", VP * 2), ("fold_sumcheck", VP), ("theta_s", VP), ("eta_s", VP)]
+
+
 class LfComb(C.Structure):
     _fields_ = [("kind", I), ("nk", I), ("tau", I), ("bsmall", I), ("mu", VP), ("q", I), ("c", VP),
                 ("S_off", VP), ("S_idx", VP)]
@@ -134,6 +147,20 @@ SIGNATURES = {
     "lf_dev_expand_planes": (I, [VP, I, VP, SZ, VP, VP]),
     "lf_ccs_create": (I, [VP, I, I, SZ, SZ, VP, VP, VP, I, C.POINTER(VP)]),
     "lf_ccs_destroy": (None, [VP]),
+    "lf_ccs_set_structure": (I, [VP, VP, SZ, I, I, VP, VP, VP, I]),
+    "lf_ccs_shape": (I, [VP, C.POINTER(I), C.POINTER(SZ), C.POINTER(SZ), C.POINTER(SZ), C.POINTER(I), C.POINTER(I)]),
+    "lf_ccs_get_structure": (I, [VP, VP, VP, VP]),
+    "lf_ccs_c_device": (VP, [VP]),
+    "lf_prover_create": (I, [VP, VP, C.POINTER(LfParams), VP, C.POINTER(VP)]),
+    "lf_prover_destroy": (None, [VP]),
+    "lf_prover_last_error": (C.c_char_p, [VP]),
+    "lf_fold_prove": (I, [VP, C.POINTER(LfLcccs), C.POINTER(LfWitness), VP, VP, C.POINTER(LfWitness),
+                          C.POINTER(LfLcccsMut), C.POINTER(LfWitness), C.POINTER(LfLfproofMut), I]),
+    "lf_dev_decompose_commit": (I, [VP, VP, C.POINTER(LfParams), SZ, C.POINTER(LfFoldStepBufs)]),
+    "lf_dev_fold_combine": (I, [VP, VP, C.POINTER(LfParams), SZ, C.POINTER(LfFoldStepBufs)]),
+    "lf_dev_fhat_evaluate": (I, [VP, I, VP, SZ, SZ, I, I, VP, VP]),
+    "lf_dev_mle_lincomb": (I, [VP, I, VP, SZ, I, I, VP, VP]),
+    "lf_ctx_device": (I, [VP]),
     "lf_dev_mz_mles": (I, [VP, VP, VP, I, I, VP]),
     "lf_dev_mz_challenged": (I, [VP, VP, VP, VP, I, I, VP]),
     "lf_dev_mz_evaluate": (I, [VP, VP, VP, I, I, VP, VP]),

@@ -1,0 +1,519 @@
+// fold_prove.hip -- the zkvm's fold() as one call: zk_latticefold_prove
+// (zkvm/src/zk_latticefold.rs:37-102) with a fresh Poseidon2 transcript
+// (zkvm/src/main.rs:394), in the reference's exact transcript order:
+//   sanity_check; absorb_public_input (:152-184);
+//   LFLinearizationProver::prove (latticefold/src/nifs/linearization.rs:153-197);
+//   LFDecompositionProver::prove of (acc, w_acc), then of the linearized
+//     (cm_i, w_i) (nifs/decomposition.rs:33-88);
+//   LFFoldingProver::prove (nifs/folding.rs:42-130).
+// This is host code above the C ABI, the way a Rust fold() would drive it: every
+// heavy step is an lf_dev_* call on the context's stream (the decomposition and
+// commitments, the Mz products, both sumchecks, the MLE evaluations, the fold),
+// the transcript stays on the host, and only the protocol's messages -- a few
+// hundred ring elements -- cross PCIe. The witnesses stay in HBM.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/lf.h"
+#include "gl.hpp"
+
+struct lf_prover {
+  lf_ctx *ctx = nullptr;
+  const lf_ajtai *aj = nullptr;
+  const lf_ccs *ccs = nullptr;
+  lf_params pr{};
+  int device = 0;
+  // shape
+  int d = 0, tb = 1, tau = 1, s = 0, K = 0, t = 0, q = 0, degree = 0, nm_lin = 0, nm_fold = 0;
+  size_t W = 0, N = 0, n = 0, nn = 0, l = 0, kappa = 0;
+  std::vector<uint64_t> c;  // q NTT elements
+  std::vector<int> S_off, S_idx;
+  std::vector<int> lin_list;  // the matrix of every linearization MLE (c_i != 0, j in S_i)
+  // device memory: one allocation, carved
+  uint64_t *mem = nullptr;
+  uint64_t *z = nullptr, *mz = nullptr, *lin = nullptr, *pt = nullptr, *beta = nullptr, *val = nullptr;
+  uint64_t *fkc[2] = {}, *fk[2] = {}, *wk[2] = {}, *y[2] = {}, *cmd[2] = {}, *xw[2] = {}, *xs = nullptr;
+  uint64_t *zdec[2] = {}, *vs = nullptr, *us = nullptr, *fold = nullptr, *coef[2] = {}, *zeta = nullptr, *mu = nullptr;
+  uint64_t *theta = nullptr, *eta = nullptr, *rho = nullptr, *rhoc = nullptr, *cm0 = nullptr, *u0 = nullptr, *x0 = nullptr,
+           *v0 = nullptr, *r0 = nullptr;
+  std::string err;
+  ~lf_prover() {
+    if (mem) {
+      int prev = -1;
+      if (hipGetDevice(&prev) == hipSuccess && prev != device) (void)hipSetDevice(device);
+      (void)hipFree(mem);
+      if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
+    }
+  }
+};
+
+namespace {
+
+// the Fq3 = Fq[u]/(u^3 - 2^40) product of two base-ring elements (tb = 3), or the Fq one
+void base_mul(const uint64_t *a, const uint64_t *b, uint64_t *o, int tb) {
+  if (tb == 1) {
+    o[0] = gl::mul(a[0], b[0]);
+    return;
+  }
+  const uint64_t nr = 1ull << 40;
+  const uint64_t c0 = gl::add(gl::mul(a[0], b[0]), gl::mul(nr, gl::add(gl::mul(a[1], b[2]), gl::mul(a[2], b[1]))));
+  const uint64_t c1 = gl::add(gl::add(gl::mul(a[0], b[1]), gl::mul(a[1], b[0])), gl::mul(nr, gl::mul(a[2], b[2])));
+  const uint64_t c2 = gl::add(gl::add(gl::mul(a[0], b[2]), gl::mul(a[1], b[1])), gl::mul(a[2], b[0]));
+  o[0] = c0;
+  o[1] = c1;
+  o[2] = c2;
+}
+
+// From<BaseRing> = from_scalar: the base-ring element in every NTT slot
+void broadcast(const uint64_t *base, int tb, int d, uint64_t *out) {
+  for (int i = 0; i < d; i++) out[i] = base[i % tb];
+}
+
+struct Run {
+  lf_prover *P;
+  lf_transcript *T;
+  hipStream_t st;
+  int rc = LF_OK;
+
+  int check(int r, const char *what) {
+    if (r != LF_OK && rc == LF_OK) {
+      rc = r;
+      P->err = std::string(what) + ": " + lf_ctx_last_error(P->ctx);
+    }
+    return r;
+  }
+  int hip(hipError_t e, const char *what) {
+    if (e != hipSuccess && rc == LF_OK) {
+      rc = e == hipErrorOutOfMemory ? LF_ERR_OUT_OF_MEMORY : LF_ERR_DEVICE;
+      P->err = std::string(what) + ": " + hipGetErrorString(e);
+    }
+    return rc;
+  }
+  int h2d(uint64_t *dst, const uint64_t *src, size_t elems) {
+    return elems ? hip(hipMemcpyAsync(dst, src, elems * 8, hipMemcpyHostToDevice, st), "upload") : rc;
+  }
+  int d2h(uint64_t *dst, const uint64_t *src, size_t elems) {
+    if (!elems) return rc;
+    hip(hipMemcpyAsync(dst, src, elems * 8, hipMemcpyDeviceToHost, st), "download");
+    return hip(hipStreamSynchronize(st), "sync");
+  }
+  int d2d(uint64_t *dst, const uint64_t *src, size_t elems) {
+    return elems ? hip(hipMemcpyAsync(dst, src, elems * 8, hipMemcpyDeviceToDevice, st), "copy") : rc;
+  }
+  void absorb(const uint64_t *e, size_t n) { lf_transcript_absorb_ring(T, e, n, P->d, LF_REPR_CANONICAL); }
+  // absorb_field_element(BaseRing::from_base_prime_field(from_be_bytes_mod_order(label)))
+  void absorb_label(const char *label) {
+    uint64_t v = 0;
+    for (const char *p = label; *p; p++) v = gl::add(gl::mul(v, 256), (uint8_t)*p);
+    std::vector<uint64_t> e(P->d, 0);
+    for (int i = 0; i < P->d; i += P->tb) e[i] = v;
+    absorb(e.data(), 1);
+  }
+  // get_challenge (fiat_shamir.rs:69-86): three samples re-observed for Fq3;
+  // one sample re-observed for Fq (this project's convention for X^d + 1)
+  void challenge(uint64_t *out) {
+    if (P->tb == 3) {
+      lf_transcript_get_challenge(T, out);
+    } else {
+      out[0] = lf_transcript_sample(T);
+      lf_transcript_observe(T, out[0]);
+    }
+  }
+  // get_challenges(n) mapped into NTT elements: [n][d]
+  std::vector<uint64_t> challenges(size_t n) {
+    std::vector<uint64_t> out(n * P->d);
+    uint64_t b[3];
+    for (size_t i = 0; i < n; i++) {
+      challenge(b);
+      broadcast(b, P->tb, P->d, out.data() + i * P->d);
+    }
+    return out;
+  }
+};
+
+int bad(lf_prover *P, int code, const char *msg) {
+  P->err = msg;
+  return code;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lf_prover_create(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, const lf_ccs *ccs, lf_prover **out) {
+  if (!ctx || !aj || !pr || !ccs || !out) return LF_ERR_INVALID_ARG;
+  *out = nullptr;
+  auto P = new lf_prover;
+  P->ctx = ctx;
+  P->aj = aj;
+  P->ccs = ccs;
+  P->pr = *pr;
+  P->device = lf_ctx_device(ctx);
+  const int d = pr->d;
+  size_t m = 0, n = 0, l = 0;
+  int t = 0, q = 0, degree = 0;
+  if (lf_ccs_shape(ccs, &t, &m, &n, &l, &q, &degree) != LF_OK || q < 1) {
+    delete P;
+    return LF_ERR_INVALID_ARG;  // lf_ccs_set_structure first
+  }
+  if (lf_ajtai_d(aj) != d || (m & (m - 1)) || m < 2 || pr->b_small < 2 || pr->K < 1 || pr->K > 16 || pr->L < 1 ||
+      n < l + 2) {
+    delete P;
+    return LF_ERR_INVALID_ARG;
+  }
+  P->d = d;
+  P->tb = d == 24 ? 3 : 1;
+  P->tau = d == 24 ? 3 : 1;
+  P->K = pr->K;
+  P->t = t;
+  P->q = q;
+  P->degree = degree;
+  P->n = n;
+  P->l = l;
+  P->W = n - l - 1;
+  P->N = P->W * (size_t)pr->L;
+  P->nn = m;
+  while (((size_t)1 << P->s) < m) P->s++;
+  P->kappa = lf_ajtai_kappa(aj);
+  // sanity_check (zk_latticefold.rs:152-158): m = max((n - l - 1) L, m).next_power_of_two();
+  // Witness::get_fhat gives MLEs of log2(N.next_power_of_two()) variables, which the
+  // sumchecks over s = log2 m variables need to be s as well
+  size_t want = std::max(P->N, m), pw = 1;
+  while (pw < want) pw <<= 1;
+  size_t npw = 1;
+  while (npw < P->N) npw <<= 1;
+  if (pw != m || npw != m || lf_ajtai_width(aj) != P->N) {
+    delete P;
+    return LF_ERR_INVALID_ARG;  // CSError::InvalidSizeBounds / a witness of another width
+  }
+  P->c.resize((size_t)q * d);
+  P->S_off.resize(q + 1);
+  lf_ccs_get_structure(ccs, P->c.data(), P->S_off.data(), nullptr);
+  P->S_idx.resize(P->S_off[q]);
+  lf_ccs_get_structure(ccs, nullptr, nullptr, P->S_idx.data());
+  for (int i = 0; i < q; i++) {
+    bool zero = true;
+    for (int k = 0; k < d; k++) zero &= P->c[(size_t)i * d + k] == 0;
+    if (zero) continue;  // prepare_lin_sumcheck_polynomial skips c_i = 0 (linearization/utils.rs:71-84)
+    for (int k = P->S_off[i]; k < P->S_off[i + 1]; k++) P->lin_list.push_back(P->S_idx[k]);
+  }
+  P->nm_lin = (int)P->lin_list.size() + 1;
+  P->nm_fold = 5 + 2 * P->K * P->tau;
+  // device memory, carved from one allocation
+  const size_t K = P->K, N = P->N, W = P->W, nn = P->nn, kd = P->kappa * d, tau = P->tau;
+  struct Part {
+    uint64_t **p;
+    size_t elems;
+  };
+  std::vector<Part> parts = {
+      {&P->z, n * d}, {&P->mz, (size_t)t * nn * d}, {&P->lin, (size_t)P->nm_lin * nn * d},
+      {&P->pt, (size_t)P->s * d}, {&P->beta, (size_t)P->s * d}, {&P->val, (size_t)(t + 3) * d},
+      {&P->fkc[0], K * N * d}, {&P->fkc[1], K * N * d}, {&P->fk[0], K * N * d}, {&P->fk[1], K * N * d},
+      {&P->wk[0], K * W * d}, {&P->wk[1], K * W * d}, {&P->y[0], K * kd}, {&P->y[1], K * kd},
+      {&P->cmd[0], kd}, {&P->cmd[1], kd}, {&P->xw[0], (l + 1) * d}, {&P->xw[1], (l + 1) * d},
+      {&P->xs, 2 * K * (l + 1) * d}, {&P->zdec[0], K * n * d}, {&P->zdec[1], K * n * d},
+      {&P->vs, 2 * K * tau * d}, {&P->us, 2 * K * t * d}, {&P->fold, (size_t)P->nm_fold * nn * d},
+      {&P->coef[0], K * tau * d}, {&P->coef[1], K * tau * d}, {&P->zeta, 2 * K * d}, {&P->mu, 2 * K * d},
+      {&P->theta, 2 * K * tau * d}, {&P->eta, 2 * K * t * d}, {&P->rho, 2 * K * d}, {&P->rhoc, 2 * K * d},
+      {&P->cm0, kd}, {&P->u0, (size_t)t * d}, {&P->x0, (l + 1) * d}, {&P->v0, tau * d}, {&P->r0, (size_t)P->s * d}};
+  size_t total = 0;
+  for (auto &x : parts) total += (x.elems + 31) / 32 * 32;  // 256-B aligned parts
+  int prev = -1;
+  if (hipGetDevice(&prev) == hipSuccess && prev != P->device) (void)hipSetDevice(P->device);
+  hipError_t e = hipMalloc(&P->mem, total * 8);
+  if (prev >= 0 && prev != P->device) (void)hipSetDevice(prev);
+  if (e != hipSuccess) {
+    P->mem = nullptr;
+    delete P;
+    return e == hipErrorOutOfMemory ? LF_ERR_OUT_OF_MEMORY : LF_ERR_DEVICE;
+  }
+  size_t off = 0;
+  for (auto &x : parts) {
+    *x.p = P->mem + off;
+    off += (x.elems + 31) / 32 * 32;
+  }
+  *out = P;
+  return LF_OK;
+}
+
+void lf_prover_destroy(lf_prover *P) { delete P; }
+
+const char *lf_prover_last_error(const lf_prover *P) { return P ? P->err.c_str() : ""; }
+
+int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, const uint64_t *cm_i,
+                  const uint64_t *x_ccs, const lf_witness *w_i, lf_lcccs_mut *out, const lf_witness *w_out,
+                  lf_lfproof_mut *proof, int repr) {
+  if (!P || !acc || !w_acc || !cm_i || (!x_ccs && P->l) || !w_i || !out || !w_out || !proof) return LF_ERR_INVALID_ARG;
+  if (repr != LF_REPR_CANONICAL && repr != LF_REPR_MONTGOMERY) return bad(P, LF_ERR_INVALID_ARG, "repr");
+  const int d = P->d, tb = P->tb, tau = P->tau, s = P->s, K = P->K, t = P->t;
+  const size_t N = P->N, W = P->W, n = P->n, nn = P->nn, l = P->l, kappa = P->kappa, kd = kappa * d;
+  const size_t ND = N * d;
+  if (acc->d != d || acc->r.n != (size_t)s || acc->v.n != (size_t)tau || acc->cm.n != kappa || acc->u.n != (size_t)t ||
+      acc->x_w.n != l || !acc->h)
+    return bad(P, LF_ERR_INCORRECT_LENGTH, "accumulator LCCCS sizes (r: s, v: tau, cm: kappa, u: t, x_w: l)");
+  if (!w_acc->f_coeff || !w_i->f_coeff || !w_i->w_ccs || !w_out->f || !w_out->f_coeff || !w_out->w_ccs)
+    return bad(P, LF_ERR_INVALID_ARG, "missing witness buffer");
+  if (!proof->lin_sumcheck || !proof->lin_v || !proof->lin_u || !proof->fold_sumcheck || !proof->theta_s ||
+      !proof->eta_s || !out->r || !out->v || !out->cm || !out->u || (l && !out->x_w) || !out->h)
+    return bad(P, LF_ERR_INVALID_ARG, "missing output buffer");
+  for (int side = 0; side < 2; side++)
+    if (!proof->u_s[side] || !proof->v_s[side] || !proof->x_s[side] || !proof->y_s[side])
+      return bad(P, LF_ERR_INVALID_ARG, "missing decomposition proof buffer");
+  // host copies of the public inputs in canonical form
+  auto canon = [&](const uint64_t *src, size_t elems) {
+    std::vector<uint64_t> v(src, src + elems);
+    if (repr == LF_REPR_MONTGOMERY)
+      for (auto &x : v) x = gl::from_mont(x);
+    return v;
+  };
+  const std::vector<uint64_t> ar = canon(acc->r.elems, (size_t)s * d), av = canon(acc->v.elems, (size_t)tau * d),
+                              acm = canon(acc->cm.elems, kd), au = canon(acc->u.elems, (size_t)t * d),
+                              axw = canon(acc->x_w.elems, l * d), ah = canon(acc->h, d), cmi = canon(cm_i, kd),
+                              xc = canon(x_ccs, l * d);
+  lf_ctx *C = P->ctx;
+  Run R{P, lf_transcript_new(), (hipStream_t)lf_ctx_get_stream(C)};
+  struct TGuard {
+    lf_transcript *t;
+    ~TGuard() { lf_transcript_free(t); }
+  } tg{R.T};
+  int prev = -1;
+  if (hipGetDevice(&prev) == hipSuccess && prev != P->device) (void)hipSetDevice(P->device);
+  struct DGuard {
+    int prev, dev;
+    ~DGuard() {
+      if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+    }
+  } dg{prev, P->device};
+  std::vector<uint64_t> one(d, 0);
+  for (int i = 0; i < d; i += tb) one[i] = 1;
+
+  // ---- absorb_public_input (zk_latticefold.rs:162-184)
+  R.absorb_label("acc");
+  R.absorb(ar.data(), s);
+  R.absorb(av.data(), tau);
+  R.absorb(acm.data(), kappa);
+  R.absorb(au.data(), t);
+  R.absorb(axw.data(), l);
+  R.absorb(ah.data(), 1);
+  R.absorb_label("cm_i");
+  R.absorb(cmi.data(), kappa);
+  R.absorb(xc.data(), l);
+
+  // ---- linearization (linearization.rs:153-197)
+  R.absorb_label("beta_s");  // squeeze_beta_challenges (linearization/utils.rs:111-124)
+  const std::vector<uint64_t> beta = R.challenges(s);
+  R.h2d(P->beta, beta.data(), (size_t)s * d);
+  // z = x_ccs || 1 || w_ccs (Instance::get_z_vector), the Mz MLEs, the MLE list + eq(beta)
+  R.h2d(P->z, xc.data(), l * d);
+  R.h2d(P->z + l * d, one.data(), d);
+  R.d2d(P->z + (l + 1) * d, w_i->w_ccs, W * d);
+  R.check(lf_dev_mz_mles(C, P->ccs, P->z, 1, s, P->mz), "Mz MLEs");
+  for (size_t k = 0; k < P->lin_list.size(); k++) R.d2d(P->lin + k * nn * d, P->mz + (size_t)P->lin_list[k] * nn * d, nn * d);
+  R.check(lf_dev_eq_table(C, d, P->beta, s, P->lin + P->lin_list.size() * nn * d), "eq(beta)");
+  std::vector<uint64_t> rnd((size_t)s * tb);
+  {
+    lf_comb cb{};
+    cb.kind = LF_COMB_LINEARIZATION;
+    cb.q = P->q;
+    cb.c = lf_ccs_c_device(P->ccs);
+    cb.S_off = P->S_off.data();
+    cb.S_idx = P->S_idx.data();
+    if (R.rc == LF_OK)
+      R.check(lf_sumcheck_prove(C, R.T, &cb, P->lin, P->nm_lin, s, d, P->degree + 1, proof->lin_sumcheck, rnd.data()),
+              "linearization sumcheck");
+  }
+  if (R.rc) return R.rc;
+  std::vector<uint64_t> r_lin((size_t)s * d);
+  for (int i = 0; i < s; i++) broadcast(rnd.data() + (size_t)i * tb, tb, d, r_lin.data() + (size_t)i * d);
+  R.h2d(P->pt, r_lin.data(), (size_t)s * d);
+  // v = f_hat(w_i) at r, u = MLE(M_j z)(r) (compute_evaluation_vectors, :130-147)
+  R.check(lf_dev_fhat_evaluate(C, d, w_i->f_coeff, N, 0, 1, s, P->pt, P->val), "v");
+  R.check(lf_dev_mle_evaluate(C, d, P->mz, t, s, P->pt, P->val + (size_t)tau * d), "u");
+  std::vector<uint64_t> lv((size_t)tau * d), lu((size_t)t * d);
+  R.d2h(lv.data(), P->val, (size_t)tau * d);
+  R.d2h(lu.data(), P->val + (size_t)tau * d, (size_t)t * d);
+  if (R.rc) return R.rc;
+  R.absorb(lv.data(), tau);
+  R.absorb(lu.data(), t);
+  // the linearized instance: {r, v, cm_i, u, x_ccs, h = ONE}
+
+  // ---- the two decompositions (decomposition.rs:33-88), device work of both first
+  R.h2d(P->cmd[0], acm.data(), kd);
+  R.h2d(P->cmd[1], cmi.data(), kd);
+  R.h2d(P->xw[0], axw.data(), l * d);  // x_w || h of each side
+  R.h2d(P->xw[0] + l * d, ah.data(), d);
+  R.h2d(P->xw[1], xc.data(), l * d);
+  R.h2d(P->xw[1] + l * d, one.data(), d);
+  for (int side = 0; side < 2; side++)
+    R.check(lf_dev_compute_x_s(C, &P->pr, P->xw[side], l + 1, P->xs + (size_t)side * K * (l + 1) * d), "compute_x_s");
+  lf_fold_step_bufs b{};
+  b.acc_f_coeff = w_acc->f_coeff;
+  b.f_coeff = const_cast<uint64_t *>(w_i->f_coeff);
+  b.acc_cm = P->cmd[0];
+  b.cm = P->cmd[1];
+  for (int side = 0; side < 2; side++) {
+    b.fk_coeff[side] = P->fkc[side];
+    b.fk[side] = P->fk[side];
+    b.wk[side] = P->wk[side];
+    b.y[side] = P->y[side];
+  }
+  if (R.rc == LF_OK) R.check(lf_dev_decompose_commit(C, P->aj, &P->pr, W, &b), "decompose + commit_witnesses");
+  // z_k = x_s[k] || w_ccs_k (compute_mz_mles, :229-256) for the u_s (and later eta_s)
+  for (int side = 0; side < 2; side++)
+    for (int k = 0; k < K; k++) {
+      uint64_t *zk = P->zdec[side] + (size_t)k * n * d;
+      R.d2d(zk, P->xs + ((size_t)side * K + k) * (l + 1) * d, (l + 1) * d);
+      R.d2d(zk + (l + 1) * d, P->wk[side] + (size_t)k * W * d, W * d);
+    }
+  std::vector<uint64_t> r_side[2] = {ar, r_lin};
+  for (int side = 0; side < 2; side++) {
+    R.h2d(P->pt, r_side[side].data(), (size_t)s * d);
+    R.check(lf_dev_fhat_evaluate(C, d, P->fkc[side], N, ND, K, s, P->pt, P->vs + (size_t)side * K * tau * d), "v_s");
+    R.check(lf_dev_mz_evaluate(C, P->ccs, P->zdec[side], K, s, P->pt, P->us + (size_t)side * K * t * d), "u_s");
+  }
+  if (R.rc) return R.rc;
+  for (int side = 0; side < 2; side++) {
+    R.d2h(proof->x_s[side], P->xs + (size_t)side * K * (l + 1) * d, (size_t)K * (l + 1) * d);
+    R.d2h(proof->y_s[side], P->y[side], (size_t)K * kd);
+    R.d2h(proof->u_s[side], P->us + (size_t)side * K * t * d, (size_t)K * t * d);
+    R.d2h(proof->v_s[side], P->vs + (size_t)side * K * tau * d, (size_t)K * tau * d);
+    if (R.rc) return R.rc;
+    for (int k = 0; k < K; k++) {  // the decomposed instances' messages (:58-64)
+      R.absorb(proof->x_s[side] + (size_t)k * (l + 1) * d, l + 1);
+      R.absorb(proof->y_s[side] + (size_t)k * kd, kappa);
+      R.absorb(proof->u_s[side] + (size_t)k * t * d, t);
+      R.absorb(proof->v_s[side] + (size_t)k * tau * d, tau);
+    }
+  }
+
+  // ---- folding (folding.rs:42-130)
+  R.absorb_label("alpha_s");  // squeeze_alpha_beta_zeta_mu (folding/utils.rs:51-96)
+  const std::vector<uint64_t> alpha = R.challenges(2 * K);
+  R.absorb_label("zeta_s");
+  const std::vector<uint64_t> zeta = R.challenges(2 * K);
+  R.absorb_label("mu_s");
+  std::vector<uint64_t> mu = R.challenges(2 * K - 1);
+  mu.insert(mu.end(), one.begin(), one.end());
+  R.absorb_label("beta_s");
+  const std::vector<uint64_t> fbeta = R.challenges(s);
+  R.h2d(P->zeta, zeta.data(), 2 * (size_t)K * d);
+  R.h2d(P->mu, mu.data(), 2 * (size_t)K * d);
+  R.h2d(P->beta, fbeta.data(), (size_t)s * d);
+  // Horner weights alpha_k^(j+1) of each side's f_hat MLEs (prepare_g1_and_3_k_mles_list, :519-541)
+  for (int side = 0; side < 2; side++) {
+    std::vector<uint64_t> cf((size_t)K * tau * d);
+    for (int k = 0; k < K; k++) {
+      const uint64_t *a = alpha.data() + (size_t)(side * K + k) * d;  // broadcast: slot 0 holds the base value
+      uint64_t pw[3] = {a[0], tb == 3 ? a[1] : 0, tb == 3 ? a[2] : 0};
+      for (int j = 0; j < tau; j++) {
+        broadcast(pw, tb, d, cf.data() + ((size_t)k * tau + j) * d);
+        uint64_t nx[3];
+        base_mul(pw, a, nx, tb);
+        memcpy(pw, nx, sizeof(pw));
+      }
+    }
+    R.h2d(P->coef[side], cf.data(), cf.size());
+  }
+  // the MLEs [eq(r_0), g1, eq(r_1), g3, eq(beta), f_hat (2K x tau)] (create_sumcheck_polynomial, :196-255)
+  uint64_t *M = P->fold;
+  const size_t mstride = nn * d;
+  for (int side = 0; side < 2; side++)
+    for (int k = 0; k < K; k++)
+      R.check(lf_dev_get_fhat(C, d, P->fkc[side] + (size_t)k * ND, N, s, M + (5 + (size_t)(side * K + k) * tau) * mstride),
+              "f_hat");
+  for (int side = 0; side < 2; side++) {
+    R.h2d(P->pt, r_side[side].data(), (size_t)s * d);
+    R.check(lf_dev_eq_table(C, d, P->pt, s, M + (size_t)(2 * side) * mstride), "eq(r_i)");
+    uint64_t *g = M + (size_t)(2 * side + 1) * mstride;
+    R.check(lf_dev_mz_challenged(C, P->ccs, P->zdec[side], P->zeta + (size_t)side * K * d, K, s, g), "challenged Mz");
+    R.check(lf_dev_mle_lincomb(C, d, M + (5 + (size_t)side * K * tau) * mstride, mstride, K * tau, s, P->coef[side], g),
+            "g");
+  }
+  R.check(lf_dev_eq_table(C, d, P->beta, s, M + 4 * mstride), "eq(beta)");
+  {
+    lf_comb cb{};
+    cb.kind = LF_COMB_FOLDING;
+    cb.nk = 2 * K;
+    cb.tau = tau;
+    cb.bsmall = (int)P->pr.b_small;
+    cb.mu = P->mu;
+    if (R.rc == LF_OK)
+      R.check(lf_sumcheck_prove(C, R.T, &cb, M, P->nm_fold, s, d, 2 * cb.bsmall, proof->fold_sumcheck, rnd.data()),
+              "folding sumcheck");
+  }
+  if (R.rc) return R.rc;
+  std::vector<uint64_t> r0((size_t)s * d);
+  for (int i = 0; i < s; i++) broadcast(rnd.data() + (size_t)i * tb, tb, d, r0.data() + (size_t)i * d);
+  R.h2d(P->r0, r0.data(), (size_t)s * d);
+  // theta_s = f_hat(w_i)(r_0), eta_s = MLE(M_j z_i)(r_0) (get_thetas / get_etas, :236-256)
+  for (int side = 0; side < 2; side++) {
+    R.check(lf_dev_fhat_evaluate(C, d, P->fkc[side], N, ND, K, s, P->r0, P->theta + (size_t)side * K * tau * d), "theta");
+    R.check(lf_dev_mz_evaluate(C, P->ccs, P->zdec[side], K, s, P->r0, P->eta + (size_t)side * K * t * d), "eta");
+  }
+  R.d2h(proof->theta_s, P->theta, 2 * (size_t)K * tau * d);
+  R.d2h(proof->eta_s, P->eta, 2 * (size_t)K * t * d);
+  if (R.rc) return R.rc;
+  for (int i = 0; i < 2 * K; i++) R.absorb(proof->theta_s + (size_t)i * tau * d, tau);
+  for (int i = 0; i < 2 * K; i++) R.absorb(proof->eta_s + (size_t)i * t * d, t);
+  // get_rhos (folding/utils.rs:116-127): 2K - 1 short challenges and ONE, then CRT
+  R.absorb_label("rho_s");
+  std::vector<uint64_t> rc(2 * (size_t)K * d, 0);
+  if (lf_transcript_get_short_challenges(R.T, d, 2 * K - 1, rc.data()) != LF_OK)
+    return bad(P, LF_ERR_CHALLENGE_BYTES, "short challenges");
+  rc[(size_t)(2 * K - 1) * d] = 1;
+  R.h2d(P->rhoc, rc.data(), rc.size());
+  R.d2d(P->rho, P->rhoc, rc.size());
+  R.check(lf_dev_crt(C, P->rho, 2 * K, d), "CRT(rho)");
+  // f_0, cm_0, Witness::from_f(f_0) (:112-122), then v_0, u_0, x_0 (compute_v0_u0_x0_cm_0, :456-517)
+  b.rho = P->rho;
+  b.f0 = w_out->f;
+  b.f0_coeff = w_out->f_coeff;
+  b.w_ccs0 = w_out->w_ccs;
+  b.cm0 = P->cm0;
+  if (R.rc == LF_OK) R.check(lf_dev_fold_combine(C, P->aj, &P->pr, W, &b), "fold");
+  R.check(lf_dev_fold_lcccs(C, d, 2 * K, P->rho, P->rhoc, P->eta, t, P->xs, l + 1, P->theta, P->u0, P->x0, P->v0),
+          "v_0, u_0, x_0");
+  if (R.rc) return R.rc;
+  // prepare_public_output (folding.rs:381-392): x_w = x_0[..l], h = x_0[l]
+  std::vector<uint64_t> x0((l + 1) * d);
+  R.d2h(out->cm, P->cm0, kd);
+  R.d2h(out->u, P->u0, (size_t)t * d);
+  R.d2h(out->v, P->v0, (size_t)tau * d);
+  R.d2h(x0.data(), P->x0, (l + 1) * d);
+  R.check(lf_ctx_sync(C), "sync");
+  if (R.rc) return R.rc;
+  memcpy(out->r, r0.data(), r0.size() * 8);
+  if (l) memcpy(out->x_w, x0.data(), l * d * 8);
+  memcpy(out->h, x0.data() + l * d, d * 8);
+  memcpy(proof->lin_v, lv.data(), lv.size() * 8);
+  memcpy(proof->lin_u, lu.data(), lu.size() * 8);
+  if (repr == LF_REPR_MONTGOMERY) {
+    auto mont = [](uint64_t *p, size_t elems) {
+      for (size_t i = 0; i < elems; i++) p[i] = gl::to_mont(p[i]);
+    };
+    mont(out->r, (size_t)s * d);
+    mont(out->v, (size_t)tau * d);
+    mont(out->cm, kd);
+    mont(out->u, (size_t)t * d);
+    mont(out->x_w, l * d);
+    mont(out->h, d);
+    mont(proof->lin_sumcheck, (size_t)s * (P->degree + 2) * d);
+    mont(proof->lin_v, (size_t)tau * d);
+    mont(proof->lin_u, (size_t)t * d);
+    for (int side = 0; side < 2; side++) {
+      mont(proof->u_s[side], (size_t)K * t * d);
+      mont(proof->v_s[side], (size_t)K * tau * d);
+      mont(proof->x_s[side], (size_t)K * (l + 1) * d);
+      mont(proof->y_s[side], (size_t)K * kd);
+    }
+    mont(proof->fold_sumcheck, (size_t)s * (2 * P->pr.b_small + 1) * d);
+    mont(proof->theta_s, 2 * (size_t)K * tau * d);
+    mont(proof->eta_s, 2 * (size_t)K * t * d);
+  }
+  return LF_OK;
+}
+
+}  // extern "C"

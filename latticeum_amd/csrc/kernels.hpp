@@ -208,6 +208,13 @@ size_t mle_eval_partial_elems(int d, int nm);
 // out[m] = sum_x eq[x] (.) mles[m][x], x < n
 hipError_t mle_dot(const uint64_t *mles, size_t stride, int nm, const uint64_t *eq, size_t n, int d,
                    uint64_t *partial, uint64_t *out, hipStream_t st);
+// out [nw][tau][d]: the f_hat MLEs of nw witnesses (f_coeff rows wstride u64 apart, N
+// elements each) evaluated against the eq table, without materialising f_hat
+hipError_t fhat_dot(const uint64_t *fc, size_t N, size_t wstride, int nw, const uint64_t *eq, size_t n, int d,
+                    uint64_t *partial, uint64_t *out, hipStream_t st);
+// io[x] += sum_m coef[m] (.) mles[m][x], x < n; coef [nm][d]
+hipError_t mle_lincomb(const uint64_t *mles, size_t stride, int nm, const uint64_t *coef, size_t n, int d,
+                       uint64_t *io, hipStream_t st);
 
 // ---------------------------------------------------------------- width-8 Poseidon2 Merkle trees (merkle.hip)
 hipError_t p2w8_permute(uint64_t *states, size_t n, hipStream_t st);

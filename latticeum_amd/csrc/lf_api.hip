@@ -73,6 +73,18 @@ struct lf_ctx {
   std::map<int, std::pair<double, long>> stats;  // nvec -> (ms, count)
 };
 
+// restores the calling thread's device on scope exit (also for destructors)
+struct DevGuardBase {
+  int prev = -1;
+  explicit DevGuardBase(int dev) {
+    int cur = -1;
+    if (dev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess) prev = cur;
+  }
+  ~DevGuardBase() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
 struct lf_ajtai {
   int device = 0;
   const uint64_t *A = nullptr;
@@ -83,11 +95,23 @@ struct lf_ajtai {
   int d = 0;
 };
 
-// the CCS matrices on the device (lf_ccs_create)
+// the CCS matrices on the device (lf_ccs_create), plus the structure the
+// linearization needs (lf_ccs_set_structure): l, the degree, c and S
 struct lf_ccs {
   int device = 0;
   lfk::CcsDev dev{};
   std::vector<void *> bufs;
+  bool structured = false;
+  size_t l = 0;
+  int degree = 0;
+  std::vector<uint64_t> c;     // q NTT elements, canonical
+  std::vector<int> S_off, S_idx;
+  uint64_t *c_dev = nullptr;   // in bufs
+  size_t c_dev_elems = 0;
+  ~lf_ccs() {  // every device buffer, also on a failed lf_ccs_create
+    DevGuardBase g(device);
+    for (void *p : bufs) (void)hipFree(p);
+  }
 };
 
 // a communicator for the accumulator exchange (RCCL over xGMI)
@@ -822,6 +846,8 @@ const char *lf_ctx_last_error(const lf_ctx *c) { return c ? c->last_error.c_str(
 
 size_t lf_witness_split_w(void) { return lfk::witness_split_w(); }
 
+int lf_ctx_device(const lf_ctx *c) { return c ? c->device : -1; }
+
 int lf_ctx_set_stream(lf_ctx *c, void *s) {
   if (!c) return LF_ERR_INVALID_ARG;
   c->cur = (hipStream_t)s;  // NULL = the HIP default (null) stream, e.g. torch's default stream
@@ -1423,6 +1449,30 @@ int lf_dev_get_fhat(lf_ctx *c, int d, const uint64_t *f_coeff, size_t N, int nv,
   return LF_OK;
 }
 
+int lf_dev_fhat_evaluate(lf_ctx *c, int d, const uint64_t *f_coeff, size_t N, size_t wstride, int nw, int nv,
+                         const uint64_t *point, uint64_t *out) {
+  if (!c || !point || !out || nw < 0 || nv < 1 || (nw && N && !f_coeff)) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  const size_t n = (size_t)1 << nv;
+  if (N > n) return fail(c, LF_ERR_INCORRECT_LENGTH, "N exceeds 2^nv");
+  const int tau = d == 24 ? 3 : 1;
+  LF_TRY(grow(c, c->sc, c->sc_elems, n * d + lfk::mle_eval_partial_elems(d, nw * tau)));
+  LF_HIP(c, lfk::eq_table(point, nv, d, c->sc, c->cur));
+  LF_HIP(c, lfk::fhat_dot(f_coeff, N, wstride ? wstride : N * d, nw, c->sc, n, d, c->sc + n * d, out, c->cur));
+  return LF_OK;
+}
+
+int lf_dev_mle_lincomb(lf_ctx *c, int d, const uint64_t *mles, size_t stride, int nm, int nv, const uint64_t *coef,
+                       uint64_t *io) {
+  if (!c || !io || nm < 0 || nv < 0 || (nm && (!mles || !coef))) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  const size_t n = (size_t)1 << nv;
+  LF_HIP(c, lfk::mle_lincomb(mles, stride ? stride : n * d, nm, coef, n, d, io, c->cur));
+  return LF_OK;
+}
+
 int lf_dev_mle_fix_first(lf_ctx *c, int d, const uint64_t *in, size_t in_stride, int nm, int nv,
                          const uint64_t *r_base, uint64_t *out, size_t out_stride) {
   if (!c || !in || !out || !r_base || nm < 1 || nv < 1) return LF_ERR_INVALID_ARG;
@@ -1525,11 +1575,61 @@ int lf_sumcheck_prove(lf_ctx *c, lf_transcript *t, const lf_comb *cb, uint64_t *
 }
 
 // ---------------------------------------------------------------- sparse Mz products
-void lf_ccs_destroy(lf_ccs *M) {
-  if (!M) return;
-  DevGuard g(M->device);
-  for (void *p : M->bufs) (void)hipFree(p);
-  delete M;
+void lf_ccs_destroy(lf_ccs *M) { delete M; }
+
+int lf_ccs_shape(const lf_ccs *M, int *t, size_t *m, size_t *n, size_t *l, int *q, int *degree) {
+  if (!M) return LF_ERR_INVALID_ARG;
+  if (t) *t = M->dev.t;
+  if (m) *m = M->dev.m;
+  if (n) *n = M->dev.n;
+  if (l) *l = M->l;
+  if (q) *q = M->structured ? (int)M->S_off.size() - 1 : 0;
+  if (degree) *degree = M->degree;
+  return M->structured ? LF_OK : LF_ERR_INVALID_ARG;
+}
+
+int lf_ccs_get_structure(const lf_ccs *M, uint64_t *cc, int *S_off, int *S_idx) {
+  if (!M || !M->structured) return LF_ERR_INVALID_ARG;
+  if (cc) std::copy(M->c.begin(), M->c.end(), cc);
+  if (S_off) std::copy(M->S_off.begin(), M->S_off.end(), S_off);
+  if (S_idx) std::copy(M->S_idx.begin(), M->S_idx.end(), S_idx);
+  return LF_OK;
+}
+
+const uint64_t *lf_ccs_c_device(const lf_ccs *M) { return M ? M->c_dev : nullptr; }
+
+int lf_ccs_set_structure(lf_ctx *c, lf_ccs *M, size_t l, int degree, int q, const uint64_t *cc, const int *S_off,
+                         const int *S_idx, int repr) {
+  if (!c || !M || q < 1 || !cc || !S_off || !S_idx || degree < 1) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  LF_TRY(check_repr(c, repr));
+  const int d = M->dev.d;
+  if (l + 1 > M->dev.n) return fail(c, LF_ERR_INVALID_ARG, "CCS: l + 1 > n");
+  if (S_off[0] != 0) return fail(c, LF_ERR_INVALID_ARG, "CCS: S_off[0] must be 0");
+  for (int i = 0; i < q; i++) {
+    if (S_off[i + 1] < S_off[i]) return fail(c, LF_ERR_INVALID_ARG, "CCS: S_off must not decrease");
+    if (S_off[i + 1] - S_off[i] > degree) return fail(c, LF_ERR_INVALID_ARG, "CCS: a multiset exceeds the degree");
+  }
+  for (int k = 0; k < S_off[q]; k++)
+    if (S_idx[k] < 0 || S_idx[k] >= M->dev.t) return fail(c, LF_ERR_INVALID_ARG, "CCS: multiset index out of range");
+  M->c.assign(cc, cc + (size_t)q * d);
+  if (repr == LF_REPR_MONTGOMERY)
+    for (auto &x : M->c) x = gl::from_mont(x);
+  M->S_off.assign(S_off, S_off + q + 1);
+  M->S_idx.assign(S_idx, S_idx + S_off[q]);
+  M->l = l;
+  M->degree = degree;
+  if (!M->c_dev || M->c_dev_elems < (size_t)q * d) {
+    void *p = nullptr;
+    LF_HIP(c, hipMalloc(&p, (size_t)q * d * 8));
+    M->bufs.push_back(p);
+    M->c_dev = (uint64_t *)p;
+    M->c_dev_elems = (size_t)q * d;
+  }
+  LF_HIP(c, hipMemcpyAsync(M->c_dev, M->c.data(), (size_t)q * d * 8, hipMemcpyHostToDevice, c->cur));
+  LF_HIP(c, hipStreamSynchronize(c->cur));
+  M->structured = true;
+  return LF_OK;
 }
 
 int lf_ccs_create(lf_ctx *c, int d, int t, size_t m, size_t n, const uint64_t *row_ptr, const uint32_t *col,
@@ -1754,6 +1854,33 @@ int lf_dev_fold_step_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, 
   const lfk::OutPtrs dst = fold_dst(pr, b, kd, b->cm);
   for (int v = 0; v < fold_nvec(pr, true); v++)
     LF_HIP(c, hipMemcpyAsync(dst.p[v], partial_sum + v * kd, kd * 8, hipMemcpyDeviceToDevice, c->cur));
+  return fold_finish(c, aj, pr, lb, lbs, W, b, b->cm);
+}
+
+// the decomposition half of fold() without commit(z): both sides' decompose_witness
+// and commit_witnesses (decomposition.rs:162-201), y_0 included; inputs
+// acc_f_coeff / acc_cm (accumulator) and f_coeff / cm (the linearized instance)
+int lf_dev_decompose_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t W,
+                            const lf_fold_step_bufs *b) {
+  DevGuard g(c);
+  int lb, lbs;
+  LF_TRY(step_check(c, aj, pr, W, b, lb, lbs));
+  if (!b->acc_f_coeff || !b->f_coeff || !b->acc_cm || !b->cm || !b->y[0] || !b->y[1] || !b->wk[0] || !b->wk[1])
+    return fail(c, LF_ERR_INVALID_ARG, "decompose_commit: missing buffer");
+  const size_t kd = aj->kappa * (size_t)pr->d;
+  LF_TRY(fold_commit(c, aj, pr, lb, lbs, W, b, b->f_coeff, nullptr, fold_dst(pr, b, kd, nullptr)));
+  for (int s = 0; s < 2; s++)
+    LF_HIP(c, lfk::commit_y0(s ? b->cm : b->acc_cm, b->y[s], aj->kappa, pr->d, lbs, pr->K, c->cur));
+  return LF_OK;
+}
+
+// the folding half, given rho: cm_0, f_0 and Witness::from_f(f_0) (folding.rs:112-122);
+// right after lf_dev_decompose_commit on the same context and buffers
+int lf_dev_fold_combine(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t W, const lf_fold_step_bufs *b) {
+  DevGuard g(c);
+  int lb, lbs;
+  LF_TRY(step_check(c, aj, pr, W, b, lb, lbs));
+  if (!b->rho || !b->f0 || !b->f0_coeff || !b->w_ccs0 || !b->cm0) return fail(c, LF_ERR_INVALID_ARG, "fold_combine: missing buffer");
   return fold_finish(c, aj, pr, lb, lbs, W, b, b->cm);
 }
 

@@ -321,6 +321,42 @@ __global__ void __launch_bounds__(RT) k_mle_dot(const uint64_t *mles, size_t str
   block_partial<TB, 1>(acc, spb, ppb, slot, lane_p, d, partial + ((size_t)blockIdx.x * nm + m) * d);
 }
 
+// evaluate_mles of Witness::get_fhat's MLEs straight from the coefficient rows
+// (no materialised f_hat): the value of MLE j at point x < N, slot s, is the
+// base-ring scalar f_coeff[x][j NS + s] (zero past N), so
+// out[w][j] = sum_x eq[x] (.) fhat_wj[x]; blockIdx.z = w tau + j
+template <int TB>
+__global__ void __launch_bounds__(RT) k_fhat_dot(const uint64_t *fc, size_t N, size_t wstride, const uint64_t *eq,
+                                                 size_t n, int d, int spb, int nsplit, uint64_t *partial, int nm) {
+  const int slot_l = threadIdx.x % spb, lane_p = threadIdx.x / spb, ppb = RT / spb;
+  const int slot = blockIdx.y * spb + slot_l, ns = d / TB, tau = TB == 3 ? 3 : 1;
+  const int m = blockIdx.z, w = m / tau, j = m - w * tau;
+  const uint64_t *f = fc + (size_t)w * wstride + (size_t)j * ns + slot;
+  SAcc<TB> la;
+  sacc_zero(la);
+  for (size_t x = (size_t)blockIdx.x * ppb + lane_p; x < n && x < N; x += (size_t)nsplit * ppb)
+    sacc_mad(la, s_load<TB>(eq + x * d + slot * TB), s_scalar<TB>(f[x * d]));
+  const Sv<TB> acc[1] = {sacc_final(la)};
+  block_partial<TB, 1>(acc, spb, ppb, slot, lane_p, d, partial + ((size_t)blockIdx.x * nm + m) * d);
+}
+
+// io[x] += sum_m coef[m] (.) mles[m][x] for the n points (one thread per point and slot)
+template <int TB>
+__global__ void __launch_bounds__(256) k_mle_lincomb(const uint64_t *mles, size_t stride, int nm, const uint64_t *coef,
+                                                     size_t n, int d, uint64_t *io) {
+  const int ns = d / TB;
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n * ns) return;
+  const size_t x = i / ns;
+  const int s = (int)(i - x * ns);
+  SAcc<TB> la;
+  sacc_zero(la);
+  for (int m = 0; m < nm; m++)
+    sacc_mad(la, s_load<TB>(coef + (size_t)m * d + s * TB), s_load<TB>(mles + m * stride + x * d + s * TB));
+  uint64_t *o = io + x * d + s * TB;
+  s_store(o, s_add(s_load<TB>(o), sacc_final(la)));
+}
+
 unsigned blocks_of(size_t n, int t) { return (unsigned)((n + t - 1) / t); }
 
 template <int TB>
@@ -478,6 +514,37 @@ hipError_t mle_dot(const uint64_t *mles, size_t stride, int nm, const uint64_t *
   if (e != hipSuccess) return e;
   const size_t len = (size_t)nm * d;
   hipLaunchKernelGGL(k_sum_partials, dim3((unsigned)len), dim3(256), 0, st, partial, nsplit, len, out);
+  return hipGetLastError();
+}
+
+hipError_t fhat_dot(const uint64_t *fc, size_t N, size_t wstride, int nw, const uint64_t *eq, size_t n, int d,
+                    uint64_t *partial, uint64_t *out, hipStream_t st) {
+  const int tb = slot_words(d), ns = d / tb, tau = tb == 3 ? 3 : 1, nm = nw * tau;
+  if (!nw || !n) return hipSuccess;
+  const int spb = ns < RT ? ns : RT, ppb = RT / spb;
+  size_t sx = (n + ppb - 1) / ppb;
+  const int nsplit = (int)(sx < 64 ? sx : 64);
+  const dim3 grid((unsigned)nsplit, (unsigned)(ns / spb), (unsigned)nm);
+  if (tb == 3)
+    hipLaunchKernelGGL(k_fhat_dot<3>, grid, dim3(RT), 0, st, fc, N, wstride, eq, n, d, spb, nsplit, partial, nm);
+  else
+    hipLaunchKernelGGL(k_fhat_dot<1>, grid, dim3(RT), 0, st, fc, N, wstride, eq, n, d, spb, nsplit, partial, nm);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const size_t len = (size_t)nm * d;
+  hipLaunchKernelGGL(k_sum_partials, dim3((unsigned)len), dim3(256), 0, st, partial, nsplit, len, out);
+  return hipGetLastError();
+}
+
+hipError_t mle_lincomb(const uint64_t *mles, size_t stride, int nm, const uint64_t *coef, size_t n, int d,
+                       uint64_t *io, hipStream_t st) {
+  if (!nm || !n) return hipSuccess;
+  const int tb = slot_words(d);
+  const size_t nt = n * (size_t)(d / tb);
+  if (tb == 3)
+    hipLaunchKernelGGL(k_mle_lincomb<3>, dim3(blocks_of(nt, 256)), dim3(256), 0, st, mles, stride, nm, coef, n, d, io);
+  else
+    hipLaunchKernelGGL(k_mle_lincomb<1>, dim3(blocks_of(nt, 256)), dim3(256), 0, st, mles, stride, nm, coef, n, d, io);
   return hipGetLastError();
 }
 

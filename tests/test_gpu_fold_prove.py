@@ -1,0 +1,151 @@
+"""lf_fold_prove (the zkvm's fold(), zk_latticefold_prove, ZK/zk_latticefold.rs:37-102)
+against the oracle's restatement (oracle/nifs.py): the folded LCCCS, the folded
+witness and every LFProof message bit-exact, and the restated NIFS verifier
+accepts the device's proof. Small satisfied CCS instances (the oracle is
+Python glue over its C primitives)."""
+import numpy as np
+import pytest
+
+import latticeum_amd as LA
+import nifs as N
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(x):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(x, np.uint64).view(np.int64).copy()).cuda()
+
+
+def zeros(n):
+    import torch
+    return torch.zeros(n, dtype=torch.int64, device="cuda")
+
+
+def host(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+def flat(xs):
+    return np.concatenate([np.asarray(x, np.uint64).ravel() for x in xs]) if len(xs) else np.zeros(0, np.uint64)
+
+
+def setup(ctx, d, W, l, t, deg, kappa, seed):
+    pr_o = N.Params(d)
+    ccs = N.satisfied_ccs(d, W, l, t, deg, seed, pr_o)
+    Nn = W * pr_o.L
+    A = O.fill_uniform(kappa * Nn * d, seed + 6)
+    sch = LA.AjtaiCommitmentScheme(ctx, A.reshape(kappa, Nn, d))
+    M = LA.CCSMatrices(ctx, d, ccs.m, ccs.n, ccs.mats)
+    prover = LA.Prover(ctx, sch, LA.goldilocks_dp(d), M, l, deg, np.concatenate(ccs.c), ccs.S)
+    return pr_o, ccs, A, prover
+
+
+def witness(ccs, pr_o, seed):
+    x, w = N.satisfying_z(ccs, ccs.n - ccs.l - 1, seed)
+    fc, f = O.witness_from_w_ccs(w, ccs.d, pr_o.B, pr_o.L)
+    return x, N.Witness(w_ccs=w, f=f, f_coeff=fc)
+
+
+def acc_dict(L):
+    return {"r": flat(L.r), "v": flat(L.v), "cm": np.asarray(L.cm, np.uint64), "u": flat(L.u), "x_w": flat(L.x_w),
+            "h": np.asarray(L.h, np.uint64)}
+
+
+def dev_wit(w):
+    return {"w_ccs": dev(w.w_ccs), "f": dev(w.f), "f_coeff": dev(w.f_coeff)}
+
+
+def proof_from_device(pf, d, K, tau, t, l, kappa):
+    el = lambda a: N.elems(a, d)
+    dec = []
+    for side in range(2):
+        dec.append({"u_s": [el(x) for x in pf["u_s"][side].reshape(K, t * d)],
+                    "v_s": [el(x) for x in pf["v_s"][side].reshape(K, tau * d)],
+                    "x_s": [el(x) for x in pf["x_s"][side].reshape(K, (l + 1) * d)],
+                    "y_s": [el(x) for x in pf["y_s"][side].reshape(K, kappa * d)]})
+    return N.Proof(lin_sumcheck=pf["lin_sumcheck"], lin_v=el(pf["lin_v"]), lin_u=el(pf["lin_u"]), dec=dec,
+                   fold_sumcheck=pf["fold_sumcheck"], theta_s=[el(x) for x in pf["theta_s"].reshape(2 * K, tau * d)],
+                   eta_s=[el(x) for x in pf["eta_s"].reshape(2 * K, t * d)])
+
+
+def check_against_oracle(out, pf, w_out, o_out, o_w0, o_proof):
+    assert np.array_equal(out["r"], flat(o_out.r)), "r_0"
+    assert np.array_equal(out["v"], flat(o_out.v)), "v_0"
+    assert np.array_equal(out["cm"], o_out.cm), "cm_0"
+    assert np.array_equal(out["u"], flat(o_out.u)), "u_0"
+    assert np.array_equal(out["x_w"], flat(o_out.x_w)), "x_w"
+    assert np.array_equal(out["h"], o_out.h), "h"
+    assert np.array_equal(pf["lin_sumcheck"], o_proof.lin_sumcheck), "linearization sumcheck"
+    assert np.array_equal(pf["lin_v"], flat(o_proof.lin_v)) and np.array_equal(pf["lin_u"], flat(o_proof.lin_u))
+    for side in range(2):
+        for k in ("u_s", "v_s", "x_s", "y_s"):
+            want = flat([flat(x) for x in o_proof.dec[side][k]])
+            assert np.array_equal(pf[k][side], want), f"{k} side {side}"
+    assert np.array_equal(pf["fold_sumcheck"], o_proof.fold_sumcheck), "folding sumcheck"
+    assert np.array_equal(pf["theta_s"], flat([flat(x) for x in o_proof.theta_s])), "theta_s"
+    assert np.array_equal(pf["eta_s"], flat([flat(x) for x in o_proof.eta_s])), "eta_s"
+    for k, want in (("f", o_w0.f), ("f_coeff", o_w0.f_coeff), ("w_ccs", o_w0.w_ccs)):
+        assert np.array_equal(host(w_out[k]), want), f"folded witness {k}"
+
+
+@pytest.mark.parametrize("d,W,l,t,deg,kappa", [(24, 5, 2, 4, 2, 3), (24, 13, 4, 6, 3, 4), (1024, 5, 2, 4, 2, 2),
+                                               (16, 7, 1, 5, 3, 3)])
+def test_fold_prove_matches_oracle(d, W, l, t, deg, kappa):
+    ctx = LA.Context(0)
+    try:
+        pr_o, ccs, A, prover = setup(ctx, d, W, l, t, deg, kappa, 7 + d + W)
+        xa, Wa = witness(ccs, pr_o, 11)
+        xi, Wi = witness(ccs, pr_o, 12)
+        Nn = W * pr_o.L
+        cma = O.ajtai_commit(A, kappa, Nn, d, Wa.f)
+        cmi = O.ajtai_commit(A, kappa, Nn, d, Wi.f)
+        acc = N.linearize_fresh(ccs, cma, xa, Wa, pr_o)
+        o_out, o_w0, o_proof = N.fold_prove(ccs, A, kappa, acc, Wa, cmi, xi, Wi, pr_o)
+        w_out = {"w_ccs": zeros(W * d), "f": zeros(Nn * d), "f_coeff": zeros(Nn * d)}
+        out, pf = prover.fold_prove(acc_dict(acc), dev_wit(Wa), cmi, flat(xi), dev_wit(Wi), w_out)
+        check_against_oracle(out, pf, w_out, o_out, o_w0, o_proof)
+        # the restated verifier accepts the device's proof and re-derives its LCCCS
+        K, tau = pr_o.K, N.tb(d) if d == 24 else 1
+        v = N.fold_verify(ccs, acc, cmi, xi, proof_from_device(pf, d, K, tau, ccs.t, l, kappa), pr_o)
+        assert np.array_equal(flat(v.r), out["r"]) and np.array_equal(v.cm, out["cm"])
+        # fold again: the device's folded accumulator with a third instance
+        x3, W3 = witness(ccs, pr_o, 13)
+        cm3 = O.ajtai_commit(A, kappa, Nn, d, W3.f)
+        acc2 = N.LCCCS(r=N.elems(out["r"], d), v=N.elems(out["v"], d), cm=out["cm"], u=N.elems(out["u"], d),
+                       x_w=N.elems(out["x_w"], d), h=out["h"])
+        wacc2 = N.Witness(w_ccs=host(w_out["w_ccs"]), f=host(w_out["f"]), f_coeff=host(w_out["f_coeff"]))
+        o_out2, o_w2, o_proof2 = N.fold_prove(ccs, A, kappa, acc2, wacc2, cm3, x3, W3, pr_o)
+        w_out2 = {"w_ccs": zeros(W * d), "f": zeros(Nn * d), "f_coeff": zeros(Nn * d)}
+        out2, pf2 = prover.fold_prove(acc_dict(acc2), w_out, cm3, flat(x3), dev_wit(W3), w_out2)
+        check_against_oracle(out2, pf2, w_out2, o_out2, o_w2, o_proof2)
+    finally:
+        ctx.close()
+
+
+def test_fold_prove_montgomery_boundary():
+    """repr = LF_REPR_MONTGOMERY: ark-ff limbs in, ark-ff limbs out (zero-copy from Rust)"""
+    d, W, l, t, deg, kappa = 24, 5, 2, 4, 2, 3
+    ctx = LA.Context(0)
+    try:
+        pr_o, ccs, A, prover = setup(ctx, d, W, l, t, deg, kappa, 31)
+        xa, Wa = witness(ccs, pr_o, 11)
+        xi, Wi = witness(ccs, pr_o, 12)
+        Nn = W * pr_o.L
+        cma, cmi = O.ajtai_commit(A, kappa, Nn, d, Wa.f), O.ajtai_commit(A, kappa, Nn, d, Wi.f)
+        acc = N.linearize_fresh(ccs, cma, xa, Wa, pr_o)
+        mont = np.vectorize(O.to_mont, otypes=[np.uint64])
+        unmont = np.vectorize(O.from_mont, otypes=[np.uint64])
+        w1 = {"w_ccs": zeros(W * d), "f": zeros(Nn * d), "f_coeff": zeros(Nn * d)}
+        out_c, pf_c = prover.fold_prove(acc_dict(acc), dev_wit(Wa), cmi, flat(xi), dev_wit(Wi), w1)
+        accm = {k: mont(v) for k, v in acc_dict(acc).items()}
+        w2 = {"w_ccs": zeros(W * d), "f": zeros(Nn * d), "f_coeff": zeros(Nn * d)}
+        out_m, pf_m = prover.fold_prove(accm, dev_wit(Wa), mont(cmi), mont(flat(xi)), dev_wit(Wi), w2,
+                                        repr=LA.REPR_MONTGOMERY)
+        for k in out_c:
+            assert np.array_equal(unmont(out_m[k]), out_c[k]) if out_c[k].size else True, k
+        assert np.array_equal(unmont(pf_m["fold_sumcheck"]), pf_c["fold_sumcheck"])
+        assert np.array_equal(unmont(pf_m["y_s"][1]), pf_c["y_s"][1])
+    finally:
+        ctx.close()
