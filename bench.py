@@ -697,7 +697,9 @@ def next_rows(LA, torch, local, cpu):
                     f"K={K} decomposed vectors",
         "challenged_mle_ms": ms_ch, "etas_ms": ms_ev,
         "challenged_gbs_values": val_bytes / (ms_ch * 1e-3) / 1e9}
-    del M, z, ch, ev
+    del z, ch, ev
+    out["fold_prove"] = fold_prove_line(LA, torch, ctx, M, S, d, nn, t, mm)
+    del M
     # the memory Merkle tree of the zkvm's 8 MB VM (8192 pages of 256 words,
     # vm.rs:106-124; commitments.rs:192-262): 8192 sponge chains of 64 width-8
     # permutations, then 13 levels of compressions
@@ -714,6 +716,62 @@ def next_rows(LA, torch, local, cpu):
     ctx.close()
     torch.cuda.empty_cache()
     return out
+
+
+def fold_prove_line(LA, torch, ctx, M, S, d, n, t, m):
+    """the zkvm's whole fold() (lf_fold_prove: zk_latticefold_prove with its
+    transcript, linearization, two decompositions and the folding prover) at the
+    zkvm's shape on the reference ring: l = 4, W = n - 5 = 19 763, kappa = 32,
+    the CCS above (t = 125, m = 2^17) with the 52 multisets of the
+    linearization line and degree 7; random (not satisfying) witnesses, which
+    the prover does not check. Wall time per call, host transcript included."""
+    l, kappa, deg = 4, 32, 7
+    W = n - l - 1
+    pr = LA.goldilocks_dp(d)
+    N = W * pr.L
+    i64 = dict(dtype=torch.int64, device=f"cuda:{torch.cuda.current_device()}")
+    A = torch.empty(kappa * N * d, **i64)
+    ctx.dev_fill_uniform(A, SEED_A)
+    sch = LA.AjtaiCommitmentScheme(ctx, device_tensor=A, kappa=kappa, ncols=N, d=d)
+    del A
+    rng = np.random.default_rng(0x4C460018)
+    c = rng.integers(0, 1 << 62, len(S) * d, dtype=np.uint64)
+    prover = LA.Prover(ctx, sch, pr, M, l, deg, c, S)
+
+    def wit(seed):
+        w = {"w_ccs": torch.empty(W * d, **i64), "f": torch.empty(N * d, **i64), "f_coeff": torch.empty(N * d, **i64)}
+        ctx.dev_fill_uniform(w["w_ccs"], seed)
+        ctx.check(ctx.lib.lf_dev_witness_from_w_ccs(ctx.h, LA._lib.C.byref(pr), w["w_ccs"].data_ptr(), W,
+                                                    w["f_coeff"].data_ptr(), w["f"].data_ptr()))
+        cm = torch.empty(kappa * d, **i64)
+        ctx.dev_ajtai_commit(sch, [w["f"]], cm)
+        x = rng.integers(0, 1 << 62, l * d, dtype=np.uint64)
+        return x, w, cm.cpu().numpy().view(np.uint64)
+
+    xa, wa, cma = wit(SEED_ACC)
+    xi, wi, cmi = wit(SEED_W)
+    acc, _ = prover.linearize(cma, xa, wa)
+    w_out = {"w_ccs": torch.empty(W * d, **i64), "f": torch.empty(N * d, **i64), "f_coeff": torch.empty(N * d, **i64)}
+    times = []
+    for _ in range(4):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        prover.fold_prove(acc, wa, cmi, xi, wi, w_out)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    t0 = time.perf_counter()
+    prover.linearize(cma, xa, wa)
+    torch.cuda.synchronize()
+    t_lin = time.perf_counter() - t0
+    del prover, sch
+    torch.cuda.empty_cache()
+    return {"workload": f"zkvm fold() end to end (lf_fold_prove): Phi_72, W={W} (n={n}, l={l}), kappa={kappa}, "
+                        f"CCS t={t} x {m} rows, {len(S)} multisets, degree {deg}; transcript on the host",
+            "ms_per_fold_prove": min(times[1:]) * 1e3, "ms_per_fold_prove_median": float(np.median(times[1:])) * 1e3,
+            "ms_per_linearize": t_lin * 1e3,
+            "note": "beside the rho-as-input step of reference_ring: this adds the linearization (Mz, degree-8 "
+                    "sumcheck), the decompositions' u_s / v_s, the folding sumcheck, theta_s / eta_s and the "
+                    "transcript"}
 
 
 EXCLUDED = ("outside the timed step (other tiers): the Poseidon2 transcript and challenge derivation (rho is an "

@@ -508,6 +508,11 @@ const uint64_t *lf_ccs_c_device(const lf_ccs *M);
 int lf_prover_create(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, const lf_ccs *ccs, lf_prover **out);
 void lf_prover_destroy(lf_prover *prover);
 const char *lf_prover_last_error(const lf_prover *prover);
+/* LFLinearizationProver::prove of a CCCS (cm, x_ccs) with witness w on a fresh
+ * transcript -- initialize_accumulator's accumulator (zkvm/src/main.rs:305-344):
+ * the LCCCS {r, v, cm, u, x_ccs, ONE} and the linearization sumcheck [s][degree + 2] */
+int lf_linearize(lf_prover *prover, const uint64_t *cm, const uint64_t *x_ccs, const lf_witness *w, lf_lcccs_mut *out,
+                 uint64_t *lin_sumcheck, int repr);
 int lf_fold_prove(lf_prover *prover, const lf_lcccs *acc, const lf_witness *w_acc, const uint64_t *cm_i,
                   const uint64_t *x_ccs, const lf_witness *w_i, lf_lcccs_mut *out, const lf_witness *w_out,
                   lf_lfproof_mut *proof, int repr);

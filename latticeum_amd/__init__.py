@@ -528,6 +528,25 @@ class Prover:
         out["x_w"] = out["x_w"][:l * d]
         return out, pf
 
+    def linearize(self, cm, x_ccs, w: dict, repr: int = REPR_CANONICAL):
+        """initialize_accumulator's LFLinearizationProver::prove on a fresh transcript:
+        -> (LCCCS dict, linearization sumcheck messages)"""
+        from ._lib import LfLcccsMut, LfWitness
+        d, s, tau, t, l = self.d, self.s, self.tau, self.t, self.l
+        out = {"r": np.zeros(s * d, np.uint64), "v": np.zeros(tau * d, np.uint64),
+               "cm": np.zeros(self.kappa * d, np.uint64), "u": np.zeros(t * d, np.uint64),
+               "x_w": np.zeros(max(l, 1) * d, np.uint64), "h": np.zeros(d, np.uint64)}
+        sc = np.zeros(s * (self.degree + 2) * d, np.uint64)
+        O_ = LfLcccsMut(*[out[k].ctypes.data for k in ("r", "v", "cm", "u", "x_w", "h")])
+        cm, xc = _u64(cm), (_u64(x_ccs) if l else np.zeros(1, np.uint64))
+        wi = LfWitness(_dptr(w["w_ccs"]), _dptr(w["f"]), _dptr(w["f_coeff"]))
+        rc = self.lib.lf_linearize(self.h, cm.ctypes.data, xc.ctypes.data, C.byref(wi), C.byref(O_), sc.ctypes.data,
+                                   repr)
+        if rc:
+            raise LfError(rc, self.lib.lf_prover_last_error(self.h).decode() or self.lib.lf_status_string(rc).decode())
+        out["x_w"] = out["x_w"][:l * d]
+        return out, sc
+
     def __del__(self):
         try:
             if self.h:

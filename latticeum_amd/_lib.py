@@ -156,6 +156,7 @@ SIGNATURES = {
     "lf_prover_last_error": (C.c_char_p, [VP]),
     "lf_fold_prove": (I, [VP, C.POINTER(LfLcccs), C.POINTER(LfWitness), VP, VP, C.POINTER(LfWitness),
                           C.POINTER(LfLcccsMut), C.POINTER(LfWitness), C.POINTER(LfLfproofMut), I]),
+    "lf_linearize": (I, [VP, VP, VP, C.POINTER(LfWitness), C.POINTER(LfLcccsMut), VP, I]),
     "lf_dev_decompose_commit": (I, [VP, VP, C.POINTER(LfParams), SZ, C.POINTER(LfFoldStepBufs)]),
     "lf_dev_fold_combine": (I, [VP, VP, C.POINTER(LfParams), SZ, C.POINTER(LfFoldStepBufs)]),
     "lf_dev_fhat_evaluate": (I, [VP, I, VP, SZ, SZ, I, I, VP, VP]),

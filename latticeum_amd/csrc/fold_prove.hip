@@ -134,6 +134,55 @@ struct Run {
   }
 };
 
+// LFLinearizationProver::prove (linearization.rs:153-197) of the CCCS (cm, x_ccs)
+// with witness w, on the transcript R.T: the sumcheck messages into lin_sumcheck
+// (host), and r, v, u of the linearized instance {r, v, cm, u, x_ccs, ONE}
+int linearize(lf_prover *P, Run &R, const std::vector<uint64_t> &xc, const lf_witness *w_i, uint64_t *lin_sumcheck,
+              std::vector<uint64_t> &r_lin, std::vector<uint64_t> &lv, std::vector<uint64_t> &lu) {
+  lf_ctx *C = P->ctx;
+  const int d = P->d, tb = P->tb, tau = P->tau, s = P->s, t = P->t;
+  const size_t W = P->W, N = P->N, nn = P->nn, l = P->l;
+  std::vector<uint64_t> one(d, 0);
+  for (int i = 0; i < d; i += tb) one[i] = 1;
+  R.absorb_label("beta_s");  // squeeze_beta_challenges (linearization/utils.rs:111-124)
+  const std::vector<uint64_t> beta = R.challenges(s);
+  R.h2d(P->beta, beta.data(), (size_t)s * d);
+  // z = x_ccs || 1 || w_ccs (Instance::get_z_vector), the Mz MLEs, the MLE list + eq(beta)
+  R.h2d(P->z, xc.data(), l * d);
+  R.h2d(P->z + l * d, one.data(), d);
+  R.d2d(P->z + (l + 1) * d, w_i->w_ccs, W * d);
+  R.check(lf_dev_mz_mles(C, P->ccs, P->z, 1, s, P->mz), "Mz MLEs");
+  for (size_t k = 0; k < P->lin_list.size(); k++) R.d2d(P->lin + k * nn * d, P->mz + (size_t)P->lin_list[k] * nn * d, nn * d);
+  R.check(lf_dev_eq_table(C, d, P->beta, s, P->lin + P->lin_list.size() * nn * d), "eq(beta)");
+  std::vector<uint64_t> rnd((size_t)s * tb);
+  {
+    lf_comb cb{};
+    cb.kind = LF_COMB_LINEARIZATION;
+    cb.q = P->q;
+    cb.c = lf_ccs_c_device(P->ccs);
+    cb.S_off = P->S_off.data();
+    cb.S_idx = P->S_idx.data();
+    if (R.rc == LF_OK)
+      R.check(lf_sumcheck_prove(C, R.T, &cb, P->lin, P->nm_lin, s, d, P->degree + 1, lin_sumcheck, rnd.data()),
+              "linearization sumcheck");
+  }
+  if (R.rc) return R.rc;
+  r_lin.assign((size_t)s * d, 0);
+  for (int i = 0; i < s; i++) broadcast(rnd.data() + (size_t)i * tb, tb, d, r_lin.data() + (size_t)i * d);
+  R.h2d(P->pt, r_lin.data(), (size_t)s * d);
+  // v = f_hat(w_i) at r, u = MLE(M_j z)(r) (compute_evaluation_vectors, :130-147)
+  R.check(lf_dev_fhat_evaluate(C, d, w_i->f_coeff, N, 0, 1, s, P->pt, P->val), "v");
+  R.check(lf_dev_mle_evaluate(C, d, P->mz, t, s, P->pt, P->val + (size_t)tau * d), "u");
+  lv.assign((size_t)tau * d, 0);
+  lu.assign((size_t)t * d, 0);
+  R.d2h(lv.data(), P->val, (size_t)tau * d);
+  R.d2h(lu.data(), P->val + (size_t)tau * d, (size_t)t * d);
+  if (R.rc) return R.rc;
+  R.absorb(lv.data(), tau);
+  R.absorb(lu.data(), t);
+  return LF_OK;
+}
+
 int bad(lf_prover *P, int code, const char *msg) {
   P->err = msg;
   return code;
@@ -241,6 +290,48 @@ int lf_prover_create(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, const
 
 void lf_prover_destroy(lf_prover *P) { delete P; }
 
+int lf_linearize(lf_prover *P, const uint64_t *cm, const uint64_t *x_ccs, const lf_witness *w, lf_lcccs_mut *out,
+                 uint64_t *lin_sumcheck, int repr) {
+  if (!P || !cm || (!x_ccs && P->l) || !w || !w->w_ccs || !w->f_coeff || !out || !lin_sumcheck || !out->r || !out->v ||
+      !out->cm || !out->u || (P->l && !out->x_w) || !out->h)
+    return LF_ERR_INVALID_ARG;
+  if (repr != LF_REPR_CANONICAL && repr != LF_REPR_MONTGOMERY) return bad(P, LF_ERR_INVALID_ARG, "repr");
+  const int d = P->d, s = P->s, tau = P->tau, t = P->t;
+  const size_t l = P->l, kd = P->kappa * d;
+  std::vector<uint64_t> cmv(cm, cm + kd), xc(x_ccs ? x_ccs : cm, x_ccs ? x_ccs + l * d : cm);
+  if (repr == LF_REPR_MONTGOMERY) {
+    for (auto &x : cmv) x = gl::from_mont(x);
+    for (auto &x : xc) x = gl::from_mont(x);
+  }
+  Run R{P, lf_transcript_new(), (hipStream_t)lf_ctx_get_stream(P->ctx)};
+  struct TGuard {
+    lf_transcript *t;
+    ~TGuard() { lf_transcript_free(t); }
+  } tg{R.T};
+  std::vector<uint64_t> r_lin, lv, lu;
+  if (linearize(P, R, xc, w, lin_sumcheck, r_lin, lv, lu)) return R.rc;
+  // the LCCCS {r, v, cm, u, x_w = x_ccs, h = ONE} (linearization.rs:185-193)
+  memcpy(out->r, r_lin.data(), r_lin.size() * 8);
+  memcpy(out->v, lv.data(), lv.size() * 8);
+  memcpy(out->cm, cmv.data(), kd * 8);
+  memcpy(out->u, lu.data(), lu.size() * 8);
+  if (l) memcpy(out->x_w, xc.data(), l * d * 8);
+  for (int i = 0; i < d; i++) out->h[i] = i % P->tb == 0 ? 1 : 0;
+  if (repr == LF_REPR_MONTGOMERY) {
+    auto mont = [](uint64_t *p, size_t elems) {
+      for (size_t i = 0; i < elems; i++) p[i] = gl::to_mont(p[i]);
+    };
+    mont(out->r, (size_t)s * d);
+    mont(out->v, (size_t)tau * d);
+    mont(out->cm, kd);
+    mont(out->u, (size_t)t * d);
+    mont(out->x_w, l * d);
+    mont(out->h, d);
+    mont(lin_sumcheck, (size_t)s * (P->degree + 2) * d);
+  }
+  return LF_OK;
+}
+
 const char *lf_prover_last_error(const lf_prover *P) { return P ? P->err.c_str() : ""; }
 
 int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, const uint64_t *cm_i,
@@ -303,41 +394,8 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
   R.absorb(xc.data(), l);
 
   // ---- linearization (linearization.rs:153-197)
-  R.absorb_label("beta_s");  // squeeze_beta_challenges (linearization/utils.rs:111-124)
-  const std::vector<uint64_t> beta = R.challenges(s);
-  R.h2d(P->beta, beta.data(), (size_t)s * d);
-  // z = x_ccs || 1 || w_ccs (Instance::get_z_vector), the Mz MLEs, the MLE list + eq(beta)
-  R.h2d(P->z, xc.data(), l * d);
-  R.h2d(P->z + l * d, one.data(), d);
-  R.d2d(P->z + (l + 1) * d, w_i->w_ccs, W * d);
-  R.check(lf_dev_mz_mles(C, P->ccs, P->z, 1, s, P->mz), "Mz MLEs");
-  for (size_t k = 0; k < P->lin_list.size(); k++) R.d2d(P->lin + k * nn * d, P->mz + (size_t)P->lin_list[k] * nn * d, nn * d);
-  R.check(lf_dev_eq_table(C, d, P->beta, s, P->lin + P->lin_list.size() * nn * d), "eq(beta)");
-  std::vector<uint64_t> rnd((size_t)s * tb);
-  {
-    lf_comb cb{};
-    cb.kind = LF_COMB_LINEARIZATION;
-    cb.q = P->q;
-    cb.c = lf_ccs_c_device(P->ccs);
-    cb.S_off = P->S_off.data();
-    cb.S_idx = P->S_idx.data();
-    if (R.rc == LF_OK)
-      R.check(lf_sumcheck_prove(C, R.T, &cb, P->lin, P->nm_lin, s, d, P->degree + 1, proof->lin_sumcheck, rnd.data()),
-              "linearization sumcheck");
-  }
-  if (R.rc) return R.rc;
-  std::vector<uint64_t> r_lin((size_t)s * d);
-  for (int i = 0; i < s; i++) broadcast(rnd.data() + (size_t)i * tb, tb, d, r_lin.data() + (size_t)i * d);
-  R.h2d(P->pt, r_lin.data(), (size_t)s * d);
-  // v = f_hat(w_i) at r, u = MLE(M_j z)(r) (compute_evaluation_vectors, :130-147)
-  R.check(lf_dev_fhat_evaluate(C, d, w_i->f_coeff, N, 0, 1, s, P->pt, P->val), "v");
-  R.check(lf_dev_mle_evaluate(C, d, P->mz, t, s, P->pt, P->val + (size_t)tau * d), "u");
-  std::vector<uint64_t> lv((size_t)tau * d), lu((size_t)t * d);
-  R.d2h(lv.data(), P->val, (size_t)tau * d);
-  R.d2h(lu.data(), P->val + (size_t)tau * d, (size_t)t * d);
-  if (R.rc) return R.rc;
-  R.absorb(lv.data(), tau);
-  R.absorb(lu.data(), t);
+  std::vector<uint64_t> r_lin, lv, lu;
+  if (linearize(P, R, xc, w_i, proof->lin_sumcheck, r_lin, lv, lu)) return R.rc;
   // the linearized instance: {r, v, cm_i, u, x_ccs, h = ONE}
 
   // ---- the two decompositions (decomposition.rs:33-88), device work of both first
@@ -433,6 +491,7 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
             "g");
   }
   R.check(lf_dev_eq_table(C, d, P->beta, s, M + 4 * mstride), "eq(beta)");
+  std::vector<uint64_t> rnd((size_t)s * tb);
   {
     lf_comb cb{};
     cb.kind = LF_COMB_FOLDING;

@@ -575,6 +575,43 @@ def satisfied_ccs(d: int, W: int, l: int, t: int, deg: int, seed: int, pr: Param
     return CCS(d=d, m=m, n=n, l=l, mats=mats, c=[one(d), from_u(P - 1, d)], S=[list(range(deg)), [deg]], degree=deg)
 
 
+def satisfied_ccs_np(d: int, W: int, l: int, t: int, deg: int, seed: int, pr: Params, per_row: int = 2,
+                     extra_density: float = 1.0):
+    """satisfied_ccs's construction vectorised with numpy for large shapes (the
+    zkvm's t = 125, m = 2^17): the same row rules (A_j, j < deg: 1..per_row
+    entries on the free columns, rows past the product columns repeating row
+    r mod nprod; matrix deg: the product column of the row's owner; extras:
+    random entries anywhere, in a random extra_density share of the rows)"""
+    rng = np.random.default_rng(seed)
+    n = l + 1 + W
+    m = 1 << ((W * pr.L) - 1).bit_length()
+    free = l + 1 + W // 2
+    nprod = n - free
+    src = np.arange(m) % nprod  # the row every row repeats (itself for r < nprod)
+    mats = []
+    for j in range(t):
+        if j == deg:
+            col = (free + src).astype(np.uint32)
+            rp = np.arange(m + 1, dtype=np.uint64)
+            val = np.tile(one(d), m)
+        else:
+            base = nprod if j < deg else m
+            cnt = rng.integers(1, per_row + 1, base)
+            if j > deg and extra_density < 1.0:
+                cnt[rng.random(base) >= extra_density] = 0
+            off = np.concatenate([[0], np.cumsum(cnt)])
+            cols = rng.integers(0, free if j < deg else n, int(off[-1])).astype(np.uint32)
+            vals = O.fill_uniform(int(off[-1]) * d, seed + 1000 + j).reshape(-1, d)
+            rows = src if j < deg else np.arange(m)
+            c_r = cnt[rows]
+            rp = np.concatenate([[0], np.cumsum(c_r)]).astype(np.uint64)
+            gather = np.repeat(off[rows], c_r) + (np.arange(int(rp[-1])) - np.repeat(rp[:-1].astype(np.int64), c_r))
+            col = cols[gather]
+            val = vals[gather].ravel()
+        mats.append((rp, col, val))
+    return CCS(d=d, m=m, n=n, l=l, mats=mats, c=[one(d), from_u(P - 1, d)], S=[list(range(deg)), [deg]], degree=deg)
+
+
 def satisfying_z(ccs: CCS, W: int, seed: int):
     """(x_ccs [l][d], w_ccs [W d]) with z = x || 1 || w satisfying satisfied_ccs's CCS:
     random free columns, then each product column = prod_j (A_j z) of its row"""

@@ -149,3 +149,82 @@ def test_fold_prove_montgomery_boundary():
         assert np.array_equal(unmont(pf_m["y_s"][1]), pf_c["y_s"][1])
     finally:
         ctx.close()
+
+
+def test_linearize_matches_oracle():
+    """lf_linearize (initialize_accumulator's LFLinearizationProver::prove) against the oracle"""
+    d, W, l, t, deg, kappa = 24, 13, 4, 6, 3, 4
+    ctx = LA.Context(0)
+    try:
+        pr_o, ccs, A, prover = setup(ctx, d, W, l, t, deg, kappa, 41)
+        x, Wt = witness(ccs, pr_o, 42)
+        cm = O.ajtai_commit(A, kappa, W * pr_o.L, d, Wt.f)
+        out, sc = prover.linearize(cm, flat(x), dev_wit(Wt))
+        tr = N.Transcript(d)
+        o, (oproof, _, _) = N.linearize(tr, ccs, cm, x, Wt, pr_o)
+        assert np.array_equal(sc, oproof)
+        for k in ("r", "v", "u", "x_w"):
+            assert np.array_equal(out[k], flat(getattr(o, k))), k
+        assert np.array_equal(out["cm"], cm) and np.array_equal(out["h"], N.one(d))
+    finally:
+        ctx.close()
+
+
+def test_fold_prove_zkvm_dimensions():
+    """the zkvm's shape (ZK/ccs.rs:26-67): Phi_72, W = 19 763 (n = 19 768, l = 4),
+    m = 2^17, t = 125 matrices, a degree-7 multiset (the Poseidon2 S-box's),
+    kappa = 32, GoldiLocksDP. The accumulator comes from lf_linearize; the
+    restated NIFS verifier accepts the device's proof and re-derives its LCCCS,
+    and that LCCCS is the folded witness's (cm_0 = A f_0, v_0, u_0)."""
+    import torch
+    d, W, l, t, deg, kappa = 24, 19763, 4, 125, 7, 32
+    pr_o = N.Params(d)
+    ccs = N.satisfied_ccs_np(d, W, l, t, deg, 0x4C46, pr_o, extra_density=1 / 16)
+    assert ccs.m == 1 << 17 and ccs.n == 19768
+    ctx = LA.Context(0)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        pr = LA.goldilocks_dp(d)
+        Nn = W * pr.L
+        A = torch.empty(kappa * Nn * d, dtype=torch.int64, device="cuda")
+        ctx.dev_fill_uniform(A, 0x4C460004)
+        sch = LA.AjtaiCommitmentScheme(ctx, device_tensor=A, kappa=kappa, ncols=Nn, d=d)
+        M = LA.CCSMatrices(ctx, d, ccs.m, ccs.n, ccs.mats)
+        prover = LA.Prover(ctx, sch, pr, M, l, deg, np.concatenate(ccs.c), ccs.S)
+
+        def dwit(seed):
+            x, w = N.satisfying_z(ccs, W, seed)
+            wd = {"w_ccs": dev(w), "f": zeros(Nn * d), "f_coeff": zeros(Nn * d)}
+            ctx.check(ctx.lib.lf_dev_witness_from_w_ccs(ctx.h, LA._lib.C.byref(pr), wd["w_ccs"].data_ptr(), W,
+                                                        wd["f_coeff"].data_ptr(), wd["f"].data_ptr()))
+            cm = zeros(kappa * d)
+            ctx.dev_ajtai_commit(sch, [wd["f"]], cm)
+            ctx.sync()
+            return flat(x), wd, host(cm)
+
+        xa, wa, cma = dwit(101)
+        xi, wi, cmi = dwit(102)
+        acc, _ = prover.linearize(cma, xa, wa)
+        w_out = {"w_ccs": zeros(W * d), "f": zeros(Nn * d), "f_coeff": zeros(Nn * d)}
+        out, pf = prover.fold_prove(acc, wa, cmi, xi, wi, w_out)
+        el = lambda a: N.elems(a, d)
+        acc_o = N.LCCCS(r=el(acc["r"]), v=el(acc["v"]), cm=acc["cm"], u=el(acc["u"]), x_w=el(acc["x_w"]), h=acc["h"])
+        v = N.fold_verify(ccs, acc_o, cmi, el(xi), proof_from_device(pf, d, pr.K, 3, t, l, kappa), pr_o)
+        for k in ("r", "v", "u", "x_w"):
+            assert np.array_equal(flat(getattr(v, k)), out[k]), k
+        assert np.array_equal(v.cm, out["cm"]) and np.array_equal(v.h, out["h"])
+        # the folded instance is the folded witness's
+        cm0 = zeros(kappa * d)
+        ctx.dev_ajtai_commit(sch, [w_out["f"]], cm0)
+        r0 = dev(out["r"])
+        v0 = zeros(3 * d)
+        ctx.check(ctx.lib.lf_dev_fhat_evaluate(ctx.h, d, w_out["f_coeff"].data_ptr(), Nn, 0, 1, 17, r0.data_ptr(),
+                                               v0.data_ptr()))
+        z0 = torch.cat([dev(out["x_w"]), dev(out["h"]), w_out["w_ccs"]])
+        u0 = zeros(t * d)
+        M.mz_evaluate(z0, 1, 17, r0, u0)
+        ctx.sync()
+        assert np.array_equal(host(cm0), out["cm"]) and np.array_equal(host(v0), out["v"])
+        assert np.array_equal(host(u0), out["u"])
+    finally:
+        ctx.close()

@@ -88,3 +88,25 @@ def test_fold_verify_rejects_unsatisfied_ccs():
     _, _, proof = N.fold_prove(ccs, A, kappa, acc, Wa, cmi, xi, Wi, pr)
     with pytest.raises(ValueError, match="linearization"):
         N.fold_verify(ccs, acc, cmi, xi, proof, pr)
+
+
+def test_vectorised_ccs_builder_is_satisfied():
+    """satisfied_ccs_np (the large-shape builder) gives satisfiable CCS instances too"""
+    pr = N.Params(24)
+    ccs = N.satisfied_ccs_np(24, 13, 4, 6, 3, 5, pr)
+    x, w = N.satisfying_z(ccs, 13, 6)
+    assert N.check_relation(ccs, np.concatenate(list(x) + [N.one(24), w]))
+    # and it folds: prove -> verify
+    Nn = 13 * pr.L
+    A = O.fill_uniform(2 * Nn * 24, 8)
+
+    def wit(ww):
+        fc, f = O.witness_from_w_ccs(ww, 24, pr.B, pr.L)
+        return N.Witness(w_ccs=ww, f=f, f_coeff=fc)
+
+    xa, wa = N.satisfying_z(ccs, 13, 9)
+    Wa, Wi = wit(wa), wit(w)
+    acc = N.linearize_fresh(ccs, O.ajtai_commit(A, 2, Nn, 24, Wa.f), xa, Wa, pr)
+    cmi = O.ajtai_commit(A, 2, Nn, 24, Wi.f)
+    out, _, proof = N.fold_prove(ccs, A, 2, acc, Wa, cmi, x, Wi, pr)
+    same_lcccs(out, N.fold_verify(ccs, acc, cmi, x, proof, pr))
