@@ -505,6 +505,24 @@ int lf_ccs_set_structure(lf_ctx *ctx, lf_ccs *M, size_t l, int degree, int q, co
 int lf_ccs_shape(const lf_ccs *M, int *t, size_t *m, size_t *n, size_t *l, int *q, int *degree);
 int lf_ccs_get_structure(const lf_ccs *M, uint64_t *c, int *S_off, int *S_idx);
 const uint64_t *lf_ccs_c_device(const lf_ccs *M);
+/* tracing spans of lf_fold_prove (the reference's #[instrument] spans): wall ms per
+ * phase, summed over calls since timing was (re)set; each phase ends with a
+ * stream sync while timing is on */
+enum {
+  LF_SPAN_PUBLIC_INPUT = 0,           /* absorb_public_input */
+  LF_SPAN_LINEARIZATION = 1,          /* beta, Mz, the degree-(d+1) sumcheck, v, u */
+  LF_SPAN_DECOMPOSITION = 2,          /* x_s, decompose + commit_witnesses, v_s, u_s */
+  LF_SPAN_DECOMPOSITION_TRANSCRIPT = 3, /* the 2K decomposed instances absorbed */
+  LF_SPAN_FOLDING_MLES = 4,           /* alpha..beta, f_hat MLEs, challenged Mz, g, eq tables */
+  LF_SPAN_FOLDING_SUMCHECK = 5,       /* the degree-2 b_small sumcheck */
+  LF_SPAN_EVALUATIONS = 6,            /* theta_s, eta_s */
+  LF_SPAN_FOLDING_TRANSCRIPT = 7,     /* theta_s, eta_s absorbed, get_rhos */
+  LF_SPAN_FOLD = 8,                   /* CRT(rho), cm_0, f_0, from_f, v_0, u_0, x_0 */
+  LF_SPAN_COUNT = 9
+};
+/* span_ms (LF_SPAN_COUNT, may be NULL) receives the sums so far; then timing is set to
+ * `enable` and the sums are cleared */
+int lf_prover_timing(lf_prover *prover, int enable, double *span_ms);
 int lf_prover_create(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, const lf_ccs *ccs, lf_prover **out);
 void lf_prover_destroy(lf_prover *prover);
 const char *lf_prover_last_error(const lf_prover *prover);

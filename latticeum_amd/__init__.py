@@ -528,6 +528,15 @@ class Prover:
         out["x_w"] = out["x_w"][:l * d]
         return out, pf
 
+    SPANS = ("public_input", "linearization", "decomposition", "decomposition_transcript", "folding_mles",
+             "folding_sumcheck", "evaluations", "folding_transcript", "fold")
+
+    def timing(self, enable: bool) -> dict:
+        """the fold() phase spans (ms, summed) since the last call; then timing on/off"""
+        ms = np.zeros(len(self.SPANS), np.float64)
+        self.lib.lf_prover_timing(self.h, int(enable), ms.ctypes.data)
+        return dict(zip(self.SPANS, ms.tolist()))
+
     def linearize(self, cm, x_ccs, w: dict, repr: int = REPR_CANONICAL):
         """initialize_accumulator's LFLinearizationProver::prove on a fresh transcript:
         -> (LCCCS dict, linearization sumcheck messages)"""

@@ -154,6 +154,7 @@ SIGNATURES = {
     "lf_prover_create": (I, [VP, VP, C.POINTER(LfParams), VP, C.POINTER(VP)]),
     "lf_prover_destroy": (None, [VP]),
     "lf_prover_last_error": (C.c_char_p, [VP]),
+    "lf_prover_timing": (I, [VP, I, VP]),
     "lf_fold_prove": (I, [VP, C.POINTER(LfLcccs), C.POINTER(LfWitness), VP, VP, C.POINTER(LfWitness),
                           C.POINTER(LfLcccsMut), C.POINTER(LfWitness), C.POINTER(LfLfproofMut), I]),
     "lf_linearize": (I, [VP, VP, VP, C.POINTER(LfWitness), C.POINTER(LfLcccsMut), VP, I]),

@@ -13,6 +13,7 @@
 // hundred ring elements -- cross PCIe. The witnesses stay in HBM.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -40,6 +41,10 @@ struct lf_prover {
   uint64_t *theta = nullptr, *eta = nullptr, *rho = nullptr, *rhoc = nullptr, *cm0 = nullptr, *u0 = nullptr, *x0 = nullptr,
            *v0 = nullptr, *r0 = nullptr;
   std::string err;
+  // tracing spans (the reference's #[instrument] spans, zkvm/src/main.rs:56-63):
+  // wall ms of each fold() phase, measured with a stream sync at its end
+  bool timing = false;
+  double span_ms[LF_SPAN_COUNT] = {};
   ~lf_prover() {
     if (mem) {
       int prev = -1;
@@ -77,6 +82,16 @@ struct Run {
   lf_transcript *T;
   hipStream_t st;
   int rc = LF_OK;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+
+  // close the span that ran since the last mark (only with timing on)
+  void mark(int span) {
+    if (!P->timing) return;
+    (void)hipStreamSynchronize(st);
+    const auto now = std::chrono::steady_clock::now();
+    P->span_ms[span] += std::chrono::duration<double, std::milli>(now - t0).count();
+    t0 = now;
+  }
 
   int check(int r, const char *what) {
     if (r != LF_OK && rc == LF_OK) {
@@ -334,6 +349,14 @@ int lf_linearize(lf_prover *P, const uint64_t *cm, const uint64_t *x_ccs, const 
 
 const char *lf_prover_last_error(const lf_prover *P) { return P ? P->err.c_str() : ""; }
 
+int lf_prover_timing(lf_prover *P, int enable, double *span_ms) {
+  if (!P) return LF_ERR_INVALID_ARG;
+  if (span_ms) memcpy(span_ms, P->span_ms, sizeof(P->span_ms));
+  P->timing = enable != 0;
+  memset(P->span_ms, 0, sizeof(P->span_ms));
+  return LF_OK;
+}
+
 int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, const uint64_t *cm_i,
                   const uint64_t *x_ccs, const lf_witness *w_i, lf_lcccs_mut *out, const lf_witness *w_out,
                   lf_lfproof_mut *proof, int repr) {
@@ -393,9 +416,11 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
   R.absorb(cmi.data(), kappa);
   R.absorb(xc.data(), l);
 
+  R.mark(LF_SPAN_PUBLIC_INPUT);
   // ---- linearization (linearization.rs:153-197)
   std::vector<uint64_t> r_lin, lv, lu;
   if (linearize(P, R, xc, w_i, proof->lin_sumcheck, r_lin, lv, lu)) return R.rc;
+  R.mark(LF_SPAN_LINEARIZATION);
   // the linearized instance: {r, v, cm_i, u, x_ccs, h = ONE}
 
   // ---- the two decompositions (decomposition.rs:33-88), device work of both first
@@ -433,6 +458,7 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
     R.check(lf_dev_mz_evaluate(C, P->ccs, P->zdec[side], K, s, P->pt, P->us + (size_t)side * K * t * d), "u_s");
   }
   if (R.rc) return R.rc;
+  R.mark(LF_SPAN_DECOMPOSITION);
   for (int side = 0; side < 2; side++) {
     R.d2h(proof->x_s[side], P->xs + (size_t)side * K * (l + 1) * d, (size_t)K * (l + 1) * d);
     R.d2h(proof->y_s[side], P->y[side], (size_t)K * kd);
@@ -447,6 +473,7 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
     }
   }
 
+  R.mark(LF_SPAN_DECOMPOSITION_TRANSCRIPT);
   // ---- folding (folding.rs:42-130)
   R.absorb_label("alpha_s");  // squeeze_alpha_beta_zeta_mu (folding/utils.rs:51-96)
   const std::vector<uint64_t> alpha = R.challenges(2 * K);
@@ -492,6 +519,7 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
   }
   R.check(lf_dev_eq_table(C, d, P->beta, s, M + 4 * mstride), "eq(beta)");
   std::vector<uint64_t> rnd((size_t)s * tb);
+  R.mark(LF_SPAN_FOLDING_MLES);
   {
     lf_comb cb{};
     cb.kind = LF_COMB_FOLDING;
@@ -504,6 +532,7 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
               "folding sumcheck");
   }
   if (R.rc) return R.rc;
+  R.mark(LF_SPAN_FOLDING_SUMCHECK);
   std::vector<uint64_t> r0((size_t)s * d);
   for (int i = 0; i < s; i++) broadcast(rnd.data() + (size_t)i * tb, tb, d, r0.data() + (size_t)i * d);
   R.h2d(P->r0, r0.data(), (size_t)s * d);
@@ -515,6 +544,7 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
   R.d2h(proof->theta_s, P->theta, 2 * (size_t)K * tau * d);
   R.d2h(proof->eta_s, P->eta, 2 * (size_t)K * t * d);
   if (R.rc) return R.rc;
+  R.mark(LF_SPAN_EVALUATIONS);
   for (int i = 0; i < 2 * K; i++) R.absorb(proof->theta_s + (size_t)i * tau * d, tau);
   for (int i = 0; i < 2 * K; i++) R.absorb(proof->eta_s + (size_t)i * t * d, t);
   // get_rhos (folding/utils.rs:116-127): 2K - 1 short challenges and ONE, then CRT
@@ -523,6 +553,7 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
   if (lf_transcript_get_short_challenges(R.T, d, 2 * K - 1, rc.data()) != LF_OK)
     return bad(P, LF_ERR_CHALLENGE_BYTES, "short challenges");
   rc[(size_t)(2 * K - 1) * d] = 1;
+  R.mark(LF_SPAN_FOLDING_TRANSCRIPT);
   R.h2d(P->rhoc, rc.data(), rc.size());
   R.d2d(P->rho, P->rhoc, rc.size());
   R.check(lf_dev_crt(C, P->rho, 2 * K, d), "CRT(rho)");
@@ -544,6 +575,7 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
   R.d2h(x0.data(), P->x0, (l + 1) * d);
   R.check(lf_ctx_sync(C), "sync");
   if (R.rc) return R.rc;
+  R.mark(LF_SPAN_FOLD);
   memcpy(out->r, r0.data(), r0.size() * 8);
   if (l) memcpy(out->x_w, x0.data(), l * d * 8);
   memcpy(out->h, x0.data() + l * d, d * 8);
