@@ -34,8 +34,11 @@
  *   zkvm/src/commitments.rs:192-340 vm_mem_comm, vm_mem_comm_with_opening, vm_code_comm
  *                                                              -> lf_vm_mem_comm, lf_dev_merkle_tree,
  *                                                                 lf_merkle_open, lf_vm_code_comm
- *   latticefold/src/nifs.rs:28-34 LFProof (ark CanonicalSerialize) -> lf_lfproof_serialize,
- *       zkvm/src/main.rs:231-234 (serialized_size)                lf_lcccs_(de)serialize
+ *   latticefold/src/nifs.rs:28-34 LFProof (ark CanonicalSerialize) -> lf_lfproof_serialize
+ *       zkvm/src/main.rs:231-234 (serialized_size); the LCCCS layout (lf_lcccs_(de)serialize)
+ *       is this project's own (the reference serialises no LCCCS)
+ *   zkvm/src/zk_latticefold.rs:37-102 zk_latticefold_prove (fold())  -> lf_fold_prove
+ *   zkvm/src/main.rs:305-344 initialize_accumulator's linearization  -> lf_linearize
  *   zkvm/src/main.rs:121-219  the proving loop, sharded over GPUs (SURVEY.md 8(b)
  *       lf_fold_reduce_allranks; no reference analogue: rayon only)
  *                                                              -> lf_comm_*, lf_dev_fold_step_sharded,
@@ -317,6 +320,10 @@ int lf_dev_fold_lcccs(lf_ctx *ctx, int d, int nwit, const uint64_t *rho, const u
 int lf_dev_compute_x_s(lf_ctx *ctx, const lf_params *pr, const uint64_t *x, size_t m, uint64_t *x_s);
 
 int lf_dev_poseidon2_permute(lf_ctx *ctx, uint64_t *states, size_t n);
+/* the permutation stopped after its initial MDS and `rounds` (<= 30) rounds: the
+ * 4 + 22 + 4 of poseidon2.rs:100-173 in order (debug entry: the reference's only
+ * round vector, sages/inverse_mds.sage, pins the initial MDS and round 0) */
+int lf_dev_poseidon2_permute_rounds(lf_ctx *ctx, uint64_t *states, size_t n, int rounds);
 /* synthetic inputs: element i = SplitMix64(seed, i) re-mixed until < p */
 int lf_dev_fill_uniform(lf_ctx *ctx, uint64_t *out, size_t n, uint64_t seed);
 /* out[c] = sum_r in[r][c] mod p  (reduce of all-gathered accumulators) */
@@ -424,10 +431,12 @@ void lf_hash_w8(const uint64_t *in, size_t n, uint64_t out4[4]);
 int lf_vm_mem_comm(const uint32_t *words, size_t nwords, uint64_t out4[4]);
 
 /* ------------------------------------------------------------ wire format
- * ark-serialize 0.5 CanonicalSerialize as derived on the reference's types
- * (compressed = uncompressed here): Fq = 8 bytes LE canonical; an NTT ring
- * element = its d slot words, no length; Vec<T> = u64 LE length + items;
- * structs = fields in declaration order. repr describes the caller's words.
+ * LFProof: ark-serialize 0.5 CanonicalSerialize as derived on the reference's
+ * types (nifs.rs:28-34; compressed = uncompressed here): Fq = 8 bytes LE
+ * canonical; an NTT ring element = its d slot words, no length; Vec<T> = u64 LE
+ * length + items; structs = fields in declaration order. LCCCS: the reference
+ * derives no CanonicalSerialize for it (arith.rs:193-194), so its layout is this
+ * project's own, written by the same rules. repr describes the caller's words.
  * out == NULL (or too small: LF_ERR_INCORRECT_LENGTH) still returns the size. */
 typedef struct {
   const uint64_t *elems; /* n ring elements (d words each) */

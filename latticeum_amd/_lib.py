@@ -117,6 +117,7 @@ SIGNATURES = {
     "lf_dev_fold": (I, [VP, I, VP, C.POINTER(VP), I, SZ, VP]),
     "lf_dev_fold_step": (I, [VP, VP, C.POINTER(LfParams), SZ, C.POINTER(LfFoldStepBufs)]),
     "lf_dev_poseidon2_permute": (I, [VP, VP, SZ]),
+    "lf_dev_poseidon2_permute_rounds": (I, [VP, VP, SZ, I]),
     "lf_dev_fill_uniform": (I, [VP, VP, SZ, U64]),
     "lf_dev_modp_sum": (I, [VP, VP, I, SZ, VP]),
     "lf_dev_limb_split": (I, [VP, VP, SZ, VP, VP]),

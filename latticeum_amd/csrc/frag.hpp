@@ -99,16 +99,20 @@ __device__ __forceinline__ void out_store(T *p, T v) {
 }
 // outputs above this many bytes per launch are written with streaming stores
 constexpr size_t STREAM_OUT_BYTES = (size_t)4 << 30;
-// The fused decompositions stream their outputs at every size: with the fold
-// in coefficient form nothing in the step re-reads f_coeff_k or f_k, and the
-// contraction's single pass over the operand rows is faster from HBM than
-// after the rows went through the caches (W = 464, 4 streams: contraction
-// 0.27 -> 0.235 ms, 1,288-1,318 -> 1,345-1,347 steps/s; the Phi72 kernel the
-// same, kernels.hip). LATTICEUM_AMD_DEC_NT=0 keeps cached stores below 4 GiB.
-inline bool dec_streaming(size_t out_bytes) {
+// Streaming (nontemporal) stores for the fused decompositions' outputs. When
+// nothing later in the step re-reads f_coeff_k or f_k (d = 1024: the fold runs
+// in coefficient form from the packed digits), they stream at every size: the
+// contraction's single pass over the operand rows is faster from HBM than after
+// the rows went through the caches (W = 464, 4 streams: contraction 0.27 ->
+// 0.235 ms, 1,288-1,318 -> 1,345-1,347 steps/s). When the step folds f_0 from
+// f_k in NTT form (`refold`: d = 4096), cached stores are kept below 4 GiB of
+// outputs so the fold finds f_k in the caches. LATTICEUM_AMD_DEC_NT=0 never
+// streams, =1 always streams.
+inline bool dec_streaming(size_t out_bytes, bool refold) {
   const char *e = getenv("LATTICEUM_AMD_DEC_NT");
-  if (e && e[0] == '0') return out_bytes > STREAM_OUT_BYTES;
-  return true;
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  return !refold || out_bytes > STREAM_OUT_BYTES;
 }
 
 // vector-major operand layout (uint4 index of digit 0; digit k adds 4k, chunk c adds c FV_CHUNK)

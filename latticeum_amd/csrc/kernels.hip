@@ -1254,7 +1254,9 @@ __device__ __forceinline__ void mds16(uint64_t *s) {  // poseidon2.rs:243-268
     for (int j = k; j < 16; j += 4) s[j] = gl::add(s[j], sum);
   }
 }
-__global__ void __launch_bounds__(256) k_p2_permute(uint64_t *states, size_t n) {
+// rounds < 30 stops after the initial MDS and that many rounds (a debug entry
+// that lets the reference's round-0 vector, sages/inverse_mds.sage, pin the device)
+__global__ void __launch_bounds__(256) k_p2_permute(uint64_t *states, size_t n, int rounds) {
   size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (e >= n) return;
   uint64_t s[16];
@@ -1266,14 +1268,16 @@ __global__ void __launch_bounds__(256) k_p2_permute(uint64_t *states, size_t n) 
     s[2 * i + 1] = gl::canon(v.y);
   }
   mds16(s);
+  const int ri = rounds < 4 ? rounds : 4, rp = rounds - 4 < 0 ? 0 : rounds - 4 > 22 ? 22 : rounds - 4;
+  const int rt = rounds - 26 < 0 ? 0 : rounds - 26 > 4 ? 4 : rounds - 26;
 #pragma unroll 1
-  for (int r = 0; r < 4; r++) {
+  for (int r = 0; r < ri; r++) {
 #pragma unroll
     for (int i = 0; i < 16; i++) s[i] = sbox7(gl::add(s[i], P2_EXT_INIT[16 * r + i]));
     mds16(s);
   }
 #pragma unroll 1
-  for (int r = 0; r < 22; r++) {
+  for (int r = 0; r < rp; r++) {
     s[0] = sbox7(gl::add(s[0], P2_INTERNAL[r]));
     uint64_t sum = 0;
 #pragma unroll
@@ -1282,7 +1286,7 @@ __global__ void __launch_bounds__(256) k_p2_permute(uint64_t *states, size_t n) 
     for (int i = 0; i < 16; i++) s[i] = gl::add(gl::mul(s[i], P2_DIAG_M1[i]), sum);
   }
 #pragma unroll 1
-  for (int r = 0; r < 4; r++) {
+  for (int r = 0; r < rt; r++) {
 #pragma unroll
     for (int i = 0; i < 16; i++) s[i] = sbox7(gl::add(s[i], P2_EXT_TERM[16 * r + i]));
     mds16(s);
@@ -1670,9 +1674,10 @@ hipError_t fold(const uint64_t *rho, const VecPtrs &x, int nwit, size_t n, int d
   return hipGetLastError();
 }
 
-hipError_t p2_permute(uint64_t *states, size_t n, hipStream_t st) {
+hipError_t p2_permute(uint64_t *states, size_t n, hipStream_t st, int rounds) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_p2_permute, dim3(blocks(n, 256)), dim3(256), 0, st, states, n);
+  if (rounds < 0 || rounds > 30) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_p2_permute, dim3(blocks(n, 256)), dim3(256), 0, st, states, n, rounds);
   return hipGetLastError();
 }
 

@@ -46,7 +46,7 @@ hipError_t commit_y0(const uint64_t *cm, uint64_t *y, size_t kappa, int d, int l
                      hipStream_t st);
 hipError_t fold(const uint64_t *rho, const VecPtrs &x, int nwit, size_t n, int d, uint64_t *out,
                 hipStream_t st, const int *run_if = nullptr);
-hipError_t p2_permute(uint64_t *states, size_t n, hipStream_t st);
+hipError_t p2_permute(uint64_t *states, size_t n, hipStream_t st, int rounds = 30);
 hipError_t fill_uniform(uint64_t *out, size_t n, uint64_t seed, hipStream_t st);
 hipError_t modp_sum(const uint64_t *in, int nparts, size_t len, uint64_t *out, hipStream_t st);
 

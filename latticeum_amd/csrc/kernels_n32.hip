@@ -595,7 +595,7 @@ hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K,
   const unsigned grid = (unsigned)((ntask + per - 1) / per);
   // outputs: f_coeff_k, f_k, frag (each K N D words per side) and w_ccs_k
   const size_t out_bytes = sd.nside * (size_t)K * N * D * 8 * 3;
-  if (dec_streaming(out_bytes))
+  if (dec_streaming(out_bytes, false))
     hipLaunchKernelGGL(k_decompose_fused<true>, dim3(grid), dim3(512), 0, st, smg, N, L, lb, K, sd, fwd.mid, frag,
                        nch, sink);
   else

@@ -527,7 +527,7 @@ hipError_t decompose_n4k(const FusedSides &sd, size_t N, int lb, int L, int K, u
     // 32 blocks per group of 8 units (8 XCDs x 4 quarters), one block per CU
     const unsigned grid = (unsigned)(ncu / 32 * 32);
     // outputs: f_coeff_k, f_k, the operand rows (each K N d words per side) and w_ccs_k
-    if (dec_streaming(sd.nside * (size_t)K * N * D4 * 8 * 3))
+    if (dec_streaming(sd.nside * (size_t)K * N * D4 * 8 * 3, true))
       hipLaunchKernelGGL(k_decompose_n4k_fused<true>, dim3(grid), dim3(512), 0, st, sm8, N, L, lb, K, sd, fwd.mid,
                          fwd.tw4, fwd.ztab, frag, nch, sink);
     else

@@ -1966,6 +1966,13 @@ int lf_dev_poseidon2_permute(lf_ctx *c, uint64_t *states, size_t n) {
   LF_HIP(c, lfk::p2_permute(states, n, c->cur));
   return LF_OK;
 }
+
+int lf_dev_poseidon2_permute_rounds(lf_ctx *c, uint64_t *states, size_t n, int rounds) {
+  if (!c || (!states && n) || rounds < 0 || rounds > 30) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  LF_HIP(c, lfk::p2_permute(states, n, c->cur, rounds));
+  return LF_OK;
+}
 int lf_dev_fill_uniform(lf_ctx *c, uint64_t *out, size_t n, uint64_t seed) {
   DevGuard g(c);
   if (!c) return LF_ERR_INVALID_ARG;

@@ -323,6 +323,16 @@ def test_dev_fold_step_without_fk(ctx, W):
     check_dev_fold_step(ctx, 1024, W, 2, steps=2, keep_fk=False)
 
 
+@pytest.mark.parametrize("mode", ["default", "0", "1"])
+@pytest.mark.parametrize("d,W", [(1024, 37), (4096, 17)])
+def test_dev_fold_step_store_modes(ctx, monkeypatch, d, W, mode):
+    """the fused d = 1024 / 4096 decompositions with cached (LATTICEUM_AMD_DEC_NT=0),
+    streaming (=1) and the default stores (frag.hpp dec_streaming) give the oracle's step"""
+    if mode != "default":
+        monkeypatch.setenv("LATTICEUM_AMD_DEC_NT", mode)
+    check_dev_fold_step(ctx, d, W, 2)
+
+
 def test_dev_fold_step_without_fk_unfused_is_an_error(ctx):
     with pytest.raises(LA.LfError):
         check_dev_fold_step(ctx, 24, 10, 3, keep_fk=False)
@@ -495,10 +505,41 @@ def test_poseidon2_batch(ctx):
     assert np.array_equal(ctx.poseidon2_permute(st), O.p2_permute(st))
 
 
-def test_poseidon2_round0_kat_via_gpu_consts(ctx):
-    # the device constant table starts with the reference's round-0 row
+def test_poseidon2_round0_kat_on_device(ctx):
+    """the device permutation stopped after round 0 reproduces the reference's
+    round vector (sages/inverse_mds.sage, external_initial_rounds.sage: initial MDS,
+    round-0 constants, s-box, MDS); one round further differs; 30 rounds is the full
+    permutation of k_p2_permute"""
+    import torch
     k = KATS["poseidon2"]["P3_round0"]
-    assert k["round0_consts"][0] == 6829280927315210738
+    x = np.array([int(v) for v in k["input"]], np.uint64)
+    st = torch.from_numpy(np.tile(x, 3).view(np.int64).copy()).cuda()
+    ctx.check(ctx.lib.lf_dev_poseidon2_permute_rounds(ctx.h, st.data_ptr(), 3, 1))
+    ctx.sync()
+    assert [int(v) for v in st.cpu().numpy().view(np.uint64)[:16]] == k["mds_sbox_mds"]
+    st2 = torch.from_numpy(x.view(np.int64).copy()).cuda()
+    ctx.check(ctx.lib.lf_dev_poseidon2_permute_rounds(ctx.h, st2.data_ptr(), 1, 2))
+    ctx.sync()
+    assert [int(v) for v in st2.cpu().numpy().view(np.uint64)] != k["mds_sbox_mds"]
+    st3 = torch.from_numpy(x.view(np.int64).copy()).cuda()
+    ctx.check(ctx.lib.lf_dev_poseidon2_permute_rounds(ctx.h, st3.data_ptr(), 1, 30))
+    ctx.sync()
+    assert np.array_equal(st3.cpu().numpy().view(np.uint64), O.p2_permute(x))
+
+
+def test_poseidon2_configs4_batch_sampled(ctx):
+    """configs[4]'s batch: 2^20 independent width-16 states, sampled states against the oracle"""
+    import torch
+    m = 1 << 20
+    st = torch.empty(16 * m, dtype=torch.int64, device="cuda")
+    ctx.dev_fill_uniform(st, 0x4C460007)
+    x = st.clone()
+    ctx.dev_poseidon2_permute(st)
+    ctx.sync()
+    picks = [0, 1, 4095, 65536, 524287, m - 1]
+    xs = x.view(m, 16)[picks].cpu().numpy().view(np.uint64).ravel()
+    got = st.view(m, 16)[picks].cpu().numpy().view(np.uint64).ravel()
+    assert np.array_equal(got, O.p2_permute(xs))
 
 
 def test_fill_uniform_and_modp_sum(ctx):
