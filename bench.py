@@ -510,18 +510,20 @@ def sharded_fold(LA, torch, LD, pg, local, rank, world, d, W, kappa, steps, warm
     comm = LD.make_comm(wl.ctxs[0], pg, world, rank)
     try:
         dt, (phases, roof) = measure(LA, torch, LD, pg, world, wl, steps, warmup, comm)
-        # the accumulator exchange of independent step streams, for reference
-        keep = wl.keeps[0]
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        LD.AccumulatorReducer(comm, [keep["cm0"], keep["f0"]]).reduce()
-        torch.cuda.synchronize()
-        t_red = LD.max_over_ranks(pg, time.perf_counter() - t0)
     finally:
         if comm is not None:
             comm.close()
         wl.close()
         del wl
+        torch.cuda.empty_cache()
+    # bit-exact self-check of the same path over the same communicator kind: each
+    # rank's shard of a world x 64-group fold against the unsharded fold on its GPU
+    ctx = LA.Context(local)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        verified = LD.verify_sharded_step(LA, ctx, pg, local, rank, world, d=d, kappa=kappa)
+    finally:
+        ctx.close()
         torch.cuda.empty_cache()
     kd = 29 * kappa * d * 8
     return {"workload": f"one commit+fold step of a w_ccs of W={world}x{W} ring elements, column-sharded "
@@ -530,9 +532,10 @@ def sharded_fold(LA, torch, LD, pg, local, rank, world, d, W, kappa, steps, warm
             "value": steps / dt, "unit": "sharded fold-steps/s", "shard_steps_per_s": world * steps / dt,
             "n_gpus": world, "steps": steps, "ms_per_step": dt / steps * 1e3, "scaling": "weak",
             "roofline": roof, "phases": phases,
-            "accumulator_reduce_ms": t_red * 1e3,
-            "accumulator_reduce": f"cm_0 + f_0 ({(kappa + W * 5) * d * 8 / 1e6:.0f} MB) summed over ranks mod p "
-                                  f"(lf_fold_reduce_allranks), timed once outside the steps"}
+            "verified": verified,
+            "verification": f"after timing, every rank's shard of a {world} x 64-group fold through the same RCCL "
+                            f"exchange equals the unsharded fold on its GPU, every output bit for bit "
+                            f"(latticeum_amd.dist.verify_sharded_step)"}
 
 
 def side_ops(LA, torch, local):
@@ -836,6 +839,8 @@ def main():
         ops = side_ops(LA, torch, local)
         nxt = next_rows(LA, torch, local, out.get("cpu_baseline") if out is not None else None)
         if out is not None:
+            if args.cpu and world == 1:  # the reference ring's own CPU baseline (the oracle restatement)
+                ref["cpu_baseline"] = cpu_baseline(24, 19763, 32)
             out["next_rows"] = nxt
             out["reference_ring"] = ref
             out["small_shape"] = small
