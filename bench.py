@@ -57,6 +57,9 @@ def parse():
                          "reported beside the default workload")
     ap.add_argument("--cu-partition", action="store_true", default=False,
                     help="give each step stream its own contiguous block of CUs (lf_stream_create_cu_mask)")
+    ap.add_argument("--packed", type=int, default=None,
+                    help="1: keep the decomposed witnesses as packed digit planes (no u64 f_k / f_coeff_k rows); "
+                         "0: write the rows; default: the ring's default (Workload)")
     ap.add_argument("--cpu-baseline", dest="cpu", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu", action="store_false")
     return ap.parse_args()
@@ -100,7 +103,8 @@ I8_DENSE_TOPS = 5000.0  # MI355X dense i8 MFMA peak (2x the dense bf16 2.5 PFLOP
 
 def coeff_fold(d, layout, keep_fk):
     """whether lf_dev_fold_step folds f_0 in coefficient form on the i8 matrix
-    cores (fold_coeff.hip): X^1024+1 after the fused decomposition, f_k kept"""
+    cores (fold_coeff.hip): X^1024+1 after the fused decomposition, f_k kept or
+    the planes packed (not the operand-rows-only mode)"""
     return d == 1024 and layout == 1 and keep_fk and os.environ.get("LATTICEUM_AMD_FOLD") != "slot"
 
 
@@ -272,10 +276,12 @@ class Workload:
         # keep_fk=False (fused X^1024+1 path only): the decomposed planes live only
         # as MFMA operand rows (lf.h: f_k buffers omitted) -- 20 GB less HBM at
         # W = 2^14, but slower, so the bench keeps f_k.
-        # packed (default for d = 24): the decomposed witnesses are kept as packed
-        # digit planes (lf_fold_step_bufs.planes, 8 B per element and plane) instead
-        # of u64 f_k / f_coeff_k rows (2 x 192 B); lf_dev_expand_planes makes the rows
-        self.packed = packed = (d == 24) if packed is None else packed
+        # packed (default for d = 24 and 1024): the decomposed witnesses are kept as
+        # packed digit planes (lf_fold_step_bufs.planes: 8 B per element and plane at
+        # d = 24, 2 B per coefficient for all planes at d = 1024) instead of u64 f_k /
+        # f_coeff_k rows (2 x 8 d B per element and plane); lf_dev_expand_planes
+        # makes the rows. d = 1024, W = 2^14: decomposition 14.0 -> 12.4 ms, 41.5 -> 44.0 steps/s
+        self.packed = packed = (d in (24, 1024)) if packed is None else packed
         self.keep_fk = keep_fk and not packed
         self.LA, self.torch = LA, torch
         self.d, self.W, self.kappa = d, W, kappa
@@ -324,7 +330,7 @@ class Workload:
                 "fk": [z(K * N * d) for _ in range(2)] if self.keep_fk else [None, None],
                 "wk": [z(K * W * d) for _ in range(2)], "y": [z(K * kappa * d) for _ in range(2)],
                 "f0": z(N * d), "f0_coeff": z(N * d), "w_ccs0": z(W * d), "cm0": z(kappa * d),
-                "planes": [z(K * N) for _ in range(2)] if packed else [None, None],
+                "planes": [z(K * N if d == 24 else N * 256) for _ in range(2)] if packed else [None, None],
             }
             bufs = LA.LfFoldStepBufs()
             for k, v in keep.items():
@@ -420,7 +426,8 @@ def phase_report(LA, wl, tot, steps):
     _, alg, operand = algorithmic_bytes(d, W, kappa, wl.pr.L, wl.pr.K)
     if not wl.keep_fk and not wl.packed:  # the planes are written once, as the operand rows: no bytes beyond B2
         operand["decompose"] = 0
-    kernel_of = kernel_names(LA, d, W, wl.sch.layout, wl.keep_fk)
+    # packed planes fold in coefficient form as with f_k (the operand rows are only the fallback's)
+    kernel_of = kernel_names(LA, d, W, wl.sch.layout, wl.keep_fk or wl.packed)
     traffic = load_traffic(d, W, kappa)
     valu = load_sq(d, W, kappa)
     phases = {}
@@ -437,10 +444,12 @@ def phase_report(LA, wl, tot, steps):
             a = wl.N * (2 * 2048 + 2 * 2 * wl.pr.K * 256 + 8 * 1024)  # packed digits in, keys out + in, f0_coeff out
         if ph == "decompose" and wl.packed:
             # B2 counts the u64 f_k / f_coeff_k rows the reference materialises; this
-            # launch writes them as packed planes (8 B per element and plane) instead
+            # launch keeps them as packed planes instead (d = 24: 8 B per element and
+            # plane written; d = 1024: the 2 B-per-coefficient words it reads anyway)
+            planes_b = wl.pr.K * wl.N * 8 if d == 24 else wl.N * 2 * d
             phases_note = {"packed_planes": True,
-                           "moved_bytes_per_launch": sides * (wl.N * 8 * d + wl.pr.K * wl.N * 8
-                                                                + wl.pr.K * W * 8 * d) + operand.get(ph, 0) * sides}
+                           "moved_bytes_per_launch": sides * (wl.N * 8 * d + planes_b + wl.pr.K * W * 8 * d)
+                           + operand.get(ph, 0) * sides}
         else:
             phases_note = {}
         if cf24:  # digit masks in (8 B per element and plane); f0_coeff, f0 (E each) and w_ccs0 out (from_f's outputs)
@@ -797,7 +806,8 @@ def main():
     pg = LD.init(world)
 
     d, W, kappa = args.d, args.w, args.kappa
-    wl = Workload(LA, torch, local, rank, d, W, kappa, args.streams, cu_partition=args.cu_partition)
+    wl = Workload(LA, torch, local, rank, d, W, kappa, args.streams, cu_partition=args.cu_partition,
+                  packed=None if args.packed is None else bool(args.packed))
     K, L, N = wl.pr.K, wl.pr.L, wl.N
     dt_max, (phases, roof) = measure(LA, torch, LD, pg, world, wl, args.steps, args.warmup)
     wl.close()

@@ -256,18 +256,20 @@ typedef struct {
   uint64_t *f0, *f0_coeff;     /* N each: folded witness */
   uint64_t *w_ccs0;            /* W */
   uint64_t *cm0;               /* kappa */
-  /* d = 24 with b_small = 2 (optional, both sides or neither): the decomposed
-   * witnesses as packed digit planes [K][N], one u64 per element and plane:
-   * bit i = coefficient i is nonzero, bit 32 + i = it is -1. With fk and
-   * fk_coeff all NULL they are the planes' only form (the u64 rows, 2 x 192 B
-   * per element and plane, are not written; lf_dev_expand_planes makes them). */
+  /* b_small = 2 (optional, both sides or neither): the decomposed witnesses as
+   * packed digit planes. d = 24: [K][N] u64, one per element and plane (bit i =
+   * coefficient i is nonzero, bit 32 + i = it is -1). d = 1024 (the fused path):
+   * N x 2 KiB, every coefficient's 16-bit sign|magnitude word, all K planes in
+   * one (the decomposition's own packed input). With fk and fk_coeff all NULL
+   * the planes are the decomposed witnesses' only form: the u64 rows (2 x 8 d B
+   * per element and plane) are not written; lf_dev_expand_planes makes them. */
   uint64_t *planes[2];
 } lf_fold_step_bufs;
-/* packed Phi_72 digit planes (lf_fold_step_bufs.planes; n elements) -> the
- * Witness forms of decompose_witness's outputs (decomposition.rs:162-167,
- * arith.rs:324-338): f_coeff (digits mod p) and / or f = CRT(f_coeff); either
- * output may be NULL */
-int lf_dev_expand_planes(lf_ctx *ctx, int d, const uint64_t *planes, size_t n, uint64_t *f_coeff, uint64_t *f);
+/* packed digit planes (lf_fold_step_bufs.planes) of N elements -> the Witness forms of
+ * decompose_witness's outputs (decomposition.rs:162-167, arith.rs:324-338):
+ * f_coeff_k [K][N] (digits mod p) and / or f_k [K][N] = CRT(f_coeff_k); either may be NULL */
+int lf_dev_expand_planes(lf_ctx *ctx, const lf_params *pr, const uint64_t *planes, size_t N, uint64_t *f_coeff_k,
+                         uint64_t *f_k);
 /* commit(z) followed by the commit+fold arithmetic of fold(), all on device */
 int lf_dev_fold_step(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, size_t W,
                      const lf_fold_step_bufs *b);

@@ -285,11 +285,12 @@ class Context:
     def dev_eq_table(self, d: int, r, nv: int, out):
         self.check(self.lib.lf_dev_eq_table(self.h, d, _dptr(r), nv, _dptr(out)))
 
-    def dev_expand_planes(self, d, planes, n, f_coeff=None, f=None):
-        """packed Phi_72 digit planes (lf_fold_step_bufs.planes) -> f_coeff and / or f = CRT(f_coeff)"""
-        self.check(self.lib.lf_dev_expand_planes(self.h, d, _dptr(planes), n,
-                                                 _dptr(f_coeff) if f_coeff is not None else None,
-                                                 _dptr(f) if f is not None else None))
+    def dev_expand_planes(self, params: LfParams, planes, N: int, f_coeff_k=None, f_k=None):
+        """packed digit planes of N elements (lf_fold_step_bufs.planes) -> f_coeff_k and / or
+        f_k = CRT(f_coeff_k), [K][N] each"""
+        self.check(self.lib.lf_dev_expand_planes(self.h, C.byref(params), _dptr(planes), N,
+                                                 _dptr(f_coeff_k) if f_coeff_k is not None else None,
+                                                 _dptr(f_k) if f_k is not None else None))
 
     def dev_get_fhat(self, d, f_coeff, N, nv, out):
         """Witness::get_fhat on the device: out [tau][2^nv][d] from f_coeff [N][d]"""

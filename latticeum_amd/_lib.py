@@ -145,7 +145,7 @@ SIGNATURES = {
     "lf_lfproof_serialize": (I, [C.POINTER(LfLfproof), I, VP, SZ, C.POINTER(SZ)]),
     "lf_dev_eq_table": (I, [VP, I, VP, I, VP]),
     "lf_dev_get_fhat": (I, [VP, I, VP, SZ, I, VP]),
-    "lf_dev_expand_planes": (I, [VP, I, VP, SZ, VP, VP]),
+    "lf_dev_expand_planes": (I, [VP, C.POINTER(LfParams), VP, SZ, VP, VP]),
     "lf_ccs_create": (I, [VP, I, I, SZ, SZ, VP, VP, VP, I, C.POINTER(VP)]),
     "lf_ccs_destroy": (None, [VP]),
     "lf_ccs_set_structure": (I, [VP, VP, SZ, I, I, VP, VP, VP, I]),

@@ -594,7 +594,9 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_fv(const uint4 *Af, VecPt
 // multiply-accumulates rho_v (.) f_v lazily; the 8 vector groups meet in LDS
 // and each output column's 16 slots go out as one 128-B run.
 __global__ void __launch_bounds__(256) k_fold_frag(const uint4 *frag, int nch, int Lp, size_t Wp, FoldRows fr,
-                                                  const uint64_t *rho, int d, size_t N, uint64_t *out) {
+                                                  const uint64_t *rho, int d, size_t N, uint64_t *out,
+                                                  const int *run_if) {
+  if (run_if && !*run_if) return;  // uniform: the coefficient-form fold produced f_0
   __shared__ uint64_t red[512 * 9];  // [output (column, slot)][vector group], rows padded to 9
   const int tid = threadIdx.x, vg = tid & 7, h = (tid >> 3) & 1, sl = (tid >> 4) & 3, qq = tid >> 6;
   const int ng = d >> 4, G = blockIdx.x % ng, c = blockIdx.x / ng;
@@ -630,11 +632,12 @@ __global__ void __launch_bounds__(256) k_fold_frag(const uint4 *frag, int nch, i
 }
 
 hipError_t fold_frag(const uint4 *frag, const FragGeom &g, const FoldRows &fr, const uint64_t *rho, int d, size_t N,
-                     uint64_t *out, hipStream_t st) {
+                     uint64_t *out, hipStream_t st, const int *run_if) {
   if (d == 24 || d % 16 || g.qperm || fr.n < 1 || fr.n > LF_MAX_VECS) return hipErrorInvalidValue;
   if (!N) return hipSuccess;
   const size_t nb = (size_t)(d / 16) * g.nch;
-  hipLaunchKernelGGL(k_fold_frag, dim3((unsigned)nb), dim3(256), 0, st, frag, g.nch, g.Lp, g.Wp, fr, rho, d, N, out);
+  hipLaunchKernelGGL(k_fold_frag, dim3((unsigned)nb), dim3(256), 0, st, frag, g.nch, g.Lp, g.Wp, fr, rho, d, N, out,
+                     run_if);
   return hipGetLastError();
 }
 

@@ -127,7 +127,7 @@ struct FoldRows {
   int n;
 };
 hipError_t fold_frag(const uint4 *frag, const FragGeom &g, const FoldRows &fr, const uint64_t *rho, int d, size_t N,
-                     uint64_t *out, hipStream_t st);
+                     uint64_t *out, hipStream_t st, const int *run_if = nullptr);
 // sink: an 8 KiB device scratch row (stores of groups past W); ncu: the device's CU count
 hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K, uint32_t *smg,
                            const ring::NegaTables &fwd, uint4 *frag, int nch, int *err, uint64_t *sink, int ncu,
@@ -167,6 +167,8 @@ hipError_t fold_phi72_masks(const uint2 *masks0, const uint2 *masks1, const uint
                             uint64_t *f0, const int *run_if, hipStream_t st);
 // packed Phi_72 planes (n elements) -> f_coeff (digits mod p) and / or f = CRT(f_coeff)
 hipError_t expand_phi72(const uint2 *planes, size_t n, uint64_t *fc, uint64_t *f, hipStream_t st);
+// d = 1024: the fused decomposition's packed sign|magnitude words of N elements -> f_coeff_k [K][N]
+hipError_t expand_sm(const uint32_t *smg, size_t N, int K, uint64_t *fck, hipStream_t st);
 // d = 4096, b_small = 2 (kernels_n4k.hip): sm4 holds nside N 1024 packed words; sink 4096 words.
 // With frag (a scheme whose geometry has Lp = L and qperm), planes k >= 1 are also
 // written as operand rows row0[side] + k - 1, as decompose_fused does for d = 1024.

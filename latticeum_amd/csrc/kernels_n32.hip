@@ -525,7 +525,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_
 #pragma unroll
           for (int q = 0; q < 16; q++) wn[q] = smg[((gg * L + ln) * 16 + q) * 32 + r];
         }
-        {  // groups past W store into `sink` (no branch around the stores: see above)
+        if (f_coeff_k) {  // uniform; groups past W store into `sink` (no branch around the stores: see above)
           uint64_t *oc = (ok ? f_coeff_k + e * D : sink) + r;
 #pragma unroll
           for (int k = 0; k < 32; k++) out_store<NT>(&oc[32 * k], from_signed(dg[k]));
@@ -578,6 +578,29 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_
       }
     }
   }
+}
+
+// the packed sign|magnitude words (k_pack_sm's layout) -> the K digit planes in
+// coefficient form: f_coeff_k[k][col][j] = sign(x_j) bit_k(|x_j|), one thread per output
+__global__ void k_expand_sm(const uint32_t *smg, size_t N, int K, uint64_t *fck) {
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < (size_t)K * N * D;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int j = (int)(t % D), k = (int)(t / ((size_t)N * D));
+    const size_t col = (t / D) % N;
+    const int r = j & 31, jt = j >> 5, q = jt >> 1, h = jt & 1;
+    const uint32_t hw = (smg[(col * 16 + q) * 32 + r] >> (16 * h)) & 0xFFFFu;
+    const int64_t bit = (hw >> k) & 1;
+    fck[t] = from_signed((hw & 0x8000u) ? -bit : bit);
+  }
+}
+
+hipError_t expand_sm(const uint32_t *smg, size_t N, int K, uint64_t *fck, hipStream_t st) {
+  if (!N) return hipSuccess;
+  if (K < 1 || K > 15) return hipErrorInvalidValue;
+  const size_t n = (size_t)K * N * D;
+  const size_t nb = (n + 255) / 256;
+  hipLaunchKernelGGL(k_expand_sm, dim3((unsigned)(nb < 65536 ? nb : 65536)), dim3(256), 0, st, smg, N, K, fck);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- launchers

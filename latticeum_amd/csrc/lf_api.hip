@@ -68,6 +68,7 @@ struct lf_ctx {
   size_t sc_elems = 0;
   lfk::FoldRows fold_rows{};    // a step without f_k buffers: where its 2K planes sit in the operand rows
   bool fold_from_frag = false;
+  bool frag_fallback = false;   // packed d = 1024 planes: fold_rows serve the not-short-rho fallback
   bool timing = false;
   std::vector<TimedLaunch> pending;
   std::map<int, std::pair<double, long>> stats;  // nvec -> (ms, count)
@@ -471,10 +472,15 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
   const bool no_fk = !b->fk[0] && !b->fk[1];
   c->fold_from_frag = false;
   c->masks24_n = 0;
+  c->frag_fallback = false;
   if (b->planes[0] || b->planes[1]) {
-    if (!fused24 || lbs != 1 || !b->planes[0] || !b->planes[1])
-      return fail(c, LF_ERR_INVALID_ARG, "packed planes: d = 24 with b_small = 2, both sides");
+    if (!(fused24 || (fused && !fv)) || lbs != 1 || !b->planes[0] || !b->planes[1])
+      return fail(c, LF_ERR_INVALID_ARG, "packed planes: d = 24 or the fused d = 1024 path, b_small = 2, both sides");
   }
+  // X^1024 + 1 without f_k / f_coeff_k: the planes stay packed (the fused
+  // decomposition's sign|magnitude words), f_0 comes from the coefficient-form
+  // fold, whose fallback for a rho that is not short reads the operand rows
+  const bool packed1024 = no_fk && fused && !fv && !b->fk_coeff[0] && !b->fk_coeff[1];
   // Phi_72 without f_k / f_coeff_k: the decomposed witnesses stay packed (digit masks)
   const bool packed24 = no_fk && fused24;
   if (packed24) {
@@ -483,6 +489,8 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       return fail(c, LF_ERR_INVALID_ARG, "Phi_72: f_k and f_coeff_k are both given or both NULL");
   } else if (no_fk) {
     if (!fused || fv) return fail(c, LF_ERR_INVALID_ARG, "f_k buffers may be omitted only on the fused X^1024+1 path");
+    if (!packed1024 && (!b->fk_coeff[0] || !b->fk_coeff[1]))
+      return fail(c, LF_ERR_INVALID_ARG, "f_coeff_k: both sides or neither");
     if (extra + 2 * (K - 1) + 2 > LF_MAX_VECS) return fail(c, LF_ERR_INVALID_ARG, "too many operand rows");
     lfk::FoldRows &fr = c->fold_rows;
     fr.n = 2 * K;
@@ -491,7 +499,10 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
         fr.row[s2 * K + k] = k > 0 ? extra + s2 * (K - 1) + k - 1 : extra + 2 * (K - 1) + s2;
         fr.rho[s2 * K + k] = s2 * K + k;
       }
-    c->fold_from_frag = true;
+    // packed planes fold in coefficient form with the rows as the fallback
+    // (LATTICEUM_AMD_FOLD=slot: from the rows)
+    c->fold_from_frag = !packed1024 || !coeff_fold_enabled();
+    c->frag_fallback = packed1024;
   } else if (!b->fk[0] || !b->fk[1]) {
     return fail(c, LF_ERR_INVALID_ARG, "f_k: both sides or neither");
   }
@@ -518,6 +529,10 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       LF_HIP(c, lfk::decompose_fused(sd, N, lb, L, K, c->smg, t->fwd, fv ? nullptr : c->frag, aj->geom.nch, c->d_err,
                                      c->sink, c->ncu, c->cur));
       c->smg_sides_n = N;  // fold_finish's coefficient-form fold reads the digits from here
+      if (b->planes[0])  // the caller keeps the packed planes: N x 512 words per side
+        for (int s = 0; s < 2; s++)
+          LF_HIP(c, hipMemcpyAsync(b->planes[s], c->smg + (size_t)s * N * 512, N * 512 * 4, hipMemcpyDeviceToDevice,
+                                   c->cur));
     } else {
       lfk::FusedSides sd{};
       sd.nside = 2;
@@ -627,10 +642,14 @@ int fold_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       const int ks_n = fs && !strcmp(fs, "0") ? 1 : lfk::fold_coeff_splits(N, K, c->ncu);
       if (ks_n > 1) LF_TRY(grow(c, c->fpart, c->fpart_elems, (size_t)ks_n * N * 1024));
       LF_HIP(c, lfk::fold_coeff(c->fkeys, tab, bad, N, K, b->f0_coeff, c->ncu, c->cur, ks_n > 1 ? c->fpart : nullptr));
-      lfk::VecPtrs fx{};
-      for (int s = 0; s < 2; s++)
-        for (int k = 0; k < K; k++) fx.p[s * K + k] = b->fk[s] + (size_t)k * N * d;
-      LF_HIP(c, lfk::fold(b->rho, fx, nw, N, d, b->f0, c->cur, bad));
+      if (c->frag_fallback) {  // packed planes: the fallback folds from the operand rows
+        LF_HIP(c, lfk::fold_frag(c->frag, aj->geom, c->fold_rows, b->rho, d, N, b->f0, c->cur, bad));
+      } else {
+        lfk::VecPtrs fx{};
+        for (int s = 0; s < 2; s++)
+          for (int k = 0; k < K; k++) fx.p[s * K + k] = b->fk[s] + (size_t)k * N * d;
+        LF_HIP(c, lfk::fold(b->rho, fx, nw, N, d, b->f0, c->cur, bad));
+      }
     }
     PhaseTimer pt(c, LF_PHASE_FROM_F);
     LF_HIP(c, lfk::from_fcoeff_n32(b->f0_coeff, W, lb, L, b->f0, b->w_ccs0, t->fwd, bad, c->cur));
@@ -1811,12 +1830,28 @@ int lf_vm_code_comm(lf_ctx *c, const uint8_t *code, size_t len, uint64_t out4[4]
   return LF_OK;
 }
 
-int lf_dev_expand_planes(lf_ctx *c, int d, const uint64_t *planes, size_t n, uint64_t *fc, uint64_t *f) {
+int lf_dev_expand_planes(lf_ctx *c, const lf_params *pr, const uint64_t *planes, size_t N, uint64_t *fck,
+                         uint64_t *fk) {
   if (!c) return LF_ERR_INVALID_ARG;
   DevGuard g(c);
-  if (d != 24) return fail(c, LF_ERR_UNSUPPORTED_RING, "packed planes: d = 24 only");
-  if (!planes && n) return fail(c, LF_ERR_INVALID_ARG, "planes is NULL");
-  LF_HIP(c, lfk::expand_phi72(reinterpret_cast<const uint2 *>(planes), n, fc, f, c->cur));
+  int lb, lbs;
+  LF_TRY(check_params(c, pr, lb, lbs));
+  const int d = pr->d, K = pr->K;
+  if (!planes && N) return fail(c, LF_ERR_INVALID_ARG, "planes is NULL");
+  if (lbs != 1) return fail(c, LF_ERR_INVALID_ARG, "packed planes need b_small = 2");
+  if (d == 24) {  // [K][N] digit masks
+    LF_HIP(c, lfk::expand_phi72(reinterpret_cast<const uint2 *>(planes), (size_t)K * N, fck, fk, c->cur));
+    return LF_OK;
+  }
+  if (d != 1024 || K > 15) return fail(c, LF_ERR_UNSUPPORTED_RING, "packed planes: d = 24 or 1024");
+  if (!fck && !fk) return LF_OK;
+  // sign|magnitude words -> f_coeff_k, then f_k = NTT(f_coeff_k) (CRT::elementwise_crt)
+  uint64_t *dst = fck ? fck : fk;
+  LF_HIP(c, lfk::expand_sm(reinterpret_cast<const uint32_t *>(planes), N, K, dst, c->cur));
+  if (fk) {
+    if (fck) LF_HIP(c, hipMemcpyAsync(fk, fck, (size_t)K * N * d * 8, hipMemcpyDeviceToDevice, c->cur));
+    LF_TRY(lf_dev_crt(c, fk, (size_t)K * N, d));
+  }
   return LF_OK;
 }
 

@@ -407,26 +407,34 @@ def test_dev_fold_step_repeated_in_place(ctx):
     check_dev_fold_step(ctx, 1024, 37, 2, steps=3)
 
 
-@pytest.mark.parametrize("W", [3, 17, 70])
+@pytest.mark.parametrize("d,W", [(24, 3), (24, 17), (24, 70), (1024, 2), (1024, 37), (1024, 130)])
 @pytest.mark.parametrize("short", [True, False])
-def test_dev_fold_step_phi72_packed_planes(ctx, W, short):
-    """Phi_72 with the decomposed witnesses kept as packed digit planes
-    (lf_fold_step_bufs.planes, no u64 f_k / f_coeff_k rows): the step's outputs
-    and the planes expanded by lf_dev_expand_planes equal the oracle's
-    decompose_witness; a rho that is not short folds from the masks in Z_p"""
-    d, K = 24, params(24).K
-    check_dev_fold_step(ctx, d, W, 3, packed=True, rho=None if short else rand(2 * K * d, 6161 + W))
+def test_dev_fold_step_packed_planes(ctx, d, W, short):
+    """the decomposed witnesses kept as packed digit planes (lf_fold_step_bufs.planes,
+    no u64 f_k / f_coeff_k rows): the step's outputs and the planes expanded by
+    lf_dev_expand_planes equal the oracle's decompose_witness; a rho that is not
+    short folds from the masks in Z_p (d = 24) or from the operand rows (d = 1024)"""
+    K = params(d).K
+    check_dev_fold_step(ctx, d, W, 3 if d == 24 else 2, packed=True, rho=None if short else rand(2 * K * d, 6161 + W))
 
 
-def test_dev_fold_step_phi72_packed_planes_slot_fold(ctx, monkeypatch):
-    """LATTICEUM_AMD_FOLD=slot with packed planes: the Z_p fold from the masks runs ungated"""
+@pytest.mark.parametrize("d", [24, 1024])
+def test_dev_fold_step_packed_planes_slot_fold(ctx, monkeypatch, d):
+    """LATTICEUM_AMD_FOLD=slot with packed planes: f_0 from the masks in Z_p (d = 24)
+    or from the operand rows (d = 1024), ungated"""
     monkeypatch.setenv("LATTICEUM_AMD_FOLD", "slot")
-    check_dev_fold_step(ctx, 24, 17, 3, packed=True)
+    check_dev_fold_step(ctx, d, 17, 3 if d == 24 else 2, packed=True)
 
 
-def test_dev_fold_step_phi72_planes_beside_rows(ctx):
+@pytest.mark.parametrize("d", [24, 1024])
+def test_dev_fold_step_planes_beside_rows(ctx, d):
     """planes given together with the u64 rows: both are written"""
-    check_dev_fold_step(ctx, 24, 17, 3, packed="both")
+    check_dev_fold_step(ctx, d, 17, 3 if d == 24 else 2, packed="both")
+
+
+def test_dev_fold_step_packed_planes_repeated(ctx):
+    """consecutive packed d = 1024 steps on the same buffers"""
+    check_dev_fold_step(ctx, 1024, 37, 2, steps=3, packed=True)
 
 
 def check_dev_fold_step(ctx, d, W, kappa, steps=1, keep_fk=True, rho=None, packed=False):
@@ -455,7 +463,7 @@ def check_dev_fold_step(ctx, d, W, kappa, steps=1, keep_fk=True, rho=None, packe
         "fk": [dev(n=K * N * d) for _ in range(2)] if keep_fk and packed is not True else [None, None],
         "wk": [dev(n=K * W * d) for _ in range(2)], "y": [dev(n=K * kappa * d) for _ in range(2)],
         "f0": dev(n=N * d), "f0_coeff": dev(n=N * d), "w_ccs0": dev(n=W * d), "cm0": dev(n=kappa * d),
-        "planes": [dev(n=K * N) for _ in range(2)] if packed else [None, None],
+        "planes": [dev(n=K * N if d == 24 else N * 256) for _ in range(2)] if packed else [None, None],
     }
     b = LA.LfFoldStepBufs()
     for k, v in keep.items():
@@ -475,7 +483,7 @@ def check_dev_fold_step(ctx, d, W, kappa, steps=1, keep_fk=True, rho=None, packe
         if packed:  # the rows as lf_dev_expand_planes makes them from the packed planes
             for s in range(2):
                 fck, fk = dev(n=K * N * d), dev(n=K * N * d)
-                ctx.dev_expand_planes(d, keep["planes"][s], K * N, fck, fk)
+                ctx.dev_expand_planes(pr, keep["planes"][s], N, fck, fk)
                 ctx.sync()
                 if packed == "both":
                     assert torch.equal(fck, keep["fk_coeff"][s]) and torch.equal(fk, keep["fk"][s])

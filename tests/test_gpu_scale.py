@@ -77,11 +77,11 @@ def check_workload(wl, seed_w, picks, cm_rows, y_rows):
     y = [host(t).reshape(K, kappa, d) for t in keep["y"]]
     fk_dev, fck_dev = keep["fk"], keep["fk_coeff"]
     if keep.get("planes", [None])[0] is not None and fk_dev[0] is None:
-        # the step kept its planes packed (d = 24): the u64 rows as lf_dev_expand_planes makes them
+        # the step kept its planes packed: the u64 rows as lf_dev_expand_planes makes them
         fk_dev, fck_dev = [], []
         for s in range(2):
             fck, fk = (torch.empty(K * N * d, dtype=torch.int64, device=keep["f"].device) for _ in range(2))
-            wl.ctxs[0].dev_expand_planes(d, keep["planes"][s], K * N, fck, fk)
+            wl.ctxs[0].dev_expand_planes(pr, keep["planes"][s], N, fck, fk)
             fk_dev.append(fk)
             fck_dev.append(fck)
         wl.ctxs[0].sync()
