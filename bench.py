@@ -175,11 +175,16 @@ def load_traffic(d, W, kappa):
 def load_sq(d, W, kappa):
     """PMC-measured VALU busy fraction per kernel (profiles/pmc_sq.json, written by
     tools/prof_summary.py sq from one SQ pass of this configuration); {} otherwise."""
-    try:
-        doc = json.loads((ROOT / "profiles" / "pmc_sq.json").read_text())
-    except (OSError, ValueError):
-        return {}
-    if doc.get("config") != {"d": d, "W": W, "kappa": kappa}:
+    doc = None
+    for name in ("pmc_sq.json", f"pmc_sq_d{d}.json"):  # the default workload's, then a side config's
+        try:
+            cand = json.loads((ROOT / "profiles" / name).read_text())
+        except (OSError, ValueError):
+            continue
+        if cand.get("config") == {"d": d, "W": W, "kappa": kappa}:
+            doc = cand
+            break
+    if doc is None:
         return {}
     t = {k: v.get("valu_busy") for k, v in doc.get("kernels", {}).items()}
     for k in list(t):

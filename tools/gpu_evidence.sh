@@ -36,6 +36,13 @@ timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CY
 rc=$?; echo "sq rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python tools/prof_summary.py sq gpurun_out/pmc_sq_$TAG gpurun_out/pmc_sq_$TAG.json 1024 16384 32 > /dev/null && \
   cp gpurun_out/pmc_sq_$TAG.json profiles/pmc_sq.json
+# the same SQ pass over the reference ring's step (d = 24 at the zkvm shape, one stream)
+timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+  SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_WAVES GRBM_GUI_ACTIVE -d gpurun_out/pmc24_sq_$TAG -o run --output-format csv -- \
+  python bench.py $A24 > gpurun_out/pmc24_sq_$TAG.log 2>&1
+rc=$?; echo "sq24 rc=$rc"; [ $rc -eq 0 ] || exit $rc
+python tools/prof_summary.py sq gpurun_out/pmc24_sq_$TAG gpurun_out/pmc_sq_d24_$TAG.json 24 19763 32 > /dev/null && \
+  cp gpurun_out/pmc_sq_d24_$TAG.json profiles/pmc_sq_d24.json
 if [ -z "$SKIP_BENCH" ]; then
 timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -c 300 gpurun_out/bench_$TAG.log; [ $rc -eq 0 ] || exit $rc
