@@ -639,3 +639,166 @@ def check_relation(ccs: CCS, z):
             had = mul(had, O.spmv(rp, col, val, d, z), d)
         total = add(total, smul(c_i, had, d))
     return not np.any(total)
+
+
+# ---------------------------------------------------------------- verifier-variable replay
+def fq3_inv(a):
+    """inverse in Fq3 = Fq[u]/(u^3 - 2^40) (via the norm)"""
+    w = 1 << 40
+    a0, a1, a2 = (int(x) for x in a)
+    t0 = (a0 * a0 - w * a1 * a2) % P
+    t1 = (w * a2 * a2 - a0 * a1) % P
+    t2 = (a1 * a1 - a0 * a2) % P
+    n = (a0 * t0 + w * (a2 * t1 + a1 * t2)) % P
+    ni = pow(n, P - 2, P)
+    return [t0 * ni % P, t1 * ni % P, t2 * ni % P]
+
+
+def fq3_mul(a, b):
+    w = 1 << 40
+    a0, a1, a2 = (int(x) for x in a)
+    b0, b1, b2 = (int(x) for x in b)
+    return [(a0 * b0 + w * (a1 * b2 + a2 * b1)) % P, (a0 * b1 + a1 * b0 + w * a2 * b2) % P,
+            (a0 * b2 + a1 * b1 + a2 * b0) % P]
+
+
+def zk_interpolate(p, r3, d: int):
+    """zk_interpolate_uni_poly (LF/utils/sumcheck/verifier.rs:267-340): the value at
+    r of the polynomial through (i, p_i) and its terms p_i L_i(r), i from len - 1 down"""
+    n = len(p)
+    terms = []
+    for i in reversed(range(n)):
+        num = [1, 0, 0]
+        den = 1
+        for j in range(n):
+            if j != i:
+                num = fq3_mul(num, [(int(r3[0]) - j) % P, int(r3[1]), int(r3[2])])
+                den = den * (i - j) % P
+        x = fq3_mul(num, [pow(den, P - 2, P), 0, 0])
+        terms.append(mul(p[i], scal(x, d), d))
+    res = zero(d)
+    for t_ in terms:
+        res = add(res, t_)
+    return res, terms
+
+
+def zk_eq(x, y, d: int):
+    """zk_eq_eval (LF/utils/sumcheck/utils.rs:100-131): eq(x, y) and its helper values"""
+    res, xy, fac, sub_res = one(d), [], [], [one(d)]
+    for xi, yi in zip(x, y):
+        p = mul(xi, yi, d)
+        xy.append(p)
+        f = add(sub(sub(add(p, p), xi), yi), one(d))
+        fac.append(f)
+        res = mul(res, f, d)
+        sub_res.append(res)
+    return res, {"xi_yis": xy, "factors": fac, "sub_res": sub_res}
+
+
+def replay_sumcheck(tr: Transcript, proof, nv: int, degree: int, claim):
+    """collect_*_sumcheck_vars (ZK/zk_latticefold.rs:283-345, 596-659)"""
+    d = tr.d
+    tr.absorb(from_u(nv, d))
+    tr.absorb(from_u(degree, d))
+    msgs = O._u64(proof).reshape(nv, degree + 1, d)
+    claimed, subterms, point = [claim], [], []
+    for i in range(nv):
+        tr.absorb(msgs[i].ravel())
+        ch = tr.get_challenge()
+        point.append(ch)
+        cs, terms = zk_interpolate(list(msgs[i]), ch, d)
+        claimed.append(cs)
+        subterms += terms
+        tr.absorb(scal(ch, d))
+    return {"claimed_sums": claimed, "subterms": subterms, "point": [scal(c, d) for c in point],
+            "expected": claimed[-1]}
+
+
+def fold_replay(ccs: CCS, acc: LCCCS, cm_i, x_ccs, proof: Proof, pr: Params):
+    """generate_verification_witness_vars (ZK/zk_latticefold.rs:111-148): the
+    transcript replay of a fold() proof and the values the in-CCS verifier needs"""
+    d, s, K, t = ccs.d, ccs.s, pr.K, ccs.t
+    assert d == 24, "the zkvm's replay is written for the Phi_72 ring (TAU = 3)"
+    tr = Transcript(d)
+    absorb_public_input(tr, acc, cm_i, x_ccs)
+    # collect_linearization_vars (:204-277)
+    tr.absorb_label(b"beta_s")
+    beta = tr.get_challenges(s)
+    lin = replay_sumcheck(tr, proof.lin_sumcheck, s, ccs.degree + 1, zero(d))
+    _, eqv = zk_eq(lin["point"], beta, d)
+    inner, products = zero(d), []
+    for c_i, S_i in zip(ccs.c, ccs.S):
+        prod = one(d)
+        for j in S_i:
+            prod = mul(prod, proof.lin_u[j], d)
+        products.append(prod)
+        inner = add(inner, mul(c_i, prod, d))
+    tr.absorb(np.concatenate(proof.lin_v))
+    tr.absorb(np.concatenate(proof.lin_u))
+    lin_lcccs = LCCCS(r=lin["point"], v=list(proof.lin_v), cm=O._u64(cm_i), u=list(proof.lin_u), x_w=list(x_ccs),
+                      h=one(d))
+    # collect_decomposition_vars (:393-432)
+    lcccs = []
+    for src, dp in ((acc, proof.dec[0]), (lin_lcccs, proof.dec[1])):
+        for k in range(K):
+            for part in (dp["x_s"][k], dp["y_s"][k], dp["u_s"][k], dp["v_s"][k]):
+                tr.absorb(np.concatenate(part))
+            xk = dp["x_s"][k]
+            lcccs.append(LCCCS(r=list(src.r), v=dp["v_s"][k], cm=np.concatenate(dp["y_s"][k]), u=dp["u_s"][k],
+                               x_w=xk[:-1], h=xk[-1]))
+    # collect_folding_vars (:465-581)
+    alpha, fbeta, zeta, mu = squeeze_alpha_beta_zeta_mu(tr, K, s)
+    h1s, h2s, g1t, g3h, g3t = [], [], [], [], []
+    g1, g3 = zero(d), zero(d)
+    for i in range(2 * K):
+        v_i, u_i = lcccs[i].v, lcccs[i].u
+        h1 = add(mul(alpha[i], v_i[2], d), v_i[1])
+        h2 = add(mul(alpha[i], h1, d), v_i[0])
+        ci = mul(alpha[i], h2, d)
+        h1s.append(h1)
+        h2s.append(h2)
+        g1t.append(ci)
+        g1 = add(g1, ci)
+        h = add(mul(zeta[i], u_i[t - 1], d), u_i[t - 2])
+        g3h.append(h)
+        for j in reversed(range(t - 2)):
+            h = add(mul(zeta[i], h, d), u_i[j])
+            g3h.append(h)
+        c3 = mul(zeta[i], h, d)
+        g3t.append(c3)
+        g3 = add(g3, c3)
+    fs = replay_sumcheck(tr, proof.fold_sumcheck, s, 2 * pr.b_small, add(g1, g3))
+    r0 = fs["point"]
+    e_ast, _ = zk_eq(fbeta, r0, d)
+    should = zero(d)
+    for i in range(2 * K):
+        e_i, _ = zk_eq(lcccs[i].r, r0, d)
+        th = proof.theta_s[i]
+        sm = mul(powers_dot(alpha[i], th, d), e_i, d)
+        norm, pw = zero(d), mu[i]
+        for t_ in th:
+            prod = t_
+            for j in range(1, pr.b_small):
+                jh = from_u(j, d)
+                prod = mul(prod, mul(sub(t_, jh), add(t_, jh), d), d)
+            norm = add(norm, mul(pw, prod, d))
+            pw = mul(pw, mu[i], d)
+        sm = add(sm, mul(e_ast, norm, d))
+        sm = add(sm, mul(e_i, powers_dot(zeta[i], proof.eta_s[i], d), d))
+        should = add(should, sm)
+    for th in proof.theta_s:
+        tr.absorb(np.concatenate(th))
+    for et in proof.eta_s:
+        tr.absorb(np.concatenate(et))
+    _, rho = get_rhos(tr, K)
+    final_cm = [mul(cm_j, rho[i], d) for i in range(2 * K) for cm_j in elems(lcccs[i].cm, d)]
+    final_u = [mul(e, rho[i], d) for i in range(2 * K) for e in proof.eta_s[i]]
+    final_x = [mul(x, rho[i], d) for i in range(2 * K) for x in list(lcccs[i].x_w) + [lcccs[i].h]]
+    return {"lin_beta": beta, "lin_claimed_sums": lin["claimed_sums"], "lin_subterms": lin["subterms"],
+            "lin_point": lin["point"], "lin_expected": lin["expected"], "lin_inner": inner,
+            "lin_products": products, "lin_eq_xy": eqv["xi_yis"], "lin_eq_factors": eqv["factors"],
+            "lin_eq_sub": eqv["sub_res"], "alpha": alpha, "beta": fbeta, "zeta": zeta, "mu": mu,
+            "claim_g1_h1": h1s, "claim_g1_h2": h2s, "claim_g1_terms": g1t, "claim_g1": g1, "claim_g3_h": g3h,
+            "claim_g3_terms": g3t, "claim_g3": g3, "fold_claimed_sums": fs["claimed_sums"],
+            "fold_subterms": fs["subterms"], "fold_point": r0, "fold_expected": fs["expected"],
+            "should_equal_s": should, "rho": rho, "final_cm": final_cm, "final_u": final_u, "final_x": final_x}

@@ -110,3 +110,33 @@ def test_vectorised_ccs_builder_is_satisfied():
     cmi = O.ajtai_commit(A, 2, Nn, 24, Wi.f)
     out, _, proof = N.fold_prove(ccs, A, 2, acc, Wa, cmi, x, Wi, pr)
     same_lcccs(out, N.fold_verify(ccs, acc, cmi, x, proof, pr))
+
+
+def test_replay_consistent_with_prover_and_verifier():
+    """the verifier-variable replay (generate_verification_witness_vars) on an honest
+    proof: its challenges are the prover's (r, r_0, the folded LCCCS's rho-weighted
+    sums), the sumcheck claims chain (claimed sum i+1 = the interpolation at the
+    round's challenge, the sum of its terms), the linearization's final claim is
+    eq(r, beta) * inner and the folding's equals should_equal_s"""
+    pr, ccs, A, kappa, acc, Wa, cmi, xi, Wi = instance(24, W=5, t=4, deg=2)
+    out, w0, proof = N.fold_prove(ccs, A, kappa, acc, Wa, cmi, xi, Wi, pr)
+    v = N.fold_replay(ccs, acc, cmi, xi, proof, pr)
+    assert all(np.array_equal(a, b) for a, b in zip(v["fold_point"], out.r))
+    assert np.array_equal(v["fold_expected"], v["should_equal_s"])
+    e, _ = N.zk_eq(v["lin_point"], v["lin_beta"], 24)
+    assert np.array_equal(N.mul(e, v["lin_inner"], 24), v["lin_expected"])
+    assert np.array_equal(v["claim_g1"], N.add(v["claim_g1"], N.zero(24)))
+    # cm_0 = sum of the final cm products
+    kd = kappa
+    cm0 = [N.zero(24) for _ in range(kd)]
+    for i in range(2 * pr.K):
+        for j in range(kd):
+            cm0[j] = N.add(cm0[j], v["final_cm"][i * kd + j])
+    assert np.array_equal(np.concatenate(cm0), out.cm)
+    # each round's terms sum to the next claimed sum
+    deg = 2 * pr.b_small + 1
+    for i in range(ccs.s):
+        tot = N.zero(24)
+        for t_ in v["fold_subterms"][i * deg:(i + 1) * deg]:
+            tot = N.add(tot, t_)
+        assert np.array_equal(tot, v["fold_claimed_sums"][i + 1])
