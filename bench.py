@@ -777,8 +777,15 @@ def fold_prove_line(LA, torch, ctx, M, S, d, n, t, m):
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     prover.timing(True)
-    prover.fold_prove(acc, wa, cmi, xi, wi, w_out)
+    _, pf = prover.fold_prove(acc, wa, cmi, xi, wi, w_out)
     spans = prover.timing(False)
+    # the verifier-variable replay of that proof (generate_verification_witness_vars,
+    # zk_latticefold.rs:111-148): host only, a second pass of the transcript per step
+    t_rep = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        prover.replay(acc, cmi, xi, pf)
+        t_rep.append(time.perf_counter() - t0)
     t0 = time.perf_counter()
     prover.linearize(cma, xa, wa)
     torch.cuda.synchronize()
@@ -788,7 +795,7 @@ def fold_prove_line(LA, torch, ctx, M, S, d, n, t, m):
     return {"workload": f"zkvm fold() end to end (lf_fold_prove): Phi_72, W={W} (n={n}, l={l}), kappa={kappa}, "
                         f"CCS t={t} x {m} rows, {len(S)} multisets, degree {deg}; transcript on the host",
             "ms_per_fold_prove": min(times[1:]) * 1e3, "ms_per_fold_prove_median": float(np.median(times[1:])) * 1e3,
-            "ms_per_linearize": t_lin * 1e3, "span_ms": spans,
+            "ms_per_linearize": t_lin * 1e3, "span_ms": spans, "ms_per_replay": min(t_rep) * 1e3,
             "note": "beside the rho-as-input step of reference_ring: this adds the linearization (Mz, degree-8 "
                     "sumcheck), the decompositions' u_s / v_s, the folding sumcheck, theta_s / eta_s and the "
                     "transcript"}

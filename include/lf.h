@@ -39,6 +39,7 @@
  *       is this project's own (the reference serialises no LCCCS)
  *   zkvm/src/zk_latticefold.rs:37-102 zk_latticefold_prove (fold())  -> lf_fold_prove
  *   zkvm/src/main.rs:305-344 initialize_accumulator's linearization  -> lf_linearize
+ *   zkvm/src/zk_latticefold.rs:111-148 generate_verification_witness_vars -> lf_fold_replay
  *   zkvm/src/main.rs:121-219  the proving loop, sharded over GPUs (SURVEY.md 8(b)
  *       lf_fold_reduce_allranks; no reference analogue: rayon only)
  *                                                              -> lf_comm_*, lf_dev_fold_step_sharded,
@@ -560,6 +561,50 @@ int lf_dev_fhat_evaluate(lf_ctx *ctx, int d, const uint64_t *f_coeff, size_t N, 
 int lf_dev_mle_lincomb(lf_ctx *ctx, int d, const uint64_t *mles, size_t stride, int nm, int nv, const uint64_t *coef,
                        uint64_t *io);
 int lf_ctx_device(const lf_ctx *ctx);
+
+/* generate_verification_witness_vars (zkvm/src/zk_latticefold.rs:111-148): the
+ * host replay of a fold() proof's transcript and the values the in-CCS folding
+ * verifier consumes (collect_linearization_vars :204-345, collect_decomposition_vars
+ * :393-432, collect_folding_vars :465-659). Phi_72 only (tau = 3). Every buffer is
+ * caller-allocated host memory of NTT elements; sizes with s = log2 m, q multisets,
+ * D1 = ccs degree + 2 (linearization evals), D2 = 2 b_small + 1 (folding evals). */
+typedef struct {
+  uint64_t *lin_beta;          /* s */
+  uint64_t *lin_claimed_sums;  /* s + 1 (claim 0 first) */
+  uint64_t *lin_subterms;      /* [s][D1] p_i L_i(r), i from D1 - 1 down */
+  uint64_t *lin_point;         /* s (r) */
+  uint64_t *lin_expected;      /* 1 */
+  uint64_t *lin_inner;         /* 1: sum_i c_i prod_{j in S_i} u_j */
+  uint64_t *lin_products;      /* q */
+  uint64_t *lin_eq_xy, *lin_eq_factors; /* s, s (zk_eq_eval of (r, beta)) */
+  uint64_t *lin_eq_sub;        /* s + 1 */
+  uint64_t *alpha, *beta, *zeta, *mu; /* 2K, s, 2K, 2K */
+  uint64_t *claim_g1_h1, *claim_g1_h2, *claim_g1_terms; /* 2K each */
+  uint64_t *claim_g1;          /* 1 */
+  uint64_t *claim_g3_h;        /* [2K][t - 1] Horner partials */
+  uint64_t *claim_g3_terms;    /* 2K */
+  uint64_t *claim_g3;          /* 1 */
+  uint64_t *fold_claimed_sums; /* s + 1 */
+  uint64_t *fold_subterms;     /* [s][D2] */
+  uint64_t *fold_point;        /* s (r_0) */
+  uint64_t *fold_expected;     /* 1 */
+  uint64_t *should_equal_s;    /* 1 */
+  uint64_t *rho;               /* 2K (NTT form) */
+  uint64_t *final_cm, *final_u, *final_x; /* [2K][kappa], [2K][t], [2K][l + 1]: rho_i-weighted */
+} lf_replay_vars;
+/* the CCS shape the replay reads (host memory; no device handle, so the verifier
+ * side runs without a GPU): t matrices of m rows, l public inputs, degree, the q
+ * coefficients c (NTT elements) and multisets S (S_off [q + 1], S_idx) */
+typedef struct {
+  int t;
+  size_t m, l;
+  int degree, q;
+  const uint64_t *c;
+  const int *S_off, *S_idx;
+} lf_ccs_desc;
+/* the proof as lf_fold_prove wrote it (read only); repr describes every buffer, c included */
+int lf_fold_replay(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *acc, const uint64_t *cm_i,
+                   const uint64_t *x_ccs, const lf_lfproof_mut *proof, lf_replay_vars *out, int repr);
 
 /* ------------------------------------------------------------ host transcript (sequential) */
 lf_transcript *lf_transcript_new(void);

@@ -490,6 +490,12 @@ class Prover:
         self.s = ccs.m.bit_length() - 1
         self.tau = 3 if params.d == 24 else 1
         self.kappa = scheme.kappa
+        self.c, self.S = c, [list(x) for x in S]
+
+    def replay(self, acc: dict, cm_i, x_ccs, proof: dict, repr: int = REPR_CANONICAL) -> dict:
+        """the verifier-variable replay (fold_replay) of a proof this prover wrote"""
+        return fold_replay(self.pr, self.t, self.ccs.m, self.l, self.degree, self.c, self.S, self.kappa, acc, cm_i,
+                           x_ccs, proof, repr)
 
     def fold_prove(self, acc: dict, w_acc: dict, cm_i, x_ccs, w_i: dict, w_out: dict, repr: int = REPR_CANONICAL):
         """acc: {r, v, cm, u, x_w, h} host arrays; w_*: {w_ccs, f, f_coeff} device tensors.
@@ -564,6 +570,47 @@ class Prover:
                 self.h = None
         except Exception:
             pass
+
+
+def fold_replay(params: LfParams, t: int, m: int, l: int, degree: int, c, S, kappa: int, acc: dict, cm_i, x_ccs,
+                proof: dict, repr: int = REPR_CANONICAL) -> dict:
+    """generate_verification_witness_vars (zkvm/src/zk_latticefold.rs:111-148) on the
+    host: replays a fold() proof (the dict Prover.fold_prove returns) and returns the
+    in-CCS verifier's values, keyed as oracle/nifs.py fold_replay names them, each a
+    flat u64 array of NTT elements. Phi_72 only; no GPU involved."""
+    from ._lib import REPLAY_FIELDS, LfCcsDesc, LfLcccs, LfLfproofMut, LfReplayVars, LfRingSlice
+    lib, d, K, bs = load(), params.d, params.K, params.b_small
+    s, q = m.bit_length() - 1, len(S)
+    c = _u64(c)
+    off = np.zeros(q + 1, np.int32)
+    off[1:] = np.cumsum([len(x) for x in S])
+    idx = np.array([j for x in S for j in x] or [0], np.int32)
+    desc = LfCcsDesc(t, m, l, degree, q, c.ctypes.data, off.ctypes.data, idx.ctypes.data)
+    keep = {k: _u64(v) for k, v in acc.items()}
+    sl = lambda a: LfRingSlice(a.ctypes.data, a.size // d)
+    A = LfLcccs(d, sl(keep["r"]), sl(keep["v"]), sl(keep["cm"]), sl(keep["u"]), sl(keep["x_w"]), keep["h"].ctypes.data)
+    pf = {k: (_u64(v) if not isinstance(v, list) else [_u64(x) for x in v]) for k, v in proof.items()}
+    PM = LfLfproofMut()
+    for k in ("lin_sumcheck", "lin_v", "lin_u", "fold_sumcheck", "theta_s", "eta_s"):
+        setattr(PM, k, pf[k].ctypes.data)
+    for k in ("u_s", "v_s", "x_s", "y_s"):
+        for side in range(2):
+            getattr(PM, k)[side] = pf[k][side].ctypes.data
+    sizes = {"lin_beta": s, "lin_claimed_sums": s + 1, "lin_subterms": s * (degree + 2), "lin_point": s,
+             "lin_expected": 1, "lin_inner": 1, "lin_products": q, "lin_eq_xy": s, "lin_eq_factors": s,
+             "lin_eq_sub": s + 1, "alpha": 2 * K, "beta": s, "zeta": 2 * K, "mu": 2 * K, "claim_g1_h1": 2 * K,
+             "claim_g1_h2": 2 * K, "claim_g1_terms": 2 * K, "claim_g1": 1, "claim_g3_h": 2 * K * (t - 1),
+             "claim_g3_terms": 2 * K, "claim_g3": 1, "fold_claimed_sums": s + 1, "fold_subterms": s * (2 * bs + 1),
+             "fold_point": s, "fold_expected": 1, "should_equal_s": 1, "rho": 2 * K, "final_cm": 2 * K * kappa,
+             "final_u": 2 * K * t, "final_x": 2 * K * (l + 1)}
+    out = {k: np.zeros(sizes[k] * d, np.uint64) for k in REPLAY_FIELDS}
+    V = LfReplayVars(*[out[k].ctypes.data for k in REPLAY_FIELDS])
+    cm, xc = _u64(cm_i), (_u64(x_ccs) if l else np.zeros(1, np.uint64))
+    rc = lib.lf_fold_replay(C.byref(desc), C.byref(params), C.byref(A), cm.ctypes.data, xc.ctypes.data, C.byref(PM),
+                            C.byref(V), repr)
+    if rc:
+        raise LfError(rc, "lf_fold_replay: " + lib.lf_status_string(rc).decode())
+    return out
 
 
 def witness_split_w() -> int:

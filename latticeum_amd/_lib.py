@@ -64,6 +64,21 @@ class LfLfproofMut(C.Structure):
                 ("x_s", VP * 2), ("y_s", VP * 2), ("fold_sumcheck", VP), ("theta_s", VP), ("eta_s", VP)]
 
 
+REPLAY_FIELDS = ("lin_beta", "lin_claimed_sums", "lin_subterms", "lin_point", "lin_expected", "lin_inner",
+                 "lin_products", "lin_eq_xy", "lin_eq_factors", "lin_eq_sub", "alpha", "beta", "zeta", "mu",
+                 "claim_g1_h1", "claim_g1_h2", "claim_g1_terms", "claim_g1", "claim_g3_h", "claim_g3_terms",
+                 "claim_g3", "fold_claimed_sums", "fold_subterms", "fold_point", "fold_expected", "should_equal_s",
+                 "rho", "final_cm", "final_u", "final_x")
+
+
+class LfReplayVars(C.Structure):
+    _fields_ = [(k, VP) for k in REPLAY_FIELDS]
+
+
+class LfCcsDesc(C.Structure):
+    _fields_ = [("t", I), ("m", SZ), ("l", SZ), ("degree", I), ("q", I), ("c", VP), ("S_off", VP), ("S_idx", VP)]
+
+
 class LfComb(C.Structure):
     _fields_ = [("kind", I), ("nk", I), ("tau", I), ("bsmall", I), ("mu", VP), ("q", I), ("c", VP),
                 ("S_off", VP), ("S_idx", VP)]
@@ -164,6 +179,8 @@ SIGNATURES = {
     "lf_dev_fhat_evaluate": (I, [VP, I, VP, SZ, SZ, I, I, VP, VP]),
     "lf_dev_mle_lincomb": (I, [VP, I, VP, SZ, I, I, VP, VP]),
     "lf_ctx_device": (I, [VP]),
+    "lf_fold_replay": (I, [C.POINTER(LfCcsDesc), C.POINTER(LfParams), C.POINTER(LfLcccs), VP, VP,
+                           C.POINTER(LfLfproofMut), C.POINTER(LfReplayVars), I]),
     "lf_dev_mz_mles": (I, [VP, VP, VP, I, I, VP]),
     "lf_dev_mz_challenged": (I, [VP, VP, VP, VP, I, I, VP]),
     "lf_dev_mz_evaluate": (I, [VP, VP, VP, I, I, VP, VP]),

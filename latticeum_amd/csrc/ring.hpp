@@ -17,10 +17,10 @@ namespace ring {
 __host__ __device__ constexpr int W(int k) { return (40 * k) % 192; }
 constexpr uint64_t KAPPA = 12297829382473034411ull;  // ntt.rs:43 literal (= 1/(2 w^4 - 1))
 
-__device__ __forceinline__ uint64_t mw(uint64_t x, int k) { return gl::shl192(x, W(k)); }
+LF_HD uint64_t mw(uint64_t x, int k) { return gl::shl192(x, W(k)); }
 
 // goldilocks/ntt.rs:326-334
-__device__ __forceinline__ void phi72_homogenize(uint64_t *c) {
+LF_HD void phi72_homogenize(uint64_t *c) {
   uint64_t t;
   c[4] = gl::neg(c[4]);
   c[7] = mw(c[7], 2);
@@ -42,7 +42,7 @@ __device__ __forceinline__ void phi72_homogenize(uint64_t *c) {
 }
 
 // goldilocks/ntt.rs:338-346
-__device__ __forceinline__ void phi72_dehomogenize(uint64_t *c) {
+LF_HD void phi72_dehomogenize(uint64_t *c) {
   uint64_t t;
   c[4] = gl::neg(c[4]);
   c[7] = mw(c[7], 22);
@@ -64,7 +64,7 @@ __device__ __forceinline__ void phi72_dehomogenize(uint64_t *c) {
 }
 
 // goldilocks/ntt.rs:135-228
-__device__ __forceinline__ void phi72_crt(uint64_t *c) {
+LF_HD void phi72_crt(uint64_t *c) {
 #pragma unroll
   for (int i = 0; i < 12; i++) {
     uint64_t a = c[i], b = c[12 + i];
@@ -95,7 +95,7 @@ __device__ __forceinline__ void phi72_crt(uint64_t *c) {
 }
 
 // goldilocks/ntt.rs:240-319
-__device__ __forceinline__ void phi72_icrt(uint64_t *c) {
+LF_HD void phi72_icrt(uint64_t *c) {
   phi72_dehomogenize(c);
   constexpr int tw[4] = {23, 17, 19, 13};
 #pragma unroll

@@ -70,6 +70,32 @@ def proof_from_device(pf, d, K, tau, t, l, kappa):
                    eta_s=[el(x) for x in pf["eta_s"].reshape(2 * K, t * d)])
 
 
+def check_replay(prover, acc, cm_i, x_ccs, pf, out, kappa):
+    """lf_fold_replay on the device prover's proof: the verifier's replayed
+    transcript meets the prover's (r_0, the claims chain, cm_0 / u_0 / x_0 as the
+    rho-weighted sums of the decomposed instances)"""
+    d, K, t, l = 24, prover.pr.K, prover.t, prover.l
+    v = prover.replay(acc, cm_i, x_ccs, pf)
+    assert np.array_equal(v["fold_point"], out["r"]), "r_0"
+    assert np.array_equal(v["fold_expected"], v["should_equal_s"]), "folding claim"
+    e, _ = N.zk_eq(N.elems(v["lin_point"], d), N.elems(v["lin_beta"], d), d)
+    assert np.array_equal(N.mul(e, v["lin_inner"], d), v["lin_expected"]), "linearization claim"
+
+    def rho_sum(a, n):
+        rows = a.reshape(2 * K, n, d)
+        tot = [N.zero(d) for _ in range(n)]
+        for i in range(2 * K):
+            for j in range(n):
+                tot[j] = N.add(tot[j], rows[i, j])
+        return flat(tot)
+
+    assert np.array_equal(rho_sum(v["final_cm"], kappa), out["cm"]), "cm_0"
+    assert np.array_equal(rho_sum(v["final_u"], t), out["u"]), "u_0"
+    x0 = rho_sum(v["final_x"], l + 1)
+    assert np.array_equal(x0[:l * d], out["x_w"]) and np.array_equal(x0[l * d:], out["h"]), "x_0"
+    return v
+
+
 def check_against_oracle(out, pf, w_out, o_out, o_w0, o_proof):
     assert np.array_equal(out["r"], flat(o_out.r)), "r_0"
     assert np.array_equal(out["v"], flat(o_out.v)), "v_0"
@@ -110,6 +136,8 @@ def test_fold_prove_matches_oracle(d, W, l, t, deg, kappa):
         K, tau = pr_o.K, N.tb(d) if d == 24 else 1
         v = N.fold_verify(ccs, acc, cmi, xi, proof_from_device(pf, d, K, tau, ccs.t, l, kappa), pr_o)
         assert np.array_equal(flat(v.r), out["r"]) and np.array_equal(v.cm, out["cm"])
+        if d == 24:
+            check_replay(prover, acc_dict(acc), cmi, flat(xi), pf, out, kappa)
         # fold again: the device's folded accumulator with a third instance
         x3, W3 = witness(ccs, pr_o, 13)
         cm3 = O.ajtai_commit(A, kappa, Nn, d, W3.f)
@@ -213,6 +241,7 @@ def test_fold_prove_zkvm_dimensions():
         for k in ("r", "v", "u", "x_w"):
             assert np.array_equal(flat(getattr(v, k)), out[k]), k
         assert np.array_equal(v.cm, out["cm"]) and np.array_equal(v.h, out["h"])
+        check_replay(prover, acc, cmi, xi, pf, out, kappa)
         # the folded instance is the folded witness's
         cm0 = zeros(kappa * d)
         ctx.dev_ajtai_commit(sch, [w_out["f"]], cm0)
