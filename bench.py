@@ -105,40 +105,30 @@ def coeff_fold(d, layout, keep_fk):
     """whether lf_dev_fold_step folds f_0 in coefficient form on the i8 matrix
     cores (fold_coeff.hip): X^1024+1 after the fused decomposition, f_k kept or
     the planes packed (not the operand-rows-only mode)"""
-    return d == 1024 and layout == 1 and keep_fk and os.environ.get("LATTICEUM_AMD_FOLD") != "slot"
+    return d == 1024 and layout == 1 and keep_fk
 
 
 def kernel_names(LA, d, W, layout, keep_fk=True):
     """the kernel each lf_dev_fold_step phase launches (for the rocprof / PMC joins)"""
-    names = _kernel_names(LA, d, W, layout, keep_fk)
-    if names["ajtai"] == "k_ajtai_mfma" and os.environ.get("LATTICEUM_AMD_AJTAI_RA", "4") in ("3", "4", "5"):
-        names["ajtai"] = "k_ajtai_mfma_ra"  # A in registers (ajtai_mfma.hip), the default
-    return names
-
-
-def _kernel_names(LA, d, W, layout, keep_fk=True):
+    mfma = "k_ajtai_mfma_ra"  # the i8 contraction, A in registers (ajtai_mfma.hip)
     if d == 24:
-        block = os.environ.get("LATTICEUM_AMD_DEC24") == "block"
-        cf24 = not block and os.environ.get("LATTICEUM_AMD_FOLD") != "slot"
-        return {"decompose": "k_decompose_phi72" if block else "k_decompose_phi72_w",
-                "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_phi72",
-                "fold": "k_fold_coeff_phi72" if cf24 else "k_fold_phi72", "from_w_ccs": "k_from_w_ccs_phi72",
-                "from_f": "k_from_f_phi72",
+        return {"decompose": "k_decompose_phi72_w", "ajtai": mfma if layout == 1 else "k_ajtai_phi72",
+                "fold": "k_fold_coeff_phi72", "from_w_ccs": "k_from_w_ccs_phi72", "from_f": "k_from_f_phi72",
                 "to_frag": "k_to_frag<true, true, true>"}
     if d == 1024:
         small = W < LA.witness_split_w()  # one half-wave per (element, limb) below this W
         cf = coeff_fold(d, layout, keep_fk)
-        return {"decompose": "k_decompose_fused", "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_nega",
+        return {"decompose": "k_decompose_fused", "ajtai": mfma if layout == 1 else "k_ajtai_nega",
                 "fold": "k_fold_coeff" if cf else "k_fold_nega" if keep_fk else "k_fold_frag",
                 "from_w_ccs": "k_from_w_ccs_split" if small else "k_from_w_ccs_n32",
                 "from_f": "k_from_fcoeff_n32" if cf else "k_from_f_split" if small else "k_from_f_n32",
                 "to_frag": "k_to_frag<true, false, true>"}
     if d == 4096:
         return {"decompose": "k_decompose_n4k_fused" if layout == 1 else "k_decompose_n4k",
-                "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_nega",
+                "ajtai": mfma if layout == 1 else "k_ajtai_nega",
                 "fold": "k_fold_nega", "from_w_ccs": "k_from_w_ccs_n4k", "from_f": "k_from_f_n4k",
                 "to_frag": "k_to_frag<true, false, true>"}
-    return {"decompose": "k_decompose_nega", "ajtai": "k_ajtai_mfma" if layout == 1 else "k_ajtai_nega",
+    return {"decompose": "k_decompose_nega", "ajtai": mfma if layout == 1 else "k_ajtai_nega",
             "fold": "k_fold_nega", "from_w_ccs": "k_from_w_ccs_nega", "from_f": "k_from_f_nega",
             "to_frag": "k_to_frag"}
 

@@ -214,103 +214,6 @@ __device__ __forceinline__ void mfma_epilogue(const v16i *acc, int lane, int kt,
 // i + 8 t of a group of 8 ktiles blocks. Blocks are dealt round-robin over the
 // 8 XCDs, so those blocks run on the same XCD at about the same time and the
 // second tile's F copies hit that XCD's L2 instead of HBM.
-template <int CPOL>
-__global__ void __launch_bounds__(256, 1) k_ajtai_mfma(const uint4 *Af, const uint4 *Ff, int d, int nch,
-                                                      int nvec, int kappa, uint64_t *partial, OutPtrs dst,
-                                                      int direct, int cps, int ktiles, int nbase, size_t tile_u4,
-                                                      int qd) {
-  __shared__ uint4 Al[2][4][8 * 64];  // 64 KiB: A copies one chunk ahead
-  __shared__ uint4 Fl[3][32 * 64];    // 96 KiB: F copies two chunks ahead
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int grp = blockIdx.x / (8 * ktiles), rem = blockIdx.x - grp * 8 * ktiles;
-  const int kt = rem >> 3, bi = grp * 8 + (rem & 7);
-  if (bi >= nbase) return;  // uniform over the block
-  const int gw = bi * 4 + w;
-  const int s = gw % d, js = gw / d;  // d % 4 == 0: one split per block, slots 4i .. 4i + 3
-  if (js >= (nch + cps - 1) / cps) return;  // uniform over the block
-  const int c0 = js * cps, c1 = min(nch, c0 + cps);
-  v16i acc[15];
-#pragma unroll
-  for (int t = 0; t < 15; t++) acc[t] = (v16i){0};
-  const uint4 *pa = Af + kt * tile_u4 + ((size_t)s * nch * 8) * 64 + lane;
-  const uint4 *ft = Ff + (size_t)(s >> 2) * nch * FV_CHUNK;  // (s/4, chunk 0) tile
-  auto stage_a = [&](int c, int buf) {
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      __builtin_amdgcn_global_load_lds((const void *)(pa + ((size_t)c * 8 + k) * 64), (lds_void *)&Al[buf][w][k * 64],
-                                       16, 0, CPOL);
-  };
-  // KiB j of an F chunk holds operand row j; wave w copies rows w, w + 4, ..
-  // and skips rows >= nvec (their products only reach discarded outputs)
-  const int nf = (nvec - w + 3) >> 2 < 8 ? (nvec - w + 3) >> 2 : 8;
-  auto stage_f = [&](int c, int buf) {
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const int j = 4 * q + w;
-      if (q < nf)
-        __builtin_amdgcn_global_load_lds((const void *)(ft + (size_t)c * FV_CHUNK + j * 64 + fl_pi(j, lane)),
-                                         (lds_void *)&Fl[buf][j * 64], 16, 0, CPOL);
-    }
-  };
-  // this lane's F operand positions: piece (rh, k, s_lo = w) sits in KiB j = rh >> 1
-  const int rh = 2 * (lane & 31) + (lane >> 5), fj = rh >> 1;
-  int fpos[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) fpos[k] = fj * 64 + fl_pi(fj, (rh & 1) * 32 + k * 4 + w);
-  // per chunk: wait until this wave's copies of chunk c have landed (the nf
-  // F copies of chunk c + 1 issued last iteration may stay in flight:
-  // vmcnt <= nf), barrier (everyone's copies landed, everyone done reading the
-  // buffers about to be refilled), read both operands into registers, issue
-  // A(c + 1) and F(c + 2), then the 64 products.
-  auto wait_vm_nf = [&]() {  // s_waitcnt takes an immediate: one per wave-uniform nf
-    switch (nf) {
-      case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-      case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-      case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-      case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-      case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-      case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-      case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-      case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    }
-  };
-  stage_a(c0, 0);
-  stage_f(c0, 0);
-  if (c0 + 1 < c1) stage_f(c0 + 1, 1);
-  int fb = 0;  // F buffer of chunk c (c - c0 mod 3)
-  for (int c = c0; c < c1; c++) {
-    const int cur = (c - c0) & 1;
-    if (c + 1 < c1)
-      wait_vm_nf();
-    else
-      __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_s_barrier();  // no fence: the waitcnt above is the only ordering needed
-    // operand reads as inline ds_read_b128: the compiler treats any LDS read
-    // after an LDS-DMA copy as dependent on all of them and would wait for the
-    // F(c + 1) copies that must stay in flight; the one lgkmcnt wait is ours
-    v4i a[8], b[8];
-    const uint32_t abase = (uint32_t)(uintptr_t)&Al[cur][w][lane];
-    const uint32_t fbase = (uint32_t)(uintptr_t)&Fl[fb][0];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(a[k]) : "v"(abase), "i"(k * 1024));
-      asm volatile("ds_read_b128 %0, %1" : "=v"(b[k]) : "v"(fbase + 16u * fpos[k]));
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (c + 1 < c1) stage_a(c + 1, cur ^ 1);
-    if (c + 2 < c1) stage_f(c + 2, fb == 0 ? 2 : fb - 1);
-    fb = fb == 2 ? 0 : fb + 1;
-#pragma unroll
-    for (int kb = 0; kb < 8; kb++)
-#pragma unroll
-      for (int ka = 0; ka < 8; ka++)
-        acc[ka + kb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ka], b[kb], acc[ka + kb], 0, 0, 0);
-  }
-  const int so = qd ? (s % qd) * 4 + s / qd : s;  // the ring slot of operand slot s
-  mfma_epilogue(acc, lane, kt, kappa, nvec, d, so, js, direct, dst, partial);
-}
-
 // The same contraction with A in registers ("ra"): a wave's A operand is its
 // own (one slot per wave), so it needs no LDS. Each wave keeps DP chunks of A
 // in flight in VGPRs (32 per chunk, next to the 240 accumulator AGPRs), and the
@@ -428,163 +331,6 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const
   mfma_epilogue(acc, lane, kt, kappa, nvec, d, so, js, direct, dst, partial);
 }
 
-// ---------------------------------------------------------------- F straight from the vectors
-// X^d + 1 in plain slot order: the block's F tile (nvec vectors x 32 columns x
-// its 4 slots) is gathered from the vectors themselves -- 32 contiguous bytes
-// (4 slots) per (vector, column) -- converted to D8 and byte-transposed in
-// registers, and written to LDS in the layout the DMA path leaves there. So
-// the decomposition writes no operand rows and commit(z)'s f needs no
-// k_to_frag. A thread owns (vector pv, column quad jq): per slot it
-// transposes 4 columns x 8 digits (v_perm) into 8 words, one ds_write_b32 per
-// (slot, digit). The global loads of chunk c + 2 are in flight while chunk c
-// multiplies; the LDS writes of chunk c + 1 follow the barrier of chunk c.
-// The four blocks that read the same 128-B line of an element (16 slots) are
-// blocks bi + 8 t (one XCD under the round-robin placement), so the line is
-// fetched into that L2 once.
-template <int CPOL>
-__global__ void __launch_bounds__(256, 1) k_ajtai_mfma_fv(const uint4 *Af, VecPtrs fv, int d, int nch, int nvec,
-                                                         int kappa, uint64_t *partial, OutPtrs dst, int direct,
-                                                         int cps, int ktiles, int nbase, size_t tile_u4, int Lp,
-                                                         size_t Wp) {
-  __shared__ uint4 Al[2][4][8 * 64];  // 64 KiB: A copies one chunk ahead
-  __shared__ uint4 Fl[2][32 * 64];    // 64 KiB: F tiles (chunk c, chunk c + 1)
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int grp = blockIdx.x / (8 * ktiles), rem = blockIdx.x - grp * 8 * ktiles;
-  const int kt = rem >> 3, bi = grp * 8 + (rem & 7);
-  if (bi >= nbase) return;  // uniform over the block
-  const int nq = d >> 2, js = bi / nq, bq = bi - js * nq;
-  const int quad = nq % 32 ? bq : (bq & ~31) + 4 * (bq & 7) + ((bq >> 3) & 3);
-  const int s = 4 * quad + w;
-  if (js >= (nch + cps - 1) / cps) return;  // uniform over the block
-  const int c0 = js * cps, c1 = min(nch, c0 + cps);
-  v16i acc[15];
-#pragma unroll
-  for (int t = 0; t < 15; t++) acc[t] = (v16i){0};
-  const uint4 *pa = Af + kt * tile_u4 + ((size_t)s * nch * 8) * 64 + lane;
-  auto stage_a = [&](int c, int buf) {
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      __builtin_amdgcn_global_load_lds((const void *)(pa + ((size_t)c * 8 + k) * 64), (lds_void *)&Al[buf][w][k * 64],
-                                       16, 0, CPOL);
-  };
-  // producer role: vector pv, columns 4 jq .. 4 jq + 3 of the chunk (half ph, bytes pb .. pb + 3 of a piece)
-  const int pv = tid >> 3, jq = tid & 7, ph = jq >> 2, pb = 4 * (jq & 3);
-  // rows >= nvec only reach discarded outputs: they copy vector 0 (no divergent path)
-  const uint64_t *fvp = fv.p[pv < nvec ? pv : 0] + 4 * quad;
-  ulonglong2 fr[8];
-  // this thread's unit u = 2 c + ph = G Lp + l, advanced by 2 per chunk (no division in the loop)
-  int uG, ul;
-  {
-    const int u = 2 * c0 + ph;
-    uG = u / Lp;
-    ul = u - uG * Lp;
-  }
-  auto load_f = [&]() {  // the next chunk's columns (the unit advances afterwards)
-    const size_t g0 = 16 * (size_t)uG + pb;  // groups g0 .. g0 + 3
-    const size_t col0 = g0 * Lp + ul;
-#pragma unroll
-    for (int cc = 0; cc < 4; cc++) {
-      // columns past the matrix meet zero columns of A: any valid row will do
-      const size_t col = g0 + cc < Wp ? col0 + (size_t)cc * Lp : 0;
-      const ulonglong2 *p = reinterpret_cast<const ulonglong2 *>(fvp + col * d);
-      fr[2 * cc] = p[0];
-      fr[2 * cc + 1] = p[1];
-    }
-    ul += 2;  // ul < Lp before, so at most two subtractions (Lp >= 1)
-#pragma unroll
-    for (int t = 0; t < 2; t++) {
-      const bool wrap = ul >= Lp;
-      ul -= wrap ? Lp : 0;
-      uG += wrap ? 1 : 0;
-    }
-  };
-  // piece (pv, ph, k, sl) of the tile sits at LDS uint4 pv 64 + fl_pi(pv, 32 ph + 4 k + sl)
-  const uint32_t fl0 = (uint32_t)(uintptr_t)&Fl[0][0], fl1 = (uint32_t)(uintptr_t)&Fl[1][0];
-  auto store_f = [&](int buf) {
-    const uint32_t base = (buf ? fl1 : fl0) + (uint32_t)(pv * 64 * 16 + pb);
-#pragma unroll
-    for (int sl = 0; sl < 4; sl++) {
-      uint32_t lo[4], hi[4];
-#pragma unroll
-      for (int cc = 0; cc < 4; cc++) {
-        const uint64_t x = d8((sl & 1) ? fr[2 * cc + (sl >> 1)].y : fr[2 * cc + (sl >> 1)].x);
-        lo[cc] = (uint32_t)x;
-        hi[cc] = (uint32_t)(x >> 32);
-      }
-      uint32_t wk[8];  // digit k of the 4 columns, column cc in byte cc
-#pragma unroll
-      for (int half = 0; half < 2; half++) {
-        const uint32_t *q = half ? hi : lo;
-#pragma unroll
-        for (int bb = 0; bb < 4; bb += 2) {
-          const uint32_t sel = (uint32_t)bb | ((uint32_t)(4 + bb) << 8) | ((uint32_t)(bb + 1) << 16) |
-                               ((uint32_t)(5 + bb) << 24);
-          const uint32_t t01 = __builtin_amdgcn_perm(q[1], q[0], sel);
-          const uint32_t t23 = __builtin_amdgcn_perm(q[3], q[2], sel);
-          wk[4 * half + bb] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
-          wk[4 * half + bb + 1] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const uint32_t addr = base + 16u * (uint32_t)fl_pi(pv, 32 * ph + 4 * k + sl);
-        asm volatile("ds_write_b32 %0, %1" ::"v"(addr), "v"(wk[k]) : "memory");
-      }
-    }
-  };
-  // this lane's F operand positions: piece (rh, k, s_lo = w) sits in KiB j = rh >> 1
-  const int rh = 2 * (lane & 31) + (lane >> 5), fj = rh >> 1;
-  int fpos[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) fpos[k] = fj * 64 + fl_pi(fj, (rh & 1) * 32 + k * 4 + w);
-  stage_a(c0, 0);
-  load_f();
-  store_f(0);
-  asm volatile("" ::: "memory");
-  load_f();
-  // every iteration runs the same copies (the last two re-copy chunk c1 - 1 /
-  // load columns past the split: harmless), so the compiler's wait analysis
-  // sees one path and waits only for what each use needs
-  for (int c = c0; c < c1; c++) {
-    const int cur = (c - c0) & 1;
-    // A(c) landed (the 8 F loads of chunk c + 1 issued after it stay in
-    // flight), this thread's F writes of chunk c done; then the barrier
-    asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    v4i a[8], b[8];
-    const uint32_t abase = (uint32_t)(uintptr_t)&Al[cur][w][lane];
-    const uint32_t fbase = cur ? fl1 : fl0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(a[k]) : "v"(abase), "i"(k * 1024));
-      asm volatile("ds_read_b128 %0, %1" : "=v"(b[k]) : "v"(fbase + 16u * fpos[k]));
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    // the F values may not be touched above this point (the compiler would
-    // otherwise convert them early and wait for every copy in flight)
-#pragma unroll
-    for (int i = 0; i < 8; i += 2)
-      asm volatile("" : "+v"(fr[i].x), "+v"(fr[i].y), "+v"(fr[i + 1].x), "+v"(fr[i + 1].y));
-    // chunk c + 1's F values (loaded an iteration ago: the only vector-memory
-    // operations outstanding here) into the buffer everyone is past reading,
-    // then the copies of A(c + 1) and the loads of F(c + 2) behind the products
-    store_f(cur ^ 1);
-    stage_a(c + 1 < c1 ? c + 1 : c1 - 1, cur ^ 1);
-    // every A copy is issued before any F load: the vmcnt(8) at the loop head
-    // then means "A(c + 1) landed" wherever the compiler places the loads
-    asm volatile("" ::: "memory");
-    load_f();
-    asm volatile("" ::: "memory");  // all of them issued before the products
-#pragma unroll
-    for (int kb = 0; kb < 8; kb++)
-#pragma unroll
-      for (int ka = 0; ka < 8; ka++)
-        acc[ka + kb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ka], b[kb], acc[ka + kb], 0, 0, 0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no copy into LDS outlives the block
-  mfma_epilogue(acc, lane, kt, kappa, nvec, d, s, js, direct, dst, partial);
-}
-
 // ---------------------------------------------------------------- f_0 from the operand rows
 // folding.rs:258-268 compute_f_0 when the step keeps the decomposed planes only
 // as D8 operand rows (the fused d = 1024 decomposition with f_k = null): a
@@ -662,15 +408,6 @@ __global__ void k_phi72_interp(const uint64_t *virt, int nvec, size_t kappa, Out
 }
 
 // ---------------------------------------------------------------- launchers
-// the F-from-vectors contraction (k_ajtai_mfma_fv) applies to X^d + 1 in plain
-// slot order. It is opt-in (LATTICEUM_AMD_AJTAI_FV=1): at d = 1024, W = 2^14 it
-// saves the decomposition its operand rows (13.8 -> 12.2 ms) but its 32-byte
-// gathers from element-major f_k run at about 1.5 TB/s, so the contraction takes
-// 12.8 ms instead of 6.9
-bool mfma_from_vectors(const FragGeom &g, int d) {
-  const char *e = getenv("LATTICEUM_AMD_AJTAI_FV");
-  return e && strcmp(e, "1") == 0 && d != 24 && d % 16 == 0 && !g.qperm;
-}
 size_t frag_elems(const FragGeom &g, int d) { return (size_t)mfma_dim(d) * g.nch * 8 * 64; }  // uint4 per buffer
 int mfma_ktiles(size_t kappa) { return (int)((kappa + 31) / 32); }
 // chunks per column split: AJ_CPS for wide rings; for few virtual slots (Phi_72)
@@ -731,15 +468,6 @@ hipError_t to_frag(const VecPtrs &rows, int nrows, int row0, const FragGeom &g, 
   return hipGetLastError();
 }
 
-// the contraction with A in registers and n chunks of each operand in flight
-// (k_ajtai_mfma_ra, n = 4 by default); LATTICEUM_AMD_AJTAI_RA=n (3..5) picks
-// n, 0 the LDS-staged A (k_ajtai_mfma). d = 1024, W = 2^14: 7.0 -> 6.7-6.9 ms
-static int ajtai_ra() {
-  const char *e = getenv("LATTICEUM_AMD_AJTAI_RA");
-  const int v = e ? atoi(e) : 4;
-  return v >= 3 && v <= 5 ? v : 0;
-}
-
 // partial: mfma_scratch_elems() u64 (split partial sums, then Phi_72's virtual-slot results)
 hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, const VecPtrs &fv, int nvec,
                       bool f_ready, uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st, hipEvent_t ev0,
@@ -750,9 +478,7 @@ hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, c
     return hipErrorInvalidValue;
   OutPtrs out{};
   for (int v = 0; v < nvec; v++) out.p[v] = cm ? cm + (size_t)v * kappa * d : dst->p[v];
-  // X^d + 1 in plain slot order: the contraction gathers F from the vectors itself
-  const bool from_vectors = !f_ready && mfma_from_vectors(g, d);
-  if (!f_ready && !from_vectors) {
+  if (!f_ready) {
     hipError_t e = to_frag(fv, nvec, 0, g, d, true, Ff, st);
     if (e != hipSuccess) return e;
   }
@@ -769,34 +495,16 @@ hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, c
   const int nbase = (int)((waves + 3) / 4);
   const dim3 grid((unsigned)((nbase + 7) / 8 * 8 * ktiles));
   const size_t tile_u4 = frag_elems(g, d);
-  // F is dv nch 8 KiB per launch (A is as large for kappa = 32)
-  if (from_vectors) {
-    if ((size_t)dv * g.nch * 8192 > STREAM_OUT_BYTES)
-      hipLaunchKernelGGL(k_ajtai_mfma_fv<2>, grid, dim3(256), 0, st, Af, fv, dv, g.nch, nvec, (int)kappa, partial,
-                         kout, nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4, g.Lp, g.Wp);
-    else
-      hipLaunchKernelGGL(k_ajtai_mfma_fv<0>, grid, dim3(256), 0, st, Af, fv, dv, g.nch, nvec, (int)kappa, partial,
-                         kout, nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4, g.Lp, g.Wp);
-  } else if (ajtai_ra()) {
-    const bool nt = (size_t)dv * g.nch * 8192 > STREAM_OUT_BYTES;
-#define LF_RA(CP, DP)                                                                                        \
-  hipLaunchKernelGGL((k_ajtai_mfma_ra<CP, DP>), grid, dim3(256), 0, st, Af, Ff, dv, g.nch, nvec, (int)kappa, partial, \
-                     kout, nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4, g.qperm ? d / 4 : 0)
-    switch (ajtai_ra() * 2 + (nt ? 1 : 0)) {
-      case 6: LF_RA(0, 3); break;
-      case 7: LF_RA(2, 3); break;
-      case 8: LF_RA(0, 4); break;
-      case 9: LF_RA(2, 4); break;
-      case 10: LF_RA(0, 5); break;
-      default: LF_RA(2, 5); break;
-    }
-#undef LF_RA
-  } else if ((size_t)dv * g.nch * 8192 > STREAM_OUT_BYTES)
-    hipLaunchKernelGGL(k_ajtai_mfma<2>, grid, dim3(256), 0, st, Af, Ff, dv, g.nch, nvec, (int)kappa, partial, kout,
-                       nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4, g.qperm ? d / 4 : 0);
+  // F is dv nch 8 KiB per launch (A is as large for kappa = 32): streamed past
+  // the caches when larger than they are; A in registers 4 chunks ahead
+  // (k_ajtai_mfma_ra; d = 1024, W = 2^14: 6.7-6.9 ms against 7.0 for A staged
+  // through LDS and no better at 3 or 5 chunks)
+  if ((size_t)dv * g.nch * 8192 > STREAM_OUT_BYTES)
+    hipLaunchKernelGGL((k_ajtai_mfma_ra<2, 4>), grid, dim3(256), 0, st, Af, Ff, dv, g.nch, nvec, (int)kappa, partial,
+                       kout, nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4, g.qperm ? d / 4 : 0);
   else
-    hipLaunchKernelGGL(k_ajtai_mfma<0>, grid, dim3(256), 0, st, Af, Ff, dv, g.nch, nvec, (int)kappa, partial, kout,
-                       nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4, g.qperm ? d / 4 : 0);
+    hipLaunchKernelGGL((k_ajtai_mfma_ra<0, 4>), grid, dim3(256), 0, st, Af, Ff, dv, g.nch, nvec, (int)kappa, partial,
+                       kout, nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4, g.qperm ? d / 4 : 0);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (ev1) (void)hipEventRecord(ev1, st);

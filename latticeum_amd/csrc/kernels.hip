@@ -1475,12 +1475,6 @@ hipError_t from_f(const uint64_t *f, size_t N, int d, int lb, int L, uint64_t *f
   return hipGetLastError();
 }
 
-// LATTICEUM_AMD_DEC24=block: the block-wide d = 24 decomposition (k_decompose_phi72) also for b_small = 2
-static bool dec24_block() {
-  const char *e = getenv("LATTICEUM_AMD_DEC24");
-  return e && !strcmp(e, "block");
-}
-
 hipError_t decompose_phi72_sides(const FusedSides &sd, size_t N, int lb, int L, int lbs, int K, int *err,
                                  uint4 *frag, int nch, hipStream_t st, bool *masks_written) {
   const size_t W = N / L;
@@ -1492,18 +1486,15 @@ hipError_t decompose_phi72_sides(const FusedSides &sd, size_t N, int lb, int L, 
     for (int s = 0; s < sd.nside; s++)
       if (sd.row0[s] < 0 || sd.row0[s] + K - 1 > 32) return hipErrorInvalidValue;
   }
-  if (lbs == 1 && L <= 8 && (L - 1) * lb < 62 && !dec24_block()) {
+  if (lbs == 1 && L <= 8 && (L - 1) * lb < 62) {
     const size_t nblk = (W + 15) / 16, waves = (size_t)sd.nside * nblk * ((K + 3) / 4);
     // streaming stores for the f_coeff_k, f_k and operand rows (mask 7):
     // nothing in the step re-reads f_coeff_k or f_k (the fold reads the digit
     // masks), and the contraction's one pass over the operand rows does not gain
     // from them sitting in the caches either (W = 19 763, 4 streams: cached 0.65
     // ms per launch, 900 steps/s; mask 3 0.50-0.53 ms; mask 7 0.47-0.49 ms with
-    // the contraction 0.385 -> 0.36 ms, 1,133-1,138 -> 1,141-1,150 steps/s);
-    // LATTICEUM_AMD_DEC24_NT overrides the mask
-    const char *nte = getenv("LATTICEUM_AMD_DEC24_NT");
-    int ntm = nte ? atoi(nte) : 7;
-    if (ntm < 0 || ntm > 7) return hipErrorInvalidValue;
+    // the contraction 0.385 -> 0.36 ms, 1,133-1,138 -> 1,141-1,150 steps/s)
+    int ntm = 7;
     // no f_coeff_k / f_k buffers: the planes stay packed (the masks must be kept)
     bool all = true, none = true;  // every side has its u64 rows / no side has
     for (int s = 0; s < sd.nside; s++) {
@@ -1514,14 +1505,14 @@ hipError_t decompose_phi72_sides(const FusedSides &sd, size_t N, int lb, int L, 
     if (none) {
       for (int s = 0; s < sd.nside; s++)
         if (!sd.masks[s]) return hipErrorInvalidValue;
-      ntm = 8 | (ntm & 4);
+      ntm = 12;  // packed only (bit 3), the operand rows still streamed
     }
     const dim3 grid((unsigned)((waves + 3) / 4));
 #define LF_PW(M)                                                                                          \
   case M:                                                                                                \
     hipLaunchKernelGGL(k_decompose_phi72_w<M>, grid, dim3(256), 0, st, sd, N, lb, L, K, err, frag, nch, nblk); \
     break;
-    switch (ntm) { LF_PW(0) LF_PW(1) LF_PW(2) LF_PW(3) LF_PW(4) LF_PW(5) LF_PW(6) LF_PW(7) LF_PW(8) LF_PW(12) default: return hipErrorInvalidValue; }
+    switch (ntm) { LF_PW(7) LF_PW(12) default: return hipErrorInvalidValue; }
 #undef LF_PW
     if (masks_written) *masks_written = sd.masks[0] != nullptr && (sd.nside < 2 || sd.masks[1] != nullptr);
     return hipGetLastError();

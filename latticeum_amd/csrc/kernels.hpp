@@ -82,7 +82,6 @@ FragGeom frag_geom(size_t ncols, int Lp);
 // d = 24 (Phi_72) contracts 40 virtual slots per element (Toom-3, ajtai_mfma.hip)
 int mfma_dim(int d);
 // whether ajtai_mfma gathers the vectors itself (no operand rows) for this geometry
-bool mfma_from_vectors(const FragGeom &g, int d);
 size_t frag_elems(const FragGeom &g, int d);  // uint4 per fragment buffer (32 operand rows)
 int mfma_ktiles(size_t kappa);
 int mfma_nsplit(const FragGeom &g, int d);

@@ -251,10 +251,8 @@ int get_tables(lf_ctx *c, int d, Tables *&out) {
     }
     LF_HIP(c, hipMalloc(&t.mem, h.size() * 8));
     LF_HIP(c, hipMemcpy(t.mem, h.data(), h.size() * 8, hipMemcpyHostToDevice));
-    // d = 1024 runs the register-resident 32 x 32 NTT kernels (kernels_n32.hip);
-    // LATTICEUM_AMD_NTT=stockham selects the workgroup radix-4 Stockham kernels
-    const char *sel = getenv("LATTICEUM_AMD_NTT");
-    const bool n32 = extra && !(sel && strcmp(sel, "stockham") == 0);
+    // d = 1024 / 4096 run the register-resident 32 x 32 NTT kernels (kernels_n32.hip, kernels_n4k.hip)
+    const bool n32 = extra != 0;
     t.fwd = {t.mem, t.mem + d, n32 ? t.mem + 4 * d : nullptr};
     t.inv = {t.mem + 2 * d, t.mem + 3 * d, n32 ? t.mem + 4 * d + 1024 : nullptr};
     if (n32 && d == 4096) {
@@ -283,8 +281,8 @@ int grow(lf_ctx *c, T *&buf, size_t &have, size_t need) {
 int reserve(lf_ctx *c, size_t elems) { return grow(c, c->scratch, c->scratch_elems, elems); }
 
 bool use_mfma(int d, size_t kappa) {
-  const char *sel = getenv("LATTICEUM_AMD_AJTAI");
-  return (d == 24 || d % 16 == 0) && lfk::mfma_ktiles(kappa) <= LF_MAX_KTILES && !(sel && strcmp(sel, "valu") == 0);
+  // kappa > 32 LF_MAX_KTILES (A tiles of 32 rows): the VALU contraction (k_ajtai_phi72 / k_ajtai_nega)
+  return (d == 24 || d % 16 == 0) && lfk::mfma_ktiles(kappa) <= LF_MAX_KTILES;
 }
 
 // RAII device buffer for the synchronous host API
@@ -333,7 +331,7 @@ int ajtai_launch(lf_ctx *c, const lf_ajtai *aj, const uint64_t *const *vecs, int
   lfk::VecPtrs vp{};
   for (int v = 0; v < nvec; v++) vp.p[v] = vecs[v];
   LF_TRY(reserve(c, partial_elems(aj, nvec)));
-  if (aj->Af && !lfk::mfma_from_vectors(aj->geom, aj->d))
+  if (aj->Af)
     LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->geom, aj->d)));
   hipEvent_t a = nullptr, b = nullptr;
   if (c->timing) {
@@ -437,12 +435,6 @@ int decompose_n4k_sides(lf_ctx *c, const Tables *t, int nside, const uint64_t *c
   return LF_OK;
 }
 
-// LATTICEUM_AMD_FOLD=slot: always fold f_0 in NTT form (k_fold_nega, k_fold_phi72), never in coefficient form
-bool coeff_fold_enabled() {
-  const char *e = getenv("LATTICEUM_AMD_FOLD");
-  return !(e && !strcmp(e, "slot"));
-}
-
 int fold_nvec(const lf_params *pr, bool commit_f) { return (commit_f ? 1 : 0) + 2 * (pr->K - 1); }
 
 int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lbs, size_t W,
@@ -460,8 +452,6 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
   // fused path (d = 1024, b_small = 2, fragment order grouped by this L): the
   // decomposition writes its digit planes straight into the MFMA operand buffer
   const bool fused = aj->Af && aj->geom.Lp == L && d == 1024 && lbs == 1 && K <= 15 && t->fwd.mid;
-  // the contraction gathers the planes from f_k itself (k_ajtai_mfma_fv): no operand rows, no k_to_frag
-  const bool fv = aj->Af && lfk::mfma_from_vectors(aj->geom, d);
   // Phi_72 (d = 24): each side's decomposition writes its planes as operand rows (kernels.hip)
   const bool fused24 = aj->Af && aj->geom.Lp == L && d == 24 && L <= 5;
   // d = 4096 (kernels_n4k.hip): the same, with the quarter-major operand slots
@@ -474,13 +464,13 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
   c->masks24_n = 0;
   c->frag_fallback = false;
   if (b->planes[0] || b->planes[1]) {
-    if (!(fused24 || (fused && !fv)) || lbs != 1 || !b->planes[0] || !b->planes[1])
+    if (!(fused24 || fused) || lbs != 1 || !b->planes[0] || !b->planes[1])
       return fail(c, LF_ERR_INVALID_ARG, "packed planes: d = 24 or the fused d = 1024 path, b_small = 2, both sides");
   }
   // X^1024 + 1 without f_k / f_coeff_k: the planes stay packed (the fused
   // decomposition's sign|magnitude words), f_0 comes from the coefficient-form
   // fold, whose fallback for a rho that is not short reads the operand rows
-  const bool packed1024 = no_fk && fused && !fv && !b->fk_coeff[0] && !b->fk_coeff[1];
+  const bool packed1024 = no_fk && fused && !b->fk_coeff[0] && !b->fk_coeff[1];
   // Phi_72 without f_k / f_coeff_k: the decomposed witnesses stay packed (digit masks)
   const bool packed24 = no_fk && fused24;
   if (packed24) {
@@ -488,7 +478,7 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
     if (b->fk_coeff[0] || b->fk_coeff[1])
       return fail(c, LF_ERR_INVALID_ARG, "Phi_72: f_k and f_coeff_k are both given or both NULL");
   } else if (no_fk) {
-    if (!fused || fv) return fail(c, LF_ERR_INVALID_ARG, "f_k buffers may be omitted only on the fused X^1024+1 path");
+    if (!fused) return fail(c, LF_ERR_INVALID_ARG, "f_k buffers may be omitted only on the fused X^1024+1 path");
     if (!packed1024 && (!b->fk_coeff[0] || !b->fk_coeff[1]))
       return fail(c, LF_ERR_INVALID_ARG, "f_coeff_k: both sides or neither");
     if (extra + 2 * (K - 1) + 2 > LF_MAX_VECS) return fail(c, LF_ERR_INVALID_ARG, "too many operand rows");
@@ -500,14 +490,13 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
         fr.rho[s2 * K + k] = s2 * K + k;
       }
     // packed planes fold in coefficient form with the rows as the fallback
-    // (LATTICEUM_AMD_FOLD=slot: from the rows)
-    c->fold_from_frag = !packed1024 || !coeff_fold_enabled();
+    c->fold_from_frag = !packed1024;
     c->frag_fallback = packed1024;
   } else if (!b->fk[0] || !b->fk[1]) {
     return fail(c, LF_ERR_INVALID_ARG, "f_k: both sides or neither");
   }
   if (fused || fused24 || fused4k) {
-    if (!fv) LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->geom, d)));
+    LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->geom, d)));
     if (fused4k) {
       const int row0[2] = {extra, extra + K - 1};
       PhaseTimer pt(c, LF_PHASE_DECOMPOSE);  // both sides in one launch
@@ -526,7 +515,7 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
         sd.row_p0[s] = no_fk ? extra + 2 * (K - 1) + s : -1;
       }
       PhaseTimer pt(c, LF_PHASE_DECOMPOSE);  // both sides in one launch
-      LF_HIP(c, lfk::decompose_fused(sd, N, lb, L, K, c->smg, t->fwd, fv ? nullptr : c->frag, aj->geom.nch, c->d_err,
+      LF_HIP(c, lfk::decompose_fused(sd, N, lb, L, K, c->smg, t->fwd, c->frag, aj->geom.nch, c->d_err,
                                      c->sink, c->ncu, c->cur));
       c->smg_sides_n = N;  // fold_finish's coefficient-form fold reads the digits from here
       if (b->planes[0])  // the caller keeps the packed planes: N x 512 words per side
@@ -538,7 +527,7 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       sd.nside = 2;
       // b_small = 2: the digit masks for fold_finish's coefficient-form fold,
       // into the caller's planes if given, else the context's scratch
-      const bool want_masks = lbs == 1 && (coeff_fold_enabled() || packed24 || b->planes[0]);
+      const bool want_masks = lbs == 1;
       if (want_masks && !b->planes[0]) LF_TRY(grow(c, c->fkeys, c->fkeys_elems, 2 * 2 * (size_t)K * N));
       for (int s = 0; s < 2; s++) {
         sd.f_coeff[s] = fc_side[s];
@@ -558,11 +547,7 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       c->masks24_n = masks ? N : 0;
     }
     lfk::VecPtrs vp{};
-    if (fv) {
-      if (commit_f) vp.p[0] = commit_f;
-      for (int s = 0; s < 2; s++)
-        for (int k = 1; k < K; k++) vp.p[extra + s * (K - 1) + k - 1] = b->fk[s] + (size_t)k * N * d;
-    } else if (commit_f) {
+    if (commit_f) {
       PhaseTimer pt(c, LF_PHASE_TO_FRAG);
       vp.p[0] = commit_f;
       LF_HIP(c, lfk::to_frag(vp, 1, 0, aj->geom, d, true, c->frag, c->cur));
@@ -573,7 +558,7 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       LF_HIP(c, hipEventCreate(&ea));
       LF_HIP(c, hipEventCreate(&eb));
     }
-    LF_HIP(c, lfk::ajtai_mfma(aj->Af, kappa, aj->geom, d, vp, nvec, !fv, c->frag, c->scratch, nullptr, c->cur, ea,
+    LF_HIP(c, lfk::ajtai_mfma(aj->Af, kappa, aj->geom, d, vp, nvec, true, c->frag, c->scratch, nullptr, c->cur, ea,
                               eb, &dst));
     if (c->timing) c->pending.push_back({ea, eb, nvec});
     return LF_OK;
@@ -625,7 +610,7 @@ int fold_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
   // forward transform per element. If a rho is not short the device flag `bad`
   // turns those kernels off and the NTT-form fold and from_f on.
   if (c->smg_sides_n == N && N && d == 1024 && lbs == 1 && K <= 15 && !c->fold_from_frag && t->fwd.mid &&
-      t->inv.mid && coeff_fold_enabled()) {
+      t->inv.mid) {
     const int nw = 2 * K;
     const size_t tab_u64 = ((size_t)nw * lfk::FOLD_RT + 7) / 8, aux = (size_t)nw * 1024 + tab_u64 + 1;
     LF_TRY(grow(c, c->fkeys, c->fkeys_elems, 2 * N * (size_t)K * 64));
@@ -637,9 +622,7 @@ int fold_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       PhaseTimer pt(c, LF_PHASE_FOLD);
       LF_HIP(c, lfk::fold_keys(c->smg, 2 * N, K, c->fkeys, c->cur));
       LF_HIP(c, lfk::fold_rho_tables(b->rho, nw, rc, tab, bad, t->inv, c->cur));
-      // LATTICEUM_AMD_FOLD_SPLIT=0: one task per 32-element tile even when there are few tiles
-      const char *fs = getenv("LATTICEUM_AMD_FOLD_SPLIT");
-      const int ks_n = fs && !strcmp(fs, "0") ? 1 : lfk::fold_coeff_splits(N, K, c->ncu);
+      const int ks_n = lfk::fold_coeff_splits(N, K, c->ncu);
       if (ks_n > 1) LF_TRY(grow(c, c->fpart, c->fpart_elems, (size_t)ks_n * N * 1024));
       LF_HIP(c, lfk::fold_coeff(c->fkeys, tab, bad, N, K, b->f0_coeff, c->ncu, c->cur, ks_n > 1 ? c->fpart : nullptr));
       if (c->frag_fallback) {  // packed planes: the fallback folds from the operand rows
@@ -662,24 +645,17 @@ int fold_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
   // NTT-form fold and Witness::from_f on
   if (c->masks24_n == N && N && d == 24 && lbs == 1 && !c->fold_from_frag) {
     const uint2 *m0 = c->masks24[0], *m1 = c->masks24[1];
-    if (!b->fk[0] || !coeff_fold_enabled()) {
-      // the planes are packed and rho is not known to be short (or LATTICEUM_AMD_FOLD=slot):
+    if (!b->fk[0]) {
+      // the planes are packed: the fallback for a rho that is not short folds
       // f_0 from the masks in Z_p, then Witness::from_f
-      const bool cf = coeff_fold_enabled();
       const int nw = 2 * K;
-      int *bad = nullptr;
-      uint32_t *rc = nullptr;
-      if (cf) {
-        LF_TRY(grow(c, c->faux, c->faux_elems, (size_t)nw * 13 + 1));
-        rc = reinterpret_cast<uint32_t *>(c->faux);
-        bad = reinterpret_cast<int *>(c->faux + (size_t)nw * 13);
-      }
+      LF_TRY(grow(c, c->faux, c->faux_elems, (size_t)nw * 13 + 1));
+      uint32_t *rc = reinterpret_cast<uint32_t *>(c->faux);
+      int *bad = reinterpret_cast<int *>(c->faux + (size_t)nw * 13);
       {
         PhaseTimer pt(c, LF_PHASE_FOLD);
-        if (cf) {
-          LF_HIP(c, lfk::fold_phi72_rho(b->rho, nw, rc, bad, c->cur));
-          LF_HIP(c, lfk::fold_phi72_coeff(m0, m1, rc, bad, N, K, L, lb, b->f0_coeff, b->f0, b->w_ccs0, c->cur));
-        }
+        LF_HIP(c, lfk::fold_phi72_rho(b->rho, nw, rc, bad, c->cur));
+        LF_HIP(c, lfk::fold_phi72_coeff(m0, m1, rc, bad, N, K, L, lb, b->f0_coeff, b->f0, b->w_ccs0, c->cur));
         LF_HIP(c, lfk::fold_phi72_masks(m0, m1, b->rho, K, N, b->f0, bad, c->cur));
       }
       PhaseTimer pt(c, LF_PHASE_FROM_F);
@@ -919,7 +895,7 @@ int lf_ctx_reserve(lf_ctx *c, size_t kappa, size_t ncols, int d, int nvec) {
     probe.Af = reinterpret_cast<uint4 *>(1);  // sizing only
     probe.geom = ajtai_geom(ncols);
     probe.geom.qperm = d == 4096;
-    if (!lfk::mfma_from_vectors(probe.geom, d)) LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(probe.geom, d)));
+    LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(probe.geom, d)));
   }
   LF_TRY(reserve(c, partial_elems(&probe, nvec)));
   return grow(c, c->ybuf, c->ybuf_elems, (size_t)nvec * kappa * d);

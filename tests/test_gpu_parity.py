@@ -166,6 +166,19 @@ def test_decompose_witness(ctx, d, W):
         assert np.array_equal(g, w_)
 
 
+@pytest.mark.parametrize("d", [24, 1024])
+def test_decompose_witness_b_small_4(ctx, d):
+    """DecompositionParams with b_small = 4 (K = 8): the block-wide Phi_72 kernel
+    (k_decompose_phi72) and the generic X^d + 1 one (k_decompose_nega)"""
+    base = params(d)
+    pr = LA.LfParams(d, base.B, base.L, 4, 8)
+    fc, _ = valid_f_coeff(d, 37, 700 + d)
+    got = ctx.decompose_witness(fc, pr)
+    want = O.decompose_witness(fc, d, pr.B, pr.L, pr.b_small, pr.K)
+    for g, w_ in zip(got, want):
+        assert np.array_equal(g, w_)
+
+
 @pytest.mark.parametrize("d", [24, 1024, 4096])
 def test_decompose_overflow_is_an_error(ctx, d):
     pr = params(d)
@@ -338,36 +351,6 @@ def test_dev_fold_step_without_fk_unfused_is_an_error(ctx):
         check_dev_fold_step(ctx, 24, 10, 3, keep_fk=False)
 
 
-def test_dev_fold_step_gathering_contraction(ctx, monkeypatch):
-    """LATTICEUM_AMD_AJTAI_FV=1: the decomposition writes no operand rows and the
-    contraction gathers the planes from f_k (k_ajtai_mfma_fv)"""
-    monkeypatch.setenv("LATTICEUM_AMD_AJTAI_FV", "1")
-    check_dev_fold_step(ctx, 1024, 37, 2)
-
-
-@pytest.mark.parametrize("variant", ["block", "nt0", "nt3", "slotfold"])
-@pytest.mark.parametrize("W", [10, 17, 70])
-def test_dev_fold_step_phi72_decomposition_variants(ctx, monkeypatch, variant, W):
-    """Phi_72: the block-wide decomposition (LATTICEUM_AMD_DEC24=block) and the
-    wave-local one with other streaming-store masks give the oracle's step too
-    (the default, wave-local with mask 7, is test_dev_fold_step_matches_oracle);
-    W = 17 leaves a 16-group unit with one live group"""
-    if variant == "block":
-        monkeypatch.setenv("LATTICEUM_AMD_DEC24", "block")
-    elif variant == "slotfold":  # f_0 from the NTT-form planes (k_fold_phi72) instead of the digit masks
-        monkeypatch.setenv("LATTICEUM_AMD_FOLD", "slot")
-    else:
-        monkeypatch.setenv("LATTICEUM_AMD_DEC24_NT", variant[2:])
-    check_dev_fold_step(ctx, 24, W, 3)
-
-
-def test_dev_fold_step_ntt_form_fold(ctx, monkeypatch):
-    """LATTICEUM_AMD_FOLD=slot: f_0 folded from the NTT-form planes (k_fold_nega)
-    instead of in coefficient form on the matrix cores (fold_coeff.hip)"""
-    monkeypatch.setenv("LATTICEUM_AMD_FOLD", "slot")
-    check_dev_fold_step(ctx, 1024, 37, 2)
-
-
 @pytest.mark.parametrize("W", [3, 17, 70])
 def test_dev_fold_step_phi72_rho_not_short(ctx, W):
     """Phi_72: rho with full-size coefficients turns the coefficient-form fold
@@ -416,14 +399,6 @@ def test_dev_fold_step_packed_planes(ctx, d, W, short):
     short folds from the masks in Z_p (d = 24) or from the operand rows (d = 1024)"""
     K = params(d).K
     check_dev_fold_step(ctx, d, W, 3 if d == 24 else 2, packed=True, rho=None if short else rand(2 * K * d, 6161 + W))
-
-
-@pytest.mark.parametrize("d", [24, 1024])
-def test_dev_fold_step_packed_planes_slot_fold(ctx, monkeypatch, d):
-    """LATTICEUM_AMD_FOLD=slot with packed planes: f_0 from the masks in Z_p (d = 24)
-    or from the operand rows (d = 1024), ungated"""
-    monkeypatch.setenv("LATTICEUM_AMD_FOLD", "slot")
-    check_dev_fold_step(ctx, d, 17, 3 if d == 24 else 2, packed=True)
 
 
 @pytest.mark.parametrize("d", [24, 1024])
@@ -583,27 +558,30 @@ def test_limb_transport_roundtrip(ctx):
     assert [int(v) for v in out.cpu().numpy().view(np.uint64)] == [int(v) for v in want]
 
 
-@pytest.mark.parametrize("layout", ["mfma", "mfma_lds", "mfma_ra3", "mfma_ra5", "valu", "fv"])
 @pytest.mark.parametrize("d,kappa,ncols,nvec", [(16, 3, 40, 5), (64, 32, 70, 29), (1024, 7, 33, 1),
                                                 (1024, 32, 96, 29), (256, 17, 64, 32), (24, 3, 40, 5),
                                                 (24, 32, 700, 29), (24, 9, 33, 1),
                                                 # kappa > 32: 32-row tiles of A (ragged last tile)
                                                 (16, 64, 40, 29), (1024, 33, 33, 3), (24, 64, 200, 29),
                                                 (4096, 40, 17, 2), (64, 128, 40, 5), (24, 100, 35, 7)])
-def test_ajtai_layouts(ctx, monkeypatch, layout, d, kappa, ncols, nvec):
-    # the i8-MFMA contraction (signed base-256 limbs) and the VALU path agree with the oracle
+def test_ajtai_mfma_shapes(ctx, d, kappa, ncols, nvec):
+    # the i8-MFMA contraction (signed base-256 limbs, A in registers) agrees with the oracle
+    check_ajtai(ctx, d, kappa, ncols, nvec, layout=1)
+
+
+@pytest.mark.parametrize("d,kappa,ncols,nvec", [(24, 129, 35, 3), (16, 160, 40, 5), (1024, 130, 9, 2)])
+def test_ajtai_valu_wide_kappa(ctx, d, kappa, ncols, nvec):
+    # kappa > 128 (more than LF_MAX_KTILES 32-row tiles of A): the VALU contraction
+    check_ajtai(ctx, d, kappa, ncols, nvec, layout=0)
+
+
+def check_ajtai(ctx, d, kappa, ncols, nvec, layout):
     import torch
-    if layout == "valu":
-        monkeypatch.setenv("LATTICEUM_AMD_AJTAI", "valu")
-    if layout == "fv":  # the opt-in contraction that gathers F from the vectors itself
-        monkeypatch.setenv("LATTICEUM_AMD_AJTAI_FV", "1")
-    if layout.startswith("mfma_"):  # A staged through LDS (0), or in registers n chunks ahead (default 4)
-        monkeypatch.setenv("LATTICEUM_AMD_AJTAI_RA", "0" if layout == "mfma_lds" else layout[-1])
     A = rand(kappa * ncols * d, 21 + d + kappa).reshape(kappa, ncols, d)
     # edge values in A: 0, p-1 and the D8 digit boundaries
     A.reshape(-1)[:6] = [0, P - 1, 0x7F7F7F7F7F7F7F7F, 0x7F7F7F7F7F7F7F80, (P - 1) // 2, 1]
     sch = LA.AjtaiCommitmentScheme(ctx, A)
-    assert sch.layout == (0 if layout == "valu" else 1)
+    assert sch.layout == layout
     F = rand(nvec * ncols * d, 31 + d)
     F[:4] = [P - 1, 0x7F7F7F7F7F7F7F7F, 0x7F7F7F7F7F7F7F80, 0]
     Ft = torch.from_numpy(F.view(np.int64)).cuda()
@@ -614,16 +592,12 @@ def test_ajtai_layouts(ctx, monkeypatch, layout, d, kappa, ncols, nvec):
     assert np.array_equal(cm.cpu().numpy().view(np.uint64), want)
 
 
-@pytest.mark.parametrize("ra", ["4", "0", "3", "5"])
 @pytest.mark.parametrize("nch", [320, 329])
-def test_ajtai_mfma_extreme_digits(ctx, monkeypatch, ra, nch):
+def test_ajtai_mfma_extreme_digits(ctx, nch):
     # all-(-128) digit products stress the i32 weight accumulators over a full
     # column split (d = 256: 320 chunks per split), and with 329 chunks a ragged
-    # second split of 9 chunks, for
-    # both contraction kernels (LATTICEUM_AMD_AJTAI_RA: A in registers n chunks
-    # ahead, 0: through LDS)
+    # second split of 9 chunks
     import torch
-    monkeypatch.setenv("LATTICEUM_AMD_AJTAI_RA", ra)
     d, kappa, ncols, nvec = 256, 32, nch * 32, 32
     A = np.full(kappa * ncols * d, P - 1, np.uint64).reshape(kappa, ncols, d)
     F = np.full(nvec * ncols * d, P - 1, np.uint64)
