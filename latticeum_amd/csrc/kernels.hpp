@@ -107,8 +107,8 @@ hipError_t decompose_n32(const uint64_t *f_coeff, size_t N, int lb, int L, int K
                          hipStream_t st);
 // b_small = 2, d = 1024: decomposition of nside (<= 2) witnesses in one launch
 // that also writes digit planes 1..K-1 of side s as i8-MFMA operand rows
-// row0[s] .. row0[s] + K - 2 (vector-major, Lp = L order); smg: nside N 512 u32
-// scratch for the packed coefficients
+// row0[s] .. row0[s] + K - 2 (vector-major, Lp = L order); smg[s]: N 512 u32
+// for side s's packed coefficients (the caller's planes or scratch)
 struct FusedSides {
   const uint64_t *f_coeff[2];
   // f_k may be null (d = 1024: the planes stay in the operand rows); d = 24: f_k and
@@ -118,6 +118,7 @@ struct FusedSides {
   int nside;
   int row_p0[2] = {-1, -1};                      // operand row of plane 0, or -1 (not written)
   uint2 *masks[2] = {nullptr, nullptr};          // d = 24, b_small = 2: digit masks [K][N] (nonzero, negative), or null
+  uint32_t *smg[2] = {nullptr, nullptr};         // d = 1024 fused: packed sign|magnitude words [N][512]
 };
 // f_0 = sum_v rho_v f_v with every f_v read from the D8 operand rows (k_fold_frag)
 struct FoldRows {
@@ -128,8 +129,7 @@ struct FoldRows {
 hipError_t fold_frag(const uint4 *frag, const FragGeom &g, const FoldRows &fr, const uint64_t *rho, int d, size_t N,
                      uint64_t *out, hipStream_t st, const int *run_if = nullptr);
 // sink: an 8 KiB device scratch row (stores of groups past W); ncu: the device's CU count
-hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K, uint32_t *smg,
-                           const ring::NegaTables &fwd, uint4 *frag, int nch, int *err, uint64_t *sink, int ncu,
+hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K, const ring::NegaTables &fwd, uint4 *frag, int nch, int *err, uint64_t *sink, int ncu,
                            hipStream_t st);
 
 // f_0 in coefficient form on the i8 matrix cores (fold_coeff.hip), X^1024 + 1, b_small = 2:

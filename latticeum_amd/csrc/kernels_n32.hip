@@ -3,6 +3,8 @@
 // one group of L elements (decompose, from_f); waves never synchronise with
 // each other and there is no s_barrier on this path. Every global access is a
 // 256-B row per half-wave (lane r touches x[r + 32 k]).
+#include <cstring>
+
 #include "digits.hpp"
 #include "frag.hpp"
 #include "kernels.hpp"
@@ -447,12 +449,12 @@ __device__ __forceinline__ uint32_t pack_sm1(uint64_t x, int K, bool &bad) {
   bad |= (m >> K) != 0;
   return (uint32_t)(m & 0x7FFF) | (a < 0 ? 0x8000u : 0u);
 }
-__global__ void k_pack_sm(FusedSides sd, size_t N, int K, uint32_t *smg, int *err) {
+__global__ void k_pack_sm(FusedSides sd, size_t N, int K, int *err) {
   const size_t t0 = 4 * (blockIdx.x * (size_t)blockDim.x + threadIdx.x);  // (side, col, q, r..r+3)
   if (t0 >= sd.nside * N * 512) return;
   const int side = t0 >= N * 512;
   const uint64_t *f_coeff = sd.f_coeff[side];
-  const size_t col = (t0 >> 9) - side * N;  // smg itself is indexed across sides
+  const size_t col = (t0 >> 9) - side * N;
   const int q = (t0 >> 5) & 15, r = t0 & 31;
   const ulonglong2 *x = reinterpret_cast<const ulonglong2 *>(f_coeff + col * D + r + 64 * q);
   const ulonglong2 a0 = x[0], a1 = x[1], c0 = x[16], c1 = x[17];
@@ -463,16 +465,79 @@ __global__ void k_pack_sm(FusedSides sd, size_t N, int K, uint32_t *smg, int *er
   o.z = pack_sm1(a1.x, K, bad) | (pack_sm1(c1.x, K, bad) << 16);
   o.w = pack_sm1(a1.y, K, bad) | (pack_sm1(c1.y, K, bad) << 16);
   if (bad) raise(err, 1);
-  *reinterpret_cast<uint4 *>(smg + t0) = o;
+  *reinterpret_cast<uint4 *>(sd.smg[side] + (t0 - side * N * 512)) = o;
 }
 
-template <bool NT>
-__global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_all, size_t N, int L, int lb,
+// Stage 1 of the digit planes' NTT on the matrix cores (MX): for one element,
+// Y[j1][m1] = sum_j2 zeta^((2 m1 + 1) j2) x[j1 + 32 j2] is a 32 x 32 x 32 product
+// of the constant matrix Z[m1][j2] = zeta^((2 m1 + 1) j2) (its 8 signed D8 byte
+// planes, az) with the ternary digits B[j2][j1] = x[j1 + 32 j2], so one
+// v_mfma_i32_32x32x32_i8 per byte plane (|sum| <= 32 * 128) replaces the two
+// integer and three field levels of neg_ct32 per lane. Lane (r, h) holds
+// Z_t[r][16 h + j] and B[16 h + j][r] (j < 16) and gets D[m1][j1 = r] for
+// m1 = (i & 3) + 8 (i >> 2) + 4 h in register i; Y = Q0 + Q1 2^32 with Q0 =
+// sum_{t < 4} 2^(8t) D_t, Q1 = sum_{t >= 4} 2^(8(t-4)) D_t (|Q| < 2^37). A wave
+// does both of its halves' elements (16 products), so the transpose into the
+// second stage's layout stays inside the wave's own LDS tiles.
+__device__ __forceinline__ v4i mx_digits(const uint32_t *w8, int kb) {
+  // words q = 8 h + i of one element: x[r + 32 (2q)] | x[r + 32 (2q + 1)] << 16 (15-bit
+  // magnitude | sign << 15); byte j of the result = digit kb of x[r + 32 (16 h + j)] in {0, 1, -1}
+  v4i b;
+#pragma unroll
+  for (int p = 0; p < 4; p++) {
+    const uint32_t w0 = w8[2 * p], w1 = w8[2 * p + 1];
+    const uint32_t m0 = (w0 >> kb) & 0x10001u, m1 = (w1 >> kb) & 0x10001u;
+    const uint32_t y0 = m0 | (((w0 >> 15) & m0) * 0xFEu), y1 = m1 | (((w1 >> 15) & m1) * 0xFEu);
+    b[p] = (int)__builtin_amdgcn_perm(y1, y0, 0x06040200u);  // bytes 0, 2 of y0, then of y1
+  }
+  return b;
+}
+// one element's stage 1 and middle factors into its transpose tile Te[m1][j1];
+// azl: the byte planes in LDS ([t][m1][j2] int8), read per product (registers
+// are the constraint here: the Horner sums and the prefetched words stay live)
+__device__ __forceinline__ v4i az_piece(const int8_t *azl, int t, int r, int h) {
+  return *reinterpret_cast<const v4i *>(azl + (t * 32 + r) * 32 + 16 * h);
+}
+__device__ __forceinline__ void mx_stage1(const int8_t *azl, const uint32_t *w8, int kb, const uint64_t *midT,
+                                          uint64_t *Te, int r, int h) {
+  const v4i b = mx_digits(w8, kb);
+  // Q = sum_t 2^(8t) D_t over 4 planes, two planes at a time (|partial| < 2^21 in int32)
+  auto quarter = [&](int t0, int64_t *q) {
+    v16i a0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(az_piece(azl, t0, r, h), b, (v16i){0}, 0, 0, 0);
+    v16i a1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(az_piece(azl, t0 + 1, r, h), b, (v16i){0}, 0, 0, 0);
+    int32_t p[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) p[i] = a0[i] + a1[i] * 256;
+    a0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(az_piece(azl, t0 + 2, r, h), b, (v16i){0}, 0, 0, 0);
+    a1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(az_piece(azl, t0 + 3, r, h), b, (v16i){0}, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 16; i++) q[i] = (int64_t)(p[i] + a0[i] * 65536) + (int64_t)a1[i] * (1ll << 24);
+  };
+  int64_t q0[16], q1[16];
+  quarter(0, q0);
+  quarter(4, q1);
+  auto fe = [](int64_t x) { return x < 0 ? (uint64_t)x + gl::P : (uint64_t)x; };  // |x| < 2^37
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const uint64_t y = gl::add(fe(q0[i]), gl::shl96(fe(q1[i]), 32));
+    const int m1 = (i & 3) + 8 * (i >> 2) + 4 * h;
+    // midT[i'][j1] = psi^((2 brv5(i') + 1) j1): row brv5(m1) = brv5(m1 without 4 h) | 4 h
+    const int row = n32::brv5((i & 3) + 8 * (i >> 2)) | (4 * h);
+    Te[m1 * n32::RS + r] = gl::mul(y, midT[row * 32 + r]);
+  }
+}
+
+template <bool NT, bool MX>
+__global__ void __launch_bounds__(512, 1) k_decompose_fused(size_t N, int L, int lb,
                                                            int K, FusedSides sd, const uint64_t *mid_fg,
-                                                           uint4 *frag, int nch, uint64_t *sink) {
+                                                           const uint64_t *az_g, uint4 *frag, int nch,
+                                                           uint64_t *sink) {
   __shared__ uint64_t lds_all[FD_LDS_U64];
   __shared__ uint64_t mid_f[n32::MID_U64];
+  __shared__ uint64_t az_l[MX ? 1024 : 1];  // MX: the 8 KiB of D8 byte planes of zeta^((2 m1 + 1) j2)
   n32::stage_mid(mid_f, mid_fg);
+  if (MX)
+    for (int q = threadIdx.x; q < 1024; q += blockDim.x) az_l[q] = az_g[q];
   __syncthreads();
   const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5, hw = 2 * wib + h;  // hw: this half's group within the block
@@ -480,6 +545,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_
   uint64_t *S = lds_all;
   const size_t W = N / L, nblk = (W + 15) / 16;
   const uint64_t b_pow = gl::mul_pow2(1, lb);  // B = 2^lb
+  const int8_t *azl = reinterpret_cast<const int8_t *>(az_l);
   // a task is one digit plane of one block of 16 groups of one side (planes
   // are independent: small W still fills the chip); consecutive blocks take
   // the planes of the same groups, so the packed words are shared through L2
@@ -487,15 +553,21 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_
     const int side = task >= nblk * K;
     const size_t B = task / K - side * nblk;
     const int kb = (int)(task % K);
-    const uint32_t *smg = smg_all + side * N * 512;
+    const uint32_t *smg = sd.smg[side];
     uint64_t *f_coeff_k = sd.f_coeff_k[side], *f_k = sd.f_k[side], *w_ccs_k = sd.w_ccs_k[side];
     const int row0 = sd.row0[side], row_p0 = sd.row_p0[side];
     const size_t g = 16 * B + hw;
     const bool ok = g < W;
     const size_t gg = ok ? g : 0;
+    // MX: words q = 8 h .. 8 h + 7 of both of the wave's elements (groups 16 B + 2 wib + e)
+    const size_t ge0 = 16 * B + 2 * wib < W ? 16 * B + 2 * wib : 0, ge1 = 16 * B + 2 * wib + 1 < W ? 16 * B + 2 * wib + 1 : 0;
+    auto word = [&](int q, size_t grp, int l) {
+      if (MX) return smg[(((q < 8 ? ge0 : ge1) * L + l) * 16 + 8 * h + (q & 7)) * 32 + r];
+      return smg[((grp * L + l) * 16 + q) * 32 + r];
+    };
     uint32_t wn[16];  // next limb's packed words
 #pragma unroll
-    for (int q = 0; q < 16; q++) wn[q] = smg[((gg * L + L - 1) * 16 + q) * 32 + r];
+    for (int q = 0; q < 16; q++) wn[q] = word(q, gg, L - 1);
     // consume the first limb's words here, so that at the limb loop's head the
     // only outstanding loads are the prefetch issued before the previous limb's
     // 64-80 stores (the compiler then needs no vmcnt wait there, instead of
@@ -510,29 +582,47 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(const uint32_t *smg_
       for (int i = 0; i < 32; i++) acc[i] = 0;
       for (int l = L - 1; l >= 0; l--) {
         const size_t e = (size_t)kb * N + gg * L + l;
-        int32_t dg[32];
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-#pragma unroll
-          for (int t = 0; t < 2; t++) {
-            const uint32_t hwd = wn[q] >> (16 * t);
-            const int32_t bit = (hwd >> kb) & 1;
-            dg[2 * q + t] = (hwd & 0x8000) ? -bit : bit;
-          }
-        }
-        {  // words for the next limb (at l = 0 a harmless reload of limb L - 1)
-          const int ln = l > 0 ? l - 1 : L - 1;
-#pragma unroll
-          for (int q = 0; q < 16; q++) wn[q] = smg[((gg * L + ln) * 16 + q) * 32 + r];
-        }
-        if (f_coeff_k) {  // uniform; groups past W store into `sink` (no branch around the stores: see above)
-          uint64_t *oc = (ok ? f_coeff_k + e * D : sink) + r;
-#pragma unroll
-          for (int k = 0; k < 32; k++) out_store<NT>(&oc[32 * k], from_signed(dg[k]));
-        }
         uint64_t v[32];
-        n32::neg_ct32_digits(dg, v);
-        n32::forward<false>(v, mid_f, T, r);
+        if (MX) {
+          uint64_t *T0 = lds_all + wib * n32::WAVE_U64;
+          mx_stage1(azl, wn, kb, mid_f, T0, r, h);
+          __builtin_amdgcn_sched_barrier(0);  // one element's products and epilogue at a time (registers)
+          mx_stage1(azl, wn + 8, kb, mid_f, T0 + n32::HALF_U64, r, h);
+          {  // words for the next limb, in flight through the second stage (at l = 0 a
+             // harmless reload of limb L - 1)
+            const int ln = l > 0 ? l - 1 : L - 1;
+#pragma unroll
+            for (int q = 0; q < 16; q++) wn[q] = word(q, gg, ln);
+          }
+          n32::wave_lds_sync();
+#pragma unroll
+          for (int j = 0; j < 32; j++) v[j] = T[r * n32::RS + j];  // lane m1 = r of element h: its 32 j1
+          n32::wave_lds_sync();
+          n32::cyc_dif32<false>(v);
+        } else {
+          int32_t dg[32];
+#pragma unroll
+          for (int q = 0; q < 16; q++) {
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+              const uint32_t hwd = wn[q] >> (16 * t);
+              const int32_t bit = (hwd >> kb) & 1;
+              dg[2 * q + t] = (hwd & 0x8000) ? -bit : bit;
+            }
+          }
+          {  // words for the next limb (at l = 0 a harmless reload of limb L - 1)
+            const int ln = l > 0 ? l - 1 : L - 1;
+#pragma unroll
+            for (int q = 0; q < 16; q++) wn[q] = word(q, gg, ln);
+          }
+          if (f_coeff_k) {  // uniform; groups past W store into `sink` (no branch around the stores: see above)
+            uint64_t *oc = (ok ? f_coeff_k + e * D : sink) + r;
+#pragma unroll
+            for (int k = 0; k < 32; k++) out_store<NT>(&oc[32 * k], from_signed(dg[k]));
+          }
+          n32::neg_ct32_digits(dg, v);
+          n32::forward<false>(v, mid_f, T, r);
+        }
         if (f_k) {  // uniform: without f_k the planes live only in the operand rows
           uint64_t *of = (ok ? f_k + e * D : sink) + r;
 #pragma unroll
@@ -604,12 +694,13 @@ hipError_t expand_sm(const uint32_t *smg, size_t N, int K, uint64_t *fck, hipStr
 }
 
 // ---------------------------------------------------------------- launchers
-hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K, uint32_t *smg,
-                           const ring::NegaTables &fwd, uint4 *frag, int nch, int *err, uint64_t *sink, int ncu,
+hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K, const ring::NegaTables &fwd, uint4 *frag, int nch, int *err, uint64_t *sink, int ncu,
                            hipStream_t st) {
   if (K > 15 || !fwd.mid || !sink || ncu < 1 || sd.nside < 1 || sd.nside > 2) return hipErrorInvalidValue;
+  for (int s = 0; s < sd.nside; s++)
+    if (!sd.smg[s]) return hipErrorInvalidValue;
   const size_t words = sd.nside * N * 512;
-  hipLaunchKernelGGL(k_pack_sm, dim3((unsigned)((words / 4 + 255) / 256)), dim3(256), 0, st, sd, N, K, smg, err);
+  hipLaunchKernelGGL(k_pack_sm, dim3((unsigned)((words / 4 + 255) / 256)), dim3(256), 0, st, sd, N, K, err);
   // one 8-wave block per CU (LDS-bound); ntask = nblk K tasks spread evenly
   const size_t ntask = (N / L + 15) / 16 * (size_t)K * sd.nside;
   // every block takes the same number of tasks (no tail round on part of the
@@ -618,13 +709,33 @@ hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K,
   const unsigned grid = (unsigned)((ntask + per - 1) / per);
   // outputs: f_coeff_k, f_k, frag (each K N D words per side) and w_ccs_k
   const size_t out_bytes = sd.nside * (size_t)K * N * D * 8 * 3;
-  if (dec_streaming(out_bytes, false))
-    hipLaunchKernelGGL(k_decompose_fused<true>, dim3(grid), dim3(512), 0, st, smg, N, L, lb, K, sd, fwd.mid, frag,
-                       nch, sink);
-  else
-    hipLaunchKernelGGL(k_decompose_fused<false>, dim3(grid), dim3(512), 0, st, smg, N, L, lb, K, sd, fwd.mid, frag,
-                       nch, sink);
-  return hipGetLastError();
+  // stage 1 on the matrix cores unless LATTICEUM_AMD_DEC_MX=0 (A/B); it writes no
+  // f_coeff_k rows itself (they are expanded from the packed words afterwards)
+  const char *mxe = getenv("LATTICEUM_AMD_DEC_MX");
+  const bool mx = fwd.az && !(mxe && !strcmp(mxe, "0"));
+  const bool nt = dec_streaming(out_bytes, false);
+#define LF_DF(NTV, MXV)                                                                                          \
+  hipLaunchKernelGGL((k_decompose_fused<NTV, MXV>), dim3(grid), dim3(512), 0, st, N, L, lb, K, sd, fwd.mid, fwd.az, \
+                     frag, nch, sink)
+  if (mx) {
+    if (nt)
+      LF_DF(true, true);
+    else
+      LF_DF(false, true);
+  } else if (nt) {
+    LF_DF(true, false);
+  } else {
+    LF_DF(false, false);
+  }
+#undef LF_DF
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !mx) return e;
+  for (int s = 0; s < sd.nside; s++)
+    if (sd.f_coeff_k[s]) {
+      e = expand_sm(sd.smg[s], N, K, sd.f_coeff_k[s], st);
+      if (e != hipSuccess) return e;
+    }
+  return hipSuccess;
 }
 static unsigned half_blocks(size_t units, unsigned cap) {
   size_t b = (units + 2 * WPB - 1) / (2 * WPB);

@@ -47,7 +47,8 @@ struct lf_ctx {
   size_t frag_elems = 0;
   uint32_t *smg = nullptr;      // packed coefficients for the fused decomposition
   size_t smg_elems = 0;
-  size_t smg_sides_n = 0;       // N when smg holds both sides of the last fused d = 1024 fold_commit, else 0
+  size_t smg_sides_n = 0;       // N when smg_side holds both sides of the last fused d = 1024 fold_commit, else 0
+  uint32_t *smg_side[2] = {nullptr, nullptr};  // those packed words: the caller's planes, or smg
   size_t masks24_n = 0;         // N when masks24 hold both sides' Phi_72 digit masks of the last fold_commit, else 0
   const uint2 *masks24[2] = {nullptr, nullptr};  // in fkeys or the caller's lf_fold_step_bufs.planes
   uint32_t *fkeys = nullptr;    // coefficient-form fold: digit keys [2 N][K][64] (fold_coeff.hip)
@@ -191,7 +192,9 @@ int get_tables(lf_ctx *c, int d, Tables *&out) {
     // 1024-point sub-transforms, then the radix-4 twists (fwd, inv) and the digit
     // butterfly table (kernels_n4k.hip)
     const size_t extra = d == 1024 ? 2048 : d == 4096 ? 2048 + 2 * 4096 + 1024 : 0;
-    std::vector<uint64_t> h(4 * (size_t)d + extra);
+    // d = 1024: then the D8 byte planes of zeta^((2 m1 + 1) j2) for the matrix-core stage 1 (1024 u64)
+    const size_t az_off = 4 * (size_t)d + extra;
+    std::vector<uint64_t> h(az_off + (d == 1024 ? 1024 : 0));
     const uint64_t psi = gl::pow(7, (gl::P - 1) / (2 * (uint64_t)d));
     const uint64_t psi_inv = gl::inv(psi), w = gl::mul(psi, psi), w_inv = gl::mul(psi_inv, psi_inv);
     const uint64_t dinv = gl::inv((uint64_t)d);
@@ -222,6 +225,18 @@ int get_tables(lf_ctx *c, int d, Tables *&out) {
           h[4 * d + r * 32 + i] = gl::pow(p1, (uint64_t)(2 * brv5(i) + 1) * r);
           h[4 * d + 1024 + r * 32 + i] = gl::mul(q1inv, gl::pow(p1_inv, (uint64_t)(2 * r + 1) * brv5(i)));
         }
+      if (d == 1024) {
+        // az[t][m1][j2] = signed byte t of D8(zeta^((2 m1 + 1) j2)), zeta = p1^32 (frag.hpp d8)
+        int8_t *az = reinterpret_cast<int8_t *>(h.data() + az_off);
+        const uint64_t zeta = gl::pow(p1, 32);
+        for (int m1 = 0; m1 < 32; m1++)
+          for (int j2 = 0; j2 < 32; j2++) {
+            const uint64_t x = gl::pow(zeta, (uint64_t)(2 * m1 + 1) * j2);
+            const uint64_t tt = x <= 0x7F7F7F7F7F7F7F7Full ? x : x + 0xFFFFFFFFull;
+            const uint64_t dd = (tt + 0x8080808080808080ull) ^ 0x8080808080808080ull;
+            for (int b = 0; b < 8; b++) az[(b * 32 + m1) * 32 + j2] = (int8_t)(uint8_t)(dd >> (8 * b));
+          }
+      }
       if (d == 4096) {
         // kernels_n4k.hip relies on psi^1024 = 2^120 (the radix-4 butterflies are shifts)
         if (gl::pow(psi, 1024) != gl::mul_pow2(1, 120)) return fail(c, LF_ERR_DEVICE, "unexpected 8th root of unity");
@@ -254,6 +269,7 @@ int get_tables(lf_ctx *c, int d, Tables *&out) {
     // d = 1024 / 4096 run the register-resident 32 x 32 NTT kernels (kernels_n32.hip, kernels_n4k.hip)
     const bool n32 = extra != 0;
     t.fwd = {t.mem, t.mem + d, n32 ? t.mem + 4 * d : nullptr};
+    if (d == 1024) t.fwd.az = t.mem + az_off;
     t.inv = {t.mem + 2 * d, t.mem + 3 * d, n32 ? t.mem + 4 * d + 1024 : nullptr};
     if (n32 && d == 4096) {
       t.fwd.tw4 = t.mem + 4 * d + 2048;
@@ -503,7 +519,8 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       LF_TRY(decompose_n4k_sides(c, t, 2, fc_side, b->fk_coeff, b->fk, b->wk, N, lb, L, K, c->frag, aj->geom.nch,
                                  row0));
     } else if (fused) {
-      LF_TRY(grow(c, c->smg, c->smg_elems, 2 * N * 512));
+      // the packed words go straight into the caller's planes when given
+      if (!b->planes[0]) LF_TRY(grow(c, c->smg, c->smg_elems, 2 * N * 512));
       lfk::FusedSides sd{};
       sd.nside = 2;
       for (int s = 0; s < 2; s++) {
@@ -513,15 +530,13 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
         sd.w_ccs_k[s] = b->wk[s];
         sd.row0[s] = extra + s * (K - 1);
         sd.row_p0[s] = no_fk ? extra + 2 * (K - 1) + s : -1;
+        sd.smg[s] = b->planes[0] ? reinterpret_cast<uint32_t *>(b->planes[s]) : c->smg + (size_t)s * N * 512;
+        c->smg_side[s] = sd.smg[s];
       }
       PhaseTimer pt(c, LF_PHASE_DECOMPOSE);  // both sides in one launch
-      LF_HIP(c, lfk::decompose_fused(sd, N, lb, L, K, c->smg, t->fwd, c->frag, aj->geom.nch, c->d_err,
+      LF_HIP(c, lfk::decompose_fused(sd, N, lb, L, K, t->fwd, c->frag, aj->geom.nch, c->d_err,
                                      c->sink, c->ncu, c->cur));
       c->smg_sides_n = N;  // fold_finish's coefficient-form fold reads the digits from here
-      if (b->planes[0])  // the caller keeps the packed planes: N x 512 words per side
-        for (int s = 0; s < 2; s++)
-          LF_HIP(c, hipMemcpyAsync(b->planes[s], c->smg + (size_t)s * N * 512, N * 512 * 4, hipMemcpyDeviceToDevice,
-                                   c->cur));
     } else {
       lfk::FusedSides sd{};
       sd.nside = 2;
@@ -620,7 +635,8 @@ int fold_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
     int *bad = reinterpret_cast<int *>(c->faux + aux - 1);
     {
       PhaseTimer pt(c, LF_PHASE_FOLD);
-      LF_HIP(c, lfk::fold_keys(c->smg, 2 * N, K, c->fkeys, c->cur));
+      for (int s = 0; s < 2; s++)
+        LF_HIP(c, lfk::fold_keys(c->smg_side[s], N, K, c->fkeys + (size_t)s * N * K * 64, c->cur));
       LF_HIP(c, lfk::fold_rho_tables(b->rho, nw, rc, tab, bad, t->inv, c->cur));
       const int ks_n = lfk::fold_coeff_splits(N, K, c->ncu);
       if (ks_n > 1) LF_TRY(grow(c, c->fpart, c->fpart_elems, (size_t)ks_n * N * 1024));

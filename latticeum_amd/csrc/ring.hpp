@@ -180,6 +180,7 @@ struct NegaTables {
                               // (d = 4096: those of its 1024-point sub-transforms, kernels_n4k.hip)
   const uint64_t *tw4 = nullptr;   // d = 4096: radix-4 twists [m0][a] (fwd psi^((2m0-3)a), inv 4^-1 psi^-((2m0-3)a))
   const uint64_t *ztab = nullptr;  // d = 4096 fwd: butterflies of four balanced bits [m0][nibble | signs << 4]
+  const uint64_t *az = nullptr;    // d = 1024 fwd: D8 byte planes of zeta^((2 m1 + 1) j2), int8 [8][32][32]
 };
 
 // Radix-4 Stockham DFT of size D over LDS buffers x -> y (ping-pong), T threads.
