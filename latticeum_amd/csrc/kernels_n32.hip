@@ -516,10 +516,17 @@ __device__ __forceinline__ void mx_stage1(const int8_t *azl, const uint32_t *w8,
   int64_t q0[16], q1[16];
   quarter(0, q0);
   quarter(4, q1);
-  auto fe = [](int64_t x) { return x < 0 ? (uint64_t)x + gl::P : (uint64_t)x; };  // |x| < 2^37
 #pragma unroll
   for (int i = 0; i < 16; i++) {
-    const uint64_t y = gl::add(fe(q0[i]), gl::shl96(fe(q1[i]), 32));
+    // Y = Q0 + Q1 2^32 == A + (Q1l + Q1h) 2^32 with Q1 = Q1h 2^32 + Q1l, A = Q0 - Q1h
+    // (2^64 == 2^32 - 1); = A.lo + T 2^32 with T = A.hi + Q1l + Q1h in (-2^7, 2^32 + 2^7),
+    // = U + th 2^64 == U + th EPS, U = T.lo:A.lo, th = T >> 32 in {-1, 0, 1} (no wrap:
+    // th = 1 leaves U < 2^39, th = -1 U > EPS). Any u64 is a valid gl::mul input.
+    const int64_t q1h = q1[i] >> 32;
+    const int64_t A = q0[i] - q1h;
+    const int64_t T = (A >> 32) + (int64_t)(uint32_t)q1[i] + q1h;
+    const uint64_t U = ((uint64_t)T << 32) | (uint32_t)A;
+    const uint64_t y = U + (uint64_t)((T >> 32) * (int64_t)gl::EPS);
     const int m1 = (i & 3) + 8 * (i >> 2) + 4 * h;
     // midT[i'][j1] = psi^((2 brv5(i') + 1) j1): row brv5(m1) = brv5(m1 without 4 h) | 4 h
     const int row = n32::brv5((i & 3) + 8 * (i >> 2)) | (4 * h);
