@@ -3,8 +3,6 @@
 // one group of L elements (decompose, from_f); waves never synchronise with
 // each other and there is no s_barrier on this path. Every global access is a
 // 256-B row per half-wave (lane r touches x[r + 32 k]).
-#include <cstring>
-
 #include "digits.hpp"
 #include "frag.hpp"
 #include "kernels.hpp"
@@ -468,7 +466,7 @@ __global__ void k_pack_sm(FusedSides sd, size_t N, int K, int *err) {
   *reinterpret_cast<uint4 *>(sd.smg[side] + (t0 - side * N * 512)) = o;
 }
 
-// Stage 1 of the digit planes' NTT on the matrix cores (MX): for one element,
+// Stage 1 of the digit planes' NTT on the matrix cores: for one element,
 // Y[j1][m1] = sum_j2 zeta^((2 m1 + 1) j2) x[j1 + 32 j2] is a 32 x 32 x 32 product
 // of the constant matrix Z[m1][j2] = zeta^((2 m1 + 1) j2) (its 8 signed D8 byte
 // planes, az) with the ternary digits B[j2][j1] = x[j1 + 32 j2], so one
@@ -534,17 +532,16 @@ __device__ __forceinline__ void mx_stage1(const int8_t *azl, const uint32_t *w8,
   }
 }
 
-template <bool NT, bool MX>
+template <bool NT>
 __global__ void __launch_bounds__(512, 1) k_decompose_fused(size_t N, int L, int lb,
                                                            int K, FusedSides sd, const uint64_t *mid_fg,
                                                            const uint64_t *az_g, uint4 *frag, int nch,
                                                            uint64_t *sink) {
   __shared__ uint64_t lds_all[FD_LDS_U64];
   __shared__ uint64_t mid_f[n32::MID_U64];
-  __shared__ uint64_t az_l[MX ? 1024 : 1];  // MX: the 8 KiB of D8 byte planes of zeta^((2 m1 + 1) j2)
+  __shared__ uint64_t az_l[1024];  // the 8 KiB of D8 byte planes of zeta^((2 m1 + 1) j2)
   n32::stage_mid(mid_f, mid_fg);
-  if (MX)
-    for (int q = threadIdx.x; q < 1024; q += blockDim.x) az_l[q] = az_g[q];
+  for (int q = threadIdx.x; q < 1024; q += blockDim.x) az_l[q] = az_g[q];
   __syncthreads();
   const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5, hw = 2 * wib + h;  // hw: this half's group within the block
@@ -561,20 +558,17 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(size_t N, int L, int
     const size_t B = task / K - side * nblk;
     const int kb = (int)(task % K);
     const uint32_t *smg = sd.smg[side];
-    uint64_t *f_coeff_k = sd.f_coeff_k[side], *f_k = sd.f_k[side], *w_ccs_k = sd.w_ccs_k[side];
+    uint64_t *f_k = sd.f_k[side], *w_ccs_k = sd.w_ccs_k[side];
     const int row0 = sd.row0[side], row_p0 = sd.row_p0[side];
     const size_t g = 16 * B + hw;
     const bool ok = g < W;
     const size_t gg = ok ? g : 0;
-    // MX: words q = 8 h .. 8 h + 7 of both of the wave's elements (groups 16 B + 2 wib + e)
+    // words q = 8 h .. 8 h + 7 of both of the wave's elements (groups 16 B + 2 wib + e; past W: group 0)
     const size_t ge0 = 16 * B + 2 * wib < W ? 16 * B + 2 * wib : 0, ge1 = 16 * B + 2 * wib + 1 < W ? 16 * B + 2 * wib + 1 : 0;
-    auto word = [&](int q, size_t grp, int l) {
-      if (MX) return smg[(((q < 8 ? ge0 : ge1) * L + l) * 16 + 8 * h + (q & 7)) * 32 + r];
-      return smg[((grp * L + l) * 16 + q) * 32 + r];
-    };
+    auto word = [&](int q, int l) { return smg[(((q < 8 ? ge0 : ge1) * L + l) * 16 + 8 * h + (q & 7)) * 32 + r]; };
     uint32_t wn[16];  // next limb's packed words
 #pragma unroll
-    for (int q = 0; q < 16; q++) wn[q] = word(q, gg, L - 1);
+    for (int q = 0; q < 16; q++) wn[q] = word(q, L - 1);
     // consume the first limb's words here, so that at the limb loop's head the
     // only outstanding loads are the prefetch issued before the previous limb's
     // 64-80 stores (the compiler then needs no vmcnt wait there, instead of
@@ -590,46 +584,21 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(size_t N, int L, int
       for (int l = L - 1; l >= 0; l--) {
         const size_t e = (size_t)kb * N + gg * L + l;
         uint64_t v[32];
-        if (MX) {
-          uint64_t *T0 = lds_all + wib * n32::WAVE_U64;
-          mx_stage1(azl, wn, kb, mid_f, T0, r, h);
-          __builtin_amdgcn_sched_barrier(0);  // one element's products and epilogue at a time (registers)
-          mx_stage1(azl, wn + 8, kb, mid_f, T0 + n32::HALF_U64, r, h);
-          {  // words for the next limb, in flight through the second stage (at l = 0 a
-             // harmless reload of limb L - 1)
-            const int ln = l > 0 ? l - 1 : L - 1;
+        uint64_t *T0 = lds_all + wib * n32::WAVE_U64;
+        mx_stage1(azl, wn, kb, mid_f, T0, r, h);
+        __builtin_amdgcn_sched_barrier(0);  // one element's products and epilogue at a time (registers)
+        mx_stage1(azl, wn + 8, kb, mid_f, T0 + n32::HALF_U64, r, h);
+        {  // words for the next limb, in flight through the second stage (at l = 0 a
+           // harmless reload of limb L - 1)
+          const int ln = l > 0 ? l - 1 : L - 1;
 #pragma unroll
-            for (int q = 0; q < 16; q++) wn[q] = word(q, gg, ln);
-          }
-          n32::wave_lds_sync();
-#pragma unroll
-          for (int j = 0; j < 32; j++) v[j] = T[r * n32::RS + j];  // lane m1 = r of element h: its 32 j1
-          n32::wave_lds_sync();
-          n32::cyc_dif32<false>(v);
-        } else {
-          int32_t dg[32];
-#pragma unroll
-          for (int q = 0; q < 16; q++) {
-#pragma unroll
-            for (int t = 0; t < 2; t++) {
-              const uint32_t hwd = wn[q] >> (16 * t);
-              const int32_t bit = (hwd >> kb) & 1;
-              dg[2 * q + t] = (hwd & 0x8000) ? -bit : bit;
-            }
-          }
-          {  // words for the next limb (at l = 0 a harmless reload of limb L - 1)
-            const int ln = l > 0 ? l - 1 : L - 1;
-#pragma unroll
-            for (int q = 0; q < 16; q++) wn[q] = word(q, gg, ln);
-          }
-          if (f_coeff_k) {  // uniform; groups past W store into `sink` (no branch around the stores: see above)
-            uint64_t *oc = (ok ? f_coeff_k + e * D : sink) + r;
-#pragma unroll
-            for (int k = 0; k < 32; k++) out_store<NT>(&oc[32 * k], from_signed(dg[k]));
-          }
-          n32::neg_ct32_digits(dg, v);
-          n32::forward<false>(v, mid_f, T, r);
+          for (int q = 0; q < 16; q++) wn[q] = word(q, ln);
         }
+        n32::wave_lds_sync();
+#pragma unroll
+        for (int j = 0; j < 32; j++) v[j] = T[r * n32::RS + j];  // lane m1 = r of element h: its 32 j1
+        n32::wave_lds_sync();
+        n32::cyc_dif32<false>(v);
         if (f_k) {  // uniform: without f_k the planes live only in the operand rows
           uint64_t *of = (ok ? f_k + e * D : sink) + r;
 #pragma unroll
@@ -716,27 +685,16 @@ hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K,
   const unsigned grid = (unsigned)((ntask + per - 1) / per);
   // outputs: f_coeff_k, f_k, frag (each K N D words per side) and w_ccs_k
   const size_t out_bytes = sd.nside * (size_t)K * N * D * 8 * 3;
-  // stage 1 on the matrix cores unless LATTICEUM_AMD_DEC_MX=0 (A/B); it writes no
-  // f_coeff_k rows itself (they are expanded from the packed words afterwards)
-  const char *mxe = getenv("LATTICEUM_AMD_DEC_MX");
-  const bool mx = fwd.az && !(mxe && !strcmp(mxe, "0"));
-  const bool nt = dec_streaming(out_bytes, false);
-#define LF_DF(NTV, MXV)                                                                                          \
-  hipLaunchKernelGGL((k_decompose_fused<NTV, MXV>), dim3(grid), dim3(512), 0, st, N, L, lb, K, sd, fwd.mid, fwd.az, \
-                     frag, nch, sink)
-  if (mx) {
-    if (nt)
-      LF_DF(true, true);
-    else
-      LF_DF(false, true);
-  } else if (nt) {
-    LF_DF(true, false);
-  } else {
-    LF_DF(false, false);
-  }
-#undef LF_DF
+  if (!fwd.az) return hipErrorInvalidValue;
+  if (dec_streaming(out_bytes, false))
+    hipLaunchKernelGGL(k_decompose_fused<true>, dim3(grid), dim3(512), 0, st, N, L, lb, K, sd, fwd.mid, fwd.az, frag,
+                       nch, sink);
+  else
+    hipLaunchKernelGGL(k_decompose_fused<false>, dim3(grid), dim3(512), 0, st, N, L, lb, K, sd, fwd.mid, fwd.az, frag,
+                       nch, sink);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess || !mx) return e;
+  if (e != hipSuccess) return e;
+  // the f_coeff_k rows, when wanted, from the packed words
   for (int s = 0; s < sd.nside; s++)
     if (sd.f_coeff_k[s]) {
       e = expand_sm(sd.smg[s], N, K, sd.f_coeff_k[s], st);
