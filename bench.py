@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--packed", type=int, default=None,
                     help="1: keep the decomposed witnesses as packed digit planes (no u64 f_k / f_coeff_k rows); "
                          "0: write the rows; default: the ring's default (Workload)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="G > 1: the step streams form groups of G whose G steps' contractions run as one "
+                         "launch (lf_dev_fold_step_batch: one pass over A for the group); 1: all streams")
     ap.add_argument("--cpu-baseline", dest="cpu", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu", action="store_false")
     return ap.parse_args()
@@ -121,7 +124,8 @@ def kernel_names(LA, d, W, layout, keep_fk=True):
         return {"decompose": "k_decompose_fused", "ajtai": mfma if layout == 1 else "k_ajtai_nega",
                 "fold": "k_fold_coeff" if cf else "k_fold_nega" if keep_fk else "k_fold_frag",
                 "from_w_ccs": "k_from_w_ccs_split" if small else "k_from_w_ccs_n32",
-                "from_f": "k_from_fcoeff_n32" if cf else "k_from_f_split" if small else "k_from_f_n32",
+                "from_f": ("k_from_fcoeff_split" if small else "k_from_fcoeff_n32") if cf
+                else "k_from_f_split" if small else "k_from_f_n32",
                 "to_frag": "k_to_frag<true, false, true>"}
     if d == 4096:
         return {"decompose": "k_decompose_n4k_fused" if layout == 1 else "k_decompose_n4k",
@@ -267,7 +271,7 @@ class Workload:
     each an lf context on its own HIP stream with its own w_ccs and outputs."""
 
     def __init__(self, LA, torch, local, rank, d, W, kappa, streams, seed_a=SEED_A, keep_fk=True, cu_partition=False,
-                 packed=None):
+                 packed=None, batch=False):
         # keep_fk=False (fused X^1024+1 path only): the decomposed planes live only
         # as MFMA operand rows (lf.h: f_k buffers omitted) -- 20 GB less HBM at
         # W = 2^14, but slower (DESIGN.md section 7), so the bench keeps f_k.
@@ -277,6 +281,13 @@ class Workload:
         # f_coeff_k rows (2 x 8 d B per element and plane); lf_dev_expand_planes
         # makes the rows. d = 1024, W = 2^14: decomposition 14.0 -> 12.4 ms, 41.5 -> 44.0 steps/s
         self.packed = packed = (d in (24, 1024)) if packed is None else packed
+        # batch = G > 1: the step streams form groups of G; each group's G steps are one
+        # lf_dev_fold_step_batch call (independent steps on their own streams, one
+        # contraction launch for the group); the groups take turns, so one group's
+        # contraction overlaps the others' decompositions. batch = 1: one group of all
+        g = streams if batch == 1 else int(batch or 0)
+        self.group = g if 1 < g <= streams and streams % g == 0 else 0
+        self.batch = self.group > 0
         self.keep_fk = keep_fk and not packed
         self.LA, self.torch = LA, torch
         self.d, self.W, self.kappa = d, W, kappa
@@ -348,7 +359,15 @@ class Workload:
         with `comm`, each step is this rank's column shard of one fold
         (lf_dev_fold_step_sharded: RCCL all-reduce of the commitments)"""
         S = streams or len(self.ctxs)
-        for i in range(steps):
+        i = 0
+        if self.batch and comm is None and S == len(self.ctxs):
+            g = self.group
+            for b in range(steps // g):
+                j = (b % (S // g)) * g
+                self.ctxs[j].dev_fold_step_batch(self.ctxs[j + 1:j + g], self.sch, self.pr, self.W,
+                                                 self.bufs[j:j + g])
+            i = steps // g * g
+        for i in range(i, steps):
             if comm is None:
                 self.ctxs[i % S].dev_fold_step(self.sch, self.pr, self.W, self.bufs[i % S])
             else:
@@ -402,6 +421,21 @@ def measure(LA, torch, LD, pg, world, wl, steps, warmup, comm=None):
     dt = time.perf_counter() - t0
     wl.sync()  # surfaces any decomposition overflow
     dt_max = LD.max_over_ranks(pg, dt)
+    if S > 1 and wl.batch and comm is None:
+        # the phase pass of batched steps: every context on the first one's stream,
+        # so the phases run one at a time and the contraction covers S steps
+        base = torch.cuda.current_stream().cuda_stream
+        for c in wl.ctxs:
+            c.set_stream(base)
+        wl.timing(True)
+        n = max(1, steps // wl.group) * wl.group
+        wl.run(n, comm)
+        wl.sync()
+        tot = wl.phase_totals()
+        wl.timing(False)
+        for c, st in zip(wl.ctxs[1:], wl.streams):
+            c.set_stream(st.cuda_stream)
+        return dt_max, phase_report(LA, wl, tot, n)
     if S > 1:  # the phase pass: one stream
         wl.ctxs[0].kernel_timing(True)
         wl.run(steps // S, comm, streams=1)
@@ -485,21 +519,25 @@ def phase_report(LA, wl, tot, steps):
     return phases, roof
 
 
-def extra_shape(LA, torch, LD, pg, local, rank, world, d, W, kappa, S, steps, warmup, what):
+def extra_shape(LA, torch, LD, pg, local, rank, world, d, W, kappa, S, steps, warmup, what, batch=False):
     """Another commit+fold workload with S concurrent step streams per GPU,
     reported beside the default one (not as `value`): the reference's own ring
     at the real zkvm shape (d = 24, W = 19 763; the bit-exact-vs-reference
     path), SURVEY.md 8(d)'s byte-equivalent shape (d = 1024, W = 464), whose
     per-GPU rate the north-star target (1e4 steps/s on 8 GPUs) is about, and
     BASELINE configs[4]'s ring (d = 4096, kappa = 64)."""
-    wl = Workload(LA, torch, local, rank, d, W, kappa, S)
+    wl = Workload(LA, torch, local, rank, d, W, kappa, S, batch=batch)
     dt, (phases, roof) = measure(LA, torch, LD, pg, world, wl, steps, warmup)
+    batched, group = wl.batch, wl.group
     wl.close()
     del wl
     torch.cuda.empty_cache()
     value = world * steps / dt
     step_bytes, _, _ = algorithmic_bytes(d, W, kappa)
-    return {"workload": f"commit+fold step, {what}, w_ccs W={W}, kappa={kappa}, {S} concurrent step streams per GPU",
+    how = (f"{S} concurrent step streams per GPU" +
+           (f", in groups of {group} whose contractions are one launch (one pass over A)"
+            if batched else ""))
+    return {"workload": f"commit+fold step, {what}, w_ccs W={W}, kappa={kappa}, {how}",
             "d": d, "W": W, "kappa": kappa, "streams": S, "value": value, "unit": "fold-steps/s", "n_gpus": world,
             "steps": steps, "ms_per_step_per_gpu": dt / steps * 1e3,
             "hbm_gbs_step_algorithmic": step_bytes * value / world / 1e9, "roofline": roof, "phases": phases}
@@ -809,7 +847,8 @@ def main():
 
     d, W, kappa = args.d, args.w, args.kappa
     wl = Workload(LA, torch, local, rank, d, W, kappa, args.streams, cu_partition=args.cu_partition,
-                  packed=None if args.packed is None else bool(args.packed))
+                  packed=None if args.packed is None else bool(args.packed), batch=bool(args.batch))
+    batched, group = wl.batch, wl.group
     K, L, N = wl.pr.K, wl.pr.L, wl.N
     dt_max, (phases, roof) = measure(LA, torch, LD, pg, world, wl, args.steps, args.warmup)
     wl.close()
@@ -833,7 +872,9 @@ def main():
                                    f"B=2^15 L=5 K=15, 29 Ajtai products in one pass over A; {EXCLUDED}",
                        "d": d, "W": W, "N": N, "kappa": kappa,
                        "parallelism": f"{world} ranks x {args.streams} independent step streams (weak, "
-                                      f"no collective on the data path)"},
+                                      f"no collective on the data path)"
+                                      + (f"; groups of {group} steps whose contractions are one launch "
+                                         f"(one pass over A per group)" if batched else "")},
             "hbm_gbs_step_algorithmic": step_bytes * value / world / 1e9,
             # the dominant phase by device time per step (HIP events on the launch
             # stream, inside the timed region); bytes per SURVEY.md 8(d)

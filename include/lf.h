@@ -30,7 +30,8 @@
  *   zkvm/src/fiat_shamir.rs:20-114  Poseidon2Transcript         -> lf_transcript_*
  *   zkvm/src/main.rs:348-367  commit()                          -> lf_commit
  *   zkvm/src/main.rs:380-404  fold() (its commit+fold arithmetic) -> lf_fold_hot /
- *                                                                 lf_dev_fold_step
+ *                                                                 lf_dev_fold_step,
+ *                                                                 lf_dev_fold_step_batch
  *   zkvm/src/commitments.rs:192-340 vm_mem_comm, vm_mem_comm_with_opening, vm_code_comm
  *                                                              -> lf_vm_mem_comm, lf_dev_merkle_tree,
  *                                                                 lf_merkle_open, lf_vm_code_comm
@@ -274,6 +275,16 @@ int lf_dev_expand_planes(lf_ctx *ctx, const lf_params *pr, const uint64_t *plane
 /* commit(z) followed by the commit+fold arithmetic of fold(), all on device */
 int lf_dev_fold_step(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, size_t W,
                      const lf_fold_step_bufs *b);
+/* nsteps (<= 4) independent commit+fold steps against one Ajtai scheme (trace-batch
+ * shard: independent witness / accumulator pairs, SURVEY.md 8(e) configs[3]), each
+ * with its own context (stream) and buffers. Every step runs lf_dev_fold_step's
+ * arithmetic on its own stream, except that their commitment contractions run
+ * as ONE launch on ctx[0]'s stream, so A (kappa x width ring elements, 21.5 GB at
+ * d = 1024, W = 2^14) is read from HBM once for all of them. Results are bit-exact
+ * with nsteps calls of lf_dev_fold_step; the streams are ordered with events (no
+ * host synchronisation). The contexts must be distinct and on aj's device. */
+int lf_dev_fold_step_batch(lf_ctx *const *ctx, int nsteps, const lf_ajtai *aj, const lf_params *pr, size_t W,
+                           const lf_fold_step_bufs *const *b);
 
 /* A column-sharded step: rank r holds the columns of groups
  * [g_r, g_r + W_r) of the witness -- its w_ccs / acc_f_coeff shards, an Ajtai

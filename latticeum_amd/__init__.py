@@ -257,6 +257,16 @@ class Context:
                       bufs: LfFoldStepBufs):
         self.check(self.lib.lf_dev_fold_step(self.h, scheme.h, C.byref(params), W, C.byref(bufs)))
 
+    def dev_fold_step_batch(self, others, scheme: "AjtaiCommitmentScheme", params: LfParams, W: int, bufs):
+        """len(bufs) independent steps: step 0 on this context, step i on others[i - 1]
+        (each its own stream); their contractions share one pass over A (lf.h)"""
+        ctxs = [self] + list(others)
+        if len(ctxs) != len(bufs):
+            raise ValueError("one context per step")
+        ch = (C.c_void_p * len(ctxs))(*[c.h for c in ctxs])
+        bh = (C.c_void_p * len(bufs))(*[C.cast(C.byref(b), C.c_void_p) for b in bufs])
+        self.check(self.lib.lf_dev_fold_step_batch(ch, len(ctxs), scheme.h, C.byref(params), W, bh))
+
     def fold_step_partial_len(self, scheme: "AjtaiCommitmentScheme", params: LfParams) -> int:
         return self.lib.lf_fold_step_partial_len(scheme.h, C.byref(params))
 

@@ -131,6 +131,7 @@ SIGNATURES = {
     "lf_dev_commit_y0": (I, [VP, C.POINTER(LfParams), VP, VP, SZ]),
     "lf_dev_fold": (I, [VP, I, VP, C.POINTER(VP), I, SZ, VP]),
     "lf_dev_fold_step": (I, [VP, VP, C.POINTER(LfParams), SZ, C.POINTER(LfFoldStepBufs)]),
+    "lf_dev_fold_step_batch": (I, [VP, I, VP, C.POINTER(LfParams), SZ, VP]),
     "lf_dev_poseidon2_permute": (I, [VP, VP, SZ]),
     "lf_dev_poseidon2_permute_rounds": (I, [VP, VP, SZ, I]),
     "lf_dev_fill_uniform": (I, [VP, VP, SZ, U64]),

@@ -59,12 +59,6 @@ FragGeom frag_geom(size_t ncols, int Lp) {
   g.nch = (int)((units + 1) / 2);
   return g;
 }
-__device__ __forceinline__ size_t frag_column(int c, int t, int Lp, size_t Wp, bool &ok) {
-  const size_t u = 2 * (size_t)c + (t >> 4);
-  const size_t G = u / Lp, l = u % Lp, g = 16 * G + (t & 15);
-  ok = g < Wp;
-  return g * Lp + l;
-}
 
 // block = (16-slot block, 32-column chunk c, group of 8 rows). LDS tile
 // [row][slot][column] of D8 words, rows padded to 34 words so the 16-B
@@ -253,17 +247,27 @@ __device__ __forceinline__ v4i gload16(const v4i *p) {
     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
   return r;
 }
-template <int CPOL, int DP>
-__global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const uint4 *Ff, int d, int nch,
-                                                         int nvec, int kappa, uint64_t *partial, OutPtrs dst,
-                                                         int direct, int cps, int ktiles, int nbase, size_t tile_u4,
-                                                         int qd) {
+// Several independent fold steps against the same A (nsteps > 1, StepOps): the
+// blocks of one (slot quad, split, ktile) for the different steps are blocks
+// i + 8 (t + ktiles st) of one group, so they run on the same XCD at about the
+// same time and A is fetched from HBM once for all of them (the siblings hit
+// that XCD's L2, or the MALL); each step contracts its own operand rows into its
+// own outputs. CPA / CPF: cache policies of the A and F copies.
+template <int CPA, int CPF, int DP>
+__global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, StepOps so_, int nsteps, int d, int nch,
+                                                         int nvec, int kappa, int direct, int cps, int ktiles,
+                                                         int nbase, size_t tile_u4, int qd) {
   static_assert(DP >= 3 && DP <= 5, "F buffers: DP x 32 KiB of LDS");
   __shared__ uint4 Fl[DP][32 * 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int grp = blockIdx.x / (8 * ktiles), rem = blockIdx.x - grp * 8 * ktiles;
-  const int kt = rem >> 3, bi = grp * 8 + (rem & 7);
+  const int per = 8 * ktiles * nsteps;
+  const int grp = blockIdx.x / per, rem = blockIdx.x - grp * per;
+  const int stp = rem / (8 * ktiles), rem2 = rem - stp * 8 * ktiles;
+  const int kt = rem2 >> 3, bi = grp * 8 + (rem2 & 7);
   if (bi >= nbase) return;  // uniform over the block
+  const uint4 *Ff = so_.Ff[stp];
+  uint64_t *partial = so_.partial[stp];
+  const OutPtrs &dst = so_.dst[stp];
   const int gw = bi * 4 + w;
   const int s = gw % d, js = gw / d;
   if (js >= (nch + cps - 1) / cps) return;  // uniform over the block
@@ -277,7 +281,7 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const
   auto load_a = [&](int c, v4i *dstr) {
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-      dstr[k] = gload16<CPOL>(pa + ((size_t)c * 8 + k) * 64);
+      dstr[k] = gload16<CPA>(pa + ((size_t)c * 8 + k) * 64);
     }
   };
   const int nf = __builtin_amdgcn_readfirstlane((nvec - w + 3) >> 2 < 8 ? (nvec - w + 3) >> 2 : 8);  // wave-uniform
@@ -287,7 +291,7 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const
       const int j = 4 * q + w;
       if (q < nf)
         __builtin_amdgcn_global_load_lds((const void *)(ft + (size_t)c * FV_CHUNK + j * 64 + fl_pi(j, lane)),
-                                         (lds_void *)&Fl[buf][j * 64], 16, 0, CPOL);
+                                         (lds_void *)&Fl[buf][j * 64], 16, 0, CPF);
     }
   };
   const int rh = 2 * (lane & 31) + (lane >> 5), fj = rh >> 1;
@@ -333,48 +337,15 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const
 
 // ---------------------------------------------------------------- f_0 from the operand rows
 // folding.rs:258-268 compute_f_0 when the step keeps the decomposed planes only
-// as D8 operand rows (the fused d = 1024 decomposition with f_k = null): a
-// block takes 16 slots (four slot quads, one 128-B line of every element) of
-// one 32-column chunk; thread (quad, slot, half, vector group) undoes the byte
-// transposition of its 16 columns for vectors v = vg, vg + 8, .. and
-// multiply-accumulates rho_v (.) f_v lazily; the 8 vector groups meet in LDS
-// and each output column's 16 slots go out as one 128-B run.
+// as D8 operand rows (the fused d = 1024 decomposition with f_k = null): one
+// block per fold_frag_block (frag.hpp). The packed-plane step runs the same
+// blocks inside k_fold_coeff's launch instead (fold_coeff.hip).
 __global__ void __launch_bounds__(256) k_fold_frag(const uint4 *frag, int nch, int Lp, size_t Wp, FoldRows fr,
                                                   const uint64_t *rho, int d, size_t N, uint64_t *out,
                                                   const int *run_if) {
   if (run_if && !*run_if) return;  // uniform: the coefficient-form fold produced f_0
   __shared__ uint64_t red[512 * 9];  // [output (column, slot)][vector group], rows padded to 9
-  const int tid = threadIdx.x, vg = tid & 7, h = (tid >> 3) & 1, sl = (tid >> 4) & 3, qq = tid >> 6;
-  const int ng = d >> 4, G = blockIdx.x % ng, c = blockIdx.x / ng;
-  const int s = 16 * G + 4 * qq + sl;
-  gl::CAcc acc[16];
-#pragma unroll
-  for (int j = 0; j < 16; j++) gl::cacc_zero(acc[j]);
-  for (int v = vg; v < fr.n; v += 8) {
-    const uint4 *pc = frag + fv_index(s, nch, c, fr.row[v], h);
-    uint4 u[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) u[k] = pc[4 * k];
-    const uint64_t rv = rho[(size_t)fr.rho[v] * d + s];
-    uint64_t x[16];
-    d8_untranspose16(u, x);
-#pragma unroll
-    for (int j = 0; j < 16; j++) gl::cacc_mad(acc[j], rv, x[j]);
-  }
-  // output o = column (32) x slot (16): o = (16 h + jj) 16 + 4 qq + sl
-#pragma unroll
-  for (int jj = 0; jj < 16; jj++) red[((16 * h + jj) * 16 + 4 * qq + sl) * 9 + vg] = gl::cacc_reduce(acc[jj]);
-  __syncthreads();
-#pragma unroll
-  for (int rep = 0; rep < 2; rep++) {
-    const int o = tid + 256 * rep, j = o >> 4, s16 = o & 15;
-    uint64_t t = red[o * 9];
-#pragma unroll
-    for (int g = 1; g < 8; g++) t = gl::add(t, red[o * 9 + g]);
-    bool ok;
-    const size_t col = frag_column(c, j, Lp, Wp, ok);
-    if (ok && col < N) out[col * d + 16 * G + s16] = t;
-  }
+  fold_frag_block(blockIdx.x, frag, nch, Lp, Wp, fr, rho, d, N, out, red);
 }
 
 hipError_t fold_frag(const uint4 *frag, const FragGeom &g, const FoldRows &fr, const uint64_t *rho, int d, size_t N,
@@ -468,56 +439,84 @@ hipError_t to_frag(const VecPtrs &rows, int nrows, int row0, const FragGeom &g, 
   return hipGetLastError();
 }
 
+// nsteps independent steps against one A: step s contracts the operand rows
+// Ff[s] into dst[s] (per vector), with partial[s] as its mfma_scratch_elems()
+// scratch (split partial sums, then Phi_72's virtual-slot results)
+hipError_t ajtai_mfma_steps(const uint4 *Af, size_t kappa, const FragGeom &g, int d, int nvec, int nsteps,
+                            const uint4 *const *Ff, uint64_t *const *partial, const OutPtrs *dst, hipStream_t st,
+                            hipEvent_t ev0, hipEvent_t ev1) {
+  const int dv = mfma_dim(d);
+  const int ktiles = mfma_ktiles(kappa);
+  if (kappa < 1 || ktiles > LF_MAX_KTILES || nvec < 1 || nvec > 32 || dv % 4 || nsteps < 1 ||
+      nsteps > LF_MAX_STEPS)
+    return hipErrorInvalidValue;
+  const int nsplit = mfma_nsplit(g, d), cps = mfma_cps(g, d);
+  // the contraction's own outputs: the results (X^d + 1), or Phi_72's virtual-slot sums
+  StepOps so{};
+  for (int s = 0; s < nsteps; s++) {
+    so.Ff[s] = Ff[s];
+    so.partial[s] = partial[s];
+    so.dst[s] = dst[s];
+    if (d == 24) {
+      uint64_t *virt = partial[s] + (nsplit > 1 ? (size_t)nsplit * nvec * kappa * dv : 0);
+      for (int v = 0; v < nvec; v++) so.dst[s].p[v] = virt + (size_t)v * kappa * dv;
+    }
+  }
+  if (ev0) (void)hipEventRecord(ev0, st);
+  const size_t waves = (size_t)dv * nsplit;
+  const int nbase = (int)((waves + 3) / 4);
+  const dim3 grid((unsigned)((nbase + 7) / 8 * 8 * ktiles * nsteps));
+  const size_t tile_u4 = frag_elems(g, d);
+  // F is dv nch 8 KiB per step (A is as large for kappa = 32): streamed past the
+  // caches when larger than they are; A too for one step, but not when several
+  // steps share it. A in registers 4 chunks ahead (d = 1024, W = 2^14: 6.7-6.9 ms
+  // against 7.0 for A staged through LDS and no better at 3 or 5 chunks,
+  // DESIGN.md section 7)
+  const bool big = (size_t)dv * g.nch * 8192 > STREAM_OUT_BYTES;
+  const int qd = g.qperm ? d / 4 : 0, direct = nsplit == 1 ? 1 : 0;
+#define LF_AJ(CA, CF)                                                                                        \
+  hipLaunchKernelGGL((k_ajtai_mfma_ra<CA, CF, 4>), grid, dim3(256), 0, st, Af, so, nsteps, dv, g.nch, nvec, \
+                     (int)kappa, direct, cps, ktiles, nbase, tile_u4, qd)
+  if (big && nsteps == 1)
+    LF_AJ(2, 2);
+  else if (big)
+    LF_AJ(0, 2);
+  else
+    LF_AJ(0, 0);
+#undef LF_AJ
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (ev1) (void)hipEventRecord(ev1, st);
+  for (int s = 0; s < nsteps; s++) {
+    if (nsplit > 1) {
+      e = sum_planes_to(partial[s], nsplit, kappa * (size_t)dv, nvec, so.dst[s], st);
+      if (e != hipSuccess) return e;
+    }
+    if (d == 24) {
+      const size_t n = (size_t)nvec * kappa * 8;
+      hipLaunchKernelGGL(k_phi72_interp, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, so.dst[s].p[0], nvec,
+                         kappa, dst[s]);
+      e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+  }
+  return hipSuccess;
+}
+
 // partial: mfma_scratch_elems() u64 (split partial sums, then Phi_72's virtual-slot results)
 hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, const VecPtrs &fv, int nvec,
                       bool f_ready, uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st, hipEvent_t ev0,
                       hipEvent_t ev1, const OutPtrs *dst) {
-  const int dv = mfma_dim(d);
-  const int ktiles = mfma_ktiles(kappa);
-  if (kappa < 1 || ktiles > LF_MAX_KTILES || nvec < 1 || nvec > 32 || dv % 4 || (!cm && !dst))
-    return hipErrorInvalidValue;
+  if (nvec < 1 || nvec > 32 || (!cm && !dst)) return hipErrorInvalidValue;
   OutPtrs out{};
   for (int v = 0; v < nvec; v++) out.p[v] = cm ? cm + (size_t)v * kappa * d : dst->p[v];
   if (!f_ready) {
     hipError_t e = to_frag(fv, nvec, 0, g, d, true, Ff, st);
     if (e != hipSuccess) return e;
   }
-  const int nsplit = mfma_nsplit(g, d), cps = mfma_cps(g, d);
-  // the contraction's own outputs: the results (X^d + 1), or Phi_72's virtual-slot sums
-  OutPtrs kout = out;
-  uint64_t *virt = nullptr;
-  if (d == 24) {
-    virt = partial + (nsplit > 1 ? (size_t)nsplit * nvec * kappa * dv : 0);
-    for (int v = 0; v < nvec; v++) kout.p[v] = virt + (size_t)v * kappa * dv;
-  }
-  if (ev0) (void)hipEventRecord(ev0, st);
-  const size_t waves = (size_t)dv * nsplit;
-  const int nbase = (int)((waves + 3) / 4);
-  const dim3 grid((unsigned)((nbase + 7) / 8 * 8 * ktiles));
-  const size_t tile_u4 = frag_elems(g, d);
-  // F is dv nch 8 KiB per launch (A is as large for kappa = 32): streamed past
-  // the caches when larger than they are; A in registers 4 chunks ahead
-  // (k_ajtai_mfma_ra; d = 1024, W = 2^14: 6.7-6.9 ms against 7.0 for A staged
-  // through LDS and no better at 3 or 5 chunks)
-  if ((size_t)dv * g.nch * 8192 > STREAM_OUT_BYTES)
-    hipLaunchKernelGGL((k_ajtai_mfma_ra<2, 4>), grid, dim3(256), 0, st, Af, Ff, dv, g.nch, nvec, (int)kappa, partial,
-                       kout, nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4, g.qperm ? d / 4 : 0);
-  else
-    hipLaunchKernelGGL((k_ajtai_mfma_ra<0, 4>), grid, dim3(256), 0, st, Af, Ff, dv, g.nch, nvec, (int)kappa, partial,
-                       kout, nsplit == 1 ? 1 : 0, cps, ktiles, nbase, tile_u4, g.qperm ? d / 4 : 0);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  if (ev1) (void)hipEventRecord(ev1, st);
-  if (nsplit > 1) {
-    e = sum_planes_to(partial, nsplit, kappa * (size_t)dv, nvec, kout, st);
-    if (e != hipSuccess) return e;
-  }
-  if (d == 24) {
-    const size_t n = (size_t)nvec * kappa * 8;
-    hipLaunchKernelGGL(k_phi72_interp, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, virt, nvec, kappa, out);
-    e = hipGetLastError();
-  }
-  return e;
+  const uint4 *ff[1] = {Ff};
+  uint64_t *pp[1] = {partial};
+  return ajtai_mfma_steps(Af, kappa, g, d, nvec, 1, ff, pp, &out, st, ev0, ev1);
 }
 
 }  // namespace lfk

@@ -24,13 +24,14 @@
 // (16 digits of one element) comes from 4 key bytes through a 256-entry LDS
 // table: key = 4 magnitude bits | 4 sign bits -> the quad's 4 digit bytes.
 //
-// Used only when every rho_i has coefficients in [-127, 127] (k_rho_tab checks
+// Used only when every rho_i has coefficients in [-127, 127] (k_rho_prep checks
 // on the device); otherwise the flag it raises makes these kernels return at
 // once and the NTT-form fold and Witness::from_f run instead (the same flag,
 // the other way round), with no host synchronisation.
 #include "digits.hpp"
 #include "frag.hpp"
 #include "kernels.hpp"
+#include "ntt32.hpp"
 
 namespace lfk {
 
@@ -106,32 +107,52 @@ __global__ void __launch_bounds__(256) k_pack_keys(const uint32_t *smg, size_t n
   }
 }
 
-// block i: the reversed table of rho_i (coefficient form, canonical) as bytes,
-// tab[i][u + 1024] = rho_i[-u] (-1023 <= u <= 0), -rho_i[1024 - u] (1 <= u <= 1023), else 0;
-// *bad = 1 if a coefficient is outside [-127, 127]
-__global__ void __launch_bounds__(256) k_rho_tab(const uint64_t *rc, uint8_t *tab, int *bad) {
-  const uint64_t *r = rc + (size_t)blockIdx.x * FD;
-  uint32_t *tb = reinterpret_cast<uint32_t *>(tab + (size_t)blockIdx.x * FOLD_RT);
-  for (int o4 = threadIdx.x; o4 < FOLD_RT / 4; o4 += blockDim.x) {
-    uint32_t wv = 0;
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-      const int u = 4 * o4 + b - 1024;
-      int64_t v = 0;
-      if (u <= 0 && u >= -1023)
-        v = signed_rep(r[-u]);
-      else if (u >= 1 && u <= 1023)
-        v = -signed_rep(r[1024 - u]);
-      wv |= (uint32_t)(uint8_t)(int8_t)v << (8 * b);
-    }
-    tb[o4] = wv;
-  }
+// rho (2K NTT elements) -> coefficients (rc), reversed byte tables and the range
+// flag in ONE launch of one block: half-wave i inverts rho_i on the register
+// 32 x 32 NTT (ntt32.hpp), then writes its coefficients and
+//   tab[i][u + 1024] = rho_i[-u] (-1023 <= u <= 0), -rho_i[1024 - u] (1 <= u <= 1023), else 0,
+// and the block's OR of "a coefficient is outside [-127, 127]" is stored to *bad
+// (no memset: the one block owns the flag). It replaces a device copy, a memset,
+// the 2K-element inverse transform and the table kernel (about 35 us of
+// serialised launches per step at W = 464 down to one).
+constexpr int RP_WAVES = 8;
+__global__ void __launch_bounds__(64 * RP_WAVES) k_rho_prep(const uint64_t *rho, int nw, uint64_t *rc, uint8_t *tab,
+                                                           int *bad, const uint64_t *mid_ig) {
+  __shared__ uint64_t lds_all[RP_WAVES * n32::WAVE_U64];
+  __shared__ uint64_t mid[n32::MID_U64];
+  __shared__ int any;
+  n32::stage_mid(mid, mid_ig);
+  if (threadIdx.x == 0) any = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  uint64_t *T = lds_all + wib * n32::WAVE_U64 + h * n32::HALF_U64;
   bool out = false;
-  for (int j = threadIdx.x; j < FD; j += blockDim.x) {
-    const int64_t s = signed_rep(r[j]);
-    out |= s > 127 || s < -127;
+  for (int i0 = 0; i0 < nw; i0 += 2 * RP_WAVES) {  // every wave runs every round (wave-uniform)
+    const int i = i0 + 2 * wib + h;
+    const bool ok = i < nw;
+    uint64_t v[32];
+    n32::load_row32(rho + (size_t)(ok ? i : 0) * FD + r, v);  // slot input layout v[m2] = X[r + 32 m2]
+    n32::inverse(v, mid, T, r);                                 // coefficient layout v[k] = x[r + 32 k]
+    if (ok) {
+      uint64_t *rci = rc + (size_t)i * FD + r;
+      uint8_t *ti = tab + (size_t)i * FOLD_RT;
+#pragma unroll
+      for (int k = 0; k < 32; k++) {
+        const int c = r + 32 * k;
+        const int64_t sv = signed_rep(v[k]);
+        out |= sv > 127 || sv < -127;
+        rci[32 * k] = v[k];
+        ti[1024 - c] = (uint8_t)(int8_t)sv;                      // u = -c
+        if (c > 0) ti[2048 - c] = (uint8_t)(int8_t)(-sv);        // u = 1024 - c
+      }
+      // u = -1024 and u >= 1024: zero (positions 0 and 2048 .. FOLD_RT - 1)
+      for (int o = 2048 + r; o < FOLD_RT; o += 32) ti[o] = 0;
+      if (r == 0) ti[0] = 0;
+    }
   }
-  if (out) raise(bad, 1);
+  if (out) any = 1;  // every writer stores the same value
+  __syncthreads();
+  if (threadIdx.x == 0) *bad = any;
 }
 
 // 16 bytes of a rho table at byte offset o (any alignment): 5 dwords, v_alignbyte
@@ -153,11 +174,25 @@ constexpr int FC_MAXW = 30;  // 2K <= 30
 // slots): task (tile, ks) sums only witnesses [ks nw / ks_n, (ks + 1) nw / ks_n)
 // and writes its exact int32 partials to part[ks][e][1024]; k_fold_coeff_sum
 // adds them up
+// *bad (rho not short): with fb.frag the launch folds f_0 in NTT form from the
+// operand rows instead (fold_frag_block, grid-stride; a separate gated launch of
+// its (d / 16) nch blocks would wait for CU resources behind other streams' work
+// even when it has nothing to do), else it returns and the NTT-form fold runs
 __global__ void __launch_bounds__(256, 2) k_fold_coeff(const uint32_t *keys, const uint8_t *tab_g, const int *bad,
-                                                      size_t N, int K, uint64_t *f0c, int ks_n, int32_t *part) {
+                                                      size_t N, int K, uint64_t *f0c, int ks_n, int32_t *part,
+                                                      FoldFallback fb) {
   __shared__ __attribute__((aligned(16))) uint8_t rt[FC_MAXW * FOLD_RT];
   __shared__ uint32_t lut[256];
-  if (*bad) return;  // rho not short: the NTT-form fold runs instead
+  static_assert(FC_MAXW * FOLD_RT >= 512 * 9 * 8, "fold_frag_block's LDS fits the rho tables'");
+  if (*bad) {
+    if (fb.frag) {
+      const size_t nvb = (size_t)(FD / 16) * fb.nch;
+      for (size_t vb = blockIdx.x; vb < nvb; vb += gridDim.x)
+        fold_frag_block(vb, fb.frag, fb.nch, fb.Lp, fb.Wp, fb.fr, fb.rho, FD, N, fb.f0,
+                        reinterpret_cast<uint64_t *>(rt));
+    }
+    return;
+  }
   const int nw = 2 * K, tid = threadIdx.x;
   for (int x = tid; x < nw * FOLD_RT / 16; x += blockDim.x)
     reinterpret_cast<uint4 *>(rt)[x] = reinterpret_cast<const uint4 *>(tab_g)[x];
@@ -282,22 +317,20 @@ hipError_t fold_keys(const uint32_t *smg, size_t ncol, int K, uint32_t *keys, hi
 hipError_t fold_rho_tables(const uint64_t *rho, int nw, uint64_t *rc, uint8_t *tab, int *bad,
                            const ring::NegaTables &inv, hipStream_t st) {
   if (nw < 1 || nw > FC_MAXW || !inv.mid) return hipErrorInvalidValue;
-  hipError_t e = hipMemcpyAsync(rc, rho, (size_t)nw * FD * 8, hipMemcpyDeviceToDevice, st);
-  if (e == hipSuccess) e = hipMemsetAsync(bad, 0, sizeof(int), st);
-  if (e == hipSuccess) e = transform_n32(rc, nw, false, inv, st);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_rho_tab, dim3(nw), dim3(256), 0, st, rc, tab, bad);
+  hipLaunchKernelGGL(k_rho_prep, dim3(1), dim3(64 * RP_WAVES), 0, st, rho, nw, rc, tab, bad, inv.mid);
   return hipGetLastError();
 }
 
 hipError_t fold_coeff(const uint32_t *keys, const uint8_t *tab, const int *bad, size_t N, int K, uint64_t *f0c,
-                      int ncu, hipStream_t st, int32_t *part) {
+                      int ncu, hipStream_t st, int32_t *part, const FoldFallback *fb) {
+  FoldFallback fbv{};
+  if (fb) fbv = *fb;
   if (K < 1 || 2 * K > FC_MAXW || ncu < 1) return hipErrorInvalidValue;
   if (!N) return hipSuccess;
   const int ks_n = part ? fold_coeff_splits(N, K, ncu) : 1;
   const size_t ntask = (N + 31) / 32 * ks_n, cap = 2 * (size_t)ncu;  // two blocks per CU (LDS 63 KB, 256 registers)
   hipLaunchKernelGGL(k_fold_coeff, dim3((unsigned)(ntask < cap ? ntask : cap)), dim3(256), 0, st, keys, tab, bad, N,
-                     K, f0c, ks_n, part);
+                     K, f0c, ks_n, part, fbv);
   if (ks_n > 1) {
     const size_t n = N * FD;
     hipLaunchKernelGGL(k_fold_coeff_sum, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, part, ks_n, n, bad,

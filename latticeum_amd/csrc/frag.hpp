@@ -5,6 +5,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include "gl.hpp"
+#include "kernels.hpp"
+
 namespace lfk {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -119,6 +122,59 @@ inline bool dec_streaming(size_t out_bytes, bool refold) {
 constexpr size_t FV_CHUNK = 32 * 2 * 8 * 4;
 __device__ __forceinline__ size_t fv_index(size_t s, int nch, int c, int r, int h) {
   return ((((s >> 2) * nch + c) * 32 + r) * 2 + h) * 32 + (s & 3);
+}
+
+// column of operand column t (< 32) of chunk c in the contraction order (Lp, Wp: FragGeom)
+__device__ __forceinline__ size_t frag_column(int c, int t, int Lp, size_t Wp, bool &ok) {
+  const size_t u = 2 * (size_t)c + (t >> 4);
+  const size_t G = u / Lp, l = u % Lp, g = 16 * G + (t & 15);
+  ok = g < Wp;
+  return g * Lp + l;
+}
+
+// folding.rs:258-268 compute_f_0 from the D8 operand rows (the packed / f_k-free
+// steps' fallback for a rho that is not short): virtual block vb < (d / 16) nch
+// takes 16 slots (four slot quads, one 128-B line of every element) of one
+// 32-column chunk; thread (quad, slot, half, vector group) undoes the byte
+// transposition of its 16 columns for vectors v = vg, vg + 8, .. and
+// multiply-accumulates rho_v (.) f_v lazily; the 8 vector groups meet in LDS
+// (red: 512 x 9 u64) and each output column's 16 slots go out as one 128-B run.
+// 256 threads; block-uniform (it synchronises the block).
+__device__ __forceinline__ void fold_frag_block(size_t vb, const uint4 *frag, int nch, int Lp, size_t Wp,
+                                                const FoldRows &fr, const uint64_t *rho, int d, size_t N,
+                                                uint64_t *out, uint64_t *red) {
+  const int tid = threadIdx.x, vg = tid & 7, h = (tid >> 3) & 1, sl = (tid >> 4) & 3, qq = tid >> 6;
+  const int ng = d >> 4, G = (int)(vb % ng), c = (int)(vb / ng);
+  const int s = 16 * G + 4 * qq + sl;
+  gl::CAcc acc[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) gl::cacc_zero(acc[j]);
+  for (int v = vg; v < fr.n; v += 8) {
+    const uint4 *pc = frag + fv_index(s, nch, c, fr.row[v], h);
+    uint4 u[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) u[k] = pc[4 * k];
+    const uint64_t rv = rho[(size_t)fr.rho[v] * d + s];
+    uint64_t x[16];
+    d8_untranspose16(u, x);
+#pragma unroll
+    for (int j = 0; j < 16; j++) gl::cacc_mad(acc[j], rv, x[j]);
+  }
+  // output o = column (32) x slot (16): o = (16 h + jj) 16 + 4 qq + sl
+#pragma unroll
+  for (int jj = 0; jj < 16; jj++) red[((16 * h + jj) * 16 + 4 * qq + sl) * 9 + vg] = gl::cacc_reduce(acc[jj]);
+  __syncthreads();
+#pragma unroll
+  for (int rep = 0; rep < 2; rep++) {
+    const int o = tid + 256 * rep, j = o >> 4, s16 = o & 15;
+    uint64_t t = red[o * 9];
+#pragma unroll
+    for (int g = 1; g < 8; g++) t = gl::add(t, red[o * 9 + g]);
+    bool ok;
+    const size_t col = frag_column(c, j, Lp, Wp, ok);
+    if (ok && col < N) out[col * d + 16 * G + s16] = t;
+  }
+  __syncthreads();  // red is free for the next virtual block
 }
 
 }  // namespace lfk

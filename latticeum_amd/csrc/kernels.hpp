@@ -8,6 +8,7 @@
 
 #define LF_MAX_VECS 32
 #define LF_MAX_KTILES 4
+#define LF_MAX_STEPS 4
 
 namespace lfk {
 
@@ -18,6 +19,13 @@ struct VecPtrs {
 // destinations of up to LF_MAX_VECS output vectors
 struct OutPtrs {
   uint64_t *p[LF_MAX_VECS];
+};
+
+// per-step operands and destinations of a contraction over several independent steps
+struct StepOps {
+  const uint4 *Ff[LF_MAX_STEPS];
+  uint64_t *partial[LF_MAX_STEPS];
+  OutPtrs dst[LF_MAX_STEPS];
 };
 
 hipError_t transform(uint64_t *data, size_t n, int d, bool fwd, const ring::NegaTables &tb,
@@ -93,6 +101,11 @@ hipError_t to_frag(const VecPtrs &rows, int nrows, int row0, const FragGeom &g, 
 hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, const VecPtrs &fv, int nvec,
                       bool f_ready, uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st,
                       hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, const OutPtrs *dst = nullptr);
+// nsteps (<= LF_MAX_STEPS) independent steps in one pass over A: step s's operand
+// rows Ff[s] (f_ready), scratch partial[s] (mfma_scratch_elems), results dst[s]
+hipError_t ajtai_mfma_steps(const uint4 *Af, size_t kappa, const FragGeom &g, int d, int nvec, int nsteps,
+                            const uint4 *const *Ff, uint64_t *const *partial, const OutPtrs *dst, hipStream_t st,
+                            hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 
 // d = 1024 kernels on the register-resident 32 x 32 NTT (kernels_n32.hip)
 // W below which from_w_ccs / from_f run one half-wave per (element, limb)
@@ -144,11 +157,24 @@ hipError_t fold_rho_tables(const uint64_t *rho, int nw, uint64_t *rc, uint8_t *t
 // part: fold_coeff_splits() N 1024 int32 of scratch for the witness-split partial
 // sums when there are few elements (or null: no split)
 int fold_coeff_splits(size_t N, int K, int ncu);
+// fold_coeff's fallback for a rho that is not short (*bad): f_0 (NTT form) from the
+// D8 operand rows in the same launch (the packed-plane step; frag == null: none)
+struct FoldFallback {
+  const uint4 *frag;
+  int nch, Lp;
+  size_t Wp;
+  FoldRows fr;
+  const uint64_t *rho;
+  uint64_t *f0;
+};
 hipError_t fold_coeff(const uint32_t *keys, const uint8_t *tab, const int *bad, size_t N, int K, uint64_t *f0c,
-                      int ncu, hipStream_t st, int32_t *part = nullptr);
-// Witness::from_f given f's coefficients: f = NTT(f_coeff), w_ccs = recompose(f); gate: as fold_coeff
-hipError_t from_fcoeff_n32(const uint64_t *f_coeff, size_t W, int lb, int L, uint64_t *f, uint64_t *w_ccs,
-                           const ring::NegaTables &fwd, const int *gate, hipStream_t st);
+                      int ncu, hipStream_t st, int32_t *part = nullptr, const FoldFallback *fb = nullptr);
+// Witness::from_f given f's coefficients: f = NTT(f_coeff), w_ccs = recompose(f); gate: as
+// fold_coeff. With inv, a set gate runs Witness::from_f of f instead (f_coeff = ICRT(f),
+// w_ccs = recompose(f)) in the same launch: the NTT-form fold's fallback path
+hipError_t from_fcoeff_n32(uint64_t *f_coeff, size_t W, int lb, int L, uint64_t *f, uint64_t *w_ccs,
+                           const ring::NegaTables &fwd, const int *gate, hipStream_t st,
+                           const ring::NegaTables *inv = nullptr);
 
 // d = 24: both sides of a fold step in one launch (blockIdx.z = side); frag as decompose_witness
 // *masks_written: whether the launch filled sd.masks (the wave-local kernel does)

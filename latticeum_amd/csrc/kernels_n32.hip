@@ -78,6 +78,16 @@ __global__ void __launch_bounds__(256) k_xform_n32(uint64_t *data, size_t n, con
   }
 }
 
+// the inverse transform with the inverse middle factors read from global (an
+// L1-resident 8 KiB table) instead of LDS: slot input -> coefficient layout
+__device__ __forceinline__ void inverse_gmid(uint64_t *v, const uint64_t *mid_ig, uint64_t *lds, int r) {
+  n32::cyc_dif32<true>(v);
+#pragma unroll
+  for (int i = 0; i < 32; i++) v[i] = gl::mul(v[i], mid_ig[r * 32 + i]);
+  n32::transpose_inv(v, lds, r);
+  n32::neg_gs32_inv(v);
+}
+
 // ---------------------------------------------------------------- Witness::from_w_ccs
 // LF/arith.rs:230-248: ICRT -> gadget_decompose(B = 2^lb, L) -> CRT; one half-wave per element.
 // The inverse middle factors read from global (L1-resident 8 KiB table),
@@ -99,11 +109,7 @@ __global__ void __launch_bounds__(256, 2) k_from_w_ccs_n32(const uint64_t *w_ccs
 #pragma unroll
       for (int k = 0; k < 32; k++) v[k] = g[32 * k];
     }
-    n32::cyc_dif32<true>(v);
-#pragma unroll
-    for (int i = 0; i < 32; i++) v[i] = gl::mul(v[i], mid_ig[x.r * 32 + i]);
-    n32::transpose_inv(v, x.lds, x.r);
-    n32::neg_gs32_inv(v);
+    inverse_gmid(v, mid_ig, x.lds, x.r);
     int64_t cur[32];
 #pragma unroll
     for (int k = 0; k < 32; k++) cur[k] = signed_rep(v[k]);
@@ -180,12 +186,43 @@ __global__ void __launch_bounds__(256) k_from_f_n32(const uint64_t *f, size_t W,
 // coefficients are the input, f = NTT(f_coeff) and w_ccs = recompose(f) in slot
 // form; one half-wave per group. gate: nothing to do when *gate != 0 (rho was
 // not short, the NTT-form fold and from_f ran instead)
-__global__ void __launch_bounds__(256, 2) k_from_fcoeff_n32(const uint64_t *f_coeff, size_t W, int lb, int L,
+// gate set and mid_ig given: Witness::from_f of f instead (f_coeff = ICRT(f),
+// w_ccs = recompose(f) in slot form), the NTT-form fold's fallback
+__device__ __forceinline__ void from_f_group(const uint64_t *f, size_t g, bool ok, int lb, int L, uint64_t *f_coeff,
+                                             uint64_t *w_ccs, const uint64_t *mid_ig, uint64_t *lds, int r) {
+  const uint64_t b_pow = gl::mul_pow2(1, lb);
+  const size_t gg = ok ? g : 0;
+  uint64_t acc[32];
+  for (int l = L - 1; l >= 0; l--) {
+    uint64_t v[32];
+    load_row32(f + (gg * L + l) * D + r, v);
+#pragma unroll
+    for (int k = 0; k < 32; k++) acc[k] = (l == L - 1) ? v[k] : gl::add(gl::mul(acc[k], b_pow), v[k]);
+    inverse_gmid(v, mid_ig, lds, r);
+    if (ok) {
+      uint64_t *oc = f_coeff + (g * L + l) * D + r;
+#pragma unroll
+      for (int k = 0; k < 32; k++) oc[32 * k] = v[k];
+    }
+  }
+  if (ok) {
+    uint64_t *ow = w_ccs + g * D + r;
+#pragma unroll
+    for (int k = 0; k < 32; k++) ow[32 * k] = acc[k];
+  }
+}
+__global__ void __launch_bounds__(256, 2) k_from_fcoeff_n32(uint64_t *f_coeff, size_t W, int lb, int L,
                                                         uint64_t *f, uint64_t *w_ccs, const uint64_t *mid_fg,
-                                                        const int *gate) {
-  if (gate && *gate) return;
+                                                        const int *gate, const uint64_t *mid_ig) {
+  if (gate && *gate && !mid_ig) return;
   __shared__ uint64_t lds_all[WPB * n32::WAVE_U64];
   __shared__ uint64_t mid_f[n32::MID_U64];
+  if (gate && *gate) {  // uniform over the grid
+    Half x = half_ctx(lds_all);
+    for (size_t g = x.unit; g < pair_bound(W); g += x.stride)
+      from_f_group(f, g, g < W, lb, L, f_coeff, w_ccs, mid_ig, x.lds, x.r);
+    return;
+  }
   n32::stage_mid(mid_f, mid_fg);
   __syncthreads();
   Half x = half_ctx(lds_all);
@@ -323,6 +360,84 @@ __global__ void __launch_bounds__(512) k_from_f_split(const uint64_t *f, size_t 
       uint64_t *oc = f_coeff + e * D + x.r;
 #pragma unroll
       for (int k = 0; k < 32; k++) oc[32 * k] = v[k];
+    }
+  }
+}
+
+// from f's coefficients (the coefficient-form fold's output) at small W: one
+// half-wave per (group, part), part p < L the forward transform of limb p, part
+// L the group's w_ccs = NTT(sum_l B^l f_coeff[jL + l]) -- the recomposition in
+// coefficient form, which by linearity equals k_from_fcoeff_n32's slot-form
+// Horner over the L transforms -- so a group is L + 1 independent transforms
+// instead of L in series on one half-wave
+__global__ void __launch_bounds__(512) k_from_fcoeff_split(uint64_t *f_coeff, size_t W, int lb, int L,
+                                                          uint64_t *f, uint64_t *w_ccs, const uint64_t *mid_fg,
+                                                          const int *gate, const uint64_t *mid_ig) {
+  if (gate && *gate && !mid_ig) return;
+  __shared__ uint64_t lds_all[SPLIT_WPB * n32::WAVE_U64];
+  __shared__ uint64_t mid_f[n32::MID_U64];
+  const bool fb = gate && *gate;  // uniform: Witness::from_f of f (the NTT-form fold's fallback)
+  if (!fb) n32::stage_mid(mid_f, mid_fg);
+  __syncthreads();
+  Half x = half_ctx<SPLIT_WPB>(lds_all);
+  const uint64_t b_pow = gl::mul_pow2(1, lb);  // B = 2^lb
+  const size_t units = ((W + 1) & ~(size_t)1) * (L + 1);
+  for (size_t u = x.unit; u < units; u += x.stride) {
+    // both halves of a wave take the same part of two adjacent groups
+    const size_t q = u >> 1;
+    const int p = (int)(q % (L + 1));
+    size_t j = 2 * (q / (L + 1)) + (u & 1);
+    const bool ok = j < W;
+    if (!ok) j = 0;
+    uint64_t v[32];
+    if (fb) {  // part p < L: f_coeff = ICRT(f) of limb p; part L: w_ccs = recompose(f) in slot form
+      if (p < L) {
+        load_row32(f + (j * L + p) * D + x.r, v);
+        inverse_gmid(v, mid_ig, x.lds, x.r);
+        if (ok) {
+          uint64_t *oc = f_coeff + (j * L + p) * D + x.r;
+#pragma unroll
+          for (int k = 0; k < 32; k++) oc[32 * k] = v[k];
+        }
+      } else {
+        load_row32(f + (j * L + L - 1) * D + x.r, v);
+        for (int l = L - 2; l >= 0; l--) {
+          uint64_t t[32];
+          load_row32(f + (j * L + l) * D + x.r, t);
+#pragma unroll
+          for (int k = 0; k < 32; k++) v[k] = gl::add(gl::mul(v[k], b_pow), t[k]);
+        }
+        if (ok) {
+          uint64_t *ow = w_ccs + j * D + x.r;
+#pragma unroll
+          for (int k = 0; k < 32; k++) ow[32 * k] = v[k];
+        }
+      }
+      continue;
+    }
+    if (p < L) {
+      load_row32(f_coeff + (j * L + p) * D + x.r, v);
+    } else {
+      load_row32(f_coeff + (j * L + L - 1) * D + x.r, v);
+      for (int l = L - 2; l >= 0; l--) {
+        uint64_t t[32];
+        load_row32(f_coeff + (j * L + l) * D + x.r, t);
+        if (lb == 15) {  // GoldiLocksDP B = 2^15: a shift instead of a product
+#pragma unroll
+          for (int k = 0; k < 32; k++) v[k] = gl::add_weak(gl::shl_small_weak(v[k], 15), t[k]);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 32; k++) v[k] = gl::add(gl::mul(v[k], b_pow), t[k]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 32; k++) v[k] = gl::canon(v[k]);
+    }
+    n32::forward(v, mid_f, x.lds, x.r);
+    if (ok) {
+      uint64_t *of = (p < L ? f + (j * L + p) * D : w_ccs + j * D) + x.r;
+#pragma unroll
+      for (int i = 0; i < 32; i++) of[32 * n32::brv5(i)] = v[i];
     }
   }
 }
@@ -747,12 +862,20 @@ hipError_t from_f_n32(const uint64_t *f, size_t W, int lb, int L, uint64_t *f_co
                      inv.mid, run_if);
   return hipGetLastError();
 }
-hipError_t from_fcoeff_n32(const uint64_t *f_coeff, size_t W, int lb, int L, uint64_t *f, uint64_t *w_ccs,
-                           const ring::NegaTables &fwd, const int *gate, hipStream_t st) {
+hipError_t from_fcoeff_n32(uint64_t *f_coeff, size_t W, int lb, int L, uint64_t *f, uint64_t *w_ccs,
+                           const ring::NegaTables &fwd, const int *gate, hipStream_t st,
+                           const ring::NegaTables *inv) {
   if (!W) return hipSuccess;
-  if (!fwd.mid) return hipErrorInvalidValue;
+  if (!fwd.mid || (inv && !inv->mid)) return hipErrorInvalidValue;
+  const uint64_t *mid_ig = inv ? inv->mid : nullptr;
+  if (W < SPLIT_W) {
+    const size_t units = ((W + 1) & ~(size_t)1) * (L + 1);
+    hipLaunchKernelGGL(k_from_fcoeff_split, dim3((unsigned)((units + 2 * SPLIT_WPB - 1) / (2 * SPLIT_WPB))),
+                       dim3(64 * SPLIT_WPB), 0, st, f_coeff, W, lb, L, f, w_ccs, fwd.mid, gate, mid_ig);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_from_fcoeff_n32, dim3(half_blocks(W, 4096)), dim3(256), 0, st, f_coeff, W, lb, L, f, w_ccs,
-                     fwd.mid, gate);
+                     fwd.mid, gate, mid_ig);
   return hipGetLastError();
 }
 hipError_t decompose_n32(const uint64_t *f_coeff, size_t N, int lb, int L, int K, uint64_t *f_coeff_k,

@@ -28,7 +28,8 @@ struct Tables {
 
 struct TimedLaunch {
   hipEvent_t a, b;
-  int nvec;  // Ajtai launches: vectors per launch; phases: -1 - LF_PHASE_*
+  int nvec;       // Ajtai launches: vectors per launch; phases: -1 - LF_PHASE_*
+  int count = 1;  // steps the launch covers (a batched contraction: every step's share)
 };
 
 }  // namespace
@@ -71,6 +72,7 @@ struct lf_ctx {
   bool fold_from_frag = false;
   bool frag_fallback = false;   // packed d = 1024 planes: fold_rows serve the not-short-rho fallback
   bool timing = false;
+  hipEvent_t join = nullptr;    // lf_dev_fold_step_batch: this stream's point to wait for / be waited on
   std::vector<TimedLaunch> pending;
   std::map<int, std::pair<double, long>> stats;  // nvec -> (ms, count)
 };
@@ -389,7 +391,7 @@ int drain_timing(lf_ctx *c) {
     LF_HIP(c, hipEventElapsedTime(&ms, t.a, t.b));
     auto &s = c->stats[t.nvec];  // nvec < 0: a phase
     s.first += ms;
-    s.second += 1;
+    s.second += t.count;
     (void)hipEventDestroy(t.a);
     (void)hipEventDestroy(t.b);
   }
@@ -453,9 +455,18 @@ int decompose_n4k_sides(lf_ctx *c, const Tables *t, int nside, const uint64_t *c
 
 int fold_nvec(const lf_params *pr, bool commit_f) { return (commit_f ? 1 : 0) + 2 * (pr->K - 1); }
 
+// a fused step's contraction left for lf_dev_fold_step_batch to launch with other steps'
+struct Deferred {
+  const uint4 *Ff = nullptr;
+  uint64_t *partial = nullptr;
+  lfk::OutPtrs dst{};
+  int nvec = 0;
+  bool set = false;
+};
+
 int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lbs, size_t W,
                 const lf_fold_step_bufs *b, const uint64_t *wi_f_coeff, const uint64_t *commit_f,
-                const lfk::OutPtrs &dst) {
+                const lfk::OutPtrs &dst, Deferred *defer = nullptr) {
   const int d = pr->d, L = pr->L, K = pr->K;
   const size_t N = W * (size_t)L, kappa = aj->kappa;
   const int extra = commit_f ? 1 : 0, nvec = fold_nvec(pr, commit_f != nullptr);
@@ -568,6 +579,14 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       LF_HIP(c, lfk::to_frag(vp, 1, 0, aj->geom, d, true, c->frag, c->cur));
     }
     LF_TRY(reserve(c, partial_elems(aj, nvec)));
+    if (defer) {  // the caller contracts this step together with others (one pass over A)
+      defer->Ff = c->frag;
+      defer->partial = c->scratch;
+      defer->dst = dst;
+      defer->nvec = nvec;
+      defer->set = true;
+      return LF_OK;
+    }
     hipEvent_t ea = nullptr, eb = nullptr;
     if (c->timing) {
       LF_HIP(c, hipEventCreate(&ea));
@@ -640,19 +659,32 @@ int fold_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       LF_HIP(c, lfk::fold_rho_tables(b->rho, nw, rc, tab, bad, t->inv, c->cur));
       const int ks_n = lfk::fold_coeff_splits(N, K, c->ncu);
       if (ks_n > 1) LF_TRY(grow(c, c->fpart, c->fpart_elems, (size_t)ks_n * N * 1024));
-      LF_HIP(c, lfk::fold_coeff(c->fkeys, tab, bad, N, K, b->f0_coeff, c->ncu, c->cur, ks_n > 1 ? c->fpart : nullptr));
-      if (c->frag_fallback) {  // packed planes: the fallback folds from the operand rows
-        LF_HIP(c, lfk::fold_frag(c->frag, aj->geom, c->fold_rows, b->rho, d, N, b->f0, c->cur, bad));
+      if (c->frag_fallback) {
+        // packed planes: the fallback (f_0 in NTT form from the operand rows) runs
+        // inside the same launch when the flag is set (no separate gated launch)
+        lfk::FoldFallback fb{};
+        fb.frag = c->frag;
+        fb.nch = aj->geom.nch;
+        fb.Lp = aj->geom.Lp;
+        fb.Wp = aj->geom.Wp;
+        fb.fr = c->fold_rows;
+        fb.rho = b->rho;
+        fb.f0 = b->f0;
+        LF_HIP(c, lfk::fold_coeff(c->fkeys, tab, bad, N, K, b->f0_coeff, c->ncu, c->cur,
+                                  ks_n > 1 ? c->fpart : nullptr, &fb));
       } else {
+        LF_HIP(c, lfk::fold_coeff(c->fkeys, tab, bad, N, K, b->f0_coeff, c->ncu, c->cur,
+                                  ks_n > 1 ? c->fpart : nullptr));
         lfk::VecPtrs fx{};
         for (int s = 0; s < 2; s++)
           for (int k = 0; k < K; k++) fx.p[s * K + k] = b->fk[s] + (size_t)k * N * d;
         LF_HIP(c, lfk::fold(b->rho, fx, nw, N, d, b->f0, c->cur, bad));
       }
     }
+    // f_0 and w_ccs from f_0's coefficients, or (flag set) Witness::from_f of the
+    // NTT-form f_0, in one launch
     PhaseTimer pt(c, LF_PHASE_FROM_F);
-    LF_HIP(c, lfk::from_fcoeff_n32(b->f0_coeff, W, lb, L, b->f0, b->w_ccs0, t->fwd, bad, c->cur));
-    LF_HIP(c, lfk::from_f(b->f0, N, d, lb, L, b->f0_coeff, b->w_ccs0, t->inv, c->cur, bad));
+    LF_HIP(c, lfk::from_fcoeff_n32(b->f0_coeff, W, lb, L, b->f0, b->w_ccs0, t->fwd, bad, c->cur, &t->inv));
     return LF_OK;
   }
   // Phi_72 after the wave-local decomposition: f_0 in coefficient form from its
@@ -848,6 +880,7 @@ void lf_ctx_destroy(lf_ctx *c) {
   if (c->limb) (void)hipFree(c->limb);
   if (c->tmp) (void)hipFree(c->tmp);
   if (c->sc) (void)hipFree(c->sc);
+  if (c->join) (void)hipEventDestroy(c->join);
   if (c->d_err) (void)hipFree(c->d_err);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
@@ -1328,12 +1361,12 @@ static int step_check(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t
   return LF_OK;
 }
 static int step_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t W, const lf_fold_step_bufs *b,
-                       int lb, int lbs, const lfk::OutPtrs &dst) {
+                       int lb, int lbs, const lfk::OutPtrs &dst, Deferred *defer = nullptr) {
   {
     PhaseTimer pt(c, LF_PHASE_FROM_W_CCS);
     LF_TRY(lf_dev_witness_from_w_ccs(c, pr, b->w_ccs, W, b->f_coeff, b->f));
   }
-  return fold_commit(c, aj, pr, lb, lbs, W, b, b->f_coeff, b->f, dst);
+  return fold_commit(c, aj, pr, lb, lbs, W, b, b->f_coeff, b->f, dst, defer);
 }
 
 int lf_dev_fold_lcccs(lf_ctx *c, int d, int nwit, const uint64_t *rho, const uint64_t *rho_coeff, const uint64_t *eta,
@@ -1853,6 +1886,68 @@ int lf_dev_fold_step(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t 
   LF_TRY(step_check(c, aj, pr, W, b, lb, lbs));
   LF_TRY(step_commit(c, aj, pr, W, b, lb, lbs, fold_dst(pr, b, aj->kappa * (size_t)pr->d, b->cm)));
   return fold_finish(c, aj, pr, lb, lbs, W, b, b->cm);
+}
+
+// nsteps independent steps (one context, stream and buffer set each): every
+// step's commit and decompositions on its own stream, one contraction of all of
+// them on ctx[0]'s stream (ajtai_mfma_steps: A read from HBM once), then every
+// step's fold_finish on its own stream again. Events order the streams; nothing
+// waits on the host.
+int lf_dev_fold_step_batch(lf_ctx *const *cs, int nsteps, const lf_ajtai *aj, const lf_params *pr, size_t W,
+                           const lf_fold_step_bufs *const *bs) {
+  if (!cs || !bs || !aj || nsteps < 1 || nsteps > LF_MAX_STEPS || !cs[0]) return LF_ERR_INVALID_ARG;
+  lf_ctx *c0 = cs[0];
+  for (int s = 0; s < nsteps; s++) {
+    if (!cs[s] || !bs[s]) return fail(c0, LF_ERR_INVALID_ARG, "null context or step buffers");
+    if (cs[s]->device != aj->device) return fail(c0, LF_ERR_INVALID_ARG, "every context must be on the scheme's device");
+    for (int t = 0; t < s; t++)
+      if (cs[t] == cs[s]) return fail(c0, LF_ERR_INVALID_ARG, "each step needs its own context");
+  }
+  if (nsteps == 1) return lf_dev_fold_step(c0, aj, pr, W, bs[0]);
+  DevGuard g(c0);
+  int lb = 0, lbs = 0;
+  for (int s = 0; s < nsteps; s++) LF_TRY(step_check(cs[s], aj, pr, W, bs[s], lb, lbs));
+  const size_t kd = aj->kappa * (size_t)pr->d;
+  Deferred dfr[LF_MAX_STEPS];
+  for (int s = 0; s < nsteps; s++) {
+    DevGuard gs(cs[s]);
+    LF_TRY(step_commit(cs[s], aj, pr, W, bs[s], lb, lbs, fold_dst(pr, bs[s], kd, bs[s]->cm), &dfr[s]));
+  }
+  // steps whose path has no fragments contracted on their own already
+  const uint4 *ff[LF_MAX_STEPS];
+  uint64_t *pp[LF_MAX_STEPS];
+  lfk::OutPtrs dd[LF_MAX_STEPS];
+  int n = 0, nvec = 0;
+  for (int s = 0; s < nsteps; s++) {
+    if (!dfr[s].set) continue;
+    ff[n] = dfr[s].Ff;
+    pp[n] = dfr[s].partial;
+    dd[n] = dfr[s].dst;
+    nvec = dfr[s].nvec;
+    n++;
+  }
+  for (int s = 0; s < nsteps; s++)
+    if (!cs[s]->join) LF_HIP(cs[s], hipEventCreateWithFlags(&cs[s]->join, hipEventDisableTiming));
+  if (n) {
+    for (int s = 1; s < nsteps; s++) {
+      LF_HIP(c0, hipEventRecord(cs[s]->join, cs[s]->cur));
+      LF_HIP(c0, hipStreamWaitEvent(c0->cur, cs[s]->join, 0));
+    }
+    hipEvent_t ea = nullptr, eb = nullptr;
+    if (c0->timing) {
+      LF_HIP(c0, hipEventCreate(&ea));
+      LF_HIP(c0, hipEventCreate(&eb));
+    }
+    LF_HIP(c0, lfk::ajtai_mfma_steps(aj->Af, aj->kappa, aj->geom, pr->d, nvec, n, ff, pp, dd, c0->cur, ea, eb));
+    if (c0->timing) c0->pending.push_back({ea, eb, nvec, n});
+    LF_HIP(c0, hipEventRecord(c0->join, c0->cur));
+    for (int s = 1; s < nsteps; s++) LF_HIP(cs[s], hipStreamWaitEvent(cs[s]->cur, c0->join, 0));
+  }
+  for (int s = 0; s < nsteps; s++) {
+    DevGuard gs(cs[s]);
+    LF_TRY(fold_finish(cs[s], aj, pr, lb, lbs, W, bs[s], bs[s]->cm));
+  }
+  return LF_OK;
 }
 
 size_t lf_fold_step_partial_len(const lf_ajtai *aj, const lf_params *pr) {

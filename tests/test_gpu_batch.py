@@ -1,0 +1,129 @@
+"""GPU parity of lf_dev_fold_step_batch: several independent commit+fold steps
+(each its own context, stream and buffers, one Ajtai scheme) whose commitment
+contractions share one launch -- every step's outputs equal the oracle's step,
+as lf_dev_fold_step's do (tests/test_gpu_parity.py::check_dev_fold_step)."""
+import numpy as np
+import pytest
+
+import latticeum_amd as LA
+import oracle as O
+from test_gpu_parity import check_fold_outputs, make_rho, params, rand, valid_f_coeff
+
+pytestmark = pytest.mark.gpu
+
+
+def make_step(torch, A, kappa, d, W, seed, packed, keep_fk=True, rho=None):
+    pr = params(d)
+    K, L = pr.K, pr.L
+    N = W * L
+    dev = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.int64)).cuda()
+    z = lambda n: torch.zeros(n, dtype=torch.int64, device="cuda")
+    w_ccs = rand(W * d, seed)
+    acc_fc, acc_f = valid_f_coeff(d, W, seed + 1)
+    acc_cm = O.ajtai_commit(A, kappa, N, d, acc_f)
+    if rho is None:
+        rho = make_rho(d, K, seed + 2)
+    keep = {
+        "w_ccs": dev(w_ccs), "acc_cm": dev(acc_cm), "acc_f_coeff": dev(acc_fc), "rho": dev(rho),
+        "f_coeff": z(N * d), "f": z(N * d), "cm": z(kappa * d),
+        "fk_coeff": [z(K * N * d) for _ in range(2)] if not packed else [None, None],
+        "fk": [z(K * N * d) for _ in range(2)] if keep_fk and not packed else [None, None],
+        "wk": [z(K * W * d) for _ in range(2)], "y": [z(K * kappa * d) for _ in range(2)],
+        "f0": z(N * d), "f0_coeff": z(N * d), "w_ccs0": z(W * d), "cm0": z(kappa * d),
+        "planes": [z(K * N if d == 24 else N * 256) for _ in range(2)] if packed else [None, None],
+    }
+    b = LA.LfFoldStepBufs()
+    for k, v in keep.items():
+        if isinstance(v, list):
+            for s in range(2):
+                getattr(b, k)[s] = v[s].data_ptr() if v[s] is not None else None
+        else:
+            setattr(b, k, v.data_ptr())
+    return {"keep": keep, "b": b, "w_ccs": w_ccs, "acc_cm": acc_cm, "acc_fc": acc_fc, "rho": rho}
+
+
+def expand(ctx, torch, pr, keep, N, d):
+    """the packed planes as the u64 rows the oracle returns (lf_dev_expand_planes)"""
+    K = pr.K
+    for s in range(2):
+        fck = torch.zeros(K * N * d, dtype=torch.int64, device="cuda")
+        fk = torch.zeros(K * N * d, dtype=torch.int64, device="cuda")
+        ctx.dev_expand_planes(pr, keep["planes"][s], N, fck, fk)
+        ctx.sync()
+        keep["fk_coeff"][s], keep["fk"][s] = fck, fk
+
+
+def run_batch(d, W, kappa, S, packed, rounds=1, rho_long=False):
+    import torch
+    pr = params(d)
+    N = W * pr.L
+    A = rand(kappa * N * d, 7000 + d)
+    ctxs = [LA.Context(0) for _ in range(S)]
+    try:
+        At = torch.from_numpy(A.view(np.int64)).cuda()
+        sch = LA.AjtaiCommitmentScheme(ctxs[0], device_tensor=At, kappa=kappa, ncols=N, d=d)
+        for rnd in range(rounds):
+            steps = [make_step(torch, A, kappa, d, W, 100 * rnd + 10 * i + 1, packed,
+                               rho=rand(2 * pr.K * d, 900 + i) if rho_long and i % 2 else None)
+                     for i in range(S)]
+            torch.cuda.synchronize()  # torch wrote the inputs on its own stream
+            ctxs[0].dev_fold_step_batch(ctxs[1:], sch, pr, W, [st["b"] for st in steps])
+            for c in ctxs:
+                c.sync()
+            h = lambda t: t.cpu().numpy().view(np.uint64)
+            for i, st in enumerate(steps):
+                if packed:
+                    expand(ctxs[0], torch, pr, st["keep"], N, d)
+                check_fold_outputs(h, st["keep"], A, kappa, d, pr, W, st["w_ccs"], st["acc_cm"], st["acc_fc"],
+                                   st["rho"])
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+@pytest.mark.parametrize("d,W,kappa,S", [(1024, 37, 2, 2), (1024, 130, 2, 4), (24, 17, 3, 3), (24, 70, 3, 4),
+                                         (4096, 17, 2, 2)])
+def test_fold_step_batch_matches_oracle(d, W, kappa, S):
+    run_batch(d, W, kappa, S, packed=False)
+
+
+@pytest.mark.parametrize("d,W,S", [(1024, 37, 4), (24, 70, 4)])
+def test_fold_step_batch_packed_planes(d, W, S):
+    """the bench's configuration: packed digit planes, four steps per batch, two
+    batches on the same contexts (each batch's contraction must see its own rows)"""
+    run_batch(d, W, 3 if d == 24 else 2, S, packed=True, rounds=2)
+
+
+def test_fold_step_batch_wide_kappa():
+    """kappa > 32: two 32-row A tiles x two steps per launch group"""
+    run_batch(1024, 37, 40, 2, packed=True)
+
+
+@pytest.mark.parametrize("d", [24, 1024])
+def test_fold_step_batch_rho_not_short(d):
+    """steps of one batch taking different fold paths (short and full-size rho)"""
+    run_batch(d, 17, 3 if d == 24 else 2, 2, packed=True, rho_long=True)
+
+
+def test_fold_step_batch_rejects_bad_arguments():
+    import torch
+    d, W, kappa = 1024, 2, 2
+    pr = params(d)
+    N = W * pr.L
+    A = rand(kappa * N * d, 7)
+    c = LA.Context(0)
+    try:
+        sch = LA.AjtaiCommitmentScheme(c, device_tensor=torch.from_numpy(A.view(np.int64)).cuda(), kappa=kappa,
+                                       ncols=N, d=d)
+        st = make_step(torch, A, kappa, d, W, 5, packed=True)
+        with pytest.raises(LA.LfError):  # the same context twice
+            c.dev_fold_step_batch([c], sch, pr, W, [st["b"], st["b"]])
+        others = [LA.Context(0) for _ in range(4)]
+        try:
+            with pytest.raises(LA.LfError):  # more steps than one launch takes
+                c.dev_fold_step_batch(others, sch, pr, W, [st["b"]] * 5)
+        finally:
+            for o in others:
+                o.close()
+    finally:
+        c.close()
