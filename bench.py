@@ -123,7 +123,7 @@ def kernel_names(LA, d, W, layout, keep_fk=True):
         cf = coeff_fold(d, layout, keep_fk)
         return {"decompose": "k_decompose_fused", "ajtai": mfma if layout == 1 else "k_ajtai_nega",
                 "fold": "k_fold_coeff" if cf else "k_fold_nega" if keep_fk else "k_fold_frag",
-                "from_w_ccs": "k_from_w_ccs_split" if small else "k_from_w_ccs_n32",
+                "from_w_ccs": "k_from_w_ccs_digits" if small else "k_from_w_ccs_n32",
                 "from_f": ("k_from_fcoeff_split" if small else "k_from_fcoeff_n32") if cf
                 else "k_from_f_split" if small else "k_from_f_n32",
                 "to_frag": "k_to_frag<true, false, true>"}

@@ -108,16 +108,17 @@ __global__ void __launch_bounds__(256) k_pack_keys(const uint32_t *smg, size_t n
 }
 
 // rho (2K NTT elements) -> coefficients (rc), reversed byte tables and the range
-// flag in ONE launch of one block: half-wave i inverts rho_i on the register
-// 32 x 32 NTT (ntt32.hpp), then writes its coefficients and
-//   tab[i][u + 1024] = rho_i[-u] (-1023 <= u <= 0), -rho_i[1024 - u] (1 <= u <= 1023), else 0,
-// and the block's OR of "a coefficient is outside [-127, 127]" is stored to *bad
-// (no memset: the one block owns the flag). It replaces a device copy, a memset,
-// the 2K-element inverse transform and the table kernel (about 35 us of
-// serialised launches per step at W = 464 down to one).
-constexpr int RP_WAVES = 8;
+// flag in ONE launch: half-wave i inverts rho_i on the register 32 x 32 NTT
+// (ntt32.hpp), then writes its coefficients and
+//   tab[i][u + 1024] = rho_i[-u] (-1023 <= u <= 0), -rho_i[1024 - u] (1 <= u <= 1023), else 0.
+// The blocks' ORs of "a coefficient is outside [-127, 127]" meet in sync[0]; the
+// last block to finish (ticket sync[1]) publishes it to *bad and resets both, so
+// sync is zero again for the next launch (no memset). It replaces a device copy,
+// a memset, the 2K-element inverse transform and the table kernel (about 35 us
+// of serialised launches per step at W = 464).
+constexpr int RP_WAVES = 2;  // 4 rho per block: 2K = 30 is 8 blocks of one round each
 __global__ void __launch_bounds__(64 * RP_WAVES) k_rho_prep(const uint64_t *rho, int nw, uint64_t *rc, uint8_t *tab,
-                                                           int *bad, const uint64_t *mid_ig) {
+                                                           int *bad, const uint64_t *mid_ig, int *sync) {
   __shared__ uint64_t lds_all[RP_WAVES * n32::WAVE_U64];
   __shared__ uint64_t mid[n32::MID_U64];
   __shared__ int any;
@@ -127,7 +128,8 @@ __global__ void __launch_bounds__(64 * RP_WAVES) k_rho_prep(const uint64_t *rho,
   const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   uint64_t *T = lds_all + wib * n32::WAVE_U64 + h * n32::HALF_U64;
   bool out = false;
-  for (int i0 = 0; i0 < nw; i0 += 2 * RP_WAVES) {  // every wave runs every round (wave-uniform)
+  // every wave runs every round (wave-uniform)
+  for (int i0 = 2 * RP_WAVES * blockIdx.x; i0 < nw; i0 += 2 * RP_WAVES * gridDim.x) {
     const int i = i0 + 2 * wib + h;
     const bool ok = i < nw;
     uint64_t v[32];
@@ -152,7 +154,14 @@ __global__ void __launch_bounds__(64 * RP_WAVES) k_rho_prep(const uint64_t *rho,
   }
   if (out) any = 1;  // every writer stores the same value
   __syncthreads();
-  if (threadIdx.x == 0) *bad = any;
+  if (threadIdx.x == 0) {
+    if (any) atomicOr(&sync[0], 1);
+    __threadfence();
+    if (atomicAdd(&sync[1], 1) == (int)gridDim.x - 1) {  // the last block: every block's flag is in
+      *bad = atomicExch(&sync[0], 0);
+      atomicExch(&sync[1], 0);
+    }
+  }
 }
 
 // 16 bytes of a rho table at byte offset o (any alignment): 5 dwords, v_alignbyte
@@ -315,9 +324,11 @@ hipError_t fold_keys(const uint32_t *smg, size_t ncol, int K, uint32_t *keys, hi
 }
 
 hipError_t fold_rho_tables(const uint64_t *rho, int nw, uint64_t *rc, uint8_t *tab, int *bad,
-                           const ring::NegaTables &inv, hipStream_t st) {
-  if (nw < 1 || nw > FC_MAXW || !inv.mid) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_rho_prep, dim3(1), dim3(64 * RP_WAVES), 0, st, rho, nw, rc, tab, bad, inv.mid);
+                           const ring::NegaTables &inv, int *sync, hipStream_t st) {
+  if (nw < 1 || nw > FC_MAXW || !inv.mid || !sync) return hipErrorInvalidValue;
+  const int per = 2 * RP_WAVES;
+  hipLaunchKernelGGL(k_rho_prep, dim3((nw + per - 1) / per), dim3(64 * RP_WAVES), 0, st, rho, nw, rc, tab, bad,
+                     inv.mid, sync);
   return hipGetLastError();
 }
 

@@ -110,7 +110,9 @@ hipError_t ajtai_mfma_steps(const uint4 *Af, size_t kappa, const FragGeom &g, in
 // d = 1024 kernels on the register-resident 32 x 32 NTT (kernels_n32.hip)
 // W below which from_w_ccs / from_f run one half-wave per (element, limb)
 size_t witness_split_w();
-hipError_t transform_n32(uint64_t *data, size_t n, bool fwd, const ring::NegaTables &tb, hipStream_t st);
+// data = transform(src), in place when src is null
+hipError_t transform_n32(uint64_t *data, size_t n, bool fwd, const ring::NegaTables &tb, hipStream_t st,
+                         const uint64_t *src = nullptr);
 hipError_t from_w_ccs_n32(const uint64_t *w_ccs, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *f,
                           const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err, hipStream_t st);
 hipError_t from_f_n32(const uint64_t *f, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *w_ccs,
@@ -152,8 +154,9 @@ hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K,
 // fold_coeff writes f0c = the canonical coefficients of sum_i rho_i f_i unless *bad
 constexpr int FOLD_RT = 2080;
 hipError_t fold_keys(const uint32_t *smg, size_t ncol, int K, uint32_t *keys, hipStream_t st);
+// sync: two ints, zero before the first launch; every launch leaves them zero
 hipError_t fold_rho_tables(const uint64_t *rho, int nw, uint64_t *rc, uint8_t *tab, int *bad,
-                           const ring::NegaTables &inv, hipStream_t st);
+                           const ring::NegaTables &inv, int *sync, hipStream_t st);
 // part: fold_coeff_splits() N 1024 int32 of scratch for the witness-split partial
 // sums when there are few elements (or null: no split)
 int fold_coeff_splits(size_t N, int K, int ncu);

@@ -37,8 +37,10 @@ __device__ __forceinline__ size_t pair_bound(size_t n) { return (n + 1) & ~(size
 }  // namespace
 
 // ---------------------------------------------------------------- transforms
+// dst = transform(src) (src == dst: in place)
 template <bool FWD>
-__global__ void __launch_bounds__(256) k_xform_n32(uint64_t *data, size_t n, const uint64_t *mid_g) {
+__global__ void __launch_bounds__(256) k_xform_n32(const uint64_t *src, uint64_t *data, size_t n,
+                                                  const uint64_t *mid_g) {
   __shared__ uint64_t lds_all[WPB * n32::WAVE_U64];
   __shared__ uint64_t mid[n32::MID_U64];
   n32::stage_mid(mid, mid_g);
@@ -48,7 +50,7 @@ __global__ void __launch_bounds__(256) k_xform_n32(uint64_t *data, size_t n, con
   // the wait for them does not also wait for the stores to drain
   uint64_t nx[32];
   {
-    const uint64_t *g = data + (x.unit < n ? x.unit : 0) * D + x.r;
+    const uint64_t *g = src + (x.unit < n ? x.unit : 0) * D + x.r;
 #pragma unroll
     for (int k = 0; k < 32; k++) nx[k] = g[32 * k];
   }
@@ -63,7 +65,7 @@ __global__ void __launch_bounds__(256) k_xform_n32(uint64_t *data, size_t n, con
     else
       n32::inverse(v, mid, x.lds, x.r);
     const size_t en = e + x.stride;
-    const uint64_t *gn = data + (en < n ? en : 0) * D + x.r;
+    const uint64_t *gn = src + (en < n ? en : 0) * D + x.r;
 #pragma unroll
     for (int k = 0; k < 32; k++) nx[k] = gn[32 * k];
     if (ok) {
@@ -269,48 +271,35 @@ __device__ __forceinline__ void split_unit(size_t u, int L, size_t &j, int &l) {
   l = (int)(p % L);
   j = 2 * (p / L) + (u & 1);
 }
-// from_w_ccs: each unit redoes its element's inverse transform (2 transforms per
-// unit instead of 1 + 1/L), then its own limb's digits (the carries of limbs
-// 0..l recomputed) and the forward transform
-__global__ void __launch_bounds__(512) k_from_w_ccs_split(const uint64_t *w_ccs, size_t W, int lb, int L,
-                                                         uint64_t *f_coeff, uint64_t *f, const uint64_t *mid_fg,
-                                                         const uint64_t *mid_ig, int *err) {
-  __shared__ uint64_t lds_all[SPLIT_WPB * n32::WAVE_U64];
-  __shared__ uint64_t mid_f[n32::MID_U64], mid_i[n32::MID_U64];
-  n32::stage_mid(mid_f, mid_fg);
-  n32::stage_mid(mid_i, mid_ig);
-  __syncthreads();
-  Half x = half_ctx<SPLIT_WPB>(lds_all);
-  const size_t units = ((W + 1) & ~(size_t)1) * L;
-  for (size_t u = x.unit; u < units; u += x.stride) {
-    size_t j;
-    int l;
-    split_unit(u, L, j, l);
+// from_w_ccs at small W in two launches: this one inverts each element once (one
+// half-wave per element, the inverse middle factors from global) and writes its
+// L digit rows (f_coeff, coefficient layout); then a forward transform per
+// (element, limb) row, f = NTT(f_coeff) (k_xform_n32, out of place). Against one
+// launch of (element, limb) units that each redid their element's inverse
+// transform: W + W L transforms instead of 2 W L, in two short latency chains
+__global__ void __launch_bounds__(256) k_from_w_ccs_digits(const uint64_t *w_ccs, size_t W, int lb, int L,
+                                                          uint64_t *f_coeff, const uint64_t *mid_ig, int *err) {
+  __shared__ uint64_t lds_all[WPB * n32::WAVE_U64];
+  Half x = half_ctx(lds_all);
+  for (size_t j = x.unit; j < pair_bound(W); j += x.stride) {
     const bool ok = j < W;
-    if (!ok) j = 0;
     uint64_t v[32];
-    load_row32(w_ccs + j * D + x.r, v);
-    n32::inverse(v, mid_i, x.lds, x.r);
+    load_row32(w_ccs + (ok ? j : 0) * D + x.r, v);
+    inverse_gmid(v, mid_ig, x.lds, x.r);
+    int64_t cur[32];
+#pragma unroll
+    for (int k = 0; k < 32; k++) cur[k] = signed_rep(v[k]);
+    for (int l = 0; l < L; l++) {
+      uint64_t *oc = f_coeff + ((ok ? j : 0) * L + l) * D + x.r;
+#pragma unroll
+      for (int k = 0; k < 32; k++) {
+        const uint64_t dg = from_signed(bal_digit(cur[k], lb));
+        if (ok) oc[32 * k] = dg;
+      }
+    }
     bool bad = false;
 #pragma unroll
-    for (int k = 0; k < 32; k++) {
-      int64_t cur = signed_rep(v[k]), dg = 0;
-      for (int t = 0; t <= l; t++) dg = bal_digit(cur, lb);
-      bad |= l == L - 1 && cur != 0;
-      v[k] = from_signed(dg);
-    }
-    const size_t e = j * L + l;
-    if (ok) {
-      uint64_t *oc = f_coeff + e * D + x.r;
-#pragma unroll
-      for (int k = 0; k < 32; k++) oc[32 * k] = v[k];
-    }
-    n32::forward(v, mid_f, x.lds, x.r);
-    if (ok) {
-      uint64_t *of = f + e * D + x.r;
-#pragma unroll
-      for (int i = 0; i < 32; i++) of[32 * n32::brv5(i)] = v[i];
-    }
+    for (int k = 0; k < 32; k++) bad |= cur[k] != 0;
     if (ok && bad) raise(err, 1);
   }
 }
@@ -823,11 +812,13 @@ static unsigned half_blocks(size_t units, unsigned cap) {
   return (unsigned)(b < cap ? b : cap);
 }
 
-hipError_t transform_n32(uint64_t *data, size_t n, bool fwd, const ring::NegaTables &tb, hipStream_t st) {
+hipError_t transform_n32(uint64_t *data, size_t n, bool fwd, const ring::NegaTables &tb, hipStream_t st,
+                         const uint64_t *src) {
+  if (!src) src = data;
   if (fwd)
-    hipLaunchKernelGGL(k_xform_n32<true>, dim3(half_blocks(n, 4096)), dim3(256), 0, st, data, n, tb.mid);
+    hipLaunchKernelGGL(k_xform_n32<true>, dim3(half_blocks(n, 4096)), dim3(256), 0, st, src, data, n, tb.mid);
   else
-    hipLaunchKernelGGL(k_xform_n32<false>, dim3(half_blocks(n, 4096)), dim3(256), 0, st, data, n, tb.mid);
+    hipLaunchKernelGGL(k_xform_n32<false>, dim3(half_blocks(n, 4096)), dim3(256), 0, st, src, data, n, tb.mid);
   return hipGetLastError();
 }
 // below this W the one-half-wave-per-element kernels leave CUs idle
@@ -839,11 +830,11 @@ size_t witness_split_w() { return SPLIT_W; }
 hipError_t from_w_ccs_n32(const uint64_t *w_ccs, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *f,
                           const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err, hipStream_t st) {
   if (W < SPLIT_W) {
-    const size_t units = ((W + 1) & ~(size_t)1) * L;
-    hipLaunchKernelGGL(k_from_w_ccs_split, dim3((unsigned)((units + 2 * SPLIT_WPB - 1) / (2 * SPLIT_WPB))),
-                       dim3(64 * SPLIT_WPB), 0, st, w_ccs, W, lb, L,
-                       f_coeff, f, fwd.mid, inv.mid, err);
-    return hipGetLastError();
+    hipLaunchKernelGGL(k_from_w_ccs_digits, dim3(half_blocks(W, 4096)), dim3(256), 0, st, w_ccs, W, lb, L, f_coeff,
+                       inv.mid, err);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return transform_n32(f, W * (size_t)L, true, fwd, st, f_coeff);
   }
   hipLaunchKernelGGL(k_from_w_ccs_n32, dim3(half_blocks(W, 4096)), dim3(256), 0, st, w_ccs, W, lb, L, f_coeff,
                      f, fwd.mid, inv.mid, err);

@@ -38,6 +38,7 @@ struct lf_ctx {
   int device = 0;
   hipStream_t own = nullptr, cur = nullptr;
   int *d_err = nullptr;
+  int *d_sync = nullptr;        // two ints, zero between launches (k_rho_prep's cross-block flag)
   std::string last_error;
   std::map<int, Tables> tables;
   uint64_t *scratch = nullptr;  // Ajtai split partial sums
@@ -656,7 +657,7 @@ int fold_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       PhaseTimer pt(c, LF_PHASE_FOLD);
       for (int s = 0; s < 2; s++)
         LF_HIP(c, lfk::fold_keys(c->smg_side[s], N, K, c->fkeys + (size_t)s * N * K * 64, c->cur));
-      LF_HIP(c, lfk::fold_rho_tables(b->rho, nw, rc, tab, bad, t->inv, c->cur));
+      LF_HIP(c, lfk::fold_rho_tables(b->rho, nw, rc, tab, bad, t->inv, c->d_sync, c->cur));
       const int ks_n = lfk::fold_coeff_splits(N, K, c->ncu);
       if (ks_n > 1) LF_TRY(grow(c, c->fpart, c->fpart_elems, (size_t)ks_n * N * 1024));
       if (c->frag_fallback) {
@@ -851,6 +852,8 @@ int lf_ctx_create(int device, lf_ctx **out) {
   c->cur = c->own;
   if (hipMalloc(&c->d_err, sizeof(int)) != hipSuccess) return LF_ERR_OUT_OF_MEMORY;
   if (hipMemset(c->d_err, 0, sizeof(int)) != hipSuccess) return LF_ERR_DEVICE;
+  if (hipMalloc(&c->d_sync, 2 * sizeof(int)) != hipSuccess) return LF_ERR_OUT_OF_MEMORY;
+  if (hipMemset(c->d_sync, 0, 2 * sizeof(int)) != hipSuccess) return LF_ERR_DEVICE;
   if (hipMalloc(&c->sink, 4096 * sizeof(uint64_t)) != hipSuccess) return LF_ERR_OUT_OF_MEMORY;
   if (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c->ncu < 1)
     return LF_ERR_DEVICE;
@@ -882,6 +885,7 @@ void lf_ctx_destroy(lf_ctx *c) {
   if (c->sc) (void)hipFree(c->sc);
   if (c->join) (void)hipEventDestroy(c->join);
   if (c->d_err) (void)hipFree(c->d_err);
+  if (c->d_sync) (void)hipFree(c->d_sync);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
 }
