@@ -48,6 +48,7 @@ def expand(ctx, torch, pr, keep, N, d):
     for s in range(2):
         fck = torch.zeros(K * N * d, dtype=torch.int64, device="cuda")
         fk = torch.zeros(K * N * d, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()  # torch's fills before the context's own stream writes the rows
         ctx.dev_expand_planes(pr, keep["planes"][s], N, fck, fk)
         ctx.sync()
         keep["fk_coeff"][s], keep["fk"][s] = fck, fk
