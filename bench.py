@@ -145,6 +145,19 @@ def kernel_names(LA, d, W, layout, keep_fk=True):
             "to_frag": "k_to_frag"}
 
 
+def by_base(t, kern):
+    """look a templated kernel (k_decompose_fused<true>, k_ajtai_mfma_ra<0, 2, 4>)
+    up by its plain name too: the instance the step launches most often (the
+    workload setup launches other instances once, e.g. the accumulator's commit)"""
+    bases = {}
+    for k in t:
+        base = k.split("<")[0]
+        if base != k and base not in t:
+            bases.setdefault(base, []).append(k)
+    for base, ks in bases.items():
+        t[base] = t[max(ks, key=lambda k: kern[k].get("launches", 0))]
+
+
 def load_traffic(d, W, kappa):
     """PMC-measured HBM bytes per launch (profiles/pmc_traffic.json, written by
     tools/prof_summary.py traffic from separate FETCH_SIZE / WRITE_SIZE passes of
@@ -160,13 +173,9 @@ def load_traffic(d, W, kappa):
             break
     if doc is None:
         return {}
-    t = {k: v["hbm_bytes_per_launch"] for k, v in doc.get("kernels", {}).items()}
-    # a kernel launched as one template instance (k_decompose_fused<true>,
-    # k_ajtai_mfma<2>) is looked up by its plain name too
-    for k in list(t):
-        base = k.split("<")[0]
-        if base != k and base not in t and sum(x.split("<")[0] == base for x in t) == 1:
-            t[base] = t[k]
+    kern = doc.get("kernels", {})
+    t = {k: v["hbm_bytes_per_launch"] for k, v in kern.items()}
+    by_base(t, kern)
     for dec, pack in (("k_decompose_fused", "k_pack_sm"), ("k_decompose_n4k_fused", "k_pack_sm4"),
                       ("k_decompose_n4k", "k_pack_sm4"), ("k_fold_coeff", "k_pack_keys")):
         if dec in t and pack in t:  # the decompose phase launches both
@@ -188,11 +197,9 @@ def load_sq(d, W, kappa):
             break
     if doc is None:
         return {}
-    t = {k: v.get("valu_busy") for k, v in doc.get("kernels", {}).items()}
-    for k in list(t):
-        base = k.split("<")[0]
-        if base != k and base not in t and sum(x.split("<")[0] == base for x in t) == 1:
-            t[base] = t[k]
+    kern = doc.get("kernels", {})
+    t = {k: v.get("valu_busy") for k, v in kern.items()}
+    by_base(t, kern)
     return t
 
 
