@@ -833,6 +833,11 @@ __global__ void k_commit_y0(const uint64_t *cm, uint64_t *y, size_t n, int lbs, 
 }
 
 // both sides' y_0 and the folded commitment in one pass (see kernels.hpp y0_cm0)
+// one thread per commitment slot; K <= Y0_KMAX: every plane's y and rho of a side
+// are loaded before the Horner chain, so the 2 (K - 1) loads of a thread are in
+// flight together instead of one latency per plane (W = 464: 18.6 us per launch
+// with the loads inside the chain)
+constexpr int Y0_KMAX = 16;
 __global__ void k_y0_cm0(const uint64_t *cm0s, const uint64_t *cm1s, uint64_t *y0, uint64_t *y1,
                          const uint64_t *rho, size_t n, int d, int lbs, int K, uint64_t *cm0) {
   const size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -840,15 +845,24 @@ __global__ void k_y0_cm0(const uint64_t *cm0s, const uint64_t *cm1s, uint64_t *y
   const int s = c % d;
   gl::CAcc a;
   gl::cacc_zero(a);
+#pragma unroll
   for (int side = 0; side < 2; side++) {
     uint64_t *y = side ? y1 : y0;
     const uint64_t *rs = rho + (size_t)side * K * d + s;
+    uint64_t yv[Y0_KMAX], rv[Y0_KMAX];
+#pragma unroll
+    for (int k = 1; k < Y0_KMAX; k++)
+      if (k < K) {
+        yv[k] = y[(size_t)k * n + c];
+        rv[k] = rs[(size_t)k * d];
+      }
     uint64_t acc = 0;
-    for (int k = K - 1; k >= 1; k--) {
-      const uint64_t v = y[(size_t)k * n + c];
-      gl::cacc_mad(a, rs[(size_t)k * d], v);
-      acc = gl::mul_pow2(gl::add(acc, v), lbs);
-    }
+#pragma unroll
+    for (int k = Y0_KMAX - 1; k >= 1; k--)
+      if (k < K) {
+        gl::cacc_mad(a, rv[k], yv[k]);
+        acc = gl::mul_pow2(gl::add(acc, yv[k]), lbs);
+      }
     const uint64_t v0 = gl::sub((side ? cm1s : cm0s)[c], acc);
     y[c] = v0;
     gl::cacc_mad(a, rs[0], v0);
@@ -1631,7 +1645,7 @@ hipError_t y0_cm0(const uint64_t *cm0s, const uint64_t *cm1s, uint64_t *y0, uint
                   size_t kappa, int d, int lbs, int K, uint64_t *cm0, hipStream_t st) {
   const size_t n = kappa * (size_t)d;
   if (n == 0) return hipSuccess;
-  if (K < 1) return hipErrorInvalidValue;
+  if (K < 1 || K > Y0_KMAX) return hipErrorInvalidValue;
   if (d == 24) {
     hipLaunchKernelGGL(k_y0_cm0_phi72, dim3(blocks(kappa * 8, 16)), dim3(256), 0, st, cm0s, cm1s, y0, y1, rho,
                        kappa * 8, lbs, K, cm0);
