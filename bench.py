@@ -867,7 +867,7 @@ def main():
 
     d, W, kappa = args.d, args.w, args.kappa
     wl = Workload(LA, torch, local, rank, d, W, kappa, args.streams, cu_partition=args.cu_partition,
-                  packed=None if args.packed is None else bool(args.packed), batch=bool(args.batch))
+                  packed=None if args.packed is None else bool(args.packed), batch=args.batch)
     batched, group = wl.batch, wl.group
     K, L, N = wl.pr.K, wl.pr.L, wl.N
     dt_max, (phases, roof) = measure(LA, torch, LD, pg, world, wl, args.steps, args.warmup)

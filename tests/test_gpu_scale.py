@@ -43,12 +43,14 @@ def blocks_to_groups(W, nblk_pick):
     return np.array(groups)
 
 
-def check_workload(wl, seed_w, picks, cm_rows, y_rows):
-    """bench.Workload `wl` has run one step; compare against the oracle."""
+def check_workload(wl, seed_w, picks, cm_rows, y_rows, stream=0):
+    """bench.Workload `wl` has run one step on step stream `stream`; compare it
+    against the oracle."""
     import torch
     d, W, kappa, pr = wl.d, wl.W, wl.kappa, wl.pr
     K, L, N = pr.K, pr.L, wl.N
-    keep = wl.keeps[0]
+    keep = wl.keeps[stream]
+    seed_w += 104729 * stream  # bench.Workload's per-stream w_ccs seed
     torch.cuda.synchronize()
     # commit(z) side: Witness::from_w_ccs of the whole vector
     w_ccs = O.fill_uniform(W * d, seed_w)
@@ -135,11 +137,11 @@ def check_workload(wl, seed_w, picks, cm_rows, y_rows):
     assert np.array_equal(host(keep["w_ccs0"].view(W, d)[gidx].contiguous()).ravel(), ow), "w_ccs_0"
 
 
-def run_workload(d, W, kappa):
+def run_workload(d, W, kappa, streams=1, batch=0):
     import torch
-    wl = bench.Workload(LA, torch, 0, 0, d, W, kappa, 1)
+    wl = bench.Workload(LA, torch, 0, 0, d, W, kappa, streams, batch=batch)
     try:
-        wl.run(1)
+        wl.run(streams)
         wl.sync()
         return wl
     except Exception:
@@ -157,6 +159,41 @@ def test_fold_step_bench_shape_d1024():
         nblk = (wl.W + 15) // 16
         check_workload(wl, bench.SEED_W, [0, 1, nblk // 2, nblk - 1], [0, 1, 15, 16, 30, 31],
                        [(0, 1, 0), (1, 14, 31), (1, 7, 16), (0, 14, 5)])
+    finally:
+        wl.close()
+        del wl
+        torch.cuda.empty_cache()
+
+
+def test_fold_step_bench_shape_d1024_batched():
+    """bench.py's default: two step streams whose contractions are one launch over
+    the 21.5 GB fragment matrix (A with the default cache policy, the operand rows
+    streamed: the instance only this size runs); both steps against the oracle"""
+    import torch
+    wl = run_workload(1024, 1 << 14, 32, streams=2, batch=2)
+    try:
+        assert wl.batch and wl.group == 2
+        nblk = (wl.W + 15) // 16
+        for st in range(2):
+            check_workload(wl, bench.SEED_W, [st, nblk // 3, nblk - 1 - st], [0, 17, 31],
+                           [(0, 1, 3), (1, 14, 30), (st, 9, 16)], stream=st)
+    finally:
+        wl.close()
+        del wl
+        torch.cuda.empty_cache()
+
+
+def test_fold_step_reference_ring_zkvm_shape_batched():
+    """the reference ring line of bench.py: four step streams, one contraction
+    launch for the four steps (the first and the last checked)"""
+    import torch
+    wl = run_workload(24, 19763, 32, streams=4, batch=4)
+    try:
+        assert wl.batch and wl.group == 4
+        nblk = (wl.W + 15) // 16
+        for st in (0, 3):
+            check_workload(wl, bench.SEED_W, [st, nblk // 2, nblk - 1], [0, 16, 31],
+                           [(0, 1, 0), (1, 14, 31), (st % 2, 7, 16)], stream=st)
     finally:
         wl.close()
         del wl
