@@ -907,8 +907,8 @@ def main():
                           "the reference ring Phi_72 = X^24 - X^12 + 1 at the real zkvm shape", batch=4)
         small = extra_shape(LA, torch, LD, pg, local, rank, world, 1024, 464, args.kappa, 4, 256, 16,
                             "X^1024+1 ring (byte-equivalent to the real zkvm step)", batch=2)
-        c4 = extra_shape(LA, torch, LD, pg, local, rank, world, 4096, 1024, 64, 1, 20, 3,
-                         "BASELINE configs[4]'s ring X^4096+1 with kappa=64")
+        c4 = extra_shape(LA, torch, LD, pg, local, rank, world, 4096, 1024, 64, 2, 20, 4,
+                         "BASELINE configs[4]'s ring X^4096+1 with kappa=64", batch=2)
         ops = side_ops(LA, torch, local)
         nxt = next_rows(LA, torch, local, out.get("cpu_baseline") if out is not None else None)
         if out is not None:

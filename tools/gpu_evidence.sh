@@ -48,7 +48,7 @@ timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -c 300 gpurun_out/bench_$TAG.log; [ $rc -eq 0 ] || exit $rc
 fi
 for cfg in "d1024_W16384:" "d1024_W464:--w 464 --streams 1 --steps 64 --warmup 8" "d24_W19763:--d 24 --w 19763 --streams 4 --batch 4 --steps 32 --warmup 4" \
-           "d4096_W1024:--d 4096 --w 1024 --kappa 64 --streams 1 --steps 10 --warmup 2"; do
+           "d4096_W1024:--d 4096 --w 1024 --kappa 64 --streams 2 --batch 2 --steps 10 --warmup 2"; do
   name=${cfg%%:*}; args=${cfg#*:}
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_$name -o run --output-format csv -- \
     python bench.py --no-cpu-baseline --no-small-shape $args > gpurun_out/benchprof_${TAG}_$name.log 2>&1
