@@ -48,6 +48,7 @@ SEED_A = 0x4C460004
 SEED_RHO = 0x4C460005
 SEED_ACC = 0x4C460006
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SHARDED_LIMIT_S = 240  # N > 1: the sharded fold's watchdog (main)
 
 
 def parse():
@@ -862,6 +863,11 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if os.environ.get("LATTICEUM_AMD_REHEARSE_ONE_GPU") == "1":
+        # rehearsal of the N > 1 control flow on a one-GPU box: every rank on
+        # cuda:0 and a gloo group (RCCL refuses two ranks on one GPU, so the
+        # sharded fold reports its communicator error instead of a timing)
+        local = 0
     torch.cuda.set_device(local)
     pg = LD.init(world)
 
@@ -920,10 +926,28 @@ def main():
             out["configs4_d4096_kappa64"] = c4
             out["side_ops"] = ops
     if world > 1:
+        # the sharded fold is the only part with a collective on the data path
+        # (its own RCCL communicator): a rank stuck in it must not cost the
+        # headline line, so past SHARDED_LIMIT_S rank 0 prints the line with the
+        # timeout recorded and every rank leaves (os._exit: no exec, no teardown
+        # of a communicator that is still waiting on its peers)
+        import threading
+
+        def give_up():
+            if out is not None:
+                out["sharded_fold"] = {"error": f"timeout after {SHARDED_LIMIT_S} s"}
+                print(json.dumps(out), flush=True)
+            sys.stderr.flush()
+            os._exit(0)
+
+        dog = threading.Timer(SHARDED_LIMIT_S, give_up)
+        dog.daemon = True
+        dog.start()
         try:
             sh = sharded_fold(LA, torch, LD, pg, local, rank, world, d, W, kappa, 5, 2)
         except Exception as e:  # reported, never fatal for the headline line
             sh = {"error": f"{type(e).__name__}: {e}"}
+        dog.cancel()
         if out is not None:
             out["sharded_fold"] = sh
     if out is not None:

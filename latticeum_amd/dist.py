@@ -21,6 +21,8 @@ whole exchange (split, all-reduce, join) is ordered on the context's stream.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -30,6 +32,8 @@ def init(world: int):
         return None
     if not dist.is_initialized():
         backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if os.environ.get("LATTICEUM_AMD_REHEARSE_ONE_GPU") == "1":
+            backend = "gloo"  # bench.py's one-GPU rehearsal of N ranks
         dist.init_process_group(backend=backend, init_method="env://")
     return dist.group.WORLD
 
