@@ -492,9 +492,7 @@ __global__ void __launch_bounds__(256) k_decompose_phi72_w(FusedSides sd, size_t
     }
     }
     uint64_t c[24];
-#pragma unroll
-    for (int i = 0; i < 24; i++) c[i] = pw_digit(nz, ng, i);
-    ring::phi72_crt(c);
+    ring::phi72_crt_ternary(nz, ng, c);
     // f_k rows through the tile
     if constexpr (ROWS) {
 #pragma unroll

@@ -94,6 +94,43 @@ LF_HD void phi72_crt(uint64_t *c) {
   phi72_homogenize(c);
 }
 
+// phi72_crt of a balanced ternary digit plane (digit i = sign bit i of ng,
+// magnitude bit i of nz): the first level is exact in int64, since
+// mw(b, 4) = 2^160 b == (1 - 2^32) b for b in {-1, 0, 1} (2^96 == -1,
+// 2^64 == 2^32 - 1), so its 12 butterflies are integer adds instead of a
+// shift and three canonical field operations each; the rest as phi72_crt
+LF_HD void phi72_crt_ternary(uint32_t nz, uint32_t ng, uint64_t *c) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const int64_t a = (nz >> i & 1) ? ((ng >> i & 1) ? -1 : 1) : 0;
+    const int64_t b = (nz >> (12 + i) & 1) ? ((ng >> (12 + i) & 1) ? -1 : 1) : 0;
+    const int64_t zb = b - b * ((int64_t)1 << 32);
+    const int64_t lo = a + zb, hi = a + b - zb;  // |.| <= 2^32 + 2
+    c[i] = lo < 0 ? (uint64_t)lo + gl::P : (uint64_t)lo;
+    c[12 + i] = hi < 0 ? (uint64_t)hi + gl::P : (uint64_t)hi;
+  }
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    uint64_t a = c[i], b = mw(c[6 + i], 2);
+    c[i] = gl::add(a, b);
+    c[6 + i] = gl::sub(a, b);
+    a = c[12 + i];
+    b = mw(c[18 + i], 10);
+    c[12 + i] = gl::add(a, b);
+    c[18 + i] = gl::sub(a, b);
+  }
+  constexpr int tw[4] = {1, 7, 5, 11};
+#pragma unroll
+  for (int q = 0; q < 4; q++)
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      uint64_t a = c[6 * q + i], b = mw(c[6 * q + 3 + i], tw[q]);
+      c[6 * q + i] = gl::add(a, b);
+      c[6 * q + 3 + i] = gl::sub(a, b);
+    }
+  phi72_homogenize(c);
+}
+
 // goldilocks/ntt.rs:240-319
 LF_HD void phi72_icrt(uint64_t *c) {
   phi72_dehomogenize(c);

@@ -1,11 +1,11 @@
 #!/bin/bash
-# quick check of HEAD: fold / witness GPU tests, then the headline and W = 464 bench phases
+# the reference ring: Phi72 GPU tests, then its bench line twice (4 streams, one batch of 4)
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-TAG=${1:-q}
-timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_batch.py \
-  tests/test_gpu_parity.py -k "${KSEL:-fold or batch or coeff or rho}" > gpurun_out/pytest_$TAG.log 2>&1
+TAG=${1:-d24}
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py \
+  tests/test_gpu_batch.py tests/test_gpu_scale.py -k "${KSEL:-24 or phi72 or reference}" > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?; tail -3 gpurun_out/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
 run() {  # name, args
   timeout -k 10 300 python -u bench.py --no-small-shape --no-cpu-baseline $2 > gpurun_out/bench_${TAG}_$1.log 2>&1 || return 1
@@ -13,5 +13,5 @@ run() {  # name, args
 import json; d=json.loads([l for l in open('gpurun_out/bench_${TAG}_$1.log') if l.startswith('{')][-1])
 print('$1', round(d['value'],2), round(d['ms_per_step'],3), {k: round(v['avg_launch_ms'],3) for k,v in d['phases'].items()})"
 }
-run head "--steps 8 --warmup 2" && run head2 "--steps 8 --warmup 2" && \
-run w464 "--w 464 --streams 4 --batch 2 --steps 256 --warmup 16"
+A="--d 24 --w 19763 --streams 4 --batch 4 --steps 128 --warmup 8"
+run a "$A" && run b "$A"
