@@ -22,76 +22,142 @@ const uint64_t W8_EXT_INIT[32] = LF_P2W8_EXT_INIT;
 const uint64_t W8_EXT_TERM[32] = LF_P2W8_EXT_TERM;
 const uint64_t W8_DIAG_M1[8] = LF_P2W8_DIAG_M1;
 
-uint64_t sbox7(uint64_t x) {
-  uint64_t x2 = gl::mul(x, x), x4 = gl::mul(x2, x2);
-  return gl::mul(gl::mul(x4, x2), x);
+// The permutation keeps its state weakly reduced (any u64 congruent mod p) and
+// canonicalises once at the end, as Plonky3's Goldilocks arithmetic does: a
+// product is one 64 x 64 -> 128 multiply and a branch-free fold, a sum one add
+// and carry fix-ups, with no per-operation comparison against p.
+// (x86-64: the carry fix-ups as sbb masks; compilers otherwise branch on the
+// carries, which are data-dependent and mispredict about half the time)
+inline uint64_t wadd(uint64_t a, uint64_t b) {  // any u64 in and out
+#if defined(__x86_64__)
+  uint64_t m;
+  // a + b; a carry wrapped by 2^64 == EPS: + EPS, which can carry once more (then the sum is < EPS)
+  asm("addq %[b], %[a]\n\tsbbq %[m], %[m]\n\tmovl %k[m], %k[m]\n\taddq %[m], %[a]\n\t"
+      "sbbq %[m], %[m]\n\tmovl %k[m], %k[m]\n\taddq %[m], %[a]"
+      : [a] "+r"(a), [m] "=&r"(m)
+      : [b] "r"(b)
+      : "cc");
+  return a;
+#else
+  uint64_t s, t;
+  const uint64_t c = __builtin_add_overflow(a, b, &s);
+  const uint64_t c2 = __builtin_add_overflow(s, c * gl::EPS, &t);
+  return t + c2 * gl::EPS;
+#endif
+}
+inline uint64_t wmul(uint64_t a, uint64_t b) {  // any u64 in and out
+  const unsigned __int128 t = (unsigned __int128)a * b;
+  uint64_t r = (uint64_t)t;
+  const uint64_t hi = (uint64_t)(t >> 64), h1 = hi >> 32, h0 = hi & gl::EPS, u = (h0 << 32) - h0;
+  // r - h1 (2^96 == -1): a borrow wrapped r by 2^64 == EPS and left r >= EPS, so - EPS;
+  // + h0 (2^32 - 1) (2^64 == EPS): after a carry r < 2^64 - EPS, so + EPS
+#if defined(__x86_64__)
+  uint64_t m;
+  asm("subq %[h1], %[r]\n\tsbbq %[m], %[m]\n\tmovl %k[m], %k[m]\n\tsubq %[m], %[r]\n\t"
+      "addq %[u], %[r]\n\tsbbq %[m], %[m]\n\tmovl %k[m], %k[m]\n\taddq %[m], %[r]"
+      : [r] "+r"(r), [m] "=&r"(m)
+      : [h1] "r"(h1), [u] "r"(u)
+      : "cc");
+  return r;
+#else
+  const uint64_t br = __builtin_sub_overflow(r, h1, &r);
+  r -= br * gl::EPS;
+  const uint64_t c = __builtin_add_overflow(r, u, &r);
+  return r + c * gl::EPS;
+#endif
+}
+inline uint64_t sbox7(uint64_t x) {
+  const uint64_t x2 = wmul(x, x), x4 = wmul(x2, x2);
+  return wmul(wmul(x4, x2), x);
+}
+// sums of up to 16 u64 in 128 bits, folded once: x = lo + 2^64 hi, hi < 2^32
+inline uint64_t wsum(const uint64_t *v, int n) {
+  unsigned __int128 acc = 0;
+#pragma unroll
+  for (int i = 0; i < n; i++) acc += v[i];
+  const uint64_t lo = (uint64_t)acc, hi = (uint64_t)(acc >> 64);
+  return wadd(lo, (hi << 32) - hi);
+}
+inline void mds4(uint64_t *x) {  // one 4 x 4 block of the external linear layer (as before: t + x_i + 2 x_(i+1))
+  const uint64_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3];
+  const uint64_t t = wadd(wadd(x0, x1), wadd(x2, x3));
+  x[0] = wadd(t, wadd(x0, wadd(x1, x1)));
+  x[1] = wadd(t, wadd(x1, wadd(x2, x2)));
+  x[2] = wadd(t, wadd(x2, wadd(x3, x3)));
+  x[3] = wadd(t, wadd(x3, wadd(x0, x0)));
 }
 void mds16(uint64_t *s) {
-  for (int c = 0; c < 16; c += 4) {
-    uint64_t x0 = s[c], x1 = s[c + 1], x2 = s[c + 2], x3 = s[c + 3];
-    uint64_t t = gl::add(gl::add(x0, x1), gl::add(x2, x3));
-    s[c] = gl::add(t, gl::add(x0, gl::add(x1, x1)));
-    s[c + 1] = gl::add(t, gl::add(x1, gl::add(x2, x2)));
-    s[c + 2] = gl::add(t, gl::add(x2, gl::add(x3, x3)));
-    s[c + 3] = gl::add(t, gl::add(x3, gl::add(x0, x0)));
-  }
+  #pragma unroll
+  for (int c = 0; c < 16; c += 4) mds4(s + c);
+  #pragma unroll
   for (int k = 0; k < 4; k++) {
-    uint64_t sum = gl::add(gl::add(s[k], s[4 + k]), gl::add(s[8 + k], s[12 + k]));
-    for (int j = k; j < 16; j += 4) s[j] = gl::add(s[j], sum);
+    const uint64_t col[4] = {s[k], s[4 + k], s[8 + k], s[12 + k]};
+    const uint64_t sum = wsum(col, 4);
+    #pragma unroll
+    for (int j = k; j < 16; j += 4) s[j] = wadd(s[j], sum);
   }
 }
 void permute(uint64_t *s) {
   mds16(s);
+  #pragma unroll
   for (int r = 0; r < 4; r++) {
-    for (int i = 0; i < 16; i++) s[i] = sbox7(gl::add(s[i], EXT_INIT[16 * r + i]));
+    #pragma unroll
+    for (int i = 0; i < 16; i++) s[i] = sbox7(wadd(s[i], EXT_INIT[16 * r + i]));
     mds16(s);
   }
+  #pragma unroll
   for (int r = 0; r < 22; r++) {
-    s[0] = sbox7(gl::add(s[0], INTERNAL[r]));
-    uint64_t sum = 0;
-    for (int i = 0; i < 16; i++) sum = gl::add(sum, s[i]);
-    for (int i = 0; i < 16; i++) s[i] = gl::add(gl::mul(s[i], DIAG_M1[i]), sum);
+    s[0] = sbox7(wadd(s[0], INTERNAL[r]));
+    const uint64_t sum = wsum(s, 16);
+    #pragma unroll
+    for (int i = 0; i < 16; i++) s[i] = wadd(wmul(s[i], DIAG_M1[i]), sum);
   }
+  #pragma unroll
   for (int r = 0; r < 4; r++) {
-    for (int i = 0; i < 16; i++) s[i] = sbox7(gl::add(s[i], EXT_TERM[16 * r + i]));
+    #pragma unroll
+    for (int i = 0; i < 16; i++) s[i] = sbox7(wadd(s[i], EXT_TERM[16 * r + i]));
     mds16(s);
   }
+  #pragma unroll
+  for (int i = 0; i < 16; i++) s[i] = gl::canon(s[i]);
 }
 // Poseidon2Goldilocks<8> (poseidon2.rs:31-49): the same round structure at
 // width 8 (MDSMat4 on both 4-chunks, then the column sums), the reference's
 // width-8 external constants (crypto_consts.rs:9-96) and Plonky3's
 // MATRIX_DIAG_8_GOLDILOCKS (not vendored: restated, parity unpinned)
 void mds8(uint64_t *s) {
-  for (int c = 0; c < 8; c += 4) {
-    uint64_t x0 = s[c], x1 = s[c + 1], x2 = s[c + 2], x3 = s[c + 3];
-    uint64_t t = gl::add(gl::add(x0, x1), gl::add(x2, x3));
-    s[c] = gl::add(t, gl::add(x0, gl::add(x1, x1)));
-    s[c + 1] = gl::add(t, gl::add(x1, gl::add(x2, x2)));
-    s[c + 2] = gl::add(t, gl::add(x2, gl::add(x3, x3)));
-    s[c + 3] = gl::add(t, gl::add(x3, gl::add(x0, x0)));
-  }
+  mds4(s);
+  mds4(s + 4);
+  #pragma unroll
   for (int k = 0; k < 4; k++) {
-    uint64_t sum = gl::add(s[k], s[4 + k]);
-    s[k] = gl::add(s[k], sum);
-    s[4 + k] = gl::add(s[4 + k], sum);
+    const uint64_t sum = wadd(s[k], s[4 + k]);
+    s[k] = wadd(s[k], sum);
+    s[4 + k] = wadd(s[4 + k], sum);
   }
 }
 void permute8(uint64_t *s) {
   mds8(s);
+  #pragma unroll
   for (int r = 0; r < 4; r++) {
-    for (int i = 0; i < 8; i++) s[i] = sbox7(gl::add(s[i], W8_EXT_INIT[8 * r + i]));
+    #pragma unroll
+    for (int i = 0; i < 8; i++) s[i] = sbox7(wadd(s[i], W8_EXT_INIT[8 * r + i]));
     mds8(s);
   }
+  #pragma unroll
   for (int r = 0; r < 22; r++) {
-    s[0] = sbox7(gl::add(s[0], INTERNAL[r]));
-    uint64_t sum = 0;
-    for (int i = 0; i < 8; i++) sum = gl::add(sum, s[i]);
-    for (int i = 0; i < 8; i++) s[i] = gl::add(gl::mul(s[i], W8_DIAG_M1[i]), sum);
+    s[0] = sbox7(wadd(s[0], INTERNAL[r]));
+    const uint64_t sum = wsum(s, 8);
+    #pragma unroll
+    for (int i = 0; i < 8; i++) s[i] = wadd(wmul(s[i], W8_DIAG_M1[i]), sum);
   }
+  #pragma unroll
   for (int r = 0; r < 4; r++) {
-    for (int i = 0; i < 8; i++) s[i] = sbox7(gl::add(s[i], W8_EXT_TERM[8 * r + i]));
+    #pragma unroll
+    for (int i = 0; i < 8; i++) s[i] = sbox7(wadd(s[i], W8_EXT_TERM[8 * r + i]));
     mds8(s);
   }
+  #pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = gl::canon(s[i]);
 }
 // PaddingFreeSponge<_, 8, 4, 4>::hash_iter: overwrite state[0..4), permute; a
 // partial last block is permuted; an empty input is the zero digest
