@@ -66,7 +66,7 @@ inline uint64_t wmul(uint64_t a, uint64_t b) {  // any u64 in and out
   return r + c * gl::EPS;
 #endif
 }
-inline uint64_t sbox7(uint64_t x) {
+inline uint64_t sbox7(uint64_t x) {  // x^7 = x^3 x^4: three products deep, not four
   const uint64_t x2 = wmul(x, x), x4 = wmul(x2, x2);
   return wmul(wmul(x4, x2), x);
 }
@@ -107,8 +107,11 @@ void permute(uint64_t *s) {
   }
   #pragma unroll
   for (int r = 0; r < 22; r++) {
+    // the sum of s_1 .. s_15 does not wait for the S-box of s_0 (its chain of
+    // products is the round's critical path)
+    const uint64_t rest = wsum(s + 1, 15);
     s[0] = sbox7(wadd(s[0], INTERNAL[r]));
-    const uint64_t sum = wsum(s, 16);
+    const uint64_t sum = wadd(rest, s[0]);
     #pragma unroll
     for (int i = 0; i < 16; i++) s[i] = wadd(wmul(s[i], DIAG_M1[i]), sum);
   }
@@ -145,8 +148,9 @@ void permute8(uint64_t *s) {
   }
   #pragma unroll
   for (int r = 0; r < 22; r++) {
+    const uint64_t rest = wsum(s + 1, 7);
     s[0] = sbox7(wadd(s[0], INTERNAL[r]));
-    const uint64_t sum = wsum(s, 8);
+    const uint64_t sum = wadd(rest, s[0]);
     #pragma unroll
     for (int i = 0; i < 8; i++) s[i] = wadd(wmul(s[i], W8_DIAG_M1[i]), sum);
   }
