@@ -216,7 +216,7 @@ uint64_t lf_transcript_sample(lf_transcript *t) {
 void lf_transcript_absorb_ring(lf_transcript *t, const uint64_t *e, size_t n, int d, int repr) {
   // fiat_shamir.rs:51-60: observe elem.0.0[0], the ark Montgomery limb
   for (size_t i = 0; i < n * (size_t)d; i++)
-    lf_transcript_observe(t, repr == LF_REPR_MONTGOMERY ? e[i] : gl::to_mont(e[i]));
+    lf_transcript_observe(t, repr == LF_REPR_MONTGOMERY ? e[i] : gl::canon(wmul(e[i], gl::EPS)));  // gl::to_mont
 }
 
 void lf_transcript_get_challenge(lf_transcript *t, uint64_t out3[3]) {
