@@ -165,18 +165,20 @@ def test_fold_step_bench_shape_d1024():
         torch.cuda.empty_cache()
 
 
-def test_fold_step_bench_shape_d1024_batched():
-    """bench.py's default: two step streams whose contractions are one launch over
-    the 21.5 GB fragment matrix (A with the default cache policy, the operand rows
-    streamed: the instance only this size runs); both steps against the oracle"""
+@pytest.mark.parametrize("streams", [2, 4])
+def test_fold_step_bench_shape_d1024_batched(streams):
+    """bench.py's default (4 step streams, one batch) and the pairs form: the
+    steps' contractions are one launch over the 21.5 GB fragment matrix (A with
+    the default cache policy, the operand rows streamed: the instance only this
+    size runs); every step against the oracle"""
     import torch
-    wl = run_workload(1024, 1 << 14, 32, streams=2, batch=2)
+    wl = run_workload(1024, 1 << 14, 32, streams=streams, batch=streams)
     try:
-        assert wl.batch and wl.group == 2
+        assert wl.batch and wl.group == streams
         nblk = (wl.W + 15) // 16
-        for st in range(2):
+        for st in range(streams):
             check_workload(wl, bench.SEED_W, [st, nblk // 3, nblk - 1 - st], [0, 17, 31],
-                           [(0, 1, 3), (1, 14, 30), (st, 9, 16)], stream=st)
+                           [(0, 1, 3), (1, 14, 30), (st % 2, 9 + st, 16)], stream=st)
     finally:
         wl.close()
         del wl
