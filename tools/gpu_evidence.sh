@@ -12,7 +12,7 @@ if [ -z "$SKIP_TESTS" ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
 fi
-ARGS="--steps 4 --warmup 2 --no-cpu-baseline --no-small-shape"
+ARGS="--steps 8 --warmup 4 --no-cpu-baseline --no-small-shape"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_$TAG -o run --output-format csv -- \
   python bench.py $ARGS > gpurun_out/pmc_fetch_$TAG.log 2>&1
 rc=$?; echo "fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
