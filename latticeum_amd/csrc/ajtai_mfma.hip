@@ -8,7 +8,12 @@
 //   C_s = sum_{t=0..14} 256^t * sum_{a+b=t} A_s^(a) F_s^(b)
 // and each A_s^(a) F_s^(b) is one v_mfma_i32_32x32x32_i8 per 32 columns. The 15
 // weight sums stay in i32 accumulators (<= 8 * 32 * 2^14 per chunk, so < 2^31
-// over AJ_CPS chunks) and are folded mod p once per wave.
+// over AJ_CPS chunks) and are folded mod p once per wave. A is in the D8 form
+// above; the vectors F, written every step by several producers, are in the
+// cheaper offset form (frag.hpp fenc: the bytes of x with their top bits
+// flipped, standing for x - FOFF), and the epilogue adds FOFF sum_j a_j per
+// (row, slot) back (`kr`, ajtai_rowsums; A is zero on the padding columns, so
+// their F bytes do not matter).
 //
 // Operands are stored in MFMA fragment order (lane map verified on gfx950 by
 // tools/probe/probe_mfma_i8.hip): lane l (r = l & 31, h = l >> 5) of the
@@ -106,7 +111,7 @@ __global__ void __launch_bounds__(256) k_to_frag(VecPtrs rows, int rlo, int rhi,
         phi72_evals<2>(e, ev);
     }
 #pragma unroll
-    for (int i = 0; i < TF_S; i++) tile[(r * TF_S + i) * TF_J + j] = d8(ev[i]);
+    for (int i = 0; i < TF_S; i++) tile[(r * TF_S + i) * TF_J + j] = VMAJOR ? fenc(ev[i]) : d8(ev[i]);
   } else {
     // load: 8 rows (or chunks) x 32 columns x (16 slots = 128 B = 8 pieces of 16 B)
 #pragma unroll
@@ -120,8 +125,8 @@ __global__ void __launch_bounds__(256) k_to_frag(VecPtrs rows, int rlo, int rhi,
       if (row >= rlo && row < rhi && c < nch && ok)
         v = *reinterpret_cast<const ulonglong2 *>(rows.p[row] + col * d + sb * TF_S + 2 * q);
       uint64_t *t = tile + (r * TF_S + 2 * q) * TF_J + j;
-      t[0] = d8(v.x);
-      t[TF_J] = d8(v.y);
+      t[0] = VMAJOR ? fenc(v.x) : d8(v.x);  // F rows in the offset form, A in D8
+      t[TF_J] = VMAJOR ? fenc(v.y) : d8(v.y);
     }
   }
   __syncthreads();
@@ -175,8 +180,10 @@ __device__ __forceinline__ int fl_pi(int j, int i) { return i ^ (((j & 7) << 1) 
 // |S_j| < 2^57; value = S0 + S1 2^32 + S2 2^64 + S3 2^96
 //                   == (S0 - S2 - S3) + (S1 + S2) 2^32   (2^64 == 2^32 - 1, 2^96 == -1)
 // so: the ring slot the wave's results belong to
+// kr (split 0 only): the offset form's correction FOFF sum_j a_j of the output's row and slot
 __device__ __forceinline__ void mfma_epilogue(const v16i *acc, int lane, int kt, int kappa, int nvec, int d, int so,
-                                              int js, int direct, const OutPtrs &dst, uint64_t *partial) {
+                                              int js, int direct, const OutPtrs &dst, uint64_t *partial,
+                                              const uint64_t *kr) {
   const int v = lane & 31, h = lane >> 5;
   auto fe = [](int64_t x) { return x < 0 ? (uint64_t)x + gl::P : (uint64_t)x; };  // |x| < 2^63 - p
 #pragma unroll
@@ -190,9 +197,10 @@ __device__ __forceinline__ void mfma_epilogue(const v16i *acc, int lane, int kt,
     int64_t S[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int t = 0; t < 15; t++) S[t >> 2] += (int64_t)x[t] << (8 * (t & 3));
-    const uint64_t r = gl::add(fe(S[0] - S[2] - S[3]), gl::mul_pow2(fe(S[1] + S[2]), 32));
+    uint64_t r = gl::add(fe(S[0] - S[2] - S[3]), gl::mul_pow2(fe(S[1] + S[2]), 32));
     const int row = 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * h;
     if (v < nvec && row < kappa) {
+      if (js == 0) r = gl::add(r, kr[(size_t)row * d + so]);
       if (direct)  // one column split: the result itself
         dst.p[v][(size_t)row * d + so] = r;
       else
@@ -268,7 +276,7 @@ __device__ __forceinline__ v4i gload16(const v4i *p) {
 // that XCD's L2, or the MALL); each step contracts its own operand rows into its
 // own outputs. CPA / CPF: cache policies of the A and F copies.
 template <int CPA, int CPF, int DP, bool IL>
-__global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, StepOps so_, int nsteps, int d, int nch,
+__global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const uint64_t *kr, StepOps so_, int nsteps, int d, int nch,
                                                          int nvec, int kappa, int direct, int cps, int ktiles,
                                                          int nbase, size_t tile_u4, int qd) {
   static_assert(DP >= 3 && DP <= 5, "F buffers: DP x 32 KiB of LDS");
@@ -389,7 +397,7 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, StepO
     }
   }
   const int so = qd ? (s % qd) * 4 + s / qd : s;
-  mfma_epilogue(acc, lane, kt, kappa, nvec, d, so, js, direct, dst, partial);
+  mfma_epilogue(acc, lane, kt, kappa, nvec, d, so, js, direct, dst, partial, kr);
 }
 
 // ---------------------------------------------------------------- f_0 from the operand rows
@@ -433,6 +441,39 @@ __global__ void k_phi72_interp(const uint64_t *virt, int nvec, size_t kappa, Out
   o[0] = gl::add(d0, gl::mul_pow2(d3, 40));
   o[1] = gl::add(d1, gl::mul_pow2(d4, 40));
   o[2] = d2;
+}
+
+// ---------------------------------------------------------------- row sums of A
+// tmp[i][w] = sum_j A[i][j][w] mod p (thread per (row, word), lazy 3-word sums)
+__global__ void k_rowsum(const uint64_t *A, size_t kappa, size_t ncols, int d, uint64_t *tmp) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t >= kappa * (size_t)d) return;
+  const size_t i = t / d;
+  const int w = (int)(t - i * d);
+  const uint64_t *p = A + i * ncols * d + w;
+  gl::Acc a;
+  gl::acc_zero(a);
+  for (size_t j = 0; j < ncols; j++) gl::acc_add(a, p[j * d]);
+  tmp[t] = gl::acc_reduce(a);
+}
+// kr[i][so] = FOFF * (row sum at output slot so): the ring slot itself, or for
+// Phi_72 the Toom-3 virtual slot (phi72_eval of the row sum, linear)
+__global__ void k_rowsum_kr(const uint64_t *tmp, size_t kappa, int d, int dv, uint64_t *kr) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t >= kappa * (size_t)dv) return;
+  const size_t i = t / dv;
+  const int vs = (int)(t - i * dv);
+  const uint64_t r = d == 24 ? ring::phi72_eval(tmp + i * 24, vs) : tmp[i * d + vs];
+  kr[t] = gl::mul(FOFF, r);
+}
+size_t ajtai_rowsums_elems(size_t kappa, int d) { return kappa * (size_t)mfma_dim(d); }
+hipError_t ajtai_rowsums(const uint64_t *A, size_t kappa, size_t ncols, int d, uint64_t *kr, uint64_t *tmp,
+                         hipStream_t st) {
+  const size_t n = kappa * (size_t)d, m = kappa * (size_t)mfma_dim(d);
+  hipLaunchKernelGGL(k_rowsum, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A, kappa, ncols, d, tmp);
+  hipLaunchKernelGGL(k_rowsum_kr, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, tmp, kappa, d, mfma_dim(d),
+                     kr);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- launchers
@@ -499,12 +540,12 @@ hipError_t to_frag(const VecPtrs &rows, int nrows, int row0, const FragGeom &g, 
 // nsteps independent steps against one A: step s contracts the operand rows
 // Ff[s] into dst[s] (per vector), with partial[s] as its mfma_scratch_elems()
 // scratch (split partial sums, then Phi_72's virtual-slot results)
-hipError_t ajtai_mfma_steps(const uint4 *Af, size_t kappa, const FragGeom &g, int d, int nvec, int nsteps,
+hipError_t ajtai_mfma_steps(const uint4 *Af, const uint64_t *kr, size_t kappa, const FragGeom &g, int d, int nvec, int nsteps,
                             const uint4 *const *Ff, uint64_t *const *partial, const OutPtrs *dst, hipStream_t st,
                             hipEvent_t ev0, hipEvent_t ev1) {
   const int dv = mfma_dim(d);
   const int ktiles = mfma_ktiles(kappa);
-  if (kappa < 1 || ktiles > LF_MAX_KTILES || nvec < 1 || nvec > 32 || dv % 4 || nsteps < 1 ||
+  if (!kr || kappa < 1 || ktiles > LF_MAX_KTILES || nvec < 1 || nvec > 32 || dv % 4 || nsteps < 1 ||
       nsteps > LF_MAX_STEPS)
     return hipErrorInvalidValue;
   const int nsplit = mfma_nsplit(g, d), cps = mfma_cps(g, d);
@@ -537,7 +578,7 @@ hipError_t ajtai_mfma_steps(const uint4 *Af, size_t kappa, const FragGeom &g, in
     return !(e && e[0] == '0');
   }();
 #define LF_AJ1(CA, CF, I)                                                                                        \
-  hipLaunchKernelGGL((k_ajtai_mfma_ra<CA, CF, 4, I>), grid, dim3(256), 0, st, Af, so, nsteps, dv, g.nch, nvec, \
+  hipLaunchKernelGGL((k_ajtai_mfma_ra<CA, CF, 4, I>), grid, dim3(256), 0, st, Af, kr, so, nsteps, dv, g.nch, nvec, \
                      (int)kappa, direct, cps, ktiles, nbase, tile_u4, qd)
 #define LF_AJ(CA, CF)     \
   do {                    \
@@ -577,7 +618,7 @@ hipError_t ajtai_mfma_steps(const uint4 *Af, size_t kappa, const FragGeom &g, in
 }
 
 // partial: mfma_scratch_elems() u64 (split partial sums, then Phi_72's virtual-slot results)
-hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, const VecPtrs &fv, int nvec,
+hipError_t ajtai_mfma(const uint4 *Af, const uint64_t *kr, size_t kappa, const FragGeom &g, int d, const VecPtrs &fv, int nvec,
                       bool f_ready, uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st, hipEvent_t ev0,
                       hipEvent_t ev1, const OutPtrs *dst) {
   if (nvec < 1 || nvec > 32 || (!cm && !dst)) return hipErrorInvalidValue;
@@ -589,7 +630,7 @@ hipError_t ajtai_mfma(const uint4 *Af, size_t kappa, const FragGeom &g, int d, c
   }
   const uint4 *ff[1] = {Ff};
   uint64_t *pp[1] = {partial};
-  return ajtai_mfma_steps(Af, kappa, g, d, nvec, 1, ff, pp, &out, st, ev0, ev1);
+  return ajtai_mfma_steps(Af, kr, kappa, g, d, nvec, 1, ff, pp, &out, st, ev0, ev1);
 }
 
 }  // namespace lfk

@@ -19,6 +19,15 @@ __device__ __forceinline__ uint64_t d8(uint64_t x) {
   const uint64_t t = x <= 0x7F7F7F7F7F7F7F7Full ? x : x + 0xFFFFFFFFull;
   return (t + 0x8080808080808080ull) ^ 0x8080808080808080ull;
 }
+// The vector operand (F) rows use the offset form instead: the bytes of the
+// canonical x with their top bits flipped. Read as signed bytes they are
+// b_k - 128, so they stand for the integer x - FOFF, FOFF = 0x80..80 =
+// 128 sum_k 256^k, and a contraction sum_j a_j F_j comes out short by FOFF
+// sum_j a_j: the scheme keeps FOFF * (row sums of A) per (row, slot) and the
+// contraction's epilogue adds them back (ajtai_mfma.hip, `kr`). Two VALU per
+// value against about nine for d8; A keeps the D8 form (it is built once).
+constexpr uint64_t FOFF = 0x8080808080808080ull;
+__device__ __forceinline__ uint64_t fenc(uint64_t x) { return x ^ FOFF; }
 
 // 16 D8 words (16 columns of one slot) -> 8 operand pieces: u[b] holds digit b
 // of the 16 columns, column jj in byte jj
@@ -63,9 +72,9 @@ __device__ __forceinline__ void byte_tr4(const uint32_t *w, uint32_t *o) {
     o[bb + 1] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
   }
 }
-// the inverse of d8_transpose16 followed by the D8 decode: 8 operand pieces
-// (digit b of 16 columns) -> the 16 residues (canonical)
-__device__ __forceinline__ void d8_untranspose16(const uint4 *u, uint64_t *x) {
+// the inverse of d8_transpose16 on offset-form (fenc) operand rows: 8 operand
+// pieces (byte b of 16 columns) -> the 16 residues (canonical)
+__device__ __forceinline__ void fenc_untranspose16(const uint4 *u, uint64_t *x) {
 #pragma unroll
   for (int q = 0; q < 4; q++) {
     uint32_t w[8], lo[4], hi[4];
@@ -74,11 +83,7 @@ __device__ __forceinline__ void d8_untranspose16(const uint4 *u, uint64_t *x) {
     byte_tr4(w, lo);
     byte_tr4(w + 4, hi);
 #pragma unroll
-    for (int cc = 0; cc < 4; cc++) {
-      const uint64_t wd = (uint64_t)lo[cc] | ((uint64_t)hi[cc] << 32);
-      const uint64_t t = (wd ^ 0x8080808080808080ull) - 0x8080808080808080ull;
-      x[4 * q + cc] = t <= 0x7F7F7F7F7F7F7F7Full ? t : t - 0xFFFFFFFFull;
-    }
+    for (int cc = 0; cc < 4; cc++) x[4 * q + cc] = ((uint64_t)lo[cc] | ((uint64_t)hi[cc] << 32)) ^ FOFF;
   }
 }
 
@@ -156,7 +161,7 @@ __device__ __forceinline__ void fold_frag_block(size_t vb, const uint4 *frag, in
     for (int k = 0; k < 8; k++) u[k] = pc[4 * k];
     const uint64_t rv = rho[(size_t)fr.rho[v] * d + s];
     uint64_t x[16];
-    d8_untranspose16(u, x);
+    fenc_untranspose16(u, x);
 #pragma unroll
     for (int j = 0; j < 16; j++) gl::cacc_mad(acc[j], rv, x[j]);
   }

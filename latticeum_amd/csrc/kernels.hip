@@ -352,7 +352,7 @@ __global__ void __launch_bounds__(256) k_decompose_phi72(FusedSides sd, size_t N
       __syncthreads();  // the copy-out and recompose reads of lds are done
       if (act) {
 #pragma unroll
-        for (int vs = 0; vs < 40; vs++) lds[t * srow + vs] = d8(ring::phi72_eval(c, vs));
+        for (int vs = 0; vs < 40; vs++) lds[t * srow + vs] = fenc(ring::phi72_eval(c, vs));
       }
       __syncthreads();
       for (int tk = t; tk < DEC_GROUPS / 16 * L * 40; tk += blockDim.x) {
@@ -521,7 +521,7 @@ __global__ void __launch_bounds__(256) k_decompose_phi72_w(FusedSides sd, size_t
 #pragma unroll
         for (int i = 0; i < 24; i += 4) asm volatile("" : "+v"(c[i]), "+v"(c[i + 1]), "+v"(c[i + 2]), "+v"(c[i + 3]));
 #pragma unroll
-        for (int v = 0; v < PW_VS; v++) S[(kq * PW_VS + v) * PW_ROW + gi] = d8(ring::phi72_eval(c, PW_VS * r + v));
+        for (int v = 0; v < PW_VS; v++) S[(kq * PW_VS + v) * PW_ROW + gi] = fenc(ring::phi72_eval(c, PW_VS * r + v));
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's tile writes landed
         const uint32_t *row = reinterpret_cast<const uint32_t *>(S + (kq_t * PW_VS + vl_t) * PW_ROW) + hf_t;
         uint32_t w[16];

@@ -721,7 +721,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(size_t N, int L, int
         if (frag && (kb > 0 || row_p0 >= 0)) {
           __syncthreads();  // every wave is past its transpose: S may overwrite T
 #pragma unroll
-          for (int i = 0; i < 32; i++) S[(r + 32 * n32::brv5(i)) * FD_SROW + hw] = d8(v[i]);
+          for (int i = 0; i < 32; i++) S[(r + 32 * n32::brv5(i)) * FD_SROW + hw] = fenc(v[i]);
           __syncthreads();
           const size_t u = B * L + l;  // contraction unit of these 16 columns
           const int c = (int)(u >> 1), uh = (int)(u & 1), row = kb > 0 ? row0 + kb - 1 : row_p0;

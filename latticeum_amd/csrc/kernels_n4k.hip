@@ -269,7 +269,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_n4k_fused(const uint32_t *
       if (kb > 0) {
         __syncthreads();  // every wave is past its transpose: S may overwrite T
 #pragma unroll
-        for (int i = 0; i < 32; i++) S[(r + 32 * n32::brv5(i)) * FQ_SROW + hw] = d8(v[i]);
+        for (int i = 0; i < 32; i++) S[(r + 32 * n32::brv5(i)) * FQ_SROW + hw] = fenc(v[i]);
         __syncthreads();
         const size_t u = B * L + l;  // contraction unit of these 16 columns
         const int c = (int)(u >> 1), uh = (int)(u & 1), row = sd.row0[side] + kb - 1;

@@ -94,6 +94,7 @@ struct lf_ajtai {
   int device = 0;
   const uint64_t *A = nullptr;
   uint4 *Af = nullptr;  // A in i8-MFMA fragment order, mfma_ktiles(kappa) tiles of 32 rows
+  uint64_t *kr = nullptr;  // FOFF x row sums of A per (row, output slot): lfk::ajtai_rowsums
   lfk::FragGeom geom{};  // contraction order of the fragments (ajtai_mfma.hip)
   bool owned = false;
   size_t kappa = 0, ncols = 0;
@@ -358,7 +359,7 @@ int ajtai_launch(lf_ctx *c, const lf_ajtai *aj, const uint64_t *const *vecs, int
     LF_HIP(c, hipEventCreate(&b));
   }
   if (aj->Af)
-    LF_HIP(c, lfk::ajtai_mfma(aj->Af, aj->kappa, aj->geom, aj->d, vp, nvec, false, c->frag, c->scratch, cm, c->cur,
+    LF_HIP(c, lfk::ajtai_mfma(aj->Af, aj->kr, aj->kappa, aj->geom, aj->d, vp, nvec, false, c->frag, c->scratch, cm, c->cur,
                               a, b));
   else
     LF_HIP(c, lfk::ajtai_commit(aj->A, aj->kappa, aj->ncols, aj->d, vp, nvec, c->scratch, cm, c->cur, a, b));
@@ -380,7 +381,15 @@ int ajtai_prepare(lf_ctx *c, lf_ajtai *aj) {
     for (int i = 0; i < nr; i++) rows.p[i] = aj->A + (size_t)(r0 + i) * aj->ncols * aj->d;
     LF_HIP(c, lfk::to_frag(rows, nr, 0, aj->geom, aj->d, false, aj->Af + n * t, c->cur));
   }
-  LF_HIP(c, hipStreamSynchronize(c->cur));
+  // the offset form's correction per (row, output slot)
+  uint64_t *tmp = nullptr;
+  LF_HIP(c, hipMalloc((void **)&aj->kr, lfk::ajtai_rowsums_elems(aj->kappa, aj->d) * sizeof(uint64_t)));
+  LF_HIP(c, hipMalloc((void **)&tmp, aj->kappa * (size_t)aj->d * sizeof(uint64_t)));
+  const hipError_t e = lfk::ajtai_rowsums(aj->A, aj->kappa, aj->ncols, aj->d, aj->kr, tmp, c->cur);
+  const hipError_t e2 = hipStreamSynchronize(c->cur);
+  (void)hipFree(tmp);
+  LF_HIP(c, e);
+  LF_HIP(c, e2);
   return LF_OK;
 }
 
@@ -593,7 +602,7 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       LF_HIP(c, hipEventCreate(&ea));
       LF_HIP(c, hipEventCreate(&eb));
     }
-    LF_HIP(c, lfk::ajtai_mfma(aj->Af, kappa, aj->geom, d, vp, nvec, true, c->frag, c->scratch, nullptr, c->cur, ea,
+    LF_HIP(c, lfk::ajtai_mfma(aj->Af, aj->kr, kappa, aj->geom, d, vp, nvec, true, c->frag, c->scratch, nullptr, c->cur, ea,
                               eb, &dst));
     if (c->timing) c->pending.push_back({ea, eb, nvec});
     return LF_OK;
@@ -1069,6 +1078,7 @@ void lf_ajtai_destroy(lf_ajtai *aj) {
   DevGuard g(aj->device);
   if (aj->owned) (void)hipFree((void *)aj->A);
   if (aj->Af) (void)hipFree(aj->Af);
+  if (aj->kr) (void)hipFree(aj->kr);
   delete aj;
 }
 size_t lf_ajtai_kappa(const lf_ajtai *aj) { return aj ? aj->kappa : 0; }
@@ -1942,7 +1952,7 @@ int lf_dev_fold_step_batch(lf_ctx *const *cs, int nsteps, const lf_ajtai *aj, co
       LF_HIP(c0, hipEventCreate(&ea));
       LF_HIP(c0, hipEventCreate(&eb));
     }
-    LF_HIP(c0, lfk::ajtai_mfma_steps(aj->Af, aj->kappa, aj->geom, pr->d, nvec, n, ff, pp, dd, c0->cur, ea, eb));
+    LF_HIP(c0, lfk::ajtai_mfma_steps(aj->Af, aj->kr, aj->kappa, aj->geom, pr->d, nvec, n, ff, pp, dd, c0->cur, ea, eb));
     if (c0->timing) c0->pending.push_back({ea, eb, nvec, n});
     LF_HIP(c0, hipEventRecord(c0->join, c0->cur));
     for (int s = 1; s < nsteps; s++) LF_HIP(cs[s], hipStreamWaitEvent(cs[s]->cur, c0->join, 0));
