@@ -411,6 +411,29 @@ __device__ __forceinline__ void st16(ulonglong2 *p, ulonglong2 v) {
 __device__ __forceinline__ uint64_t pw_digit(uint32_t nz, uint32_t ng, int i) {
   return (nz >> i & 1) ? ((ng >> i & 1) ? gl::P - 1 : 1) : 0;
 }
+// the coefficients of every (element, limb) of both sides as 16-bit
+// sign|magnitude (bit 15 the sign, bits 0..14 |x|) once, so the K planes'
+// waves read 48 B and take a bit instead of 24 u64 and a signed magnitude each
+// (the range check |x| < 2^K is here too); thread = (side, element, pair)
+__global__ void k_pack_sm24(FusedSides sd, size_t N, int K, int *err) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t >= (size_t)sd.nside * N * 12) return;
+  const int side = t >= N * 12;
+  const size_t q = t - side * N * 12;  // (element, pair)
+  const ulonglong2 v2 = reinterpret_cast<const ulonglong2 *>(sd.f_coeff[side])[q];
+  bool bad = false;
+  uint32_t o = 0;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int64_t v = signed_rep(h ? v2.y : v2.x);
+    const uint64_t m = v < 0 ? (uint64_t)(-v) : (uint64_t)v;
+    bad |= (m >> K) != 0;
+    o |= ((uint32_t)(m & 0x7FFF) | (v < 0 ? 0x8000u : 0u)) << (16 * h);
+  }
+  if (bad) raise(err, 1);
+  sd.smg[side][q] = o;
+}
+
 // NTM: streaming stores, bit 0 f_coeff_k, bit 1 f_k, bit 2 operand pieces; bit 3:
 // packed planes only -- no u64 f_coeff_k / f_k rows, the decomposed witnesses
 // stay as the digit masks (lf_fold_step_bufs.planes, lf_dev_expand_planes)
@@ -432,7 +455,6 @@ __global__ void __launch_bounds__(256) k_decompose_phi72_w(FusedSides sd, size_t
   const bool kok = k < K;
   const size_t W = N / L, g = 16 * G + gi;
   const bool ok = g < W;
-  const uint64_t *f_coeff = sd.f_coeff[side];
   uint64_t *f_coeff_k = sd.f_coeff_k[side], *f_k = sd.f_k[side], *w_ccs_k = sd.w_ccs_k[side];
   const int row0 = sd.row0[side];
   // this lane's operand task: plane kq_t, virtual slot PW_VS r + vl_t, digit half hf_t
@@ -449,23 +471,21 @@ __global__ void __launch_bounds__(256) k_decompose_phi72_w(FusedSides sd, size_t
     return x;
   };
   auto row_live = [&](int j) { return 16 * G + (j & 15) < W && 4 * pass + (j >> 4) < K; };
-  bool bad = false;
   uint32_t nzm[8], ngm[8];
   for (int l = L - 1; l >= 0; l--) {
     uint32_t nz = 0, ng = 0;
-    if (ok) {
-      const ulonglong2 *src = reinterpret_cast<const ulonglong2 *>(f_coeff + (g * L + l) * 24);
+    if (ok && kok) {  // plane k of the 24 packed sign|magnitude coefficients (k_pack_sm24)
+      const uint4 *src = reinterpret_cast<const uint4 *>(sd.smg[side] + (g * L + l) * 12);
 #pragma unroll
-      for (int i = 0; i < 12; i++) {
-        const ulonglong2 v2 = src[i];
+      for (int q = 0; q < 3; q++) {
+        const uint4 w4 = src[q];
+        const uint32_t w[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-          const int64_t v = signed_rep(h ? v2.y : v2.x);
-          const uint64_t m = v < 0 ? (uint64_t)(-v) : (uint64_t)v;
-          bad |= (m >> K) != 0;
-          const uint32_t bit = kok ? (uint32_t)(m >> k) & 1u : 0u;
-          nz |= bit << (2 * i + h);
-          ng |= (v < 0 ? bit : 0u) << (2 * i + h);
+        for (int i = 0; i < 8; i++) {
+          const uint32_t hw = w[i >> 1] >> (16 * (i & 1));
+          const uint32_t bit = (hw >> k) & 1u;
+          nz |= bit << (8 * q + i);
+          ng |= (bit & (hw >> 15)) << (8 * q + i);
         }
       }
     }
@@ -571,7 +591,6 @@ __global__ void __launch_bounds__(256) k_decompose_phi72_w(FusedSides sd, size_t
         reinterpret_cast<ulonglong2 *>(w_ccs_k + ((size_t)(4 * pass + (j >> 4)) * W + 16 * G + (j & 15)) * 24)[pq] = v;
     }
   }
-  if (pass == 0 && kq == 0 && ok && bad) raise(err, 1);
 }
 
 // negacyclic: one workgroup per group of L elements; coefficients of the
@@ -1498,8 +1517,14 @@ hipError_t decompose_phi72_sides(const FusedSides &sd, size_t N, int lb, int L, 
     for (int s = 0; s < sd.nside; s++)
       if (sd.row0[s] < 0 || sd.row0[s] + K - 1 > 32) return hipErrorInvalidValue;
   }
-  if (lbs == 1 && L <= 8 && (L - 1) * lb < 62) {
+  bool packed_sm = K <= 15;  // the wave kernel reads k_pack_sm24's 16-bit words
+  for (int s = 0; s < sd.nside; s++) packed_sm &= sd.smg[s] != nullptr;
+  if (lbs == 1 && L <= 8 && (L - 1) * lb < 62 && packed_sm) {
     const size_t nblk = (W + 15) / 16, waves = (size_t)sd.nside * nblk * ((K + 3) / 4);
+    {
+      const size_t np = (size_t)sd.nside * N * 12;
+      hipLaunchKernelGGL(k_pack_sm24, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, st, sd, N, K, err);
+    }
     // streaming stores for the f_coeff_k, f_k and operand rows (mask 7):
     // nothing in the step re-reads f_coeff_k or f_k (the fold reads the digit
     // masks), and the contraction's one pass over the operand rows does not gain

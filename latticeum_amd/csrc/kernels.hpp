@@ -138,7 +138,7 @@ struct FusedSides {
   int nside;
   int row_p0[2] = {-1, -1};                      // operand row of plane 0, or -1 (not written)
   uint2 *masks[2] = {nullptr, nullptr};          // d = 24, b_small = 2: digit masks [K][N] (nonzero, negative), or null
-  uint32_t *smg[2] = {nullptr, nullptr};         // d = 1024 fused: packed sign|magnitude words [N][512]
+  uint32_t *smg[2] = {nullptr, nullptr};         // packed sign|magnitude words: d = 1024 fused [N][512], d = 24 [N][12]
 };
 // f_0 = sum_v rho_v f_v with every f_v read from the D8 operand rows (k_fold_frag)
 struct FoldRows {

@@ -565,12 +565,14 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       // into the caller's planes if given, else the context's scratch
       const bool want_masks = lbs == 1;
       if (want_masks && !b->planes[0]) LF_TRY(grow(c, c->fkeys, c->fkeys_elems, 2 * 2 * (size_t)K * N));
+      LF_TRY(grow(c, c->smg, c->smg_elems, 2 * N * 12));  // the coefficients as 16-bit sign|magnitude
       for (int s = 0; s < 2; s++) {
         sd.f_coeff[s] = fc_side[s];
         sd.f_coeff_k[s] = b->fk_coeff[s];
         sd.f_k[s] = b->fk[s];
         sd.w_ccs_k[s] = b->wk[s];
         sd.row0[s] = extra + s * (K - 1);
+        sd.smg[s] = c->smg + (size_t)s * N * 12;
         if (want_masks)
           sd.masks[s] = b->planes[s] ? reinterpret_cast<uint2 *>(b->planes[s])
                                      : reinterpret_cast<uint2 *>(c->fkeys) + (size_t)s * K * N;
