@@ -275,7 +275,7 @@ __device__ __forceinline__ v4i gload16(const v4i *p) {
 // same time and A is fetched from HBM once for all of them (the siblings hit
 // that XCD's L2, or the MALL); each step contracts its own operand rows into its
 // own outputs. CPA / CPF: cache policies of the A and F copies.
-template <int CPA, int CPF, int DP, bool IL>
+template <int CPA, int CPF, int DP>
 __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const uint64_t *kr, StepOps so_, int nsteps, int d, int nch,
                                                          int nvec, int kappa, int direct, int cps, int ktiles,
                                                          int nbase, size_t tile_u4, int qd) {
@@ -342,55 +342,39 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const
       __builtin_amdgcn_s_barrier();  // every wave's F(c) landed; every wave is done reading F(c - 1)
       v4i b[8];
       const uint32_t fbase = (uint32_t)(uintptr_t)&Fl[j][0];
-      if (!IL) {
-        if (c + DP - 1 < c1) stage_f(c + DP - 1, (j + DP - 1) % DP);
+      // the copies ride between the products instead of in front of them: F(c)
+      // is read right after the barrier and each digit's 8 products wait only
+      // for that digit; F(c + DP - 1)'s pieces follow the digit groups, and
+      // A(c + DP)'s loads follow the last product reading that register
+      // (the issue order F then A is unchanged, so vm_wait_chunk still holds)
 #pragma unroll
-        for (int k = 0; k < 8; k++) asm volatile("ds_read_b128 %0, %1" : "=v"(b[k]) : "v"(fbase + 16u * fpos[k]));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        // the products read the operands only after the waits above
+      for (int k = 0; k < 8; k++) asm volatile("ds_read_b128 %0, %1" : "=v"(b[k]) : "v"(fbase + 16u * fpos[k]));
+      const bool more_f = c + DP - 1 < c1, more_a = c + DP < c1;
+      const int fb = (j + DP - 1) % DP;
 #pragma unroll
-        for (int k = 0; k < 8; k++) asm volatile("" : "+v"(b[k]), "+v"(ra[j][k]));
+      for (int kb = 0; kb < 8; kb++) {
+        lgkm_wait_digit(kb);
+        asm volatile("" : "+v"(b[kb]));
+        if (kb == 0) {
 #pragma unroll
-        for (int kb = 0; kb < 8; kb++)
+          for (int k = 0; k < 8; k++) asm volatile("" : "+v"(ra[j][k]));
+        }
+        if (kb < 7) {
 #pragma unroll
           for (int ka = 0; ka < 8; ka++)
             acc[ka + kb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ra[j][ka], b[kb], acc[ka + kb], 0, 0, 0);
-        if (c + DP < c1) load_a(c + DP, ra[j]);
-      } else {
-        // the copies ride between the products instead of in front of them: F(c)
-        // is read right after the barrier and each digit's 8 products wait only
-        // for that digit; F(c + DP - 1)'s pieces follow the digit groups, and
-        // A(c + DP)'s loads follow the last product reading that register
-        // (the issue order F then A is unchanged, so vm_wait_chunk still holds)
+          __builtin_amdgcn_sched_barrier(0);
+          if (more_f && kb < nf) stage_f_piece(c + DP - 1, fb, kb);
+          __builtin_amdgcn_sched_barrier(0);
+        } else {
+          if (more_f && nf == 8) stage_f_piece(c + DP - 1, fb, 7);
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int k = 0; k < 8; k++) asm volatile("ds_read_b128 %0, %1" : "=v"(b[k]) : "v"(fbase + 16u * fpos[k]));
-        const bool more_f = c + DP - 1 < c1, more_a = c + DP < c1;
-        const int fb = (j + DP - 1) % DP;
-#pragma unroll
-        for (int kb = 0; kb < 8; kb++) {
-          lgkm_wait_digit(kb);
-          asm volatile("" : "+v"(b[kb]));
-          if (kb == 0) {
-#pragma unroll
-            for (int k = 0; k < 8; k++) asm volatile("" : "+v"(ra[j][k]));
-          }
-          if (kb < 7) {
-#pragma unroll
-            for (int ka = 0; ka < 8; ka++)
-              acc[ka + kb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ra[j][ka], b[kb], acc[ka + kb], 0, 0, 0);
+          for (int ka = 0; ka < 8; ka++) {
+            acc[ka + 7] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ra[j][ka], b[7], acc[ka + 7], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
-            if (more_f && kb < nf) stage_f_piece(c + DP - 1, fb, kb);
+            if (more_a) ra[j][ka] = gload16<CPA>(pa + ((size_t)(c + DP) * 8 + ka) * 64);
             __builtin_amdgcn_sched_barrier(0);
-          } else {
-            if (more_f && nf == 8) stage_f_piece(c + DP - 1, fb, 7);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int ka = 0; ka < 8; ka++) {
-              acc[ka + 7] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ra[j][ka], b[7], acc[ka + 7], 0, 0, 0);
-              __builtin_amdgcn_sched_barrier(0);
-              if (more_a) ra[j][ka] = gload16<CPA>(pa + ((size_t)(c + DP) * 8 + ka) * 64);
-              __builtin_amdgcn_sched_barrier(0);
-            }
           }
         }
       }
@@ -402,7 +386,7 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const
 
 // ---------------------------------------------------------------- f_0 from the operand rows
 // folding.rs:258-268 compute_f_0 when the step keeps the decomposed planes only
-// as D8 operand rows (the fused d = 1024 decomposition with f_k = null): one
+// as operand rows (offset form; the fused d = 1024 decomposition with f_k = null): one
 // block per fold_frag_block (frag.hpp). The packed-plane step runs the same
 // blocks inside k_fold_coeff's launch instead (fold_coeff.hip).
 __global__ void __launch_bounds__(256) k_fold_frag(const uint4 *frag, int nch, int Lp, size_t Wp, FoldRows fr,
@@ -572,21 +556,9 @@ hipError_t ajtai_mfma_steps(const uint4 *Af, const uint64_t *kr, size_t kappa, c
   // DESIGN.md section 7)
   const bool big = (size_t)dv * g.nch * 8192 > STREAM_OUT_BYTES;
   const int qd = g.qperm ? d / 4 : 0, direct = nsplit == 1 ? 1 : 0;
-  // IL: the operand copies interleaved with the products (LATTICEUM_AMD_AJTAI_IL=0: in front of them)
-  static const bool il = [] {
-    const char *e = getenv("LATTICEUM_AMD_AJTAI_IL");
-    return !(e && e[0] == '0');
-  }();
-#define LF_AJ1(CA, CF, I)                                                                                        \
-  hipLaunchKernelGGL((k_ajtai_mfma_ra<CA, CF, 4, I>), grid, dim3(256), 0, st, Af, kr, so, nsteps, dv, g.nch, nvec, \
+#define LF_AJ(CA, CF)                                                                                          \
+  hipLaunchKernelGGL((k_ajtai_mfma_ra<CA, CF, 4>), grid, dim3(256), 0, st, Af, kr, so, nsteps, dv, g.nch, nvec, \
                      (int)kappa, direct, cps, ktiles, nbase, tile_u4, qd)
-#define LF_AJ(CA, CF)     \
-  do {                    \
-    if (il)               \
-      LF_AJ1(CA, CF, true);  \
-    else                  \
-      LF_AJ1(CA, CF, false); \
-  } while (0)
   // batched: A cached so the sibling blocks hit it, F streamed (A/B on one box,
   // W = 2^14, 2 steps: 49.6 steps/s against 49.2 both streamed, 49.4 both
   // cached, 48.3 A streamed / F cached)
@@ -597,7 +569,6 @@ hipError_t ajtai_mfma_steps(const uint4 *Af, const uint64_t *kr, size_t kappa, c
   else
     LF_AJ(0, 0);
 #undef LF_AJ
-#undef LF_AJ1
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (ev1) (void)hipEventRecord(ev1, st);
