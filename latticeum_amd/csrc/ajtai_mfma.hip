@@ -276,7 +276,8 @@ __device__ __forceinline__ v4i gload16(const v4i *p) {
 // that XCD's L2, or the MALL); each step contracts its own operand rows into its
 // own outputs. CPA / CPF: cache policies of the A and F copies.
 template <int CPA, int CPF, int DP>
-__global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const uint64_t *kr, StepOps so_, int nsteps, int d, int nch,
+__global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const uint64_t *kr, StepOps so_, int nsteps,
+                                                         int d, int nch,
                                                          int nvec, int kappa, int direct, int cps, int ktiles,
                                                          int nbase, size_t tile_u4, int qd) {
   static_assert(DP >= 3 && DP <= 5, "F buffers: DP x 32 KiB of LDS");
@@ -524,7 +525,8 @@ hipError_t to_frag(const VecPtrs &rows, int nrows, int row0, const FragGeom &g, 
 // nsteps independent steps against one A: step s contracts the operand rows
 // Ff[s] into dst[s] (per vector), with partial[s] as its mfma_scratch_elems()
 // scratch (split partial sums, then Phi_72's virtual-slot results)
-hipError_t ajtai_mfma_steps(const uint4 *Af, const uint64_t *kr, size_t kappa, const FragGeom &g, int d, int nvec, int nsteps,
+hipError_t ajtai_mfma_steps(const uint4 *Af, const uint64_t *kr, size_t kappa, const FragGeom &g, int d, int nvec,
+                            int nsteps,
                             const uint4 *const *Ff, uint64_t *const *partial, const OutPtrs *dst, hipStream_t st,
                             hipEvent_t ev0, hipEvent_t ev1) {
   const int dv = mfma_dim(d);
@@ -589,7 +591,8 @@ hipError_t ajtai_mfma_steps(const uint4 *Af, const uint64_t *kr, size_t kappa, c
 }
 
 // partial: mfma_scratch_elems() u64 (split partial sums, then Phi_72's virtual-slot results)
-hipError_t ajtai_mfma(const uint4 *Af, const uint64_t *kr, size_t kappa, const FragGeom &g, int d, const VecPtrs &fv, int nvec,
+hipError_t ajtai_mfma(const uint4 *Af, const uint64_t *kr, size_t kappa, const FragGeom &g, int d, const VecPtrs &fv,
+                      int nvec,
                       bool f_ready, uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st, hipEvent_t ev0,
                       hipEvent_t ev1, const OutPtrs *dst) {
   if (nvec < 1 || nvec > 32 || (!cm && !dst)) return hipErrorInvalidValue;

@@ -103,12 +103,14 @@ hipError_t to_frag(const VecPtrs &rows, int nrows, int row0, const FragGeom &g, 
 hipError_t ajtai_rowsums(const uint64_t *A, size_t kappa, size_t ncols, int d, uint64_t *kr, uint64_t *tmp,
                          hipStream_t st);
 size_t ajtai_rowsums_elems(size_t kappa, int d);  // u64 of kr; tmp needs kappa d
-hipError_t ajtai_mfma(const uint4 *Af, const uint64_t *kr, size_t kappa, const FragGeom &g, int d, const VecPtrs &fv, int nvec,
+hipError_t ajtai_mfma(const uint4 *Af, const uint64_t *kr, size_t kappa, const FragGeom &g, int d, const VecPtrs &fv,
+                      int nvec,
                       bool f_ready, uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st,
                       hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, const OutPtrs *dst = nullptr);
 // nsteps (<= LF_MAX_STEPS) independent steps in one pass over A: step s's operand
 // rows Ff[s] (f_ready), scratch partial[s] (mfma_scratch_elems), results dst[s]
-hipError_t ajtai_mfma_steps(const uint4 *Af, const uint64_t *kr, size_t kappa, const FragGeom &g, int d, int nvec, int nsteps,
+hipError_t ajtai_mfma_steps(const uint4 *Af, const uint64_t *kr, size_t kappa, const FragGeom &g, int d, int nvec,
+                            int nsteps,
                             const uint4 *const *Ff, uint64_t *const *partial, const OutPtrs *dst, hipStream_t st,
                             hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 

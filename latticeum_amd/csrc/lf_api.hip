@@ -359,7 +359,8 @@ int ajtai_launch(lf_ctx *c, const lf_ajtai *aj, const uint64_t *const *vecs, int
     LF_HIP(c, hipEventCreate(&b));
   }
   if (aj->Af)
-    LF_HIP(c, lfk::ajtai_mfma(aj->Af, aj->kr, aj->kappa, aj->geom, aj->d, vp, nvec, false, c->frag, c->scratch, cm, c->cur,
+    LF_HIP(c, lfk::ajtai_mfma(aj->Af, aj->kr, aj->kappa, aj->geom, aj->d, vp, nvec, false, c->frag, c->scratch, cm,
+                              c->cur,
                               a, b));
   else
     LF_HIP(c, lfk::ajtai_commit(aj->A, aj->kappa, aj->ncols, aj->d, vp, nvec, c->scratch, cm, c->cur, a, b));
@@ -604,7 +605,8 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       LF_HIP(c, hipEventCreate(&ea));
       LF_HIP(c, hipEventCreate(&eb));
     }
-    LF_HIP(c, lfk::ajtai_mfma(aj->Af, aj->kr, kappa, aj->geom, d, vp, nvec, true, c->frag, c->scratch, nullptr, c->cur, ea,
+    LF_HIP(c, lfk::ajtai_mfma(aj->Af, aj->kr, kappa, aj->geom, d, vp, nvec, true, c->frag, c->scratch, nullptr, c->cur,
+                              ea,
                               eb, &dst));
     if (c->timing) c->pending.push_back({ea, eb, nvec});
     return LF_OK;
