@@ -56,6 +56,24 @@ def test_hash_iter_matches_oracle(n):
     assert np.array_equal(LA.hash_iter(vals), O.p2_hash_iter(vals))
 
 
+@pytest.mark.parametrize("fill", ["p-1", "max", "edges"])
+def test_hash_iter_edge_values_match_oracle(fill):
+    """the host permutation keeps its state weakly reduced (transcript.cpp):
+    inputs at the top of the field and of u64 (canonicalised on absorption), and
+    a mix of 0, 1, p-1, 2^63 and 2^64-1, against the oracle's canonical one"""
+    P = (1 << 64) - (1 << 32) + 1
+    n = 12 * 40 + 5
+    if fill == "p-1":
+        vals = np.full(n, P - 1, np.uint64)
+    elif fill == "max":
+        vals = np.full(n, (1 << 64) - 1, np.uint64)
+    else:
+        edge = np.array([0, 1, P - 1, P - 2, 1 << 63, (1 << 64) - 1, (1 << 32) - 1, 1 << 32], np.uint64)
+        vals = edge[np.arange(n) % len(edge)]
+    canon = np.where(vals >= np.uint64(P), vals - np.uint64(P), vals).astype(np.uint64)
+    assert np.array_equal(LA.hash_iter(vals), O.p2_hash_iter(canon))
+
+
 def test_transcript_matches_oracle():
     t = LA.Poseidon2Transcript()
     o = O.new_transcript()
