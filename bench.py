@@ -82,7 +82,7 @@ def algorithmic_bytes(d, W, kappa, L=5, K=15):
     launch of each step phase: its inputs read once and its outputs written
     once in the Witness forms the reference materialises (u64 per residue).
     `operand` is what a phase moves on top of that because the contraction
-    runs on the i8 matrix cores: the D8 operand rows the fused decompositions
+    runs on the i8 matrix cores: the operand rows (offset form) the fused decompositions
     write (F bytes per element; Phi_72 has 40 Toom-3 virtual slots, F = 320 B
     against E = 192 B) and the larger operand form of A and the vectors."""
     E, N = 8 * d, W * L
