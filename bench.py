@@ -54,8 +54,8 @@ SHARDED_LIMIT_S = 240  # N > 1: the sharded fold's watchdog (main)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=8)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=16)
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--d", type=int, default=1024)
     ap.add_argument("--w", type=int, default=1 << 14, help="w_ccs length W (ring elements)")
     ap.add_argument("--kappa", type=int, default=32)
