@@ -110,6 +110,26 @@ def algorithmic_bytes(d, W, kappa, L=5, K=15):
     return step, alg, operand
 
 
+def step_hbm(d, W, kappa, group, phases, value_per_gpu, L=5, K=15):
+    """Step-level HBM figures beside SURVEY B1..B5 (which count A twice per step):
+    the bytes the step needs when A is read once per `group` steps (one batched
+    contraction launch), and the PMC-measured bytes summed over the step's kernels
+    (traffic per launch x launches per step; null if any phase lacks a PMC figure)."""
+    E, N = 8 * d, W * L
+    survey, _, _ = algorithmic_bytes(d, W, kappa, L, K)
+    needed = survey - 2 * E * kappa * N + E * kappa * N / max(1, group)
+    tr = [p.get("traffic_bytes_per_launch") for p in phases.values()]
+    pmc = None if not tr or any(t is None for t in tr) else \
+        sum(p["traffic_bytes_per_launch"] * p["launches_per_step"] for p in phases.values())
+    out = {"survey_bytes_per_step": survey, "needed_bytes_per_step": needed, "steps_per_A_read": max(1, group),
+           "needed_gbs": needed * value_per_gpu / 1e9, "needed_frac_hbm": needed * value_per_gpu / 1e9 / HBM_PEAK_GBS,
+           "pmc_bytes_per_step": pmc}
+    if pmc is not None:
+        out["pmc_gbs"] = pmc * value_per_gpu / 1e9
+        out["pmc_frac_hbm"] = out["pmc_gbs"] / HBM_PEAK_GBS
+    return out
+
+
 I8_DENSE_TOPS = 5000.0  # MI355X dense i8 MFMA peak (2x the dense bf16 2.5 PFLOP/s)
 
 
@@ -160,11 +180,12 @@ def by_base(t, kern):
 
 
 def load_traffic(d, W, kappa):
-    """PMC-measured HBM bytes per launch (profiles/pmc_traffic.json, written by
+    """PMC-measured HBM bytes per launch (profiles/pmc_traffic_d<d>_W<W>_k<kappa>.json, written by
     tools/prof_summary.py traffic from separate FETCH_SIZE / WRITE_SIZE passes of
     this same configuration); {} when absent or for another configuration."""
     doc = None
-    for name in ("pmc_traffic.json", f"pmc_traffic_d{d}.json"):  # the default workload's, then a side config's
+    # the configuration's own file (tools/gpu_evidence.sh writes one per bench line)
+    for name in (f"pmc_traffic_d{d}_W{W}_k{kappa}.json",):
         try:
             cand = json.loads((ROOT / "profiles" / name).read_text())
         except (OSError, ValueError):
@@ -185,10 +206,10 @@ def load_traffic(d, W, kappa):
 
 
 def load_sq(d, W, kappa):
-    """PMC-measured VALU busy fraction per kernel (profiles/pmc_sq.json, written by
+    """PMC-measured VALU busy fraction per kernel (profiles/pmc_sq_d<d>_W<W>_k<kappa>.json, written by
     tools/prof_summary.py sq from one SQ pass of this configuration); {} otherwise."""
     doc = None
-    for name in ("pmc_sq.json", f"pmc_sq_d{d}.json"):  # the default workload's, then a side config's
+    for name in (f"pmc_sq_d{d}_W{W}_k{kappa}.json",):
         try:
             cand = json.loads((ROOT / "profiles" / name).read_text())
         except (OSError, ValueError):
@@ -264,6 +285,43 @@ def cpu_baseline(d, W_full, kappa):
             "sample": f"1 step at W={w_all} on {cores} threads ({t_all:.2f} s) and at W={w_one} on 1 thread "
                       f"({t_one:.2f} s), d={d}, kappa={kappa}; scaled linearly to W={W_full}",
             "single_core": {"value": v_one, "cores": 1}}
+
+
+class _Roctx:
+    """roctx ranges (librocprofiler-sdk-roctx) around the serialized phase pass of
+    every workload, so `tools/prof_summary.py stats` can keep exactly the kernels
+    the bench line's per-phase HIP-event times come from (rocprofv3
+    --marker-trace); a no-op when the library is absent."""
+
+    def __init__(self):
+        import ctypes
+        self.lib = None
+        for name in ("librocprofiler-sdk-roctx.so.1", "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1"):
+            try:
+                lib = ctypes.CDLL(name)
+                lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                lib.roctxRangePushA.restype = ctypes.c_int
+                lib.roctxRangePop.restype = ctypes.c_int
+                self.lib = lib
+                break
+            except OSError:
+                continue
+
+    def push(self, msg):
+        if self.lib is not None:
+            self.lib.roctxRangePushA(msg.encode())
+
+    def pop(self):
+        if self.lib is not None:
+            self.lib.roctxRangePop()
+
+
+ROCTX = _Roctx()
+
+
+def window_name(wl, what="phase_pass"):
+    """the roctx range name of a workload's serialized pass (prof_summary keys on it)"""
+    return f"{what} d={wl.d} W={wl.W} kappa={wl.kappa}"
 
 
 _STREAMS = {}
@@ -436,27 +494,35 @@ def measure(LA, torch, LD, pg, world, wl, steps, warmup, comm=None):
     # batched contraction's first launch (code object load) is not timed
     wl.run(warmup_steps(wl, warmup, comm), comm)
     wl.sync()
-    if S == 1:
+    serial = S == 1  # one stream: the timed steps are the phase pass
+    if serial:
         wl.timing(True)
     LD.barrier(pg)
     torch.cuda.synchronize()
+    if serial:
+        ROCTX.push(window_name(wl))
     t0 = time.perf_counter()
     wl.run(steps, comm)
     torch.cuda.synchronize()
+    if serial:
+        ROCTX.pop()
     LD.barrier(pg)
     dt = time.perf_counter() - t0
     wl.sync()  # surfaces any decomposition overflow
     dt_max = LD.max_over_ranks(pg, dt)
     if S > 1 and wl.batch and comm is None:
         # the phase pass of batched steps: every context on the first one's stream,
-        # so the phases run one at a time and the contraction covers S steps
+        # so the phases run one at a time and the contraction covers `group` steps
         base = torch.cuda.current_stream().cuda_stream
         for c in wl.ctxs:
             c.set_stream(base)
         wl.timing(True)
         n = max(1, steps // wl.group) * wl.group
+        torch.cuda.synchronize()
+        ROCTX.push(window_name(wl))
         wl.run(n, comm)
         wl.sync()
+        ROCTX.pop()
         tot = wl.phase_totals()
         wl.timing(False)
         for c, st in zip(wl.ctxs[1:], wl.streams):
@@ -464,8 +530,11 @@ def measure(LA, torch, LD, pg, world, wl, steps, warmup, comm=None):
         return dt_max, phase_report(LA, wl, tot, n)
     if S > 1:  # the phase pass: one stream
         wl.ctxs[0].kernel_timing(True)
+        torch.cuda.synchronize()
+        ROCTX.push(window_name(wl))
         wl.run(steps // S, comm, streams=1)
         wl.sync()
+        ROCTX.pop()
         tot = wl.phase_totals()
         wl.timing(False)
         return dt_max, phase_report(LA, wl, tot, steps // S)
@@ -509,6 +578,15 @@ def phase_report(LA, wl, tot, steps):
             phases_note = {}
         if cf24:  # digit masks in (8 B per element and plane); f0_coeff, f0 (E each) and w_ccs0 out (from_f's outputs)
             a = wl.N * (2 * wl.pr.K * 8 + 2 * 8 * d) + wl.W * 8 * d
+        if ph == "ajtai" and wl.batch:
+            # one launch covers `group` steps and reads A once for all of them; the
+            # context records it as `group` launches, so avg / bytes here are per step
+            # and A counts 1 / group of its bytes (SURVEY B1 + B3 count it twice per step)
+            E = 8 * d
+            nvec = 2 * (wl.pr.K - 1) + 1
+            phases_note = {"steps_per_launch": wl.group, "launch_ms": avg * wl.group,
+                           "survey_bytes_per_step": alg[ph]}
+            a = E * (kappa * wl.N / wl.group + nvec * wl.N + nvec * kappa)
         gbs = a / (avg * 1e-3) / 1e9
         extra = operand.get(ph, 0) * sides
         tr = traffic.get(kernel_of[ph])
@@ -546,7 +624,10 @@ def phase_report(LA, wl, tot, steps):
     roof = {"kernel": p["kernel"], "phase": dom, "bound": "hbm", "achieved": p["achieved_gbs"],
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": p["frac_hbm"], "traffic": p["traffic_bytes_per_launch"],
             "avg_launch_ms": p["avg_launch_ms"], "bytes_per_launch": p["algorithmic_bytes_per_launch"],
-            "extra_bytes": p["operand_bytes_per_launch"], "valu_busy": p["valu_busy"]}
+            "extra_bytes": p["operand_bytes_per_launch"], "valu_busy": p["valu_busy"],
+            # the roctx range whose kernels these HIP-event times cover (rocprofv3
+            # --marker-trace; tools/prof_summary.py stats summarises that window)
+            "profile_window": window_name(wl)}
     return phases, roof
 
 
@@ -571,7 +652,9 @@ def extra_shape(LA, torch, LD, pg, local, rank, world, d, W, kappa, S, steps, wa
     return {"workload": f"commit+fold step, {what}, w_ccs W={W}, kappa={kappa}, {how}",
             "d": d, "W": W, "kappa": kappa, "streams": S, "value": value, "unit": "fold-steps/s", "n_gpus": world,
             "steps": steps, "ms_per_step_per_gpu": dt / steps * 1e3,
-            "hbm_gbs_step_algorithmic": step_bytes * value / world / 1e9, "roofline": roof, "phases": phases}
+            "hbm_gbs_step_algorithmic": step_bytes * value / world / 1e9,
+            "step_hbm": step_hbm(d, W, kappa, group if batched else 1, phases, value / world),
+            "roofline": roof, "phases": phases}
 
 
 def sharded_fold(LA, torch, LD, pg, local, rank, world, d, W, kappa, steps, warmup):
@@ -914,6 +997,7 @@ def main():
                                       + (f"; groups of {group} steps whose contractions are one launch "
                                          f"(one pass over A per group)" if batched else "")},
             "hbm_gbs_step_algorithmic": step_bytes * value / world / 1e9,
+            "step_hbm": step_hbm(d, W, kappa, group if batched else 1, phases, value / world, L, K),
             # the dominant phase by device time per step (HIP events on the launch
             # stream, inside the timed region); bytes per SURVEY.md 8(d)
             "roofline": roof,

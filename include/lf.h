@@ -632,6 +632,38 @@ int lf_transcript_get_short_challenges(lf_transcript *t, int d, size_t count, ui
 /* WideZkVMPoseidon2::hash_iter (poseidon2.rs:206-235) */
 void lf_hash_iter(const uint64_t *in, size_t n, uint64_t out4[4]);
 
+/* ------------------------------------------------------------ IVC step commitments (zkvm/src/commitments.rs)
+ * hash_iter's second output, IntermediateStates (poseidon2.rs:199-202): one
+ * PermutationIntermediateStates (:91-96) per permutation, LF_P2_STATES x 16
+ * canonical words: after_initial_mds, after_ext_init_rounds[4],
+ * after_internal_rounds[22], after_ext_terminal_rounds[4]. ivc.rs:24,63 carries the
+ * ivc_step_comm's states into the next step's witness (ccs.rs:517-580 reads them). */
+#define LF_P2_STATES 31
+/* permutations hash_iter runs on n inputs: ceil(n / 12) (0 for an empty input) */
+size_t lf_hash_iter_nperm(size_t n);
+/* (digest, IntermediateStates): states [nperm][31][16] (NULL: digest only), cap >= nperm */
+int lf_hash_iter_states(const uint64_t *in, size_t n, uint64_t out4[4], uint64_t *states, size_t cap);
+/* ZkVmCommitter::acc_comm (commitments.rs:143-176): the LCCCS's r, v, cm, u, x_w, h
+ * flattened (:349-361: every NTT element ICRT'd, each coefficient's ark Montgomery
+ * limb taken as a Goldilocks value) and hashed with hash_iter. Phi_72 only (d = 24,
+ * the zkvm's ring); repr describes acc's words. zkvm/src/main.rs:106,195 */
+int lf_acc_comm(const lf_lcccs *acc, int repr, uint64_t out4[4]);
+/* ZkVmCommitter::ivc_step_comm (commitments.rs:76-105): hash_iter of [i, state_0_comm,
+ * state_i_comm, acc_comm] -- 13 elements, 2 permutations: states [2][31][16] or NULL.
+ * zkvm/src/main.rs:107,196 */
+int lf_ivc_step_comm(uint64_t i, const uint64_t state_0_comm[4], const uint64_t state_i_comm[4],
+                     const uint64_t acc_comm[4], uint64_t out4[4], uint64_t *states);
+/* ZkVmCommitter::state_i_comm (commitments.rs:107-141) given its parts (code_comm =
+ * lf_vm_code_comm, regs_comm = lf_vm_regs_comm): hash_iter of the 17 elements */
+int lf_state_i_comm(const uint64_t code_comm[4], uint64_t pc, const uint64_t memory_comm[4],
+                    const uint64_t regs_comm[4], const uint64_t mem_ops_vec_comm[4], uint64_t out4[4]);
+/* ZkVmCommitter::vm_regs_comm (commitments.rs:178-189): hash_iter of the registers */
+int lf_vm_regs_comm(const uint32_t *regs, size_t n, uint64_t out4[4]);
+/* ZkVmCommitter::vm_mem_ops_vec_comm (commitments.rs:290-307): the width-8
+ * TruncatedPermutation of [previous_comm, (cycle, address, value, 0)] */
+int lf_vm_mem_ops_vec_comm(const uint64_t prev[4], uint64_t cycle, uint32_t address, uint32_t value,
+                           uint64_t out4[4]);
+
 #ifdef __cplusplus
 }
 #endif

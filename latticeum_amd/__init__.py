@@ -728,6 +728,70 @@ def hash_iter(vals) -> np.ndarray:
     return out
 
 
+def _chk(rc: int, what: str):
+    if rc:
+        raise LfError(rc, f"{what}: " + load().lf_status_string(rc).decode())
+
+
+def hash_iter_states(vals) -> tuple[np.ndarray, np.ndarray]:
+    """hash_iter with its IntermediateStates (zkvm poseidon2.rs:199-235):
+    (digest, states [nperm][31][16])"""
+    lib = load()
+    x = _u64(vals) if len(vals) else np.zeros(1, np.uint64)
+    k = lib.lf_hash_iter_nperm(len(vals))
+    out = np.zeros(4, np.uint64)
+    st = np.zeros((max(k, 1), 31, 16), np.uint64)
+    _chk(lib.lf_hash_iter_states(_ptr(x), len(vals), _ptr(out), _ptr(st), k), "lf_hash_iter_states")
+    return out, st[:k]
+
+
+def acc_comm(acc: dict, d: int = 24, repr: int = REPR_CANONICAL) -> np.ndarray:
+    """ZkVmCommitter::acc_comm (zkvm commitments.rs:143-176) of an LCCCS dict
+    {r, v, cm, u, x_w, h} (the dicts Prover.fold_prove / linearize return)"""
+    from ._lib import LfLcccs, LfRingSlice
+    keep = {k: _u64(acc[k]) for k in ("r", "v", "cm", "u", "x_w", "h")}
+    sl = lambda a: LfRingSlice(a.ctypes.data if a.size else None, a.size // d)
+    A = LfLcccs(d, sl(keep["r"]), sl(keep["v"]), sl(keep["cm"]), sl(keep["u"]), sl(keep["x_w"]), keep["h"].ctypes.data)
+    out = np.zeros(4, np.uint64)
+    _chk(load().lf_acc_comm(C.byref(A), repr, _ptr(out)), "lf_acc_comm")
+    return out
+
+
+def ivc_step_comm(i: int, state_0_comm, state_i_comm, accc) -> tuple[np.ndarray, np.ndarray]:
+    """ZkVmCommitter::ivc_step_comm (commitments.rs:76-105): (digest, states [2][31][16])"""
+    a, b, c = _u64(state_0_comm), _u64(state_i_comm), _u64(accc)
+    out = np.zeros(4, np.uint64)
+    st = np.zeros((2, 31, 16), np.uint64)
+    _chk(load().lf_ivc_step_comm(int(i) % P, _ptr(a), _ptr(b), _ptr(c), _ptr(out), _ptr(st)), "lf_ivc_step_comm")
+    return out, st
+
+
+def state_i_comm(code_comm, pc: int, memory_comm, regs_comm, mem_ops_vec_comm) -> np.ndarray:
+    """ZkVmCommitter::state_i_comm (commitments.rs:107-141) from its parts"""
+    parts = [_u64(x) for x in (code_comm, memory_comm, regs_comm, mem_ops_vec_comm)]
+    out = np.zeros(4, np.uint64)
+    _chk(load().lf_state_i_comm(_ptr(parts[0]), int(pc) % P, _ptr(parts[1]), _ptr(parts[2]), _ptr(parts[3]),
+                                _ptr(out)), "lf_state_i_comm")
+    return out
+
+
+def vm_regs_comm(regs) -> np.ndarray:
+    """ZkVmCommitter::vm_regs_comm (commitments.rs:178-189)"""
+    r = np.ascontiguousarray(np.asarray(regs, dtype=np.uint32))
+    out = np.zeros(4, np.uint64)
+    _chk(load().lf_vm_regs_comm(r.ctypes.data if r.size else None, r.size, _ptr(out)), "lf_vm_regs_comm")
+    return out
+
+
+def vm_mem_ops_vec_comm(prev, cycle: int, address: int, value: int) -> np.ndarray:
+    """ZkVmCommitter::vm_mem_ops_vec_comm (commitments.rs:290-307)"""
+    pv = _u64(prev)
+    out = np.zeros(4, np.uint64)
+    _chk(load().lf_vm_mem_ops_vec_comm(_ptr(pv), int(cycle) % P, address & 0xFFFFFFFF, value & 0xFFFFFFFF,
+                                       _ptr(out)), "lf_vm_mem_ops_vec_comm")
+    return out
+
+
 def merkle_nodes_len(nrows: int) -> int:
     """digests in a tree over nrows rows (Plonky3's even-padded layers)"""
     return load().lf_merkle_nodes_len(nrows)
@@ -762,5 +826,6 @@ def vm_mem_comm(words) -> np.ndarray:
 
 __all__ = ["Context", "AjtaiCommitmentScheme", "Communicator", "Comb", "CCSMatrices", "Prover", "witness_split_w", "Poseidon2Transcript",
            "LfParams", "LfFoldStepBufs", "merkle_nodes_len", "merkle_depth", "hash_w8", "vm_mem_comm",
-           "LfError", "goldilocks_dp", "short_challenge", "hash_iter", "P", "REPR_CANONICAL",
+           "LfError", "goldilocks_dp", "short_challenge", "hash_iter", "hash_iter_states", "acc_comm",
+           "ivc_step_comm", "state_i_comm", "vm_regs_comm", "vm_mem_ops_vec_comm", "P", "REPR_CANONICAL",
            "REPR_MONTGOMERY", "load"]

@@ -147,6 +147,13 @@ SIGNATURES = {
     "lf_transcript_squeeze_bytes": (None, [VP, VP, SZ]),
     "lf_transcript_get_short_challenges": (I, [VP, I, SZ, VP]),
     "lf_hash_iter": (None, [VP, SZ, VP]),
+    "lf_hash_iter_nperm": (SZ, [SZ]),
+    "lf_hash_iter_states": (I, [VP, SZ, VP, VP, SZ]),
+    "lf_acc_comm": (I, [C.POINTER(LfLcccs), I, VP]),
+    "lf_ivc_step_comm": (I, [U64, VP, VP, VP, VP, VP]),
+    "lf_state_i_comm": (I, [VP, U64, VP, VP, VP, VP]),
+    "lf_vm_regs_comm": (I, [VP, SZ, VP]),
+    "lf_vm_mem_ops_vec_comm": (I, [VP, U64, C.c_uint32, C.c_uint32, VP]),
     "lf_witness_split_w": (SZ, []),
     "lf_dev_poseidon2_w8_permute": (I, [VP, VP, SZ]),
     "lf_dev_merkle_tree": (I, [VP, VP, SZ, SZ, VP]),

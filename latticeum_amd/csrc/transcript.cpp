@@ -11,6 +11,7 @@
 
 #include "../../include/lf.h"
 #include "gl.hpp"
+#include "ring.hpp"
 
 namespace {
 #include "p2_consts.inc"
@@ -122,6 +123,35 @@ void permute(uint64_t *s) {
     mds16(s);
   }
   #pragma unroll
+  for (int i = 0; i < 16; i++) s[i] = gl::canon(s[i]);
+}
+// permute() with WideZkVMPoseidon2Perm::permute_mut's PermutationIntermediateStates
+// (poseidon2.rs:91-96, 104-171): the state after the initial MDS, after each of
+// the 4 initial external, 22 internal and 4 terminal rounds -- 31 x 16 words,
+// canonical (the in-CCS verifier reads them with as_canonical_u64, ccs.rs:517-580)
+void permute_states(uint64_t *s, uint64_t *st) {
+  auto keep = [&](int k) {
+    for (int i = 0; i < 16; i++) st[16 * k + i] = gl::canon(s[i]);
+  };
+  mds16(s);
+  keep(0);
+  for (int r = 0; r < 4; r++) {
+    for (int i = 0; i < 16; i++) s[i] = sbox7(wadd(s[i], EXT_INIT[16 * r + i]));
+    mds16(s);
+    keep(1 + r);
+  }
+  for (int r = 0; r < 22; r++) {
+    const uint64_t rest = wsum(s + 1, 15);
+    s[0] = sbox7(wadd(s[0], INTERNAL[r]));
+    const uint64_t sum = wadd(rest, s[0]);
+    for (int i = 0; i < 16; i++) s[i] = wadd(wmul(s[i], DIAG_M1[i]), sum);
+    keep(5 + r);
+  }
+  for (int r = 0; r < 4; r++) {
+    for (int i = 0; i < 16; i++) s[i] = sbox7(wadd(s[i], EXT_TERM[16 * r + i]));
+    mds16(s);
+    keep(27 + r);
+  }
   for (int i = 0; i < 16; i++) s[i] = gl::canon(s[i]);
 }
 // Poseidon2Goldilocks<8> (poseidon2.rs:31-49): the same round structure at
@@ -259,6 +289,97 @@ void lf_hash_iter(const uint64_t *in, size_t n, uint64_t out4[4]) {
     }
     permute(s);
   }
+}
+
+size_t lf_hash_iter_nperm(size_t n) { return (n + 11) / 12; }
+
+int lf_hash_iter_states(const uint64_t *in, size_t n, uint64_t out4[4], uint64_t *states, size_t cap) {
+  if ((!in && n) || !out4 || (states && cap < lf_hash_iter_nperm(n))) return LF_ERR_INVALID_ARG;
+  uint64_t s[16] = {0};
+  size_t pos = 0, np = 0;
+  auto perm = [&]() {  // poseidon2.rs:221,226: one IntermediateStates record per permutation
+    if (states) permute_states(s, states + (size_t)LF_P2_STATES * 16 * np);
+    else permute(s);
+    np++;
+  };
+  for (;;) {  // poseidon2.rs:215-227
+    for (int i = 0; i < 12; i++) {
+      if (pos < n) {
+        s[i] = gl::canon(in[pos++]);
+      } else {
+        if (i != 0) perm();
+        memcpy(out4, s, 4 * sizeof(uint64_t));
+        return LF_OK;
+      }
+    }
+    perm();
+  }
+}
+
+int lf_acc_comm(const lf_lcccs *acc, int repr, uint64_t out4[4]) {
+  // commitments.rs:143-176 + flatten (:349-361): r, v, cm, u, x_w, h in that
+  // order, every NTT element ICRT'd and each coefficient's ark limb (its
+  // Montgomery form) hashed as a Goldilocks value. The ICRT is linear, so on
+  // Montgomery-limb input it yields the coefficients' Montgomery limbs directly.
+  if (!acc || !out4 || (repr != LF_REPR_CANONICAL && repr != LF_REPR_MONTGOMERY)) return LF_ERR_INVALID_ARG;
+  if (acc->d != 24) return LF_ERR_UNSUPPORTED_RING;  // the zkvm's GoldilocksRingNTT
+  const lf_ring_slice parts[6] = {acc->r, acc->v, acc->cm, acc->u, acc->x_w, {acc->h, 1}};
+  std::vector<uint64_t> flat;
+  for (const lf_ring_slice &p : parts) {
+    if (p.n && !p.elems) return LF_ERR_INVALID_ARG;
+    for (size_t e = 0; e < p.n; e++) {
+      uint64_t c[24];
+      for (int i = 0; i < 24; i++) c[i] = gl::canon(p.elems[e * 24 + i]);
+      ring::phi72_icrt(c);
+      for (int i = 0; i < 24; i++) flat.push_back(repr == LF_REPR_MONTGOMERY ? c[i] : gl::to_mont(c[i]));
+    }
+  }
+  return lf_hash_iter_states(flat.data(), flat.size(), out4, nullptr, 0);
+}
+
+int lf_ivc_step_comm(uint64_t i, const uint64_t state_0_comm[4], const uint64_t state_i_comm[4],
+                     const uint64_t acc_comm[4], uint64_t out4[4], uint64_t *states) {
+  if (!state_0_comm || !state_i_comm || !acc_comm) return LF_ERR_INVALID_ARG;
+  uint64_t in[13];  // commitments.rs:83-105
+  in[0] = i;
+  for (int k = 0; k < 4; k++) {
+    in[1 + k] = state_0_comm[k];
+    in[5 + k] = state_i_comm[k];
+    in[9 + k] = acc_comm[k];
+  }
+  return lf_hash_iter_states(in, 13, out4, states, 2);
+}
+
+int lf_state_i_comm(const uint64_t code_comm[4], uint64_t pc, const uint64_t memory_comm[4],
+                    const uint64_t regs_comm[4], const uint64_t mem_ops_vec_comm[4], uint64_t out4[4]) {
+  if (!code_comm || !memory_comm || !regs_comm || !mem_ops_vec_comm) return LF_ERR_INVALID_ARG;
+  uint64_t in[17];  // commitments.rs:107-141
+  for (int k = 0; k < 4; k++) {
+    in[k] = code_comm[k];
+    in[5 + k] = memory_comm[k];
+    in[9 + k] = regs_comm[k];
+    in[13 + k] = mem_ops_vec_comm[k];
+  }
+  in[4] = pc;
+  return lf_hash_iter_states(in, 17, out4, nullptr, 0);
+}
+
+int lf_vm_regs_comm(const uint32_t *regs, size_t n, uint64_t out4[4]) {
+  if (!regs && n) return LF_ERR_INVALID_ARG;  // commitments.rs:178-189 (N_REGS = 32)
+  std::vector<uint64_t> in(regs, regs + n);
+  return lf_hash_iter_states(in.data(), n, out4, nullptr, 0);
+}
+
+int lf_vm_mem_ops_vec_comm(const uint64_t prev[4], uint64_t cycle, uint32_t address, uint32_t value,
+                           uint64_t out4[4]) {
+  // commitments.rs:290-307: TruncatedPermutation<Poseidon2<8>, 2, 4, 8>::compress of
+  // [previous_comm, (cycle, address, value, 0)]: permute the concatenation, keep 4
+  if (!prev || !out4) return LF_ERR_INVALID_ARG;
+  uint64_t s[8] = {gl::canon(prev[0]), gl::canon(prev[1]), gl::canon(prev[2]), gl::canon(prev[3]),
+                   gl::canon(cycle), address, value, 0};
+  permute8(s);
+  memcpy(out4, s, 4 * sizeof(uint64_t));
+  return LF_OK;
 }
 
 void lf_hash_w8(const uint64_t *in, size_t n, uint64_t out4[4]) {

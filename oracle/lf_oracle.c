@@ -652,6 +652,52 @@ void lfo_p2_permute(uint64_t *s) { /* ZK/poseidon2.rs:100-173 */
     lfo_p2_mds16(s);
   }
 }
+/* WideZkVMPoseidon2Perm::permute_mut's PermutationIntermediateStates
+ * (ZK/poseidon2.rs:91-96, 100-173): st[0] after the initial MDS (:131-132),
+ * st[1..4] after each initial external round (:134-146), st[5..26] after each
+ * internal round (:150-154), st[27..30] after each terminal external round (:157-169) */
+void lfo_p2_permute_states(uint64_t *s, uint64_t *st) {
+  lfo_p2_mds16(s);
+  memcpy(st, s, 16 * sizeof(uint64_t));
+  for (int r = 0; r < 4; r++) {
+    for (int i = 0; i < 16; i++) s[i] = sbox(s[i], EXT_INIT[16 * r + i]);
+    lfo_p2_mds16(s);
+    memcpy(st + 16 * (1 + r), s, 16 * sizeof(uint64_t));
+  }
+  for (int r = 0; r < 22; r++) {
+    s[0] = sbox(s[0], INTERNAL[r]);
+    uint64_t sum = 0;
+    for (int i = 0; i < 16; i++) sum = lfo_add(sum, s[i]);
+    for (int i = 0; i < 16; i++) s[i] = lfo_add(lfo_mul(s[i], DIAG_M1[i]), sum);
+    memcpy(st + 16 * (5 + r), s, 16 * sizeof(uint64_t));
+  }
+  for (int r = 0; r < 4; r++) {
+    for (int i = 0; i < 16; i++) s[i] = sbox(s[i], EXT_TERM[16 * r + i]);
+    lfo_p2_mds16(s);
+    memcpy(st + 16 * (27 + r), s, 16 * sizeof(uint64_t));
+  }
+}
+/* hash_iter returning IntermediateStates (ZK/poseidon2.rs:206-235): one 31 x 16
+ * record per permutation, in order; returns the number of permutations */
+size_t lfo_p2_hash_iter_states(const uint64_t *in, size_t n, uint64_t out[4], uint64_t *states) {
+  uint64_t s[16] = {0};
+  size_t pos = 0, np = 0;
+  for (;;) {
+    int i;
+    for (i = 0; i < 12; i++) {
+      if (pos < n) {
+        s[i] = in[pos++];
+      } else {
+        if (i != 0) lfo_p2_permute_states(s, states + 31 * 16 * np++);
+        goto done;
+      }
+    }
+    lfo_p2_permute_states(s, states + 31 * 16 * np++);
+  }
+done:
+  memcpy(out, s, 4 * sizeof(uint64_t));
+  return np;
+}
 static void p2_range(void *p, size_t lo, size_t hi) {
   uint64_t *st = p;
   for (size_t i = lo; i < hi; i++) lfo_p2_permute(st + 16 * i);

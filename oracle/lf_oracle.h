@@ -114,6 +114,10 @@ void lfo_p2_permute(uint64_t *s);
 void lfo_p2_permute_batch(uint64_t *states, size_t n, int nthreads);
 /* hash_iter (ZK/poseidon2.rs:206-235): overwrite sponge, rate 12, out state[0..4] */
 void lfo_p2_hash_iter(const uint64_t *in, size_t n, uint64_t out[4]);
+/* PermutationIntermediateStates (ZK/poseidon2.rs:91-96): st = 31 x 16 words */
+void lfo_p2_permute_states(uint64_t *s, uint64_t *st);
+/* hash_iter's IntermediateStates: states [nperm][31][16]; returns nperm = ceil(n / 12) */
+size_t lfo_p2_hash_iter_states(const uint64_t *in, size_t n, uint64_t out[4], uint64_t *states);
 
 /* ---- width-8 Poseidon2 and Merkle trees (zkvm commitments.rs; parity unpinned: Plonky3 diag) ---- */
 void lfo_p2w8_permute(uint64_t *s);

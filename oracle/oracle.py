@@ -71,6 +71,8 @@ def lib():
         "lfo_p2_mds16": (None, [u64p]), "lfo_p2_permute": (None, [u64p]),
         "lfo_p2_permute_batch": (None, [u64p, SZ, I]),
         "lfo_p2_hash_iter": (None, [u64p, SZ, u64p]),
+        "lfo_p2_permute_states": (None, [u64p, u64p]),
+        "lfo_p2_hash_iter_states": (SZ, [u64p, SZ, u64p, u64p]),
         "lfo_tr_init": (None, [C.POINTER(Transcript)]),
         "lfo_tr_observe": (None, [C.POINTER(Transcript), U64]),
         "lfo_tr_sample": (U64, [C.POINTER(Transcript)]),
@@ -418,6 +420,66 @@ def p2_hash_iter(vals) -> np.ndarray:
     x = _u64(vals) if len(vals) else np.zeros(1, np.uint64)
     lib().lfo_p2_hash_iter(x, len(vals), out)
     return out
+
+
+def p2_permute_states(state) -> tuple[np.ndarray, np.ndarray]:
+    """one permutation and its PermutationIntermediateStates (ZK/poseidon2.rs:91-96):
+    (final state, 31 x 16 captured states)"""
+    x = _u64(state).copy()
+    st = np.zeros((31, 16), np.uint64)
+    lib().lfo_p2_permute_states(x, st)
+    return x, st
+
+
+def p2_hash_iter_states(vals) -> tuple[np.ndarray, np.ndarray]:
+    """hash_iter (ZK/poseidon2.rs:206-235): (digest, IntermediateStates as [nperm][31][16])"""
+    n = len(vals)
+    out = np.zeros(4, np.uint64)
+    x = _u64(vals) if n else np.zeros(1, np.uint64)
+    st = np.zeros((max(1, -(-n // 12)), 31, 16), np.uint64)
+    k = lib().lfo_p2_hash_iter_states(x, n, out, st)
+    return out, st[:k]
+
+
+# ---------------------------------------------------------------- zkvm step commitments (ZK/commitments.rs)
+def flatten_mont(elems, d: int = 24) -> np.ndarray:
+    """commitments.rs:343-361 flatten(): ICRT every NTT element (ICRT::icrt), then each
+    coefficient's ark limb `fq.0.0[0]` -- its Montgomery form -- as a Plonky3
+    Goldilocks (from_u64). Canonical NTT elements in, Montgomery limbs out."""
+    c = icrt(elems, d) if len(elems) else np.zeros(0, np.uint64)
+    return np.array([to_mont(int(v)) for v in c], np.uint64)
+
+
+def acc_comm(acc: dict, d: int = 24) -> np.ndarray:
+    """ZkVmCommitter::acc_comm (commitments.rs:143-176): r, v, cm, u, x_w, h flattened
+    in that order and hashed with hash_iter; acc holds canonical NTT elements"""
+    parts = [flatten_mont(_u64(acc[k]).ravel(), d) for k in ("r", "v", "cm", "u", "x_w", "h")]
+    return p2_hash_iter(np.concatenate(parts))
+
+
+def ivc_step_comm(i: int, state0, state_i, accc) -> tuple[np.ndarray, np.ndarray]:
+    """ZkVmCommitter::ivc_step_comm (commitments.rs:76-105): hash_iter of
+    [i, state_0_comm, state_i_comm, acc_comm] (13 elements, 2 permutations)"""
+    vals = [int(i) % P] + [int(x) for x in state0] + [int(x) for x in state_i] + [int(x) for x in accc]
+    return p2_hash_iter_states(vals)
+
+
+def state_i_comm(code_comm, pc: int, memory_comm, regs_comm, mem_ops_vec_comm) -> np.ndarray:
+    """ZkVmCommitter::state_i_comm (commitments.rs:107-141), given code_comm and regs_comm"""
+    vals = [int(x) for x in code_comm] + [int(pc) % P] + [int(x) for x in memory_comm] + \
+           [int(x) for x in regs_comm] + [int(x) for x in mem_ops_vec_comm]
+    return p2_hash_iter(vals)
+
+
+def vm_regs_comm(regs) -> np.ndarray:
+    """ZkVmCommitter::vm_regs_comm (commitments.rs:178-189): hash_iter of the 32 u32 registers"""
+    return p2_hash_iter([int(r) & 0xFFFFFFFF for r in regs])
+
+
+def vm_mem_ops_vec_comm(prev, cycle: int, address: int, value: int) -> np.ndarray:
+    """ZkVmCommitter::vm_mem_ops_vec_comm (commitments.rs:290-307): TruncatedPermutation<8>
+    compress of [prev, (cycle, address, value, 0)]"""
+    return p2w8_compress(_u64(prev), _u64([cycle % P, address & 0xFFFFFFFF, value & 0xFFFFFFFF, 0]))
 
 
 def new_transcript() -> Transcript:

@@ -242,6 +242,17 @@ def test_fold_prove_zkvm_dimensions():
             assert np.array_equal(flat(getattr(v, k)), out[k]), k
         assert np.array_equal(v.cm, out["cm"]) and np.array_equal(v.h, out["h"])
         check_replay(prover, acc, cmi, xi, pf, out, kappa)
+        # the IVC step commitments of the folded accumulator (main.rs:195-196): acc_comm
+        # over its 182 ring elements (364 permutations), both reprs, and ivc_step_comm
+        assert [out[k].size // d for k in ("r", "v", "cm", "u", "x_w", "h")] == [17, 3, 32, 125, 4, 1]
+        ac = LA.acc_comm(out)
+        assert np.array_equal(ac, O.acc_comm(out))
+        mont = np.vectorize(O.to_mont, otypes=[np.uint64])
+        assert np.array_equal(LA.acc_comm({k: mont(x) for k, x in out.items()}, repr=LA.REPR_MONTGOMERY), ac)
+        z0c = O.fill_uniform(4, 9)
+        dg, st = LA.ivc_step_comm(1, z0c, O.fill_uniform(4, 10), ac)
+        odg, ost = O.ivc_step_comm(1, z0c, O.fill_uniform(4, 10), ac)
+        assert np.array_equal(dg, odg) and np.array_equal(st, ost)
         # the folded instance is the folded witness's
         cm0 = zeros(kappa * d)
         ctx.dev_ajtai_commit(sch, [w_out["f"]], cm0)

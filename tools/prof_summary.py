@@ -35,14 +35,61 @@ def short(name):
     return n.replace("void ", "").strip()
 
 
+def marker_windows(prof_dir, prefix="phase_pass"):
+    """roctx ranges bench.py pushes around each workload's serialized phase pass
+    (rocprofv3 --marker-trace): {name: [(start_ns, end_ns), ...]}"""
+    hits = sorted(glob.glob(os.path.join(prof_dir, "**", "*marker_api_trace.csv"), recursive=True))
+    wins = defaultdict(list)
+    for f in hits:
+        for r in csv.DictReader(open(f)):
+            name = next((v for v in r.values() if isinstance(v, str) and v.startswith(prefix)), None)
+            if name is not None:
+                wins[name].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    return wins
+
+
+def window_table(trace, lo, hi):
+    """per kernel (and grid for the contraction): launches, avg us inside [lo, hi],
+    and the window's largest number of kernels in flight at once (1 = serialized)"""
+    inside = [t for t in trace if int(t["Start_Timestamp"]) >= lo and int(t["End_Timestamp"]) <= hi]
+    by = defaultdict(list)
+    ev = []
+    for t in inside:
+        s, e = int(t["Start_Timestamp"]), int(t["End_Timestamp"])
+        key = short(t["Kernel_Name"]) + (f" grid={grid(t)}" if "ajtai" in t["Kernel_Name"] else "")
+        by[key].append((e - s) / 1e3)
+        ev += [(s, 1), (e, -1)]
+    conc = cur = 0
+    for _, dlt in sorted(ev, key=lambda x: (x[0], x[1])):
+        cur += dlt
+        conc = max(conc, cur)
+    return by, conc
+
+
 def stats(prof_dir, out_md):
     rows = list(csv.DictReader(open(find(prof_dir, "kernel_stats.csv"))))
-    lines = ["| kernel | calls | avg us | total ms | % |", "|---|---|---|---|---|"]
+    trace = list(csv.DictReader(open(find(prof_dir, "kernel_trace.csv"))))
+    lines = []
+    side = {}
+    for name, spans in sorted(marker_windows(prof_dir).items()):
+        lo, hi = min(s for s, _ in spans), max(e for _, e in spans)
+        by, conc = window_table(trace, lo, hi)
+        lines += [f"## window `{name}` (roctx range, {(hi - lo) / 1e6:.2f} ms; at most {conc} kernel(s) in flight)",
+                  "", "| kernel | launches | avg us | total ms |", "|---|---|---|---|"]
+        tot = sum(sum(v) for v in by.values())
+        for k, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
+            lines.append(f"| `{k}` | {len(v)} | {sum(v) / len(v):.1f} | {sum(v) / 1e3:.2f} |")
+        lines += [f"| (all) | {sum(len(v) for v in by.values())} | | {tot / 1e3:.2f} |", ""]
+        side[name] = {"window_ms": (hi - lo) / 1e6, "max_in_flight": conc,
+                      "kernels": {k: {"launches": len(v), "avg_us": sum(v) / len(v)} for k, v in by.items()}}
+    if side:
+        json.dump(side, open(os.path.splitext(out_md)[0] + ".windows.json", "w"), indent=1)
+        lines += ["## whole process (every stream; concurrent launches stretch each other's durations)", ""]
+    lines += ["| kernel | calls | avg us | total ms | % |", "|---|---|---|---|---|"]
     for r in rows:
         lines.append(f"| `{short(r['Name'])}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
                      f"{float(r['TotalDurationNs']) / 1e6:.2f} | {float(r['Percentage']):.2f} |")
     # per-grid breakdown of the Ajtai kernel (batched vs single launches differ in grid)
-    trace = list(csv.DictReader(open(find(prof_dir, "kernel_trace.csv"))))
     by = defaultdict(list)
     for t in trace:
         if "ajtai" in t["Kernel_Name"]:
