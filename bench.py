@@ -140,7 +140,7 @@ def coeff_fold(d, layout, keep_fk):
     return d == 1024 and layout == 1 and keep_fk
 
 
-def kernel_names(LA, d, W, layout, keep_fk=True):
+def kernel_names(LA, d, W, layout, keep_fk=True, packed=False):
     """the kernel each lf_dev_fold_step phase launches (for the rocprof / PMC joins)"""
     mfma = "k_ajtai_mfma_ra"  # the i8 contraction, A in registers (ajtai_mfma.hip)
     if d == 24:
@@ -156,10 +156,11 @@ def kernel_names(LA, d, W, layout, keep_fk=True):
                 "from_f": ("k_from_fcoeff_split" if small else "k_from_fcoeff_n32") if cf
                 else "k_from_f_split" if small else "k_from_f_n32",
                 "to_frag": "k_to_frag<true, false, true>"}
-    if d == 4096:
+    if d == 4096:  # packed planes fold f_0 from the operand rows
         return {"decompose": "k_decompose_n4k_fused" if layout == 1 else "k_decompose_n4k",
                 "ajtai": mfma if layout == 1 else "k_ajtai_nega",
-                "fold": "k_fold_nega", "from_w_ccs": "k_from_w_ccs_n4k", "from_f": "k_from_f_n4k",
+                "fold": "k_fold_frag" if packed else "k_fold_nega", "from_w_ccs": "k_from_w_ccs_n4k",
+                "from_f": "k_from_f_n4k",
                 "to_frag": "k_to_frag<true, false, true>"}
     return {"decompose": "k_decompose_nega", "ajtai": mfma if layout == 1 else "k_ajtai_nega",
             "fold": "k_fold_nega", "from_w_ccs": "k_from_w_ccs_nega", "from_f": "k_from_f_nega",
@@ -225,16 +226,27 @@ def load_sq(d, W, kappa):
     return t
 
 
+def cpu_limits():
+    """the host's CPU picture, each figure separately: the machine's CPUs
+    (os.cpu_count(); the whole host on the GPU box), this process's affinity set,
+    and the cgroup CPU quota in CPUs (None when unlimited or absent)"""
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    return {"machine_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_quota_cpus": quota}
+
+
 def host_cores():
     """CPUs this process may use: its affinity set, capped by a cgroup CPU quota
     (the GPU box shows the whole machine in os.cpu_count())"""
-    n = len(os.sched_getaffinity(0))
-    try:
-        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()
-        if quota != "max":
-            n = min(n, -(-int(quota) // int(period)))
-    except (OSError, ValueError):
-        pass
+    lim = cpu_limits()
+    n = lim["affinity_cpus"]
+    if lim["cgroup_quota_cpus"] is not None:
+        n = min(n, -(-int(lim["cgroup_quota_cpus"] * 1000) // 1000))
     return max(1, n)
 
 
@@ -267,23 +279,27 @@ def cpu_step_seconds(O, d, kappa, W, threads):
 def cpu_baseline(d, W_full, kappa):
     """The oracle's C restatement of the same step (kind "port": the Rust
     reference cannot be built here), parallelised where the reference uses
-    rayon, timed on all host cores and on one core over bounded samples of the
-    workload and scaled linearly in W (every stage is linear in W). It is the
+    rayon, timed on all host cores the process may use and on one core. Each is
+    one step on a bounded sample of about 10 s of CPU work: the whole workload
+    when that fits (the reference ring's W = 19 763 on all cores), else a prefix
+    of the witness scaled linearly in W (every stage is linear in W). It is the
     naive u128-% restatement, not a tuned rayon build, so it understates what
     the reference's own CPU path would reach."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle as O
 
     cores = host_cores()
-    w_all = max(1, min(W_full, 512 if d >= 1024 else 4096))
-    w_one = max(1, min(W_full, 64 if d >= 1024 else 512))
+    w_all = max(1, min(W_full, 4096 if d >= 1024 else W_full))
+    w_one = max(1, min(W_full, 256 if d >= 1024 else 4096))
     t_all = cpu_step_seconds(O, d, kappa, w_all, cores)
     t_one = cpu_step_seconds(O, d, kappa, w_one, 1)
     v_all = 1.0 / (t_all * W_full / w_all)
     v_one = 1.0 / (t_one * W_full / w_one)
+    scaled = lambda w: "the full workload" if w == W_full else f"scaled linearly from W={w} to W={W_full}"
     return {"value": v_all, "unit": "fold-steps/s", "cores": cores, "kind": "port",
-            "sample": f"1 step at W={w_all} on {cores} threads ({t_all:.2f} s) and at W={w_one} on 1 thread "
-                      f"({t_one:.2f} s), d={d}, kappa={kappa}; scaled linearly to W={W_full}",
+            "sample": f"1 step at W={w_all} on {cores} threads ({t_all:.2f} s; {scaled(w_all)}) and at W={w_one} on "
+                      f"1 thread ({t_one:.2f} s; {scaled(w_one)}), d={d}, kappa={kappa}",
+            "host": cpu_limits(),
             "single_core": {"value": v_one, "cores": 1}}
 
 
@@ -354,7 +370,7 @@ class Workload:
         # d = 24, 2 B per coefficient for all planes at d = 1024) instead of u64 f_k /
         # f_coeff_k rows (2 x 8 d B per element and plane); lf_dev_expand_planes
         # makes the rows. d = 1024, W = 2^14: decomposition 14.0 -> 12.4 ms, 41.5 -> 44.0 steps/s
-        self.packed = packed = (d in (24, 1024)) if packed is None else packed
+        self.packed = packed = (d in (24, 1024, 4096)) if packed is None else packed
         # batch = G > 1: the step streams form groups of G; each group's G steps are one
         # lf_dev_fold_step_batch call (independent steps on their own streams, one
         # contraction launch for the group); the groups take turns, so one group's
@@ -410,7 +426,8 @@ class Workload:
                 "fk": [z(K * N * d) for _ in range(2)] if self.keep_fk else [None, None],
                 "wk": [z(K * W * d) for _ in range(2)], "y": [z(K * kappa * d) for _ in range(2)],
                 "f0": z(N * d), "f0_coeff": z(N * d), "w_ccs0": z(W * d), "cm0": z(kappa * d),
-                "planes": [z(K * N if d == 24 else N * 256) for _ in range(2)] if packed else [None, None],
+                "planes": [z(K * N if d == 24 else N * 256 if d == 1024 else N * K * 128) for _ in range(2)]
+                if packed else [None, None],
             }
             bufs = LA.LfFoldStepBufs()
             for k, v in keep.items():
@@ -551,7 +568,7 @@ def phase_report(LA, wl, tot, steps):
     if not wl.keep_fk and not wl.packed:  # the planes are written once, as the operand rows: no bytes beyond B2
         operand["decompose"] = 0
     # packed planes fold in coefficient form as with f_k (the operand rows are only the fallback's)
-    kernel_of = kernel_names(LA, d, W, wl.sch.layout, wl.keep_fk or wl.packed)
+    kernel_of = kernel_names(LA, d, W, wl.sch.layout, wl.keep_fk or wl.packed, wl.packed)
     traffic = load_traffic(d, W, kappa)
     valu = load_sq(d, W, kappa)
     phases = {}
@@ -570,7 +587,7 @@ def phase_report(LA, wl, tot, steps):
             # B2 counts the u64 f_k / f_coeff_k rows the reference materialises; this
             # launch keeps them as packed planes instead (d = 24: 8 B per element and
             # plane written; d = 1024: the 2 B-per-coefficient words it reads anyway)
-            planes_b = wl.pr.K * wl.N * 8 if d == 24 else wl.N * 2 * d
+            planes_b = wl.pr.K * wl.N * 8 if d == 24 else wl.N * 2 * d if d == 1024 else wl.pr.K * wl.N * d // 4
             phases_note = {"packed_planes": True,
                            "moved_bytes_per_launch": sides * (wl.N * 8 * d + planes_b + wl.pr.K * W * 8 * d)
                            + operand.get(ph, 0) * sides}
@@ -770,10 +787,10 @@ def next_rows(LA, torch, local, cpu):
     del m
     torch.cuda.empty_cache()
     if cpu is not None:
-        # the oracle's prover over the same comb at log m = 9, scaled by 2^(17-9)
+        # the oracle's prover over the same comb at log m = 12, scaled by 2^(17-12)
         sys.path.insert(0, str(ROOT / "oracle"))
         import oracle as O
-        nvs = 9
+        nvs = 12
         mles = O.fill_uniform(nm * (1 << nvs) * d, 5)
         mu_h = O.fill_uniform(nk * d, 6)
         t0 = time.perf_counter()
@@ -858,6 +875,7 @@ def next_rows(LA, torch, local, cpu):
         "challenged_gbs_values": val_bytes / (ms_ch * 1e-3) / 1e9}
     del z, ch, ev
     out["fold_prove"] = fold_prove_line(LA, torch, ctx, M, S, d, nn, t, mm)
+    out["zkvm_chain"] = zkvm_chain(LA, torch, ctx, M, S, d, nn, t, mm)
     del M
     # the memory Merkle tree of the zkvm's 8 MB VM (8192 pages of 256 words,
     # vm.rs:106-124; commitments.rs:192-262): 8192 sponge chains of 64 width-8
@@ -911,23 +929,32 @@ def fold_prove_line(LA, torch, ctx, M, S, d, n, t, m):
     xi, wi, cmi = wit(SEED_W)
     acc, _ = prover.linearize(cma, xa, wa)
     w_out = {"w_ccs": torch.empty(W * d, **i64), "f": torch.empty(N * d, **i64), "f_coeff": torch.empty(N * d, **i64)}
-    times = []
+    times, times_v = [], []
     for _ in range(4):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         prover.fold_prove(acc, wa, cmi, xi, wi, w_out)
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
+    # fold() + generate_verification_witness_vars as the zkvm loop runs them (main.rs:175-185):
+    # lf_fold_prove_vars, the vars from the call's own sample log
+    for _ in range(4):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        prover.fold_prove(acc, wa, cmi, xi, wi, w_out, vars=True)
+        torch.cuda.synchronize()
+        times_v.append(time.perf_counter() - t0)
     prover.timing(True)
-    _, pf = prover.fold_prove(acc, wa, cmi, xi, wi, w_out)
+    _, pf, vv = prover.fold_prove(acc, wa, cmi, xi, wi, w_out, vars=True)
     spans = prover.timing(False)
-    # the verifier-variable replay of that proof (generate_verification_witness_vars,
-    # zk_latticefold.rs:111-148): host only, a second pass of the transcript per step
+    # the standalone verifier-variable replay of that proof (lf_fold_replay: a second
+    # pass of the Poseidon2 transcript), the check the sample-log vars must equal
     t_rep = []
     for _ in range(3):
         t0 = time.perf_counter()
-        prover.replay(acc, cmi, xi, pf)
+        vr = prover.replay(acc, cmi, xi, pf)
         t_rep.append(time.perf_counter() - t0)
+    vars_equal = all(np.array_equal(vv[k], vr[k]) for k in vr)
     t0 = time.perf_counter()
     prover.linearize(cma, xa, wa)
     torch.cuda.synchronize()
@@ -937,10 +964,120 @@ def fold_prove_line(LA, torch, ctx, M, S, d, n, t, m):
     return {"workload": f"zkvm fold() end to end (lf_fold_prove): Phi_72, W={W} (n={n}, l={l}), kappa={kappa}, "
                         f"CCS t={t} x {m} rows, {len(S)} multisets, degree {deg}; transcript on the host",
             "ms_per_fold_prove": min(times[1:]) * 1e3, "ms_per_fold_prove_median": float(np.median(times[1:])) * 1e3,
+            "ms_per_fold_prove_vars": min(times_v[1:]) * 1e3,
+            "ms_per_fold_prove_vars_median": float(np.median(times_v[1:])) * 1e3,
             "ms_per_linearize": t_lin * 1e3, "span_ms": spans, "ms_per_replay": min(t_rep) * 1e3,
+            "vars_equal_replay": vars_equal,
             "note": "beside the rho-as-input step of reference_ring: this adds the linearization (Mz, degree-8 "
                     "sumcheck), the decompositions' u_s / v_s, the folding sumcheck, theta_s / eta_s and the "
                     "transcript"}
+
+
+def zkvm_chain(LA, torch, ctx, M, S, d, n, t, m, steps=16, warmup=2):
+    """The zkvm's proving loop (zkvm/src/main.rs:121-219) at its shape, chained: every
+    step commits a new z (commit(), :348-367: the witness uploaded from the host,
+    Witness::from_w_ccs and the Ajtai commitment on the device), folds it into the
+    running accumulator with fold() + generate_verification_witness_vars
+    (lf_fold_prove_vars), and seals the step with acc_comm and ivc_step_comm
+    (:187-196; state_i_comm from register / code / memory commitments). The folded
+    accumulator and its witness feed the next step; the next z's public input
+    x_ccs is this step's ivc_step_comm (arithmetize, ivc.rs:107-109). The VM trace
+    itself is not reproducible here, so w_ccs is synthetic (seeded per step);
+    initialize_accumulator (:305-344) linearizes the zero witness."""
+    l, kappa, deg = 4, 32, 7
+    W = n - l - 1
+    pr = LA.goldilocks_dp(d)
+    N = W * pr.L
+    dev = f"cuda:{torch.cuda.current_device()}"
+    i64 = dict(dtype=torch.int64, device=dev)
+    A = torch.empty(kappa * N * d, **i64)
+    ctx.dev_fill_uniform(A, SEED_A)
+    sch = LA.AjtaiCommitmentScheme(ctx, device_tensor=A, kappa=kappa, ncols=N, d=d)
+    del A
+    rng = np.random.default_rng(0x4C460018)
+    c = rng.integers(0, 1 << 62, len(S) * d, dtype=np.uint64)
+    prover = LA.Prover(ctx, sch, pr, M, l, deg, c, S)
+    wit = lambda: {"w_ccs": torch.empty(W * d, **i64), "f": torch.empty(N * d, **i64),
+                   "f_coeff": torch.empty(N * d, **i64)}
+    accw, nxt, wi = wit(), wit(), wit()
+    # the synthetic VM witnesses, host-resident as arithmetize leaves them (pinned for the upload)
+    total = warmup + steps
+    zs = torch.empty((total, W * d), dtype=torch.int64).pin_memory()
+    tmp = torch.empty(W * d, **i64)
+    for i in range(total):
+        ctx.dev_fill_uniform(tmp, SEED_W + 31 * i)
+        zs[i].copy_(tmp)
+    del tmp
+    cm = torch.empty(kappa * d, **i64)
+    pr_c = LA._lib.C.byref(pr)
+
+    def broadcast4(comm):  # GoldilocksRingNTT::from(u64) of each limb (main.rs:320-325)
+        x = np.zeros(4 * d, np.uint64)
+        for k in range(4):
+            x[k * d:(k + 1) * d:3] = np.uint64(int(comm[k]))
+        return x
+
+    def commit(w):
+        ctx.check(ctx.lib.lf_dev_witness_from_w_ccs(ctx.h, pr_c, w["w_ccs"].data_ptr(), W, w["f_coeff"].data_ptr(),
+                                                    w["f"].data_ptr()))
+        ctx.dev_ajtai_commit(sch, [w["f"]], cm)
+        return cm.cpu().numpy().view(np.uint64).copy()
+
+    # initialize_accumulator: the zero witness, x_ccs = the zero step commitment
+    accw["w_ccs"].zero_()
+    zero4 = np.zeros(4, np.uint64)
+    cm0 = commit(accw)
+    acc, _ = prover.linearize(cm0, broadcast4(zero4), accw)
+    regs = np.arange(32, dtype=np.uint32)
+    # the VM's code / memory / memory-ops commitments (synthetic: the zkvm computes them
+    # with the width-8 Merkle trees, lf_vm_code_comm / lf_dev_merkle_tree)
+    code_comm, mem_comm, ops_comm = [LA.hash_iter(np.arange(4 * k, 4 * k + 4, dtype=np.uint64)) for k in range(3)]
+    z0_comm = LA.state_i_comm(code_comm, 0, mem_comm, LA.vm_regs_comm(regs), ops_comm)
+    acc_comm = LA.acc_comm(acc)
+    h, _ = LA.ivc_step_comm(0, z0_comm, z0_comm, acc_comm)
+    t_commit = t_fold = t_comm = 0.0
+    vv = pf = None
+    x_ccs = cm_i = None
+    for i in range(total):
+        if i == warmup:
+            torch.cuda.synchronize()
+            prover.timing(True)
+            t_start = time.perf_counter()
+        t0 = time.perf_counter()
+        x_ccs = broadcast4(h)  # z = [x_ccs | 1 | w_ccs]: the public input is the previous h_i
+        wi["w_ccs"].copy_(zs[i], non_blocking=True)
+        cm_i = commit(wi)
+        t1 = time.perf_counter()
+        prev_acc = acc
+        acc, pf, vv = prover.fold_prove(acc, accw, cm_i, x_ccs, wi, nxt, vars=True)
+        t2 = time.perf_counter()
+        regs[1] = i  # the VM state after step i (synthetic registers)
+        state_i = LA.state_i_comm(code_comm, 4 * (i + 1), mem_comm, LA.vm_regs_comm(regs), ops_comm)
+        acc_comm = LA.acc_comm(acc)
+        h, _ = LA.ivc_step_comm(i + 1, z0_comm, state_i, acc_comm)
+        t3 = time.perf_counter()
+        accw, nxt = nxt, accw  # the folded witness is the next step's w_acc
+        if i >= warmup:
+            t_commit += t1 - t0
+            t_fold += t2 - t1
+            t_comm += t3 - t2
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t_start
+    sp = prover.timing(False)
+    # the last step's vars against the standalone replay (a second transcript pass)
+    vr = prover.replay(prev_acc, cm_i, x_ccs, pf)
+    vars_equal = all(np.array_equal(vv[k], vr[k]) for k in vr)
+    del prover, sch
+    torch.cuda.empty_cache()
+    return {"workload": f"the zkvm proving loop (main.rs:121-219), {steps} chained steps at its shape: commit(z) "
+                        f"(upload + from_w_ccs + Ajtai), fold() + generate_verification_witness_vars "
+                        f"(lf_fold_prove_vars), acc_comm + state_i_comm + ivc_step_comm; Phi_72, W={W}, kappa={kappa}, "
+                        f"CCS t={t} x {m} rows, degree {deg}; synthetic VM witnesses, x_ccs = the previous h_i",
+            "value": steps / dt, "unit": "IVC steps/s", "steps": steps, "warmup": warmup, "ms_per_step": dt / steps * 1e3,
+            "ms_per_step_commit": t_commit / steps * 1e3, "ms_per_step_fold_vars": t_fold / steps * 1e3,
+            "ms_per_step_commitments": t_comm / steps * 1e3,
+            "span_ms_per_step": {k: v / steps for k, v in sp.items()},
+            "last_vars_equal_replay": vars_equal}
 
 
 EXCLUDED = ("outside the timed step (other tiers): the Poseidon2 transcript and challenge derivation (rho is an "

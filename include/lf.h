@@ -88,7 +88,8 @@ enum lf_status {
   LF_ERR_CHALLENGE_BYTES = 8,         /* ChallengeSetError::TooFewBytes */
   LF_ERR_DEVICE = 9,                  /* HIP runtime error (see lf_ctx_last_error) */
   LF_ERR_OUT_OF_MEMORY = 10,
-  LF_ERR_COMM = 11                    /* RCCL error (see lf_ctx_last_error) */
+  LF_ERR_COMM = 11,                   /* RCCL error (see lf_ctx_last_error) */
+  LF_ERR_VERIFICATION = 12            /* lf_fold_verify rejected the proof (which check: lf_verify_check) */
 };
 enum lf_repr { LF_REPR_CANONICAL = 0, LF_REPR_MONTGOMERY = 1 };
 
@@ -264,7 +265,11 @@ typedef struct {
    * N x 2 KiB, every coefficient's 16-bit sign|magnitude word, all K planes in
    * one (the decomposition's own packed input). With fk and fk_coeff all NULL
    * the planes are the decomposed witnesses' only form: the u64 rows (2 x 8 d B
-   * per element and plane) are not written; lf_dev_expand_planes makes them. */
+   * per element and plane) are not written; lf_dev_expand_planes makes them.
+   * d = 4096 (the fused path): N x K KiB, one byte per coefficient quad and plane
+   * (bit b = the digit of coefficient a + 1024 b is nonzero, bit 4 + b = that
+   * coefficient is negative; byte ((e K + k) 32 + r) 32 + j holds a = r + 32 j), and
+   * f_0 is folded from the operand rows. */
   uint64_t *planes[2];
 } lf_fold_step_bufs;
 /* packed digit planes (lf_fold_step_bufs.planes) of N elements -> the Witness forms of
@@ -541,7 +546,8 @@ enum {
   LF_SPAN_EVALUATIONS = 6,            /* theta_s, eta_s */
   LF_SPAN_FOLDING_TRANSCRIPT = 7,     /* theta_s, eta_s absorbed, get_rhos */
   LF_SPAN_FOLD = 8,                   /* CRT(rho), cm_0, f_0, from_f, v_0, u_0, x_0 */
-  LF_SPAN_COUNT = 9
+  LF_SPAN_VARS = 9,                   /* lf_fold_prove_vars: the verification vars from the sample log */
+  LF_SPAN_COUNT = 10
 };
 /* span_ms (LF_SPAN_COUNT, may be NULL) receives the sums so far; then timing is set to
  * `enable` and the sums are cleared */
@@ -616,6 +622,36 @@ typedef struct {
 /* the proof as lf_fold_prove wrote it (read only); repr describes every buffer, c included */
 int lf_fold_replay(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *acc, const uint64_t *cm_i,
                    const uint64_t *x_ccs, const lf_lfproof_mut *proof, lf_replay_vars *out, int repr);
+/* the same replay with its challenges taken from the prover's sample log
+ * (lf_prover_samples) instead of a second Poseidon2 pass: LF_ERR_INCORRECT_LENGTH
+ * unless the replay draws exactly the logged samples */
+int lf_fold_replay_samples(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *acc, const uint64_t *cm_i,
+                           const uint64_t *x_ccs, const lf_lfproof_mut *proof, const uint64_t *samples, size_t nsamples,
+                           lf_replay_vars *out, int repr);
+/* NIFSVerifier::verify (latticefold/src/nifs.rs:117-162) over the zkvm's public-input
+ * absorption, as main.rs:408-426 (verify_folding, the `debug` feature) runs it after every
+ * fold(): on the host, no device needed. LF_OK with the folded LCCCS in `out` (r s, v tau,
+ * cm kappa, u t, x_w l, h 1), or LF_ERR_VERIFICATION with the failed check in *failed. */
+enum lf_verify_check {
+  LF_VERIFY_OK = 0,
+  LF_VERIFY_LIN_SUMCHECK = 1,  /* a linearization sumcheck round: p(0) + p(1) != claim */
+  LF_VERIFY_LIN_CLAIM = 2,     /* e(r, beta) sum c_i prod u_j != the sumcheck's final claim */
+  LF_VERIFY_DEC_Y = 3,         /* sum_k b^k y_k != cm (either decomposition) */
+  LF_VERIFY_DEC_V = 4,
+  LF_VERIFY_DEC_U = 5,
+  LF_VERIFY_DEC_X = 6,
+  LF_VERIFY_FOLD_SUMCHECK = 7, /* a folding sumcheck round */
+  LF_VERIFY_FOLD_CLAIM = 8     /* compute_sumcheck_claim_expected_value != the final claim */
+};
+int lf_fold_verify(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *acc, const uint64_t *cm_i,
+                   const uint64_t *x_ccs, const lf_lfproof_mut *proof, lf_lcccs_mut *out, int *failed, int repr);
+/* every value the last lf_fold_prove sampled from its transcript (count returned, up to cap copied) */
+size_t lf_prover_samples(const lf_prover *prover, uint64_t *out, size_t cap);
+/* fold() then generate_verification_witness_vars (main.rs:175-185) in one call: lf_fold_prove,
+ * then the vars from its own sample log (bit-exact with lf_fold_replay; Phi_72 only) */
+int lf_fold_prove_vars(lf_prover *prover, const lf_lcccs *acc, const lf_witness *w_acc, const uint64_t *cm_i,
+                       const uint64_t *x_ccs, const lf_witness *w_i, lf_lcccs_mut *out, const lf_witness *w_out,
+                       lf_lfproof_mut *proof, lf_replay_vars *vars, int repr);
 
 /* ------------------------------------------------------------ host transcript (sequential) */
 lf_transcript *lf_transcript_new(void);
@@ -631,6 +667,16 @@ void lf_transcript_squeeze_bytes(lf_transcript *t, uint8_t *out, size_t n);
 int lf_transcript_get_short_challenges(lf_transcript *t, int d, size_t count, uint64_t *coeffs);
 /* WideZkVMPoseidon2::hash_iter (poseidon2.rs:206-235) */
 void lf_hash_iter(const uint64_t *in, size_t n, uint64_t out4[4]);
+/* sample log: lf_transcript_record starts (and clears) a log of every sampled value;
+ * lf_transcript_samples copies up to cap of them and returns the count. A playback
+ * transcript returns the logged samples in order and drops every observe, so a
+ * transcript pass that absorbs the same messages in the same order (a verifier's
+ * replay of a recorded proof) draws the same challenges without one permutation;
+ * lf_transcript_playback_status: LF_OK iff exactly the logged samples were drawn. */
+void lf_transcript_record(lf_transcript *t);
+size_t lf_transcript_samples(const lf_transcript *t, uint64_t *out, size_t cap);
+lf_transcript *lf_transcript_new_playback(const uint64_t *samples, size_t n);
+int lf_transcript_playback_status(const lf_transcript *t);
 
 /* ------------------------------------------------------------ IVC step commitments (zkvm/src/commitments.rs)
  * hash_iter's second output, IntermediateStates (poseidon2.rs:199-202): one

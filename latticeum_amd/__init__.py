@@ -507,10 +507,13 @@ class Prover:
         return fold_replay(self.pr, self.t, self.ccs.m, self.l, self.degree, self.c, self.S, self.kappa, acc, cm_i,
                            x_ccs, proof, repr)
 
-    def fold_prove(self, acc: dict, w_acc: dict, cm_i, x_ccs, w_i: dict, w_out: dict, repr: int = REPR_CANONICAL):
+    def fold_prove(self, acc: dict, w_acc: dict, cm_i, x_ccs, w_i: dict, w_out: dict, repr: int = REPR_CANONICAL,
+                   vars: bool = False):
         """acc: {r, v, cm, u, x_w, h} host arrays; w_*: {w_ccs, f, f_coeff} device tensors.
-        Returns (folded LCCCS dict, LFProof dict) as host arrays; w_out is filled."""
-        from ._lib import LfLcccs, LfLcccsMut, LfLfproofMut, LfRingSlice, LfWitness
+        Returns (folded LCCCS dict, LFProof dict) as host arrays; w_out is filled.
+        vars=True: lf_fold_prove_vars, returning (LCCCS, LFProof, verification vars) with
+        the vars replayed from the call's own sample log (keys as fold_replay's)."""
+        from ._lib import REPLAY_FIELDS, LfLcccs, LfLcccsMut, LfLfproofMut, LfReplayVars, LfRingSlice, LfWitness
         d, s, tau, t, l, K, kappa = self.d, self.s, self.tau, self.t, self.l, self.pr.K, self.kappa
         keep = {k: _u64(v) for k, v in acc.items()}
         sl = lambda a: LfRingSlice(a.ctypes.data, a.size // d)
@@ -538,15 +541,29 @@ class Prover:
         cm = _u64(cm_i)
         xc = _u64(x_ccs) if l else np.zeros(1, np.uint64)
         wa, wi, wo = wit(w_acc), wit(w_i), wit(w_out)
-        rc = self.lib.lf_fold_prove(self.h, C.byref(A), C.byref(wa), cm.ctypes.data, xc.ctypes.data, C.byref(wi),
-                                    C.byref(O_), C.byref(wo), C.byref(PM), repr)
+        if vars:
+            vout = {k: np.zeros(n * d, np.uint64) for k, n in replay_sizes(self.pr, self.t, self.ccs.m, l, self.degree,
+                                                                           len(self.S), kappa).items()}
+            V = LfReplayVars(*[vout[k].ctypes.data for k in REPLAY_FIELDS])
+            rc = self.lib.lf_fold_prove_vars(self.h, C.byref(A), C.byref(wa), cm.ctypes.data, xc.ctypes.data,
+                                             C.byref(wi), C.byref(O_), C.byref(wo), C.byref(PM), C.byref(V), repr)
+        else:
+            rc = self.lib.lf_fold_prove(self.h, C.byref(A), C.byref(wa), cm.ctypes.data, xc.ctypes.data, C.byref(wi),
+                                        C.byref(O_), C.byref(wo), C.byref(PM), repr)
         if rc:
             raise LfError(rc, self.lib.lf_prover_last_error(self.h).decode() or self.lib.lf_status_string(rc).decode())
         out["x_w"] = out["x_w"][:l * d]
-        return out, pf
+        return (out, pf, vout) if vars else (out, pf)
+
+    def samples(self) -> np.ndarray:
+        """every value the last fold_prove sampled from its transcript, in order"""
+        n = self.lib.lf_prover_samples(self.h, None, 0)
+        out = np.zeros(max(n, 1), np.uint64)
+        self.lib.lf_prover_samples(self.h, out.ctypes.data, n)
+        return out[:n]
 
     SPANS = ("public_input", "linearization", "decomposition", "decomposition_transcript", "folding_mles",
-             "folding_sumcheck", "evaluations", "folding_transcript", "fold")
+             "folding_sumcheck", "evaluations", "folding_transcript", "fold", "vars")
 
     def timing(self, enable: bool) -> dict:
         """the fold() phase spans (ms, summed) since the last call; then timing on/off"""
@@ -582,12 +599,25 @@ class Prover:
             pass
 
 
+def replay_sizes(params: LfParams, t: int, m: int, l: int, degree: int, q: int, kappa: int) -> dict:
+    """NTT elements of every lf_replay_vars field"""
+    K, bs, s = params.K, params.b_small, m.bit_length() - 1
+    return {"lin_beta": s, "lin_claimed_sums": s + 1, "lin_subterms": s * (degree + 2), "lin_point": s,
+            "lin_expected": 1, "lin_inner": 1, "lin_products": q, "lin_eq_xy": s, "lin_eq_factors": s,
+            "lin_eq_sub": s + 1, "alpha": 2 * K, "beta": s, "zeta": 2 * K, "mu": 2 * K, "claim_g1_h1": 2 * K,
+            "claim_g1_h2": 2 * K, "claim_g1_terms": 2 * K, "claim_g1": 1, "claim_g3_h": 2 * K * (t - 1),
+            "claim_g3_terms": 2 * K, "claim_g3": 1, "fold_claimed_sums": s + 1, "fold_subterms": s * (2 * bs + 1),
+            "fold_point": s, "fold_expected": 1, "should_equal_s": 1, "rho": 2 * K, "final_cm": 2 * K * kappa,
+            "final_u": 2 * K * t, "final_x": 2 * K * (l + 1)}
+
+
 def fold_replay(params: LfParams, t: int, m: int, l: int, degree: int, c, S, kappa: int, acc: dict, cm_i, x_ccs,
-                proof: dict, repr: int = REPR_CANONICAL) -> dict:
+                proof: dict, repr: int = REPR_CANONICAL, samples=None) -> dict:
     """generate_verification_witness_vars (zkvm/src/zk_latticefold.rs:111-148) on the
     host: replays a fold() proof (the dict Prover.fold_prove returns) and returns the
     in-CCS verifier's values, keyed as oracle/nifs.py fold_replay names them, each a
-    flat u64 array of NTT elements. Phi_72 only; no GPU involved."""
+    flat u64 array of NTT elements. Phi_72 only; no GPU involved. samples: the
+    prover's sample log (lf_fold_replay_samples: no second Poseidon2 pass)."""
     from ._lib import REPLAY_FIELDS, LfCcsDesc, LfLcccs, LfLfproofMut, LfReplayVars, LfRingSlice
     lib, d, K, bs = load(), params.d, params.K, params.b_small
     s, q = m.bit_length() - 1, len(S)
@@ -606,20 +636,69 @@ def fold_replay(params: LfParams, t: int, m: int, l: int, degree: int, c, S, kap
     for k in ("u_s", "v_s", "x_s", "y_s"):
         for side in range(2):
             getattr(PM, k)[side] = pf[k][side].ctypes.data
-    sizes = {"lin_beta": s, "lin_claimed_sums": s + 1, "lin_subterms": s * (degree + 2), "lin_point": s,
-             "lin_expected": 1, "lin_inner": 1, "lin_products": q, "lin_eq_xy": s, "lin_eq_factors": s,
-             "lin_eq_sub": s + 1, "alpha": 2 * K, "beta": s, "zeta": 2 * K, "mu": 2 * K, "claim_g1_h1": 2 * K,
-             "claim_g1_h2": 2 * K, "claim_g1_terms": 2 * K, "claim_g1": 1, "claim_g3_h": 2 * K * (t - 1),
-             "claim_g3_terms": 2 * K, "claim_g3": 1, "fold_claimed_sums": s + 1, "fold_subterms": s * (2 * bs + 1),
-             "fold_point": s, "fold_expected": 1, "should_equal_s": 1, "rho": 2 * K, "final_cm": 2 * K * kappa,
-             "final_u": 2 * K * t, "final_x": 2 * K * (l + 1)}
+    sizes = replay_sizes(params, t, m, l, degree, q, kappa)
     out = {k: np.zeros(sizes[k] * d, np.uint64) for k in REPLAY_FIELDS}
     V = LfReplayVars(*[out[k].ctypes.data for k in REPLAY_FIELDS])
     cm, xc = _u64(cm_i), (_u64(x_ccs) if l else np.zeros(1, np.uint64))
-    rc = lib.lf_fold_replay(C.byref(desc), C.byref(params), C.byref(A), cm.ctypes.data, xc.ctypes.data, C.byref(PM),
-                            C.byref(V), repr)
+    if samples is None:
+        rc = lib.lf_fold_replay(C.byref(desc), C.byref(params), C.byref(A), cm.ctypes.data, xc.ctypes.data,
+                                C.byref(PM), C.byref(V), repr)
+    else:
+        sm = _u64(samples) if len(samples) else np.zeros(1, np.uint64)
+        rc = lib.lf_fold_replay_samples(C.byref(desc), C.byref(params), C.byref(A), cm.ctypes.data, xc.ctypes.data,
+                                        C.byref(PM), sm.ctypes.data, len(samples), C.byref(V), repr)
     if rc:
         raise LfError(rc, "lf_fold_replay: " + lib.lf_status_string(rc).decode())
+    return out
+
+
+VERIFY_CHECKS = {1: "linearization sumcheck", 2: "linearization evaluation claim", 3: "decomposition recompose y",
+                 4: "decomposition recompose v", 5: "decomposition recompose u", 6: "decomposition recompose x",
+                 7: "folding sumcheck", 8: "folding evaluation claim"}
+
+
+class VerificationError(LfError):
+    def __init__(self, check: int):
+        super().__init__(12, VERIFY_CHECKS.get(check, str(check)))
+        self.check = check
+
+
+def fold_verify(params: LfParams, t: int, m: int, l: int, degree: int, c, S, kappa: int, acc: dict, cm_i, x_ccs,
+                proof: dict, repr: int = REPR_CANONICAL) -> dict:
+    """NIFSVerifier::verify of a fold() proof (lf_fold_verify; zkvm main.rs:408-426): the
+    folded LCCCS dict {r, v, cm, u, x_w, h}, or VerificationError naming the failed check.
+    Host only (Phi_72)."""
+    from ._lib import LfCcsDesc, LfLcccs, LfLcccsMut, LfLfproofMut, LfRingSlice
+    lib, d = load(), params.d
+    s, q = m.bit_length() - 1, len(S)
+    c = _u64(c)
+    off = np.zeros(q + 1, np.int32)
+    off[1:] = np.cumsum([len(x) for x in S])
+    idx = np.array([j for x in S for j in x] or [0], np.int32)
+    desc = LfCcsDesc(t, m, l, degree, q, c.ctypes.data, off.ctypes.data, idx.ctypes.data)
+    keep = {k: _u64(v) for k, v in acc.items()}
+    sl = lambda a: LfRingSlice(a.ctypes.data, a.size // d)
+    A = LfLcccs(d, sl(keep["r"]), sl(keep["v"]), sl(keep["cm"]), sl(keep["u"]), sl(keep["x_w"]), keep["h"].ctypes.data)
+    pf = {k: (_u64(v) if not isinstance(v, list) else [_u64(x) for x in v]) for k, v in proof.items()}
+    PM = LfLfproofMut()
+    for k in ("lin_sumcheck", "lin_v", "lin_u", "fold_sumcheck", "theta_s", "eta_s"):
+        setattr(PM, k, pf[k].ctypes.data)
+    for k in ("u_s", "v_s", "x_s", "y_s"):
+        for side in range(2):
+            getattr(PM, k)[side] = pf[k][side].ctypes.data
+    tau = 3 if d == 24 else 1
+    out = {"r": np.zeros(s * d, np.uint64), "v": np.zeros(tau * d, np.uint64), "cm": np.zeros(kappa * d, np.uint64),
+           "u": np.zeros(t * d, np.uint64), "x_w": np.zeros(max(l, 1) * d, np.uint64), "h": np.zeros(d, np.uint64)}
+    O_ = LfLcccsMut(*[out[k].ctypes.data for k in ("r", "v", "cm", "u", "x_w", "h")])
+    cm, xc = _u64(cm_i), (_u64(x_ccs) if l else np.zeros(1, np.uint64))
+    failed = C.c_int(0)
+    rc = lib.lf_fold_verify(C.byref(desc), C.byref(params), C.byref(A), cm.ctypes.data, xc.ctypes.data, C.byref(PM),
+                            C.byref(O_), C.byref(failed), repr)
+    if rc == 12:
+        raise VerificationError(failed.value)
+    if rc:
+        raise LfError(rc, "lf_fold_verify: " + lib.lf_status_string(rc).decode())
+    out["x_w"] = out["x_w"][:l * d]
     return out
 
 
@@ -827,5 +906,6 @@ def vm_mem_comm(words) -> np.ndarray:
 __all__ = ["Context", "AjtaiCommitmentScheme", "Communicator", "Comb", "CCSMatrices", "Prover", "witness_split_w", "Poseidon2Transcript",
            "LfParams", "LfFoldStepBufs", "merkle_nodes_len", "merkle_depth", "hash_w8", "vm_mem_comm",
            "LfError", "goldilocks_dp", "short_challenge", "hash_iter", "hash_iter_states", "acc_comm",
-           "ivc_step_comm", "state_i_comm", "vm_regs_comm", "vm_mem_ops_vec_comm", "P", "REPR_CANONICAL",
+           "ivc_step_comm", "state_i_comm", "vm_regs_comm", "vm_mem_ops_vec_comm", "fold_verify",
+           "VerificationError", "P", "REPR_CANONICAL",
            "REPR_MONTGOMERY", "load"]

@@ -189,6 +189,18 @@ SIGNATURES = {
     "lf_ctx_device": (I, [VP]),
     "lf_fold_replay": (I, [C.POINTER(LfCcsDesc), C.POINTER(LfParams), C.POINTER(LfLcccs), VP, VP,
                            C.POINTER(LfLfproofMut), C.POINTER(LfReplayVars), I]),
+    "lf_fold_verify": (I, [C.POINTER(LfCcsDesc), C.POINTER(LfParams), C.POINTER(LfLcccs), VP, VP,
+                           C.POINTER(LfLfproofMut), C.POINTER(LfLcccsMut), C.POINTER(I), I]),
+    "lf_fold_replay_samples": (I, [C.POINTER(LfCcsDesc), C.POINTER(LfParams), C.POINTER(LfLcccs), VP, VP,
+                                   C.POINTER(LfLfproofMut), VP, SZ, C.POINTER(LfReplayVars), I]),
+    "lf_prover_samples": (SZ, [VP, VP, SZ]),
+    "lf_fold_prove_vars": (I, [VP, C.POINTER(LfLcccs), C.POINTER(LfWitness), VP, VP, C.POINTER(LfWitness),
+                               C.POINTER(LfLcccsMut), C.POINTER(LfWitness), C.POINTER(LfLfproofMut),
+                               C.POINTER(LfReplayVars), I]),
+    "lf_transcript_record": (None, [VP]),
+    "lf_transcript_samples": (SZ, [VP, VP, SZ]),
+    "lf_transcript_new_playback": (VP, [VP, SZ]),
+    "lf_transcript_playback_status": (I, [VP]),
     "lf_dev_mz_mles": (I, [VP, VP, VP, I, I, VP]),
     "lf_dev_mz_challenged": (I, [VP, VP, VP, VP, I, I, VP]),
     "lf_dev_mz_evaluate": (I, [VP, VP, VP, I, I, VP, VP]),

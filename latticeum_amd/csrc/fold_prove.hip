@@ -41,17 +41,27 @@ struct lf_prover {
   uint64_t *theta = nullptr, *eta = nullptr, *rho = nullptr, *rhoc = nullptr, *cm0 = nullptr, *u0 = nullptr, *x0 = nullptr,
            *v0 = nullptr, *r0 = nullptr;
   std::string err;
+  // every value the last lf_fold_prove sampled from its transcript, in order
+  // (lf_fold_prove_vars replays the proof on them instead of a second sponge)
+  std::vector<uint64_t> samples;
   // tracing spans (the reference's #[instrument] spans, zkvm/src/main.rs:56-63):
   // wall ms of each fold() phase, measured with a stream sync at its end
   bool timing = false;
   double span_ms[LF_SPAN_COUNT] = {};
+  // pinned host staging: the messages the host absorbs come back through it with
+  // asynchronous copies (so the device keeps working while the host hashes), and
+  // the points the device needs go out through it
+  uint64_t *pin = nullptr;
+  uint64_t *hx[2] = {}, *hy[2] = {}, *hu[2] = {}, *hv[2] = {}, *hr[2] = {}, *htheta = nullptr, *heta = nullptr;
+  hipEvent_t ev[3] = {};
   ~lf_prover() {
-    if (mem) {
-      int prev = -1;
-      if (hipGetDevice(&prev) == hipSuccess && prev != device) (void)hipSetDevice(device);
-      (void)hipFree(mem);
-      if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
-    }
+    int prev = -1;
+    if (hipGetDevice(&prev) == hipSuccess && prev != device) (void)hipSetDevice(device);
+    if (mem) (void)hipFree(mem);
+    if (pin) (void)hipHostFree(pin);
+    for (auto &e : ev)
+      if (e) (void)hipEventDestroy(e);
+    if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
   }
 };
 
@@ -84,10 +94,12 @@ struct Run {
   int rc = LF_OK;
   std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
 
-  // close the span that ran since the last mark (only with timing on)
-  void mark(int span) {
+  // close the span that ran since the last mark (only with timing on); sync = false
+  // where the device work of the span overlaps the next span's host work (the
+  // span then ends when its work is enqueued, and the wait lands in the next one)
+  void mark(int span, bool sync = true) {
     if (!P->timing) return;
-    (void)hipStreamSynchronize(st);
+    if (sync) (void)hipStreamSynchronize(st);
     const auto now = std::chrono::steady_clock::now();
     P->span_ms[span] += std::chrono::duration<double, std::milli>(now - t0).count();
     t0 = now;
@@ -118,6 +130,17 @@ struct Run {
   int d2d(uint64_t *dst, const uint64_t *src, size_t elems) {
     return elems ? hip(hipMemcpyAsync(dst, src, elems * 8, hipMemcpyDeviceToDevice, st), "copy") : rc;
   }
+  // device -> pinned host, asynchronous (completion: an event recorded after it)
+  int d2p(uint64_t *dst, const uint64_t *src, size_t elems) {
+    return elems ? hip(hipMemcpyAsync(dst, src, elems * 8, hipMemcpyDeviceToHost, st), "download") : rc;
+  }
+  // host -> device through a pinned copy of the source (no stream synchronisation)
+  int h2p2d(uint64_t *dst, uint64_t *pinned, const uint64_t *src, size_t elems) {
+    if (!elems) return rc;
+    memcpy(pinned, src, elems * 8);
+    return hip(hipMemcpyAsync(dst, pinned, elems * 8, hipMemcpyHostToDevice, st), "upload");
+  }
+  int wait(hipEvent_t e) { return hip(hipEventSynchronize(e), "event wait"); }
   void absorb(const uint64_t *e, size_t n) { lf_transcript_absorb_ring(T, e, n, P->d, LF_REPR_CANONICAL); }
   // absorb_field_element(BaseRing::from_base_prime_field(from_be_bytes_mod_order(label)))
   void absorb_label(const char *label) {
@@ -299,6 +322,27 @@ int lf_prover_create(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, const
     *x.p = P->mem + off;
     off += (x.elems + 31) / 32 * 32;
   }
+  std::vector<Part> pins = {
+      {&P->hx[0], K * (l + 1) * d}, {&P->hx[1], K * (l + 1) * d}, {&P->hy[0], K * kd}, {&P->hy[1], K * kd},
+      {&P->hu[0], K * t * d}, {&P->hu[1], K * t * d}, {&P->hv[0], K * tau * d}, {&P->hv[1], K * tau * d},
+      {&P->hr[0], (size_t)P->s * d}, {&P->hr[1], (size_t)P->s * d}, {&P->htheta, 2 * K * tau * d},
+      {&P->heta, 2 * K * t * d}};
+  size_t ptotal = 0;
+  for (auto &x : pins) ptotal += (x.elems + 7) / 8 * 8;
+  if (hipGetDevice(&prev) == hipSuccess && prev != P->device) (void)hipSetDevice(P->device);
+  e = hipHostMalloc(reinterpret_cast<void **>(&P->pin), ptotal * 8, hipHostMallocDefault);
+  for (auto &ev : P->ev)
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  if (prev >= 0 && prev != P->device) (void)hipSetDevice(prev);
+  if (e != hipSuccess) {
+    delete P;
+    return e == hipErrorOutOfMemory ? LF_ERR_OUT_OF_MEMORY : LF_ERR_DEVICE;
+  }
+  off = 0;
+  for (auto &x : pins) {
+    *x.p = P->pin + off;
+    off += (x.elems + 7) / 8 * 8;
+  }
   *out = P;
   return LF_OK;
 }
@@ -393,6 +437,8 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
     lf_transcript *t;
     ~TGuard() { lf_transcript_free(t); }
   } tg{R.T};
+  lf_transcript_record(R.T);
+  P->samples.clear();
   int prev = -1;
   if (hipGetDevice(&prev) == hipSuccess && prev != P->device) (void)hipSetDevice(P->device);
   struct DGuard {
@@ -451,20 +497,40 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
       R.d2d(zk, P->xs + ((size_t)side * K + k) * (l + 1) * d, (l + 1) * d);
       R.d2d(zk + (l + 1) * d, P->wk[side] + (size_t)k * W * d, W * d);
     }
-  std::vector<uint64_t> r_side[2] = {ar, r_lin};
+  // per side: v_s, u_s at the side's point, then its messages back to pinned memory
+  // behind an event, so the host absorbs side 0 while the device evaluates side 1
+  // and prepares the challenge-independent folding MLEs (the f_hat MLEs of the 2K
+  // decomposed witnesses, eq(r_i); create_sumcheck_polynomial, folding/utils.rs:196-255)
+  const std::vector<uint64_t> *r_side[2] = {&ar, &r_lin};
+  uint64_t *M = P->fold;
+  const size_t mstride = nn * d;
   for (int side = 0; side < 2; side++) {
-    R.h2d(P->pt, r_side[side].data(), (size_t)s * d);
+    R.h2p2d(P->pt, P->hr[side], r_side[side]->data(), (size_t)s * d);
     R.check(lf_dev_fhat_evaluate(C, d, P->fkc[side], N, ND, K, s, P->pt, P->vs + (size_t)side * K * tau * d), "v_s");
     R.check(lf_dev_mz_evaluate(C, P->ccs, P->zdec[side], K, s, P->pt, P->us + (size_t)side * K * t * d), "u_s");
+    R.d2p(P->hx[side], P->xs + (size_t)side * K * (l + 1) * d, (size_t)K * (l + 1) * d);
+    R.d2p(P->hy[side], P->y[side], (size_t)K * kd);
+    R.d2p(P->hu[side], P->us + (size_t)side * K * t * d, (size_t)K * t * d);
+    R.d2p(P->hv[side], P->vs + (size_t)side * K * tau * d, (size_t)K * tau * d);
+    R.hip(hipEventRecord(P->ev[side], R.st), "event");
+  }
+  for (int side = 0; side < 2; side++)
+    for (int k = 0; k < K; k++)
+      R.check(lf_dev_get_fhat(C, d, P->fkc[side] + (size_t)k * ND, N, s, M + (5 + (size_t)(side * K + k) * tau) * mstride),
+              "f_hat");
+  for (int side = 0; side < 2; side++) {
+    // the pinned copy of r_side still holds the point: upload it again for eq(r_i)
+    R.hip(hipMemcpyAsync(P->pt, P->hr[side], (size_t)s * d * 8, hipMemcpyHostToDevice, R.st), "upload");
+    R.check(lf_dev_eq_table(C, d, P->pt, s, M + (size_t)(2 * side) * mstride), "eq(r_i)");
   }
   if (R.rc) return R.rc;
-  R.mark(LF_SPAN_DECOMPOSITION);
+  R.mark(LF_SPAN_DECOMPOSITION, false);
   for (int side = 0; side < 2; side++) {
-    R.d2h(proof->x_s[side], P->xs + (size_t)side * K * (l + 1) * d, (size_t)K * (l + 1) * d);
-    R.d2h(proof->y_s[side], P->y[side], (size_t)K * kd);
-    R.d2h(proof->u_s[side], P->us + (size_t)side * K * t * d, (size_t)K * t * d);
-    R.d2h(proof->v_s[side], P->vs + (size_t)side * K * tau * d, (size_t)K * tau * d);
-    if (R.rc) return R.rc;
+    if (R.wait(P->ev[side])) return R.rc;
+    memcpy(proof->x_s[side], P->hx[side], (size_t)K * (l + 1) * d * 8);
+    memcpy(proof->y_s[side], P->hy[side], (size_t)K * kd * 8);
+    memcpy(proof->u_s[side], P->hu[side], (size_t)K * t * d * 8);
+    memcpy(proof->v_s[side], P->hv[side], (size_t)K * tau * d * 8);
     for (int k = 0; k < K; k++) {  // the decomposed instances' messages (:58-64)
       R.absorb(proof->x_s[side] + (size_t)k * (l + 1) * d, l + 1);
       R.absorb(proof->y_s[side] + (size_t)k * kd, kappa);
@@ -473,7 +539,7 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
     }
   }
 
-  R.mark(LF_SPAN_DECOMPOSITION_TRANSCRIPT);
+  R.mark(LF_SPAN_DECOMPOSITION_TRANSCRIPT, false);
   // ---- folding (folding.rs:42-130)
   R.absorb_label("alpha_s");  // squeeze_alpha_beta_zeta_mu (folding/utils.rs:51-96)
   const std::vector<uint64_t> alpha = R.challenges(2 * K);
@@ -502,16 +568,9 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
     }
     R.h2d(P->coef[side], cf.data(), cf.size());
   }
-  // the MLEs [eq(r_0), g1, eq(r_1), g3, eq(beta), f_hat (2K x tau)] (create_sumcheck_polynomial, :196-255)
-  uint64_t *M = P->fold;
-  const size_t mstride = nn * d;
-  for (int side = 0; side < 2; side++)
-    for (int k = 0; k < K; k++)
-      R.check(lf_dev_get_fhat(C, d, P->fkc[side] + (size_t)k * ND, N, s, M + (5 + (size_t)(side * K + k) * tau) * mstride),
-              "f_hat");
+  // the MLEs [eq(r_0), g1, eq(r_1), g3, eq(beta), f_hat (2K x tau)] (create_sumcheck_polynomial,
+  // :196-255); the f_hat MLEs and eq(r_i) were enqueued before the decomposition transcript
   for (int side = 0; side < 2; side++) {
-    R.h2d(P->pt, r_side[side].data(), (size_t)s * d);
-    R.check(lf_dev_eq_table(C, d, P->pt, s, M + (size_t)(2 * side) * mstride), "eq(r_i)");
     uint64_t *g = M + (size_t)(2 * side + 1) * mstride;
     R.check(lf_dev_mz_challenged(C, P->ccs, P->zdec[side], P->zeta + (size_t)side * K * d, K, s, g), "challenged Mz");
     R.check(lf_dev_mle_lincomb(C, d, M + (5 + (size_t)side * K * tau) * mstride, mstride, K * tau, s, P->coef[side], g),
@@ -536,17 +595,27 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
   std::vector<uint64_t> r0((size_t)s * d);
   for (int i = 0; i < s; i++) broadcast(rnd.data() + (size_t)i * tb, tb, d, r0.data() + (size_t)i * d);
   R.h2d(P->r0, r0.data(), (size_t)s * d);
-  // theta_s = f_hat(w_i)(r_0), eta_s = MLE(M_j z_i)(r_0) (get_thetas / get_etas, :236-256)
-  for (int side = 0; side < 2; side++) {
+  // theta_s = f_hat(w_i)(r_0), eta_s = MLE(M_j z_i)(r_0) (get_thetas / get_etas, :236-256):
+  // theta_s and side 0's eta_s come back first, so the host absorbs them while the
+  // device evaluates side 1's eta_s
+  for (int side = 0; side < 2; side++)
     R.check(lf_dev_fhat_evaluate(C, d, P->fkc[side], N, ND, K, s, P->r0, P->theta + (size_t)side * K * tau * d), "theta");
+  R.d2p(P->htheta, P->theta, 2 * (size_t)K * tau * d);
+  for (int side = 0; side < 2; side++) {
     R.check(lf_dev_mz_evaluate(C, P->ccs, P->zdec[side], K, s, P->r0, P->eta + (size_t)side * K * t * d), "eta");
+    R.d2p(P->heta + (size_t)side * K * t * d, P->eta + (size_t)side * K * t * d, (size_t)K * t * d);
+    R.hip(hipEventRecord(P->ev[side], R.st), "event");
   }
-  R.d2h(proof->theta_s, P->theta, 2 * (size_t)K * tau * d);
-  R.d2h(proof->eta_s, P->eta, 2 * (size_t)K * t * d);
   if (R.rc) return R.rc;
-  R.mark(LF_SPAN_EVALUATIONS);
+  R.mark(LF_SPAN_EVALUATIONS, false);
+  if (R.wait(P->ev[0])) return R.rc;
+  memcpy(proof->theta_s, P->htheta, 2 * (size_t)K * tau * d * 8);
   for (int i = 0; i < 2 * K; i++) R.absorb(proof->theta_s + (size_t)i * tau * d, tau);
-  for (int i = 0; i < 2 * K; i++) R.absorb(proof->eta_s + (size_t)i * t * d, t);
+  for (int side = 0; side < 2; side++) {
+    if (side && R.wait(P->ev[1])) return R.rc;
+    memcpy(proof->eta_s + (size_t)side * K * t * d, P->heta + (size_t)side * K * t * d, (size_t)K * t * d * 8);
+    for (int k = 0; k < K; k++) R.absorb(proof->eta_s + ((size_t)side * K + k) * t * d, t);
+  }
   // get_rhos (folding/utils.rs:116-127): 2K - 1 short challenges and ONE, then CRT
   R.absorb_label("rho_s");
   std::vector<uint64_t> rc(2 * (size_t)K * d, 0);
@@ -576,6 +645,8 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
   R.check(lf_ctx_sync(C), "sync");
   if (R.rc) return R.rc;
   R.mark(LF_SPAN_FOLD);
+  P->samples.resize(lf_transcript_samples(R.T, nullptr, 0));
+  lf_transcript_samples(R.T, P->samples.data(), P->samples.size());
   memcpy(out->r, r0.data(), r0.size() * 8);
   if (l) memcpy(out->x_w, x0.data(), l * d * 8);
   memcpy(out->h, x0.data() + l * d, d * 8);
@@ -605,6 +676,43 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
     mont(proof->eta_s, 2 * (size_t)K * t * d);
   }
   return LF_OK;
+}
+
+// fold() followed by generate_verification_witness_vars (zk_latticefold.rs:111-148),
+// as main.rs:175-185 runs them: the vars come from a replay of the proof on this
+// call's own sample log (lf_fold_replay_samples) -- bit for bit what lf_fold_replay's
+// second Poseidon2 pass over the same messages gives, without the permutations
+int lf_fold_prove_vars(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, const uint64_t *cm_i,
+                       const uint64_t *x_ccs, const lf_witness *w_i, lf_lcccs_mut *out, const lf_witness *w_out,
+                       lf_lfproof_mut *proof, lf_replay_vars *vars, int repr) {
+  if (!vars) return LF_ERR_INVALID_ARG;
+  const int rc = lf_fold_prove(P, acc, w_acc, cm_i, x_ccs, w_i, out, w_out, proof, repr);
+  if (rc != LF_OK) return rc;
+  if (P->d != 24) return bad(P, LF_ERR_UNSUPPORTED_RING, "verification vars: Phi_72 only (TAU = 3)");
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<uint64_t> c = P->c;
+  if (repr == LF_REPR_MONTGOMERY)
+    for (auto &x : c) x = gl::to_mont(x);
+  lf_ccs_desc desc{};
+  desc.t = P->t;
+  desc.m = P->nn;
+  desc.l = P->l;
+  desc.degree = P->degree;
+  desc.q = P->q;
+  desc.c = c.data();
+  desc.S_off = P->S_off.data();
+  desc.S_idx = P->S_idx.data();
+  const int r = lf_fold_replay_samples(&desc, &P->pr, acc, cm_i, x_ccs, proof, P->samples.data(), P->samples.size(),
+                                       vars, repr);
+  if (P->timing)
+    P->span_ms[LF_SPAN_VARS] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return r == LF_OK ? LF_OK : bad(P, r, "verification vars replay");
+}
+
+size_t lf_prover_samples(const lf_prover *P, uint64_t *out, size_t cap) {
+  if (!P) return 0;
+  if (out) memcpy(out, P->samples.data(), (cap < P->samples.size() ? cap : P->samples.size()) * 8);
+  return P->samples.size();
 }
 
 }  // extern "C"

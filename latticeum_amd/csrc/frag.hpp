@@ -144,13 +144,16 @@ __device__ __forceinline__ size_t frag_column(int c, int t, int Lp, size_t Wp, b
 // transposition of its 16 columns for vectors v = vg, vg + 8, .. and
 // multiply-accumulates rho_v (.) f_v lazily; the 8 vector groups meet in LDS
 // (red: 512 x 9 u64) and each output column's 16 slots go out as one 128-B run.
-// 256 threads; block-uniform (it synchronises the block).
+// 256 threads; block-uniform (it synchronises the block). qd > 0: the operand slots
+// are quarter-major (FragGeom::qperm, d = 4096): operand slot o holds slot
+// (o % qd) 4 + o / qd, so one block's 16 operand slots are every 4th slot.
+__device__ __forceinline__ int frag_slot(int o, int qd) { return qd ? (o % qd) * 4 + o / qd : o; }
 __device__ __forceinline__ void fold_frag_block(size_t vb, const uint4 *frag, int nch, int Lp, size_t Wp,
                                                 const FoldRows &fr, const uint64_t *rho, int d, size_t N,
-                                                uint64_t *out, uint64_t *red) {
+                                                uint64_t *out, uint64_t *red, int qd = 0) {
   const int tid = threadIdx.x, vg = tid & 7, h = (tid >> 3) & 1, sl = (tid >> 4) & 3, qq = tid >> 6;
   const int ng = d >> 4, G = (int)(vb % ng), c = (int)(vb / ng);
-  const int s = 16 * G + 4 * qq + sl;
+  const int s = 16 * G + 4 * qq + sl, sr = frag_slot(s, qd);
   gl::CAcc acc[16];
 #pragma unroll
   for (int j = 0; j < 16; j++) gl::cacc_zero(acc[j]);
@@ -159,7 +162,7 @@ __device__ __forceinline__ void fold_frag_block(size_t vb, const uint4 *frag, in
     uint4 u[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) u[k] = pc[4 * k];
-    const uint64_t rv = rho[(size_t)fr.rho[v] * d + s];
+    const uint64_t rv = rho[(size_t)fr.rho[v] * d + sr];
     uint64_t x[16];
     fenc_untranspose16(u, x);
 #pragma unroll
@@ -177,7 +180,7 @@ __device__ __forceinline__ void fold_frag_block(size_t vb, const uint4 *frag, in
     for (int g = 1; g < 8; g++) t = gl::add(t, red[o * 9 + g]);
     bool ok;
     const size_t col = frag_column(c, j, Lp, Wp, ok);
-    if (ok && col < N) out[col * d + 16 * G + s16] = t;
+    if (ok && col < N) out[col * d + frag_slot(16 * G + s16, qd)] = t;
   }
   __syncthreads();  // red is free for the next virtual block
 }

@@ -140,7 +140,8 @@ struct FusedSides {
   int nside;
   int row_p0[2] = {-1, -1};                      // operand row of plane 0, or -1 (not written)
   uint2 *masks[2] = {nullptr, nullptr};          // d = 24, b_small = 2: digit masks [K][N] (nonzero, negative), or null
-  uint32_t *smg[2] = {nullptr, nullptr};         // packed sign|magnitude words: d = 1024 fused [N][512], d = 24 [N][12]
+  uint32_t *smg[2] = {nullptr, nullptr};         // packed sign|magnitude words: d = 1024 fused [N][512], d = 24 [N][12];
+                                                 // d = 4096 fused: [N][K][256] bytes (nibble | signs << 4)
 };
 // f_0 = sum_v rho_v f_v with every f_v read from the D8 operand rows (k_fold_frag)
 struct FoldRows {
@@ -204,6 +205,8 @@ hipError_t fold_phi72_masks(const uint2 *masks0, const uint2 *masks1, const uint
 hipError_t expand_phi72(const uint2 *planes, size_t n, uint64_t *fc, uint64_t *f, hipStream_t st);
 // d = 1024: the fused decomposition's packed sign|magnitude words of N elements -> f_coeff_k [K][N]
 hipError_t expand_sm(const uint32_t *smg, size_t N, int K, uint64_t *fck, hipStream_t st);
+// d = 4096: the fused decomposition's packed bytes (N K 256 words) -> f_coeff_k [K][N][4096]
+hipError_t expand_sm8(const uint32_t *sm8, size_t N, int K, uint64_t *fck, hipStream_t st);
 // d = 4096, b_small = 2 (kernels_n4k.hip): sm4 holds nside N 1024 packed words; sink 4096 words.
 // With frag (a scheme whose geometry has Lp = L and qperm), planes k >= 1 are also
 // written as operand rows row0[side] + k - 1, as decompose_fused does for d = 1024.

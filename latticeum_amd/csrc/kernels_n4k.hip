@@ -171,7 +171,7 @@ constexpr int FQ_LDS_U64 = FQ_T_U64 > FQ_S_U64 ? FQ_T_U64 : FQ_S_U64;
 
 // byte (element e, plane kb, lane r, k) at ((e K + kb) 32 + r) 32 + k; one
 // thread per (side, e, r, j) packs k = 4 j .. 4 j + 3 (one word per plane)
-__global__ void k_pack_sm8(FusedSides sd, size_t N, int K, uint32_t *sm8, int *err) {
+__global__ void k_pack_sm8(FusedSides sd, size_t N, int K, int *err) {
   const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // (side, element, r, j)
   if (t >= sd.nside * N * 256) return;
   const int side = t >= N * 256;
@@ -187,7 +187,7 @@ __global__ void k_pack_sm8(FusedSides sd, size_t N, int K, uint32_t *sm8, int *e
     for (int b = 0; b < 4; b++) w[k] |= spread4(sign_mag16(x[32 * k + b * Q4], K, bad)) << b;
   }
   if (bad) raise(err, 1);
-  uint32_t *o = sm8 + ((side * N + e) * K * 32 + r) * 8 + j;
+  uint32_t *o = sd.smg[side] + (e * K * 32 + r) * 8 + j;
   for (int kb = 0; kb < K; kb++) {
     uint32_t q = 0;
 #pragma unroll
@@ -198,7 +198,7 @@ __global__ void k_pack_sm8(FusedSides sd, size_t N, int K, uint32_t *sm8, int *e
 }
 
 template <bool NT>
-__global__ void __launch_bounds__(512, 1) k_decompose_n4k_fused(const uint32_t *sm8, size_t N, int L, int lb, int K,
+__global__ void __launch_bounds__(512, 1) k_decompose_n4k_fused(size_t N, int L, int lb, int K,
                                                                FusedSides sd, const uint64_t *mid_fg,
                                                                const uint64_t *tw_g, const uint64_t *ztab_g,
                                                                uint4 *frag, int nch, uint64_t *sink) {
@@ -226,7 +226,12 @@ __global__ void __launch_bounds__(512, 1) k_decompose_n4k_fused(const uint32_t *
     const bool ok = g < W;
     const size_t gg = ok ? g : 0;
     // this lane's 32 bytes of limb l: 8 words
-    auto bytes_of = [&](int l) { return sm8 + (((side * N + gg * L + l) * K + kb) * 32 + r) * 8; };
+    const uint32_t *sm8 = sd.smg[side];
+    auto bytes_of = [&](int l) { return sm8 + (((gg * L + l) * K + kb) * 32 + r) * 8; };
+    // f_coeff_k / f_k rows only when the caller keeps them (side-uniform); packed
+    // steps keep the bytes above as the decomposed witnesses' only form
+    uint64_t *fck = sd.f_coeff_k[side], *fk = sd.f_k[side];
+    const int row = kb > 0 ? sd.row0[side] + kb - 1 : sd.row_p0[side];
     uint32_t wn[8];
     {
       const uint4 *p = reinterpret_cast<const uint4 *>(bytes_of(L - 1));
@@ -252,27 +257,27 @@ __global__ void __launch_bounds__(512, 1) k_decompose_n4k_fused(const uint32_t *
         const uint4 a = p[0], c = p[1];
         wn[0] = a.x, wn[1] = a.y, wn[2] = a.z, wn[3] = a.w, wn[4] = c.x, wn[5] = c.y, wn[6] = c.z, wn[7] = c.w;
       }
-      {
-        uint64_t *oc = (ok ? sd.f_coeff_k[side] + e * D4 + m0 * Q4 : sink) + r;
+      if (fck) {
+        uint64_t *oc = (ok ? fck + e * D4 + m0 * Q4 : sink) + r;
 #pragma unroll
         for (int k = 0; k < 32; k++) out_store<NT>(&oc[32 * k], own[k]);
       }
 #pragma unroll
       for (int k = 0; k < 32; k++) v[k] = gl::mul(v[k], twl[r + 32 * k]);
       n32::forward(v, mid_f, T, r);
-      {
-        uint64_t *of = (ok ? sd.f_k[side] + e * D4 : sink) + m0 + 4 * r;
+      if (fk) {
+        uint64_t *of = (ok ? fk + e * D4 : sink) + m0 + 4 * r;
 #pragma unroll
         for (int i = 0; i < 32; i++) of[128 * n32::brv5(i)] = v[i];
       }
       horner_step(acc, v, l == L - 1, lb, b_pow);
-      if (kb > 0) {
+      if (row >= 0) {  // planes k >= 1, and plane 0 when it has a row (the f_k-free steps fold from the rows)
         __syncthreads();  // every wave is past its transpose: S may overwrite T
 #pragma unroll
         for (int i = 0; i < 32; i++) S[(r + 32 * n32::brv5(i)) * FQ_SROW + hw] = fenc(v[i]);
         __syncthreads();
         const size_t u = B * L + l;  // contraction unit of these 16 columns
-        const int c = (int)(u >> 1), uh = (int)(u & 1), row = sd.row0[side] + kb - 1;
+        const int c = (int)(u >> 1), uh = (int)(u & 1);
 #pragma unroll
         for (int rep = 0; rep < 2; rep++) {
           const int m1 = threadIdx.x + 512 * rep;
@@ -293,6 +298,28 @@ __global__ void __launch_bounds__(512, 1) k_decompose_n4k_fused(const uint32_t *
 #pragma unroll
     for (int i = 0; i < 32; i++) ow[128 * n32::brv5(i)] = gl::canon(acc[i]);
   }
+}
+
+// the packed bytes (k_pack_sm8's layout) -> the K digit planes in coefficient form:
+// f_coeff_k[k][e][a + 1024 b] = digit k of that coefficient, one thread per output
+__global__ void k_expand_sm8(const uint32_t *sm8, size_t N, int K, uint64_t *fck) {
+  const uint8_t *by = reinterpret_cast<const uint8_t *>(sm8);
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < (size_t)K * N * D4;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int j = (int)(t % D4), kb = (int)(t / ((size_t)N * D4));
+    const size_t e = (t / D4) % N;
+    const int a = j & (Q4 - 1), b = j >> 10, r = a & 31, k = a >> 5;
+    const uint32_t byte = by[((e * K + kb) * 32 + r) * 32 + k];
+    const uint32_t bit = (byte >> b) & 1u, neg = (byte >> (4 + b)) & 1u;
+    fck[t] = bit ? (neg ? gl::P - 1 : 1) : 0;
+  }
+}
+hipError_t expand_sm8(const uint32_t *sm8, size_t N, int K, uint64_t *fck, hipStream_t st) {
+  if (!N) return hipSuccess;
+  if (K < 1 || K > 15) return hipErrorInvalidValue;
+  const size_t n = (size_t)K * N * D4, nb = (n + 255) / 256;
+  hipLaunchKernelGGL(k_expand_sm8, dim3((unsigned)(nb < 65536 ? nb : 65536)), dim3(256), 0, st, sm8, N, K, fck);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- Witness::from_f / from_w_ccs, d = 4096
@@ -518,20 +545,25 @@ hipError_t decompose_n4k(const FusedSides &sd, size_t N, int lb, int L, int K, u
     return hipErrorInvalidValue;
   if (N == 0) return hipSuccess;
   if (frag) {
-    for (int s = 0; s < sd.nside; s++)
-      if (sd.row0[s] < 0 || sd.row0[s] + K - 1 > 32) return hipErrorInvalidValue;
+    FusedSides s8 = sd;
+    bool refold = false;
+    for (int s = 0; s < sd.nside; s++) {
+      if (sd.row0[s] < 0 || sd.row0[s] + K - 1 > 32 || sd.row_p0[s] > 32) return hipErrorInvalidValue;
+      // the packed bytes (N K 256 words per side): the caller's planes, else the scratch
+      if (!s8.smg[s]) s8.smg[s] = reinterpret_cast<uint32_t *>(sm4) + (size_t)s * N * K * 256;
+      refold |= sd.f_k[s] != nullptr;
+    }
     if (ncu < 32) return hipErrorInvalidValue;
-    uint32_t *sm8 = reinterpret_cast<uint32_t *>(sm4);  // nside N K 256 words
     const size_t threads = sd.nside * N * 256;
-    hipLaunchKernelGGL(k_pack_sm8, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, sd, N, K, sm8, err);
+    hipLaunchKernelGGL(k_pack_sm8, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, s8, N, K, err);
     // 32 blocks per group of 8 units (8 XCDs x 4 quarters), one block per CU
     const unsigned grid = (unsigned)(ncu / 32 * 32);
     // outputs: f_coeff_k, f_k, the operand rows (each K N d words per side) and w_ccs_k
-    if (dec_streaming(sd.nside * (size_t)K * N * D4 * 8 * 3, true))
-      hipLaunchKernelGGL(k_decompose_n4k_fused<true>, dim3(grid), dim3(512), 0, st, sm8, N, L, lb, K, sd, fwd.mid,
+    if (dec_streaming(sd.nside * (size_t)K * N * D4 * 8 * 3, refold))
+      hipLaunchKernelGGL(k_decompose_n4k_fused<true>, dim3(grid), dim3(512), 0, st, N, L, lb, K, s8, fwd.mid,
                          fwd.tw4, fwd.ztab, frag, nch, sink);
     else
-      hipLaunchKernelGGL(k_decompose_n4k_fused<false>, dim3(grid), dim3(512), 0, st, sm8, N, L, lb, K, sd, fwd.mid,
+      hipLaunchKernelGGL(k_decompose_n4k_fused<false>, dim3(grid), dim3(512), 0, st, N, L, lb, K, s8, fwd.mid,
                          fwd.tw4, fwd.ztab, frag, nch, sink);
     return hipGetLastError();
   }

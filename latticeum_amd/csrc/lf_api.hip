@@ -446,9 +446,12 @@ struct PhaseTimer {
 bool n4k_ok(const Tables *t, int d, int lbs, int K) { return d == 4096 && lbs == 1 && K <= 15 && t->fwd.tw4; }
 int decompose_n4k_sides(lf_ctx *c, const Tables *t, int nside, const uint64_t *const *fc, uint64_t *const *fck,
                         uint64_t *const *fk, uint64_t *const *wk, size_t N, int lb, int L, int K,
-                        uint4 *frag = nullptr, int nch = 0, const int *row0 = nullptr) {
-  // packed digits: one u64 per 4 coefficients, or (fused) one byte per 4 coefficients and plane
-  LF_TRY(grow(c, c->smg, c->smg_elems, (size_t)nside * N * (frag ? (size_t)K * 256 : 2048)));
+                        uint4 *frag = nullptr, int nch = 0, const int *row0 = nullptr, const int *row_p0 = nullptr,
+                        uint64_t *const *planes = nullptr) {
+  // packed digits: one u64 per 4 coefficients, or (fused) one byte per 4 coefficients and
+  // plane -- into the caller's planes when given (the packed step's decomposed witnesses)
+  const bool own = !(frag && planes && planes[0]);
+  if (own) LF_TRY(grow(c, c->smg, c->smg_elems, (size_t)nside * N * (frag ? (size_t)K * 256 : 2048)));
   c->smg_sides_n = 0;
   lfk::FusedSides sd{};
   sd.nside = nside;
@@ -458,9 +461,11 @@ int decompose_n4k_sides(lf_ctx *c, const Tables *t, int nside, const uint64_t *c
     sd.f_k[s] = fk[s];
     sd.w_ccs_k[s] = wk[s];
     sd.row0[s] = row0 ? row0[s] : 0;
+    sd.row_p0[s] = row_p0 ? row_p0[s] : -1;
+    if (!own) sd.smg[s] = reinterpret_cast<uint32_t *>(planes[s]);
   }
-  LF_HIP(c, lfk::decompose_n4k(sd, N, lb, L, K, reinterpret_cast<uint64_t *>(c->smg), t->fwd, c->d_err, c->sink,
-                               c->ncu, c->cur, frag, nch));
+  LF_HIP(c, lfk::decompose_n4k(sd, N, lb, L, K, own ? reinterpret_cast<uint64_t *>(c->smg) : nullptr, t->fwd, c->d_err,
+                               c->sink, c->ncu, c->cur, frag, nch));
   return LF_OK;
 }
 
@@ -502,8 +507,9 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
   c->masks24_n = 0;
   c->frag_fallback = false;
   if (b->planes[0] || b->planes[1]) {
-    if (!(fused24 || fused) || lbs != 1 || !b->planes[0] || !b->planes[1])
-      return fail(c, LF_ERR_INVALID_ARG, "packed planes: d = 24 or the fused d = 1024 path, b_small = 2, both sides");
+    if (!(fused24 || fused || fused4k) || lbs != 1 || !b->planes[0] || !b->planes[1])
+      return fail(c, LF_ERR_INVALID_ARG,
+                  "packed planes: d = 24 or the fused d = 1024 / 4096 paths, b_small = 2, both sides");
   }
   // X^1024 + 1 without f_k / f_coeff_k: the planes stay packed (the fused
   // decomposition's sign|magnitude words), f_0 comes from the coefficient-form
@@ -516,8 +522,11 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
     if (b->fk_coeff[0] || b->fk_coeff[1])
       return fail(c, LF_ERR_INVALID_ARG, "Phi_72: f_k and f_coeff_k are both given or both NULL");
   } else if (no_fk) {
-    if (!fused) return fail(c, LF_ERR_INVALID_ARG, "f_k buffers may be omitted only on the fused X^1024+1 path");
-    if (!packed1024 && (!b->fk_coeff[0] || !b->fk_coeff[1]))
+    if (!fused && !fused4k)
+      return fail(c, LF_ERR_INVALID_ARG, "f_k buffers may be omitted only on the fused X^1024+1 / X^4096+1 paths");
+    if (fused4k && (b->fk_coeff[0] || b->fk_coeff[1]) && !(b->fk_coeff[0] && b->fk_coeff[1]))
+      return fail(c, LF_ERR_INVALID_ARG, "f_coeff_k: both sides or neither");
+    if (fused && !packed1024 && (!b->fk_coeff[0] || !b->fk_coeff[1]))
       return fail(c, LF_ERR_INVALID_ARG, "f_coeff_k: both sides or neither");
     if (extra + 2 * (K - 1) + 2 > LF_MAX_VECS) return fail(c, LF_ERR_INVALID_ARG, "too many operand rows");
     lfk::FoldRows &fr = c->fold_rows;
@@ -536,10 +545,13 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
   if (fused || fused24 || fused4k) {
     LF_TRY(grow(c, c->frag, c->frag_elems, lfk::frag_elems(aj->geom, d)));
     if (fused4k) {
+      // without f_k, plane 0 of each side gets an operand row too and f_0 is folded
+      // from the rows (fold_finish: k_fold_frag over the quarter-major slots)
       const int row0[2] = {extra, extra + K - 1};
+      const int row_p0[2] = {no_fk ? extra + 2 * (K - 1) : -1, no_fk ? extra + 2 * (K - 1) + 1 : -1};
       PhaseTimer pt(c, LF_PHASE_DECOMPOSE);  // both sides in one launch
       LF_TRY(decompose_n4k_sides(c, t, 2, fc_side, b->fk_coeff, b->fk, b->wk, N, lb, L, K, c->frag, aj->geom.nch,
-                                 row0));
+                                 row0, row_p0, b->planes));
     } else if (fused) {
       // the packed words go straight into the caller's planes when given
       if (!b->planes[0]) LF_TRY(grow(c, c->smg, c->smg_elems, 2 * N * 512));
@@ -846,6 +858,7 @@ const char *lf_status_string(int s) {
     case LF_ERR_DEVICE: return "HIP device error";
     case LF_ERR_OUT_OF_MEMORY: return "out of device memory";
     case LF_ERR_COMM: return "RCCL communicator error";
+    case LF_ERR_VERIFICATION: return "the folding proof does not verify";
   }
   return "unknown status";
 }
@@ -1886,11 +1899,15 @@ int lf_dev_expand_planes(lf_ctx *c, const lf_params *pr, const uint64_t *planes,
     LF_HIP(c, lfk::expand_phi72(reinterpret_cast<const uint2 *>(planes), (size_t)K * N, fck, fk, c->cur));
     return LF_OK;
   }
-  if (d != 1024 || K > 15) return fail(c, LF_ERR_UNSUPPORTED_RING, "packed planes: d = 24 or 1024");
+  if ((d != 1024 && d != 4096) || K > 15) return fail(c, LF_ERR_UNSUPPORTED_RING, "packed planes: d = 24, 1024 or 4096");
   if (!fck && !fk) return LF_OK;
-  // sign|magnitude words -> f_coeff_k, then f_k = NTT(f_coeff_k) (CRT::elementwise_crt)
+  // sign|magnitude words (d = 4096: the digit bytes) -> f_coeff_k, then f_k = NTT(f_coeff_k)
+  // (CRT::elementwise_crt)
   uint64_t *dst = fck ? fck : fk;
-  LF_HIP(c, lfk::expand_sm(reinterpret_cast<const uint32_t *>(planes), N, K, dst, c->cur));
+  if (d == 1024)
+    LF_HIP(c, lfk::expand_sm(reinterpret_cast<const uint32_t *>(planes), N, K, dst, c->cur));
+  else
+    LF_HIP(c, lfk::expand_sm8(reinterpret_cast<const uint32_t *>(planes), N, K, dst, c->cur));
   if (fk) {
     if (fck) LF_HIP(c, hipMemcpyAsync(fk, fck, (size_t)K * N * d * 8, hipMemcpyDeviceToDevice, c->cur));
     LF_TRY(lf_dev_crt(c, fk, (size_t)K * N, d));

@@ -73,7 +73,8 @@ Elem at(const uint64_t *p, size_t i) { return Elem(p + i * D, p + (i + 1) * D); 
 void put(uint64_t *p, size_t i, const Elem &e) { memcpy(p + i * D, e.data(), D * 8); }
 
 struct Tr {
-  lf_transcript *t = lf_transcript_new();
+  lf_transcript *t;
+  explicit Tr(lf_transcript *tt) : t(tt) {}
   ~Tr() { lf_transcript_free(t); }
   void absorb(const uint64_t *e, size_t n) { lf_transcript_absorb_ring(t, e, n, D, LF_REPR_CANONICAL); }
   void absorb(const Elem &e) { absorb(e.data(), 1); }
@@ -150,12 +151,12 @@ Elem eq(const uint64_t *x, const uint64_t *y, int n, uint64_t *xy, uint64_t *fac
   return res;
 }
 
-}  // namespace
-
-extern "C" {
-
-int lf_fold_replay(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *acc, const uint64_t *cm_i,
-                   const uint64_t *x_ccs, const lf_lfproof_mut *proof, lf_replay_vars *out, int repr) {
+// the replay on transcript `tr` (owned: freed here) -- a fresh one, or a playback
+// of the prover's own sample log
+int replay(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *acc, const uint64_t *cm_i,
+           const uint64_t *x_ccs, const lf_lfproof_mut *proof, lf_replay_vars *out, int repr, lf_transcript *tr) {
+  Tr T(tr);
+  if (!tr) return LF_ERR_INVALID_ARG;
   if (!ccs || !pr || !acc || !cm_i || !proof || !out) return LF_ERR_INVALID_ARG;
   if (pr->d != D || acc->d != D) return LF_ERR_UNSUPPORTED_RING;  // TAU = 3 (zk_latticefold.rs:487)
   const int t = ccs->t, q = ccs->q, degree = ccs->degree;
@@ -196,7 +197,6 @@ int lf_fold_replay(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *
     xs[side] = cp(proof->x_s[side], (size_t)K * (l + 1) * D);
     ys[side] = cp(proof->y_s[side], (size_t)K * kappa * D);
   }
-  Tr T;
   // absorb_public_input (:162-184)
   T.label("acc");
   T.absorb(ar.data(), s);
@@ -313,6 +313,8 @@ int lf_fold_replay(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *
     for (size_t j = 0; j <= l; j++)
       put(out->final_x, (size_t)i * (l + 1) + j, mul(at(xs[side].data() + (size_t)k * (l + 1) * D, j), r));
   }
+  const int pb = lf_transcript_playback_status(T.t);
+  if (pb != LF_ERR_INVALID_ARG && pb != LF_OK) return pb;  // a playback must draw exactly the logged samples
   if (repr == LF_REPR_MONTGOMERY) {
     uint64_t *bufs[] = {out->lin_beta, out->lin_claimed_sums, out->lin_subterms, out->lin_point, out->lin_expected,
                         out->lin_inner, out->lin_products, out->lin_eq_xy, out->lin_eq_factors, out->lin_eq_sub,
@@ -330,6 +332,152 @@ int lf_fold_replay(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *
       for (size_t i = 0; i < lens[b] * D; i++) bufs[b][i] = gl::to_mont(bufs[b][i]);
   }
   return LF_OK;
+}
+
+// RotSum of the short challenges (coefficient form) with the flattened theta_i:
+// v0[j][c] = sum_i sum_r theta_i[r][c] coeff_j(X^r rho_i) (rotation.rs:84-101), Phi_72
+// (X^24 = X^12 - 1, X^36 = -1); the host twin of kernels.hip k_rot_lin
+uint64_t rot_coeff(const uint64_t *a, int j, int r) {
+  uint64_t v = j >= r ? a[j - r] : 0;
+  if (j >= 12 && r > j - 12) v = gl::add(v, a[j + 12 - r]);
+  if (j < 12 && r > j) v = gl::sub(v, a[j + 24 - r]);
+  if (j < 12 && r > j + 12) v = gl::sub(v, a[j + 36 - r]);
+  return v;
+}
+
+bool same(const uint64_t *a, const Elem &b) { return memcmp(a, b.data(), D * 8) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int lf_fold_verify(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *acc, const uint64_t *cm_i,
+                   const uint64_t *x_ccs, const lf_lfproof_mut *proof, lf_lcccs_mut *out, int *failed, int repr) {
+  if (failed) *failed = LF_VERIFY_OK;
+  if (!ccs || !pr || !acc || !cm_i || !proof || !out) return LF_ERR_INVALID_ARG;
+  if (pr->d != D || acc->d != D) return LF_ERR_UNSUPPORTED_RING;
+  if (repr != LF_REPR_CANONICAL && repr != LF_REPR_MONTGOMERY) return LF_ERR_INVALID_ARG;
+  const int t = ccs->t, q = ccs->q, degree = ccs->degree, K = pr->K, bs = (int)pr->b_small, tau = 3;
+  const size_t m = ccs->m, l = ccs->l, kappa = acc->cm.n;
+  int s = 0;
+  while (m && ((size_t)1 << s) < m) s++;
+  // the replay draws the challenges and forms every claim (generate_verification_witness_vars
+  // computes exactly what NIFSVerifier::verify checks, nifs.rs:117-162)
+  const size_t L1 = l + 1;
+  std::vector<uint64_t> vb[30];
+  const size_t lens[30] = {(size_t)s, (size_t)s + 1, (size_t)s * (degree + 2), (size_t)s, 1, 1, (size_t)q, (size_t)s,
+                           (size_t)s, (size_t)s + 1, 2 * (size_t)K, (size_t)s, 2 * (size_t)K, 2 * (size_t)K,
+                           2 * (size_t)K, 2 * (size_t)K, 2 * (size_t)K, 1, 2 * (size_t)K * (t > 1 ? t - 1 : 1),
+                           2 * (size_t)K, 1, (size_t)s + 1, (size_t)s * (2 * bs + 1), (size_t)s, 1, 1, 2 * (size_t)K,
+                           2 * (size_t)K * kappa, 2 * (size_t)K * t, 2 * (size_t)K * L1};
+  for (int i = 0; i < 30; i++) vb[i].assign(lens[i] * D, 0);
+  lf_replay_vars V;
+  uint64_t **f = reinterpret_cast<uint64_t **>(&V);
+  for (int i = 0; i < 30; i++) f[i] = vb[i].data();
+  const int rc = replay(ccs, pr, acc, cm_i, x_ccs, proof, &V, repr, lf_transcript_new());
+  if (rc != LF_OK) return rc;
+  if (repr == LF_REPR_MONTGOMERY)
+    for (auto &v : vb)
+      for (auto &x : v) x = gl::from_mont(x);
+  auto cp = [&](const uint64_t *p, size_t elems) {
+    std::vector<uint64_t> v(p, p + elems);
+    if (repr == LF_REPR_MONTGOMERY)
+      for (auto &x : v) x = gl::from_mont(x);
+    return v;
+  };
+  auto reject = [&](int what) {
+    if (failed) *failed = what;
+    return LF_ERR_VERIFICATION;
+  };
+  // sumcheck rounds (verifier.rs): p_i(0) + p_i(1) = the running claim
+  auto rounds = [&](const std::vector<uint64_t> &msgs, int deg1, const uint64_t *claimed) {
+    for (int i = 0; i < s; i++) {
+      const uint64_t *p0 = msgs.data() + (size_t)i * deg1 * D;
+      if (!same(claimed + (size_t)i * D, add(at(p0, 0), at(p0, 1)))) return false;
+    }
+    return true;
+  };
+  const auto lsc = cp(proof->lin_sumcheck, (size_t)s * (degree + 2) * D);
+  if (!rounds(lsc, degree + 2, vb[1].data())) return reject(LF_VERIFY_LIN_SUMCHECK);
+  // linearization.rs:265-285: e(r, beta) sum_i c_i prod_{j in S_i} u_j = the final claim
+  if (!same(vb[4].data(), mul(at(vb[9].data(), s), at(vb[5].data(), 0)))) return reject(LF_VERIFY_LIN_CLAIM);
+  // decomposition.rs:90-155: every decomposed vector recomposes (b^k weights) to its source
+  const auto lv = cp(proof->lin_v, tau * D), lu = cp(proof->lin_u, (size_t)t * D);
+  const auto acm = cp(acc->cm.elems, kappa * D), av = cp(acc->v.elems, tau * D), au = cp(acc->u.elems, (size_t)t * D),
+             axw = cp(acc->x_w.elems, l * D), ah = cp(acc->h, D), cmi = cp(cm_i, kappa * D),
+             xc = cp(x_ccs ? x_ccs : cm_i, x_ccs ? l * D : 0);
+  std::vector<uint64_t> xh[2] = {axw, xc};
+  xh[0].insert(xh[0].end(), ah.begin(), ah.end());
+  const Elem onev = one();
+  xh[1].insert(xh[1].end(), onev.begin(), onev.end());
+  const std::vector<uint64_t> *src_cm[2] = {&acm, &cmi}, *src_v[2] = {&av, &lv}, *src_u[2] = {&au, &lu};
+  for (int side = 0; side < 2; side++) {
+    const auto ys = cp(proof->y_s[side], (size_t)K * kappa * D), vs = cp(proof->v_s[side], (size_t)K * tau * D),
+               us = cp(proof->u_s[side], (size_t)K * t * D), xs = cp(proof->x_s[side], (size_t)K * L1 * D);
+    struct Chk {
+      const std::vector<uint64_t> &parts, &want;
+      size_t n;
+      int code;
+    } chks[4] = {{ys, *src_cm[side], kappa, LF_VERIFY_DEC_Y}, {vs, *src_v[side], (size_t)tau, LF_VERIFY_DEC_V},
+                 {us, *src_u[side], (size_t)t, LF_VERIFY_DEC_U}, {xs, xh[side], L1, LF_VERIFY_DEC_X}};
+    for (const Chk &c : chks)
+      for (size_t j = 0; j < c.n; j++) {
+        Elem acc_e = zero();
+        uint64_t bk = 1;
+        for (int k = 0; k < K; k++) {
+          acc_e = add(acc_e, mul(at(c.parts.data(), (size_t)k * c.n + j), fromu(bk)));
+          bk = gl::mul(bk, pr->b_small % gl::P);
+        }
+        if (!same(c.want.data() + j * D, acc_e)) return reject(c.code);
+      }
+  }
+  // folding.rs:133-200: the rounds from sum_i (alpha_i powers . v_i + zeta_i powers . u_i)
+  // (the replay's claim_g1 + claim_g3), then the expected evaluation
+  const auto fsc = cp(proof->fold_sumcheck, (size_t)s * (2 * bs + 1) * D);
+  if (!rounds(fsc, 2 * bs + 1, vb[21].data())) return reject(LF_VERIFY_FOLD_SUMCHECK);
+  if (!same(vb[24].data(), at(vb[25].data(), 0))) return reject(LF_VERIFY_FOLD_CLAIM);
+  // the folded instance (compute_v0_u0_x0_cm_0, folding/utils.rs:456-517; prepare_public_output)
+  std::vector<uint64_t> cm0(kappa * D, 0), u0((size_t)t * D, 0), x0(L1 * D, 0), v0(tau * D, 0);
+  for (int i = 0; i < 2 * K; i++) {
+    for (size_t j = 0; j < kappa; j++) put(cm0.data(), j, add(at(cm0.data(), j), at(vb[27].data(), (size_t)i * kappa + j)));
+    for (int j = 0; j < t; j++) put(u0.data(), j, add(at(u0.data(), j), at(vb[28].data(), (size_t)i * t + j)));
+    for (size_t j = 0; j < L1; j++) put(x0.data(), j, add(at(x0.data(), j), at(vb[29].data(), (size_t)i * L1 + j)));
+  }
+  const auto th = cp(proof->theta_s, 2 * (size_t)K * tau * D);
+  for (int i = 0; i < 2 * K; i++) {
+    uint64_t rc_i[D];
+    memcpy(rc_i, vb[26].data() + (size_t)i * D, D * 8);
+    ring::phi72_icrt(rc_i);  // rho_i in coefficient form
+    const uint64_t *ti = th.data() + (size_t)i * tau * D;  // theta_i flattened: 24 Fq3 values
+    for (int j = 0; j < D; j++)
+      for (int c = 0; c < 3; c++) {
+        uint64_t acc_v = v0[(size_t)j * 3 + c];
+        for (int r = 0; r < D; r++) acc_v = gl::add(acc_v, gl::mul(ti[(size_t)r * 3 + c], rot_coeff(rc_i, j, r)));
+        v0[(size_t)j * 3 + c] = acc_v;
+      }
+  }
+  auto emit = [&](uint64_t *dst, const uint64_t *src, size_t elems) {
+    for (size_t i = 0; i < elems; i++) dst[i] = repr == LF_REPR_MONTGOMERY ? gl::to_mont(src[i]) : src[i];
+  };
+  emit(out->r, vb[23].data(), (size_t)s * D);
+  emit(out->v, v0.data(), tau * D);
+  emit(out->cm, cm0.data(), kappa * D);
+  emit(out->u, u0.data(), (size_t)t * D);
+  if (l) emit(out->x_w, x0.data(), l * D);
+  emit(out->h, x0.data() + l * D, D);
+  return LF_OK;
+}
+
+int lf_fold_replay(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *acc, const uint64_t *cm_i,
+                   const uint64_t *x_ccs, const lf_lfproof_mut *proof, lf_replay_vars *out, int repr) {
+  return replay(ccs, pr, acc, cm_i, x_ccs, proof, out, repr, lf_transcript_new());
+}
+
+int lf_fold_replay_samples(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *acc, const uint64_t *cm_i,
+                           const uint64_t *x_ccs, const lf_lfproof_mut *proof, const uint64_t *samples, size_t nsamples,
+                           lf_replay_vars *out, int repr) {
+  if (!samples && nsamples) return LF_ERR_INVALID_ARG;
+  return replay(ccs, pr, acc, cm_i, x_ccs, proof, out, repr, lf_transcript_new_playback(samples, nsamples));
 }
 
 }  // extern "C"

@@ -217,6 +217,14 @@ void sponge8(Next next, size_t n, uint64_t out4[4]) {
 struct lf_transcript {
   uint64_t state[16] = {0};
   std::vector<uint64_t> in, out;
+  // record: every sampled value is appended to `log`. playback: samples come
+  // from `log` in order and observes are dropped -- a transcript that absorbs
+  // the same messages in the same order samples the same values, so a replay of
+  // a recorded proof needs no permutation at all
+  bool recording = false, playback = false;
+  std::vector<uint64_t> log;
+  size_t pos = 0;
+  bool underrun = false;
   void duplexing() {  // Plonky3 DuplexChallenger::duplexing (overwrite mode)
     for (size_t i = 0; i < in.size(); i++) state[i] = in[i];
     in.clear();
@@ -231,16 +239,43 @@ lf_transcript *lf_transcript_new(void) { return new lf_transcript; }
 void lf_transcript_free(lf_transcript *t) { delete t; }
 
 void lf_transcript_observe(lf_transcript *t, uint64_t v) {
+  if (t->playback) return;
   t->out.clear();
   t->in.push_back(gl::canon(v));
   if (t->in.size() == 12) t->duplexing();
 }
 
 uint64_t lf_transcript_sample(lf_transcript *t) {
+  if (t->playback) {
+    if (t->pos < t->log.size()) return t->log[t->pos++];
+    t->underrun = true;
+    return 0;
+  }
   if (!t->in.empty() || t->out.empty()) t->duplexing();
   uint64_t v = t->out.back();
   t->out.pop_back();
+  if (t->recording) t->log.push_back(v);
   return v;
+}
+
+void lf_transcript_record(lf_transcript *t) {
+  t->recording = true;
+  t->log.clear();
+}
+size_t lf_transcript_samples(const lf_transcript *t, uint64_t *out, size_t cap) {
+  if (out) memcpy(out, t->log.data(), (cap < t->log.size() ? cap : t->log.size()) * sizeof(uint64_t));
+  return t->log.size();
+}
+lf_transcript *lf_transcript_new_playback(const uint64_t *samples, size_t n) {
+  if (!samples && n) return nullptr;
+  lf_transcript *t = new lf_transcript;
+  t->playback = true;
+  t->log.assign(samples, samples + n);
+  return t;
+}
+int lf_transcript_playback_status(const lf_transcript *t) {
+  if (!t->playback) return LF_ERR_INVALID_ARG;
+  return t->underrun || t->pos != t->log.size() ? LF_ERR_INCORRECT_LENGTH : LF_OK;
 }
 
 void lf_transcript_absorb_ring(lf_transcript *t, const uint64_t *e, size_t n, int d, int repr) {

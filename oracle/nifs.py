@@ -117,9 +117,15 @@ def powers_dot(base, vals, d: int):
 
 # ---------------------------------------------------------------- transcript (ZK/fiat_shamir.rs)
 class Transcript:
-    def __init__(self, d: int):
+    def __init__(self, d: int, log: list | None = None):
         self.d = d
         self.t = O.new_transcript()
+        self.log = log  # a list: every sampled value is appended (the product's sample log)
+
+    def _sample(self) -> int:
+        v = O.lib().lfo_tr_sample(O.C.byref(self.t))
+        self.log.append(int(v))
+        return v
 
     def absorb(self, elems):
         e = O._u64(elems)
@@ -136,9 +142,14 @@ class Transcript:
         project's convention for the X^d + 1 rings)"""
         if tb(self.d) == 3:
             out = np.zeros(3, np.uint64)
-            O.lib().lfo_tr_get_challenge(O.C.byref(self.t), out)
+            if self.log is None:
+                O.lib().lfo_tr_get_challenge(O.C.byref(self.t), out)
+            else:  # lfo_tr_get_challenge's three samples, then their observes
+                out[:] = [self._sample() for _ in range(3)]
+                for v in out:
+                    O.lib().lfo_tr_observe(O.C.byref(self.t), int(v))
             return out
-        v = O.lib().lfo_tr_sample(O.C.byref(self.t))
+        v = O.lib().lfo_tr_sample(O.C.byref(self.t)) if self.log is None else self._sample()
         O.lib().lfo_tr_observe(O.C.byref(self.t), v)
         return np.array([v], np.uint64)
 
@@ -147,6 +158,8 @@ class Transcript:
         return [scal(self.get_challenge(), self.d) for _ in range(n)]
 
     def squeeze_bytes(self, n: int) -> bytes:
+        if self.log is not None:  # lfo_tr_squeeze_bytes: one sample per 8 bytes, little-endian
+            return b"".join(int(self._sample()).to_bytes(8, "little") for _ in range(-(-n // 8)))[:n]
         out = np.zeros(n, np.uint8)
         O.lib().lfo_tr_squeeze_bytes(O.C.byref(self.t), out, n)
         return out.tobytes()
@@ -714,12 +727,13 @@ def replay_sumcheck(tr: Transcript, proof, nv: int, degree: int, claim):
             "expected": claimed[-1]}
 
 
-def fold_replay(ccs: CCS, acc: LCCCS, cm_i, x_ccs, proof: Proof, pr: Params):
+def fold_replay(ccs: CCS, acc: LCCCS, cm_i, x_ccs, proof: Proof, pr: Params, log: list | None = None):
     """generate_verification_witness_vars (ZK/zk_latticefold.rs:111-148): the
-    transcript replay of a fold() proof and the values the in-CCS verifier needs"""
+    transcript replay of a fold() proof and the values the in-CCS verifier needs.
+    log: a list that receives every sampled value (the product's sample log)"""
     d, s, K, t = ccs.d, ccs.s, pr.K, ccs.t
     assert d == 24, "the zkvm's replay is written for the Phi_72 ring (TAU = 3)"
-    tr = Transcript(d)
+    tr = Transcript(d, log)
     absorb_public_input(tr, acc, cm_i, x_ccs)
     # collect_linearization_vars (:204-277)
     tr.absorb_label(b"beta_s")

@@ -12,6 +12,11 @@ from test_gpu_parity import check_fold_outputs, make_rho, params, rand, valid_f_
 pytestmark = pytest.mark.gpu
 
 
+def planes_u64(d, K, N):
+    """u64 words of one side's packed planes (lf.h lf_fold_step_bufs.planes)"""
+    return K * N if d == 24 else N * 256 if d == 1024 else N * K * 128
+
+
 def make_step(torch, A, kappa, d, W, seed, packed, keep_fk=True, rho=None):
     pr = params(d)
     K, L = pr.K, pr.L
@@ -30,7 +35,7 @@ def make_step(torch, A, kappa, d, W, seed, packed, keep_fk=True, rho=None):
         "fk": [z(K * N * d) for _ in range(2)] if keep_fk and not packed else [None, None],
         "wk": [z(K * W * d) for _ in range(2)], "y": [z(K * kappa * d) for _ in range(2)],
         "f0": z(N * d), "f0_coeff": z(N * d), "w_ccs0": z(W * d), "cm0": z(kappa * d),
-        "planes": [z(K * N if d == 24 else N * 256) for _ in range(2)] if packed else [None, None],
+        "planes": [z(planes_u64(d, K, N)) for _ in range(2)] if packed else [None, None],
     }
     b = LA.LfFoldStepBufs()
     for k, v in keep.items():
@@ -88,10 +93,11 @@ def test_fold_step_batch_matches_oracle(d, W, kappa, S):
     run_batch(d, W, kappa, S, packed=False)
 
 
-@pytest.mark.parametrize("d,W,S", [(1024, 37, 4), (24, 70, 4)])
+@pytest.mark.parametrize("d,W,S", [(1024, 37, 4), (24, 70, 4), (4096, 17, 4), (4096, 33, 2)])
 def test_fold_step_batch_packed_planes(d, W, S):
     """the bench's configuration: packed digit planes, four steps per batch, two
-    batches on the same contexts (each batch's contraction must see its own rows)"""
+    batches on the same contexts (each batch's contraction must see its own rows);
+    d = 4096 folds f_0 from the quarter-major operand rows (k_fold_frag)"""
     run_batch(d, W, 3 if d == 24 else 2, S, packed=True, rounds=2)
 
 
@@ -100,7 +106,7 @@ def test_fold_step_batch_wide_kappa():
     run_batch(1024, 37, 40, 2, packed=True)
 
 
-@pytest.mark.parametrize("d", [24, 1024])
+@pytest.mark.parametrize("d", [24, 1024, 4096])
 def test_fold_step_batch_rho_not_short(d):
     """steps of one batch taking different fold paths (short and full-size rho)"""
     run_batch(d, 17, 3 if d == 24 else 2, 2, packed=True, rho_long=True)

@@ -137,7 +137,13 @@ def test_fold_prove_matches_oracle(d, W, l, t, deg, kappa):
         v = N.fold_verify(ccs, acc, cmi, xi, proof_from_device(pf, d, K, tau, ccs.t, l, kappa), pr_o)
         assert np.array_equal(flat(v.r), out["r"]) and np.array_equal(v.cm, out["cm"])
         if d == 24:
-            check_replay(prover, acc_dict(acc), cmi, flat(xi), pf, out, kappa)
+            v = check_replay(prover, acc_dict(acc), cmi, flat(xi), pf, out, kappa)
+            # lf_fold_prove_vars: the same fold() with the vars from its own sample log
+            w_v = {"w_ccs": zeros(W * d), "f": zeros(Nn * d), "f_coeff": zeros(Nn * d)}
+            out_v, pf_v, vv = prover.fold_prove(acc_dict(acc), dev_wit(Wa), cmi, flat(xi), dev_wit(Wi), w_v, vars=True)
+            check_against_oracle(out_v, pf_v, w_v, o_out, o_w0, o_proof)
+            for k in v:
+                assert np.array_equal(vv[k], v[k]), k
         # fold again: the device's folded accumulator with a third instance
         x3, W3 = witness(ccs, pr_o, 13)
         cm3 = O.ajtai_commit(A, kappa, Nn, d, W3.f)
@@ -166,11 +172,13 @@ def test_fold_prove_montgomery_boundary():
         mont = np.vectorize(O.to_mont, otypes=[np.uint64])
         unmont = np.vectorize(O.from_mont, otypes=[np.uint64])
         w1 = {"w_ccs": zeros(W * d), "f": zeros(Nn * d), "f_coeff": zeros(Nn * d)}
-        out_c, pf_c = prover.fold_prove(acc_dict(acc), dev_wit(Wa), cmi, flat(xi), dev_wit(Wi), w1)
+        out_c, pf_c, vc = prover.fold_prove(acc_dict(acc), dev_wit(Wa), cmi, flat(xi), dev_wit(Wi), w1, vars=True)
         accm = {k: mont(v) for k, v in acc_dict(acc).items()}
         w2 = {"w_ccs": zeros(W * d), "f": zeros(Nn * d), "f_coeff": zeros(Nn * d)}
-        out_m, pf_m = prover.fold_prove(accm, dev_wit(Wa), mont(cmi), mont(flat(xi)), dev_wit(Wi), w2,
-                                        repr=LA.REPR_MONTGOMERY)
+        out_m, pf_m, vm = prover.fold_prove(accm, dev_wit(Wa), mont(cmi), mont(flat(xi)), dev_wit(Wi), w2,
+                                            repr=LA.REPR_MONTGOMERY, vars=True)
+        for k in vc:
+            assert np.array_equal(unmont(vm[k]), vc[k]), k
         for k in out_c:
             assert np.array_equal(unmont(out_m[k]), out_c[k]) if out_c[k].size else True, k
         assert np.array_equal(unmont(pf_m["fold_sumcheck"]), pf_c["fold_sumcheck"])
@@ -234,14 +242,16 @@ def test_fold_prove_zkvm_dimensions():
         xi, wi, cmi = dwit(102)
         acc, _ = prover.linearize(cma, xa, wa)
         w_out = {"w_ccs": zeros(W * d), "f": zeros(Nn * d), "f_coeff": zeros(Nn * d)}
-        out, pf = prover.fold_prove(acc, wa, cmi, xi, wi, w_out)
+        out, pf, vv = prover.fold_prove(acc, wa, cmi, xi, wi, w_out, vars=True)
         el = lambda a: N.elems(a, d)
         acc_o = N.LCCCS(r=el(acc["r"]), v=el(acc["v"]), cm=acc["cm"], u=el(acc["u"]), x_w=el(acc["x_w"]), h=acc["h"])
         v = N.fold_verify(ccs, acc_o, cmi, el(xi), proof_from_device(pf, d, pr.K, 3, t, l, kappa), pr_o)
         for k in ("r", "v", "u", "x_w"):
             assert np.array_equal(flat(getattr(v, k)), out[k]), k
         assert np.array_equal(v.cm, out["cm"]) and np.array_equal(v.h, out["h"])
-        check_replay(prover, acc, cmi, xi, pf, out, kappa)
+        v = check_replay(prover, acc, cmi, xi, pf, out, kappa)
+        for k in v:  # the vars from the prover's sample log = the full replay's
+            assert np.array_equal(vv[k], v[k]), k
         # the IVC step commitments of the folded accumulator (main.rs:195-196): acc_comm
         # over its 182 ring elements (364 permutations), both reprs, and ivc_step_comm
         assert [out[k].size // d for k in ("r", "v", "cm", "u", "x_w", "h")] == [17, 3, 32, 125, 4, 1]

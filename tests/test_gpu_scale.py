@@ -137,9 +137,9 @@ def check_workload(wl, seed_w, picks, cm_rows, y_rows, stream=0):
     assert np.array_equal(host(keep["w_ccs0"].view(W, d)[gidx].contiguous()).ravel(), ow), "w_ccs_0"
 
 
-def run_workload(d, W, kappa, streams=1, batch=0):
+def run_workload(d, W, kappa, streams=1, batch=0, packed=None):
     import torch
-    wl = bench.Workload(LA, torch, 0, 0, d, W, kappa, streams, batch=batch)
+    wl = bench.Workload(LA, torch, 0, 0, d, W, kappa, streams, batch=batch, packed=packed)
     try:
         wl.run(streams)
         wl.sync()
@@ -220,10 +220,13 @@ def test_fold_step_reference_ring_zkvm_shape():
         torch.cuda.empty_cache()
 
 
-def test_fold_step_configs4_d4096_kappa64():
-    """BASELINE configs[4]'s ring: d=4096 with kappa=64 (two 32-row MFMA tiles)"""
+@pytest.mark.parametrize("packed", [True, False])
+def test_fold_step_configs4_d4096_kappa64(packed):
+    """BASELINE configs[4]'s ring: d=4096 with kappa=64 (two 32-row MFMA tiles);
+    packed (the bench's default): digit bytes instead of u64 f_k / f_coeff_k rows,
+    f_0 folded from the quarter-major operand rows"""
     import torch
-    wl = run_workload(4096, 1024, 64)
+    wl = run_workload(4096, 1024, 64, packed=packed)
     try:
         assert wl.sch.layout == 1
         nblk = (wl.W + 15) // 16

@@ -50,11 +50,63 @@ def case(W=5, l=2, t=4, deg=2, kappa=3, seed=7):
     return pr, ccs, kappa, acc, cmi, xi, proof, out
 
 
-def replay(ccs, kappa, acc, cmi, xi, proof, repr=LA.REPR_CANONICAL, conv=lambda a: a):
+def replay(ccs, kappa, acc, cmi, xi, proof, repr=LA.REPR_CANONICAL, conv=lambda a: a, samples=None):
     return LA.fold_replay(LA.goldilocks_dp(24), ccs.t, ccs.m, ccs.l, ccs.degree, conv(flat(ccs.c)), ccs.S, kappa,
                           {k: conv(v) for k, v in acc_dict(acc).items()}, conv(np.asarray(cmi, np.uint64)),
                           conv(flat(xi)), {k: ([conv(x) for x in v] if isinstance(v, list) else conv(v))
-                                           for k, v in proof_dict(proof).items()}, repr)
+                                           for k, v in proof_dict(proof).items()}, repr, samples=samples)
+
+
+@pytest.mark.parametrize("W,l,t,deg,kappa", [(5, 2, 4, 2, 3), (13, 4, 6, 3, 4)])
+def test_replay_from_sample_log(W, l, t, deg, kappa):
+    """lf_fold_replay_samples: the replay's challenges from a sample log (what
+    lf_fold_prove records) instead of a second sponge -- every variable equal to
+    the full replay's; a short or long log is rejected"""
+    pr, ccs, kappa, acc, cmi, xi, proof, _ = case(W, l, t, deg, kappa, seed=W + t)
+    log = []
+    N.fold_replay(ccs, acc, cmi, xi, proof, pr, log=log)
+    full = replay(ccs, kappa, acc, cmi, xi, proof)
+    got = replay(ccs, kappa, acc, cmi, xi, proof, samples=log)
+    for k in full:
+        assert np.array_equal(got[k], full[k]), k
+    mont = np.vectorize(O.to_mont, otypes=[np.uint64])
+    unmont = np.vectorize(O.from_mont, otypes=[np.uint64])
+    gm = replay(ccs, kappa, acc, cmi, xi, proof, LA.REPR_MONTGOMERY, mont, samples=log)
+    for k in full:
+        assert np.array_equal(unmont(gm[k]), full[k]), k
+    for bad in (log[:-1], log + [5]):
+        with pytest.raises(LA.LfError):
+            replay(ccs, kappa, acc, cmi, xi, proof, samples=bad)
+
+
+def test_transcript_record_and_playback():
+    """a recording transcript's samples, played back to a transcript that observes
+    the same values (dropped) and samples in the same pattern, come out in order"""
+    lib = LA.load()
+    rng = np.random.default_rng(3)
+    t = lib.lf_transcript_new()
+    lib.lf_transcript_record(t)
+    ops, drawn = [], []
+    for _ in range(300):
+        if rng.integers(0, 3):
+            v = int(rng.integers(0, 1 << 63, dtype=np.uint64))
+            lib.lf_transcript_observe(t, v)
+            ops.append(("o", v))
+        else:
+            drawn.append(lib.lf_transcript_sample(t))
+            ops.append(("s", None))
+    n = lib.lf_transcript_samples(t, None, 0)
+    log = np.zeros(n, np.uint64)
+    lib.lf_transcript_samples(t, log.ctypes.data, n)
+    lib.lf_transcript_free(t)
+    assert [int(x) for x in log] == drawn
+    pb = lib.lf_transcript_new_playback(log.ctypes.data, n)
+    again = [lib.lf_transcript_sample(pb) if op == "s" else lib.lf_transcript_observe(pb, v) for op, v in ops]
+    assert [x for (op, _), x in zip(ops, again) if op == "s"] == drawn
+    assert lib.lf_transcript_playback_status(pb) == 0
+    lib.lf_transcript_sample(pb)  # one past the log
+    assert lib.lf_transcript_playback_status(pb) != 0
+    lib.lf_transcript_free(pb)
 
 
 @pytest.mark.parametrize("W,l,t,deg,kappa", [(5, 2, 4, 2, 3), (13, 4, 6, 3, 4), (7, 0, 3, 2, 2)])
