@@ -389,6 +389,9 @@ int lf_dev_mle_fix_first(lf_ctx *ctx, int d, const uint64_t *in, size_t in_strid
 /* out[m] = mle_m(point) (nm NTT elements); point: nv NTT elements on the device */
 int lf_dev_mle_evaluate(lf_ctx *ctx, int d, const uint64_t *mles, int nm, int nv, const uint64_t *point,
                         uint64_t *out);
+/* the same from the point's eq table (2^nv NTT elements, lf_dev_eq_table) */
+int lf_dev_mle_evaluate_eq(lf_ctx *ctx, int d, const uint64_t *mles, int nm, int nv, const uint64_t *eq,
+                           uint64_t *out);
 /* one prover round's message: evals[e] = sum_b comb(mle(2b) + e (mle(2b+1) - mle(2b))),
  * e <= degree (folding: degree = 2 bsmall) */
 int lf_dev_sumcheck_round(lf_ctx *ctx, const lf_comb *comb, const uint64_t *mles, size_t stride, int nm, int nv,
@@ -397,6 +400,12 @@ int lf_dev_sumcheck_round(lf_ctx *ctx, const lf_comb *comb, const uint64_t *mles
  * and randomness [nv][1 or 3] in host memory; the MLEs are clobbered */
 int lf_sumcheck_prove(lf_ctx *ctx, lf_transcript *t, const lf_comb *comb, uint64_t *mles, int nm, int nv, int d,
                       int degree, uint64_t *proof, uint64_t *randomness);
+/* the same prover over MLEs that stay where they are: mles is a host array of nm
+ * device pointers (one per MLE of 2^nv elements, repeats allowed), read in the first
+ * round only and never written; work: a device buffer of nm x 2^(nv-2) elements for
+ * the later rounds (the linearization sumcheck reads its Mz MLEs in place) */
+int lf_sumcheck_prove_ptrs(lf_ctx *ctx, lf_transcript *t, const lf_comb *comb, const uint64_t *const *mles, int nm,
+                           int nv, int d, int degree, uint64_t *work, uint64_t *proof, uint64_t *randomness);
 
 /* ------------------------------------------------------------ sparse Mz products
  * CCS.M (latticefold/src/arith.rs:51-74): t matrices m x n of ring elements,
@@ -418,6 +427,12 @@ int lf_dev_mz_challenged(lf_ctx *ctx, const lf_ccs *M, const uint64_t *z, const 
                          uint64_t *out);
 int lf_dev_mz_evaluate(lf_ctx *ctx, const lf_ccs *M, const uint64_t *z, int nz, int nv, const uint64_t *point,
                        uint64_t *out);
+/* lf_dev_mz_evaluate in two halves, so one point's weights serve several z sets:
+ * w [t][n] = M_j^T eq (eq: an eq table of 2^nv NTT elements, lf_dev_eq_table), then
+ * out [nz][t] = w_j . z_i. lf_ccs_weights_len: the u64 of w. */
+size_t lf_ccs_weights_len(const lf_ccs *M);
+int lf_dev_mz_weights(lf_ctx *ctx, const lf_ccs *M, int nv, const uint64_t *eq, uint64_t *w);
+int lf_dev_mz_dots(lf_ctx *ctx, const lf_ccs *M, const uint64_t *w, const uint64_t *z, int nz, uint64_t *out);
 
 /* ------------------------------------------------------------ width-8 Poseidon2 commitments
  * zkvm/src/commitments.rs:192-340, over Poseidon2Goldilocks<8> (poseidon2.rs:31-49;
@@ -574,6 +589,9 @@ int lf_dev_fold_combine(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, si
  * (wstride u64 apart, 0 = N d): out [nw][tau] NTT elements; point: nv NTT elements */
 int lf_dev_fhat_evaluate(lf_ctx *ctx, int d, const uint64_t *f_coeff, size_t N, size_t wstride, int nw, int nv,
                          const uint64_t *point, uint64_t *out);
+/* the same with the point's eq table given (2^nv NTT elements, lf_dev_eq_table) */
+int lf_dev_fhat_evaluate_eq(lf_ctx *ctx, int d, const uint64_t *f_coeff, size_t N, size_t wstride, int nw, int nv,
+                            const uint64_t *eq, uint64_t *out);
 /* io[x] += sum_m coef[m] (.) mles[m][x] over 2^nv points (stride 0 = 2^nv d) */
 int lf_dev_mle_lincomb(lf_ctx *ctx, int d, const uint64_t *mles, size_t stride, int nm, int nv, const uint64_t *coef,
                        uint64_t *io);

@@ -204,10 +204,16 @@ SIGNATURES = {
     "lf_dev_mz_mles": (I, [VP, VP, VP, I, I, VP]),
     "lf_dev_mz_challenged": (I, [VP, VP, VP, VP, I, I, VP]),
     "lf_dev_mz_evaluate": (I, [VP, VP, VP, I, I, VP, VP]),
+    "lf_ccs_weights_len": (SZ, [VP]),
+    "lf_dev_mz_weights": (I, [VP, VP, I, VP, VP]),
+    "lf_dev_mz_dots": (I, [VP, VP, VP, VP, I, VP]),
+    "lf_dev_fhat_evaluate_eq": (I, [VP, I, VP, SZ, SZ, I, I, VP, VP]),
     "lf_dev_mle_fix_first": (I, [VP, I, VP, SZ, I, I, VP, VP, SZ]),
     "lf_dev_mle_evaluate": (I, [VP, I, VP, I, I, VP, VP]),
+    "lf_dev_mle_evaluate_eq": (I, [VP, I, VP, I, I, VP, VP]),
     "lf_dev_sumcheck_round": (I, [VP, C.POINTER(LfComb), VP, SZ, I, I, I, I, VP]),
     "lf_sumcheck_prove": (I, [VP, VP, C.POINTER(LfComb), VP, I, I, I, I, VP, VP]),
+    "lf_sumcheck_prove_ptrs": (I, [VP, VP, C.POINTER(LfComb), VP, I, I, I, I, VP, VP, VP]),
     "lf_fold_lcccs": (I, [VP, I, I, VP, VP, VP, SZ, VP, SZ, VP, VP, VP, VP, I]),
     "lf_dev_fold_lcccs": (I, [VP, I, I, VP, VP, VP, SZ, VP, SZ, VP, VP, VP, VP]),
     "lf_compute_x_s": (I, [VP, C.POINTER(LfParams), VP, SZ, VP, I]),

@@ -40,6 +40,8 @@ struct lf_prover {
   uint64_t *zdec[2] = {}, *vs = nullptr, *us = nullptr, *fold = nullptr, *coef[2] = {}, *zeta = nullptr, *mu = nullptr;
   uint64_t *theta = nullptr, *eta = nullptr, *rho = nullptr, *rhoc = nullptr, *cm0 = nullptr, *u0 = nullptr, *x0 = nullptr,
            *v0 = nullptr, *r0 = nullptr;
+  // eq(r_0) and one point's Mz weights M_j^T eq (shared by the sides evaluated there)
+  uint64_t *eq0 = nullptr, *mzw = nullptr;
   std::string err;
   // every value the last lf_fold_prove sampled from its transcript, in order
   // (lf_fold_prove_vars replays the proof on them instead of a second sponge)
@@ -190,8 +192,28 @@ int linearize(lf_prover *P, Run &R, const std::vector<uint64_t> &xc, const lf_wi
   R.h2d(P->z + l * d, one.data(), d);
   R.d2d(P->z + (l + 1) * d, w_i->w_ccs, W * d);
   R.check(lf_dev_mz_mles(C, P->ccs, P->z, 1, s, P->mz), "Mz MLEs");
-  for (size_t k = 0; k < P->lin_list.size(); k++) R.d2d(P->lin + k * nn * d, P->mz + (size_t)P->lin_list[k] * nn * d, nn * d);
-  R.check(lf_dev_eq_table(C, d, P->beta, s, P->lin + P->lin_list.size() * nn * d), "eq(beta)");
+  // The MLE list is [MLE(M_j z) for each (i, j in S_i) with c_i != 0] + [eq(beta)]
+  // (linearization/utils.rs:71-84), and the combination reads list position j for
+  // matrix index j (as the reference does) and the last entry -- so only those
+  // positions are live. Their MLEs are read where the Mz products left them (a
+  // pointer table; no copies), the dead positions are never fixed, and eq(beta)
+  // sits at the front of P->lin, the rest of which serves the later rounds.
+  std::vector<int> live_of(P->lin_list.size(), -1), S_live(P->S_idx.size());
+  std::vector<const uint64_t *> ptr;
+  for (size_t k = 0; k < P->S_idx.size(); k++) {
+    const int p = P->S_idx[k];
+    if (p < 0 || (size_t)p >= P->lin_list.size()) {
+      P->err = "multiset index past the MLE list";
+      return R.rc = LF_ERR_INVALID_ARG;
+    }
+    if (live_of[p] < 0) {
+      live_of[p] = (int)ptr.size();
+      ptr.push_back(P->mz + (size_t)P->lin_list[p] * nn * d);
+    }
+    S_live[k] = live_of[p];
+  }
+  R.check(lf_dev_eq_table(C, d, P->beta, s, P->lin), "eq(beta)");
+  ptr.push_back(P->lin);
   std::vector<uint64_t> rnd((size_t)s * tb);
   {
     lf_comb cb{};
@@ -199,18 +221,22 @@ int linearize(lf_prover *P, Run &R, const std::vector<uint64_t> &xc, const lf_wi
     cb.q = P->q;
     cb.c = lf_ccs_c_device(P->ccs);
     cb.S_off = P->S_off.data();
-    cb.S_idx = P->S_idx.data();
+    cb.S_idx = S_live.data();
     if (R.rc == LF_OK)
-      R.check(lf_sumcheck_prove(C, R.T, &cb, P->lin, P->nm_lin, s, d, P->degree + 1, lin_sumcheck, rnd.data()),
+      R.check(lf_sumcheck_prove_ptrs(C, R.T, &cb, ptr.data(), (int)ptr.size(), s, d, P->degree + 1, P->lin + nn * d,
+                                     lin_sumcheck, rnd.data()),
               "linearization sumcheck");
   }
   if (R.rc) return R.rc;
   r_lin.assign((size_t)s * d, 0);
   for (int i = 0; i < s; i++) broadcast(rnd.data() + (size_t)i * tb, tb, d, r_lin.data() + (size_t)i * d);
   R.h2d(P->pt, r_lin.data(), (size_t)s * d);
-  // v = f_hat(w_i) at r, u = MLE(M_j z)(r) (compute_evaluation_vectors, :130-147)
-  R.check(lf_dev_fhat_evaluate(C, d, w_i->f_coeff, N, 0, 1, s, P->pt, P->val), "v");
-  R.check(lf_dev_mle_evaluate(C, d, P->mz, t, s, P->pt, P->val + (size_t)tau * d), "u");
+  // v = f_hat(w_i) at r, u = MLE(M_j z)(r) (compute_evaluation_vectors, :130-147), from one
+  // eq(r) table -- built where the folding prover's eq(r_1) MLE lives, which it is
+  uint64_t *eq_lin = P->fold + 2 * nn * d;
+  R.check(lf_dev_eq_table(C, d, P->pt, s, eq_lin), "eq(r)");
+  R.check(lf_dev_fhat_evaluate_eq(C, d, w_i->f_coeff, N, 0, 1, s, eq_lin, P->val), "v");
+  R.check(lf_dev_mle_evaluate_eq(C, d, P->mz, t, s, eq_lin, P->val + (size_t)tau * d), "u");
   lv.assign((size_t)tau * d, 0);
   lu.assign((size_t)t * d, 0);
   R.d2h(lv.data(), P->val, (size_t)tau * d);
@@ -305,7 +331,8 @@ int lf_prover_create(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, const
       {&P->vs, 2 * K * tau * d}, {&P->us, 2 * K * t * d}, {&P->fold, (size_t)P->nm_fold * nn * d},
       {&P->coef[0], K * tau * d}, {&P->coef[1], K * tau * d}, {&P->zeta, 2 * K * d}, {&P->mu, 2 * K * d},
       {&P->theta, 2 * K * tau * d}, {&P->eta, 2 * K * t * d}, {&P->rho, 2 * K * d}, {&P->rhoc, 2 * K * d},
-      {&P->cm0, kd}, {&P->u0, (size_t)t * d}, {&P->x0, (l + 1) * d}, {&P->v0, tau * d}, {&P->r0, (size_t)P->s * d}};
+      {&P->cm0, kd}, {&P->u0, (size_t)t * d}, {&P->x0, (l + 1) * d}, {&P->v0, tau * d}, {&P->r0, (size_t)P->s * d},
+      {&P->eq0, nn * d}, {&P->mzw, lf_ccs_weights_len(ccs)}};
   size_t total = 0;
   for (auto &x : parts) total += (x.elems + 31) / 32 * 32;  // 256-B aligned parts
   int prev = -1;
@@ -501,13 +528,17 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
   // behind an event, so the host absorbs side 0 while the device evaluates side 1
   // and prepares the challenge-independent folding MLEs (the f_hat MLEs of the 2K
   // decomposed witnesses, eq(r_i); create_sumcheck_polynomial, folding/utils.rs:196-255)
-  const std::vector<uint64_t> *r_side[2] = {&ar, &r_lin};
   uint64_t *M = P->fold;
   const size_t mstride = nn * d;
+  // eq(r_i) of each side is the folding prover's eq(r_i) MLE (M slots 0 and 2; the
+  // linearization left eq(r_lin) in slot 2): v_s and u_s read it from there
+  R.h2p2d(P->pt, P->hr[0], ar.data(), (size_t)s * d);
+  R.check(lf_dev_eq_table(C, d, P->pt, s, M), "eq(r_0)");
   for (int side = 0; side < 2; side++) {
-    R.h2p2d(P->pt, P->hr[side], r_side[side]->data(), (size_t)s * d);
-    R.check(lf_dev_fhat_evaluate(C, d, P->fkc[side], N, ND, K, s, P->pt, P->vs + (size_t)side * K * tau * d), "v_s");
-    R.check(lf_dev_mz_evaluate(C, P->ccs, P->zdec[side], K, s, P->pt, P->us + (size_t)side * K * t * d), "u_s");
+    const uint64_t *eq_s = M + (size_t)(2 * side) * mstride;
+    R.check(lf_dev_fhat_evaluate_eq(C, d, P->fkc[side], N, ND, K, s, eq_s, P->vs + (size_t)side * K * tau * d), "v_s");
+    R.check(lf_dev_mz_weights(C, P->ccs, s, eq_s, P->mzw), "u_s weights");
+    R.check(lf_dev_mz_dots(C, P->ccs, P->mzw, P->zdec[side], K, P->us + (size_t)side * K * t * d), "u_s");
     R.d2p(P->hx[side], P->xs + (size_t)side * K * (l + 1) * d, (size_t)K * (l + 1) * d);
     R.d2p(P->hy[side], P->y[side], (size_t)K * kd);
     R.d2p(P->hu[side], P->us + (size_t)side * K * t * d, (size_t)K * t * d);
@@ -518,11 +549,6 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
     for (int k = 0; k < K; k++)
       R.check(lf_dev_get_fhat(C, d, P->fkc[side] + (size_t)k * ND, N, s, M + (5 + (size_t)(side * K + k) * tau) * mstride),
               "f_hat");
-  for (int side = 0; side < 2; side++) {
-    // the pinned copy of r_side still holds the point: upload it again for eq(r_i)
-    R.hip(hipMemcpyAsync(P->pt, P->hr[side], (size_t)s * d * 8, hipMemcpyHostToDevice, R.st), "upload");
-    R.check(lf_dev_eq_table(C, d, P->pt, s, M + (size_t)(2 * side) * mstride), "eq(r_i)");
-  }
   if (R.rc) return R.rc;
   R.mark(LF_SPAN_DECOMPOSITION, false);
   for (int side = 0; side < 2; side++) {
@@ -598,11 +624,15 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
   // theta_s = f_hat(w_i)(r_0), eta_s = MLE(M_j z_i)(r_0) (get_thetas / get_etas, :236-256):
   // theta_s and side 0's eta_s come back first, so the host absorbs them while the
   // device evaluates side 1's eta_s
+  // one eq(r_0) table and one set of Mz weights at r_0 for both sides
+  R.check(lf_dev_eq_table(C, d, P->r0, s, P->eq0), "eq(r_0)");
   for (int side = 0; side < 2; side++)
-    R.check(lf_dev_fhat_evaluate(C, d, P->fkc[side], N, ND, K, s, P->r0, P->theta + (size_t)side * K * tau * d), "theta");
+    R.check(lf_dev_fhat_evaluate_eq(C, d, P->fkc[side], N, ND, K, s, P->eq0, P->theta + (size_t)side * K * tau * d),
+            "theta");
   R.d2p(P->htheta, P->theta, 2 * (size_t)K * tau * d);
+  R.check(lf_dev_mz_weights(C, P->ccs, s, P->eq0, P->mzw), "eta weights");
   for (int side = 0; side < 2; side++) {
-    R.check(lf_dev_mz_evaluate(C, P->ccs, P->zdec[side], K, s, P->r0, P->eta + (size_t)side * K * t * d), "eta");
+    R.check(lf_dev_mz_dots(C, P->ccs, P->mzw, P->zdec[side], K, P->eta + (size_t)side * K * t * d), "eta");
     R.d2p(P->heta + (size_t)side * K * t * d, P->eta + (size_t)side * K * t * d, (size_t)K * t * d);
     R.hip(hipEventRecord(P->ev[side], R.st), "event");
   }

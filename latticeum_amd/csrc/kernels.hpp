@@ -233,8 +233,9 @@ hipError_t eq_table(const uint64_t *r, int nv, int d, uint64_t *out, hipStream_t
 // Witness::get_fhat: tau = d / slots MLEs of 2^nv points from N <= 2^nv coefficient elements
 hipError_t get_fhat(const uint64_t *f_coeff, size_t N, int d, int nv, uint64_t *out, hipStream_t st);
 // out[m][b] = in[m][2b] + r (in[m][2b+1] - in[m][2b]), b < half; r_base: slot_words(d) words
+// ptrs (device, nm pointers, optional): MLE m at ptrs[m] instead of in + m in_stride
 hipError_t mle_fix_first(const uint64_t *in, size_t in_stride, int nm, size_t half, int d, const uint64_t *r_base,
-                         uint64_t *out, size_t out_stride, hipStream_t st);
+                         uint64_t *out, size_t out_stride, hipStream_t st, const uint64_t *const *ptrs = nullptr);
 // nf: the f_hat MLEs the folding round may split over chunks (1 for linearization)
 size_t round_partial_elems(int d, size_t half, int nevals, int nf);
 hipError_t fold_weights(const uint64_t *mu, int nk, int tau, int d, uint64_t *w, hipStream_t st);
@@ -243,7 +244,8 @@ hipError_t fold_weights(const uint64_t *mu, int nk, int tau, int d, uint64_t *w,
 hipError_t round_folding(const uint64_t *mles, size_t stride, int nf, const uint64_t *w, int bsmall, size_t half, int d,
                          uint64_t *partial, uint64_t *evals, hipStream_t st);
 hipError_t round_lin(const uint64_t *mles, size_t stride, int nm, const uint64_t *c, const CombS &cs, int degree,
-                     size_t half, int d, uint64_t *partial, uint64_t *evals, hipStream_t st);
+                     size_t half, int d, uint64_t *partial, uint64_t *evals, hipStream_t st,
+                     const uint64_t *const *ptrs = nullptr);
 size_t mle_eval_partial_elems(int d, int nm);
 // out[m] = sum_x eq[x] (.) mles[m][x], x < n
 hipError_t mle_dot(const uint64_t *mles, size_t stride, int nm, const uint64_t *eq, size_t n, int d,
@@ -288,6 +290,10 @@ hipError_t mz_mles(const CcsDev &M, const uint64_t *z, int nz, int nv, uint64_t 
 hipError_t mz_challenged(const CcsDev &M, const uint64_t *z, const uint64_t *zeta, int nz, int nv, uint64_t *out,
                          uint64_t *scratch, hipStream_t st);
 // out [nz][t][d] = MLE(M_j z_i)(point)
+// the evaluation route in two halves: w [t][n] = M_j^T eq (one point, any number of z
+// sets), then out [nz][t] = w_j . z_i
+hipError_t mz_weights(const CcsDev &M, const uint64_t *eq, uint64_t *w, hipStream_t st);
+hipError_t mz_dots(const CcsDev &M, const uint64_t *w, const uint64_t *z, int nz, uint64_t *out, hipStream_t st);
 hipError_t mz_evaluate(const CcsDev &M, const uint64_t *z, int nz, int nv, const uint64_t *point, uint64_t *out,
                        uint64_t *scratch, hipStream_t st);
 

@@ -69,6 +69,8 @@ struct lf_ctx {
   size_t tmp_elems = 0;
   uint64_t *sc = nullptr;       // sumcheck: fixed MLEs of the next round, round partial sums, weights
   size_t sc_elems = 0;
+  uint64_t *ptrs = nullptr;     // lf_sumcheck_prove_ptrs: the MLE pointer table
+  size_t ptrs_elems = 0;
   lfk::FoldRows fold_rows{};    // a step without f_k buffers: where its 2K planes sit in the operand rows
   bool fold_from_frag = false;
   bool frag_fallback = false;   // packed d = 1024 planes: fold_rows serve the not-short-rho fallback
@@ -909,6 +911,7 @@ void lf_ctx_destroy(lf_ctx *c) {
   if (c->limb) (void)hipFree(c->limb);
   if (c->tmp) (void)hipFree(c->tmp);
   if (c->sc) (void)hipFree(c->sc);
+  if (c->ptrs) (void)hipFree(c->ptrs);
   if (c->join) (void)hipEventDestroy(c->join);
   if (c->d_err) (void)hipFree(c->d_err);
   if (c->d_sync) (void)hipFree(c->d_sync);
@@ -1538,6 +1541,19 @@ int lf_dev_fhat_evaluate(lf_ctx *c, int d, const uint64_t *f_coeff, size_t N, si
   return LF_OK;
 }
 
+int lf_dev_fhat_evaluate_eq(lf_ctx *c, int d, const uint64_t *f_coeff, size_t N, size_t wstride, int nw, int nv,
+                            const uint64_t *eq, uint64_t *out) {
+  if (!c || !eq || !out || nw < 0 || nv < 1 || (nw && N && !f_coeff)) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  const size_t n = (size_t)1 << nv;
+  if (N > n) return fail(c, LF_ERR_INCORRECT_LENGTH, "N exceeds 2^nv");
+  const int tau = d == 24 ? 3 : 1;
+  LF_TRY(grow(c, c->sc, c->sc_elems, lfk::mle_eval_partial_elems(d, nw * tau)));
+  LF_HIP(c, lfk::fhat_dot(f_coeff, N, wstride ? wstride : N * d, nw, eq, n, d, c->sc, out, c->cur));
+  return LF_OK;
+}
+
 int lf_dev_mle_lincomb(lf_ctx *c, int d, const uint64_t *mles, size_t stride, int nm, int nv, const uint64_t *coef,
                        uint64_t *io) {
   if (!c || !io || nm < 0 || nv < 0 || (nm && (!mles || !coef))) return LF_ERR_INVALID_ARG;
@@ -1554,6 +1570,16 @@ int lf_dev_mle_fix_first(lf_ctx *c, int d, const uint64_t *in, size_t in_stride,
   DevGuard g(c);
   if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
   LF_HIP(c, lfk::mle_fix_first(in, in_stride, nm, (size_t)1 << (nv - 1), d, r_base, out, out_stride, c->cur));
+  return LF_OK;
+}
+
+int lf_dev_mle_evaluate_eq(lf_ctx *c, int d, const uint64_t *mles, int nm, int nv, const uint64_t *eq, uint64_t *out) {
+  if (!c || !mles || !eq || !out || nm < 1 || nv < 1) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  const size_t n = (size_t)1 << nv;
+  LF_TRY(grow(c, c->sc, c->sc_elems, lfk::mle_eval_partial_elems(d, nm)));
+  LF_HIP(c, lfk::mle_dot(mles, n * d, nm, eq, n, d, c->sc, out, c->cur));
   return LF_OK;
 }
 
@@ -1590,18 +1616,18 @@ int lf_dev_sumcheck_round(lf_ctx *c, const lf_comb *cb, const uint64_t *mles, si
   return LF_OK;
 }
 
-int lf_sumcheck_prove(lf_ctx *c, lf_transcript *t, const lf_comb *cb, uint64_t *mles, int nm, int nv, int d,
-                      int degree, uint64_t *proof, uint64_t *randomness) {
-  if (!c || !t || !mles || !proof || !randomness || nv < 1 || nm < 1) return LF_ERR_INVALID_ARG;
-  DevGuard g(c);
-  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
-  lfk::CombS cs;
-  LF_TRY(comb_check(c, cb, nm, d, degree, &cs));
+// MLSumcheck::prove_as_subprotocol (sumcheck.rs:61-88). Round 0 reads the MLEs at
+// `mles` (stride 2^nv d) or, with ptrs (device array of nm pointers), wherever
+// those point; every round fixes them into the next buffer: the context scratch
+// (2^(nv-1) points) and `alt` (2^(nv-2) points; the input itself when ptrs is null)
+static int sumcheck_run(lf_ctx *c, lf_transcript *t, const lf_comb *cb, const lfk::CombS &cs, const uint64_t *mles,
+                        const uint64_t *const *ptrs, uint64_t *alt, int nm, int nv, int d, int degree, uint64_t *proof,
+                        uint64_t *randomness) {
   const int tb = lfk::slot_words(d), nev = degree + 1;
   const size_t n = (size_t)1 << nv;
-  // scratch: the MLEs fixed by the first challenge (later rounds ping-pong with
-  // `mles` itself), the round's partial sums, the evaluations, the weights
-  // the partial sums of every round fit the largest round's (chunks only split the small ones)
+  // scratch: the MLEs fixed by the first challenge, the round's partial sums, the
+  // evaluations, the weights; the partial sums of every round fit the largest
+  // round's (chunks only split the small ones)
   const int nfc = cb->kind == LF_COMB_FOLDING ? cb->nk * cb->tau : cb->q;  // the chunked sum (f_hat MLEs / multisets)
   size_t part = 0;
   for (size_t h = n / 2; h >= 1; h /= 2) part = std::max(part, lfk::round_partial_elems(d, h, nev, nfc));
@@ -1610,13 +1636,14 @@ int lf_sumcheck_prove(lf_ctx *c, lf_transcript *t, const lf_comb *cb, uint64_t *
   LF_TRY(grow(c, c->sc, c->sc_elems, fixed + part + (size_t)nev * d + wlen));
   uint64_t *buf = c->sc, *partial = buf + fixed, *ev = partial + part, *w = ev + (size_t)nev * d;
   if (wlen) LF_HIP(c, lfk::fold_weights(cb->mu, cb->nk, cb->tau, d, w, c->cur));
-  // MLSumcheck::prove_as_subprotocol (sumcheck.rs:61-88): absorb R::from(nvars), R::from(degree)
+  // absorb R::from(nvars), R::from(degree)
   std::vector<uint64_t> scal(d, 0);
   for (int i = 0; i < d; i += tb) scal[i] = (uint64_t)nv;
   lf_transcript_absorb_ring(t, scal.data(), 1, d, LF_REPR_CANONICAL);
   for (int i = 0; i < d; i += tb) scal[i] = (uint64_t)degree;
   lf_transcript_absorb_ring(t, scal.data(), 1, d, LF_REPR_CANONICAL);
   const uint64_t *cur = mles;
+  const uint64_t *const *cptrs = ptrs;
   size_t stride = n * d;
   for (int i = 0; i < nv; i++) {
     const size_t half = n >> (i + 1);
@@ -1624,7 +1651,7 @@ int lf_sumcheck_prove(lf_ctx *c, lf_transcript *t, const lf_comb *cb, uint64_t *
     if (cb->kind == LF_COMB_FOLDING)
       LF_HIP(c, lfk::round_folding(cur, stride, cb->nk * cb->tau, w, cb->bsmall, half, d, partial, ev, c->cur));
     else
-      LF_HIP(c, lfk::round_lin(cur, stride, nm, cb->c, cs, degree, half, d, partial, ev, c->cur));
+      LF_HIP(c, lfk::round_lin(cur, stride, nm, cb->c, cs, degree, half, d, partial, ev, c->cur, cptrs));
     LF_HIP(c, hipMemcpyAsync(msg, ev, (size_t)nev * d * 8, hipMemcpyDeviceToHost, c->cur));
     LF_HIP(c, hipStreamSynchronize(c->cur));
     // prover message absorbed, challenge sampled (fiat_shamir.rs:69-86; one sample for Fq) and absorbed
@@ -1640,13 +1667,40 @@ int lf_sumcheck_prove(lf_ctx *c, lf_transcript *t, const lf_comb *cb, uint64_t *
     lf_transcript_absorb_ring(t, scal.data(), 1, d, LF_REPR_CANONICAL);
     // fix_variables(r) of every MLE (prover.rs:75-78), into the other buffer
     if (half >= 1 && i + 1 < nv) {
-      uint64_t *dst = (i % 2 == 0) ? buf : mles;
-      LF_HIP(c, lfk::mle_fix_first(cur, stride, nm, half, d, ch, dst, half * d, c->cur));
+      uint64_t *dst = (i % 2 == 0) ? buf : alt;
+      LF_HIP(c, lfk::mle_fix_first(cur, stride, nm, half, d, ch, dst, half * d, c->cur, cptrs));
       cur = dst;
+      cptrs = nullptr;
       stride = half * d;
     }
   }
   return LF_OK;
+}
+
+int lf_sumcheck_prove(lf_ctx *c, lf_transcript *t, const lf_comb *cb, uint64_t *mles, int nm, int nv, int d,
+                      int degree, uint64_t *proof, uint64_t *randomness) {
+  if (!c || !t || !mles || !proof || !randomness || nv < 1 || nm < 1) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  lfk::CombS cs;
+  LF_TRY(comb_check(c, cb, nm, d, degree, &cs));
+  return sumcheck_run(c, t, cb, cs, mles, nullptr, mles, nm, nv, d, degree, proof, randomness);
+}
+
+int lf_sumcheck_prove_ptrs(lf_ctx *c, lf_transcript *t, const lf_comb *cb, const uint64_t *const *mles, int nm, int nv,
+                           int d, int degree, uint64_t *work, uint64_t *proof, uint64_t *randomness) {
+  if (!c || !t || !mles || !work || !proof || !randomness || nv < 1 || nm < 1) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  for (int m = 0; m < nm; m++)
+    if (!mles[m]) return fail(c, LF_ERR_INVALID_ARG, "null MLE pointer");
+  lfk::CombS cs;
+  LF_TRY(comb_check(c, cb, nm, d, degree, &cs));
+  // the pointer table on the device, behind the scratch the rounds use
+  LF_TRY(grow(c, c->ptrs, c->ptrs_elems, (size_t)nm));
+  LF_HIP(c, hipMemcpyAsync(c->ptrs, mles, (size_t)nm * sizeof(uint64_t), hipMemcpyHostToDevice, c->cur));
+  return sumcheck_run(c, t, cb, cs, nullptr, reinterpret_cast<const uint64_t *const *>(c->ptrs), work, nm, nv, d,
+                      degree, proof, randomness);
 }
 
 // ---------------------------------------------------------------- sparse Mz products
@@ -1825,6 +1879,23 @@ int lf_dev_mz_evaluate(lf_ctx *c, const lf_ccs *M, const uint64_t *z, int nz, in
   LF_HIP(c, lfk::mz_evaluate(M->dev, z, nz, nv, point, out, c->tmp, c->cur));
   return LF_OK;
 }
+
+int lf_dev_mz_weights(lf_ctx *c, const lf_ccs *M, int nv, const uint64_t *eq, uint64_t *w) {
+  if (!c || !eq || !w) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  LF_TRY(mz_check(c, M, 1, nv));
+  LF_HIP(c, lfk::mz_weights(M->dev, eq, w, c->cur));
+  return LF_OK;
+}
+
+int lf_dev_mz_dots(lf_ctx *c, const lf_ccs *M, const uint64_t *w, const uint64_t *z, int nz, uint64_t *out) {
+  if (!c || !M || !w || !z || !out || nz < 1) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  LF_HIP(c, lfk::mz_dots(M->dev, w, z, nz, out, c->cur));
+  return LF_OK;
+}
+
+size_t lf_ccs_weights_len(const lf_ccs *M) { return M ? (size_t)M->dev.t * M->dev.n * M->dev.d : 0; }
 
 // ---------------------------------------------------------------- width-8 Poseidon2 Merkle trees
 int lf_dev_poseidon2_w8_permute(lf_ctx *c, uint64_t *states, size_t n) {

@@ -156,15 +156,24 @@ hipError_t mz_challenged(const CcsDev &M, const uint64_t *z, const uint64_t *zet
   return csr(M.hrp, 0, 1, M.hcol, M.hidx, M.val, M.m, M.d, y, 0, out, 0, 1, st);
 }
 
+hipError_t mz_weights(const CcsDev &M, const uint64_t *eq, uint64_t *w, hipStream_t st) {
+  // w_j[c] = sum over column c of M_j of value (.) eq[row]
+  return csr(M.crp, M.n + 1, M.t, M.crow, M.cidx, M.val, M.n, M.d, eq, 0, w, M.n * M.d, M.t, st);
+}
+
 hipError_t mz_evaluate(const CcsDev &M, const uint64_t *z, int nz, int nv, const uint64_t *point, uint64_t *out,
                        uint64_t *scratch, hipStream_t st) {
   if (M.m > ((size_t)1 << nv)) return hipErrorInvalidValue;
   uint64_t *eq = scratch, *w = scratch + ((size_t)1 << nv) * M.d;
   hipError_t e = eq_table(point, nv, M.d, eq, st);
   if (e != hipSuccess) return e;
-  // w_j[c] = sum over column c of M_j of value (.) eq[row]
-  e = csr(M.crp, M.n + 1, M.t, M.crow, M.cidx, M.val, M.n, M.d, eq, 0, w, M.n * M.d, M.t, st);
+  e = mz_weights(M, eq, w, st);
   if (e != hipSuccess) return e;
+  return mz_dots(M, w, z, nz, out, st);
+}
+
+hipError_t mz_dots(const CcsDev &M, const uint64_t *w, const uint64_t *z, int nz, uint64_t *out, hipStream_t st) {
+  if (!nz) return hipSuccess;
   const int tb = slot_words(M.d), ns = M.d / tb, spb = ns < MT ? ns : MT;
   const dim3 grid((unsigned)M.t, (unsigned)nz, (unsigned)(ns / spb));
   if (tb == 3)

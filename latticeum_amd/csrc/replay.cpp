@@ -7,7 +7,9 @@
 //   collect_folding_vars (:465-581) with its sumcheck (:596-659).
 // Sequential scalar work (the transcript and a few thousand Fq3 products), so
 // it is host code; Phi_72 only (the replay is written for TAU = 3).
+#include <array>
 #include <cstring>
+
 #include <vector>
 
 #include "../../include/lf.h"
@@ -16,13 +18,20 @@
 namespace {
 
 constexpr int D = 24, S8 = 8;
-using Elem = std::vector<uint64_t>;  // one NTT element: 8 Fq3 slots
+using Elem = std::array<uint64_t, 24>;  // one NTT element: 8 Fq3 slots (no heap traffic per operation)
 
+// Fq3 product: each output is a sum of products taken in 128 bits and reduced
+// once (gl::reduce128 takes any 128-bit value); the nonresidue 2^40 a shift
+inline uint64_t dot2(uint64_t a, uint64_t b, uint64_t c, uint64_t e) {  // a b + c e mod p
+  const unsigned __int128 x = (unsigned __int128)a * b, y = (unsigned __int128)c * e;
+  const unsigned __int128 s = x + y;
+  const uint64_t r = gl::canon(gl::reduce128((uint64_t)s, (uint64_t)(s >> 64)));
+  return s < x ? gl::add(r, 0xFFFFFFFE00000001ull) : r;  // a carry out: + 2^128 == -2^32 == p - 2^32
+}
 void f3mul(const uint64_t *a, const uint64_t *b, uint64_t *o) {
-  const uint64_t nr = 1ull << 40;
-  const uint64_t c0 = gl::add(gl::mul(a[0], b[0]), gl::mul(nr, gl::add(gl::mul(a[1], b[2]), gl::mul(a[2], b[1]))));
-  const uint64_t c1 = gl::add(gl::add(gl::mul(a[0], b[1]), gl::mul(a[1], b[0])), gl::mul(nr, gl::mul(a[2], b[2])));
-  const uint64_t c2 = gl::add(gl::add(gl::mul(a[0], b[2]), gl::mul(a[1], b[1])), gl::mul(a[2], b[0]));
+  const uint64_t c0 = gl::add(gl::mul(a[0], b[0]), gl::shl96(dot2(a[1], b[2], a[2], b[1]), 40));
+  const uint64_t c1 = gl::add(dot2(a[0], b[1], a[1], b[0]), gl::shl96(gl::mul(a[2], b[2]), 40));
+  const uint64_t c2 = gl::add(dot2(a[0], b[2], a[1], b[1]), gl::mul(a[2], b[0]));
   o[0] = c0;
   o[1] = c1;
   o[2] = c2;
@@ -40,9 +49,16 @@ void f3inv(const uint64_t *a, uint64_t *o) {
   o[1] = gl::mul(t1, ni);
   o[2] = gl::mul(t2, ni);
 }
-Elem zero() { return Elem(D, 0); }
+// the per-instance loops (2K instances, each writing only its own outputs; the
+// sums over instances are taken afterwards)
+template <class F>
+void each(int n, F fn) {
+  for (int i = 0; i < n; i++) fn(i);
+}
+
+Elem zero() { return Elem{}; }
 Elem scal(const uint64_t *b) {  // from_scalar of an Fq3
-  Elem e(D);
+  Elem e;
   for (int i = 0; i < D; i++) e[i] = b[i % 3];
   return e;
 }
@@ -55,21 +71,25 @@ Elem fromu(uint64_t x) {
   return scal(b);
 }
 Elem mul(const Elem &a, const Elem &b) {
-  Elem r(D);
+  Elem r;
   for (int s = 0; s < S8; s++) f3mul(&a[3 * s], &b[3 * s], &r[3 * s]);
   return r;
 }
 Elem add(const Elem &a, const Elem &b) {
-  Elem r(D);
+  Elem r;
   for (int i = 0; i < D; i++) r[i] = gl::add(a[i], b[i]);
   return r;
 }
 Elem sub(const Elem &a, const Elem &b) {
-  Elem r(D);
+  Elem r;
   for (int i = 0; i < D; i++) r[i] = gl::sub(a[i], b[i]);
   return r;
 }
-Elem at(const uint64_t *p, size_t i) { return Elem(p + i * D, p + (i + 1) * D); }
+Elem at(const uint64_t *p, size_t i) {
+  Elem e;
+  memcpy(e.data(), p + i * D, D * 8);
+  return e;
+}
 void put(uint64_t *p, size_t i, const Elem &e) { memcpy(p + i * D, e.data(), D * 8); }
 
 struct Tr {
@@ -243,7 +263,7 @@ int replay(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *acc, con
   T.label("beta_s");
   for (int i = 0; i < s; i++) put(out->beta, i, T.challenge());
   Elem g1 = zero(), g3 = zero();
-  for (int i = 0; i < 2 * K; i++) {
+  each(2 * K, [&](int i) {
     const int side = i / K, k = i % K;
     const uint64_t *v = vs[side].data() + (size_t)k * tau * D, *u = us[side].data() + (size_t)k * t * D;
     const Elem a = at(out->alpha, i), z = at(out->zeta, i);
@@ -253,7 +273,6 @@ int replay(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *acc, con
     put(out->claim_g1_h1, i, h1);
     put(out->claim_g1_h2, i, h2);
     put(out->claim_g1_terms, i, ci);
-    g1 = add(g1, ci);
     Elem h = add(mul(z, at(u, t - 1)), at(u, t - 2));
     size_t hk = (size_t)i * (t - 1);
     put(out->claim_g3_h, hk++, h);
@@ -261,9 +280,11 @@ int replay(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *acc, con
       h = add(mul(z, h), at(u, j));
       put(out->claim_g3_h, hk++, h);
     }
-    const Elem c3 = mul(z, h);
-    put(out->claim_g3_terms, i, c3);
-    g3 = add(g3, c3);
+    put(out->claim_g3_terms, i, mul(z, h));
+  });
+  for (int i = 0; i < 2 * K; i++) {
+    g1 = add(g1, at(out->claim_g1_terms, i));
+    g3 = add(g3, at(out->claim_g3_terms, i));
   }
   put(out->claim_g1, 0, g1);
   put(out->claim_g3, 0, g3);
@@ -272,7 +293,8 @@ int replay(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *acc, con
   // compute_sumcheck_claim_expected_value (folding/utils.rs:380-421)
   const Elem e_ast = eq(out->beta, out->fold_point, s, nullptr, nullptr, nullptr);
   Elem should = zero();
-  for (int i = 0; i < 2 * K; i++) {
+  std::vector<Elem> should_i(2 * K);
+  each(2 * K, [&](int i) {
     const uint64_t *ri = i < K ? ar.data() : out->lin_point;
     const Elem e_i = eq(ri, out->fold_point, s, nullptr, nullptr, nullptr);
     const Elem a = at(out->alpha, i), z = at(out->zeta, i), mu = at(out->mu, i);
@@ -286,13 +308,19 @@ int replay(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *acc, con
       norm = add(norm, mul(pm, prod));
       pm = mul(pm, mu);
     }
-    Elem se = zero(), pz = z;
+    // zeta_i is a base-ring challenge in every slot, so its powers are one Fq3 chain
+    Elem se = zero();
+    uint64_t pz[3], z3[3] = {z[0], z[1], z[2]};
+    memcpy(pz, z3, 24);
     for (int j = 0; j < t; j++) {
-      se = add(se, mul(pz, at(et.data(), (size_t)i * t + j)));
-      pz = mul(pz, z);
+      se = add(se, mul(scal(pz), at(et.data(), (size_t)i * t + j)));
+      uint64_t nx[3];
+      f3mul(pz, z3, nx);
+      memcpy(pz, nx, 24);
     }
-    should = add(should, add(add(mul(sa, e_i), mul(e_ast, norm)), mul(e_i, se)));
-  }
+    should_i[i] = add(add(mul(sa, e_i), mul(e_ast, norm)), mul(e_i, se));
+  });
+  for (int i = 0; i < 2 * K; i++) should = add(should, should_i[i]);
   put(out->should_equal_s, 0, should);
   for (int i = 0; i < 2 * K; i++) T.absorb(th.data() + (size_t)i * tau * D, tau);
   for (int i = 0; i < 2 * K; i++) T.absorb(et.data() + (size_t)i * t * D, t);
@@ -304,7 +332,7 @@ int replay(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *acc, con
   memcpy(out->rho, rc.data(), rc.size() * 8);
   for (int i = 0; i < 2 * K; i++) ring::phi72_crt(out->rho + (size_t)i * D);
   // the rho-weighted products of the folded instance (:549-569)
-  for (int i = 0; i < 2 * K; i++) {
+  each(2 * K, [&](int i) {
     const int side = i / K, k = i % K;
     const Elem r = at(out->rho, i);
     for (size_t j = 0; j < kappa; j++)
@@ -312,7 +340,7 @@ int replay(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *acc, con
     for (int j = 0; j < t; j++) put(out->final_u, (size_t)i * t + j, mul(at(et.data(), (size_t)i * t + j), r));
     for (size_t j = 0; j <= l; j++)
       put(out->final_x, (size_t)i * (l + 1) + j, mul(at(xs[side].data() + (size_t)k * (l + 1) * D, j), r));
-  }
+  });
   const int pb = lf_transcript_playback_status(T.t);
   if (pb != LF_ERR_INVALID_ARG && pb != LF_OK) return pb;  // a playback must draw exactly the logged samples
   if (repr == LF_REPR_MONTGOMERY) {

@@ -44,16 +44,18 @@ __global__ void k_eq_table(const uint64_t *r, int nv, int d, uint64_t *out) {
 // ---------------------------------------------------------------- fix_variables
 // dense.rs:171-199 for one point: out[m][b] = in[m][2b] + r (in[m][2b+1] - in[m][2b]),
 // r a base-ring value in every slot; out-of-place (ping-pong buffers)
+// ptrs (optional, device): MLE m starts at ptrs[m] instead of in + m in_stride (the
+// linearization's first round reads its MLEs where the Mz products left them)
 template <int TB>
-__global__ void k_fix_first(const uint64_t *in, size_t in_stride, int nm, size_t half, int d, Sv<TB> r,
-                            uint64_t *out, size_t out_stride) {
+__global__ void k_fix_first(const uint64_t *in, size_t in_stride, const uint64_t *const *ptrs, int nm, size_t half,
+                            int d, Sv<TB> r, uint64_t *out, size_t out_stride) {
   const int ns = d / TB;
   const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // (m, b, slot)
   if (i >= (size_t)nm * half * ns) return;
   const size_t mb = i / ns;
   const int s = (int)(i - mb * ns);
   const size_t m = mb / half, b = mb - m * half;
-  const uint64_t *p = in + m * in_stride + 2 * b * d + s * TB;
+  const uint64_t *p = (ptrs ? ptrs[m] : in + m * in_stride) + 2 * b * d + s * TB;
   const Sv<TB> left = s_load<TB>(p), right = s_load<TB>(p + d);
   s_store(out + m * out_stride + b * d + s * TB, s_add(left, s_mul(r, s_sub(right, left))));
 }
@@ -204,8 +206,9 @@ __global__ void k_fold_weights(const uint64_t *mu, int nk, int tau, int d, uint6
 //   comb = v_last * sum_i c_i prod_(j in S_i) v_j
 // v_j indexes the MLE list by the matrix index j, as the reference does.
 template <int TB, int DEG>
-__global__ void __launch_bounds__(RT) k_round_lin(const uint64_t *mles, size_t stride, int nm, const uint64_t *c,
-                                                  CombS cs, size_t half, int d, int spb, uint64_t *partial) {
+__global__ void __launch_bounds__(RT) k_round_lin(const uint64_t *mles, size_t stride, const uint64_t *const *ptrs,
+                                                  int nm, const uint64_t *c, CombS cs, size_t half, int d, int spb,
+                                                  uint64_t *partial) {
   const int slot_l = threadIdx.x % spb, lane_p = threadIdx.x / spb, ppb = RT / spb;
   const int slot = blockIdx.y * spb + slot_l;
   // the sum over the multisets is split over blockIdx.z chunks when the points are few
@@ -216,8 +219,9 @@ __global__ void __launch_bounds__(RT) k_round_lin(const uint64_t *mles, size_t s
 #pragma unroll
   for (int e = 0; e <= degree; e++) acc[e] = s_zero<TB>();
   for (size_t b = (size_t)blockIdx.x * ppb + lane_p; b < half; b += (size_t)gridDim.x * ppb) {
-    const uint64_t *pb = mles + 2 * b * d + slot * TB;
-    const uint64_t *pe = pb + (size_t)(nm - 1) * stride;
+    const size_t pofs = 2 * b * d + slot * TB;
+    auto mle = [&](int m) { return (ptrs ? ptrs[m] : mles + (size_t)m * stride) + pofs; };
+    const uint64_t *pe = mle(nm - 1);
     // every MLE value of a multiset is loaded once and walked along the line
     // x(e) = a + e (b - a) by additions, multiplied into all degree + 1 terms
     Sv<TB> sum[degree + 1];
@@ -235,7 +239,7 @@ __global__ void __launch_bounds__(RT) k_round_lin(const uint64_t *mles, size_t s
         // c_i times the first one or two factors in coefficient form (2 or 6
         // products instead of 9 or 18), then the values at e = 0 .. degree by
         // forward differences (additions only)
-        const uint64_t *p = pb + (size_t)cs.idx[s0] * stride;
+        const uint64_t *p = mle(cs.idx[s0]);
         const Sv<TB> a = s_load<TB>(p);
         const Sv<TB> u0 = s_mul(ci, a), u1 = s_mul(ci, s_sub(s_load<TB>(p + d), a));  // c_i x1(e) = u0 + u1 e
         if (s1 - s0 == 1) {
@@ -246,7 +250,7 @@ __global__ void __launch_bounds__(RT) k_round_lin(const uint64_t *mles, size_t s
             if (e < degree) x = s_add(x, u1);
           }
         } else {
-          const uint64_t *q = pb + (size_t)cs.idx[s0 + 1] * stride;
+          const uint64_t *q = mle(cs.idx[s0 + 1]);
           const Sv<TB> g0 = s_load<TB>(q), g1 = s_sub(s_load<TB>(q + d), g0);  // x2(e) = g0 + g1 e
           // (u0 + u1 e)(g0 + g1 e) = k0 + k1 e + k2 e^2: f(0) = k0, delta_0 = k1 + k2, second difference 2 k2
           const Sv<TB> k0 = s_mul(u0, g0), k2 = s_mul(u1, g1);
@@ -264,7 +268,7 @@ __global__ void __launch_bounds__(RT) k_round_lin(const uint64_t *mles, size_t s
         }
       }
       for (int sx = s0 + 2 < s1 ? s0 + 2 : s1; sx < s1; sx++) {
-        const uint64_t *p = pb + (size_t)cs.idx[sx] * stride;
+        const uint64_t *p = mle(cs.idx[sx]);
         Sv<TB> x = s_load<TB>(p);
         const Sv<TB> st = s_sub(s_load<TB>(p + d), x);
 #pragma unroll
@@ -376,20 +380,20 @@ hipError_t eq_table(const uint64_t *r, int nv, int d, uint64_t *out, hipStream_t
 }
 
 hipError_t mle_fix_first(const uint64_t *in, size_t in_stride, int nm, size_t half, int d, const uint64_t *r_base,
-                         uint64_t *out, size_t out_stride, hipStream_t st) {
+                         uint64_t *out, size_t out_stride, hipStream_t st, const uint64_t *const *ptrs) {
   const int tb = slot_words(d);
   const size_t n = (size_t)nm * half * (d / tb);
   if (!n) return hipSuccess;
   if (tb == 3) {
     Sv<3> r;
     for (int i = 0; i < 3; i++) r.c[i] = r_base[i];
-    hipLaunchKernelGGL(k_fix_first<3>, dim3(blocks_of(n, 256)), dim3(256), 0, st, in, in_stride, nm, half, d, r, out,
-                       out_stride);
+    hipLaunchKernelGGL(k_fix_first<3>, dim3(blocks_of(n, 256)), dim3(256), 0, st, in, in_stride, ptrs, nm, half, d, r,
+                       out, out_stride);
   } else {
     Sv<1> r;
     r.c[0] = r_base[0];
-    hipLaunchKernelGGL(k_fix_first<1>, dim3(blocks_of(n, 256)), dim3(256), 0, st, in, in_stride, nm, half, d, r, out,
-                       out_stride);
+    hipLaunchKernelGGL(k_fix_first<1>, dim3(blocks_of(n, 256)), dim3(256), 0, st, in, in_stride, ptrs, nm, half, d, r,
+                       out, out_stride);
   }
   return hipGetLastError();
 }
@@ -462,13 +466,14 @@ hipError_t round_folding(const uint64_t *mles, size_t stride, int nf, const uint
 }
 
 hipError_t round_lin(const uint64_t *mles, size_t stride, int nm, const uint64_t *c, const CombS &cs, int degree,
-                     size_t half, int d, uint64_t *partial, uint64_t *evals, hipStream_t st) {
+                     size_t half, int d, uint64_t *partial, uint64_t *evals, hipStream_t st,
+                     const uint64_t *const *ptrs) {
   if (degree + 1 > MAX_EVALS || degree < 1 || !half) return hipErrorInvalidValue;
   int spb;
   dim3 grid;
   round_geom(d, half, cs.q, spb, grid);
 #define LF_RL(TB, DG) \
-  hipLaunchKernelGGL((k_round_lin<TB, DG>), grid, dim3(RT), 0, st, mles, stride, nm, c, cs, half, d, spb, partial)
+  hipLaunchKernelGGL((k_round_lin<TB, DG>), grid, dim3(RT), 0, st, mles, stride, ptrs, nm, c, cs, half, d, spb, partial)
 #define LF_RL_DEG(TB)                          \
   switch (degree) {                            \
     case 1: LF_RL(TB, 1); break;               \

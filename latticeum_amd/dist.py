@@ -5,9 +5,12 @@ Two ways to spread the commit+fold path over the GPUs of a node:
 
 * independent step streams (BASELINE.json configs[3], the trace-batch shard):
   every rank folds its own trace-step witnesses. Steps never exchange data,
-  so there is no collective on the data path (weak scaling); the ranks'
-  folded accumulators can be summed once with ``AccumulatorReducer``
-  (lf_fold_reduce_allranks).
+  so there is no collective on the data path (weak scaling), and the ranks'
+  accumulators stay separate: summing unrelated accumulators has no
+  LatticeFold meaning, so bench.py's N > 1 line does not do it.
+  ``AccumulatorReducer`` (lf_fold_reduce_allranks, a mod-p sum of field
+  vectors over ranks) remains as a plumbing utility for callers that do own
+  a sum over ranks; nothing on the measured path calls it.
 * one fold sharded by columns: rank r owns the witness
   columns of groups ``shard_groups(W, r, world)`` and the matching columns of
   the Ajtai matrix. The commitments are sums over columns, so each rank's are
@@ -83,8 +86,8 @@ def shard_groups(W: int, rank: int, world: int, align: int = 16):
 
 class AccumulatorReducer:
     """In place, t <- sum over ranks of t (mod p) for each field vector t, over
-    the C ABI's RCCL communicator on the context stream (independent step
-    streams: the ranks' folded accumulators cm_0 and f_0)."""
+    the C ABI's RCCL communicator on the context stream. A utility only: the
+    bench's N > 1 lines never sum accumulators (see the module docstring)."""
 
     def __init__(self, comm, tensors):
         self.comm = comm
