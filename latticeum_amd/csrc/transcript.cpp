@@ -79,32 +79,64 @@ inline uint64_t wsum(const uint64_t *v, int n) {
   const uint64_t lo = (uint64_t)acc, hi = (uint64_t)(acc >> 64);
   return wadd(lo, (hi << 32) - hi);
 }
-inline void mds4(uint64_t *x) {  // one 4 x 4 block of the external linear layer (as before: t + x_i + 2 x_(i+1))
-  const uint64_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3];
-  const uint64_t t = wadd(wadd(x0, x1), wadd(x2, x3));
-  x[0] = wadd(t, wadd(x0, wadd(x1, x1)));
-  x[1] = wadd(t, wadd(x1, wadd(x2, x2)));
-  x[2] = wadd(t, wadd(x2, wadd(x3, x3)));
-  x[3] = wadd(t, wadd(x3, wadd(x0, x0)));
+// a b + c with one 128-bit fold (any u64 in and out; a b + c < 2^128)
+inline uint64_t wmuladd(uint64_t a, uint64_t b, uint64_t c) {
+  const unsigned __int128 t = (unsigned __int128)a * b + c;
+  uint64_t r = (uint64_t)t;
+  const uint64_t hi = (uint64_t)(t >> 64), h1 = hi >> 32, h0 = hi & gl::EPS, u = (h0 << 32) - h0;
+#if defined(__x86_64__)
+  uint64_t m;
+  asm("subq %[h1], %[r]\n\tsbbq %[m], %[m]\n\tmovl %k[m], %k[m]\n\tsubq %[m], %[r]\n\t"
+      "addq %[u], %[r]\n\tsbbq %[m], %[m]\n\tmovl %k[m], %k[m]\n\taddq %[m], %[r]"
+      : [r] "+r"(r), [m] "=&r"(m)
+      : [h1] "r"(h1), [u] "r"(u)
+      : "cc");
+  return r;
+#else
+  const uint64_t br = __builtin_sub_overflow(r, h1, &r);
+  r -= br * gl::EPS;
+  const uint64_t cr = __builtin_add_overflow(r, u, &r);
+  return r + cr * gl::EPS;
+#endif
 }
-void mds16(uint64_t *s) {
-  #pragma unroll
-  for (int c = 0; c < 16; c += 4) mds4(s + c);
-  #pragma unroll
+typedef unsigned __int128 u128;
+inline uint64_t red96(u128 v) {  // v < 2^96: lo + hi (2^32 - 1)
+  const uint64_t lo = (uint64_t)v, hi = (uint64_t)(v >> 64);
+  return wadd(lo, (hi << 32) - hi);
+}
+// The external linear layer (MDSMat4 on each 4-chunk, then the column sums) on
+// 128-bit sums of the u64 inputs with one fold per output, and the next round's
+// constants (rc, or none) added inside the same sum: 16 folds instead of the 76
+// modular additions of the word-by-word form (mds16)
+inline void mds16_rc(uint64_t *s, const uint64_t *rc) {
+  u128 y[16];
+#pragma unroll
+  for (int c = 0; c < 16; c += 4) {
+    const u128 x0 = s[c], x1 = s[c + 1], x2 = s[c + 2], x3 = s[c + 3];
+    const u128 t = x0 + x1 + x2 + x3;
+    y[c] = t + x0 + 2 * x1;  // as mds4: t + x_i + 2 x_(i+1)
+    y[c + 1] = t + x1 + 2 * x2;
+    y[c + 2] = t + x2 + 2 * x3;
+    y[c + 3] = t + x3 + 2 * x0;
+  }
+#pragma unroll
   for (int k = 0; k < 4; k++) {
-    const uint64_t col[4] = {s[k], s[4 + k], s[8 + k], s[12 + k]};
-    const uint64_t sum = wsum(col, 4);
-    #pragma unroll
-    for (int j = k; j < 16; j += 4) s[j] = wadd(s[j], sum);
+    const u128 col = y[k] + y[4 + k] + y[8 + k] + y[12 + k];
+#pragma unroll
+    for (int j = k; j < 16; j += 4) s[j] = red96(y[j] + col + (rc ? rc[j] : 0));
   }
 }
+void mds16(uint64_t *s) { mds16_rc(s, nullptr); }
+// The sponge's permutation. Round constants ride in the preceding layer's sums
+// (the initial MDS carries round 0's, the last internal round adds the terminal
+// rounds' first); the internal rounds' diagonal product and the sum share one fold.
 void permute(uint64_t *s) {
-  mds16(s);
+  mds16_rc(s, EXT_INIT);
   #pragma unroll
   for (int r = 0; r < 4; r++) {
     #pragma unroll
-    for (int i = 0; i < 16; i++) s[i] = sbox7(wadd(s[i], EXT_INIT[16 * r + i]));
-    mds16(s);
+    for (int i = 0; i < 16; i++) s[i] = sbox7(s[i]);
+    mds16_rc(s, r < 3 ? EXT_INIT + 16 * (r + 1) : nullptr);
   }
   #pragma unroll
   for (int r = 0; r < 22; r++) {
@@ -114,13 +146,15 @@ void permute(uint64_t *s) {
     s[0] = sbox7(wadd(s[0], INTERNAL[r]));
     const uint64_t sum = wadd(rest, s[0]);
     #pragma unroll
-    for (int i = 0; i < 16; i++) s[i] = wadd(wmul(s[i], DIAG_M1[i]), sum);
+    for (int i = 0; i < 16; i++) s[i] = wmuladd(s[i], DIAG_M1[i], sum);
   }
+  #pragma unroll
+  for (int i = 0; i < 16; i++) s[i] = wadd(s[i], EXT_TERM[i]);
   #pragma unroll
   for (int r = 0; r < 4; r++) {
     #pragma unroll
-    for (int i = 0; i < 16; i++) s[i] = sbox7(wadd(s[i], EXT_TERM[16 * r + i]));
-    mds16(s);
+    for (int i = 0; i < 16; i++) s[i] = sbox7(s[i]);
+    mds16_rc(s, r < 3 ? EXT_TERM + 16 * (r + 1) : nullptr);
   }
   #pragma unroll
   for (int i = 0; i < 16; i++) s[i] = gl::canon(s[i]);
@@ -144,7 +178,7 @@ void permute_states(uint64_t *s, uint64_t *st) {
     const uint64_t rest = wsum(s + 1, 15);
     s[0] = sbox7(wadd(s[0], INTERNAL[r]));
     const uint64_t sum = wadd(rest, s[0]);
-    for (int i = 0; i < 16; i++) s[i] = wadd(wmul(s[i], DIAG_M1[i]), sum);
+    for (int i = 0; i < 16; i++) s[i] = wmuladd(s[i], DIAG_M1[i], sum);
     keep(5 + r);
   }
   for (int r = 0; r < 4; r++) {
@@ -158,23 +192,33 @@ void permute_states(uint64_t *s, uint64_t *st) {
 // width 8 (MDSMat4 on both 4-chunks, then the column sums), the reference's
 // width-8 external constants (crypto_consts.rs:9-96) and Plonky3's
 // MATRIX_DIAG_8_GOLDILOCKS (not vendored: restated, parity unpinned)
-void mds8(uint64_t *s) {
-  mds4(s);
-  mds4(s + 4);
-  #pragma unroll
+// width 8: MDSMat4 on both 4-chunks, then the column sums, on 128-bit sums with the
+// next round's constants inside (as mds16_rc)
+inline void mds8_rc(uint64_t *s, const uint64_t *rc) {
+  u128 y[8];
+#pragma unroll
+  for (int c = 0; c < 8; c += 4) {
+    const u128 x0 = s[c], x1 = s[c + 1], x2 = s[c + 2], x3 = s[c + 3];
+    const u128 t = x0 + x1 + x2 + x3;
+    y[c] = t + x0 + 2 * x1;
+    y[c + 1] = t + x1 + 2 * x2;
+    y[c + 2] = t + x2 + 2 * x3;
+    y[c + 3] = t + x3 + 2 * x0;
+  }
+#pragma unroll
   for (int k = 0; k < 4; k++) {
-    const uint64_t sum = wadd(s[k], s[4 + k]);
-    s[k] = wadd(s[k], sum);
-    s[4 + k] = wadd(s[4 + k], sum);
+    const u128 col = y[k] + y[4 + k];
+    s[k] = red96(y[k] + col + (rc ? rc[k] : 0));
+    s[4 + k] = red96(y[4 + k] + col + (rc ? rc[4 + k] : 0));
   }
 }
 void permute8(uint64_t *s) {
-  mds8(s);
+  mds8_rc(s, W8_EXT_INIT);
   #pragma unroll
   for (int r = 0; r < 4; r++) {
     #pragma unroll
-    for (int i = 0; i < 8; i++) s[i] = sbox7(wadd(s[i], W8_EXT_INIT[8 * r + i]));
-    mds8(s);
+    for (int i = 0; i < 8; i++) s[i] = sbox7(s[i]);
+    mds8_rc(s, r < 3 ? W8_EXT_INIT + 8 * (r + 1) : nullptr);
   }
   #pragma unroll
   for (int r = 0; r < 22; r++) {
@@ -182,13 +226,15 @@ void permute8(uint64_t *s) {
     s[0] = sbox7(wadd(s[0], INTERNAL[r]));
     const uint64_t sum = wadd(rest, s[0]);
     #pragma unroll
-    for (int i = 0; i < 8; i++) s[i] = wadd(wmul(s[i], W8_DIAG_M1[i]), sum);
+    for (int i = 0; i < 8; i++) s[i] = wmuladd(s[i], W8_DIAG_M1[i], sum);
   }
+  #pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = wadd(s[i], W8_EXT_TERM[i]);
   #pragma unroll
   for (int r = 0; r < 4; r++) {
     #pragma unroll
-    for (int i = 0; i < 8; i++) s[i] = sbox7(wadd(s[i], W8_EXT_TERM[8 * r + i]));
-    mds8(s);
+    for (int i = 0; i < 8; i++) s[i] = sbox7(s[i]);
+    mds8_rc(s, r < 3 ? W8_EXT_TERM + 8 * (r + 1) : nullptr);
   }
   #pragma unroll
   for (int i = 0; i < 8; i++) s[i] = gl::canon(s[i]);
