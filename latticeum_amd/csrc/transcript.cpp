@@ -262,7 +262,9 @@ void sponge8(Next next, size_t n, uint64_t out4[4]) {
 
 struct lf_transcript {
   uint64_t state[16] = {0};
-  std::vector<uint64_t> in, out;
+  // Plonky3 DuplexChallenger's input and output buffers (at most RATE = 12 each)
+  uint64_t in[12], out[12];
+  int nin = 0, nout = 0;
   // record: every sampled value is appended to `log`. playback: samples come
   // from `log` in order and observes are dropped -- a transcript that absorbs
   // the same messages in the same order samples the same values, so a replay of
@@ -272,10 +274,16 @@ struct lf_transcript {
   size_t pos = 0;
   bool underrun = false;
   void duplexing() {  // Plonky3 DuplexChallenger::duplexing (overwrite mode)
-    for (size_t i = 0; i < in.size(); i++) state[i] = in[i];
-    in.clear();
+    for (int i = 0; i < nin; i++) state[i] = in[i];
+    nin = 0;
     permute(state);
-    out.assign(state, state + 12);
+    memcpy(out, state, sizeof(out));
+    nout = 12;
+  }
+  void observe(uint64_t v) {  // v canonical
+    nout = 0;
+    in[nin++] = v;
+    if (nin == 12) duplexing();
   }
 };
 
@@ -286,9 +294,7 @@ void lf_transcript_free(lf_transcript *t) { delete t; }
 
 void lf_transcript_observe(lf_transcript *t, uint64_t v) {
   if (t->playback) return;
-  t->out.clear();
-  t->in.push_back(gl::canon(v));
-  if (t->in.size() == 12) t->duplexing();
+  t->observe(gl::canon(v));
 }
 
 uint64_t lf_transcript_sample(lf_transcript *t) {
@@ -297,9 +303,8 @@ uint64_t lf_transcript_sample(lf_transcript *t) {
     t->underrun = true;
     return 0;
   }
-  if (!t->in.empty() || t->out.empty()) t->duplexing();
-  uint64_t v = t->out.back();
-  t->out.pop_back();
+  if (t->nin || !t->nout) t->duplexing();
+  const uint64_t v = t->out[--t->nout];
   if (t->recording) t->log.push_back(v);
   return v;
 }
@@ -326,8 +331,13 @@ int lf_transcript_playback_status(const lf_transcript *t) {
 
 void lf_transcript_absorb_ring(lf_transcript *t, const uint64_t *e, size_t n, int d, int repr) {
   // fiat_shamir.rs:51-60: observe elem.0.0[0], the ark Montgomery limb
-  for (size_t i = 0; i < n * (size_t)d; i++)
-    lf_transcript_observe(t, repr == LF_REPR_MONTGOMERY ? e[i] : gl::canon(wmul(e[i], gl::EPS)));  // gl::to_mont
+  if (t->playback) return;
+  const size_t m = n * (size_t)d;
+  if (repr == LF_REPR_MONTGOMERY) {
+    for (size_t i = 0; i < m; i++) t->observe(gl::canon(e[i]));
+  } else {
+    for (size_t i = 0; i < m; i++) t->observe(gl::canon(wmul(e[i], gl::EPS)));  // gl::to_mont
+  }
 }
 
 void lf_transcript_get_challenge(lf_transcript *t, uint64_t out3[3]) {
