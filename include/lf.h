@@ -406,6 +406,16 @@ int lf_sumcheck_prove(lf_ctx *ctx, lf_transcript *t, const lf_comb *comb, uint64
  * the later rounds (the linearization sumcheck reads its Mz MLEs in place) */
 int lf_sumcheck_prove_ptrs(lf_ctx *ctx, lf_transcript *t, const lf_comb *comb, const uint64_t *const *mles, int nm,
                            int nv, int d, int degree, uint64_t *work, uint64_t *proof, uint64_t *randomness);
+/* the linearization sumcheck (LFLinearizationProver::prove's, linearization.rs:153-197
+ * over linearization/utils.rs:63-104) with eq(beta) given by beta itself: the proof and
+ * randomness of lf_sumcheck_prove over [mles..., eq(beta)] (same transcript), with
+ * eq(beta) split off each round (eq(beta_i, X) and eq over the unbound variables), so
+ * the device evaluates a polynomial of one degree less. mles: nm device pointers as in
+ * lf_sumcheck_prove_ptrs (S_idx < nm); beta: host [nv][d] broadcast base-ring values;
+ * every multiset has fewer than `degree` entries; work: nm x 2^(nv-2) elements */
+int lf_sumcheck_prove_lin(lf_ctx *ctx, lf_transcript *t, const lf_comb *comb, const uint64_t *const *mles, int nm,
+                          int nv, int d, int degree, const uint64_t *beta, uint64_t *work, uint64_t *proof,
+                          uint64_t *randomness);
 
 /* ------------------------------------------------------------ sparse Mz products
  * CCS.M (latticefold/src/arith.rs:51-74): t matrices m x n of ring elements,

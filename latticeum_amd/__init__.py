@@ -329,6 +329,20 @@ class Context:
                                               degree, _ptr(proof), _ptr(rnd)))
         return proof, rnd
 
+    def sumcheck_prove_lin(self, transcript: "Poseidon2Transcript", comb: "Comb", mles, nv: int, d: int,
+                           degree: int, beta, work):
+        """the linearization sumcheck with eq(beta) split off (lf_sumcheck_prove_lin): mles a
+        list of device tensors (one MLE of 2^nv elements each, read only), beta [nv][d] host
+        values; the proof and randomness of sumcheck_prove over [mles..., eq(beta)]"""
+        tau = 3 if d == 24 else 1
+        proof = np.zeros(nv * (degree + 1) * d, np.uint64)
+        rnd = np.zeros(nv * tau, np.uint64)
+        ptrs = (C.c_void_p * len(mles))(*[_dptr(m) for m in mles])
+        b = _u64(beta)
+        self.check(self.lib.lf_sumcheck_prove_lin(self.h, transcript.h, C.byref(comb.s), ptrs, len(mles), nv, d,
+                                                  degree, _ptr(b), _dptr(work), _ptr(proof), _ptr(rnd)))
+        return proof, rnd
+
     # ---------------------------------------------------------------- width-8 Merkle trees
     def dev_poseidon2_w8_permute(self, t):
         self.check(self.lib.lf_dev_poseidon2_w8_permute(self.h, _dptr(t), t.numel() // 8))

@@ -214,6 +214,7 @@ SIGNATURES = {
     "lf_dev_sumcheck_round": (I, [VP, C.POINTER(LfComb), VP, SZ, I, I, I, I, VP]),
     "lf_sumcheck_prove": (I, [VP, VP, C.POINTER(LfComb), VP, I, I, I, I, VP, VP]),
     "lf_sumcheck_prove_ptrs": (I, [VP, VP, C.POINTER(LfComb), VP, I, I, I, I, VP, VP, VP]),
+    "lf_sumcheck_prove_lin": (I, [VP, VP, C.POINTER(LfComb), VP, I, I, I, I, VP, VP, VP, VP]),
     "lf_fold_lcccs": (I, [VP, I, I, VP, VP, VP, SZ, VP, SZ, VP, VP, VP, VP, I]),
     "lf_dev_fold_lcccs": (I, [VP, I, I, VP, VP, VP, SZ, VP, SZ, VP, VP, VP, VP]),
     "lf_compute_x_s": (I, [VP, C.POINTER(LfParams), VP, SZ, VP, I]),

@@ -20,6 +20,7 @@
 
 #include "../../include/lf.h"
 #include "gl.hpp"
+#include "kernels.hpp"
 
 struct lf_prover {
   lf_ctx *ctx = nullptr;
@@ -55,7 +56,8 @@ struct lf_prover {
   // the points the device needs go out through it
   uint64_t *pin = nullptr;
   uint64_t *hx[2] = {}, *hy[2] = {}, *hu[2] = {}, *hv[2] = {}, *hr[2] = {}, *htheta = nullptr, *heta = nullptr;
-  hipEvent_t ev[3] = {};
+  // ev[0], ev[1]: per-side / theta readiness; ev[2 + g]: instance group g's messages
+  hipEvent_t ev[2 + 2 * 16] = {};
   ~lf_prover() {
     int prev = -1;
     if (hipGetDevice(&prev) == hipSuccess && prev != device) (void)hipSetDevice(device);
@@ -68,6 +70,10 @@ struct lf_prover {
 };
 
 namespace {
+
+// instances per u_s / eta_s launch (and per host wait): two fill the chip with
+// t blocks each, and the host starts absorbing after the first group
+constexpr int MZ_GROUP = 2;
 
 // the Fq3 = Fq[u]/(u^3 - 2^40) product of two base-ring elements (tb = 3), or the Fq one
 void base_mul(const uint64_t *a, const uint64_t *b, uint64_t *o, int tb) {
@@ -196,8 +202,9 @@ int linearize(lf_prover *P, Run &R, const std::vector<uint64_t> &xc, const lf_wi
   // (linearization/utils.rs:71-84), and the combination reads list position j for
   // matrix index j (as the reference does) and the last entry -- so only those
   // positions are live. Their MLEs are read where the Mz products left them (a
-  // pointer table; no copies), the dead positions are never fixed, and eq(beta)
-  // sits at the front of P->lin, the rest of which serves the later rounds.
+  // pointer table; no copies), the dead positions are never fixed, and eq(beta) is
+  // split off each round (lf_sumcheck_prove_lin: beta itself, no eq MLE); P->lin
+  // serves the later rounds.
   std::vector<int> live_of(P->lin_list.size(), -1), S_live(P->S_idx.size());
   std::vector<const uint64_t *> ptr;
   for (size_t k = 0; k < P->S_idx.size(); k++) {
@@ -212,8 +219,6 @@ int linearize(lf_prover *P, Run &R, const std::vector<uint64_t> &xc, const lf_wi
     }
     S_live[k] = live_of[p];
   }
-  R.check(lf_dev_eq_table(C, d, P->beta, s, P->lin), "eq(beta)");
-  ptr.push_back(P->lin);
   std::vector<uint64_t> rnd((size_t)s * tb);
   {
     lf_comb cb{};
@@ -223,8 +228,8 @@ int linearize(lf_prover *P, Run &R, const std::vector<uint64_t> &xc, const lf_wi
     cb.S_off = P->S_off.data();
     cb.S_idx = S_live.data();
     if (R.rc == LF_OK)
-      R.check(lf_sumcheck_prove_ptrs(C, R.T, &cb, ptr.data(), (int)ptr.size(), s, d, P->degree + 1, P->lin + nn * d,
-                                     lin_sumcheck, rnd.data()),
+      R.check(lf_sumcheck_prove_lin(C, R.T, &cb, ptr.data(), (int)ptr.size(), s, d, P->degree + 1, beta.data(),
+                                    P->lin, lin_sumcheck, rnd.data()),
               "linearization sumcheck");
   }
   if (R.rc) return R.rc;
@@ -517,53 +522,57 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
     b.y[side] = P->y[side];
   }
   if (R.rc == LF_OK) R.check(lf_dev_decompose_commit(C, P->aj, &P->pr, W, &b), "decompose + commit_witnesses");
-  // z_k = x_s[k] || w_ccs_k (compute_mz_mles, :229-256) for the u_s (and later eta_s)
+  // z_k = x_s[k] || w_ccs_k (compute_mz_mles, :229-256) for the u_s (and later eta_s), one
+  // launch per side (the stream's queue holds a bounded number of commands: every one
+  // saved is host time the transcript gets back)
   for (int side = 0; side < 2; side++)
-    for (int k = 0; k < K; k++) {
-      uint64_t *zk = P->zdec[side] + (size_t)k * n * d;
-      R.d2d(zk, P->xs + ((size_t)side * K + k) * (l + 1) * d, (l + 1) * d);
-      R.d2d(zk + (l + 1) * d, P->wk[side] + (size_t)k * W * d, W * d);
-    }
+    R.hip(lfk::assemble_z(P->xs + (size_t)side * K * (l + 1) * d, P->wk[side], K, l + 1, W, d, P->zdec[side], R.st),
+          "z_k");
   // per side: v_s, u_s at the side's point, then its messages back to pinned memory
-  // behind an event, so the host absorbs side 0 while the device evaluates side 1
-  // and prepares the challenge-independent folding MLEs (the f_hat MLEs of the 2K
-  // decomposed witnesses, eq(r_i); create_sumcheck_polynomial, folding/utils.rs:196-255)
+  // behind events, so the host absorbs while the device evaluates: x_s, y_s and v_s
+  // of a side first, then u_s in groups of MZ_GROUP instances (one event each: the
+  // host starts on instance 0 as soon as its u_s is back), and the challenge-
+  // independent folding MLEs (the f_hat MLEs of the 2K decomposed witnesses, eq(r_i);
+  // create_sumcheck_polynomial, folding/utils.rs:196-255) behind them
   uint64_t *M = P->fold;
   const size_t mstride = nn * d;
   // eq(r_i) of each side is the folding prover's eq(r_i) MLE (M slots 0 and 2; the
   // linearization left eq(r_lin) in slot 2): v_s and u_s read it from there
   R.h2p2d(P->pt, P->hr[0], ar.data(), (size_t)s * d);
   R.check(lf_dev_eq_table(C, d, P->pt, s, M), "eq(r_0)");
+  const int G = MZ_GROUP, ng = (K + G - 1) / G;
   for (int side = 0; side < 2; side++) {
     const uint64_t *eq_s = M + (size_t)(2 * side) * mstride;
     R.check(lf_dev_fhat_evaluate_eq(C, d, P->fkc[side], N, ND, K, s, eq_s, P->vs + (size_t)side * K * tau * d), "v_s");
-    R.check(lf_dev_mz_weights(C, P->ccs, s, eq_s, P->mzw), "u_s weights");
-    R.check(lf_dev_mz_dots(C, P->ccs, P->mzw, P->zdec[side], K, P->us + (size_t)side * K * t * d), "u_s");
     R.d2p(P->hx[side], P->xs + (size_t)side * K * (l + 1) * d, (size_t)K * (l + 1) * d);
     R.d2p(P->hy[side], P->y[side], (size_t)K * kd);
-    R.d2p(P->hu[side], P->us + (size_t)side * K * t * d, (size_t)K * t * d);
     R.d2p(P->hv[side], P->vs + (size_t)side * K * tau * d, (size_t)K * tau * d);
-    R.hip(hipEventRecord(P->ev[side], R.st), "event");
-  }
-  for (int side = 0; side < 2; side++)
-    for (int k = 0; k < K; k++)
-      R.check(lf_dev_get_fhat(C, d, P->fkc[side] + (size_t)k * ND, N, s, M + (5 + (size_t)(side * K + k) * tau) * mstride),
-              "f_hat");
-  if (R.rc) return R.rc;
-  R.mark(LF_SPAN_DECOMPOSITION, false);
-  for (int side = 0; side < 2; side++) {
-    if (R.wait(P->ev[side])) return R.rc;
-    memcpy(proof->x_s[side], P->hx[side], (size_t)K * (l + 1) * d * 8);
-    memcpy(proof->y_s[side], P->hy[side], (size_t)K * kd * 8);
-    memcpy(proof->u_s[side], P->hu[side], (size_t)K * t * d * 8);
-    memcpy(proof->v_s[side], P->hv[side], (size_t)K * tau * d * 8);
-    for (int k = 0; k < K; k++) {  // the decomposed instances' messages (:58-64)
-      R.absorb(proof->x_s[side] + (size_t)k * (l + 1) * d, l + 1);
-      R.absorb(proof->y_s[side] + (size_t)k * kd, kappa);
-      R.absorb(proof->u_s[side] + (size_t)k * t * d, t);
-      R.absorb(proof->v_s[side] + (size_t)k * tau * d, tau);
+    R.check(lf_dev_mz_weights(C, P->ccs, s, eq_s, P->mzw), "u_s weights");
+    for (int g = 0; g < ng; g++) {
+      const int k0 = g * G, nk = std::min(G, K - k0);
+      uint64_t *us = P->us + ((size_t)side * K + k0) * t * d;
+      R.check(lf_dev_mz_dots(C, P->ccs, P->mzw, P->zdec[side] + (size_t)k0 * n * d, nk, us), "u_s");
+      R.d2p(P->hu[side] + (size_t)k0 * t * d, us, (size_t)nk * t * d);
+      R.hip(hipEventRecord(P->ev[2 + side * ng + g], R.st), "event");
     }
   }
+  for (int side = 0; side < 2; side++)
+    R.hip(lfk::get_fhat(P->fkc[side], N, d, s, M + (5 + (size_t)side * K * tau) * mstride, R.st, K, ND), "f_hat");
+  if (R.rc) return R.rc;
+  R.mark(LF_SPAN_DECOMPOSITION, false);
+  for (int side = 0; side < 2; side++)
+    for (int k = 0; k < K; k++) {  // the decomposed instances' messages (:58-64)
+      if (k % G == 0 && R.wait(P->ev[2 + side * ng + k / G])) return R.rc;
+      const size_t ox = (size_t)k * (l + 1) * d, oy = (size_t)k * kd, ou = (size_t)k * t * d, ov = (size_t)k * tau * d;
+      memcpy(proof->x_s[side] + ox, P->hx[side] + ox, (l + 1) * d * 8);
+      memcpy(proof->y_s[side] + oy, P->hy[side] + oy, kd * 8);
+      memcpy(proof->u_s[side] + ou, P->hu[side] + ou, (size_t)t * d * 8);
+      memcpy(proof->v_s[side] + ov, P->hv[side] + ov, (size_t)tau * d * 8);
+      R.absorb(proof->x_s[side] + ox, l + 1);
+      R.absorb(proof->y_s[side] + oy, kappa);
+      R.absorb(proof->u_s[side] + ou, t);
+      R.absorb(proof->v_s[side] + ov, tau);
+    }
 
   R.mark(LF_SPAN_DECOMPOSITION_TRANSCRIPT, false);
   // ---- folding (folding.rs:42-130)
@@ -630,22 +639,27 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
     R.check(lf_dev_fhat_evaluate_eq(C, d, P->fkc[side], N, ND, K, s, P->eq0, P->theta + (size_t)side * K * tau * d),
             "theta");
   R.d2p(P->htheta, P->theta, 2 * (size_t)K * tau * d);
+  R.hip(hipEventRecord(P->ev[0], R.st), "event");
   R.check(lf_dev_mz_weights(C, P->ccs, s, P->eq0, P->mzw), "eta weights");
-  for (int side = 0; side < 2; side++) {
-    R.check(lf_dev_mz_dots(C, P->ccs, P->mzw, P->zdec[side], K, P->eta + (size_t)side * K * t * d), "eta");
-    R.d2p(P->heta + (size_t)side * K * t * d, P->eta + (size_t)side * K * t * d, (size_t)K * t * d);
-    R.hip(hipEventRecord(P->ev[side], R.st), "event");
+  for (int g = 0; g < 2 * ng; g++) {  // instance groups of both sides, in absorb order
+    const int side = g / ng, k0 = (g % ng) * G, nk = std::min(G, K - k0);
+    const size_t o = ((size_t)side * K + k0) * t * d;
+    R.check(lf_dev_mz_dots(C, P->ccs, P->mzw, P->zdec[side] + (size_t)k0 * n * d, nk, P->eta + o), "eta");
+    R.d2p(P->heta + o, P->eta + o, (size_t)nk * t * d);
+    R.hip(hipEventRecord(P->ev[2 + g], R.st), "event");
   }
   if (R.rc) return R.rc;
   R.mark(LF_SPAN_EVALUATIONS, false);
   if (R.wait(P->ev[0])) return R.rc;
   memcpy(proof->theta_s, P->htheta, 2 * (size_t)K * tau * d * 8);
   for (int i = 0; i < 2 * K; i++) R.absorb(proof->theta_s + (size_t)i * tau * d, tau);
-  for (int side = 0; side < 2; side++) {
-    if (side && R.wait(P->ev[1])) return R.rc;
-    memcpy(proof->eta_s + (size_t)side * K * t * d, P->heta + (size_t)side * K * t * d, (size_t)K * t * d * 8);
-    for (int k = 0; k < K; k++) R.absorb(proof->eta_s + ((size_t)side * K + k) * t * d, t);
-  }
+  for (int side = 0; side < 2; side++)
+    for (int k = 0; k < K; k++) {
+      if (k % G == 0 && R.wait(P->ev[2 + side * ng + k / G])) return R.rc;
+      const size_t o = ((size_t)side * K + k) * t * d;
+      memcpy(proof->eta_s + o, P->heta + o, (size_t)t * d * 8);
+      R.absorb(proof->eta_s + o, t);
+    }
   // get_rhos (folding/utils.rs:116-127): 2K - 1 short challenges and ONE, then CRT
   R.absorb_label("rho_s");
   std::vector<uint64_t> rc(2 * (size_t)K * d, 0);

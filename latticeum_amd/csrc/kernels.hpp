@@ -231,7 +231,12 @@ struct CombS {
 int slot_words(int d);  // words of one NTT slot: 3 (Fq3, Phi_72) or 1
 hipError_t eq_table(const uint64_t *r, int nv, int d, uint64_t *out, hipStream_t st);
 // Witness::get_fhat: tau = d / slots MLEs of 2^nv points from N <= 2^nv coefficient elements
-hipError_t get_fhat(const uint64_t *f_coeff, size_t N, int d, int nv, uint64_t *out, hipStream_t st);
+// nw witnesses wstride u64 apart -> nw consecutive groups of tau MLEs
+hipError_t get_fhat(const uint64_t *f_coeff, size_t N, int d, int nv, uint64_t *out, hipStream_t st, int nw = 1,
+                    size_t wstride = 0);
+// z_k = x_k || w_k for nz instances: out [nz][l1 + W][d]
+hipError_t assemble_z(const uint64_t *x, const uint64_t *w, int nz, size_t l1, size_t W, int d, uint64_t *out,
+                      hipStream_t st);
 // out[m][b] = in[m][2b] + r (in[m][2b+1] - in[m][2b]), b < half; r_base: slot_words(d) words
 // ptrs (device, nm pointers, optional): MLE m at ptrs[m] instead of in + m in_stride
 hipError_t mle_fix_first(const uint64_t *in, size_t in_stride, int nm, size_t half, int d, const uint64_t *r_base,
@@ -246,6 +251,13 @@ hipError_t round_folding(const uint64_t *mles, size_t stride, int nf, const uint
 hipError_t round_lin(const uint64_t *mles, size_t stride, int nm, const uint64_t *c, const CombS &cs, int degree,
                      size_t half, int d, uint64_t *partial, uint64_t *evals, hipStream_t st,
                      const uint64_t *const *ptrs = nullptr);
+// evals [degree][d]: q(0 .. degree-1) of the linearization round with eq(beta) split
+// off (E: eq over the unbound variables, half points); see k_round_lin_eq
+hipError_t round_lin_eq(const uint64_t *mles, size_t stride, const uint64_t *E, const uint64_t *c, const CombS &cs,
+                        int degree, size_t half, int d, uint64_t *partial, uint64_t *evals, hipStream_t st,
+                        const uint64_t *const *ptrs = nullptr);
+// E_next[b] = E[2b] + E[2b+1] for b < half (whole ring elements)
+hipError_t pair_sum(const uint64_t *E, size_t half, int d, uint64_t *out, hipStream_t st);
 size_t mle_eval_partial_elems(int d, int nm);
 // out[m] = sum_x eq[x] (.) mles[m][x], x < n
 hipError_t mle_dot(const uint64_t *mles, size_t stride, int nm, const uint64_t *eq, size_t n, int d,
@@ -293,7 +305,11 @@ hipError_t mz_challenged(const CcsDev &M, const uint64_t *z, const uint64_t *zet
 // the evaluation route in two halves: w [t][n] = M_j^T eq (one point, any number of z
 // sets), then out [nz][t] = w_j . z_i
 hipError_t mz_weights(const CcsDev &M, const uint64_t *eq, uint64_t *w, hipStream_t st);
-hipError_t mz_dots(const CcsDev &M, const uint64_t *w, const uint64_t *z, int nz, uint64_t *out, hipStream_t st);
+// partial (optional): mz_dots_partial_elems(M, nz) u64 of scratch for column splits
+// when t nz blocks would not fill the chip
+hipError_t mz_dots(const CcsDev &M, const uint64_t *w, const uint64_t *z, int nz, uint64_t *out, hipStream_t st,
+                   uint64_t *partial = nullptr);
+size_t mz_dots_partial_elems(const CcsDev &M, int nz);
 hipError_t mz_evaluate(const CcsDev &M, const uint64_t *z, int nz, int nv, const uint64_t *point, uint64_t *out,
                        uint64_t *scratch, hipStream_t st);
 

@@ -1703,6 +1703,150 @@ int lf_sumcheck_prove_ptrs(lf_ctx *c, lf_transcript *t, const lf_comb *cb, const
                       degree, proof, randomness);
 }
 
+// The linearization sumcheck over [mles..., eq(beta)] with eq(beta) split off
+// (lfk::round_lin_eq): round i sums q_i(e) = sum_b E_i[b] inner(e, b) for e < degree
+// on the device, E_i = eq(beta_(i+1) ..) over the unbound variables (E_0 an eq table,
+// then pair sums); the host extrapolates q_i(degree) (q_i has degree < degree:
+// q(n) = sum_(k<n) (-1)^(n-1-k) C(n, k) q(k)) and forms the message
+//   p_i(e) = P_i eq(beta_i, e) q_i(e),  P_i = prod_(k<i) eq(beta_k, r_k),
+// the same field elements as the unsplit round sums, so the transcript is the same.
+static int sumcheck_run_lin(lf_ctx *c, lf_transcript *t, const lf_comb *cb, const lfk::CombS &cs,
+                            const uint64_t *const *ptrs, uint64_t *alt, int nm, int nv, int d, int degree,
+                            const uint64_t *beta, uint64_t *proof, uint64_t *randomness) {
+  const int tb = lfk::slot_words(d), nev = degree + 1, nq = degree, ns = d / tb;
+  const size_t n = (size_t)1 << nv;
+  size_t part = 0;
+  for (size_t h = n / 2; h >= 1; h /= 2) part = std::max(part, lfk::round_partial_elems(d, h, nq, cb->q));
+  const size_t fixed = (size_t)nm * (n / 2) * d;
+  // scratch: fixed MLEs | partial sums | q | E tables (n/2 + n/4 + .. + 1 < n elements) | beta
+  LF_TRY(grow(c, c->sc, c->sc_elems, fixed + part + (size_t)nq * d + n * d + (size_t)nv * d));
+  uint64_t *buf = c->sc, *partial = buf + fixed, *qd = partial + part, *Et = qd + (size_t)nq * d,
+           *bd = Et + n * d;
+  LF_HIP(c, hipMemcpyAsync(bd, beta, (size_t)nv * d * 8, hipMemcpyHostToDevice, c->cur));
+  if (nv > 1) {
+    LF_HIP(c, lfk::eq_table(bd + d, nv - 1, d, Et, c->cur));
+  } else {
+    std::vector<uint64_t> one(d, 0);
+    for (int k = 0; k < d; k += tb) one[k] = 1;
+    LF_HIP(c, hipMemcpyAsync(Et, one.data(), (size_t)d * 8, hipMemcpyHostToDevice, c->cur));
+    LF_HIP(c, hipStreamSynchronize(c->cur));
+  }
+  // (-1)^(nq-1-k) C(nq, k): q(nq) from q(0 .. nq-1)
+  std::vector<uint64_t> wext(nq);
+  for (int k = 0; k < nq; k++) {
+    uint64_t b = 1;
+    for (int j = 0; j < k; j++) b = b * (uint64_t)(nq - j) / (uint64_t)(j + 1);
+    wext[k] = (nq - 1 - k) % 2 ? gl::neg(b % gl::P) : b % gl::P;
+  }
+  auto bmul = [tb](const uint64_t *a, const uint64_t *b, uint64_t *o) {
+    if (tb == 3) {
+      uint64_t r[3];
+      gl::fq3_mul(a, b, r);
+      o[0] = r[0], o[1] = r[1], o[2] = r[2];
+    } else {
+      o[0] = gl::mul(a[0], b[0]);
+    }
+  };
+  // eq(beta, x) = (1 - beta) + x (2 beta - 1) for a base-ring x
+  auto eqv = [tb](const uint64_t *be, const uint64_t *x, uint64_t *o) {
+    uint64_t a[3] = {0, 0, 0}, s[3] = {0, 0, 0};
+    for (int w = 0; w < tb; w++) {
+      a[w] = gl::neg(be[w]);
+      s[w] = gl::add(be[w], be[w]);
+    }
+    a[0] = gl::add(a[0], 1);
+    s[0] = gl::sub(s[0], 1);
+    uint64_t m[3];
+    if (tb == 3) {
+      gl::fq3_mul(s, x, m);
+    } else {
+      m[0] = gl::mul(s[0], x[0]);
+    }
+    for (int w = 0; w < tb; w++) o[w] = gl::add(a[w], m[w]);
+  };
+  std::vector<uint64_t> scal(d, 0);
+  for (int i = 0; i < d; i += tb) scal[i] = (uint64_t)nv;
+  lf_transcript_absorb_ring(t, scal.data(), 1, d, LF_REPR_CANONICAL);
+  for (int i = 0; i < d; i += tb) scal[i] = (uint64_t)degree;
+  lf_transcript_absorb_ring(t, scal.data(), 1, d, LF_REPR_CANONICAL);
+  std::vector<uint64_t> qh((size_t)nq * d);
+  uint64_t pfx[3] = {1, 0, 0};
+  const uint64_t *cur = nullptr;
+  const uint64_t *const *cptrs = ptrs;
+  size_t stride = 0;
+  uint64_t *E = Et;
+  for (int i = 0; i < nv; i++) {
+    const size_t half = n >> (i + 1);
+    uint64_t *msg = proof + (size_t)i * nev * d;
+    LF_HIP(c, lfk::round_lin_eq(cur, stride, E, cb->c, cs, degree, half, d, partial, qd, c->cur, cptrs));
+    LF_HIP(c, hipMemcpyAsync(qh.data(), qd, (size_t)nq * d * 8, hipMemcpyDeviceToHost, c->cur));
+    LF_HIP(c, hipStreamSynchronize(c->cur));
+    const uint64_t *be = beta + (size_t)i * d;  // slot 0 holds the base-ring value
+    for (int e = 0; e < nev; e++) {
+      uint64_t x[3] = {(uint64_t)e, 0, 0}, ev[3], f[3];
+      eqv(be, x, ev);
+      bmul(pfx, ev, f);
+      for (int s = 0; s < ns; s++) {
+        uint64_t qv[3] = {0, 0, 0};
+        if (e < nq) {
+          for (int w = 0; w < tb; w++) qv[w] = qh[(size_t)e * d + s * tb + w];
+        } else {
+          for (int k = 0; k < nq; k++)
+            for (int w = 0; w < tb; w++) qv[w] = gl::add(qv[w], gl::mul(wext[k], qh[(size_t)k * d + s * tb + w]));
+        }
+        bmul(f, qv, msg + (size_t)e * d + s * tb);
+      }
+    }
+    lf_transcript_absorb_ring(t, msg, (size_t)nev, d, LF_REPR_CANONICAL);
+    uint64_t *ch = randomness + (size_t)i * tb;
+    if (tb == 3) {
+      lf_transcript_get_challenge(t, ch);
+    } else {
+      ch[0] = lf_transcript_sample(t);
+      lf_transcript_observe(t, ch[0]);
+    }
+    for (int k = 0; k < d; k++) scal[k] = ch[k % tb];
+    lf_transcript_absorb_ring(t, scal.data(), 1, d, LF_REPR_CANONICAL);
+    {
+      uint64_t ev[3], np[3];
+      eqv(be, ch, ev);
+      bmul(pfx, ev, np);
+      for (int w = 0; w < tb; w++) pfx[w] = np[w];
+    }
+    if (i + 1 < nv) {
+      uint64_t *dst = (i % 2 == 0) ? buf : alt;
+      LF_HIP(c, lfk::mle_fix_first(cur, stride, nm, half, d, ch, dst, half * d, c->cur, cptrs));
+      LF_HIP(c, lfk::pair_sum(E, half / 2, d, E + half * d, c->cur));
+      E += half * d;
+      cur = dst;
+      cptrs = nullptr;
+      stride = half * d;
+    }
+  }
+  return LF_OK;
+}
+
+int lf_sumcheck_prove_lin(lf_ctx *c, lf_transcript *t, const lf_comb *cb, const uint64_t *const *mles, int nm, int nv,
+                          int d, int degree, const uint64_t *beta, uint64_t *work, uint64_t *proof,
+                          uint64_t *randomness) {
+  if (!c || !t || !mles || !beta || !work || !proof || !randomness || nv < 1 || nm < 1) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  for (int m = 0; m < nm; m++)
+    if (!mles[m]) return fail(c, LF_ERR_INVALID_ARG, "null MLE pointer");
+  if (cb && cb->kind != LF_COMB_LINEARIZATION)
+    return fail(c, LF_ERR_INVALID_ARG, "lf_sumcheck_prove_lin: a linearization combination");
+  lfk::CombS cs;
+  LF_TRY(comb_check(c, cb, nm + 1, d, degree, &cs));  // the list with eq(beta) last
+  for (int i = 0; i < cs.q; i++)
+    if (cs.off[i + 1] - cs.off[i] > degree - 1)
+      return fail(c, LF_ERR_INVALID_ARG, "linearization sumcheck: a multiset of degree or more factors");
+  LF_TRY(grow(c, c->ptrs, c->ptrs_elems, (size_t)nm));
+  LF_HIP(c, hipMemcpyAsync(c->ptrs, mles, (size_t)nm * sizeof(uint64_t), hipMemcpyHostToDevice, c->cur));
+  return sumcheck_run_lin(c, t, cb, cs, reinterpret_cast<const uint64_t *const *>(c->ptrs), work, nm, nv, d, degree,
+                          beta, proof, randomness);
+}
+
 // ---------------------------------------------------------------- sparse Mz products
 void lf_ccs_destroy(lf_ccs *M) { delete M; }
 
@@ -1891,7 +2035,8 @@ int lf_dev_mz_weights(lf_ctx *c, const lf_ccs *M, int nv, const uint64_t *eq, ui
 int lf_dev_mz_dots(lf_ctx *c, const lf_ccs *M, const uint64_t *w, const uint64_t *z, int nz, uint64_t *out) {
   if (!c || !M || !w || !z || !out || nz < 1) return LF_ERR_INVALID_ARG;
   DevGuard g(c);
-  LF_HIP(c, lfk::mz_dots(M->dev, w, z, nz, out, c->cur));
+  LF_TRY(grow(c, c->tmp, c->tmp_elems, lfk::mz_dots_partial_elems(M->dev, nz)));
+  LF_HIP(c, lfk::mz_dots(M->dev, w, z, nz, out, c->cur, c->tmp));
   return LF_OK;
 }
 

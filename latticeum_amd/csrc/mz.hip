@@ -77,18 +77,21 @@ __global__ void k_zcomb(const uint64_t *pw, const uint64_t *z, int nz, int t, si
   s_store(y + jc * d + s * TB, sacc_final(acc));
 }
 
-// out[i][j] = sum_c w[j][c] (.) z_i[c]: one block per (i, j, slot chunk)
+// out[i][j] = sum_c w[j][c] (.) z_i[c]: one block per (i, j, slot chunk, column split);
+// with nsplit > 1 the block sums columns [split n / nsplit, (split + 1) n / nsplit) into
+// out[split][i][j] (the partial sums k_dots_sum adds up)
 template <int TB>
-__global__ void __launch_bounds__(MT) k_dots(const uint64_t *w, const uint64_t *z, int t, size_t n, int d, int spb,
-                                            uint64_t *out) {
+__global__ void __launch_bounds__(MT) k_dots(const uint64_t *w, const uint64_t *z, int t, int nz, size_t n, int d,
+                                            int spb, int nsplit, uint64_t *out) {
   __shared__ uint64_t red[MT * TB];
   const int slot_l = threadIdx.x % spb, lane_c = threadIdx.x / spb, cpb = MT / spb;
-  const int slot = blockIdx.z * spb + slot_l;
+  const int split = blockIdx.z % nsplit, slot = (blockIdx.z / nsplit) * spb + slot_l;
   const int i = blockIdx.y, j = blockIdx.x;
   const uint64_t *wj = w + (size_t)j * n * d + slot * TB, *zi = z + (size_t)i * n * d + slot * TB;
+  const size_t c0 = n * split / nsplit, c1 = n * (split + 1) / nsplit;
   SAcc<TB> la;
   sacc_zero(la);
-  for (size_t c = lane_c; c < n; c += cpb) sacc_mad(la, s_load<TB>(wj + c * d), s_load<TB>(zi + c * d));
+  for (size_t c = c0 + lane_c; c < c1; c += cpb) sacc_mad(la, s_load<TB>(wj + c * d), s_load<TB>(zi + c * d));
   s_store(red + threadIdx.x * TB, sacc_final(la));
   __syncthreads();
   for (int h = cpb / 2; h > 0; h >>= 1) {
@@ -96,7 +99,25 @@ __global__ void __launch_bounds__(MT) k_dots(const uint64_t *w, const uint64_t *
       s_store(red + threadIdx.x * TB, s_add(s_load<TB>(red + threadIdx.x * TB), s_load<TB>(red + (threadIdx.x + h * spb) * TB)));
     __syncthreads();
   }
-  if (lane_c == 0) s_store(out + ((size_t)i * t + j) * d + slot * TB, s_load<TB>(red + threadIdx.x * TB));
+  if (lane_c == 0)
+    s_store(out + (((size_t)split * nz + i) * t + j) * d + slot * TB, s_load<TB>(red + threadIdx.x * TB));
+}
+// out[x] = sum_s part[s][x], one thread per word
+__global__ void k_dots_sum(const uint64_t *part, int nsplit, size_t len, uint64_t *out) {
+  const size_t x = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (x >= len) return;
+  uint64_t a = part[x];
+  for (int s = 1; s < nsplit; s++) a = gl::add(a, part[(size_t)s * len + x]);
+  out[x] = a;
+}
+// column splits: enough blocks for the chip (about 2048) when t nz is small
+int dots_nsplit(const CcsDev &M, int nz) {
+  const int tb = slot_words(M.d), ns = M.d / tb, spb = ns < MT ? ns : MT;
+  const size_t blocks = (size_t)M.t * nz * (ns / spb);
+  int k = (int)((2048 + blocks - 1) / blocks);
+  if (k > 16) k = 16;
+  if ((size_t)k * 64 > M.n) k = (int)(M.n / 64) > 1 ? (int)(M.n / 64) : 1;
+  return k < 1 ? 1 : k;
 }
 
 unsigned nblk(size_t n, int t) { return (unsigned)((n + t - 1) / t); }
@@ -120,7 +141,7 @@ hipError_t csr(const uint64_t *rp, size_t rp_stride, int na, const uint32_t *col
 
 size_t mz_scratch_elems(const CcsDev &M, int nz, int nv) {
   const size_t e = ((size_t)1 << nv) * M.d, tn = (size_t)M.t * M.n * M.d;
-  const size_t chall = (size_t)M.t * nz * M.d + tn, eval = e + tn;
+  const size_t chall = (size_t)M.t * nz * M.d + tn, eval = e + tn + mz_dots_partial_elems(M, nz);
   return chall > eval ? chall : eval;
 }
 
@@ -169,17 +190,29 @@ hipError_t mz_evaluate(const CcsDev &M, const uint64_t *z, int nz, int nv, const
   if (e != hipSuccess) return e;
   e = mz_weights(M, eq, w, st);
   if (e != hipSuccess) return e;
-  return mz_dots(M, w, z, nz, out, st);
+  return mz_dots(M, w, z, nz, out, st, w + (size_t)M.t * M.n * M.d);
 }
 
-hipError_t mz_dots(const CcsDev &M, const uint64_t *w, const uint64_t *z, int nz, uint64_t *out, hipStream_t st) {
+size_t mz_dots_partial_elems(const CcsDev &M, int nz) {
+  const int k = dots_nsplit(M, nz);
+  return k > 1 ? (size_t)k * nz * M.t * M.d : 0;
+}
+
+hipError_t mz_dots(const CcsDev &M, const uint64_t *w, const uint64_t *z, int nz, uint64_t *out, hipStream_t st,
+                   uint64_t *partial) {
   if (!nz) return hipSuccess;
   const int tb = slot_words(M.d), ns = M.d / tb, spb = ns < MT ? ns : MT;
-  const dim3 grid((unsigned)M.t, (unsigned)nz, (unsigned)(ns / spb));
+  const int nsplit = partial ? dots_nsplit(M, nz) : 1;
+  uint64_t *dst = nsplit > 1 ? partial : out;
+  const dim3 grid((unsigned)M.t, (unsigned)nz, (unsigned)(ns / spb * nsplit));
   if (tb == 3)
-    hipLaunchKernelGGL(k_dots<3>, grid, dim3(MT), 0, st, w, z, M.t, M.n, M.d, spb, out);
+    hipLaunchKernelGGL(k_dots<3>, grid, dim3(MT), 0, st, w, z, M.t, nz, M.n, M.d, spb, nsplit, dst);
   else
-    hipLaunchKernelGGL(k_dots<1>, grid, dim3(MT), 0, st, w, z, M.t, M.n, M.d, spb, out);
+    hipLaunchKernelGGL(k_dots<1>, grid, dim3(MT), 0, st, w, z, M.t, nz, M.n, M.d, spb, nsplit, dst);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || nsplit == 1) return e;
+  const size_t len = (size_t)nz * M.t * M.d;
+  hipLaunchKernelGGL(k_dots_sum, dim3(nblk(len, 256)), dim3(256), 0, st, partial, nsplit, len, out);
   return hipGetLastError();
 }
 

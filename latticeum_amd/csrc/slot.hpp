@@ -69,23 +69,66 @@ __device__ __forceinline__ Sv<1> s_mul(const Sv<1> &a, const Sv<1> &b) {
 // shifts) so each output word is one carry-chain accumulator and one reduction
 __device__ __forceinline__ Sv<3> s_mul(const Sv<3> &a, const Sv<3> &b) {
   const uint64_t b1n = gl::shl96(b.c[1], 40), b2n = gl::shl96(b.c[2], 40);
-  gl::CAcc x0, x1, x2;
-  gl::cacc_zero(x0);
-  gl::cacc_zero(x1);
-  gl::cacc_zero(x2);
-  gl::cacc_mad(x0, a.c[0], b.c[0]);
-  gl::cacc_mad(x0, a.c[1], b2n);
-  gl::cacc_mad(x0, a.c[2], b1n);
-  gl::cacc_mad(x1, a.c[0], b.c[1]);
-  gl::cacc_mad(x1, a.c[1], b.c[0]);
-  gl::cacc_mad(x1, a.c[2], b2n);
-  gl::cacc_mad(x2, a.c[0], b.c[2]);
-  gl::cacc_mad(x2, a.c[1], b.c[1]);
-  gl::cacc_mad(x2, a.c[2], b.c[0]);
+  // word by word (each accumulator reduced before the next starts: 9 live
+  // accumulator registers instead of 27)
   Sv<3> r;
-  r.c[0] = gl::cacc_reduce(x0);
-  r.c[1] = gl::cacc_reduce(x1);
-  r.c[2] = gl::cacc_reduce(x2);
+  gl::CAcc x;
+  gl::cacc_zero(x);
+  gl::cacc_mad(x, a.c[0], b.c[0]);
+  gl::cacc_mad(x, a.c[1], b2n);
+  gl::cacc_mad(x, a.c[2], b1n);
+  r.c[0] = gl::cacc_reduce(x);
+  gl::cacc_zero(x);
+  gl::cacc_mad(x, a.c[0], b.c[1]);
+  gl::cacc_mad(x, a.c[1], b.c[0]);
+  gl::cacc_mad(x, a.c[2], b2n);
+  r.c[1] = gl::cacc_reduce(x);
+  gl::cacc_zero(x);
+  gl::cacc_mad(x, a.c[0], b.c[2]);
+  gl::cacc_mad(x, a.c[1], b.c[1]);
+  gl::cacc_mad(x, a.c[2], b.c[0]);
+  r.c[2] = gl::cacc_reduce(x);
+  return r;
+}
+// a b + u v, word by word with one reduction per word
+__device__ __forceinline__ Sv<1> s_mad2(const Sv<1> &a, const Sv<1> &b, const Sv<1> &u, const Sv<1> &v) {
+  gl::CAcc x;
+  gl::cacc_zero(x);
+  gl::cacc_mad(x, a.c[0], b.c[0]);
+  gl::cacc_mad(x, u.c[0], v.c[0]);
+  Sv<1> r;
+  r.c[0] = gl::cacc_reduce(x);
+  return r;
+}
+__device__ __forceinline__ Sv<3> s_mad2(const Sv<3> &a, const Sv<3> &b, const Sv<3> &u, const Sv<3> &v) {
+  const uint64_t b1n = gl::shl96(b.c[1], 40), b2n = gl::shl96(b.c[2], 40);
+  const uint64_t v1n = gl::shl96(v.c[1], 40), v2n = gl::shl96(v.c[2], 40);
+  Sv<3> r;
+  gl::CAcc x;
+  gl::cacc_zero(x);
+  gl::cacc_mad(x, a.c[0], b.c[0]);
+  gl::cacc_mad(x, a.c[1], b2n);
+  gl::cacc_mad(x, a.c[2], b1n);
+  gl::cacc_mad(x, u.c[0], v.c[0]);
+  gl::cacc_mad(x, u.c[1], v2n);
+  gl::cacc_mad(x, u.c[2], v1n);
+  r.c[0] = gl::cacc_reduce(x);
+  gl::cacc_zero(x);
+  gl::cacc_mad(x, a.c[0], b.c[1]);
+  gl::cacc_mad(x, a.c[1], b.c[0]);
+  gl::cacc_mad(x, a.c[2], b2n);
+  gl::cacc_mad(x, u.c[0], v.c[1]);
+  gl::cacc_mad(x, u.c[1], v.c[0]);
+  gl::cacc_mad(x, u.c[2], v2n);
+  r.c[1] = gl::cacc_reduce(x);
+  gl::cacc_zero(x);
+  gl::cacc_mad(x, a.c[0], b.c[2]);
+  gl::cacc_mad(x, a.c[1], b.c[1]);
+  gl::cacc_mad(x, a.c[2], b.c[0]);
+  gl::cacc_mad(x, u.c[0], v.c[2]);
+  gl::cacc_mad(x, u.c[1], v.c[1]);
+  gl::cacc_mad(x, u.c[2], v.c[0]);
+  r.c[2] = gl::cacc_reduce(x);
   return r;
 }
 template <int TB>

@@ -292,6 +292,197 @@ __global__ void __launch_bounds__(RT) k_round_lin(const uint64_t *mles, size_t s
                                 partial + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * (degree + 1) * d);
 }
 
+// ---------------------------------------------------------------- linearization with eq split off
+// The same round polynomial with eq(beta, x) factored as eq(beta_0, X) E[b]
+// (E = eq over the variables not yet bound, a constant along each line):
+//   p(X) = P eq(beta_0, X) q(X),  q(X) = sum_b E[b] sum_i c_i prod_(j in S_i) m_j(X, b)
+// q has one degree less than p, so NQ = degree values q(0 .. NQ-1) suffice; the
+// host extrapolates q(NQ) and multiplies in the eq factors (sumcheck_run_lin,
+// lf_api.hip). p(e) is the same field element either way, so the messages are
+// the reference's (prover.rs:62-168 over linearization/utils.rs:63-104).
+//
+// A multiset's product c_i prod_f (a_f + d_f e) is formed in two groups in
+// coefficient form (c_i and the first KA factors; the other KB), each walked
+// along e = 0 .. NQ-1 by forward differences, and the groups multiplied
+// pointwise: for |S_i| = 7 that is 20 + 10 + 8 products instead of 6 + 5 x 9.
+
+// c <- c (a + d e) for a degree-M polynomial in coefficient form (in place, from the top;
+// each new coefficient one lazy multiply-accumulate pair)
+template <int TB, int M>
+__device__ __forceinline__ void poly_mul_lin(Sv<TB> (&c)[5], const Sv<TB> &a, const Sv<TB> &dd) {
+  c[M + 1] = s_mul(c[M], dd);
+#pragma unroll
+  for (int j = M; j >= 1; j--) c[j] = s_mad2(c[j], a, c[j - 1], dd);
+  c[0] = s_mul(c[0], a);
+}
+
+// coefficients -> the forward-difference table at e = 0: D_j = sum_k c_k j! S(k, j)
+//   D1 = c1 + c2 + c3 + c4, D2 = 2 c2 + 6 c3 + 14 c4, D3 = 6 c3 + 36 c4, D4 = 24 c4
+template <int TB, int M>
+__device__ __forceinline__ void poly_to_diff(Sv<TB> (&c)[5]) {
+  if constexpr (M == 1) return;
+  if constexpr (M == 2) {
+    c[1] = s_add(c[1], c[2]);
+    c[2] = s_add(c[2], c[2]);
+  }
+  if constexpr (M == 3) {
+    const Sv<TB> c3x6 = s_smul(c[3], 6);
+    c[1] = s_add(s_add(c[1], c[2]), c[3]);
+    c[2] = s_add(s_add(c[2], c[2]), c3x6);
+    c[3] = c3x6;
+  }
+  if constexpr (M == 4) {
+    const Sv<TB> c3x6 = s_smul(c[3], 6);
+    c[1] = s_add(s_add(c[1], c[2]), s_add(c[3], c[4]));
+    c[2] = s_add(s_add(s_add(c[2], c[2]), c3x6), s_smul(c[4], 14));
+    c[3] = s_add(c3x6, s_smul(c[4], 36));
+    c[4] = s_smul(c[4], 24);
+  }
+}
+
+template <int TB, int M>
+__device__ __forceinline__ void diff_step(Sv<TB> (&c)[5]) {
+#pragma unroll
+  for (int j = 0; j < M; j++) c[j] = s_add(c[j], c[j + 1]);
+}
+
+// sum[e] += c_i prod_(f < KA + KB) (a_f + d_f e), e < NQ; fac(f, a, d) loads factor f
+template <int TB, int NQ, int KA, int KB, class Fac>
+__device__ __forceinline__ void multiset_add(const Sv<TB> &ci, Fac fac, Sv<TB> (&sum)[NQ]) {
+  Sv<TB> A[5], B[5], a, dd;
+  fac(0, a, dd);
+  A[0] = s_mul(ci, a);
+  A[1] = s_mul(ci, dd);
+#pragma unroll
+  for (int f = 1; f < KA; f++) {
+    __builtin_amdgcn_sched_barrier(0);  // one factor's loads and products at a time (registers)
+    fac(f, a, dd);
+    if (f == 1) poly_mul_lin<TB, 1>(A, a, dd);
+    if (f == 2) poly_mul_lin<TB, 2>(A, a, dd);
+    if (f == 3) poly_mul_lin<TB, 3>(A, a, dd);
+  }
+  poly_to_diff<TB, KA>(A);
+  if constexpr (KB == 0) {
+#pragma unroll
+    for (int e = 0; e < NQ; e++) {
+      sum[e] = s_add(sum[e], A[0]);
+      if (e + 1 < NQ) diff_step<TB, KA>(A);
+    }
+  } else {
+    __builtin_amdgcn_sched_barrier(0);
+    fac(KA, B[0], B[1]);
+#pragma unroll
+    for (int f = 1; f < KB; f++) {
+      __builtin_amdgcn_sched_barrier(0);
+      fac(KA + f, a, dd);
+      if (f == 1) poly_mul_lin<TB, 1>(B, a, dd);
+      if (f == 2) poly_mul_lin<TB, 2>(B, a, dd);
+      if (f == 3) poly_mul_lin<TB, 3>(B, a, dd);
+    }
+    poly_to_diff<TB, KB>(B);
+#pragma unroll
+    for (int e = 0; e < NQ; e++) {
+      __builtin_amdgcn_sched_barrier(0);
+      sum[e] = s_add(sum[e], s_mul(A[0], B[0]));
+      if (e + 1 < NQ) {
+        diff_step<TB, KA>(A);
+        diff_step<TB, KB>(B);
+      }
+    }
+  }
+}
+
+template <int TB, int NQ>
+__global__ void __launch_bounds__(RT) k_round_lin_eq(const uint64_t *mles, size_t stride, const uint64_t *const *ptrs,
+                                                     const uint64_t *E, const uint64_t *c, CombS cs, size_t half, int d,
+                                                     int spb, uint64_t *partial) {
+  const int slot_l = threadIdx.x % spb, lane_p = threadIdx.x / spb, ppb = RT / spb;
+  const int slot = blockIdx.y * spb + slot_l;
+  const int chunk = blockIdx.z, nchunk = gridDim.z;
+  const int i0 = (int)((long)cs.q * chunk / nchunk), i1 = (int)((long)cs.q * (chunk + 1) / nchunk);
+  // the per-thread sums over points live in LDS (word w of value e at [e TB + w][thread]),
+  // which leaves the registers to the multiset products
+  __shared__ uint64_t lacc[NQ * TB * RT];
+#pragma unroll
+  for (int k = 0; k < NQ * TB; k++) lacc[k * RT + threadIdx.x] = 0;
+  for (size_t b = (size_t)blockIdx.x * ppb + lane_p; b < half; b += (size_t)gridDim.x * ppb) {
+    const size_t pofs = 2 * b * d + slot * TB;
+    Sv<TB> sum[NQ];
+#pragma unroll
+    for (int e = 0; e < NQ; e++) sum[e] = s_zero<TB>();
+    for (int i = i0; i < i1; i++) {
+      // no per-slot zero test: a branch on c_i would make the multiset loop divergent
+      // and move the (uniform) multiset indices and MLE pointers into vector registers
+      const Sv<TB> ci = s_load<TB>(c + (size_t)i * d + slot * TB);
+      const int s0 = cs.off[i], k = cs.off[i + 1] - s0;
+      auto fac = [&](int f, Sv<TB> &a, Sv<TB> &dd) {
+        const int m = cs.idx[s0 + f];
+        const uint64_t *p = (ptrs ? ptrs[m] : mles + (size_t)m * stride) + pofs;
+        a = s_load<TB>(p);
+        dd = s_sub(s_load<TB>(p + d), a);
+      };
+      if (k == 0) {
+#pragma unroll
+        for (int e = 0; e < NQ; e++) sum[e] = s_add(sum[e], ci);
+      } else if (k == 1) {
+        multiset_add<TB, NQ, 1, 0>(ci, fac, sum);
+      } else if (k == 2) {
+        multiset_add<TB, NQ, 2, 0>(ci, fac, sum);
+      } else {
+        // c_i and the first two factors in coefficient form, walked along e by
+        // differences; every further factor multiplied in at the NQ points
+        Sv<TB> term[NQ], A[5], a, dd;
+        fac(0, a, dd);
+        A[0] = s_mul(ci, a);
+        A[1] = s_mul(ci, dd);
+        fac(1, a, dd);
+        poly_mul_lin<TB, 1>(A, a, dd);
+        poly_to_diff<TB, 2>(A);
+#pragma unroll
+        for (int e = 0; e < NQ; e++) {
+          term[e] = A[0];
+          if (e + 1 < NQ) diff_step<TB, 2>(A);
+        }
+        for (int f = 2; f < k; f++) {
+          fac(f, a, dd);
+#pragma unroll
+          for (int e = 0; e < NQ; e++) {
+            term[e] = s_mul(term[e], a);
+            if (e + 1 < NQ) a = s_add(a, dd);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < NQ; e++) sum[e] = s_add(sum[e], term[e]);
+      }
+    }
+    const Sv<TB> w = s_load<TB>(E + b * d + slot * TB);
+#pragma unroll
+    for (int e = 0; e < NQ; e++) {
+      const Sv<TB> v = s_mul(sum[e], w);
+#pragma unroll
+      for (int k = 0; k < TB; k++) {
+        uint64_t &a = lacc[(e * TB + k) * RT + threadIdx.x];
+        a = gl::add(a, v.c[k]);
+      }
+    }
+  }
+  Sv<TB> acc[NQ];
+#pragma unroll
+  for (int e = 0; e < NQ; e++)
+#pragma unroll
+    for (int k = 0; k < TB; k++) acc[e].c[k] = lacc[(e * TB + k) * RT + threadIdx.x];
+  block_partial<TB, NQ>(acc, spb, ppb, slot, lane_p, d,
+                        partial + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * NQ * d);
+}
+
+// E_next[b] = E[2b] + E[2b + 1]: eq over one variable fewer (eq(beta, 0) + eq(beta, 1) = 1)
+__global__ void k_pair_sum(const uint64_t *in, size_t half, int d, uint64_t *out) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= half * d) return;
+  const size_t b = i / d, w = i - b * d;
+  out[i] = gl::add(in[2 * b * d + w], in[(2 * b + 1) * d + w]);
+}
+
 // out[i] = sum over blocks of partial[blk][i]: one block per output word,
 // its threads striding over the blocks, then an LDS tree
 __global__ void __launch_bounds__(256) k_sum_partials(const uint64_t *partial, int nblk, size_t len, uint64_t *out) {
@@ -501,6 +692,50 @@ hipError_t round_lin(const uint64_t *mles, size_t stride, int nm, const uint64_t
   return hipGetLastError();
 }
 
+hipError_t round_lin_eq(const uint64_t *mles, size_t stride, const uint64_t *E, const uint64_t *c, const CombS &cs,
+                        int degree, size_t half, int d, uint64_t *partial, uint64_t *evals, hipStream_t st,
+                        const uint64_t *const *ptrs) {
+  if (degree + 1 > MAX_EVALS || degree < 1 || !half) return hipErrorInvalidValue;
+  int spb;
+  dim3 grid;
+  round_geom(d, half, cs.q, spb, grid);
+#define LF_RLE(TB, NQ)                                                                                      \
+  hipLaunchKernelGGL((k_round_lin_eq<TB, NQ>), grid, dim3(RT), 0, st, mles, stride, ptrs, E, c, cs, half, d, spb, \
+                     partial)
+#define LF_RLE_DEG(TB)                \
+  switch (degree) {                   \
+    case 1: LF_RLE(TB, 1); break;     \
+    case 2: LF_RLE(TB, 2); break;     \
+    case 3: LF_RLE(TB, 3); break;     \
+    case 4: LF_RLE(TB, 4); break;     \
+    case 5: LF_RLE(TB, 5); break;     \
+    case 6: LF_RLE(TB, 6); break;     \
+    case 7: LF_RLE(TB, 7); break;     \
+    case 8: LF_RLE(TB, 8); break;     \
+    default: LF_RLE(TB, 9); break;    \
+  }
+  if (slot_words(d) == 3) {
+    LF_RLE_DEG(3)
+  } else {
+    LF_RLE_DEG(1)
+  }
+#undef LF_RLE_DEG
+#undef LF_RLE
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const size_t len = (size_t)degree * d;
+  hipLaunchKernelGGL(k_sum_partials, dim3((unsigned)len), dim3(256), 0, st, partial, (int)(grid.x * grid.z), len,
+                     evals);
+  return hipGetLastError();
+}
+
+hipError_t pair_sum(const uint64_t *E, size_t half, int d, uint64_t *out, hipStream_t st) {
+  const size_t n = half * d;
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_pair_sum, dim3(blocks_of(n, 256)), dim3(256), 0, st, E, half, d, out);
+  return hipGetLastError();
+}
+
 size_t mle_eval_partial_elems(int d, int nm) { return (size_t)64 * nm * d; }
 
 hipError_t mle_dot(const uint64_t *mles, size_t stride, int nm, const uint64_t *eq, size_t n, int d,
@@ -559,28 +794,51 @@ hipError_t mle_lincomb(const uint64_t *mles, size_t stride, int nm, const uint64
 // base-ring value (Phi_72: (c, 0, 0) in an Fq3 slot, D = 8 slots; X^d + 1:
 // tau = 1, the coefficients themselves); points N .. 2^nv - 1 are zero (the
 // reference's truncated MLE read as zero padding). One thread per output word.
-__global__ void k_get_fhat(const uint64_t *f_coeff, size_t N, int d, size_t npts, uint64_t *out) {
-  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+__global__ void k_get_fhat(const uint64_t *f_coeff, size_t N, size_t wstride, int d, size_t npts, size_t per,
+                           size_t total, uint64_t *out) {
+  const size_t t0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t0 >= total) return;
   const int tau = d == 24 ? 3 : 1;
-  if (t >= (size_t)tau * npts * d) return;
+  const size_t wi = t0 / per, t = t0 - wi * per;  // witness wi, word t of its tau MLEs
+  const uint64_t *fc = f_coeff + wi * wstride;
   const size_t w = t % d, ji = t / d, i = ji % npts;
   const int j = (int)(ji / npts);
   uint64_t v = 0;
   if (i < N) {
     if (d == 24)
-      v = w % 3 == 0 ? f_coeff[i * 24 + 8 * j + w / 3] : 0;
+      v = w % 3 == 0 ? fc[i * 24 + 8 * j + w / 3] : 0;
     else
-      v = f_coeff[i * d + w];
+      v = fc[i * d + w];
   }
-  out[t] = v;
+  out[t0] = v;
 }
 
-hipError_t get_fhat(const uint64_t *f_coeff, size_t N, int d, int nv, uint64_t *out, hipStream_t st) {
+// z_k = x_s[k] || w_ccs_k for nz instances (compute_mz_mles, decomposition.rs:229-256):
+// out [nz][l1 + W][d] from x [nz][l1][d] and w [nz][W][d], one thread per word
+__global__ void k_assemble_z(const uint64_t *x, const uint64_t *w, size_t l1, size_t W, int d, size_t total,
+                             uint64_t *out) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const size_t n = (l1 + W) * d, k = t / n, o = t - k * n;
+  out[t] = o < l1 * d ? x[k * l1 * d + o] : w[k * W * d + o - l1 * d];
+}
+
+hipError_t get_fhat(const uint64_t *f_coeff, size_t N, int d, int nv, uint64_t *out, hipStream_t st, int nw,
+                    size_t wstride) {
   const size_t npts = (size_t)1 << nv;
-  if (N > npts) return hipErrorInvalidValue;
-  const size_t n = (size_t)(d == 24 ? 3 : 1) * npts * d;
-  if (!n) return hipSuccess;
-  hipLaunchKernelGGL(k_get_fhat, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, f_coeff, N, d, npts, out);
+  if (N > npts || nw < 1) return hipErrorInvalidValue;
+  const size_t per = (size_t)(d == 24 ? 3 : 1) * npts * d, total = per * nw;
+  if (!total) return hipSuccess;
+  hipLaunchKernelGGL(k_get_fhat, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, f_coeff, N, wstride, d, npts,
+                     per, total, out);
+  return hipGetLastError();
+}
+
+hipError_t assemble_z(const uint64_t *x, const uint64_t *w, int nz, size_t l1, size_t W, int d, uint64_t *out,
+                      hipStream_t st) {
+  const size_t total = (size_t)nz * (l1 + W) * d;
+  if (!total) return hipSuccess;
+  hipLaunchKernelGGL(k_assemble_z, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, x, w, l1, W, d, total, out);
   return hipGetLastError();
 }
 

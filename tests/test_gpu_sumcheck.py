@@ -165,3 +165,59 @@ def test_get_fhat_matches_oracle(ctx, d, N, nv):
     want = O.get_fhat_phi72(fc).reshape(tau, N, d) if d == 24 else fc.reshape(1, N, d)
     assert np.array_equal(got[:, :N], want)
     assert not got[:, N:].any()
+
+
+def lin_eq_case(d, nv, sizes, seed):
+    """multisets of the given sizes over nmz Mz MLEs (indices repeat across multisets), a
+    coefficient that is zero in some slots, and the MLE list [mz..., eq(beta)]"""
+    rng = np.random.default_rng(seed)
+    n = 1 << nv
+    nmz = max(3, max(sizes))
+    S = [[int(j) for j in rng.integers(0, nmz, k)] for k in sizes]
+    c = rand(len(sizes) * d, seed + 1)
+    c[:d // 2] = 0  # c_0 vanishes in the first slots
+    mz = [rand(n * d, seed + 2 + j) for j in range(nmz)]
+    beta = rand(nv * d, seed + 99)
+    tb = 3 if d == 24 else 1
+    beta = np.concatenate([O.broadcast(beta[i * d:i * d + tb], d) for i in range(nv)])  # base-ring challenges
+    return c, S, mz, beta
+
+
+@pytest.mark.parametrize("d,nv,sizes", [(24, 6, [7, 1, 2, 0, 3]), (24, 5, [8, 5, 6, 4, 1]), (64, 4, [7, 2, 5]),
+                                        (24, 1, [3, 2]), (1024, 3, [4, 7])])
+def test_linearization_prove_lin_matches_oracle(ctx, d, nv, sizes):
+    """lf_sumcheck_prove_lin (eq(beta) split off, pointer table, two-group products) gives
+    the oracle's proof over [mz..., eq(beta)], multisets of 0 .. 8 factors"""
+    c, S, mz, beta = lin_eq_case(d, nv, sizes, 1000 + d + nv)
+    degree = max(sizes) + 1
+    mles = np.concatenate(mz + [O.eq_table(beta, nv, d)])
+    want_p, want_r = O.sumcheck_prove(O.new_transcript(), O.SumcheckComb.linearization(c, S), mles, len(mz) + 1, nv,
+                                      d, degree)
+    work = dev(n=max(1, len(mz) * (1 << max(nv - 2, 0)) * d))
+    proof, rnd = ctx.sumcheck_prove_lin(LA.Poseidon2Transcript(), LA.Comb.linearization(dev(c), S),
+                                        [dev(m) for m in mz], nv, d, degree, beta, work)
+    assert np.array_equal(proof, want_p) and np.array_equal(rnd, want_r)
+
+
+def test_linearization_prove_lin_matches_unsplit_at_size(ctx):
+    """the zkvm's shape in miniature on the device: Phi_72, 14 variables, 7-factor S-box
+    multisets and 1- and 2-factor ones; the split prover against the unsplit one"""
+    d, nv = 24, 14
+    n = 1 << nv
+    sizes = [7] * 6 + [1, 2] * 6
+    rng = np.random.default_rng(77)
+    nmz = 40
+    S = [[int(j) for j in rng.integers(0, nmz, k)] for k in sizes]
+    c = rand(len(sizes) * d, 78)
+    mz = dev(n=nmz * n * d)
+    ctx.dev_fill_uniform(mz, 79)
+    beta = np.concatenate([O.broadcast(rand(3, 80 + i), d) for i in range(nv)])
+    full = dev(n=(nmz + 1) * n * d)
+    full[:nmz * n * d] = mz
+    ctx.dev_eq_table(d, dev(beta), nv, full[nmz * n * d:])
+    want_p, want_r = ctx.sumcheck_prove(LA.Poseidon2Transcript(), LA.Comb.linearization(dev(c), S), full, nmz + 1, nv,
+                                        d, 8)
+    work = dev(n=nmz * (n // 4) * d)
+    proof, rnd = ctx.sumcheck_prove_lin(LA.Poseidon2Transcript(), LA.Comb.linearization(dev(c), S),
+                                        [mz[j * n * d:(j + 1) * n * d] for j in range(nmz)], nv, d, 8, beta, work)
+    assert np.array_equal(proof, want_p) and np.array_equal(rnd, want_r)

@@ -1,17 +1,20 @@
 #!/bin/bash
-# quick check of HEAD: fold / witness GPU tests, then the headline and W = 464 bench phases
+# a short GPU pass while iterating: selected -m gpu test files ($TESTS), then a kernel
+# trace of fold() at the zkvm shape (tools/fold_prof.py)
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-TAG=${1:-q}
-timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_batch.py \
-  tests/test_gpu_parity.py -k "${KSEL:-fold or batch or coeff or rho}" > gpurun_out/pytest_$TAG.log 2>&1
-rc=$?; tail -3 gpurun_out/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
-run() {  # name, args
-  timeout -k 10 300 python -u bench.py --no-small-shape --no-cpu-baseline $2 > gpurun_out/bench_${TAG}_$1.log 2>&1 || return 1
-  python3 -c "
-import json; d=json.loads([l for l in open('gpurun_out/bench_${TAG}_$1.log') if l.startswith('{')][-1])
-print('$1', round(d['value'],2), round(d['ms_per_step'],3), {k: round(v['avg_launch_ms'],3) for k,v in d['phases'].items()})"
-}
-run head "--steps 8 --warmup 2" && run head2 "--steps 8 --warmup 2" && \
-run w464 "--w 464 --streams 4 --batch 2 --steps 256 --warmup 16"
+TAG=${1:-quick}
+TESTS=${TESTS:-tests/test_gpu_sumcheck.py tests/test_gpu_fold_prove.py}
+timeout -k 10 600 python -u -m pytest $TESTS -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/proffold_$TAG -o run --output-format csv -- \
+  python tools/fold_prof.py > gpurun_out/fold_prof_$TAG.log 2>&1
+rc=$?; echo "fold prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
+python3 -c "
+import json; d=json.loads([l for l in open('gpurun_out/fold_prof_$TAG.log') if l.startswith('{')][-1])
+print({k: (round(v,2) if isinstance(v,float) else v) for k,v in d.items() if k.startswith('ms') or k.startswith('vars')})
+print({k: round(v,2) for k,v in d['span_ms'].items()})"
+python tools/prof_summary.py stats gpurun_out/proffold_$TAG gpurun_out/stats_fold_$TAG.md > /dev/null
+head -14 gpurun_out/stats_fold_$TAG.md
+if [ -n "$P2" ]; then bash tools/exp/p2_box.sh; fi
