@@ -412,10 +412,12 @@ int lf_sumcheck_prove_ptrs(lf_ctx *ctx, lf_transcript *t, const lf_comb *comb, c
  * eq(beta) split off each round (eq(beta_i, X) and eq over the unbound variables), so
  * the device evaluates a polynomial of one degree less. mles: nm device pointers as in
  * lf_sumcheck_prove_ptrs (S_idx < nm); beta: host [nv][d] broadcast base-ring values;
- * every multiset has fewer than `degree` entries; work: nm x 2^(nv-2) elements */
+ * every multiset has fewer than `degree` entries; work: nm x 2^(nv-2) elements; evals
+ * (device, nm ring elements, may be NULL): the MLEs at the challenge point (their
+ * values after the last round's fix: MLE(M_j z)(r) for the linearization's u) */
 int lf_sumcheck_prove_lin(lf_ctx *ctx, lf_transcript *t, const lf_comb *comb, const uint64_t *const *mles, int nm,
                           int nv, int d, int degree, const uint64_t *beta, uint64_t *work, uint64_t *proof,
-                          uint64_t *randomness);
+                          uint64_t *randomness, uint64_t *evals);
 
 /* ------------------------------------------------------------ sparse Mz products
  * CCS.M (latticefold/src/arith.rs:51-74): t matrices m x n of ring elements,
@@ -433,6 +435,10 @@ int lf_ccs_create(lf_ctx *ctx, int d, int t, size_t m, size_t n, const uint64_t 
                   const uint64_t *val, int repr, lf_ccs **out);
 void lf_ccs_destroy(lf_ccs *M);
 int lf_dev_mz_mles(lf_ctx *ctx, const lf_ccs *M, const uint64_t *z, int nz, int nv, uint64_t *out);
+/* the MLEs of the selected matrices only, out[i] = MLE(M_sel[i] z) (sel: host, nsel
+ * indices < t; one z) */
+int lf_dev_mz_mles_sel(lf_ctx *ctx, const lf_ccs *M, const uint64_t *z, const int *sel, int nsel, int nv,
+                       uint64_t *out);
 int lf_dev_mz_challenged(lf_ctx *ctx, const lf_ccs *M, const uint64_t *z, const uint64_t *zeta, int nz, int nv,
                          uint64_t *out);
 int lf_dev_mz_evaluate(lf_ctx *ctx, const lf_ccs *M, const uint64_t *z, int nz, int nv, const uint64_t *point,

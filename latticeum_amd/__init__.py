@@ -330,17 +330,19 @@ class Context:
         return proof, rnd
 
     def sumcheck_prove_lin(self, transcript: "Poseidon2Transcript", comb: "Comb", mles, nv: int, d: int,
-                           degree: int, beta, work):
+                           degree: int, beta, work, evals=None):
         """the linearization sumcheck with eq(beta) split off (lf_sumcheck_prove_lin): mles a
         list of device tensors (one MLE of 2^nv elements each, read only), beta [nv][d] host
-        values; the proof and randomness of sumcheck_prove over [mles..., eq(beta)]"""
+        values; the proof and randomness of sumcheck_prove over [mles..., eq(beta)]; evals
+        (device, len(mles) d, optional) receives the MLEs at the challenge point"""
         tau = 3 if d == 24 else 1
         proof = np.zeros(nv * (degree + 1) * d, np.uint64)
         rnd = np.zeros(nv * tau, np.uint64)
         ptrs = (C.c_void_p * len(mles))(*[_dptr(m) for m in mles])
         b = _u64(beta)
         self.check(self.lib.lf_sumcheck_prove_lin(self.h, transcript.h, C.byref(comb.s), ptrs, len(mles), nv, d,
-                                                  degree, _ptr(b), _dptr(work), _ptr(proof), _ptr(rnd)))
+                                                  degree, _ptr(b), _dptr(work), _ptr(proof), _ptr(rnd),
+                                                  _dptr(evals) if evals is not None else None))
         return proof, rnd
 
     # ---------------------------------------------------------------- width-8 Merkle trees
@@ -477,6 +479,11 @@ class CCSMatrices:
 
     def mz_mles(self, z, nz: int, nv: int, out):
         self.ctx.check(self.lib.lf_dev_mz_mles(self.ctx.h, self.h, _dptr(z), nz, nv, _dptr(out)))
+
+    def mz_mles_sel(self, z, sel, nv: int, out):
+        """the MLEs of the selected matrices only (lf_dev_mz_mles_sel): out[i] = MLE(M_sel[i] z)"""
+        s = np.ascontiguousarray(np.asarray(sel, np.int32))
+        self.ctx.check(self.lib.lf_dev_mz_mles_sel(self.ctx.h, self.h, _dptr(z), _ptr(s), len(s), nv, _dptr(out)))
 
     def mz_challenged(self, z, zeta, nz: int, nv: int, out):
         self.ctx.check(self.lib.lf_dev_mz_challenged(self.ctx.h, self.h, _dptr(z), _dptr(zeta), nz, nv, _dptr(out)))

@@ -202,6 +202,7 @@ SIGNATURES = {
     "lf_transcript_new_playback": (VP, [VP, SZ]),
     "lf_transcript_playback_status": (I, [VP]),
     "lf_dev_mz_mles": (I, [VP, VP, VP, I, I, VP]),
+    "lf_dev_mz_mles_sel": (I, [VP, VP, VP, VP, I, I, VP]),
     "lf_dev_mz_challenged": (I, [VP, VP, VP, VP, I, I, VP]),
     "lf_dev_mz_evaluate": (I, [VP, VP, VP, I, I, VP, VP]),
     "lf_ccs_weights_len": (SZ, [VP]),
@@ -214,7 +215,7 @@ SIGNATURES = {
     "lf_dev_sumcheck_round": (I, [VP, C.POINTER(LfComb), VP, SZ, I, I, I, I, VP]),
     "lf_sumcheck_prove": (I, [VP, VP, C.POINTER(LfComb), VP, I, I, I, I, VP, VP]),
     "lf_sumcheck_prove_ptrs": (I, [VP, VP, C.POINTER(LfComb), VP, I, I, I, I, VP, VP, VP]),
-    "lf_sumcheck_prove_lin": (I, [VP, VP, C.POINTER(LfComb), VP, I, I, I, I, VP, VP, VP, VP]),
+    "lf_sumcheck_prove_lin": (I, [VP, VP, C.POINTER(LfComb), VP, I, I, I, I, VP, VP, VP, VP, VP]),
     "lf_fold_lcccs": (I, [VP, I, I, VP, VP, VP, SZ, VP, SZ, VP, VP, VP, VP, I]),
     "lf_dev_fold_lcccs": (I, [VP, I, I, VP, VP, VP, SZ, VP, SZ, VP, VP, VP, VP]),
     "lf_compute_x_s": (I, [VP, C.POINTER(LfParams), VP, SZ, VP, I]),

@@ -34,6 +34,12 @@ struct lf_prover {
   std::vector<uint64_t> c;  // q NTT elements
   std::vector<int> S_off, S_idx;
   std::vector<int> lin_list;  // the matrix of every linearization MLE (c_i != 0, j in S_i)
+  // the Mz MLEs are materialised live matrices first (mz_order: the matrices read by the
+  // linearization's combination, then the others); S_live: each multiset entry's
+  // position among the nlive live ones; bad_S: a multiset index past the MLE list
+  std::vector<int> mz_order, S_live;
+  int nlive = 0;
+  bool bad_S = false;
   // device memory: one allocation, carved
   uint64_t *mem = nullptr;
   uint64_t *z = nullptr, *mz = nullptr, *lin = nullptr, *pt = nullptr, *beta = nullptr, *val = nullptr;
@@ -43,6 +49,7 @@ struct lf_prover {
            *v0 = nullptr, *r0 = nullptr;
   // eq(r_0) and one point's Mz weights M_j^T eq (shared by the sides evaluated there)
   uint64_t *eq0 = nullptr, *mzw = nullptr;
+  uint64_t *lev = nullptr;  // the live Mz MLEs at r_lin (the linearization sumcheck's final values)
   std::string err;
   // every value the last lf_fold_prove sampled from its transcript, in order
   // (lf_fold_prove_vars replays the proof on them instead of a second sponge)
@@ -180,45 +187,44 @@ struct Run {
   }
 };
 
-// LFLinearizationProver::prove (linearization.rs:153-197) of the CCCS (cm, x_ccs)
-// with witness w, on the transcript R.T: the sumcheck messages into lin_sumcheck
-// (host), and r, v, u of the linearized instance {r, v, cm, u, x_ccs, ONE}
-int linearize(lf_prover *P, Run &R, const std::vector<uint64_t> &xc, const lf_witness *w_i, uint64_t *lin_sumcheck,
-              std::vector<uint64_t> &r_lin, std::vector<uint64_t> &lv, std::vector<uint64_t> &lu) {
+// z = x_ccs || 1 || w_ccs (Instance::get_z_vector) and its Mz MLEs: independent of the
+// transcript, so enqueued before the public input is absorbed (the device computes
+// them while the host hashes). Live matrices first (lf_prover::mz_order).
+int linearize_prepare(lf_prover *P, Run &R, const std::vector<uint64_t> &xc, const lf_witness *w_i) {
   lf_ctx *C = P->ctx;
-  const int d = P->d, tb = P->tb, tau = P->tau, s = P->s, t = P->t;
-  const size_t W = P->W, N = P->N, nn = P->nn, l = P->l;
+  const int d = P->d, tb = P->tb;
+  const size_t W = P->W, l = P->l;
+  if (P->bad_S) {
+    P->err = "multiset index past the MLE list";
+    return R.rc = LF_ERR_INVALID_ARG;
+  }
   std::vector<uint64_t> one(d, 0);
   for (int i = 0; i < d; i += tb) one[i] = 1;
-  R.absorb_label("beta_s");  // squeeze_beta_challenges (linearization/utils.rs:111-124)
-  const std::vector<uint64_t> beta = R.challenges(s);
-  R.h2d(P->beta, beta.data(), (size_t)s * d);
-  // z = x_ccs || 1 || w_ccs (Instance::get_z_vector), the Mz MLEs, the MLE list + eq(beta)
   R.h2d(P->z, xc.data(), l * d);
   R.h2d(P->z + l * d, one.data(), d);
   R.d2d(P->z + (l + 1) * d, w_i->w_ccs, W * d);
-  R.check(lf_dev_mz_mles(C, P->ccs, P->z, 1, s, P->mz), "Mz MLEs");
+  return R.check(lf_dev_mz_mles_sel(C, P->ccs, P->z, P->mz_order.data(), P->t, P->s, P->mz), "Mz MLEs");
+}
+
+// LFLinearizationProver::prove (linearization.rs:153-197) of the CCCS (cm, x_ccs)
+// with witness w (its Mz MLEs from linearize_prepare), on the transcript R.T: the
+// sumcheck messages into lin_sumcheck (host), and r, v, u of the linearized instance
+// {r, v, cm, u, x_ccs, ONE}
+int linearize(lf_prover *P, Run &R, const lf_witness *w_i, uint64_t *lin_sumcheck, std::vector<uint64_t> &r_lin,
+              std::vector<uint64_t> &lv, std::vector<uint64_t> &lu) {
+  lf_ctx *C = P->ctx;
+  const int d = P->d, tb = P->tb, tau = P->tau, s = P->s, t = P->t, nlive = P->nlive;
+  const size_t N = P->N, nn = P->nn, len = nn * d;
+  R.absorb_label("beta_s");  // squeeze_beta_challenges (linearization/utils.rs:111-124)
+  const std::vector<uint64_t> beta = R.challenges(s);
   // The MLE list is [MLE(M_j z) for each (i, j in S_i) with c_i != 0] + [eq(beta)]
   // (linearization/utils.rs:71-84), and the combination reads list position j for
-  // matrix index j (as the reference does) and the last entry -- so only those
-  // positions are live. Their MLEs are read where the Mz products left them (a
-  // pointer table; no copies), the dead positions are never fixed, and eq(beta) is
-  // split off each round (lf_sumcheck_prove_lin: beta itself, no eq MLE); P->lin
-  // serves the later rounds.
-  std::vector<int> live_of(P->lin_list.size(), -1), S_live(P->S_idx.size());
-  std::vector<const uint64_t *> ptr;
-  for (size_t k = 0; k < P->S_idx.size(); k++) {
-    const int p = P->S_idx[k];
-    if (p < 0 || (size_t)p >= P->lin_list.size()) {
-      P->err = "multiset index past the MLE list";
-      return R.rc = LF_ERR_INVALID_ARG;
-    }
-    if (live_of[p] < 0) {
-      live_of[p] = (int)ptr.size();
-      ptr.push_back(P->mz + (size_t)P->lin_list[p] * nn * d);
-    }
-    S_live[k] = live_of[p];
-  }
+  // matrix index j (as the reference does) and the last entry -- so only the live
+  // matrices' MLEs are read, each where the Mz products left it (a pointer table;
+  // no copies), and eq(beta) is split off each round (lf_sumcheck_prove_lin: beta
+  // itself, no eq MLE); P->lin (nlive x m/4 elements) serves the later rounds.
+  std::vector<const uint64_t *> ptr(nlive);
+  for (int i = 0; i < nlive; i++) ptr[i] = P->mz + (size_t)i * len;
   std::vector<uint64_t> rnd((size_t)s * tb);
   {
     lf_comb cb{};
@@ -226,27 +232,36 @@ int linearize(lf_prover *P, Run &R, const std::vector<uint64_t> &xc, const lf_wi
     cb.q = P->q;
     cb.c = lf_ccs_c_device(P->ccs);
     cb.S_off = P->S_off.data();
-    cb.S_idx = S_live.data();
+    cb.S_idx = P->S_live.data();
     if (R.rc == LF_OK)
-      R.check(lf_sumcheck_prove_lin(C, R.T, &cb, ptr.data(), (int)ptr.size(), s, d, P->degree + 1, beta.data(),
-                                    P->lin, lin_sumcheck, rnd.data()),
+      R.check(lf_sumcheck_prove_lin(C, R.T, &cb, ptr.data(), nlive, s, d, P->degree + 1, beta.data(), P->lin,
+                                    lin_sumcheck, rnd.data(), P->lev),
               "linearization sumcheck");
   }
   if (R.rc) return R.rc;
   r_lin.assign((size_t)s * d, 0);
   for (int i = 0; i < s; i++) broadcast(rnd.data() + (size_t)i * tb, tb, d, r_lin.data() + (size_t)i * d);
   R.h2d(P->pt, r_lin.data(), (size_t)s * d);
-  // v = f_hat(w_i) at r, u = MLE(M_j z)(r) (compute_evaluation_vectors, :130-147), from one
-  // eq(r) table -- built where the folding prover's eq(r_1) MLE lives, which it is
+  // v = f_hat(w_i) at r, u = MLE(M_j z)(r) (compute_evaluation_vectors, :130-147): the
+  // live matrices' u are the sumcheck's final values, the others are evaluated against
+  // one eq(r) table -- built where the folding prover's eq(r_1) MLE lives, which it is
   uint64_t *eq_lin = P->fold + 2 * nn * d;
   R.check(lf_dev_eq_table(C, d, P->pt, s, eq_lin), "eq(r)");
   R.check(lf_dev_fhat_evaluate_eq(C, d, w_i->f_coeff, N, 0, 1, s, eq_lin, P->val), "v");
-  R.check(lf_dev_mle_evaluate_eq(C, d, P->mz, t, s, eq_lin, P->val + (size_t)tau * d), "u");
+  if (t > nlive)
+    R.check(lf_dev_mle_evaluate_eq(C, d, P->mz + (size_t)nlive * len, t - nlive, s, eq_lin, P->val + (size_t)tau * d),
+            "u");
   lv.assign((size_t)tau * d, 0);
-  lu.assign((size_t)t * d, 0);
+  std::vector<uint64_t> ub((size_t)t * d);
   R.d2h(lv.data(), P->val, (size_t)tau * d);
-  R.d2h(lu.data(), P->val + (size_t)tau * d, (size_t)t * d);
+  R.d2h(ub.data(), P->val + (size_t)tau * d, (size_t)(t - nlive) * d);
+  R.d2h(ub.data() + (size_t)(t - nlive) * d, P->lev, (size_t)nlive * d);
   if (R.rc) return R.rc;
+  lu.assign((size_t)t * d, 0);
+  for (int i = 0; i < t; i++) {  // position i of mz_order is matrix mz_order[i]
+    const uint64_t *src = i < nlive ? ub.data() + (size_t)(t - nlive + i) * d : ub.data() + (size_t)(i - nlive) * d;
+    memcpy(lu.data() + (size_t)P->mz_order[i] * d, src, d * 8);
+  }
   R.absorb(lv.data(), tau);
   R.absorb(lu.data(), t);
   return LF_OK;
@@ -319,6 +334,27 @@ int lf_prover_create(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, const
     for (int k = P->S_off[i]; k < P->S_off[i + 1]; k++) P->lin_list.push_back(P->S_idx[k]);
   }
   P->nm_lin = (int)P->lin_list.size() + 1;
+  {
+    std::vector<int> pos_of(t, -1);
+    P->S_live.resize(P->S_idx.size());
+    for (size_t k = 0; k < P->S_idx.size(); k++) {
+      const int p = P->S_idx[k];
+      if (p < 0 || (size_t)p >= P->lin_list.size()) {
+        P->bad_S = true;
+        P->S_live[k] = 0;
+        continue;
+      }
+      const int j = P->lin_list[p];
+      if (pos_of[j] < 0) {
+        pos_of[j] = (int)P->mz_order.size();
+        P->mz_order.push_back(j);
+      }
+      P->S_live[k] = pos_of[j];
+    }
+    P->nlive = (int)P->mz_order.size();
+    for (int j = 0; j < t; j++)
+      if (pos_of[j] < 0) P->mz_order.push_back(j);
+  }
   P->nm_fold = 5 + 2 * P->K * P->tau;
   // device memory, carved from one allocation
   const size_t K = P->K, N = P->N, W = P->W, nn = P->nn, kd = P->kappa * d, tau = P->tau;
@@ -327,7 +363,7 @@ int lf_prover_create(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, const
     size_t elems;
   };
   std::vector<Part> parts = {
-      {&P->z, n * d}, {&P->mz, (size_t)t * nn * d}, {&P->lin, (size_t)P->nm_lin * nn * d},
+      {&P->z, n * d}, {&P->mz, (size_t)t * nn * d}, {&P->lin, (size_t)std::max(P->nlive, 1) * std::max<size_t>(nn / 4, 1) * d},
       {&P->pt, (size_t)P->s * d}, {&P->beta, (size_t)P->s * d}, {&P->val, (size_t)(t + 3) * d},
       {&P->fkc[0], K * N * d}, {&P->fkc[1], K * N * d}, {&P->fk[0], K * N * d}, {&P->fk[1], K * N * d},
       {&P->wk[0], K * W * d}, {&P->wk[1], K * W * d}, {&P->y[0], K * kd}, {&P->y[1], K * kd},
@@ -337,7 +373,7 @@ int lf_prover_create(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, const
       {&P->coef[0], K * tau * d}, {&P->coef[1], K * tau * d}, {&P->zeta, 2 * K * d}, {&P->mu, 2 * K * d},
       {&P->theta, 2 * K * tau * d}, {&P->eta, 2 * K * t * d}, {&P->rho, 2 * K * d}, {&P->rhoc, 2 * K * d},
       {&P->cm0, kd}, {&P->u0, (size_t)t * d}, {&P->x0, (l + 1) * d}, {&P->v0, tau * d}, {&P->r0, (size_t)P->s * d},
-      {&P->eq0, nn * d}, {&P->mzw, lf_ccs_weights_len(ccs)}};
+      {&P->eq0, nn * d}, {&P->mzw, lf_ccs_weights_len(ccs)}, {&P->lev, (size_t)t * d}};
   size_t total = 0;
   for (auto &x : parts) total += (x.elems + 31) / 32 * 32;  // 256-B aligned parts
   int prev = -1;
@@ -400,7 +436,7 @@ int lf_linearize(lf_prover *P, const uint64_t *cm, const uint64_t *x_ccs, const 
     ~TGuard() { lf_transcript_free(t); }
   } tg{R.T};
   std::vector<uint64_t> r_lin, lv, lu;
-  if (linearize(P, R, xc, w, lin_sumcheck, r_lin, lv, lu)) return R.rc;
+  if (linearize_prepare(P, R, xc, w) || linearize(P, R, w, lin_sumcheck, r_lin, lv, lu)) return R.rc;
   // the LCCCS {r, v, cm, u, x_w = x_ccs, h = ONE} (linearization.rs:185-193)
   memcpy(out->r, r_lin.data(), r_lin.size() * 8);
   memcpy(out->v, lv.data(), lv.size() * 8);
@@ -482,6 +518,8 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
   std::vector<uint64_t> one(d, 0);
   for (int i = 0; i < d; i += tb) one[i] = 1;
 
+  // the linearization's Mz MLEs need no challenge: on the device while the host absorbs
+  if (linearize_prepare(P, R, xc, w_i)) return R.rc;
   // ---- absorb_public_input (zk_latticefold.rs:162-184)
   R.absorb_label("acc");
   R.absorb(ar.data(), s);
@@ -494,10 +532,10 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
   R.absorb(cmi.data(), kappa);
   R.absorb(xc.data(), l);
 
-  R.mark(LF_SPAN_PUBLIC_INPUT);
+  R.mark(LF_SPAN_PUBLIC_INPUT, false);
   // ---- linearization (linearization.rs:153-197)
   std::vector<uint64_t> r_lin, lv, lu;
-  if (linearize(P, R, xc, w_i, proof->lin_sumcheck, r_lin, lv, lu)) return R.rc;
+  if (linearize(P, R, w_i, proof->lin_sumcheck, r_lin, lv, lu)) return R.rc;
   R.mark(LF_SPAN_LINEARIZATION);
   // the linearized instance: {r, v, cm_i, u, x_ccs, h = ONE}
 
@@ -541,7 +579,7 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
   R.h2p2d(P->pt, P->hr[0], ar.data(), (size_t)s * d);
   R.check(lf_dev_eq_table(C, d, P->pt, s, M), "eq(r_0)");
   const int G = MZ_GROUP, ng = (K + G - 1) / G;
-  for (int side = 0; side < 2; side++) {
+  auto enqueue_side = [&](int side) {
     const uint64_t *eq_s = M + (size_t)(2 * side) * mstride;
     R.check(lf_dev_fhat_evaluate_eq(C, d, P->fkc[side], N, ND, K, s, eq_s, P->vs + (size_t)side * K * tau * d), "v_s");
     R.d2p(P->hx[side], P->xs + (size_t)side * K * (l + 1) * d, (size_t)K * (l + 1) * d);
@@ -555,9 +593,11 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
       R.d2p(P->hu[side] + (size_t)k0 * t * d, us, (size_t)nk * t * d);
       R.hip(hipEventRecord(P->ev[2 + side * ng + g], R.st), "event");
     }
-  }
-  for (int side = 0; side < 2; side++)
-    R.hip(lfk::get_fhat(P->fkc[side], N, d, s, M + (5 + (size_t)side * K * tau) * mstride, R.st, K, ND), "f_hat");
+  };
+  // side 1's work and the f_hat MLEs are enqueued while the host absorbs side 0 (a
+  // stream holds a bounded number of commands in flight: enqueued all at once, the
+  // host would block on the queue instead of hashing)
+  enqueue_side(0);
   if (R.rc) return R.rc;
   R.mark(LF_SPAN_DECOMPOSITION, false);
   for (int side = 0; side < 2; side++)
@@ -572,6 +612,11 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
       R.absorb(proof->y_s[side] + oy, kappa);
       R.absorb(proof->u_s[side] + ou, t);
       R.absorb(proof->v_s[side] + ov, tau);
+      if (side == 0 && k == 0) enqueue_side(1);
+      if (side == 0 && k == std::min(G, K) - 1)
+        for (int sd = 0; sd < 2; sd++)
+          R.hip(lfk::get_fhat(P->fkc[sd], N, d, s, M + (5 + (size_t)sd * K * tau) * mstride, R.st, K, ND), "f_hat");
+      if (R.rc) return R.rc;
     }
 
   R.mark(LF_SPAN_DECOMPOSITION_TRANSCRIPT, false);
@@ -641,18 +686,22 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
   R.d2p(P->htheta, P->theta, 2 * (size_t)K * tau * d);
   R.hip(hipEventRecord(P->ev[0], R.st), "event");
   R.check(lf_dev_mz_weights(C, P->ccs, s, P->eq0, P->mzw), "eta weights");
-  for (int g = 0; g < 2 * ng; g++) {  // instance groups of both sides, in absorb order
-    const int side = g / ng, k0 = (g % ng) * G, nk = std::min(G, K - k0);
-    const size_t o = ((size_t)side * K + k0) * t * d;
-    R.check(lf_dev_mz_dots(C, P->ccs, P->mzw, P->zdec[side] + (size_t)k0 * n * d, nk, P->eta + o), "eta");
-    R.d2p(P->heta + o, P->eta + o, (size_t)nk * t * d);
-    R.hip(hipEventRecord(P->ev[2 + g], R.st), "event");
-  }
+  auto enqueue_eta = [&](int side) {  // instance groups of one side, in absorb order
+    for (int gg = 0; gg < ng; gg++) {
+      const int g = side * ng + gg, k0 = gg * G, nk = std::min(G, K - k0);
+      const size_t o = ((size_t)side * K + k0) * t * d;
+      R.check(lf_dev_mz_dots(C, P->ccs, P->mzw, P->zdec[side] + (size_t)k0 * n * d, nk, P->eta + o), "eta");
+      R.d2p(P->heta + o, P->eta + o, (size_t)nk * t * d);
+      R.hip(hipEventRecord(P->ev[2 + g], R.st), "event");
+    }
+  };
+  enqueue_eta(0);
   if (R.rc) return R.rc;
   R.mark(LF_SPAN_EVALUATIONS, false);
   if (R.wait(P->ev[0])) return R.rc;
   memcpy(proof->theta_s, P->htheta, 2 * (size_t)K * tau * d * 8);
   for (int i = 0; i < 2 * K; i++) R.absorb(proof->theta_s + (size_t)i * tau * d, tau);
+  enqueue_eta(1);  // while the host absorbs side 0's eta_s
   for (int side = 0; side < 2; side++)
     for (int k = 0; k < K; k++) {
       if (k % G == 0 && R.wait(P->ev[2 + side * ng + k / G])) return R.rc;

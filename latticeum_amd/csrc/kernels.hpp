@@ -297,7 +297,9 @@ struct CcsDev {
 };
 size_t mz_scratch_elems(const CcsDev &M, int nz, int nv);
 // out [nz][t][2^nv][d] = MLE(M_j z_i), zero-padded; z [nz][n][d]
-hipError_t mz_mles(const CcsDev &M, const uint64_t *z, int nz, int nv, uint64_t *out, hipStream_t st);
+// sel (device, optional): out holds the MLEs of matrices sel[0 .. nsel) in that order
+hipError_t mz_mles(const CcsDev &M, const uint64_t *z, int nz, int nv, uint64_t *out, hipStream_t st,
+                   const int *sel = nullptr, int nsel = 0);
 // out [2^nv][d] = sum_i sum_j zeta_i^(j+1) MLE(M_j z_i)
 hipError_t mz_challenged(const CcsDev &M, const uint64_t *z, const uint64_t *zeta, int nz, int nv, uint64_t *out,
                          uint64_t *scratch, hipStream_t st);

@@ -71,6 +71,8 @@ struct lf_ctx {
   size_t sc_elems = 0;
   uint64_t *ptrs = nullptr;     // lf_sumcheck_prove_ptrs: the MLE pointer table
   size_t ptrs_elems = 0;
+  int *sel = nullptr;           // lf_dev_mz_mles_sel: the selected matrices
+  size_t sel_elems = 0;
   lfk::FoldRows fold_rows{};    // a step without f_k buffers: where its 2K planes sit in the operand rows
   bool fold_from_frag = false;
   bool frag_fallback = false;   // packed d = 1024 planes: fold_rows serve the not-short-rho fallback
@@ -912,6 +914,7 @@ void lf_ctx_destroy(lf_ctx *c) {
   if (c->tmp) (void)hipFree(c->tmp);
   if (c->sc) (void)hipFree(c->sc);
   if (c->ptrs) (void)hipFree(c->ptrs);
+  if (c->sel) (void)hipFree(c->sel);
   if (c->join) (void)hipEventDestroy(c->join);
   if (c->d_err) (void)hipFree(c->d_err);
   if (c->d_sync) (void)hipFree(c->d_sync);
@@ -1712,7 +1715,7 @@ int lf_sumcheck_prove_ptrs(lf_ctx *c, lf_transcript *t, const lf_comb *cb, const
 // the same field elements as the unsplit round sums, so the transcript is the same.
 static int sumcheck_run_lin(lf_ctx *c, lf_transcript *t, const lf_comb *cb, const lfk::CombS &cs,
                             const uint64_t *const *ptrs, uint64_t *alt, int nm, int nv, int d, int degree,
-                            const uint64_t *beta, uint64_t *proof, uint64_t *randomness) {
+                            const uint64_t *beta, uint64_t *proof, uint64_t *randomness, uint64_t *evals) {
   const int tb = lfk::slot_words(d), nev = degree + 1, nq = degree, ns = d / tb;
   const size_t n = (size_t)1 << nv;
   size_t part = 0;
@@ -1813,6 +1816,8 @@ static int sumcheck_run_lin(lf_ctx *c, lf_transcript *t, const lf_comb *cb, cons
       bmul(pfx, ev, np);
       for (int w = 0; w < tb; w++) pfx[w] = np[w];
     }
+    if (i + 1 == nv && evals)  // the MLEs at the whole challenge point (the prover's final values)
+      LF_HIP(c, lfk::mle_fix_first(cur, stride, nm, half, d, ch, evals, d, c->cur, cptrs));
     if (i + 1 < nv) {
       uint64_t *dst = (i % 2 == 0) ? buf : alt;
       LF_HIP(c, lfk::mle_fix_first(cur, stride, nm, half, d, ch, dst, half * d, c->cur, cptrs));
@@ -1828,7 +1833,7 @@ static int sumcheck_run_lin(lf_ctx *c, lf_transcript *t, const lf_comb *cb, cons
 
 int lf_sumcheck_prove_lin(lf_ctx *c, lf_transcript *t, const lf_comb *cb, const uint64_t *const *mles, int nm, int nv,
                           int d, int degree, const uint64_t *beta, uint64_t *work, uint64_t *proof,
-                          uint64_t *randomness) {
+                          uint64_t *randomness, uint64_t *evals) {
   if (!c || !t || !mles || !beta || !work || !proof || !randomness || nv < 1 || nm < 1) return LF_ERR_INVALID_ARG;
   DevGuard g(c);
   if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
@@ -1844,7 +1849,7 @@ int lf_sumcheck_prove_lin(lf_ctx *c, lf_transcript *t, const lf_comb *cb, const 
   LF_TRY(grow(c, c->ptrs, c->ptrs_elems, (size_t)nm));
   LF_HIP(c, hipMemcpyAsync(c->ptrs, mles, (size_t)nm * sizeof(uint64_t), hipMemcpyHostToDevice, c->cur));
   return sumcheck_run_lin(c, t, cb, cs, reinterpret_cast<const uint64_t *const *>(c->ptrs), work, nm, nv, d, degree,
-                          beta, proof, randomness);
+                          beta, proof, randomness, evals);
 }
 
 // ---------------------------------------------------------------- sparse Mz products
@@ -2001,6 +2006,20 @@ int lf_dev_mz_mles(lf_ctx *c, const lf_ccs *M, const uint64_t *z, int nz, int nv
   DevGuard g(c);
   LF_TRY(mz_check(c, M, nz, nv));
   LF_HIP(c, lfk::mz_mles(M->dev, z, nz, nv, out, c->cur));
+  return LF_OK;
+}
+
+int lf_dev_mz_mles_sel(lf_ctx *c, const lf_ccs *M, const uint64_t *z, const int *sel, int nsel, int nv,
+                       uint64_t *out) {
+  if (!c || !z || !out || (!sel && nsel) || nsel < 0) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  LF_TRY(mz_check(c, M, 1, nv));
+  for (int i = 0; i < nsel; i++)
+    if (sel[i] < 0 || sel[i] >= M->dev.t) return fail(c, LF_ERR_INVALID_ARG, "matrix index out of range");
+  if (!nsel) return LF_OK;
+  LF_TRY(grow(c, c->sel, c->sel_elems, (size_t)nsel));
+  LF_HIP(c, hipMemcpyAsync(c->sel, sel, (size_t)nsel * sizeof(int), hipMemcpyHostToDevice, c->cur));
+  LF_HIP(c, lfk::mz_mles(M->dev, z, 1, nv, out, c->cur, c->sel, nsel));
   return LF_OK;
 }
 

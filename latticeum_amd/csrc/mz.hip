@@ -24,18 +24,19 @@ namespace {
 constexpr int MT = 256;
 
 // out[task][r] = sum_k val[vidx ? vidx[k] : k] (.) z[col[k]], k in [rp[r], rp[r+1]);
-// task = (a, b) = (task % na, task / na) selects rp + a rp_stride and z + b z_stride
+// task = (a, b) = (task % na, task / na) selects rp + A rp_stride (A = sel ? sel[a] : a)
+// and z + b z_stride
 template <int TB>
-__global__ void __launch_bounds__(MT) k_csr(const uint64_t *rp, size_t rp_stride, int na, const uint32_t *col,
-                                           const uint32_t *vidx, const uint64_t *val, size_t nrows, int d,
-                                           const uint64_t *z, size_t z_stride, uint64_t *out, size_t out_stride,
-                                           int spb) {
+__global__ void __launch_bounds__(MT) k_csr(const uint64_t *rp, size_t rp_stride, int na, const int *sel,
+                                           const uint32_t *col, const uint32_t *vidx, const uint64_t *val,
+                                           size_t nrows, int d, const uint64_t *z, size_t z_stride, uint64_t *out,
+                                           size_t out_stride, int spb) {
   const int slot_l = threadIdx.x % spb, lane_r = threadIdx.x / spb, rpb = MT / spb;
   const int slot = blockIdx.z * spb + slot_l;
   const size_t r = (size_t)blockIdx.x * rpb + lane_r;
   if (r >= nrows) return;
   const int task = blockIdx.y, a = task % na, b = task / na;
-  const uint64_t *rpa = rp + a * rp_stride;
+  const uint64_t *rpa = rp + (size_t)(sel ? sel[a] : a) * rp_stride;
   const uint64_t *zb = z + b * z_stride + slot * TB;
   SAcc<TB> acc;
   sacc_zero(acc);
@@ -122,18 +123,26 @@ int dots_nsplit(const CcsDev &M, int nz) {
 
 unsigned nblk(size_t n, int t) { return (unsigned)((n + t - 1) / t); }
 
+// out[i][from + x] = 0 for x < tail, i < total / tail (MLE i of len u64)
+__global__ void k_zero_tails(uint64_t *out, size_t len, size_t from, size_t tail, size_t total) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const size_t i = t / tail;
+  out[i * len + from + (t - i * tail)] = 0;
+}
+
 hipError_t csr(const uint64_t *rp, size_t rp_stride, int na, const uint32_t *col, const uint32_t *vidx,
                const uint64_t *val, size_t nrows, int d, const uint64_t *z, size_t z_stride, uint64_t *out,
-               size_t out_stride, int ntask, hipStream_t st) {
+               size_t out_stride, int ntask, hipStream_t st, const int *sel = nullptr) {
   if (!nrows || !ntask) return hipSuccess;
   const int tb = slot_words(d), ns = d / tb, spb = ns < MT ? ns : MT;
   const dim3 grid(nblk(nrows, MT / spb), (unsigned)ntask, (unsigned)(ns / spb));
   if (tb == 3)
-    hipLaunchKernelGGL(k_csr<3>, grid, dim3(MT), 0, st, rp, rp_stride, na, col, vidx, val, nrows, d, z, z_stride, out,
-                       out_stride, spb);
+    hipLaunchKernelGGL(k_csr<3>, grid, dim3(MT), 0, st, rp, rp_stride, na, sel, col, vidx, val, nrows, d, z, z_stride,
+                       out, out_stride, spb);
   else
-    hipLaunchKernelGGL(k_csr<1>, grid, dim3(MT), 0, st, rp, rp_stride, na, col, vidx, val, nrows, d, z, z_stride, out,
-                       out_stride, spb);
+    hipLaunchKernelGGL(k_csr<1>, grid, dim3(MT), 0, st, rp, rp_stride, na, sel, col, vidx, val, nrows, d, z, z_stride,
+                       out, out_stride, spb);
   return hipGetLastError();
 }
 
@@ -145,12 +154,19 @@ size_t mz_scratch_elems(const CcsDev &M, int nz, int nv) {
   return chall > eval ? chall : eval;
 }
 
-hipError_t mz_mles(const CcsDev &M, const uint64_t *z, int nz, int nv, uint64_t *out, hipStream_t st) {
+hipError_t mz_mles(const CcsDev &M, const uint64_t *z, int nz, int nv, uint64_t *out, hipStream_t st, const int *sel,
+                   int nsel) {
   const size_t len = ((size_t)1 << nv) * M.d;
   if (M.m > ((size_t)1 << nv)) return hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(out, 0, (size_t)nz * M.t * len * 8, st);  // the MLEs' zero padding
-  if (e != hipSuccess) return e;
-  return csr(M.rp, M.m + 1, M.t, M.col, nullptr, M.val, M.m, M.d, z, M.n * M.d, out, len, nz * M.t, st);
+  const int na = sel ? nsel : M.t;
+  if (na < 1) return hipSuccess;
+  if (M.m < ((size_t)1 << nv)) {  // the MLEs' zero padding: rows m .. 2^nv - 1 of each
+    const size_t tail = len - M.m * M.d, total = (size_t)nz * na * tail;
+    hipLaunchKernelGGL(k_zero_tails, dim3(nblk(total, 256)), dim3(256), 0, st, out, len, M.m * M.d, tail, total);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return csr(M.rp, M.m + 1, na, M.col, nullptr, M.val, M.m, M.d, z, M.n * M.d, out, len, nz * na, st, sel);
 }
 
 hipError_t mz_challenged(const CcsDev &M, const uint64_t *z, const uint64_t *zeta, int nz, int nv, uint64_t *out,

@@ -798,7 +798,6 @@ __global__ void k_get_fhat(const uint64_t *f_coeff, size_t N, size_t wstride, in
                            size_t total, uint64_t *out) {
   const size_t t0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (t0 >= total) return;
-  const int tau = d == 24 ? 3 : 1;
   const size_t wi = t0 / per, t = t0 - wi * per;  // witness wi, word t of its tau MLEs
   const uint64_t *fc = f_coeff + wi * wstride;
   const size_t w = t % d, ji = t / d, i = ji % npts;

@@ -64,6 +64,14 @@ def test_mz_products_match_oracle(ctx, d):
     ctx.sync()
     want = np.concatenate([O.mz_mles(mats, z, nv, d) for z in zs])
     assert np.array_equal(host(out), want)
+    # the selected matrices only, in the given order (padding rows zeroed over stale data)
+    sel = [3, 0, 4, 1]
+    part = dev(n=len(sel) * (1 << nv) * d)
+    ctx.dev_fill_uniform(part, 55 + d)
+    M.mz_mles_sel(zd, sel, nv, part)
+    ctx.sync()
+    L = (1 << nv) * d
+    assert np.array_equal(host(part), np.concatenate([want[j * L:(j + 1) * L] for j in sel]))
     zeta = O.fill_uniform(nz * d, 60 + d)
     ch = dev(n=(1 << nv) * d)
     M.mz_challenged(zd, dev(zeta), nz, nv, ch)

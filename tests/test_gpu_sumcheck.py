@@ -194,9 +194,15 @@ def test_linearization_prove_lin_matches_oracle(ctx, d, nv, sizes):
     want_p, want_r = O.sumcheck_prove(O.new_transcript(), O.SumcheckComb.linearization(c, S), mles, len(mz) + 1, nv,
                                       d, degree)
     work = dev(n=max(1, len(mz) * (1 << max(nv - 2, 0)) * d))
+    evals = dev(n=len(mz) * d)
     proof, rnd = ctx.sumcheck_prove_lin(LA.Poseidon2Transcript(), LA.Comb.linearization(dev(c), S),
-                                        [dev(m) for m in mz], nv, d, degree, beta, work)
+                                        [dev(m) for m in mz], nv, d, degree, beta, work, evals)
     assert np.array_equal(proof, want_p) and np.array_equal(rnd, want_r)
+    # the MLEs' final values are their evaluations at the challenge point
+    tau = 3 if d == 24 else 1
+    point = np.concatenate([O.broadcast(rnd[i * tau:(i + 1) * tau], d) for i in range(nv)])
+    ctx.sync()
+    assert np.array_equal(host(evals), np.concatenate([O.mle_evaluate(m, nv, d, point) for m in mz]))
 
 
 def test_linearization_prove_lin_matches_unsplit_at_size(ctx):
