@@ -73,6 +73,8 @@ struct lf_ctx {
   size_t ptrs_elems = 0;
   int *sel = nullptr;           // lf_dev_mz_mles_sel: the selected matrices
   size_t sel_elems = 0;
+  uint64_t *hmsg = nullptr;     // pinned host staging of the sumcheck round messages
+  size_t hmsg_elems = 0;
   lfk::FoldRows fold_rows{};    // a step without f_k buffers: where its 2K planes sit in the operand rows
   bool fold_from_frag = false;
   bool frag_fallback = false;   // packed d = 1024 planes: fold_rows serve the not-short-rho fallback
@@ -303,6 +305,21 @@ int grow(lf_ctx *c, T *&buf, size_t &have, size_t need) {
   return LF_OK;
 }
 int reserve(lf_ctx *c, size_t elems) { return grow(c, c->scratch, c->scratch_elems, elems); }
+// a round message back through pinned memory (a pageable destination costs an extra
+// staging copy per round)
+int download_msg(lf_ctx *c, uint64_t *dst, const uint64_t *src, size_t elems) {
+  if (elems > c->hmsg_elems) {
+    if (c->hmsg) LF_HIP(c, hipHostFree(c->hmsg));
+    c->hmsg = nullptr;
+    c->hmsg_elems = 0;
+    LF_HIP(c, hipHostMalloc((void **)&c->hmsg, elems * 8, hipHostMallocDefault));
+    c->hmsg_elems = elems;
+  }
+  LF_HIP(c, hipMemcpyAsync(c->hmsg, src, elems * 8, hipMemcpyDeviceToHost, c->cur));
+  LF_HIP(c, hipStreamSynchronize(c->cur));
+  memcpy(dst, c->hmsg, elems * 8);
+  return LF_OK;
+}
 
 bool use_mfma(int d, size_t kappa) {
   // kappa > 32 LF_MAX_KTILES (A tiles of 32 rows): the VALU contraction (k_ajtai_phi72 / k_ajtai_nega)
@@ -915,6 +932,7 @@ void lf_ctx_destroy(lf_ctx *c) {
   if (c->sc) (void)hipFree(c->sc);
   if (c->ptrs) (void)hipFree(c->ptrs);
   if (c->sel) (void)hipFree(c->sel);
+  if (c->hmsg) (void)hipHostFree(c->hmsg);
   if (c->join) (void)hipEventDestroy(c->join);
   if (c->d_err) (void)hipFree(c->d_err);
   if (c->d_sync) (void)hipFree(c->d_sync);
@@ -1655,8 +1673,7 @@ static int sumcheck_run(lf_ctx *c, lf_transcript *t, const lf_comb *cb, const lf
       LF_HIP(c, lfk::round_folding(cur, stride, cb->nk * cb->tau, w, cb->bsmall, half, d, partial, ev, c->cur));
     else
       LF_HIP(c, lfk::round_lin(cur, stride, nm, cb->c, cs, degree, half, d, partial, ev, c->cur, cptrs));
-    LF_HIP(c, hipMemcpyAsync(msg, ev, (size_t)nev * d * 8, hipMemcpyDeviceToHost, c->cur));
-    LF_HIP(c, hipStreamSynchronize(c->cur));
+    LF_TRY(download_msg(c, msg, ev, (size_t)nev * d));
     // prover message absorbed, challenge sampled (fiat_shamir.rs:69-86; one sample for Fq) and absorbed
     lf_transcript_absorb_ring(t, msg, (size_t)nev, d, LF_REPR_CANONICAL);
     uint64_t *ch = randomness + (size_t)i * tb;
@@ -1782,8 +1799,7 @@ static int sumcheck_run_lin(lf_ctx *c, lf_transcript *t, const lf_comb *cb, cons
     const size_t half = n >> (i + 1);
     uint64_t *msg = proof + (size_t)i * nev * d;
     LF_HIP(c, lfk::round_lin_eq(cur, stride, E, cb->c, cs, degree, half, d, partial, qd, c->cur, cptrs));
-    LF_HIP(c, hipMemcpyAsync(qh.data(), qd, (size_t)nq * d * 8, hipMemcpyDeviceToHost, c->cur));
-    LF_HIP(c, hipStreamSynchronize(c->cur));
+    LF_TRY(download_msg(c, qh.data(), qd, (size_t)nq * d));
     const uint64_t *be = beta + (size_t)i * d;  // slot 0 holds the base-ring value
     for (int e = 0; e < nev; e++) {
       uint64_t x[3] = {(uint64_t)e, 0, 0}, ev[3], f[3];

@@ -475,6 +475,41 @@ __global__ void __launch_bounds__(RT) k_round_lin_eq(const uint64_t *mles, size_
                         partial + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * NQ * d);
 }
 
+// The same sums for rounds with few points (late rounds): one thread per (point, slot,
+// multiset chunk, evaluation point e), so a thread multiplies |S_i| + 1 values instead
+// of walking all NQ points of a multiset (the chain of dependent products, not the
+// work, bounds those rounds). partial[(chunk gx + x) NQ + e][slot]
+template <int TB>
+__global__ void __launch_bounds__(RT) k_round_lin_eq_pt(const uint64_t *mles, size_t stride,
+                                                        const uint64_t *const *ptrs, const uint64_t *E,
+                                                        const uint64_t *c, CombS cs, size_t half, int d, int spb,
+                                                        int nq, uint64_t *partial) {
+  const int slot_l = threadIdx.x % spb, lane_p = threadIdx.x / spb, ppb = RT / spb;
+  const int slot = blockIdx.y * spb + slot_l;
+  const int e = blockIdx.z % nq, chunk = blockIdx.z / nq, nchunk = gridDim.z / nq;
+  const int i0 = (int)((long)cs.q * chunk / nchunk), i1 = (int)((long)cs.q * (chunk + 1) / nchunk);
+  Sv<TB> acc[1];
+  acc[0] = s_zero<TB>();
+  for (size_t b = (size_t)blockIdx.x * ppb + lane_p; b < half; b += (size_t)gridDim.x * ppb) {
+    const size_t pofs = 2 * b * d + slot * TB;
+    Sv<TB> sum = s_zero<TB>();
+    for (int i = i0; i < i1; i++) {
+      Sv<TB> term = s_load<TB>(c + (size_t)i * d + slot * TB);
+      for (int f = cs.off[i]; f < cs.off[i + 1]; f++) {
+        const int m = cs.idx[f];
+        const uint64_t *p = (ptrs ? ptrs[m] : mles + (size_t)m * stride) + pofs;
+        const Sv<TB> a = s_load<TB>(p);
+        const Sv<TB> x = s_add(a, s_smul(s_sub(s_load<TB>(p + d), a), (uint64_t)e));  // a + e (b - a)
+        term = s_mul(term, x);
+      }
+      sum = s_add(sum, term);
+    }
+    acc[0] = s_add(acc[0], s_mul(sum, s_load<TB>(E + b * d + slot * TB)));
+  }
+  block_partial<TB, 1>(acc, spb, ppb, slot, lane_p, d,
+                       partial + (((size_t)chunk * gridDim.x + blockIdx.x) * nq + e) * d);
+}
+
 // E_next[b] = E[2b] + E[2b + 1]: eq over one variable fewer (eq(beta, 0) + eq(beta, 1) = 1)
 __global__ void k_pair_sum(const uint64_t *in, size_t half, int d, uint64_t *out) {
   const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -594,6 +629,8 @@ hipError_t mle_fix_first(const uint64_t *in, size_t in_stride, int nm, size_t ha
 // when the points are too few to fill the chip (late rounds) -- the f_hat
 // MLEs split over up to `nf` chunks (grid.z)
 constexpr size_t FILL_THREADS = (size_t)1 << 18;
+// at or below this many (point, slot) threads the linearization round runs per evaluation point
+constexpr size_t PT_THREADS = (size_t)1 << 13;
 static void round_geom(int d, size_t half, int nf, int &spb, dim3 &grid) {
   const int ns = d / slot_words(d);
   spb = ns < RT ? ns : RT;
@@ -699,6 +736,21 @@ hipError_t round_lin_eq(const uint64_t *mles, size_t stride, const uint64_t *E, 
   int spb;
   dim3 grid;
   round_geom(d, half, cs.q, spb, grid);
+  if (half * (size_t)(d / slot_words(d)) <= PT_THREADS) {  // few points: a thread per (point, slot, chunk, e)
+    const dim3 g2(grid.x, grid.y, grid.z * degree);
+    if (slot_words(d) == 3)
+      hipLaunchKernelGGL(k_round_lin_eq_pt<3>, g2, dim3(RT), 0, st, mles, stride, ptrs, E, c, cs, half, d, spb, degree,
+                         partial);
+    else
+      hipLaunchKernelGGL(k_round_lin_eq_pt<1>, g2, dim3(RT), 0, st, mles, stride, ptrs, E, c, cs, half, d, spb, degree,
+                         partial);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const size_t len = (size_t)degree * d;
+    hipLaunchKernelGGL(k_sum_partials, dim3((unsigned)len), dim3(256), 0, st, partial, (int)(grid.x * grid.z), len,
+                       evals);
+    return hipGetLastError();
+  }
 #define LF_RLE(TB, NQ)                                                                                      \
   hipLaunchKernelGGL((k_round_lin_eq<TB, NQ>), grid, dim3(RT), 0, st, mles, stride, ptrs, E, c, cs, half, d, spb, \
                      partial)
