@@ -406,6 +406,17 @@ int lf_sumcheck_prove(lf_ctx *ctx, lf_transcript *t, const lf_comb *comb, uint64
  * the later rounds (the linearization sumcheck reads its Mz MLEs in place) */
 int lf_sumcheck_prove_ptrs(lf_ctx *ctx, lf_transcript *t, const lf_comb *comb, const uint64_t *const *mles, int nm,
                            int nv, int d, int degree, uint64_t *work, uint64_t *proof, uint64_t *randomness);
+/* the folding sumcheck (folding.rs:42-130 over folding/utils.rs:196-331, B_SMALL = 2) with
+ * its 2K tau f_hat MLEs given as the decomposed witnesses' digit coefficient rows (fc0: the
+ * K witnesses of side 0, fc1 of side 1, wstride u64 apart, N elements each; every value
+ * 0, 1 or -1, as the decomposition guarantees) instead of materialised MLEs: mles5 holds
+ * the 5 general MLEs [eq(r_0), g1, eq(r_1), g3, eq(beta)] (2^nv elements each); round 0
+ * runs on the digits, the later rounds on the fixed MLEs in work (5 + 2K tau MLEs of
+ * 2^(nv-2) elements) and the context scratch. The proof and randomness of lf_sumcheck_prove
+ * over the materialised list. */
+int lf_sumcheck_prove_fold_digits(lf_ctx *ctx, lf_transcript *t, const lf_comb *comb, const uint64_t *mles5,
+                                  const uint64_t *fc0, const uint64_t *fc1, int K, size_t N, size_t wstride, int nv,
+                                  int d, uint64_t *work, uint64_t *proof, uint64_t *randomness);
 /* the linearization sumcheck (LFLinearizationProver::prove's, linearization.rs:153-197
  * over linearization/utils.rs:63-104) with eq(beta) given by beta itself: the proof and
  * randomness of lf_sumcheck_prove over [mles..., eq(beta)] (same transcript), with

@@ -329,6 +329,19 @@ class Context:
                                               degree, _ptr(proof), _ptr(rnd)))
         return proof, rnd
 
+    def sumcheck_prove_fold_digits(self, transcript: "Poseidon2Transcript", comb: "Comb", mles5, fc0, fc1, K: int,
+                                   N: int, wstride: int, nv: int, d: int, work):
+        """the folding sumcheck with its f_hat MLEs as digit coefficient rows
+        (lf_sumcheck_prove_fold_digits): the proof and randomness of sumcheck_prove over
+        [mles5..., get_fhat of the 2K witnesses]"""
+        tau = 3 if d == 24 else 1
+        proof = np.zeros(nv * 5 * d, np.uint64)
+        rnd = np.zeros(nv * tau, np.uint64)
+        self.check(self.lib.lf_sumcheck_prove_fold_digits(self.h, transcript.h, C.byref(comb.s), _dptr(mles5), _dptr(fc0),
+                                                          _dptr(fc1), K, N, wstride, nv, d, _dptr(work), _ptr(proof),
+                                                          _ptr(rnd)))
+        return proof, rnd
+
     def sumcheck_prove_lin(self, transcript: "Poseidon2Transcript", comb: "Comb", mles, nv: int, d: int,
                            degree: int, beta, work, evals=None):
         """the linearization sumcheck with eq(beta) split off (lf_sumcheck_prove_lin): mles a

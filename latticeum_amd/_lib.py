@@ -216,6 +216,7 @@ SIGNATURES = {
     "lf_sumcheck_prove": (I, [VP, VP, C.POINTER(LfComb), VP, I, I, I, I, VP, VP]),
     "lf_sumcheck_prove_ptrs": (I, [VP, VP, C.POINTER(LfComb), VP, I, I, I, I, VP, VP, VP]),
     "lf_sumcheck_prove_lin": (I, [VP, VP, C.POINTER(LfComb), VP, I, I, I, I, VP, VP, VP, VP, VP]),
+    "lf_sumcheck_prove_fold_digits": (I, [VP, VP, C.POINTER(LfComb), VP, VP, VP, I, SZ, SZ, I, I, VP, VP, VP]),
     "lf_fold_lcccs": (I, [VP, I, I, VP, VP, VP, SZ, VP, SZ, VP, VP, VP, VP, I]),
     "lf_dev_fold_lcccs": (I, [VP, I, I, VP, VP, VP, SZ, VP, SZ, VP, VP, VP, VP]),
     "lf_compute_x_s": (I, [VP, C.POINTER(LfParams), VP, SZ, VP, I]),

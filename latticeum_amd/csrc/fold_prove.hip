@@ -598,8 +598,10 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
   // absorb loop measured 1.2 ms slower: the host then waits on the queue mid-hash)
   enqueue_side(0);
   enqueue_side(1);
-  for (int sd = 0; sd < 2; sd++)
-    R.hip(lfk::get_fhat(P->fkc[sd], N, d, s, M + (5 + (size_t)sd * K * tau) * mstride, R.st, K, ND), "f_hat");
+  const bool digits = P->pr.b_small == 2;  // f_hat values in {-1, 0, 1}: read from the coefficient rows
+  if (!digits)
+    for (int sd = 0; sd < 2; sd++)
+      R.hip(lfk::get_fhat(P->fkc[sd], N, d, s, M + (5 + (size_t)sd * K * tau) * mstride, R.st, K, ND), "f_hat");
   if (R.rc) return R.rc;
   R.mark(LF_SPAN_DECOMPOSITION, false);
   for (int side = 0; side < 2; side++)
@@ -647,12 +649,18 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
     R.h2d(P->coef[side], cf.data(), cf.size());
   }
   // the MLEs [eq(r_0), g1, eq(r_1), g3, eq(beta), f_hat (2K x tau)] (create_sumcheck_polynomial,
-  // :196-255); the f_hat MLEs and eq(r_i) were enqueued before the decomposition transcript
+  // :196-255): eq(r_i) were enqueued before the decomposition transcript; the f_hat MLEs
+  // (Witness::get_fhat of the decomposed witnesses) are not materialised for B_SMALL = 2 --
+  // their values are the digits of the coefficient rows P->fkc, which g1 / g3 and the
+  // sumcheck's first round read directly (lf_sumcheck_prove_fold_digits)
   for (int side = 0; side < 2; side++) {
     uint64_t *g = M + (size_t)(2 * side + 1) * mstride;
     R.check(lf_dev_mz_challenged(C, P->ccs, P->zdec[side], P->zeta + (size_t)side * K * d, K, s, g), "challenged Mz");
-    R.check(lf_dev_mle_lincomb(C, d, M + (5 + (size_t)side * K * tau) * mstride, mstride, K * tau, s, P->coef[side], g),
-            "g");
+    if (digits)
+      R.hip(lfk::fhat_lincomb_digits(P->fkc[side], K, N, ND, P->coef[side], s, d, g, R.st), "g");
+    else
+      R.check(lf_dev_mle_lincomb(C, d, M + (5 + (size_t)side * K * tau) * mstride, mstride, K * tau, s, P->coef[side], g),
+              "g");
   }
   R.check(lf_dev_eq_table(C, d, P->beta, s, M + 4 * mstride), "eq(beta)");
   std::vector<uint64_t> rnd((size_t)s * tb);
@@ -665,7 +673,10 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
     cb.bsmall = (int)P->pr.b_small;
     cb.mu = P->mu;
     if (R.rc == LF_OK)
-      R.check(lf_sumcheck_prove(C, R.T, &cb, M, P->nm_fold, s, d, 2 * cb.bsmall, proof->fold_sumcheck, rnd.data()),
+      R.check(digits
+                  ? lf_sumcheck_prove_fold_digits(C, R.T, &cb, M, P->fkc[0], P->fkc[1], K, N, ND, s, d, M + 5 * mstride,
+                                                  proof->fold_sumcheck, rnd.data())
+                  : lf_sumcheck_prove(C, R.T, &cb, M, P->nm_fold, s, d, 2 * cb.bsmall, proof->fold_sumcheck, rnd.data()),
               "folding sumcheck");
   }
   if (R.rc) return R.rc;

@@ -248,6 +248,19 @@ hipError_t fold_weights(const uint64_t *mu, int nk, int tau, int d, uint64_t *w,
 // mles: 5 + nf MLEs at stride u64 apart; w: nf Horner weights
 hipError_t round_folding(const uint64_t *mles, size_t stride, int nf, const uint64_t *w, int bsmall, size_t half, int d,
                          uint64_t *partial, uint64_t *evals, hipStream_t st);
+// the folding round 0 (b_small = 2) with the 2K tau f_hat MLEs given by digit coefficient
+// rows (fc0: the K witnesses of side 0, fc1 of side 1, wstride u64 apart, N elements):
+// mles holds only the 5 general MLEs; evals [5][d]
+hipError_t round_folding0_digits(const uint64_t *mles, size_t stride, const uint64_t *fc0, const uint64_t *fc1, int K,
+                                size_t N, size_t wstride, int nf, const uint64_t *w, size_t half, int d,
+                                uint64_t *partial, uint64_t *evals, hipStream_t st);
+// those f_hat MLEs fixed by the first challenge (out: nf MLEs of half elements, out_stride apart)
+hipError_t fix_fhat_digits(const uint64_t *fc0, const uint64_t *fc1, int K, size_t N, size_t wstride, int nf,
+                           size_t half, int d, const uint64_t *r_base, uint64_t *out, size_t out_stride,
+                           hipStream_t st);
+// io[x] += sum_(k, j) coef[k tau + j] fhat_(k, j)[x] for the nw digit witnesses of fc (2^nv points)
+hipError_t fhat_lincomb_digits(const uint64_t *fc, int nw, size_t N, size_t wstride, const uint64_t *coef, int nv,
+                               int d, uint64_t *io, hipStream_t st);
 hipError_t round_lin(const uint64_t *mles, size_t stride, int nm, const uint64_t *c, const CombS &cs, int degree,
                      size_t half, int d, uint64_t *partial, uint64_t *evals, hipStream_t st,
                      const uint64_t *const *ptrs = nullptr);

@@ -1641,9 +1641,15 @@ int lf_dev_sumcheck_round(lf_ctx *c, const lf_comb *cb, const uint64_t *mles, si
 // `mles` (stride 2^nv d) or, with ptrs (device array of nm pointers), wherever
 // those point; every round fixes them into the next buffer: the context scratch
 // (2^(nv-1) points) and `alt` (2^(nv-2) points; the input itself when ptrs is null)
+// the folding polynomial's f_hat MLEs as digit coefficient rows (lf_sumcheck_prove_fold_digits)
+struct DigitFhat {
+  const uint64_t *fc0, *fc1;
+  int K;
+  size_t N, wstride;
+};
 static int sumcheck_run(lf_ctx *c, lf_transcript *t, const lf_comb *cb, const lfk::CombS &cs, const uint64_t *mles,
                         const uint64_t *const *ptrs, uint64_t *alt, int nm, int nv, int d, int degree, uint64_t *proof,
-                        uint64_t *randomness) {
+                        uint64_t *randomness, const DigitFhat *dg = nullptr) {
   const int tb = lfk::slot_words(d), nev = degree + 1;
   const size_t n = (size_t)1 << nv;
   // scratch: the MLEs fixed by the first challenge, the round's partial sums, the
@@ -1669,7 +1675,10 @@ static int sumcheck_run(lf_ctx *c, lf_transcript *t, const lf_comb *cb, const lf
   for (int i = 0; i < nv; i++) {
     const size_t half = n >> (i + 1);
     uint64_t *msg = proof + (size_t)i * nev * d;
-    if (cb->kind == LF_COMB_FOLDING)
+    if (dg && i == 0)  // round 0 straight from the digits (cur: the 5 general MLEs)
+      LF_HIP(c, lfk::round_folding0_digits(cur, stride, dg->fc0, dg->fc1, dg->K, dg->N, dg->wstride, cb->nk * cb->tau, w,
+                                           half, d, partial, ev, c->cur));
+    else if (cb->kind == LF_COMB_FOLDING)
       LF_HIP(c, lfk::round_folding(cur, stride, cb->nk * cb->tau, w, cb->bsmall, half, d, partial, ev, c->cur));
     else
       LF_HIP(c, lfk::round_lin(cur, stride, nm, cb->c, cs, degree, half, d, partial, ev, c->cur, cptrs));
@@ -1688,13 +1697,36 @@ static int sumcheck_run(lf_ctx *c, lf_transcript *t, const lf_comb *cb, const lf
     // fix_variables(r) of every MLE (prover.rs:75-78), into the other buffer
     if (half >= 1 && i + 1 < nv) {
       uint64_t *dst = (i % 2 == 0) ? buf : alt;
-      LF_HIP(c, lfk::mle_fix_first(cur, stride, nm, half, d, ch, dst, half * d, c->cur, cptrs));
+      if (dg && i == 0) {  // the 5 general MLEs, then the f_hat ones from the digits
+        LF_HIP(c, lfk::mle_fix_first(cur, stride, 5, half, d, ch, dst, half * d, c->cur, cptrs));
+        LF_HIP(c, lfk::fix_fhat_digits(dg->fc0, dg->fc1, dg->K, dg->N, dg->wstride, nm - 5, half, d, ch,
+                                       dst + 5 * half * d, half * d, c->cur));
+      } else {
+        LF_HIP(c, lfk::mle_fix_first(cur, stride, nm, half, d, ch, dst, half * d, c->cur, cptrs));
+      }
       cur = dst;
       cptrs = nullptr;
       stride = half * d;
     }
   }
   return LF_OK;
+}
+
+int lf_sumcheck_prove_fold_digits(lf_ctx *c, lf_transcript *t, const lf_comb *cb, const uint64_t *mles5,
+                                  const uint64_t *fc0, const uint64_t *fc1, int K, size_t N, size_t wstride, int nv,
+                                  int d, uint64_t *work, uint64_t *proof, uint64_t *randomness) {
+  if (!c || !t || !cb || !mles5 || !fc0 || !fc1 || !work || !proof || !randomness || nv < 1 || K < 1)
+    return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  const int tau = d == 24 ? 3 : 1;
+  if (cb->kind != LF_COMB_FOLDING || cb->bsmall != 2 || cb->nk != 2 * K || cb->tau != tau || N > ((size_t)1 << nv))
+    return fail(c, LF_ERR_INVALID_ARG, "fold_digits: a folding combination with B_SMALL = 2 over 2K witnesses");
+  lfk::CombS cs;
+  const int nm = 5 + cb->nk * cb->tau;
+  LF_TRY(comb_check(c, cb, nm, d, 4, &cs));
+  const DigitFhat dg{fc0, fc1, K, N, wstride};
+  return sumcheck_run(c, t, cb, cs, mles5, nullptr, work, nm, nv, d, 4, proof, randomness, &dg);
 }
 
 int lf_sumcheck_prove(lf_ctx *c, lf_transcript *t, const lf_comb *cb, uint64_t *mles, int nm, int nv, int d,

@@ -187,6 +187,164 @@ __global__ void __launch_bounds__(RT) k_round_folding(const uint64_t *mles, size
                                 partial + ((size_t)chunk * gridDim.x + blockIdx.x) * (degree + 1) * d);
 }
 
+// ---------------------------------------------------------------- folding round 0 on digits
+// In lf_fold_prove the folding polynomial's f_hat MLEs are Witness::get_fhat of the
+// decomposed witnesses, whose coefficients are balanced base-2 digits (b_small = 2):
+// every f_hat value of round 0 is 0, 1 or -1. On the line f(e) = a + e dd with a, a + dd
+// in {-1, 0, 1}, g(f) = f^3 - f is the cubic C1 e + C2 e^2 + C3 e^3 (C0 = a^3 - a = 0)
+// with C1 = (3 a^2 - 1) dd, C2 = 3 a dd^2, C3 = dd^3, small integers, so
+// S(e) = sum_f w_f g(f(e)) = A1 e + A2 e^2 + A3 e^3 with A_k = sum_f C_k(f) w_f: three
+// small-integer multiply-accumulates of the weight per value instead of four Fq3
+// products and four lazy Fq3 products, read straight from the coefficient rows (no
+// f_hat MLEs). The same field elements as k_round_folding<TB, 2> on the materialised
+// MLEs. C + 12 is non-negative, so A_k = sum_f (C_k + 12) w_f - 12 W, W = sum_f w_f.
+struct SmallAcc {  // sum of u64 x small (< 2^32): lo + 2^64 c + 2^32 mid
+  uint64_t lo, mid;
+  uint32_t c;
+};
+__device__ __forceinline__ void small_mad(SmallAcc &a, uint64_t x, uint32_t k) {
+  uint64_t t;
+  a.c += gl::addc64(a.lo, (uint64_t)(uint32_t)x * k, t);
+  a.lo = t;
+  a.mid += (x >> 32) * k;
+}
+__device__ __forceinline__ uint64_t small_final(const SmallAcc &a) {
+  gl::CAcc x;
+  gl::cacc_zero(x);
+  x.s0 = a.lo;
+  x.c0 = a.c;
+  x.s1 = a.mid;
+  return gl::cacc_reduce(x);
+}
+__device__ __forceinline__ int digit_of(uint64_t v) { return v == 0 ? 0 : (v == 1 ? 1 : -1); }
+
+// f_hat value (w, j) at point x, slot: f_coeff_w[x][j ns + slot] (zero past N)
+template <int TB>
+__global__ void __launch_bounds__(RT) k_round_folding0_digits(const uint64_t *mles, size_t stride,
+                                                              const uint64_t *fc0, const uint64_t *fc1, int K,
+                                                              size_t N, size_t wstride, int nf, const uint64_t *w,
+                                                              size_t half, int d, int spb, uint64_t *partial) {
+  constexpr int tau = TB == 3 ? 3 : 1;
+  const int slot_l = threadIdx.x % spb, lane_p = threadIdx.x / spb, ppb = RT / spb;
+  const int slot = blockIdx.y * spb + slot_l, ns = d / TB;
+  const int chunk = blockIdx.z, nchunk = gridDim.z;
+  const int f0 = (int)((long)nf * chunk / nchunk), f1 = (int)((long)nf * (chunk + 1) / nchunk);
+  constexpr int degree = 4;
+  Sv<TB> acc[degree + 1];
+#pragma unroll
+  for (int e = 0; e <= degree; e++) acc[e] = s_zero<TB>();
+  // 12 W over this chunk's weights (the offset's correction, the same at every point)
+  Sv<TB> w12 = s_zero<TB>();
+  for (int f = f0; f < f1; f++) w12 = s_add(w12, s_load<TB>(w + (size_t)f * d + slot * TB));
+  w12 = s_smul(w12, 12);
+  for (size_t b = (size_t)blockIdx.x * ppb + lane_p; b < half; b += (size_t)gridDim.x * ppb) {
+    const size_t x0 = 2 * b;
+    SmallAcc A[3][TB];
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+#pragma unroll
+      for (int q = 0; q < TB; q++) A[k][q] = SmallAcc{0, 0, 0};
+    for (int f = f0; f < f1; f++) {
+      const int kg = f / tau, j = f - kg * tau;
+      const uint64_t *fc = (kg < K ? fc0 + (size_t)kg * wstride : fc1 + (size_t)(kg - K) * wstride) + (size_t)j * ns + slot;
+      const int a = x0 < N ? digit_of(fc[x0 * d]) : 0;
+      const int bv = x0 + 1 < N ? digit_of(fc[(x0 + 1) * d]) : 0;
+      const int dd = bv - a;
+      const uint32_t c1 = (uint32_t)((3 * a * a - 1) * dd + 12), c2 = (uint32_t)(3 * a * dd * dd + 12),
+                     c3 = (uint32_t)(dd * dd * dd + 12);
+      const Sv<TB> wf = s_load<TB>(w + (size_t)f * d + slot * TB);
+#pragma unroll
+      for (int q = 0; q < TB; q++) {
+        small_mad(A[0][q], wf.c[q], c1);
+        small_mad(A[1][q], wf.c[q], c2);
+        small_mad(A[2][q], wf.c[q], c3);
+      }
+    }
+    Sv<TB> Ak[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+#pragma unroll
+      for (int q = 0; q < TB; q++) Ak[k].c[q] = small_final(A[k][q]);
+      Ak[k] = s_sub(Ak[k], w12);
+    }
+    const uint64_t *pb = mles + 2 * b * d + slot * TB;
+    Sv<TB> v[5], sv[5];
+#pragma unroll
+    for (int m = 0; m < 5; m++) {
+      const uint64_t *p = pb + (size_t)m * stride;
+      v[m] = s_load<TB>(p);
+      sv[m] = s_sub(s_load<TB>(p + d), v[m]);
+    }
+#pragma unroll
+    for (int e = 0; e <= degree; e++) {
+      // S(e) = ((A3 e + A2) e + A1) e
+      const Sv<TB> S = s_smul(s_add(s_smul(s_add(s_smul(Ak[2], e), Ak[1]), e), Ak[0]), e);
+      Sv<TB> t = s_mul(v[4], S);
+      if (chunk == 0) t = s_add(t, s_add(s_mul(v[0], v[1]), s_mul(v[2], v[3])));
+      acc[e] = s_add(acc[e], t);
+#pragma unroll
+      for (int m = 0; m < 5; m++) v[m] = s_add(v[m], sv[m]);
+    }
+  }
+  block_partial<TB, degree + 1>(acc, spb, ppb, slot, lane_p, d,
+                                partial + ((size_t)chunk * gridDim.x + blockIdx.x) * (degree + 1) * d);
+}
+
+// the f_hat MLEs fixed by the first challenge r, from the digits: out[f][b] =
+// a + r (b - a) (a base-ring digit plus r times a small integer), f = (k, j) as above
+template <int TB>
+__global__ void k_fix_fhat_digits(const uint64_t *fc0, const uint64_t *fc1, int K, size_t N, size_t wstride, int nf,
+                                  size_t half, int d, Sv<TB> r, uint64_t *out, size_t out_stride) {
+  constexpr int tau = TB == 3 ? 3 : 1;
+  const int ns = d / TB;
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // (f, b, slot)
+  if (i >= (size_t)nf * half * ns) return;
+  const size_t fb = i / ns;
+  const int s = (int)(i - fb * ns);
+  const int f = (int)(fb / half);
+  const size_t b = fb - (size_t)f * half, x0 = 2 * b;
+  const int kg = f / tau, j = f - kg * tau;
+  const uint64_t *fc = (kg < K ? fc0 + (size_t)kg * wstride : fc1 + (size_t)(kg - K) * wstride) + (size_t)j * ns + s;
+  const int a = x0 < N ? digit_of(fc[x0 * d]) : 0;
+  const int bv = x0 + 1 < N ? digit_of(fc[(x0 + 1) * d]) : 0;
+  const int dd = bv - a;
+  Sv<TB> o;
+#pragma unroll
+  for (int q = 0; q < TB; q++) {
+    const uint64_t m = gl::mul(r.c[q], (uint64_t)(dd < 0 ? -dd : dd));
+    o.c[q] = dd < 0 ? gl::neg(m) : m;
+  }
+  o.c[0] = gl::add(o.c[0], a < 0 ? gl::P - 1 : (uint64_t)a);
+  s_store(out + (size_t)f * out_stride + b * d + s * TB, o);
+}
+
+// io[x] += sum_(k, j) coef[k tau + j] fhat_(k, j)[x] from the digits (x < npts)
+template <int TB>
+__global__ void k_fhat_lincomb_digits(const uint64_t *fc, int nw, size_t N, size_t wstride, const uint64_t *coef,
+                                      size_t npts, int d, uint64_t *io) {
+  constexpr int tau = TB == 3 ? 3 : 1;
+  const int ns = d / TB;
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= npts * ns) return;
+  const size_t x = i / ns;
+  const int s = (int)(i - x * ns);
+  Sv<TB> pos = s_zero<TB>(), neg = s_zero<TB>();
+  if (x < N)
+    for (int k = 0; k < nw; k++)
+      for (int j = 0; j < tau; j++) {
+        const int a = digit_of(fc[(size_t)k * wstride + x * d + (size_t)j * ns + s]);
+        if (a) {
+          const Sv<TB> cf = s_load<TB>(coef + (size_t)(k * tau + j) * d + s * TB);
+          if (a > 0)
+            pos = s_add(pos, cf);
+          else
+            neg = s_add(neg, cf);
+        }
+      }
+  uint64_t *o = io + x * d + s * TB;
+  s_store(o, s_add(s_load<TB>(o), s_sub(pos, neg)));
+}
+
 // w_(k,dd) = mu_k^(dd+1), the Horner weights of the folding combination
 template <int TB>
 __global__ void k_fold_weights(const uint64_t *mu, int nk, int tau, int d, uint64_t *w) {
@@ -690,6 +848,59 @@ hipError_t round_folding(const uint64_t *mles, size_t stride, int nf, const uint
   const size_t len = (size_t)(2 * bsmall + 1) * d;
   hipLaunchKernelGGL(k_sum_partials, dim3((unsigned)len), dim3(256), 0, st, partial, (int)(grid.x * grid.z), len,
                      evals);
+  return hipGetLastError();
+}
+
+hipError_t round_folding0_digits(const uint64_t *mles, size_t stride, const uint64_t *fc0, const uint64_t *fc1, int K,
+                                size_t N, size_t wstride, int nf, const uint64_t *w, size_t half, int d,
+                                uint64_t *partial, uint64_t *evals, hipStream_t st) {
+  if (!half) return hipErrorInvalidValue;
+  int spb;
+  dim3 grid;
+  round_geom(d, half, nf, spb, grid);
+  if (slot_words(d) == 3)
+    hipLaunchKernelGGL(k_round_folding0_digits<3>, grid, dim3(RT), 0, st, mles, stride, fc0, fc1, K, N, wstride, nf, w,
+                       half, d, spb, partial);
+  else
+    hipLaunchKernelGGL(k_round_folding0_digits<1>, grid, dim3(RT), 0, st, mles, stride, fc0, fc1, K, N, wstride, nf, w,
+                       half, d, spb, partial);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const size_t len = (size_t)5 * d;
+  hipLaunchKernelGGL(k_sum_partials, dim3((unsigned)len), dim3(256), 0, st, partial, (int)(grid.x * grid.z), len,
+                     evals);
+  return hipGetLastError();
+}
+
+hipError_t fix_fhat_digits(const uint64_t *fc0, const uint64_t *fc1, int K, size_t N, size_t wstride, int nf,
+                           size_t half, int d, const uint64_t *r_base, uint64_t *out, size_t out_stride,
+                           hipStream_t st) {
+  const int tb = slot_words(d);
+  const size_t n = (size_t)nf * half * (d / tb);
+  if (!n) return hipSuccess;
+  if (tb == 3) {
+    Sv<3> r;
+    for (int i = 0; i < 3; i++) r.c[i] = r_base[i];
+    hipLaunchKernelGGL(k_fix_fhat_digits<3>, dim3(blocks_of(n, 256)), dim3(256), 0, st, fc0, fc1, K, N, wstride, nf,
+                       half, d, r, out, out_stride);
+  } else {
+    Sv<1> r;
+    r.c[0] = r_base[0];
+    hipLaunchKernelGGL(k_fix_fhat_digits<1>, dim3(blocks_of(n, 256)), dim3(256), 0, st, fc0, fc1, K, N, wstride, nf,
+                       half, d, r, out, out_stride);
+  }
+  return hipGetLastError();
+}
+
+hipError_t fhat_lincomb_digits(const uint64_t *fc, int nw, size_t N, size_t wstride, const uint64_t *coef, int nv,
+                               int d, uint64_t *io, hipStream_t st) {
+  const size_t npts = (size_t)1 << nv, n = npts * (size_t)(d / slot_words(d));
+  if (slot_words(d) == 3)
+    hipLaunchKernelGGL(k_fhat_lincomb_digits<3>, dim3(blocks_of(n, 256)), dim3(256), 0, st, fc, nw, N, wstride, coef,
+                       npts, d, io);
+  else
+    hipLaunchKernelGGL(k_fhat_lincomb_digits<1>, dim3(blocks_of(n, 256)), dim3(256), 0, st, fc, nw, N, wstride, coef,
+                       npts, d, io);
   return hipGetLastError();
 }
 

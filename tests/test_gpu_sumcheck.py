@@ -227,3 +227,38 @@ def test_linearization_prove_lin_matches_unsplit_at_size(ctx):
     proof, rnd = ctx.sumcheck_prove_lin(LA.Poseidon2Transcript(), LA.Comb.linearization(dev(c), S),
                                         [mz[j * n * d:(j + 1) * n * d] for j in range(nmz)], nv, d, 8, beta, work)
     assert np.array_equal(proof, want_p) and np.array_equal(rnd, want_r)
+
+
+@pytest.mark.parametrize("d,nv,K,N", [(24, 6, 3, 50), (24, 9, 4, 512), (16, 5, 2, 30), (1024, 3, 2, 7)])
+def test_folding_prove_digits_matches_materialised(ctx, d, nv, K, N):
+    """lf_sumcheck_prove_fold_digits (round 0 and its fix read from the digit rows, no f_hat
+    MLEs) gives the proof of the prover over the materialised get_fhat MLEs; N < 2^nv and
+    N = 2^nv (zero padding and none)"""
+    import torch
+    tau = 3 if d == 24 else 1
+    n = 1 << nv
+    rng = np.random.default_rng(d * 7 + nv)
+
+    def digits():
+        x = rng.integers(-1, 2, N * d)
+        return np.where(x < 0, np.uint64(P - 1), x.astype(np.uint64))
+    fc0 = dev(np.concatenate([digits() for _ in range(K)]))
+    fc1 = dev(np.concatenate([digits() for _ in range(K)]))
+    gen = [rand(n * d, 1300 + d + i) for i in range(5)]
+    mu = rand(2 * K * d, 1310 + d)
+    nm = 5 + 2 * K * tau
+    full = dev(n=nm * n * d)
+    full[:5 * n * d] = dev(np.concatenate(gen))
+    for side, fc in enumerate((fc0, fc1)):
+        for k in range(K):
+            o = (5 + (side * K + k) * tau) * n * d
+            ctx.dev_get_fhat(d, fc[k * N * d:(k + 1) * N * d], N, nv, full[o:o + tau * n * d])
+    mles5 = full[:5 * n * d].clone()
+    want_p, want_r = ctx.sumcheck_prove(LA.Poseidon2Transcript(), LA.Comb.folding(dev(mu), 2 * K, tau, 2), full, nm, nv,
+                                        d, 4)
+    work = dev(n=nm * max(n // 4, 1) * d)
+    got_p, got_r = ctx.sumcheck_prove_fold_digits(LA.Poseidon2Transcript(), LA.Comb.folding(dev(mu), 2 * K, tau, 2),
+                                                  mles5, fc0, fc1, K, N, N * d, nv, d, work)
+    assert np.array_equal(got_p, want_p) and np.array_equal(got_r, want_r)
+    del full
+    torch.cuda.empty_cache()
