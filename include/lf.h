@@ -429,6 +429,17 @@ int lf_sumcheck_prove_fold_digits(lf_ctx *ctx, lf_transcript *t, const lf_comb *
 int lf_sumcheck_prove_lin(lf_ctx *ctx, lf_transcript *t, const lf_comb *comb, const uint64_t *const *mles, int nm,
                           int nv, int d, int degree, const uint64_t *beta, uint64_t *work, uint64_t *proof,
                           uint64_t *randomness, uint64_t *evals);
+/* lf_sumcheck_prove_lin whose first round visits, for multiset i, only the points
+ * act[act_off[i] .. act_off[i + 1]) (act: device uint32 point indices b < 2^(nv-1);
+ * act_off: host, q + 1 entries, act_off[0] = 0). The caller guarantees that at every
+ * other point b some factor of S_i is zero on both rows 2b and 2b + 1, so the term is
+ * zero at every evaluation point -- the zero short-cut of the reference's product
+ * (linearization/utils.rs:86-104), decided once from the CCS rows (lf_ccs_row_live)
+ * instead of per value. Same proof, randomness and evals as lf_sumcheck_prove_lin. */
+int lf_sumcheck_prove_lin_sparse(lf_ctx *ctx, lf_transcript *t, const lf_comb *comb, const uint64_t *const *mles,
+                                 int nm, int nv, int d, int degree, const uint64_t *beta, const uint32_t *act,
+                                 const uint32_t *act_off, uint64_t *work, uint64_t *proof, uint64_t *randomness,
+                                 uint64_t *evals);
 
 /* ------------------------------------------------------------ sparse Mz products
  * CCS.M (latticefold/src/arith.rs:51-74): t matrices m x n of ring elements,
@@ -575,6 +586,8 @@ int lf_ccs_set_structure(lf_ctx *ctx, lf_ccs *M, size_t l, int degree, int q, co
 int lf_ccs_shape(const lf_ccs *M, int *t, size_t *m, size_t *n, size_t *l, int *q, int *degree);
 int lf_ccs_get_structure(const lf_ccs *M, uint64_t *c, int *S_off, int *S_idx);
 const uint64_t *lf_ccs_c_device(const lf_ccs *M);
+/* out[r] = 1 if row r of M_j holds an entry (so MLE(M_j z) may be nonzero there), else 0; m bytes */
+int lf_ccs_row_live(const lf_ccs *M, int j, uint8_t *out);
 /* tracing spans of lf_fold_prove (the reference's #[instrument] spans): wall ms per
  * phase, summed over calls since timing was (re)set; each phase ends with a
  * stream sync while timing is on */

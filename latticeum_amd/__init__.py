@@ -358,6 +358,23 @@ class Context:
                                                   _dptr(evals) if evals is not None else None))
         return proof, rnd
 
+    def sumcheck_prove_lin_sparse(self, transcript: "Poseidon2Transcript", comb: "Comb", mles, nv: int, d: int,
+                                  degree: int, beta, act, act_off, work, evals=None):
+        """sumcheck_prove_lin with round 0 over each multiset's active points only
+        (lf_sumcheck_prove_lin_sparse): act a device int32 tensor of point indices,
+        act_off (host, q + 1) each multiset's range in it"""
+        tau = 3 if d == 24 else 1
+        proof = np.zeros(nv * (degree + 1) * d, np.uint64)
+        rnd = np.zeros(nv * tau, np.uint64)
+        ptrs = (C.c_void_p * len(mles))(*[_dptr(m) for m in mles])
+        b = _u64(beta)
+        off = np.ascontiguousarray(act_off, dtype=np.uint32)
+        self.check(self.lib.lf_sumcheck_prove_lin_sparse(self.h, transcript.h, C.byref(comb.s), ptrs, len(mles), nv,
+                                                         d, degree, _ptr(b), _dptr(act), off.ctypes.data,
+                                                         _dptr(work), _ptr(proof), _ptr(rnd),
+                                                         _dptr(evals) if evals is not None else None))
+        return proof, rnd
+
     # ---------------------------------------------------------------- width-8 Merkle trees
     def dev_poseidon2_w8_permute(self, t):
         self.check(self.lib.lf_dev_poseidon2_w8_permute(self.h, _dptr(t), t.numel() // 8))
@@ -497,6 +514,12 @@ class CCSMatrices:
         """the MLEs of the selected matrices only (lf_dev_mz_mles_sel): out[i] = MLE(M_sel[i] z)"""
         s = np.ascontiguousarray(np.asarray(sel, np.int32))
         self.ctx.check(self.lib.lf_dev_mz_mles_sel(self.ctx.h, self.h, _dptr(z), _ptr(s), len(s), nv, _dptr(out)))
+
+    def row_live(self, j: int, m: int):
+        """which rows of M_j hold an entry (lf_ccs_row_live): m bools"""
+        out = np.zeros(m, np.uint8)
+        self.ctx.check(self.lib.lf_ccs_row_live(self.h, j, out.ctypes.data))
+        return out.astype(bool)
 
     def mz_challenged(self, z, zeta, nz: int, nv: int, out):
         self.ctx.check(self.lib.lf_dev_mz_challenged(self.ctx.h, self.h, _dptr(z), _dptr(zeta), nz, nv, _dptr(out)))

@@ -175,6 +175,7 @@ SIGNATURES = {
     "lf_ccs_shape": (I, [VP, C.POINTER(I), C.POINTER(SZ), C.POINTER(SZ), C.POINTER(SZ), C.POINTER(I), C.POINTER(I)]),
     "lf_ccs_get_structure": (I, [VP, VP, VP, VP]),
     "lf_ccs_c_device": (VP, [VP]),
+    "lf_ccs_row_live": (I, [VP, I, VP]),
     "lf_prover_create": (I, [VP, VP, C.POINTER(LfParams), VP, C.POINTER(VP)]),
     "lf_prover_destroy": (None, [VP]),
     "lf_prover_last_error": (C.c_char_p, [VP]),
@@ -216,6 +217,7 @@ SIGNATURES = {
     "lf_sumcheck_prove": (I, [VP, VP, C.POINTER(LfComb), VP, I, I, I, I, VP, VP]),
     "lf_sumcheck_prove_ptrs": (I, [VP, VP, C.POINTER(LfComb), VP, I, I, I, I, VP, VP, VP]),
     "lf_sumcheck_prove_lin": (I, [VP, VP, C.POINTER(LfComb), VP, I, I, I, I, VP, VP, VP, VP, VP]),
+    "lf_sumcheck_prove_lin_sparse": (I, [VP, VP, C.POINTER(LfComb), VP, I, I, I, I, VP, VP, VP, VP, VP, VP, VP]),
     "lf_sumcheck_prove_fold_digits": (I, [VP, VP, C.POINTER(LfComb), VP, VP, VP, I, SZ, SZ, I, I, VP, VP, VP]),
     "lf_fold_lcccs": (I, [VP, I, I, VP, VP, VP, SZ, VP, SZ, VP, VP, VP, VP, I]),
     "lf_dev_fold_lcccs": (I, [VP, I, I, VP, VP, VP, SZ, VP, SZ, VP, VP, VP, VP]),

@@ -40,6 +40,11 @@ struct lf_prover {
   std::vector<int> mz_order, S_live;
   int nlive = 0;
   bool bad_S = false;
+  // the linearization's round-0 points per multiset: b is active for S_i when every
+  // factor's matrix has an entry in row 2b or 2b + 1 (lf_sumcheck_prove_lin_sparse);
+  // act_off [q + 1] into the device list act
+  std::vector<uint32_t> act_off, act_host;
+  uint32_t *act = nullptr;
   // device memory: one allocation, carved
   uint64_t *mem = nullptr;
   uint64_t *z = nullptr, *mz = nullptr, *lin = nullptr, *pt = nullptr, *beta = nullptr, *val = nullptr;
@@ -234,8 +239,8 @@ int linearize(lf_prover *P, Run &R, const lf_witness *w_i, uint64_t *lin_sumchec
     cb.S_off = P->S_off.data();
     cb.S_idx = P->S_live.data();
     if (R.rc == LF_OK)
-      R.check(lf_sumcheck_prove_lin(C, R.T, &cb, ptr.data(), nlive, s, d, P->degree + 1, beta.data(), P->lin,
-                                    lin_sumcheck, rnd.data(), P->lev),
+      R.check(lf_sumcheck_prove_lin_sparse(C, R.T, &cb, ptr.data(), nlive, s, d, P->degree + 1, beta.data(), P->act,
+                                           P->act_off.data(), P->lin, lin_sumcheck, rnd.data(), P->lev),
               "linearization sumcheck");
   }
   if (R.rc) return R.rc;
@@ -355,6 +360,27 @@ int lf_prover_create(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, const
     for (int j = 0; j < t; j++)
       if (pos_of[j] < 0) P->mz_order.push_back(j);
   }
+  if (!P->bad_S) {
+    const size_t half = m / 2;
+    std::vector<uint8_t> row(m);
+    std::vector<std::vector<uint8_t>> pair(P->nlive, std::vector<uint8_t>(half));
+    for (int i = 0; i < P->nlive; i++) {
+      lf_ccs_row_live(ccs, P->mz_order[i], row.data());
+      for (size_t b = 0; b < half; b++) pair[i][b] = row[2 * b] | row[2 * b + 1];
+    }
+    P->act_off.assign(q + 1, 0);
+    for (int i = 0; i < q; i++) {
+      bool zero = true;  // c_i = 0: no active point
+      for (int k = 0; k < d; k++) zero &= P->c[(size_t)i * d + k] == 0;
+      if (!zero)
+        for (size_t b = 0; b < half; b++) {
+          bool on = true;
+          for (int k = P->S_off[i]; k < P->S_off[i + 1] && on; k++) on = pair[P->S_live[k]][b];
+          if (on) P->act_host.push_back((uint32_t)b);
+        }
+      P->act_off[i + 1] = (uint32_t)P->act_host.size();
+    }
+  }
   P->nm_fold = 5 + 2 * P->K * P->tau;
   // device memory, carved from one allocation
   const size_t K = P->K, N = P->N, W = P->W, nn = P->nn, kd = P->kappa * d, tau = P->tau;
@@ -373,7 +399,8 @@ int lf_prover_create(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, const
       {&P->coef[0], K * tau * d}, {&P->coef[1], K * tau * d}, {&P->zeta, 2 * K * d}, {&P->mu, 2 * K * d},
       {&P->theta, 2 * K * tau * d}, {&P->eta, 2 * K * t * d}, {&P->rho, 2 * K * d}, {&P->rhoc, 2 * K * d},
       {&P->cm0, kd}, {&P->u0, (size_t)t * d}, {&P->x0, (l + 1) * d}, {&P->v0, tau * d}, {&P->r0, (size_t)P->s * d},
-      {&P->eq0, nn * d}, {&P->mzw, lf_ccs_weights_len(ccs)}, {&P->lev, (size_t)t * d}};
+      {&P->eq0, nn * d}, {&P->mzw, lf_ccs_weights_len(ccs)}, {&P->lev, (size_t)t * d},
+      {reinterpret_cast<uint64_t **>(&P->act), (P->act_host.size() + 1) / 2}};
   size_t total = 0;
   for (auto &x : parts) total += (x.elems + 31) / 32 * 32;  // 256-B aligned parts
   int prev = -1;
@@ -389,6 +416,16 @@ int lf_prover_create(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, const
   for (auto &x : parts) {
     *x.p = P->mem + off;
     off += (x.elems + 31) / 32 * 32;
+  }
+  if (!P->act_host.empty()) {
+    if (hipGetDevice(&prev) == hipSuccess && prev != P->device) (void)hipSetDevice(P->device);
+    e = hipMemcpy(P->act, P->act_host.data(), P->act_host.size() * 4, hipMemcpyHostToDevice);
+    if (prev >= 0 && prev != P->device) (void)hipSetDevice(prev);
+    if (e != hipSuccess) {
+      delete P;
+      return LF_ERR_DEVICE;
+    }
+    P->act_host = std::vector<uint32_t>();
   }
   std::vector<Part> pins = {
       {&P->hx[0], K * (l + 1) * d}, {&P->hx[1], K * (l + 1) * d}, {&P->hy[0], K * kd}, {&P->hy[1], K * kd},

@@ -269,6 +269,13 @@ hipError_t round_lin(const uint64_t *mles, size_t stride, int nm, const uint64_t
 hipError_t round_lin_eq(const uint64_t *mles, size_t stride, const uint64_t *E, const uint64_t *c, const CombS &cs,
                         int degree, size_t half, int d, uint64_t *partial, uint64_t *evals, hipStream_t st,
                         const uint64_t *const *ptrs = nullptr);
+// round 0 of the split-eq linearization over the multisets' active points: block g
+// runs multiset bms[g] on act[boff[g] .. bend[g]); evals [degree][d]
+hipError_t round_lin_eq_sparse(const uint64_t *const *ptrs, const uint64_t *E, const uint64_t *c, const CombS &cs,
+                               int degree, const uint32_t *act, const int *bms, const uint32_t *boff,
+                               const uint32_t *bend, int nblk, int d, uint64_t *partial, uint64_t *evals,
+                               hipStream_t st);
+size_t round_lin_sparse_ppb(int d);  // points per block pass of round_lin_eq_sparse
 // E_next[b] = E[2b] + E[2b+1] for b < half (whole ring elements)
 hipError_t pair_sum(const uint64_t *E, size_t half, int d, uint64_t *out, hipStream_t st);
 size_t mle_eval_partial_elems(int d, int nm);

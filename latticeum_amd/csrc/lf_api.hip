@@ -118,6 +118,7 @@ struct lf_ccs {
   int degree = 0;
   std::vector<uint64_t> c;     // q NTT elements, canonical
   std::vector<int> S_off, S_idx;
+  std::vector<uint8_t> live;   // [t][m]: row r of M_j holds an entry
   uint64_t *c_dev = nullptr;   // in bufs
   size_t c_dev_elems = 0;
   ~lf_ccs() {  // every device buffer, also on a failed lf_ccs_create
@@ -307,7 +308,7 @@ int grow(lf_ctx *c, T *&buf, size_t &have, size_t need) {
 int reserve(lf_ctx *c, size_t elems) { return grow(c, c->scratch, c->scratch_elems, elems); }
 // a round message back through pinned memory (a pageable destination costs an extra
 // staging copy per round)
-int download_msg(lf_ctx *c, uint64_t *dst, const uint64_t *src, size_t elems) {
+int pinned(lf_ctx *c, size_t elems) {
   if (elems > c->hmsg_elems) {
     if (c->hmsg) LF_HIP(c, hipHostFree(c->hmsg));
     c->hmsg = nullptr;
@@ -315,6 +316,10 @@ int download_msg(lf_ctx *c, uint64_t *dst, const uint64_t *src, size_t elems) {
     LF_HIP(c, hipHostMalloc((void **)&c->hmsg, elems * 8, hipHostMallocDefault));
     c->hmsg_elems = elems;
   }
+  return LF_OK;
+}
+int download_msg(lf_ctx *c, uint64_t *dst, const uint64_t *src, size_t elems) {
+  LF_TRY(pinned(c, elems));
   LF_HIP(c, hipMemcpyAsync(c->hmsg, src, elems * 8, hipMemcpyDeviceToHost, c->cur));
   LF_HIP(c, hipStreamSynchronize(c->cur));
   memcpy(dst, c->hmsg, elems * 8);
@@ -1764,17 +1769,42 @@ int lf_sumcheck_prove_ptrs(lf_ctx *c, lf_transcript *t, const lf_comb *cb, const
 // the same field elements as the unsplit round sums, so the transcript is the same.
 static int sumcheck_run_lin(lf_ctx *c, lf_transcript *t, const lf_comb *cb, const lfk::CombS &cs,
                             const uint64_t *const *ptrs, uint64_t *alt, int nm, int nv, int d, int degree,
-                            const uint64_t *beta, uint64_t *proof, uint64_t *randomness, uint64_t *evals) {
+                            const uint64_t *beta, uint64_t *proof, uint64_t *randomness, uint64_t *evals,
+                            const uint32_t *act = nullptr, const uint32_t *act_off = nullptr) {
   const int tb = lfk::slot_words(d), nev = degree + 1, nq = degree, ns = d / tb;
   const size_t n = (size_t)1 << nv;
   size_t part = 0;
   for (size_t h = n / 2; h >= 1; h /= 2) part = std::max(part, lfk::round_partial_elems(d, h, nq, cb->q));
-  const size_t fixed = (size_t)nm * (n / 2) * d;
-  // scratch: fixed MLEs | partial sums | q | E tables (n/2 + n/4 + .. + 1 < n elements) | beta
-  LF_TRY(grow(c, c->sc, c->sc_elems, fixed + part + (size_t)nq * d + n * d + (size_t)nv * d));
+  // sparse round 0: block g runs multiset bms[g] over act[boff[g] .. bend[g]), about 8
+  // points per thread
+  std::vector<uint32_t> blk;  // bms | boff | bend
+  int nblk = 0;
+  if (act) {
+    const uint32_t per = (uint32_t)lfk::round_lin_sparse_ppb(d) * 8;
+    std::vector<uint32_t> bms, bo, be;
+    for (int i = 0; i < cs.q; i++)
+      for (uint32_t p = act_off[i]; p < act_off[i + 1]; p += per) {
+        bms.push_back((uint32_t)i);
+        bo.push_back(p);
+        be.push_back(std::min(p + per, act_off[i + 1]));
+      }
+    nblk = (int)bms.size();
+    blk = bms;
+    blk.insert(blk.end(), bo.begin(), bo.end());
+    blk.insert(blk.end(), be.begin(), be.end());
+    part = std::max(part, (size_t)nblk * nq * d);
+  }
+  const size_t fixed = (size_t)nm * (n / 2) * d, blk_elems = (blk.size() + 1) / 2;
+  // scratch: fixed MLEs | partial sums | q | E tables (n/2 + n/4 + .. + 1 < n elements) | beta | blocks
+  LF_TRY(grow(c, c->sc, c->sc_elems, fixed + part + (size_t)nq * d + n * d + (size_t)nv * d + blk_elems));
   uint64_t *buf = c->sc, *partial = buf + fixed, *qd = partial + part, *Et = qd + (size_t)nq * d,
-           *bd = Et + n * d;
+           *bd = Et + n * d, *bk = bd + (size_t)nv * d;
   LF_HIP(c, hipMemcpyAsync(bd, beta, (size_t)nv * d * 8, hipMemcpyHostToDevice, c->cur));
+  if (nblk) {  // through the pinned staging, grown here so no round frees it under the copy
+    LF_TRY(pinned(c, std::max(blk_elems, (size_t)nq * d)));
+    memcpy(c->hmsg, blk.data(), blk.size() * 4);
+    LF_HIP(c, hipMemcpyAsync(bk, c->hmsg, blk.size() * 4, hipMemcpyHostToDevice, c->cur));
+  }
   if (nv > 1) {
     LF_HIP(c, lfk::eq_table(bd + d, nv - 1, d, Et, c->cur));
   } else {
@@ -1830,7 +1860,17 @@ static int sumcheck_run_lin(lf_ctx *c, lf_transcript *t, const lf_comb *cb, cons
   for (int i = 0; i < nv; i++) {
     const size_t half = n >> (i + 1);
     uint64_t *msg = proof + (size_t)i * nev * d;
-    LF_HIP(c, lfk::round_lin_eq(cur, stride, E, cb->c, cs, degree, half, d, partial, qd, c->cur, cptrs));
+    if (i == 0 && act) {
+      if (nblk) {
+        const uint32_t *b32 = reinterpret_cast<const uint32_t *>(bk);
+        LF_HIP(c, lfk::round_lin_eq_sparse(cptrs, E, cb->c, cs, degree, act, reinterpret_cast<const int *>(b32),
+                                           b32 + nblk, b32 + 2 * nblk, nblk, d, partial, qd, c->cur));
+      } else {
+        LF_HIP(c, hipMemsetAsync(qd, 0, (size_t)nq * d * 8, c->cur));
+      }
+    } else {
+      LF_HIP(c, lfk::round_lin_eq(cur, stride, E, cb->c, cs, degree, half, d, partial, qd, c->cur, cptrs));
+    }
     LF_TRY(download_msg(c, qh.data(), qd, (size_t)nq * d));
     const uint64_t *be = beta + (size_t)i * d;  // slot 0 holds the base-ring value
     for (int e = 0; e < nev; e++) {
@@ -1900,6 +1940,33 @@ int lf_sumcheck_prove_lin(lf_ctx *c, lf_transcript *t, const lf_comb *cb, const 
                           beta, proof, randomness, evals);
 }
 
+int lf_sumcheck_prove_lin_sparse(lf_ctx *c, lf_transcript *t, const lf_comb *cb, const uint64_t *const *mles, int nm,
+                                 int nv, int d, int degree, const uint64_t *beta, const uint32_t *act,
+                                 const uint32_t *act_off, uint64_t *work, uint64_t *proof, uint64_t *randomness,
+                                 uint64_t *evals) {
+  if (!c || !t || !cb || !mles || !beta || !act || !act_off || !work || !proof || !randomness || nv < 1 || nm < 1)
+    return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  if (!ring_ok(d)) return fail(c, LF_ERR_UNSUPPORTED_RING, "unsupported ring degree");
+  for (int m = 0; m < nm; m++)
+    if (!mles[m]) return fail(c, LF_ERR_INVALID_ARG, "null MLE pointer");
+  if (cb->kind != LF_COMB_LINEARIZATION)
+    return fail(c, LF_ERR_INVALID_ARG, "lf_sumcheck_prove_lin_sparse: a linearization combination");
+  lfk::CombS cs;
+  LF_TRY(comb_check(c, cb, nm + 1, d, degree, &cs));
+  for (int i = 0; i < cs.q; i++) {
+    if (cs.off[i + 1] - cs.off[i] > degree - 1)
+      return fail(c, LF_ERR_INVALID_ARG, "linearization sumcheck: a multiset of degree or more factors");
+    if (act_off[i + 1] < act_off[i] || act_off[i + 1] - act_off[i] > ((size_t)1 << (nv - 1)))
+      return fail(c, LF_ERR_INVALID_ARG, "sparse linearization: act_off must not decrease, at most 2^(nv-1) points each");
+  }
+  if (act_off[0] != 0) return fail(c, LF_ERR_INVALID_ARG, "sparse linearization: act_off[0] must be 0");
+  LF_TRY(grow(c, c->ptrs, c->ptrs_elems, (size_t)nm));
+  LF_HIP(c, hipMemcpyAsync(c->ptrs, mles, (size_t)nm * sizeof(uint64_t), hipMemcpyHostToDevice, c->cur));
+  return sumcheck_run_lin(c, t, cb, cs, reinterpret_cast<const uint64_t *const *>(c->ptrs), work, nm, nv, d, degree,
+                          beta, proof, randomness, evals, act, act_off);
+}
+
 // ---------------------------------------------------------------- sparse Mz products
 void lf_ccs_destroy(lf_ccs *M) { delete M; }
 
@@ -1923,6 +1990,12 @@ int lf_ccs_get_structure(const lf_ccs *M, uint64_t *cc, int *S_off, int *S_idx) 
 }
 
 const uint64_t *lf_ccs_c_device(const lf_ccs *M) { return M ? M->c_dev : nullptr; }
+
+int lf_ccs_row_live(const lf_ccs *M, int j, uint8_t *out) {
+  if (!M || !out || j < 0 || j >= M->dev.t) return LF_ERR_INVALID_ARG;
+  std::copy(M->live.begin() + (size_t)j * M->dev.m, M->live.begin() + (size_t)(j + 1) * M->dev.m, out);
+  return LF_OK;
+}
 
 int lf_ccs_set_structure(lf_ctx *c, lf_ccs *M, size_t l, int degree, int q, const uint64_t *cc, const int *S_off,
                          const int *S_idx, int repr) {
@@ -2006,6 +2079,10 @@ int lf_ccs_create(lf_ctx *c, int d, int t, size_t m, size_t n, const uint64_t *r
   }
   auto M = std::make_unique<lf_ccs>();
   M->device = c->device;
+  M->live.resize((size_t)t * m);
+  for (int j = 0; j < t; j++)
+    for (size_t r = 0; r < m; r++)
+      M->live[(size_t)j * m + r] = row_ptr[(size_t)j * (m + 1) + r + 1] > row_ptr[(size_t)j * (m + 1) + r];
   auto put = [&](const void *h, size_t bytes, void **dst) -> int {
     LF_HIP(c, hipMalloc(dst, bytes ? bytes : 8));
     M->bufs.push_back(*dst);

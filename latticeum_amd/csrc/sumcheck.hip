@@ -633,6 +633,70 @@ __global__ void __launch_bounds__(RT) k_round_lin_eq(const uint64_t *mles, size_
                         partial + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * NQ * d);
 }
 
+// Round 0 of the split-eq linearization over each multiset's active points only: a
+// point b whose line (rows 2b, 2b + 1) is identically zero in some factor of S_i has a
+// zero term at every e (the reference's zero short-cut, linearization/utils.rs:86-104
+// skips such products), and which lines are identically zero is fixed by the CCS rows
+// alone. Block g works on multiset bms[g] and its active points act[boff[g] ..
+// boff[g] + PPB ST) (ST points per thread, strided); E[b] is folded into c_i (one
+// product per term instead of NQ at the end). partial[g][e][slot].
+template <int TB, int NQ>
+__global__ void __launch_bounds__(RT) k_round_lin_eq_sparse(const uint64_t *const *ptrs, const uint64_t *E,
+                                                            const uint64_t *c, CombS cs, const uint32_t *act,
+                                                            const int *bms, const uint32_t *boff, const uint32_t *bend,
+                                                            int d, int spb, uint64_t *partial) {
+  const int slot_l = threadIdx.x % spb, lane_p = threadIdx.x / spb, ppb = RT / spb;
+  const int slot = blockIdx.y * spb + slot_l;
+  const int i = bms[blockIdx.x];
+  const uint32_t p0 = boff[blockIdx.x], p1 = bend[blockIdx.x];
+  const int s0 = cs.off[i], k = cs.off[i + 1] - s0;
+  Sv<TB> acc[NQ];
+#pragma unroll
+  for (int e = 0; e < NQ; e++) acc[e] = s_zero<TB>();
+  const Sv<TB> ci0 = s_load<TB>(c + (size_t)i * d + slot * TB);
+  for (uint32_t p = p0 + lane_p; p < p1; p += ppb) {
+    const size_t b = act[p], pofs = 2 * b * d + slot * TB;
+    const Sv<TB> ci = s_mul(ci0, s_load<TB>(E + b * d + slot * TB));
+    auto fac = [&](int f, Sv<TB> &a, Sv<TB> &dd) {
+      const uint64_t *q = ptrs[cs.idx[s0 + f]] + pofs;
+      a = s_load<TB>(q);
+      dd = s_sub(s_load<TB>(q + d), a);
+    };
+    if (k == 0) {
+#pragma unroll
+      for (int e = 0; e < NQ; e++) acc[e] = s_add(acc[e], ci);
+    } else if (k == 1) {
+      multiset_add<TB, NQ, 1, 0>(ci, fac, acc);
+    } else if (k == 2) {
+      multiset_add<TB, NQ, 2, 0>(ci, fac, acc);
+    } else {
+      Sv<TB> term[NQ], A[5], a, dd;
+      fac(0, a, dd);
+      A[0] = s_mul(ci, a);
+      A[1] = s_mul(ci, dd);
+      fac(1, a, dd);
+      poly_mul_lin<TB, 1>(A, a, dd);
+      poly_to_diff<TB, 2>(A);
+#pragma unroll
+      for (int e = 0; e < NQ; e++) {
+        term[e] = A[0];
+        if (e + 1 < NQ) diff_step<TB, 2>(A);
+      }
+      for (int f = 2; f < k; f++) {
+        fac(f, a, dd);
+#pragma unroll
+        for (int e = 0; e < NQ; e++) {
+          term[e] = s_mul(term[e], a);
+          if (e + 1 < NQ) a = s_add(a, dd);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < NQ; e++) acc[e] = s_add(acc[e], term[e]);
+    }
+  }
+  block_partial<TB, NQ>(acc, spb, ppb, slot, lane_p, d, partial + (size_t)blockIdx.x * NQ * d);
+}
+
 // The same sums for rounds with few points (late rounds): one thread per (point, slot,
 // multiset chunk, evaluation point e), so a thread multiplies |S_i| + 1 values instead
 // of walking all NQ points of a multiset (the chain of dependent products, not the
@@ -990,6 +1054,46 @@ hipError_t round_lin_eq(const uint64_t *mles, size_t stride, const uint64_t *E, 
   hipLaunchKernelGGL(k_sum_partials, dim3((unsigned)len), dim3(256), 0, st, partial, (int)(grid.x * grid.z), len,
                      evals);
   return hipGetLastError();
+}
+
+hipError_t round_lin_eq_sparse(const uint64_t *const *ptrs, const uint64_t *E, const uint64_t *c, const CombS &cs,
+                               int degree, const uint32_t *act, const int *bms, const uint32_t *boff,
+                               const uint32_t *bend, int nblk, int d, uint64_t *partial, uint64_t *evals,
+                               hipStream_t st) {
+  if (degree + 1 > MAX_EVALS || degree < 1 || nblk < 1) return hipErrorInvalidValue;
+  const int ns = d / slot_words(d), spb = ns < RT ? ns : RT;
+  const dim3 grid((unsigned)nblk, (unsigned)(ns / spb), 1);
+#define LF_RLS(TB, NQ)                                                                                          \
+  hipLaunchKernelGGL((k_round_lin_eq_sparse<TB, NQ>), grid, dim3(RT), 0, st, ptrs, E, c, cs, act, bms, boff, bend, \
+                     d, spb, partial)
+#define LF_RLS_DEG(TB)                \
+  switch (degree) {                   \
+    case 1: LF_RLS(TB, 1); break;     \
+    case 2: LF_RLS(TB, 2); break;     \
+    case 3: LF_RLS(TB, 3); break;     \
+    case 4: LF_RLS(TB, 4); break;     \
+    case 5: LF_RLS(TB, 5); break;     \
+    case 6: LF_RLS(TB, 6); break;     \
+    case 7: LF_RLS(TB, 7); break;     \
+    case 8: LF_RLS(TB, 8); break;     \
+    default: LF_RLS(TB, 9); break;    \
+  }
+  if (slot_words(d) == 3) {
+    LF_RLS_DEG(3)
+  } else {
+    LF_RLS_DEG(1)
+  }
+#undef LF_RLS_DEG
+#undef LF_RLS
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const size_t len = (size_t)degree * d;
+  hipLaunchKernelGGL(k_sum_partials, dim3((unsigned)len), dim3(256), 0, st, partial, nblk, len, evals);
+  return hipGetLastError();
+}
+size_t round_lin_sparse_ppb(int d) {
+  const int ns = d / slot_words(d);
+  return RT / (ns < RT ? ns : RT);
 }
 
 hipError_t pair_sum(const uint64_t *E, size_t half, int d, uint64_t *out, hipStream_t st) {

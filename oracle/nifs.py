@@ -550,14 +550,17 @@ def random_ring(n: int, d: int, seed: int):
     return O.fill_uniform(n * d, seed)
 
 
-def satisfied_ccs(d: int, W: int, l: int, t: int, deg: int, seed: int, pr: Params, per_row: int = 2):
+def satisfied_ccs(d: int, W: int, l: int, t: int, deg: int, seed: int, pr: Params, per_row: int = 2,
+                  empty: float = 0.0):
     """A CCS of t matrices, q = 2 multisets S = [[0, .., deg-1], [deg]] and
     c = [1, -1] (a degree-`deg` R1CS generalisation) with m = (W L) rounded up to
     a power of two: A_j (j < deg) read only the 'free' columns (x, 1, the first
     half of w); matrix deg reads one 'product' column in each of the first
     rows; later rows repeat earlier ones; matrices past deg are random extras.
-    satisfying_z makes z vectors that satisfy it."""
+    satisfying_z makes z vectors that satisfy it. empty: the share of A_j rows (j < deg)
+    left without entries (their product column is then 0)."""
     rng = np.random.default_rng(seed)
+    rng_e = np.random.default_rng(seed + 7)
     n = l + 1 + W
     m = 1 << ((W * pr.L) - 1).bit_length()
     free = l + 1 + W // 2
@@ -570,6 +573,8 @@ def satisfied_ccs(d: int, W: int, l: int, t: int, deg: int, seed: int, pr: Param
                 rows[j].append(rows[j][r_ % nprod])
             elif j == deg:
                 rows[j].append(([free + r_], [one(d)]))
+            elif j < deg and empty and rng_e.random() < empty:
+                rows[j].append(([], []))
             else:
                 k = int(rng.integers(1, per_row + 1))
                 cols = sorted(set(int(c) for c in rng.integers(0, free if j < deg else n, k)))

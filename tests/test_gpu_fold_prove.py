@@ -31,9 +31,9 @@ def flat(xs):
     return np.concatenate([np.asarray(x, np.uint64).ravel() for x in xs]) if len(xs) else np.zeros(0, np.uint64)
 
 
-def setup(ctx, d, W, l, t, deg, kappa, seed):
+def setup(ctx, d, W, l, t, deg, kappa, seed, empty=0.0):
     pr_o = N.Params(d)
-    ccs = N.satisfied_ccs(d, W, l, t, deg, seed, pr_o)
+    ccs = N.satisfied_ccs(d, W, l, t, deg, seed, pr_o, empty=empty)
     Nn = W * pr_o.L
     A = O.fill_uniform(kappa * Nn * d, seed + 6)
     sch = LA.AjtaiCommitmentScheme(ctx, A.reshape(kappa, Nn, d))
@@ -154,6 +154,36 @@ def test_fold_prove_matches_oracle(d, W, l, t, deg, kappa):
         w_out2 = {"w_ccs": zeros(W * d), "f": zeros(Nn * d), "f_coeff": zeros(Nn * d)}
         out2, pf2 = prover.fold_prove(acc_dict(acc2), w_out, cm3, flat(x3), dev_wit(W3), w_out2)
         check_against_oracle(out2, pf2, w_out2, o_out2, o_w2, o_proof2)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("d,W,l,t,deg,kappa", [(24, 13, 4, 6, 3, 4), (1024, 9, 2, 4, 2, 2)])
+def test_fold_prove_empty_rows_matches_oracle(d, W, l, t, deg, kappa):
+    """A_j rows without entries (some lines of every multiset's factors vanish, so the
+    linearization's round 0 skips points: lf_sumcheck_prove_lin_sparse): the oracle's
+    fold(), bit for bit"""
+    ctx = LA.Context(0)
+    try:
+        pr_o, ccs, A, prover = setup(ctx, d, W, l, t, deg, kappa, 31 + d + W, empty=0.5)
+        M = LA.CCSMatrices(ctx, d, ccs.m, ccs.n, ccs.mats)
+        active = np.ones(ccs.m // 2, bool)
+        for j in range(deg):
+            live = M.row_live(j, ccs.m)
+            assert np.array_equal(live, np.diff(ccs.mats[j][0].astype(np.int64)) > 0)
+            active &= live.reshape(-1, 2).any(1)
+        assert not active.all(), "the case must skip some points"
+        del M
+        xa, Wa = witness(ccs, pr_o, 21)
+        xi, Wi = witness(ccs, pr_o, 22)
+        Nn = W * pr_o.L
+        cma = O.ajtai_commit(A, kappa, Nn, d, Wa.f)
+        cmi = O.ajtai_commit(A, kappa, Nn, d, Wi.f)
+        acc = N.linearize_fresh(ccs, cma, xa, Wa, pr_o)
+        o_out, o_w0, o_proof = N.fold_prove(ccs, A, kappa, acc, Wa, cmi, xi, Wi, pr_o)
+        w_out = {"w_ccs": zeros(W * d), "f": zeros(Nn * d), "f_coeff": zeros(Nn * d)}
+        out, pf = prover.fold_prove(acc_dict(acc), dev_wit(Wa), cmi, flat(xi), dev_wit(Wi), w_out)
+        check_against_oracle(out, pf, w_out, o_out, o_w0, o_proof)
     finally:
         ctx.close()
 

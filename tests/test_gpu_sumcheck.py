@@ -33,6 +33,11 @@ def dev(x=None, n=None):
     return torch.zeros(n, dtype=torch.int64, device="cuda")
 
 
+def dev32(x):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(x, np.int32)).cuda()
+
+
 def host(t):
     return t.cpu().numpy().view(np.uint64)
 
@@ -203,6 +208,77 @@ def test_linearization_prove_lin_matches_oracle(ctx, d, nv, sizes):
     point = np.concatenate([O.broadcast(rnd[i * tau:(i + 1) * tau], d) for i in range(nv)])
     ctx.sync()
     assert np.array_equal(host(evals), np.concatenate([O.mle_evaluate(m, nv, d, point) for m in mz]))
+
+
+def sparse_lists(mz, S, c, nv, d, rng, frac=0.3):
+    """zero whole lines (rows 2b, 2b + 1) of each MLE with probability frac; the active
+    points of each multiset (every factor's line nonzero; none when c_i vanishes)"""
+    half = 1 << (nv - 1)
+    live = []
+    for m in mz:
+        on = rng.random(half) >= frac
+        m.reshape(half, 2 * d)[~on] = 0
+        live.append(on)
+    act, off = [], [0]
+    for i, Si in enumerate(S):
+        on = np.ones(half, bool)
+        for j in Si:
+            on &= live[j]
+        if not c[i * d:(i + 1) * d].any():
+            on[:] = False
+        act.extend(np.nonzero(on)[0].tolist())
+        off.append(len(act))
+    return np.array(act or [0], np.int32), np.array(off, np.uint32)
+
+
+@pytest.mark.parametrize("d,nv,sizes", [(24, 6, [7, 1, 2, 0, 3]), (24, 5, [8, 5, 6, 4, 1]), (64, 4, [7, 2, 5]),
+                                        (24, 1, [3, 2]), (1024, 3, [4, 7])])
+def test_linearization_prove_lin_sparse_matches_oracle(ctx, d, nv, sizes):
+    """lf_sumcheck_prove_lin_sparse (round 0 over each multiset's active points only) on
+    MLEs with zero lines gives the oracle's proof and final values; one multiset's c
+    vanishes entirely and gets no points"""
+    c, S, mz, beta = lin_eq_case(d, nv, sizes, 2000 + d + nv)
+    c[(len(sizes) - 1) * d:] = 0
+    act, off = sparse_lists(mz, S, c, nv, d, np.random.default_rng(d + nv))
+    degree = max(sizes) + 1
+    mles = np.concatenate(mz + [O.eq_table(beta, nv, d)])
+    want_p, want_r = O.sumcheck_prove(O.new_transcript(), O.SumcheckComb.linearization(c, S), mles, len(mz) + 1, nv,
+                                      d, degree)
+    work = dev(n=max(1, len(mz) * (1 << max(nv - 2, 0)) * d))
+    evals = dev(n=len(mz) * d)
+    act_d = dev32(act)
+    proof, rnd = ctx.sumcheck_prove_lin_sparse(LA.Poseidon2Transcript(), LA.Comb.linearization(dev(c), S),
+                                               [dev(m) for m in mz], nv, d, degree, beta, act_d, off, work, evals)
+    assert np.array_equal(proof, want_p) and np.array_equal(rnd, want_r)
+    tau = 3 if d == 24 else 1
+    point = np.concatenate([O.broadcast(rnd[i * tau:(i + 1) * tau], d) for i in range(nv)])
+    ctx.sync()
+    assert np.array_equal(host(evals), np.concatenate([O.mle_evaluate(m, nv, d, point) for m in mz]))
+
+
+def test_linearization_prove_lin_sparse_matches_dense_at_size(ctx):
+    """Phi_72, 14 variables, the zkvm's multiset sizes, a third of the lines zero: the
+    sparse round 0 against the dense prover"""
+    d, nv = 24, 14
+    n = 1 << nv
+    sizes = [7] * 6 + [1, 2] * 6 + [0]
+    rng = np.random.default_rng(81)
+    nmz = 40
+    S = [[int(j) for j in rng.integers(0, nmz, k)] for k in sizes]
+    c = rand(len(sizes) * d, 82)
+    mz = [rand(n * d, 83 + j) for j in range(nmz)]
+    act, off = sparse_lists(mz, S, c, nv, d, rng)
+    beta = np.concatenate([O.broadcast(rand(3, 180 + i), d) for i in range(nv)])
+    mzd = [dev(m) for m in mz]
+    work = dev(n=nmz * (n // 4) * d)
+    ev0, ev1 = dev(n=nmz * d), dev(n=nmz * d)
+    want_p, want_r = ctx.sumcheck_prove_lin(LA.Poseidon2Transcript(), LA.Comb.linearization(dev(c), S), mzd, nv, d, 8,
+                                            beta, work, ev0)
+    proof, rnd = ctx.sumcheck_prove_lin_sparse(LA.Poseidon2Transcript(), LA.Comb.linearization(dev(c), S), mzd, nv, d,
+                                               8, beta, dev32(act), off, work, ev1)
+    ctx.sync()
+    assert np.array_equal(proof, want_p) and np.array_equal(rnd, want_r)
+    assert np.array_equal(host(ev0), host(ev1))
 
 
 def test_linearization_prove_lin_matches_unsplit_at_size(ctx):
