@@ -844,6 +844,7 @@ def next_rows(LA, torch, local, cpu):
         mt[2] = hv[off * d:(off + k) * d]
         off += k
     M = LA.CCSMatrices(ctx, d, mm, nn, mats)
+    structure = [(mt[0], mt[1]) for mt in mats]
     del hv, mats
     z = torch.empty(K * nn * d, **i64)
     ctx.dev_fill_uniform(z, 0x4C460014)
@@ -873,9 +874,38 @@ def next_rows(LA, torch, local, cpu):
                     f"K={K} decomposed vectors",
         "challenged_mle_ms": ms_ch, "etas_ms": ms_ev,
         "challenged_gbs_values": val_bytes / (ms_ch * 1e-3) / 1e9}
-    del z, ch, ev
     out["fold_prove"] = fold_prove_line(LA, torch, ctx, M, S, d, nn, t, mm)
+    del M
+    torch.cuda.empty_cache()
+    # the same rows with scalar values, as the zkvm's R1CS-derived matrices hold
+    # (R::one(), negations, from_goldilocks constants: zkvm/src/constraints.rs:127-364):
+    # the products then read one word per entry (lf_ccs_is_scalar)
+    sv = torch.empty(nnz, **i64)
+    ctx.dev_fill_uniform(sv, 0x4C460019)
+    hs = sv.cpu().numpy().view(np.uint64)
+    del sv
+    full = np.zeros((nnz, d), np.uint64)
+    full[:, ::3] = hs[:, None]
+    full = full.ravel()
+    mats, off = [], 0
+    for rp, col in structure:
+        k = int(rp[-1])
+        mats.append([rp, col, full[off * d:(off + k) * d]])
+        off += k
+    M = LA.CCSMatrices(ctx, d, mm, nn, mats)
+    assert M.scalar
+    del full, hs, mats, structure
+    ms_ch_s = ev_ms(lambda: M.mz_challenged(z, zeta, K, nv, ch))
+    ms_ev_s = ev_ms(lambda: M.mz_evaluate(z, K, nv, point, ev))
+    out["mz_products_scalar"] = {
+        "workload": f"the rows of mz_products with scalar values (the zkvm's matrices: R::one(), -1, "
+                    f"from_goldilocks constants), {nnz} entries of one word each, K={K} decomposed vectors",
+        "challenged_mle_ms": ms_ch_s, "etas_ms": ms_ev_s}
+    del z, ch, ev
+    out["fold_prove_scalar"] = fold_prove_line(LA, torch, ctx, M, S, d, nn, t, mm)
+    out["fold_prove_scalar"]["workload"] += "; the CCS values scalars as the zkvm's (lf_ccs_is_scalar)"
     out["zkvm_chain"] = zkvm_chain(LA, torch, ctx, M, S, d, nn, t, mm)
+    out["zkvm_chain"]["workload"] += "; the CCS values scalars as the zkvm's (lf_ccs_is_scalar)"
     del M
     # the memory Merkle tree of the zkvm's 8 MB VM (8192 pages of 256 words,
     # vm.rs:106-124; commitments.rs:192-262): 8192 sponge chains of 64 width-8

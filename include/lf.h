@@ -586,6 +586,10 @@ int lf_ccs_set_structure(lf_ctx *ctx, lf_ccs *M, size_t l, int degree, int q, co
 int lf_ccs_shape(const lf_ccs *M, int *t, size_t *m, size_t *n, size_t *l, int *q, int *degree);
 int lf_ccs_get_structure(const lf_ccs *M, uint64_t *c, int *S_off, int *S_idx);
 const uint64_t *lf_ccs_c_device(const lf_ccs *M);
+/* 1 if every entry of the matrices is a scalar (from_scalar: its value in word 0 of
+ * every slot, zero elsewhere -- the zkvm's R1CS-derived matrices), which the Mz
+ * products then read as one word per entry; else 0 */
+int lf_ccs_is_scalar(const lf_ccs *M);
 /* out[r] = 1 if row r of M_j holds an entry (so MLE(M_j z) may be nonzero there), else 0; m bytes */
 int lf_ccs_row_live(const lf_ccs *M, int j, uint8_t *out);
 /* tracing spans of lf_fold_prove (the reference's #[instrument] spans): wall ms per

@@ -515,6 +515,11 @@ class CCSMatrices:
         s = np.ascontiguousarray(np.asarray(sel, np.int32))
         self.ctx.check(self.lib.lf_dev_mz_mles_sel(self.ctx.h, self.h, _dptr(z), _ptr(s), len(s), nv, _dptr(out)))
 
+    @property
+    def scalar(self) -> bool:
+        """every entry a scalar (lf_ccs_is_scalar): the products read one word per entry"""
+        return bool(self.lib.lf_ccs_is_scalar(self.h))
+
     def row_live(self, j: int, m: int):
         """which rows of M_j hold an entry (lf_ccs_row_live): m bools"""
         out = np.zeros(m, np.uint8)

@@ -176,6 +176,7 @@ SIGNATURES = {
     "lf_ccs_get_structure": (I, [VP, VP, VP, VP]),
     "lf_ccs_c_device": (VP, [VP]),
     "lf_ccs_row_live": (I, [VP, I, VP]),
+    "lf_ccs_is_scalar": (I, [VP]),
     "lf_prover_create": (I, [VP, VP, C.POINTER(LfParams), VP, C.POINTER(VP)]),
     "lf_prover_destroy": (None, [VP]),
     "lf_prover_last_error": (C.c_char_p, [VP]),

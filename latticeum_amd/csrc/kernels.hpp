@@ -308,6 +308,7 @@ struct CcsDev {
   const uint64_t *rp;  // [t][m + 1], absolute offsets into col / val
   const uint32_t *col;
   const uint64_t *val;  // [nnz][d]
+  const uint64_t *sval = nullptr;  // [nnz] when every entry is a scalar (v in every slot word 0, zero elsewhere)
   const uint64_t *hrp;  // [m + 1]
   const uint32_t *hcol;  // j n + col
   const uint32_t *hidx;  // value index

@@ -1991,6 +1991,8 @@ int lf_ccs_get_structure(const lf_ccs *M, uint64_t *cc, int *S_off, int *S_idx) 
 
 const uint64_t *lf_ccs_c_device(const lf_ccs *M) { return M ? M->c_dev : nullptr; }
 
+int lf_ccs_is_scalar(const lf_ccs *M) { return M && M->dev.sval ? 1 : 0; }
+
 int lf_ccs_row_live(const lf_ccs *M, int j, uint8_t *out) {
   if (!M || !out || j < 0 || j >= M->dev.t) return LF_ERR_INVALID_ARG;
   std::copy(M->live.begin() + (size_t)j * M->dev.m, M->live.begin() + (size_t)(j + 1) * M->dev.m, out);
@@ -2102,6 +2104,27 @@ int lf_ccs_create(lf_ctx *c, int d, int t, size_t m, size_t n, const uint64_t *r
   LF_TRY(put(val, nnz * d * 8, &p));
   D.val = (const uint64_t *)p;
   if (repr == LF_REPR_MONTGOMERY && nnz) LF_HIP(c, lfk::mont((uint64_t *)p, nnz * d, false, c->cur));
+  {  // every entry a scalar (its value in word 0 of each slot, zero elsewhere: from_scalar,
+     // ntt_form.rs:689-692)? then the products read one word per entry (CcsDev::sval)
+    const int tb = lfk::slot_words(d);
+    bool scalar = nnz > 0;
+    for (size_t k = 0; k < nnz && scalar; k++) {
+      const uint64_t *v = val + k * d;
+      for (int w = 0; w < d; w++)
+        if (v[w] != (w % tb == 0 ? v[0] : 0)) {
+          scalar = false;
+          break;
+        }
+    }
+    if (scalar) {
+      std::vector<uint64_t> sv(nnz);
+      for (size_t k = 0; k < nnz; k++) sv[k] = val[k * d];
+      LF_TRY(put(sv.data(), nnz * 8, &p));
+      D.sval = (const uint64_t *)p;
+      if (repr == LF_REPR_MONTGOMERY) LF_HIP(c, lfk::mont((uint64_t *)p, nnz, false, c->cur));
+      LF_HIP(c, hipStreamSynchronize(c->cur));  // sv goes out of scope
+    }
+  }
   LF_TRY(put(hrp.data(), hrp.size() * 8, &p));
   D.hrp = (const uint64_t *)p;
   LF_TRY(put(hcol.data(), nnz * 4, &p));

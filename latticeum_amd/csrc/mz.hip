@@ -25,8 +25,9 @@ constexpr int MT = 256;
 
 // out[task][r] = sum_k val[vidx ? vidx[k] : k] (.) z[col[k]], k in [rp[r], rp[r+1]);
 // task = (a, b) = (task % na, task / na) selects rp + A rp_stride (A = sel ? sel[a] : a)
-// and z + b z_stride
-template <int TB>
+// and z + b z_stride. SC: val holds one scalar per entry (CcsDev::sval), the zkvm's
+// matrices (R::one(), from_goldilocks constants: zkvm/src/constraints.rs:127-364)
+template <int TB, bool SC>
 __global__ void __launch_bounds__(MT) k_csr(const uint64_t *rp, size_t rp_stride, int na, const int *sel,
                                            const uint32_t *col, const uint32_t *vidx, const uint64_t *val,
                                            size_t nrows, int d, const uint64_t *z, size_t z_stride, uint64_t *out,
@@ -42,7 +43,10 @@ __global__ void __launch_bounds__(MT) k_csr(const uint64_t *rp, size_t rp_stride
   sacc_zero(acc);
   for (uint64_t k = rpa[r], e = rpa[r + 1]; k < e; k++) {
     const uint64_t vi = vidx ? vidx[k] : k;
-    sacc_mad(acc, s_load<TB>(val + vi * d + slot * TB), s_load<TB>(zb + (size_t)col[k] * d));
+    if (SC)
+      sacc_smad(acc, val[vi], s_load<TB>(zb + (size_t)col[k] * d));
+    else
+      sacc_mad(acc, s_load<TB>(val + vi * d + slot * TB), s_load<TB>(zb + (size_t)col[k] * d));
   }
   s_store(out + task * out_stride + r * d + slot * TB, sacc_final(acc));
 }
@@ -131,18 +135,28 @@ __global__ void k_zero_tails(uint64_t *out, size_t len, size_t from, size_t tail
   out[i * len + from + (t - i * tail)] = 0;
 }
 
-hipError_t csr(const uint64_t *rp, size_t rp_stride, int na, const uint32_t *col, const uint32_t *vidx,
-               const uint64_t *val, size_t nrows, int d, const uint64_t *z, size_t z_stride, uint64_t *out,
+hipError_t csr(const CcsDev &M, const uint64_t *rp, size_t rp_stride, int na, const uint32_t *col,
+               const uint32_t *vidx, size_t nrows, const uint64_t *z, size_t z_stride, uint64_t *out,
                size_t out_stride, int ntask, hipStream_t st, const int *sel = nullptr) {
   if (!nrows || !ntask) return hipSuccess;
-  const int tb = slot_words(d), ns = d / tb, spb = ns < MT ? ns : MT;
+  const int d = M.d, tb = slot_words(d), ns = d / tb, spb = ns < MT ? ns : MT;
   const dim3 grid(nblk(nrows, MT / spb), (unsigned)ntask, (unsigned)(ns / spb));
-  if (tb == 3)
-    hipLaunchKernelGGL(k_csr<3>, grid, dim3(MT), 0, st, rp, rp_stride, na, sel, col, vidx, val, nrows, d, z, z_stride,
-                       out, out_stride, spb);
-  else
-    hipLaunchKernelGGL(k_csr<1>, grid, dim3(MT), 0, st, rp, rp_stride, na, sel, col, vidx, val, nrows, d, z, z_stride,
-                       out, out_stride, spb);
+  const uint64_t *val = M.sval ? M.sval : M.val;
+#define LF_CSR(TB, SC)                                                                                            \
+  hipLaunchKernelGGL((k_csr<TB, SC>), grid, dim3(MT), 0, st, rp, rp_stride, na, sel, col, vidx, val, nrows, d, z, \
+                     z_stride, out, out_stride, spb)
+  if (tb == 3) {
+    if (M.sval)
+      LF_CSR(3, true);
+    else
+      LF_CSR(3, false);
+  } else {
+    if (M.sval)
+      LF_CSR(1, true);
+    else
+      LF_CSR(1, false);
+  }
+#undef LF_CSR
   return hipGetLastError();
 }
 
@@ -166,7 +180,7 @@ hipError_t mz_mles(const CcsDev &M, const uint64_t *z, int nz, int nv, uint64_t 
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  return csr(M.rp, M.m + 1, na, M.col, nullptr, M.val, M.m, M.d, z, M.n * M.d, out, len, nz * na, st, sel);
+  return csr(M, M.rp, M.m + 1, na, M.col, nullptr, M.m, z, M.n * M.d, out, len, nz * na, st, sel);
 }
 
 hipError_t mz_challenged(const CcsDev &M, const uint64_t *z, const uint64_t *zeta, int nz, int nv, uint64_t *out,
@@ -190,12 +204,12 @@ hipError_t mz_challenged(const CcsDev &M, const uint64_t *z, const uint64_t *zet
     e = hipMemsetAsync(out + M.m * M.d, 0, (len - M.m * M.d) * 8, st);
     if (e != hipSuccess) return e;
   }
-  return csr(M.hrp, 0, 1, M.hcol, M.hidx, M.val, M.m, M.d, y, 0, out, 0, 1, st);
+  return csr(M, M.hrp, 0, 1, M.hcol, M.hidx, M.m, y, 0, out, 0, 1, st);
 }
 
 hipError_t mz_weights(const CcsDev &M, const uint64_t *eq, uint64_t *w, hipStream_t st) {
   // w_j[c] = sum over column c of M_j of value (.) eq[row]
-  return csr(M.crp, M.n + 1, M.t, M.crow, M.cidx, M.val, M.n, M.d, eq, 0, w, M.n * M.d, M.t, st);
+  return csr(M, M.crp, M.n + 1, M.t, M.crow, M.cidx, M.n, eq, 0, w, M.n * M.d, M.t, st);
 }
 
 hipError_t mz_evaluate(const CcsDev &M, const uint64_t *z, int nz, int nv, const uint64_t *point, uint64_t *out,

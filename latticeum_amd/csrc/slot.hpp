@@ -172,6 +172,13 @@ __device__ __forceinline__ void sacc_mad(SAcc<3> &a, const Sv<3> &x, const Sv<3>
   gl::cacc_mad(a.x2, x.c[1], y.c[1]);
   gl::cacc_mad(a.x2, x.c[2], y.c[0]);
 }
+// a scalar (s, 0, 0) times y: one product per word, no nonresidue
+__device__ __forceinline__ void sacc_smad(SAcc<1> &a, uint64_t s, const Sv<1> &y) { gl::cacc_mad(a.x, s, y.c[0]); }
+__device__ __forceinline__ void sacc_smad(SAcc<3> &a, uint64_t s, const Sv<3> &y) {
+  gl::cacc_mad(a.x0, s, y.c[0]);
+  gl::cacc_mad(a.x1, s, y.c[1]);
+  gl::cacc_mad(a.x2, s, y.c[2]);
+}
 __device__ __forceinline__ Sv<1> sacc_final(const SAcc<1> &a) {
   Sv<1> r;
   r.c[0] = gl::cacc_reduce(a.x);

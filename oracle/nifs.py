@@ -551,14 +551,15 @@ def random_ring(n: int, d: int, seed: int):
 
 
 def satisfied_ccs(d: int, W: int, l: int, t: int, deg: int, seed: int, pr: Params, per_row: int = 2,
-                  empty: float = 0.0):
+                  empty: float = 0.0, scalar: bool = False):
     """A CCS of t matrices, q = 2 multisets S = [[0, .., deg-1], [deg]] and
     c = [1, -1] (a degree-`deg` R1CS generalisation) with m = (W L) rounded up to
     a power of two: A_j (j < deg) read only the 'free' columns (x, 1, the first
     half of w); matrix deg reads one 'product' column in each of the first
     rows; later rows repeat earlier ones; matrices past deg are random extras.
     satisfying_z makes z vectors that satisfy it. empty: the share of A_j rows (j < deg)
-    left without entries (their product column is then 0)."""
+    left without entries (their product column is then 0). scalar: every entry a
+    scalar (from_u), as the zkvm's R1CS-derived matrices hold."""
     rng = np.random.default_rng(seed)
     rng_e = np.random.default_rng(seed + 7)
     n = l + 1 + W
@@ -578,7 +579,10 @@ def satisfied_ccs(d: int, W: int, l: int, t: int, deg: int, seed: int, pr: Param
             else:
                 k = int(rng.integers(1, per_row + 1))
                 cols = sorted(set(int(c) for c in rng.integers(0, free if j < deg else n, k)))
-                vals = [random_ring(1, d, vseed + i) for i in range(len(cols))]
+                if scalar:
+                    vals = [from_u(int(O.fill_uniform(1, vseed + i)[0]), d) for i in range(len(cols))]
+                else:
+                    vals = [random_ring(1, d, vseed + i) for i in range(len(cols))]
                 vseed += len(cols)
                 rows[j].append((cols, vals))
     mats = []

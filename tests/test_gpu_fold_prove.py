@@ -31,9 +31,9 @@ def flat(xs):
     return np.concatenate([np.asarray(x, np.uint64).ravel() for x in xs]) if len(xs) else np.zeros(0, np.uint64)
 
 
-def setup(ctx, d, W, l, t, deg, kappa, seed, empty=0.0):
+def setup(ctx, d, W, l, t, deg, kappa, seed, empty=0.0, scalar=False):
     pr_o = N.Params(d)
-    ccs = N.satisfied_ccs(d, W, l, t, deg, seed, pr_o, empty=empty)
+    ccs = N.satisfied_ccs(d, W, l, t, deg, seed, pr_o, empty=empty, scalar=scalar)
     Nn = W * pr_o.L
     A = O.fill_uniform(kappa * Nn * d, seed + 6)
     sch = LA.AjtaiCommitmentScheme(ctx, A.reshape(kappa, Nn, d))
@@ -158,15 +158,18 @@ def test_fold_prove_matches_oracle(d, W, l, t, deg, kappa):
         ctx.close()
 
 
+@pytest.mark.parametrize("scalar", [False, True])
 @pytest.mark.parametrize("d,W,l,t,deg,kappa", [(24, 13, 4, 6, 3, 4), (1024, 9, 2, 4, 2, 2)])
-def test_fold_prove_empty_rows_matches_oracle(d, W, l, t, deg, kappa):
+def test_fold_prove_empty_rows_matches_oracle(d, W, l, t, deg, kappa, scalar):
     """A_j rows without entries (some lines of every multiset's factors vanish, so the
-    linearization's round 0 skips points: lf_sumcheck_prove_lin_sparse): the oracle's
-    fold(), bit for bit"""
+    linearization's round 0 skips points: lf_sumcheck_prove_lin_sparse), and with
+    scalar-valued matrices as the zkvm's (lf_ccs_is_scalar): the oracle's fold(), bit
+    for bit"""
     ctx = LA.Context(0)
     try:
-        pr_o, ccs, A, prover = setup(ctx, d, W, l, t, deg, kappa, 31 + d + W, empty=0.5)
+        pr_o, ccs, A, prover = setup(ctx, d, W, l, t, deg, kappa, 31 + d + W, empty=0.5, scalar=scalar)
         M = LA.CCSMatrices(ctx, d, ccs.m, ccs.n, ccs.mats)
+        assert M.scalar == scalar
         active = np.ones(ccs.m // 2, bool)
         for j in range(deg):
             live = M.row_live(j, ccs.m)

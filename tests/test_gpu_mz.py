@@ -35,7 +35,16 @@ def host(t):
     return t.cpu().numpy().view(np.uint64)
 
 
-def random_ccs(t, m, n, d, seed, max_per_row=3):
+def scalars(v, d):
+    """one scalar per entry as ring elements in NTT form (from_scalar: v in word 0 of
+    every slot, zero elsewhere)"""
+    tb = 3 if d == 24 else 1
+    out = np.zeros((len(v), d), np.uint64)
+    out[:, ::tb] = np.asarray(v, np.uint64)[:, None]
+    return out.ravel()
+
+
+def random_ccs(t, m, n, d, seed, max_per_row=3, scalar=False):
     rng = np.random.default_rng(seed)
     mats = []
     for j in range(t):
@@ -47,16 +56,26 @@ def random_ccs(t, m, n, d, seed, max_per_row=3):
         col = rng.integers(0, n, int(rp[-1])).astype(np.uint32)
         if col.size > 1:
             col[1] = col[0]  # a repeated column
-        val = O.fill_uniform(int(rp[-1]) * d, seed + 7 * j)
+        if scalar:  # the zkvm's values: small constants, -1 and arbitrary field elements
+            v = O.fill_uniform(int(rp[-1]), seed + 7 * j)
+            v[::3] = 1
+            v[1::5] = LA.P - 1
+            val = scalars(v, d)
+        else:
+            val = O.fill_uniform(int(rp[-1]) * d, seed + 7 * j)
         mats.append((rp, col, val))
     return mats
 
 
+@pytest.mark.parametrize("scalar", [False, True])
 @pytest.mark.parametrize("d", [24, 16, 1024])
-def test_mz_products_match_oracle(ctx, d):
+def test_mz_products_match_oracle(ctx, d, scalar):
+    """ring-valued matrices, and scalar-valued ones (the zkvm's; read one word per
+    entry, lf_ccs_is_scalar)"""
     t, m, n, nz, nv = 5, 100, 37, 3, 7
-    mats = random_ccs(t, m, n, d, 40 + d)
+    mats = random_ccs(t, m, n, d, 40 + d, scalar=scalar)
     M = LA.CCSMatrices(ctx, d, m, n, mats)
+    assert M.scalar == scalar
     zs = [O.fill_uniform(n * d, 50 + d + i) for i in range(nz)]
     zd = dev(np.concatenate(zs))
     out = dev(n=nz * t * (1 << nv) * d)

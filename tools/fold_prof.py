@@ -1,6 +1,7 @@
 """fold() at the zkvm's shape (bench.py next_rows' CCS and fold_prove_line) on its
-own, for rocprofv3 kernel traces of lf_fold_prove: `python tools/fold_prof.py [reps]`
-prints the line bench.py reports as next_rows.fold_prove."""
+own, for rocprofv3 kernel traces of lf_fold_prove: `python tools/fold_prof.py [--scalar]`
+prints the line bench.py reports as next_rows.fold_prove (with --scalar:
+next_rows.fold_prove_scalar, the same rows with scalar values as the zkvm's)."""
 import json
 import sys
 from pathlib import Path
@@ -31,9 +32,16 @@ def main():
         rp = np.concatenate([[0], np.cumsum(cnt)]).astype(np.uint64)
         mats.append([rp, rng.integers(0, nn, int(rp[-1])).astype(np.uint32), None])
         nnz += int(rp[-1])
-    vals = torch.empty(nnz * d, **i64)
-    ctx.dev_fill_uniform(vals, 0x4C460013)
-    hv = vals.cpu().numpy().view(np.uint64)
+    if "--scalar" in sys.argv:
+        sv = torch.empty(nnz, **i64)
+        ctx.dev_fill_uniform(sv, 0x4C460019)
+        hv = np.zeros((nnz, d), np.uint64)
+        hv[:, ::3] = sv.cpu().numpy().view(np.uint64)[:, None]
+        hv = hv.ravel()
+    else:
+        vals = torch.empty(nnz * d, **i64)
+        ctx.dev_fill_uniform(vals, 0x4C460013)
+        hv = vals.cpu().numpy().view(np.uint64)
     off = 0
     for mt in mats:
         k = int(mt[0][-1])

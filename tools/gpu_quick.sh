@@ -9,7 +9,7 @@ TESTS=${TESTS:-tests/test_gpu_sumcheck.py tests/test_gpu_fold_prove.py}
 timeout -k 10 600 python -u -m pytest $TESTS -m gpu -q -x -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/proffold_$TAG -o run --output-format csv -- \
-  python tools/fold_prof.py > gpurun_out/fold_prof_$TAG.log 2>&1
+  python tools/fold_prof.py $FOLD_ARGS > gpurun_out/fold_prof_$TAG.log 2>&1
 rc=$?; echo "fold prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python3 -c "
 import json; d=json.loads([l for l in open('gpurun_out/fold_prof_$TAG.log') if l.startswith('{')][-1])
