@@ -12,6 +12,11 @@
 #include "../../include/lf.h"
 #include "gl.hpp"
 #include "ring.hpp"
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+#define LF_P2_AVX512 1
+#include <cstdlib>
+#include "p2_avx512.hpp"
+#endif
 
 namespace {
 #include "p2_consts.inc"
@@ -127,10 +132,58 @@ inline void mds16_rc(uint64_t *s, const uint64_t *rc) {
   }
 }
 void mds16(uint64_t *s) { mds16_rc(s, nullptr); }
+#if LF_P2_AVX512
+// permute() on AVX-512: the external rounds' S-boxes and layers on the two state
+// registers; in the internal rounds s_0's S-box chain runs in scalar registers (it
+// is the round's critical path) while the diagonal layer runs on the vectors, the
+// next round's s_0 from the scalar copy and the sum of the rest from the lanes.
+// The same field elements as the scalar form (tools/exp/p2_avx_test.cpp).
+LF_AVX512 void permute_avx512(uint64_t *s) {
+  using namespace p2avx;
+  __m512i x0 = _mm512_loadu_si512(s), x1 = _mm512_loadu_si512(s + 8);
+  mds16_rc8(x0, x1, EXT_INIT);
+  for (int r = 0; r < 4; r++) {
+    x0 = sbox8(x0);
+    x1 = sbox8(x1);
+    mds16_rc8(x0, x1, r < 3 ? EXT_INIT + 16 * (r + 1) : nullptr);
+  }
+  {
+    const __m512i D0 = _mm512_loadu_si512(DIAG_M1), D1 = _mm512_loadu_si512(DIAG_M1 + 8);
+    uint64_t s0 = (uint64_t)_mm_cvtsi128_si64(_mm512_castsi512_si128(x0)), sl, sh;
+    hsum_rest8(x0, x1, sl, sh);
+    for (int r = 0; r < 22; r++) {
+      const uint64_t rest = red96((u128)sl + ((u128)sh << 32));
+      s0 = sbox7(wadd(s0, INTERNAL[r]));
+      const uint64_t sum = wadd(rest, s0);
+      const __m512i S = _mm512_set1_epi64((long long)sum);
+      x0 = wmuladd8(_mm512_mask_mov_epi64(x0, 1, _mm512_set1_epi64((long long)s0)), D0, S);
+      x1 = wmuladd8(x1, D1, S);
+      s0 = wmuladd(s0, DIAG_M1[0], sum);
+      hsum_rest8(x0, x1, sl, sh);
+    }
+  }
+  x0 = wadd8(x0, _mm512_loadu_si512(EXT_TERM));
+  x1 = wadd8(x1, _mm512_loadu_si512(EXT_TERM + 8));
+  for (int r = 0; r < 4; r++) {
+    x0 = sbox8(x0);
+    x1 = sbox8(x1);
+    mds16_rc8(x0, x1, r < 3 ? EXT_TERM + 16 * (r + 1) : nullptr);
+  }
+  _mm512_storeu_si512(s, x0);
+  _mm512_storeu_si512(s + 8, x1);
+  for (int i = 0; i < 16; i++) s[i] = gl::canon(s[i]);
+}
+// AVX-512F present, unless LATTICEUM_AMD_P2_SCALAR=1 (the scalar form, for A/B runs)
+bool use_avx512() {
+  static const bool on = __builtin_cpu_supports("avx512f") && !(getenv("LATTICEUM_AMD_P2_SCALAR") &&
+                                                                 getenv("LATTICEUM_AMD_P2_SCALAR")[0] == '1');
+  return on;
+}
+#endif
 // The sponge's permutation. Round constants ride in the preceding layer's sums
 // (the initial MDS carries round 0's, the last internal round adds the terminal
 // rounds' first); the internal rounds' diagonal product and the sum share one fold.
-void permute(uint64_t *s) {
+void permute_scalar(uint64_t *s) {
   mds16_rc(s, EXT_INIT);
   #pragma unroll
   for (int r = 0; r < 4; r++) {
@@ -158,6 +211,12 @@ void permute(uint64_t *s) {
   }
   #pragma unroll
   for (int i = 0; i < 16; i++) s[i] = gl::canon(s[i]);
+}
+void permute(uint64_t *s) {
+#if LF_P2_AVX512
+  if (use_avx512()) return permute_avx512(s);
+#endif
+  permute_scalar(s);
 }
 // permute() with WideZkVMPoseidon2Perm::permute_mut's PermutationIntermediateStates
 // (poseidon2.rs:91-96, 104-171): the state after the initial MDS, after each of
