@@ -132,3 +132,28 @@ def test_hash_iter_states_capacity_checked():
     assert lib.lf_hash_iter_states(x.ctypes.data, 25, out.ctypes.data, st.ctypes.data, 2) != 0  # needs 3
     assert lib.lf_hash_iter_states(x.ctypes.data, 25, out.ctypes.data, None, 0) == 0
     assert np.array_equal(out, O.p2_hash_iter(x))
+
+
+def test_permutation_avx512_and_scalar_agree():
+    """the host permutation's AVX-512 form (selected at run time) and its scalar form
+    (LATTICEUM_AMD_P2_SCALAR=1, in a child process) give the same hash_iter digests and
+    transcript samples, on random and extreme inputs, both equal to the oracle's"""
+    import subprocess
+    import os
+    rng = np.random.default_rng(9)
+    xs = [rng.integers(0, LA.P, 12 * 40 + 5, dtype=np.uint64),
+          np.full(100, LA.P - 1, np.uint64), np.zeros(13, np.uint64)]
+    code = ("import sys, numpy as np; sys.path.insert(0, %r); import latticeum_amd as LA\n"
+            "rng = np.random.default_rng(9)\n"
+            "xs = [rng.integers(0, LA.P, 12 * 40 + 5, dtype=np.uint64), np.full(100, LA.P - 1, np.uint64), "
+            "np.zeros(13, np.uint64)]\n"
+            "print(' '.join(str(int(v)) for x in xs for v in LA.hash_iter(x)))\n") % str(ROOT)
+    outs = []
+    for flag in ("0", "1"):
+        env = dict(os.environ, LATTICEUM_AMD_P2_SCALAR=flag)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        outs.append(r.stdout.split())
+    assert outs[0] == outs[1]
+    want = [str(int(v)) for x in xs for v in O.p2_hash_iter(x)]
+    assert outs[0] == want
