@@ -309,6 +309,8 @@ struct CcsDev {
   const uint32_t *col;
   const uint64_t *val;  // [nnz][d]
   const uint64_t *sval = nullptr;  // [nnz] when every entry is a scalar (v in every slot word 0, zero elsewhere)
+  const uint64_t *svh = nullptr;   // sval in the row-merged order (svh[k] = sval[hidx[k]])
+  const uint64_t *svc = nullptr;   // sval in the transposes' order (svc[k] = sval[cidx[k]])
   const uint64_t *hrp;  // [m + 1]
   const uint32_t *hcol;  // j n + col
   const uint32_t *hidx;  // value index

@@ -2117,12 +2117,22 @@ int lf_ccs_create(lf_ctx *c, int d, int t, size_t m, size_t n, const uint64_t *r
         }
     }
     if (scalar) {
-      std::vector<uint64_t> sv(nnz);
+      // also in the row-merged and transposed orders, so those products read them
+      // sequentially instead of gathering one word per entry through hidx / cidx
+      std::vector<uint64_t> sv(nnz), sh(nnz), sc(nnz);
       for (size_t k = 0; k < nnz; k++) sv[k] = val[k * d];
-      LF_TRY(put(sv.data(), nnz * 8, &p));
-      D.sval = (const uint64_t *)p;
-      if (repr == LF_REPR_MONTGOMERY) LF_HIP(c, lfk::mont((uint64_t *)p, nnz, false, c->cur));
-      LF_HIP(c, hipStreamSynchronize(c->cur));  // sv goes out of scope
+      for (size_t k = 0; k < nnz; k++) {
+        sh[k] = sv[hidx[k]];
+        sc[k] = sv[cidx[k]];
+      }
+      const uint64_t **dst[3] = {&D.sval, &D.svh, &D.svc};
+      const std::vector<uint64_t> *src[3] = {&sv, &sh, &sc};
+      for (int q = 0; q < 3; q++) {
+        LF_TRY(put(src[q]->data(), nnz * 8, &p));
+        *dst[q] = (const uint64_t *)p;
+        if (repr == LF_REPR_MONTGOMERY) LF_HIP(c, lfk::mont((uint64_t *)p, nnz, false, c->cur));
+      }
+      LF_HIP(c, hipStreamSynchronize(c->cur));  // the host vectors go out of scope
     }
   }
   LF_TRY(put(hrp.data(), hrp.size() * 8, &p));

@@ -41,13 +41,28 @@ __global__ void __launch_bounds__(MT) k_csr(const uint64_t *rp, size_t rp_stride
   const uint64_t *zb = z + b * z_stride + slot * TB;
   SAcc<TB> acc;
   sacc_zero(acc);
-  for (uint64_t k = rpa[r], e = rpa[r + 1]; k < e; k++) {
-    const uint64_t vi = vidx ? vidx[k] : k;
+  auto term = [&](uint64_t vi, uint32_t c) {
     if (SC)
-      sacc_smad(acc, val[vi], s_load<TB>(zb + (size_t)col[k] * d));
+      sacc_smad(acc, val[vi], s_load<TB>(zb + (size_t)c * d));
     else
-      sacc_mad(acc, s_load<TB>(val + vi * d + slot * TB), s_load<TB>(zb + (size_t)col[k] * d));
+      sacc_mad(acc, s_load<TB>(val + vi * d + slot * TB), s_load<TB>(zb + (size_t)c * d));
+  };
+  uint64_t k = rpa[r];
+  const uint64_t e = rpa[r + 1];
+  // four entries at a time: their index loads, then their value and z loads, are issued
+  // together (long rows -- the row-merged matrix, the transposes -- are load-latency bound)
+  for (; k + 4 <= e; k += 4) {
+    uint64_t vi[4];
+    uint32_t c[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      vi[u] = vidx ? vidx[k + u] : k + u;
+      c[u] = col[k + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) term(vi[u], c[u]);
   }
+  for (; k < e; k++) term(vidx ? vidx[k] : k, col[k]);
   s_store(out + task * out_stride + r * d + slot * TB, sacc_final(acc));
 }
 
@@ -135,13 +150,16 @@ __global__ void k_zero_tails(uint64_t *out, size_t len, size_t from, size_t tail
   out[i * len + from + (t - i * tail)] = 0;
 }
 
+// sv: the scalar values in this CSR's entry order (CcsDev::sval / svh / svc), read
+// without vidx; otherwise the ring values through vidx
 hipError_t csr(const CcsDev &M, const uint64_t *rp, size_t rp_stride, int na, const uint32_t *col,
-               const uint32_t *vidx, size_t nrows, const uint64_t *z, size_t z_stride, uint64_t *out,
-               size_t out_stride, int ntask, hipStream_t st, const int *sel = nullptr) {
+               const uint32_t *vidx, const uint64_t *sv, size_t nrows, const uint64_t *z, size_t z_stride,
+               uint64_t *out, size_t out_stride, int ntask, hipStream_t st, const int *sel = nullptr) {
   if (!nrows || !ntask) return hipSuccess;
   const int d = M.d, tb = slot_words(d), ns = d / tb, spb = ns < MT ? ns : MT;
   const dim3 grid(nblk(nrows, MT / spb), (unsigned)ntask, (unsigned)(ns / spb));
-  const uint64_t *val = M.sval ? M.sval : M.val;
+  const uint64_t *val = M.sval ? sv : M.val;
+  if (M.sval) vidx = nullptr;
 #define LF_CSR(TB, SC)                                                                                            \
   hipLaunchKernelGGL((k_csr<TB, SC>), grid, dim3(MT), 0, st, rp, rp_stride, na, sel, col, vidx, val, nrows, d, z, \
                      z_stride, out, out_stride, spb)
@@ -180,7 +198,7 @@ hipError_t mz_mles(const CcsDev &M, const uint64_t *z, int nz, int nv, uint64_t 
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  return csr(M, M.rp, M.m + 1, na, M.col, nullptr, M.m, z, M.n * M.d, out, len, nz * na, st, sel);
+  return csr(M, M.rp, M.m + 1, na, M.col, nullptr, M.sval, M.m, z, M.n * M.d, out, len, nz * na, st, sel);
 }
 
 hipError_t mz_challenged(const CcsDev &M, const uint64_t *z, const uint64_t *zeta, int nz, int nv, uint64_t *out,
@@ -204,12 +222,12 @@ hipError_t mz_challenged(const CcsDev &M, const uint64_t *z, const uint64_t *zet
     e = hipMemsetAsync(out + M.m * M.d, 0, (len - M.m * M.d) * 8, st);
     if (e != hipSuccess) return e;
   }
-  return csr(M, M.hrp, 0, 1, M.hcol, M.hidx, M.m, y, 0, out, 0, 1, st);
+  return csr(M, M.hrp, 0, 1, M.hcol, M.hidx, M.svh, M.m, y, 0, out, 0, 1, st);
 }
 
 hipError_t mz_weights(const CcsDev &M, const uint64_t *eq, uint64_t *w, hipStream_t st) {
   // w_j[c] = sum over column c of M_j of value (.) eq[row]
-  return csr(M, M.crp, M.n + 1, M.t, M.crow, M.cidx, M.n, eq, 0, w, M.n * M.d, M.t, st);
+  return csr(M, M.crp, M.n + 1, M.t, M.crow, M.cidx, M.svc, M.n, eq, 0, w, M.n * M.d, M.t, st);
 }
 
 hipError_t mz_evaluate(const CcsDev &M, const uint64_t *z, int nz, int nv, const uint64_t *point, uint64_t *out,

@@ -32,6 +32,9 @@ LF_AVX512 uint64_t check_ops(std::mt19937_64 &g) {
     }
     _mm512_store_si512(m, wmul8(_mm512_load_si512(a), _mm512_load_si512(b)));
     _mm512_store_si512(w, wadd8(_mm512_load_si512(a), _mm512_load_si512(b)));
+    alignas(64) uint64_t q[8];
+    _mm512_store_si512(q, wsqr8(_mm512_load_si512(a)));
+    for (int i = 0; i < 8; i++) badop += gl::canon(q[i]) != gl::mul(gl::canon(a[i]), gl::canon(a[i]));
     for (int i = 0; i < 8; i++) {
       badop += gl::canon(m[i]) != gl::canon(wmul(a[i], b[i])) ||
                gl::canon(m[i]) != gl::mul(gl::canon(a[i]), gl::canon(b[i]));
