@@ -80,9 +80,9 @@ LF_AVX512 inline __m512i wsqr8(__m512i a) {
   const __m512i r2 = _mm512_add_epi64(r, u);
   return _mm512_mask_add_epi64(r2, _mm512_cmplt_epu64_mask(r2, u), r2, M);
 }
-LF_AVX512 inline __m512i sbox8(__m512i x) {
-  const __m512i x2 = wsqr8(x), x4 = wsqr8(x2);
-  return wmul8(wmul8(x4, x2), x);
+LF_AVX512 inline __m512i sbox8(__m512i x) {  // x^3 x^4: three products deep
+  const __m512i x2 = wsqr8(x), x3 = wmul8(x2, x), x4 = wsqr8(x2);
+  return wmul8(x4, x3);
 }
 // a + b, any u64 (as wadd): a carry + EPS, which can carry once more
 LF_AVX512 inline __m512i wadd8(__m512i a, __m512i b) {

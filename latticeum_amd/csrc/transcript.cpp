@@ -73,8 +73,8 @@ inline uint64_t wmul(uint64_t a, uint64_t b) {  // any u64 in and out
 #endif
 }
 inline uint64_t sbox7(uint64_t x) {  // x^7 = x^3 x^4: three products deep, not four
-  const uint64_t x2 = wmul(x, x), x4 = wmul(x2, x2);
-  return wmul(wmul(x4, x2), x);
+  const uint64_t x2 = wmul(x, x), x3 = wmul(x2, x), x4 = wmul(x2, x2);
+  return wmul(x4, x3);
 }
 // sums of up to 16 u64 in 128 bits, folded once: x = lo + 2^64 hi, hi < 2^32
 inline uint64_t wsum(const uint64_t *v, int n) {
@@ -149,16 +149,20 @@ LF_AVX512 void permute_avx512(uint64_t *s) {
   }
   {
     const __m512i D0 = _mm512_loadu_si512(DIAG_M1), D1 = _mm512_loadu_si512(DIAG_M1 + 8);
-    uint64_t s0 = (uint64_t)_mm_cvtsi128_si64(_mm512_castsi512_si128(x0)), sl, sh;
+    uint64_t sl, sh;
     hsum_rest8(x0, x1, sl, sh);
+    // t0 = s_0 + the round's constant; the next one is y (d_0 + 1) + (rest + rc'), so the
+    // chain between S-boxes is one multiply-add (rest + rc' forms beside the S-box)
+    uint64_t t0 = wadd((uint64_t)_mm_cvtsi128_si64(_mm512_castsi512_si128(x0)), INTERNAL[0]);
     for (int r = 0; r < 22; r++) {
       const uint64_t rest = red96((u128)sl + ((u128)sh << 32));
-      s0 = sbox7(wadd(s0, INTERNAL[r]));
-      const uint64_t sum = wadd(rest, s0);
+      const uint64_t rest_rc = r + 1 < 22 ? wadd(rest, INTERNAL[r + 1]) : 0;
+      const uint64_t y = sbox7(t0);
+      const uint64_t sum = wadd(rest, y);
       const __m512i S = _mm512_set1_epi64((long long)sum);
-      x0 = wmuladd8(_mm512_mask_mov_epi64(x0, 1, _mm512_set1_epi64((long long)s0)), D0, S);
+      x0 = wmuladd8(_mm512_mask_mov_epi64(x0, 1, _mm512_set1_epi64((long long)y)), D0, S);
       x1 = wmuladd8(x1, D1, S);
-      s0 = wmuladd(s0, DIAG_M1[0], sum);
+      if (r + 1 < 22) t0 = wmuladd(y, DIAG_M1[0] + 1, rest_rc);  // y d_0 + y + rest + rc
       hsum_rest8(x0, x1, sl, sh);
     }
   }

@@ -19,6 +19,12 @@ print('value', round(b['value'],2), 'ms', round(b['ms_per_step'],3))
 for k in ('reference_ring','small_shape','configs4_d4096_kappa64'): print(k, round(b[k]['value'],1))
 fp=b['next_rows']['fold_prove']; print('fold', {k: round(v,2) if isinstance(v,float) else v for k,v in fp.items() if k.startswith('ms') or k.startswith('vars')})
 print('spans', {k: round(v,2) for k,v in fp['span_ms'].items()})
+fs=b['next_rows'].get('fold_prove_scalar')
+if fs:
+    print('fold scalar CCS', {k: round(v,2) if isinstance(v,float) else v for k,v in fs.items() if k.startswith('ms') or k.startswith('vars')})
+    print('spans scalar', {k: round(v,2) for k,v in fs['span_ms'].items()})
+    print('mz', b['next_rows']['mz_products'].get('challenged_mle_ms'), b['next_rows']['mz_products'].get('etas_ms'),
+          'scalar', b['next_rows']['mz_products_scalar'])
 ch=b['next_rows']['zkvm_chain']; print('chain', {k: (round(v,2) if isinstance(v,float) else v) for k,v in ch.items() if k not in ('workload','span_ms_per_step')})
 print('chain spans', {k: round(v,2) for k,v in ch['span_ms_per_step'].items()})
 print('cpu', b['cpu_baseline']['sample'], b['reference_ring']['cpu_baseline']['sample'])
