@@ -81,6 +81,63 @@ __global__ void k_zeta_pows(const uint64_t *zeta, int nz, int t, int d, uint64_t
   }
 }
 
+// Fq3 (d = 24): the powers with their pairwise sums, pk[j][i][slot] = (p0, p1, p2,
+// p0 + p1, p0 + p2, p1 + p2), for the Karatsuba form of k_zcomb3
+__global__ void k_zeta_pows3k(const uint64_t *zeta, int nz, int t, int d, uint64_t *pk) {
+  const int ns = d / 3;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (instance, slot)
+  if (i >= nz * ns) return;
+  const int zi = i / ns, s = i - zi * ns;
+  const Sv<3> zt = s_load<3>(zeta + (size_t)zi * d + s * 3);
+  Sv<3> p = zt;
+  for (int j = 0; j < t; j++) {
+    uint64_t *o = pk + ((size_t)j * nz + zi) * 2 * d + s * 6;
+    o[0] = p.c[0];
+    o[1] = p.c[1];
+    o[2] = p.c[2];
+    o[3] = gl::add(p.c[0], p.c[1]);
+    o[4] = gl::add(p.c[0], p.c[2]);
+    o[5] = gl::add(p.c[1], p.c[2]);
+    p = s_mul(p, zt);
+  }
+}
+// y[j][c] = sum_i pw[j][i] (.) z_i[c] in Fq3 with Karatsuba's six products per term, each
+// summed lazily over i (P_k = sum p_k z_k, Q_kl = sum (p_k + p_l)(z_k + z_l)) and combined
+// once: a1 b2 + a2 b1 = Q12 - P1 - P2 and so on; c0 = P0 + 2^40 (a1 b2 + a2 b1),
+// c1 = (a0 b1 + a1 b0) + 2^40 P2, c2 = (a0 b2 + a2 b0) + P1. Six multiply-accumulates
+// and three additions per term instead of nine and two shifts (goldilocks/mod.rs:34-54).
+__global__ void k_zcomb3k(const uint64_t *pk, const uint64_t *z, int nz, int t, size_t n, int d, uint64_t *y) {
+  const int ns = d / 3;
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // (j, c, slot)
+  if (i >= (size_t)t * n * ns) return;
+  const size_t jc = i / ns;
+  const int s = (int)(i - jc * ns);
+  const size_t j = jc / n, c = jc - j * n;
+  gl::CAcc a[6];
+#pragma unroll
+  for (int k = 0; k < 6; k++) gl::cacc_zero(a[k]);
+  for (int zi = 0; zi < nz; zi++) {
+    const uint64_t *pp = pk + (j * nz + zi) * 2 * d + s * 6;
+    const Sv<3> zv = s_load<3>(z + (zi * n + c) * d + s * 3);
+    gl::cacc_mad(a[0], pp[0], zv.c[0]);
+    gl::cacc_mad(a[1], pp[1], zv.c[1]);
+    gl::cacc_mad(a[2], pp[2], zv.c[2]);
+    gl::cacc_mad(a[3], pp[3], gl::add(zv.c[0], zv.c[1]));
+    gl::cacc_mad(a[4], pp[4], gl::add(zv.c[0], zv.c[2]));
+    gl::cacc_mad(a[5], pp[5], gl::add(zv.c[1], zv.c[2]));
+  }
+  uint64_t v[6];
+#pragma unroll
+  for (int k = 0; k < 6; k++) v[k] = gl::cacc_reduce(a[k]);
+  const uint64_t m12 = gl::sub(gl::sub(v[5], v[1]), v[2]);  // sum a1 b2 + a2 b1
+  const uint64_t m01 = gl::sub(gl::sub(v[3], v[0]), v[1]);
+  const uint64_t m02 = gl::sub(gl::sub(v[4], v[0]), v[2]);
+  uint64_t *o = y + jc * d + s * 3;
+  o[0] = gl::add(v[0], gl::shl96(m12, 40));
+  o[1] = gl::add(m01, gl::shl96(v[2], 40));
+  o[2] = gl::add(m02, v[1]);
+}
+
 // y[j][c] = sum_i pw[j][i] (.) z_i[c]
 template <int TB>
 __global__ void k_zcomb(const uint64_t *pw, const uint64_t *z, int nz, int t, size_t n, int d, uint64_t *y) {
@@ -182,7 +239,7 @@ hipError_t csr(const CcsDev &M, const uint64_t *rp, size_t rp_stride, int na, co
 
 size_t mz_scratch_elems(const CcsDev &M, int nz, int nv) {
   const size_t e = ((size_t)1 << nv) * M.d, tn = (size_t)M.t * M.n * M.d;
-  const size_t chall = (size_t)M.t * nz * M.d + tn, eval = e + tn + mz_dots_partial_elems(M, nz);
+  const size_t chall = 2 * (size_t)M.t * nz * M.d + tn, eval = e + tn + mz_dots_partial_elems(M, nz);
   return chall > eval ? chall : eval;
 }
 
@@ -206,14 +263,14 @@ hipError_t mz_challenged(const CcsDev &M, const uint64_t *z, const uint64_t *zet
   const size_t len = ((size_t)1 << nv) * M.d;
   if (M.m > ((size_t)1 << nv)) return hipErrorInvalidValue;
   const int tb = slot_words(M.d), ns = M.d / tb;
-  uint64_t *pw = scratch, *y = scratch + (size_t)M.t * nz * M.d;
+  uint64_t *pw = scratch, *y = scratch + 2 * (size_t)M.t * nz * M.d;
   if (tb == 3)
-    hipLaunchKernelGGL(k_zeta_pows<3>, dim3(nblk((size_t)nz * ns, 256)), dim3(256), 0, st, zeta, nz, M.t, M.d, pw);
+    hipLaunchKernelGGL(k_zeta_pows3k, dim3(nblk((size_t)nz * ns, 256)), dim3(256), 0, st, zeta, nz, M.t, M.d, pw);
   else
     hipLaunchKernelGGL(k_zeta_pows<1>, dim3(nblk((size_t)nz * ns, 256)), dim3(256), 0, st, zeta, nz, M.t, M.d, pw);
   const size_t ny = (size_t)M.t * M.n * ns;
   if (tb == 3)
-    hipLaunchKernelGGL(k_zcomb<3>, dim3(nblk(ny, 256)), dim3(256), 0, st, pw, z, nz, M.t, M.n, M.d, y);
+    hipLaunchKernelGGL(k_zcomb3k, dim3(nblk(ny, 256)), dim3(256), 0, st, pw, z, nz, M.t, M.n, M.d, y);
   else
     hipLaunchKernelGGL(k_zcomb<1>, dim3(nblk(ny, 256)), dim3(256), 0, st, pw, z, nz, M.t, M.n, M.d, y);
   hipError_t e = hipGetLastError();
