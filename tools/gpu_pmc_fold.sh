@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 TAG=${1:-pmcfold}
 timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
   SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_WAVES GRBM_GUI_ACTIVE -d gpurun_out/pmcs_$TAG -o run --output-format csv -- \
-  python tools/fold_prof.py > gpurun_out/pmcs_$TAG.log 2>&1
+  python tools/fold_prof.py $FOLD_ARGS > gpurun_out/pmcs_$TAG.log 2>&1
 rc=$?; echo "pmc rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python3 - <<PY
 import csv, glob, collections, re
