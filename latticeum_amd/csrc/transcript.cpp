@@ -396,11 +396,18 @@ void lf_transcript_absorb_ring(lf_transcript *t, const uint64_t *e, size_t n, in
   // fiat_shamir.rs:51-60: observe elem.0.0[0], the ark Montgomery limb
   if (t->playback) return;
   const size_t m = n * (size_t)d;
-  if (repr == LF_REPR_MONTGOMERY) {
-    for (size_t i = 0; i < m; i++) t->observe(gl::canon(e[i]));
-  } else {
-    for (size_t i = 0; i < m; i++) t->observe(gl::canon(wmul(e[i], gl::EPS)));  // gl::to_mont
-  }
+  auto limb = [repr](uint64_t x) { return gl::canon(repr == LF_REPR_MONTGOMERY ? x : wmul(x, gl::EPS)); };
+  size_t i = 0;
+  // whole rate blocks straight into the state (what observe() does 12 times: overwrite
+  // state[0..12), permute, the outputs become the sample buffer)
+  if (t->nin == 0)
+    for (; i + 12 <= m; i += 12) {
+      for (int k = 0; k < 12; k++) t->state[k] = limb(e[i + k]);
+      permute(t->state);
+      memcpy(t->out, t->state, sizeof(t->out));
+      t->nout = 12;
+    }
+  for (; i < m; i++) t->observe(limb(e[i]));
 }
 
 void lf_transcript_get_challenge(lf_transcript *t, uint64_t out3[3]) {

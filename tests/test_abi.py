@@ -93,6 +93,15 @@ def test_transcript_matches_oracle():
     ob = np.zeros(18, np.uint8)
     L.lfo_tr_squeeze_bytes(C.byref(o), ob, 18)
     assert b == ob.tobytes()
+    # absorbs that start mid-block and end mid-block, between observes and samples
+    for k, (pre, nel, dd) in enumerate([(5, 3, 24), (0, 1, 24), (11, 2, 16), (0, 5, 16), (7, 1, 1024)]):
+        for v in range(pre):
+            t.observe(100 + v)
+            L.lfo_tr_observe(C.byref(o), 100 + v)
+        x = O.fill_uniform(nel * dd, 50 + k)
+        t.absorb_ring(x, dd)
+        L.lfo_tr_absorb_ring(C.byref(o), x, nel, dd)
+        assert t.sample() == L.lfo_tr_sample(C.byref(o)), k
     # Montgomery-repr absorb is the same stream as canonical absorb
     t1, t2 = LA.Poseidon2Transcript(), LA.Poseidon2Transcript()
     t1.absorb_ring(elems, 24)
