@@ -296,7 +296,11 @@ LF_HD void cacc_mad(CAcc &a, uint64_t x, uint64_t y) {
 // against 70 for the term-by-term fold, cacc_reduce_terms)
 // (written on 32-bit carry chains: the compiler's 64-bit lowering of the same sums
 // zero-extends every limb with moves)
-LF_HD uint64_t cacc_reduce(const CAcc &a) {
+LF_HD uint64_t cacc_reduce_weak(const CAcc &a);
+LF_HD uint64_t cacc_reduce(const CAcc &a) { return canon(cacc_reduce_weak(a)); }
+// the same fold without the final canonicalisation: any u64 congruent to V (for
+// products that feed further products, which accept any u64 on this side)
+LF_HD uint64_t cacc_reduce_weak(const CAcc &a) {
   const uint32_t s0l = (uint32_t)a.s0, s0h = (uint32_t)(a.s0 >> 32), s1l = (uint32_t)a.s1,
                  s1h = (uint32_t)(a.s1 >> 32), s2l = (uint32_t)a.s2, s2h = (uint32_t)(a.s2 >> 32);
   unsigned int k1, ka, kb, kc, kd;
@@ -322,7 +326,7 @@ LF_HD uint64_t cacc_reduce(const CAcc &a) {
   uint32_t wh = __builtin_subc(vh, sc, b3, &b3);
   wl = __builtin_subc(wl, 0u - b3, 0u, &b4);
   wh = __builtin_subc(wh, 0u, b4, &b4);
-  return canon(((uint64_t)wh << 32) | wl);
+  return ((uint64_t)wh << 32) | wl;
 }
 LF_HD uint64_t cacc_reduce_terms(const CAcc &a) {
   uint64_t r = canon(a.s0);

@@ -90,6 +90,44 @@ __device__ __forceinline__ Sv<3> s_mul(const Sv<3> &a, const Sv<3> &b) {
   r.c[2] = gl::cacc_reduce(x);
   return r;
 }
+// a b with a any u64 words (weakly reduced) and b canonical, the result weakly reduced:
+// for chains of products (each output feeds the next product's left operand), with
+// one canonicalisation at the chain's end (s_canon)
+__device__ __forceinline__ Sv<1> s_mul_w(const Sv<1> &a, const Sv<1> &b) {
+  uint64_t lo, hi;
+  gl::mul_wide(a.c[0], b.c[0], lo, hi);
+  Sv<1> r;
+  r.c[0] = gl::reduce128(lo, hi);
+  return r;
+}
+__device__ __forceinline__ Sv<3> s_mul_w(const Sv<3> &a, const Sv<3> &b) {
+  const uint64_t b1n = gl::shl96(b.c[1], 40), b2n = gl::shl96(b.c[2], 40);
+  Sv<3> r;
+  gl::CAcc x;
+  gl::cacc_zero(x);
+  gl::cacc_mad(x, a.c[0], b.c[0]);
+  gl::cacc_mad(x, a.c[1], b2n);
+  gl::cacc_mad(x, a.c[2], b1n);
+  r.c[0] = gl::cacc_reduce_weak(x);
+  gl::cacc_zero(x);
+  gl::cacc_mad(x, a.c[0], b.c[1]);
+  gl::cacc_mad(x, a.c[1], b.c[0]);
+  gl::cacc_mad(x, a.c[2], b2n);
+  r.c[1] = gl::cacc_reduce_weak(x);
+  gl::cacc_zero(x);
+  gl::cacc_mad(x, a.c[0], b.c[2]);
+  gl::cacc_mad(x, a.c[1], b.c[1]);
+  gl::cacc_mad(x, a.c[2], b.c[0]);
+  r.c[2] = gl::cacc_reduce_weak(x);
+  return r;
+}
+template <int TB>
+__device__ __forceinline__ Sv<TB> s_canon(const Sv<TB> &a) {
+  Sv<TB> r;
+#pragma unroll
+  for (int i = 0; i < TB; i++) r.c[i] = gl::canon(a.c[i]);
+  return r;
+}
 // a b + u v, word by word with one reduction per word
 __device__ __forceinline__ Sv<1> s_mad2(const Sv<1> &a, const Sv<1> &b, const Sv<1> &u, const Sv<1> &v) {
   gl::CAcc x;

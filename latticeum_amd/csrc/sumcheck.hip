@@ -57,7 +57,8 @@ __global__ void k_fix_first(const uint64_t *in, size_t in_stride, const uint64_t
   const size_t m = mb / half, b = mb - m * half;
   const uint64_t *p = (ptrs ? ptrs[m] : in + m * in_stride) + 2 * b * d + s * TB;
   const Sv<TB> left = s_load<TB>(p), right = s_load<TB>(p + d);
-  s_store(out + m * out_stride + b * d + s * TB, s_add(left, s_mul(r, s_sub(right, left))));
+  // r on the right: the nonresidue shifts of its words are uniform (scalar unit), not per lane
+  s_store(out + m * out_stride + b * d + s * TB, s_add(left, s_mul(s_sub(right, left), r)));
 }
 
 // ---------------------------------------------------------------- round sums
@@ -128,7 +129,8 @@ __global__ void __launch_bounds__(RT) k_round_folding(const uint64_t *mles, size
         const uint64_t *p = pb + (size_t)(5 + f) * stride;
         const Sv<TB> a = s_load<TB>(p), st = s_sub(s_load<TB>(p + d), a);
         const Sv<TB> wf = s_load<TB>(w + (size_t)f * d + slot * TB);
-        const Sv<TB> ws = s_mul(wf, st), ws2 = s_mul(ws, st), a2 = s_mul(a, a), wa = s_mul(wf, a);
+        // ws, ws2 and wa only enter products on their left (any u64 there): weakly reduced
+        const Sv<TB> ws = s_mul_w(wf, st), ws2 = s_mul_w(ws, st), a2 = s_mul(a, a), wa = s_mul_w(wf, a);
         sacc_mad(c3, ws2, st);
         sacc_mad(c2, ws2, a);
         sacc_mad(c1, ws, s_sub(s_smul(a2, 3), s_one<TB>()));
@@ -605,12 +607,12 @@ __global__ void __launch_bounds__(RT) k_round_lin_eq(const uint64_t *mles, size_
           fac(f, a, dd);
 #pragma unroll
           for (int e = 0; e < NQ; e++) {
-            term[e] = s_mul(term[e], a);
+            term[e] = s_mul_w(term[e], a);  // weakly reduced along the chain
             if (e + 1 < NQ) a = s_add(a, dd);
           }
         }
 #pragma unroll
-        for (int e = 0; e < NQ; e++) sum[e] = s_add(sum[e], term[e]);
+        for (int e = 0; e < NQ; e++) sum[e] = s_add(sum[e], s_canon(term[e]));
       }
     }
     const Sv<TB> w = s_load<TB>(E + b * d + slot * TB);
@@ -686,12 +688,12 @@ __global__ void __launch_bounds__(RT) k_round_lin_eq_sparse(const uint64_t *cons
         fac(f, a, dd);
 #pragma unroll
         for (int e = 0; e < NQ; e++) {
-          term[e] = s_mul(term[e], a);
+          term[e] = s_mul_w(term[e], a);  // weakly reduced along the chain
           if (e + 1 < NQ) a = s_add(a, dd);
         }
       }
 #pragma unroll
-      for (int e = 0; e < NQ; e++) acc[e] = s_add(acc[e], term[e]);
+      for (int e = 0; e < NQ; e++) acc[e] = s_add(acc[e], s_canon(term[e]));
     }
   }
   block_partial<TB, NQ>(acc, spb, ppb, slot, lane_p, d, partial + (size_t)blockIdx.x * NQ * d);

@@ -145,3 +145,25 @@ def test_mz_zkvm_dimensions(ctx):
     assert torch.equal(ev, ev2)
     del out
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("d", [24, 1024])
+def test_scalar_ccs_montgomery_input(ctx, d):
+    """scalar-valued matrices handed over as Montgomery limbs (the zero-copy form of the
+    Rust structs) are still detected as scalars and give the canonical products"""
+    t, m, n, nz, nv = 4, 64, 21, 2, 6
+    mats = random_ccs(t, m, n, d, 90 + d, scalar=True)
+    mont = [(rp, col, np.array([(int(v) << 64) % LA.P for v in val], np.uint64)) for rp, col, val in mats]
+    A = LA.CCSMatrices(ctx, d, m, n, mats)
+    B = LA.CCSMatrices(ctx, d, m, n, mont, repr=LA.REPR_MONTGOMERY)
+    assert A.scalar and B.scalar
+    zd = dev(O.fill_uniform(nz * n * d, 91 + d))
+    oa, ob = dev(n=nz * t * (1 << nv) * d), dev(n=nz * t * (1 << nv) * d)
+    A.mz_mles(zd, nz, nv, oa)
+    B.mz_mles(zd, nz, nv, ob)
+    point = dev(O.fill_uniform(nv * d, 92 + d))
+    ea, eb = dev(n=nz * t * d), dev(n=nz * t * d)
+    A.mz_evaluate(zd, nz, nv, point, ea)
+    B.mz_evaluate(zd, nz, nv, point, eb)
+    ctx.sync()
+    assert np.array_equal(host(oa), host(ob)) and np.array_equal(host(ea), host(eb))

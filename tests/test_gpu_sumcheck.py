@@ -338,3 +338,15 @@ def test_folding_prove_digits_matches_materialised(ctx, d, nv, K, N):
     assert np.array_equal(got_p, want_p) and np.array_equal(got_r, want_r)
     del full
     torch.cuda.empty_cache()
+
+
+def test_linearization_prove_lin_sparse_rejects_bad_lists(ctx):
+    """act_off must start at 0, not decrease and hold at most 2^(nv-1) points per multiset"""
+    d, nv, sizes = 24, 4, [3, 1]
+    c, S, mz, beta = lin_eq_case(d, nv, sizes, 3001)
+    work = dev(n=len(mz) * (1 << (nv - 2)) * d)
+    act = dev32(np.zeros(4, np.int32))
+    for off in ([1, 2, 3], [0, 3, 2], [0, 9, 9]):
+        with pytest.raises(LA.LfError):
+            ctx.sumcheck_prove_lin_sparse(LA.Poseidon2Transcript(), LA.Comb.linearization(dev(c), S),
+                                          [dev(m) for m in mz], nv, d, 4, beta, act, np.array(off, np.uint32), work)
