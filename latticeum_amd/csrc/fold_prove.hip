@@ -13,9 +13,11 @@
 // hundred ring elements -- cross PCIe. The witnesses stay in HBM.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/lf.h"
@@ -616,34 +618,55 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
   R.h2p2d(P->pt, P->hr[0], ar.data(), (size_t)s * d);
   R.check(lf_dev_eq_table(C, d, P->pt, s, M), "eq(r_0)");
   const int G = MZ_GROUP, ng = (K + G - 1) / G;
-  auto enqueue_side = [&](int side) {
+  // The u_s groups go to the device from a second host thread (its own Run, so the
+  // error state is not shared): with the stream's queue deep, every enqueue blocks the
+  // calling thread for tens of microseconds, which the transcript thread would
+  // otherwise spend before and between its absorbs. `posted` counts the groups whose
+  // event is recorded; the absorb loop waits on a group's event only after that.
+  const bool digits = P->pr.b_small == 2;  // f_hat values in {-1, 0, 1}: read from the coefficient rows
+  std::atomic<int> posted{0};
+  Run RE = R;
+  auto enqueue_side = [&](Run &Q, int side) {
     const uint64_t *eq_s = M + (size_t)(2 * side) * mstride;
-    R.check(lf_dev_fhat_evaluate_eq(C, d, P->fkc[side], N, ND, K, s, eq_s, P->vs + (size_t)side * K * tau * d), "v_s");
-    R.d2p(P->hx[side], P->xs + (size_t)side * K * (l + 1) * d, (size_t)K * (l + 1) * d);
-    R.d2p(P->hy[side], P->y[side], (size_t)K * kd);
-    R.d2p(P->hv[side], P->vs + (size_t)side * K * tau * d, (size_t)K * tau * d);
-    R.check(lf_dev_mz_weights(C, P->ccs, s, eq_s, P->mzw), "u_s weights");
+    Q.check(lf_dev_fhat_evaluate_eq(C, d, P->fkc[side], N, ND, K, s, eq_s, P->vs + (size_t)side * K * tau * d), "v_s");
+    Q.d2p(P->hx[side], P->xs + (size_t)side * K * (l + 1) * d, (size_t)K * (l + 1) * d);
+    Q.d2p(P->hy[side], P->y[side], (size_t)K * kd);
+    Q.d2p(P->hv[side], P->vs + (size_t)side * K * tau * d, (size_t)K * tau * d);
+    Q.check(lf_dev_mz_weights(C, P->ccs, s, eq_s, P->mzw), "u_s weights");
     for (int g = 0; g < ng; g++) {
       const int k0 = g * G, nk = std::min(G, K - k0);
       uint64_t *us = P->us + ((size_t)side * K + k0) * t * d;
-      R.check(lf_dev_mz_dots(C, P->ccs, P->mzw, P->zdec[side] + (size_t)k0 * n * d, nk, us), "u_s");
-      R.d2p(P->hu[side] + (size_t)k0 * t * d, us, (size_t)nk * t * d);
-      R.hip(hipEventRecord(P->ev[2 + side * ng + g], R.st), "event");
+      Q.check(lf_dev_mz_dots(C, P->ccs, P->mzw, P->zdec[side] + (size_t)k0 * n * d, nk, us), "u_s");
+      Q.d2p(P->hu[side] + (size_t)k0 * t * d, us, (size_t)nk * t * d);
+      Q.hip(hipEventRecord(P->ev[2 + side * ng + g], Q.st), "event");
+      posted.store(side * ng + g + 1, std::memory_order_release);
     }
   };
-  // both sides and the f_hat MLEs enqueued up front (enqueueing side 1 from inside the
-  // absorb loop measured 1.2 ms slower: the host then waits on the queue mid-hash)
-  enqueue_side(0);
-  enqueue_side(1);
-  const bool digits = P->pr.b_small == 2;  // f_hat values in {-1, 0, 1}: read from the coefficient rows
-  if (!digits)
-    for (int sd = 0; sd < 2; sd++)
-      R.hip(lfk::get_fhat(P->fkc[sd], N, d, s, M + (5 + (size_t)sd * K * tau) * mstride, R.st, K, ND), "f_hat");
-  if (R.rc) return R.rc;
+  std::thread enq([&] {
+    (void)hipSetDevice(P->device);
+    if (RE.rc == LF_OK) {
+      enqueue_side(RE, 0);
+      enqueue_side(RE, 1);
+      if (!digits)
+        for (int sd = 0; sd < 2; sd++)
+          RE.hip(lfk::get_fhat(P->fkc[sd], N, d, s, M + (5 + (size_t)sd * K * tau) * mstride, RE.st, K, ND), "f_hat");
+    }
+    posted.store(1 << 30, std::memory_order_release);  // done (also on an error)
+  });
+  auto join = [&] {
+    if (enq.joinable()) enq.join();
+    if (RE.rc != LF_OK && R.rc == LF_OK) R.rc = RE.rc;
+    return R.rc;
+  };
   R.mark(LF_SPAN_DECOMPOSITION, false);
   for (int side = 0; side < 2; side++)
     for (int k = 0; k < K; k++) {  // the decomposed instances' messages (:58-64)
-      if (k % G == 0 && R.wait(P->ev[2 + side * ng + k / G])) return R.rc;
+      if (k % G == 0) {
+        const int g = side * ng + k / G;
+        while (posted.load(std::memory_order_acquire) <= g) std::this_thread::yield();
+        if (posted.load(std::memory_order_acquire) >= (1 << 30) && RE.rc != LF_OK) return join();
+        if (R.wait(P->ev[2 + g])) return join();
+      }
       const size_t ox = (size_t)k * (l + 1) * d, oy = (size_t)k * kd, ou = (size_t)k * t * d, ov = (size_t)k * tau * d;
       memcpy(proof->x_s[side] + ox, P->hx[side] + ox, (l + 1) * d * 8);
       memcpy(proof->y_s[side] + oy, P->hy[side] + oy, kd * 8);
@@ -653,9 +676,8 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
       R.absorb(proof->y_s[side] + oy, kappa);
       R.absorb(proof->u_s[side] + ou, t);
       R.absorb(proof->v_s[side] + ov, tau);
-
     }
-
+  if (join()) return R.rc;
   R.mark(LF_SPAN_DECOMPOSITION_TRANSCRIPT, false);
   // ---- folding (folding.rs:42-130)
   R.absorb_label("alpha_s");  // squeeze_alpha_beta_zeta_mu (folding/utils.rs:51-96)
@@ -732,29 +754,45 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
   R.d2p(P->htheta, P->theta, 2 * (size_t)K * tau * d);
   R.hip(hipEventRecord(P->ev[0], R.st), "event");
   R.check(lf_dev_mz_weights(C, P->ccs, s, P->eq0, P->mzw), "eta weights");
-  auto enqueue_eta = [&](int side) {  // instance groups of one side, in absorb order
-    for (int gg = 0; gg < ng; gg++) {
-      const int g = side * ng + gg, k0 = gg * G, nk = std::min(G, K - k0);
-      const size_t o = ((size_t)side * K + k0) * t * d;
-      R.check(lf_dev_mz_dots(C, P->ccs, P->mzw, P->zdec[side] + (size_t)k0 * n * d, nk, P->eta + o), "eta");
-      R.d2p(P->heta + o, P->eta + o, (size_t)nk * t * d);
-      R.hip(hipEventRecord(P->ev[2 + g], R.st), "event");
-    }
-  };
-  enqueue_eta(0);
   if (R.rc) return R.rc;
+  // the eta_s groups of both sides from a second host thread, as the u_s groups above
+  std::atomic<int> eposted{0};
+  Run RQ = R;
+  std::thread eenq([&] {
+    (void)hipSetDevice(P->device);
+    for (int side = 0; side < 2 && RQ.rc == LF_OK; side++)
+      for (int gg = 0; gg < ng; gg++) {  // instance groups in absorb order
+        const int g = side * ng + gg, k0 = gg * G, nk = std::min(G, K - k0);
+        const size_t o = ((size_t)side * K + k0) * t * d;
+        RQ.check(lf_dev_mz_dots(C, P->ccs, P->mzw, P->zdec[side] + (size_t)k0 * n * d, nk, P->eta + o), "eta");
+        RQ.d2p(P->heta + o, P->eta + o, (size_t)nk * t * d);
+        RQ.hip(hipEventRecord(P->ev[2 + g], RQ.st), "event");
+        eposted.store(g + 1, std::memory_order_release);
+      }
+    eposted.store(1 << 30, std::memory_order_release);
+  });
+  auto ejoin = [&] {
+    if (eenq.joinable()) eenq.join();
+    if (RQ.rc != LF_OK && R.rc == LF_OK) R.rc = RQ.rc;
+    return R.rc;
+  };
   R.mark(LF_SPAN_EVALUATIONS, false);
-  if (R.wait(P->ev[0])) return R.rc;
+  if (R.wait(P->ev[0])) return ejoin();
   memcpy(proof->theta_s, P->htheta, 2 * (size_t)K * tau * d * 8);
   for (int i = 0; i < 2 * K; i++) R.absorb(proof->theta_s + (size_t)i * tau * d, tau);
-  enqueue_eta(1);  // while the host absorbs side 0's eta_s
   for (int side = 0; side < 2; side++)
     for (int k = 0; k < K; k++) {
-      if (k % G == 0 && R.wait(P->ev[2 + side * ng + k / G])) return R.rc;
+      if (k % G == 0) {
+        const int g = side * ng + k / G;
+        while (eposted.load(std::memory_order_acquire) <= g) std::this_thread::yield();
+        if (eposted.load(std::memory_order_acquire) >= (1 << 30) && RQ.rc != LF_OK) return ejoin();
+        if (R.wait(P->ev[2 + g])) return ejoin();
+      }
       const size_t o = ((size_t)side * K + k) * t * d;
       memcpy(proof->eta_s + o, P->heta + o, (size_t)t * d * 8);
       R.absorb(proof->eta_s + o, t);
     }
+  if (ejoin()) return R.rc;
   // get_rhos (folding/utils.rs:116-127): 2K - 1 short challenges and ONE, then CRT
   R.absorb_label("rho_s");
   std::vector<uint64_t> rc(2 * (size_t)K * d, 0);
