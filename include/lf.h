@@ -463,6 +463,11 @@ int lf_dev_mz_mles_sel(lf_ctx *ctx, const lf_ccs *M, const uint64_t *z, const in
                        uint64_t *out);
 int lf_dev_mz_challenged(lf_ctx *ctx, const lf_ccs *M, const uint64_t *z, const uint64_t *zeta, int nz, int nv,
                          uint64_t *out);
+/* two lf_dev_mz_challenged at once (the folding prover's g1 and g3 parts, one per
+ * decomposed side), reading the matrices' entries once for both */
+int lf_dev_mz_challenged_pair(lf_ctx *ctx, const lf_ccs *M, const uint64_t *z0, const uint64_t *zeta0,
+                              const uint64_t *z1, const uint64_t *zeta1, int nz, int nv, uint64_t *out0,
+                              uint64_t *out1);
 int lf_dev_mz_evaluate(lf_ctx *ctx, const lf_ccs *M, const uint64_t *z, int nz, int nv, const uint64_t *point,
                        uint64_t *out);
 /* lf_dev_mz_evaluate in two halves, so one point's weights serve several z sets:

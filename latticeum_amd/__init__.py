@@ -529,6 +529,11 @@ class CCSMatrices:
     def mz_challenged(self, z, zeta, nz: int, nv: int, out):
         self.ctx.check(self.lib.lf_dev_mz_challenged(self.ctx.h, self.h, _dptr(z), _dptr(zeta), nz, nv, _dptr(out)))
 
+    def mz_challenged_pair(self, z0, zeta0, z1, zeta1, nz: int, nv: int, out0, out1):
+        """two challenged Mz MLEs over one pass of the matrices (lf_dev_mz_challenged_pair)"""
+        self.ctx.check(self.lib.lf_dev_mz_challenged_pair(self.ctx.h, self.h, _dptr(z0), _dptr(zeta0), _dptr(z1),
+                                                          _dptr(zeta1), nz, nv, _dptr(out0), _dptr(out1)))
+
     def mz_evaluate(self, z, nz: int, nv: int, point, out):
         self.ctx.check(self.lib.lf_dev_mz_evaluate(self.ctx.h, self.h, _dptr(z), nz, nv, _dptr(point), _dptr(out)))
 

@@ -206,6 +206,7 @@ SIGNATURES = {
     "lf_dev_mz_mles": (I, [VP, VP, VP, I, I, VP]),
     "lf_dev_mz_mles_sel": (I, [VP, VP, VP, VP, I, I, VP]),
     "lf_dev_mz_challenged": (I, [VP, VP, VP, VP, I, I, VP]),
+    "lf_dev_mz_challenged_pair": (I, [VP, VP, VP, VP, VP, VP, I, I, VP, VP]),
     "lf_dev_mz_evaluate": (I, [VP, VP, VP, I, I, VP, VP]),
     "lf_ccs_weights_len": (SZ, [VP]),
     "lf_dev_mz_weights": (I, [VP, VP, I, VP, VP]),

@@ -712,9 +712,12 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
   // (Witness::get_fhat of the decomposed witnesses) are not materialised for B_SMALL = 2 --
   // their values are the digits of the coefficient rows P->fkc, which g1 / g3 and the
   // sumcheck's first round read directly (lf_sumcheck_prove_fold_digits)
+  // both sides' challenged Mz MLEs in one pass over the matrices (g1, g3 slots)
+  R.check(lf_dev_mz_challenged_pair(C, P->ccs, P->zdec[0], P->zeta, P->zdec[1], P->zeta + (size_t)K * d, K, s,
+                                    M + mstride, M + 3 * mstride),
+          "challenged Mz");
   for (int side = 0; side < 2; side++) {
     uint64_t *g = M + (size_t)(2 * side + 1) * mstride;
-    R.check(lf_dev_mz_challenged(C, P->ccs, P->zdec[side], P->zeta + (size_t)side * K * d, K, s, g), "challenged Mz");
     if (digits)
       R.hip(lfk::fhat_lincomb_digits(P->fkc[side], K, N, ND, P->coef[side], s, d, g, R.st), "g");
     else

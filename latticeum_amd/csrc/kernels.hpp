@@ -324,6 +324,11 @@ size_t mz_scratch_elems(const CcsDev &M, int nz, int nv);
 hipError_t mz_mles(const CcsDev &M, const uint64_t *z, int nz, int nv, uint64_t *out, hipStream_t st,
                    const int *sel = nullptr, int nsel = 0);
 // out [2^nv][d] = sum_i sum_j zeta_i^(j+1) MLE(M_j z_i)
+// mz_challenged for two (z, zeta) at once over one pass of the row-merged matrix;
+// scratch: 2 (2 t nz d + t n d) elements
+hipError_t mz_challenged_pair(const CcsDev &M, const uint64_t *z0, const uint64_t *zeta0, const uint64_t *z1,
+                              const uint64_t *zeta1, int nz, int nv, uint64_t *out0, uint64_t *out1,
+                              uint64_t *scratch, hipStream_t st);
 hipError_t mz_challenged(const CcsDev &M, const uint64_t *z, const uint64_t *zeta, int nz, int nv, uint64_t *out,
                          uint64_t *scratch, hipStream_t st);
 // out [nz][t][d] = MLE(M_j z_i)(point)

@@ -2191,6 +2191,18 @@ int lf_dev_mz_challenged(lf_ctx *c, const lf_ccs *M, const uint64_t *z, const ui
   return LF_OK;
 }
 
+int lf_dev_mz_challenged_pair(lf_ctx *c, const lf_ccs *M, const uint64_t *z0, const uint64_t *zeta0,
+                              const uint64_t *z1, const uint64_t *zeta1, int nz, int nv, uint64_t *out0,
+                              uint64_t *out1) {
+  if (!c || !z0 || !zeta0 || !z1 || !zeta1 || !out0 || !out1) return LF_ERR_INVALID_ARG;
+  DevGuard g(c);
+  LF_TRY(mz_check(c, M, nz, nv));
+  const lfk::CcsDev &D = M->dev;
+  LF_TRY(grow(c, c->tmp, c->tmp_elems, 2 * (2 * (size_t)D.t * nz * D.d + (size_t)D.t * D.n * D.d)));
+  LF_HIP(c, lfk::mz_challenged_pair(D, z0, zeta0, z1, zeta1, nz, nv, out0, out1, c->tmp, c->cur));
+  return LF_OK;
+}
+
 int lf_dev_mz_evaluate(lf_ctx *c, const lf_ccs *M, const uint64_t *z, int nz, int nv, const uint64_t *point,
                        uint64_t *out) {
   if (!c || !z || !point || !out) return LF_ERR_INVALID_ARG;

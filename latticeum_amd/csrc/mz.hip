@@ -66,6 +66,50 @@ __global__ void __launch_bounds__(MT) k_csr(const uint64_t *rp, size_t rp_stride
   s_store(out + task * out_stride + r * d + slot * TB, sacc_final(acc));
 }
 
+// Two challenged products over the same rows (the folding prover's g1 and g3, one per
+// decomposed side): each entry's index and value are read once for both
+template <int TB, bool SC>
+__global__ void __launch_bounds__(MT) k_csr_pair(const uint64_t *rp, const uint32_t *col, const uint32_t *vidx,
+                                                const uint64_t *val, size_t nrows, int d, const uint64_t *z0,
+                                                const uint64_t *z1, uint64_t *out0, uint64_t *out1, int spb) {
+  const int slot_l = threadIdx.x % spb, lane_r = threadIdx.x / spb, rpb = MT / spb;
+  const int slot = blockIdx.z * spb + slot_l;
+  const size_t r = (size_t)blockIdx.x * rpb + lane_r;
+  if (r >= nrows) return;
+  const uint64_t *zb0 = z0 + slot * TB, *zb1 = z1 + slot * TB;
+  SAcc<TB> a0, a1;
+  sacc_zero(a0);
+  sacc_zero(a1);
+  auto term = [&](uint64_t vi, uint32_t c) {
+    const Sv<TB> y0 = s_load<TB>(zb0 + (size_t)c * d), y1 = s_load<TB>(zb1 + (size_t)c * d);
+    if (SC) {
+      const uint64_t v = val[vi];
+      sacc_smad(a0, v, y0);
+      sacc_smad(a1, v, y1);
+    } else {
+      const Sv<TB> v = s_load<TB>(val + vi * d + slot * TB);
+      sacc_mad(a0, v, y0);
+      sacc_mad(a1, v, y1);
+    }
+  };
+  uint64_t k = rp[r];
+  const uint64_t e = rp[r + 1];
+  for (; k + 4 <= e; k += 4) {
+    uint64_t vi[4];
+    uint32_t c[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      vi[u] = vidx ? vidx[k + u] : k + u;
+      c[u] = col[k + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) term(vi[u], c[u]);
+  }
+  for (; k < e; k++) term(vidx ? vidx[k] : k, col[k]);
+  s_store(out0 + r * d + slot * TB, sacc_final(a0));
+  s_store(out1 + r * d + slot * TB, sacc_final(a1));
+}
+
 // pw[j][i] = zeta_i^(j+1)
 template <int TB>
 __global__ void k_zeta_pows(const uint64_t *zeta, int nz, int t, int d, uint64_t *pw) {
@@ -280,6 +324,58 @@ hipError_t mz_challenged(const CcsDev &M, const uint64_t *z, const uint64_t *zet
     if (e != hipSuccess) return e;
   }
   return csr(M, M.hrp, 0, 1, M.hcol, M.hidx, M.svh, M.m, y, 0, out, 0, 1, st);
+}
+
+hipError_t mz_challenged_pair(const CcsDev &M, const uint64_t *z0, const uint64_t *zeta0, const uint64_t *z1,
+                              const uint64_t *zeta1, int nz, int nv, uint64_t *out0, uint64_t *out1,
+                              uint64_t *scratch, hipStream_t st) {
+  const size_t len = ((size_t)1 << nv) * M.d;
+  if (M.m > ((size_t)1 << nv)) return hipErrorInvalidValue;
+  const int tb = slot_words(M.d), ns = M.d / tb;
+  const size_t per = 2 * (size_t)M.t * nz * M.d + (size_t)M.t * M.n * M.d;  // pw | y of one side
+  const uint64_t *zs[2] = {z0, z1}, *zetas[2] = {zeta0, zeta1};
+  uint64_t *ys[2], *outs[2] = {out0, out1};
+  for (int q = 0; q < 2; q++) {
+    uint64_t *pw = scratch + q * per, *y = pw + 2 * (size_t)M.t * nz * M.d;
+    ys[q] = y;
+    if (tb == 3)
+      hipLaunchKernelGGL(k_zeta_pows3k, dim3(nblk((size_t)nz * ns, 256)), dim3(256), 0, st, zetas[q], nz, M.t, M.d, pw);
+    else
+      hipLaunchKernelGGL(k_zeta_pows<1>, dim3(nblk((size_t)nz * ns, 256)), dim3(256), 0, st, zetas[q], nz, M.t, M.d,
+                         pw);
+    const size_t ny = (size_t)M.t * M.n * ns;
+    if (tb == 3)
+      hipLaunchKernelGGL(k_zcomb3k, dim3(nblk(ny, 256)), dim3(256), 0, st, pw, zs[q], nz, M.t, M.n, M.d, y);
+    else
+      hipLaunchKernelGGL(k_zcomb<1>, dim3(nblk(ny, 256)), dim3(256), 0, st, pw, zs[q], nz, M.t, M.n, M.d, y);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (len > M.m * M.d) {
+      e = hipMemsetAsync(outs[q] + M.m * M.d, 0, (len - M.m * M.d) * 8, st);
+      if (e != hipSuccess) return e;
+    }
+  }
+  if (!M.m) return hipSuccess;
+  const int spb = ns < MT ? ns : MT;
+  const dim3 grid(nblk(M.m, MT / spb), 1, (unsigned)(ns / spb));
+  const uint64_t *val = M.sval ? M.svh : M.val;
+  const uint32_t *vidx = M.sval ? nullptr : M.hidx;
+#define LF_CSRP(TB, SC)                                                                                       \
+  hipLaunchKernelGGL((k_csr_pair<TB, SC>), grid, dim3(MT), 0, st, M.hrp, M.hcol, vidx, val, M.m, M.d, ys[0], ys[1], \
+                     out0, out1, spb)
+  if (tb == 3) {
+    if (M.sval)
+      LF_CSRP(3, true);
+    else
+      LF_CSRP(3, false);
+  } else {
+    if (M.sval)
+      LF_CSRP(1, true);
+    else
+      LF_CSRP(1, false);
+  }
+#undef LF_CSRP
+  return hipGetLastError();
 }
 
 hipError_t mz_weights(const CcsDev &M, const uint64_t *eq, uint64_t *w, hipStream_t st) {

@@ -96,6 +96,16 @@ def test_mz_products_match_oracle(ctx, d, scalar):
     M.mz_challenged(zd, dev(zeta), nz, nv, ch)
     ctx.sync()
     assert np.array_equal(host(ch), O.mz_challenged(mats, zs, [zeta[i * d:(i + 1) * d] for i in range(nz)], nv, d))
+    # the pair form: a second (z, zeta) beside the first, one pass over the entries
+    zs2 = [O.fill_uniform(n * d, 150 + d + i) for i in range(nz)]
+    zeta2 = O.fill_uniform(nz * d, 160 + d)
+    c0, c1 = dev(n=(1 << nv) * d), dev(n=(1 << nv) * d)
+    ctx.dev_fill_uniform(c0, 5)
+    ctx.dev_fill_uniform(c1, 6)  # padding rows zeroed over stale data
+    M.mz_challenged_pair(zd, dev(zeta), dev(np.concatenate(zs2)), dev(zeta2), nz, nv, c0, c1)
+    ctx.sync()
+    assert np.array_equal(host(c0), host(ch))
+    assert np.array_equal(host(c1), O.mz_challenged(mats, zs2, [zeta2[i * d:(i + 1) * d] for i in range(nz)], nv, d))
     point = O.fill_uniform(nv * d, 70 + d)
     ev = dev(n=nz * t * d)
     M.mz_evaluate(zd, nz, nv, dev(point), ev)
