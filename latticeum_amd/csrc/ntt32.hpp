@@ -151,6 +151,40 @@ __device__ __forceinline__ void transpose_inv(uint64_t *v, uint64_t *lds, int r)
   wave_lds_sync();
 }
 
+// The same two transposes through a 32-bit tile (the low words, then the high
+// words): half the LDS per half-wave, for kernels whose occupancy the LDS bounds
+constexpr int HALF_U32 = 32 * RS;  // u32 scratch per half-wave
+// (the transposed low words go into the low halves of v, which the first pass
+// has already written out, so no extra registers)
+__device__ __forceinline__ void transpose_fwd_w(uint64_t *v, uint32_t *lds, int r) {
+#pragma unroll
+  for (int i = 0; i < 32; i++) lds[brv5(i) * RS + r] = (uint32_t)v[i];
+  wave_lds_sync();
+#pragma unroll
+  for (int j = 0; j < 32; j++) v[j] = (v[j] & 0xFFFFFFFF00000000ull) | lds[r * RS + j];  // new low, old high
+  wave_lds_sync();
+#pragma unroll
+  for (int i = 0; i < 32; i++) lds[brv5(i) * RS + r] = (uint32_t)(v[i] >> 32);
+  wave_lds_sync();
+#pragma unroll
+  for (int j = 0; j < 32; j++) v[j] = ((uint64_t)lds[r * RS + j] << 32) | (uint32_t)v[j];
+  wave_lds_sync();
+}
+__device__ __forceinline__ void transpose_inv_w(uint64_t *v, uint32_t *lds, int r) {
+#pragma unroll
+  for (int i = 0; i < 32; i++) lds[brv5(i) * RS + r] = (uint32_t)v[i];
+  wave_lds_sync();
+#pragma unroll
+  for (int i = 0; i < 32; i++) v[i] = (v[i] & 0xFFFFFFFF00000000ull) | lds[r * RS + brv5(i)];
+  wave_lds_sync();
+#pragma unroll
+  for (int i = 0; i < 32; i++) lds[brv5(i) * RS + r] = (uint32_t)(v[i] >> 32);
+  wave_lds_sync();
+#pragma unroll
+  for (int i = 0; i < 32; i++) v[i] = ((uint64_t)lds[r * RS + brv5(i)] << 32) | (uint32_t)v[i];
+  wave_lds_sync();
+}
+
 // middle factors: v[i] *= mid[r][i]. The 32 x 32 table is staged once per
 // block into LDS as midT[i][r] (conflict-free column reads; LDS waits do not
 // drain the wave's outstanding global stores the way a vmcnt wait would).
@@ -185,6 +219,19 @@ __device__ __forceinline__ void forward(uint64_t *v, const uint64_t *mid, uint64
   mul_mid(v, mid, r);
   transpose_fwd(v, lds, r);
   cyc_dif32<false>(v);
+}
+// forward / inverse with the 32-bit-tile transposes
+__device__ __forceinline__ void forward_w(uint64_t *v, const uint64_t *mid, uint32_t *lds, int r) {
+  neg_ct32(v);
+  mul_mid(v, mid, r);
+  transpose_fwd_w(v, lds, r);
+  cyc_dif32<false>(v);
+}
+__device__ __forceinline__ void inverse_w(uint64_t *v, const uint64_t *mid_inv, uint32_t *lds, int r) {
+  cyc_dif32<true>(v);
+  mul_mid(v, mid_inv, r);
+  transpose_inv_w(v, lds, r);
+  neg_gs32_inv(v);
 }
 // inverse from slot input layout v[m2] = X[r + 32 m2] to coefficient layout
 __device__ __forceinline__ void inverse(uint64_t *v, const uint64_t *mid_inv, uint64_t *lds, int r) {
