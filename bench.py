@@ -74,6 +74,9 @@ def parse():
                          "launch (lf_dev_fold_step_batch: one pass over A for the group); 1: all streams")
     ap.add_argument("--cpu-baseline", dest="cpu", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu", action="store_false")
+    ap.add_argument("--detail", default=DETAIL_DEFAULT,
+                    help="file for the full record (every side workload and phase); the printed line is the compact "
+                         "headline, which names this file")
     return ap.parse_args()
 
 
@@ -121,7 +124,8 @@ def step_hbm(d, W, kappa, group, phases, value_per_gpu, L=5, K=15):
     tr = [p.get("traffic_bytes_per_launch") for p in phases.values()]
     pmc = None if not tr or any(t is None for t in tr) else \
         sum(p["traffic_bytes_per_launch"] * p["launches_per_step"] for p in phases.values())
-    out = {"survey_bytes_per_step": survey, "needed_bytes_per_step": needed, "steps_per_A_read": max(1, group),
+    out = {"survey_bytes_per_step": survey, "survey_frac_hbm": survey * value_per_gpu / 1e9 / HBM_PEAK_GBS,
+           "needed_bytes_per_step": needed, "steps_per_A_read": max(1, group),
            "needed_gbs": needed * value_per_gpu / 1e9, "needed_frac_hbm": needed * value_per_gpu / 1e9 / HBM_PEAK_GBS,
            "pmc_bytes_per_step": pmc}
     if pmc is not None:
@@ -180,20 +184,46 @@ def by_base(t, kern):
         t[base] = t[max(ks, key=lambda k: kern[k].get("launches", 0))]
 
 
+def kernel_source_hash():
+    """sha256 (12 hex digits) over the product's device and host sources
+    (latticeum_amd/csrc): the PMC files carry the hash of the code they were
+    collected on, and bench.py uses a file only while the sources still hash
+    the same (no git on the GPU box, so not the revision)."""
+    import hashlib
+    h = hashlib.sha256()
+    src = ROOT / "latticeum_amd" / "csrc"
+    for p in sorted(src.iterdir()):
+        if p.suffix in (".hip", ".hpp", ".cpp", ".inc", ".h"):
+            h.update(p.name.encode())
+            h.update(p.read_bytes())
+    return h.hexdigest()[:12]
+
+
+_PMC_STALE = set()
+
+
+def _pmc_doc(kind, d, W, kappa):
+    """profiles/pmc_<kind>_d<d>_W<W>_k<kappa>.json when it is this configuration's
+    and was collected on the current kernel sources; None otherwise (a stale file
+    is recorded in _PMC_STALE and reported as such, never paired with new timings)"""
+    name = f"pmc_{kind}_d{d}_W{W}_k{kappa}.json"
+    try:
+        doc = json.loads((ROOT / "profiles" / name).read_text())
+    except (OSError, ValueError):
+        return None
+    if doc.get("config") != {"d": d, "W": W, "kappa": kappa}:
+        return None
+    if doc.get("src_hash") != kernel_source_hash():
+        _PMC_STALE.add(name)
+        return None
+    return doc
+
+
 def load_traffic(d, W, kappa):
     """PMC-measured HBM bytes per launch (profiles/pmc_traffic_d<d>_W<W>_k<kappa>.json, written by
     tools/prof_summary.py traffic from separate FETCH_SIZE / WRITE_SIZE passes of
-    this same configuration); {} when absent or for another configuration."""
-    doc = None
-    # the configuration's own file (tools/gpu_evidence.sh writes one per bench line)
-    for name in (f"pmc_traffic_d{d}_W{W}_k{kappa}.json",):
-        try:
-            cand = json.loads((ROOT / "profiles" / name).read_text())
-        except (OSError, ValueError):
-            continue
-        if cand.get("config") == {"d": d, "W": W, "kappa": kappa}:
-            doc = cand
-            break
+    this same configuration on the same kernel sources); {} otherwise."""
+    doc = _pmc_doc("traffic", d, W, kappa)
     if doc is None:
         return {}
     kern = doc.get("kernels", {})
@@ -208,16 +238,8 @@ def load_traffic(d, W, kappa):
 
 def load_sq(d, W, kappa):
     """PMC-measured VALU busy fraction per kernel (profiles/pmc_sq_d<d>_W<W>_k<kappa>.json, written by
-    tools/prof_summary.py sq from one SQ pass of this configuration); {} otherwise."""
-    doc = None
-    for name in (f"pmc_sq_d{d}_W{W}_k{kappa}.json",):
-        try:
-            cand = json.loads((ROOT / "profiles" / name).read_text())
-        except (OSError, ValueError):
-            continue
-        if cand.get("config") == {"d": d, "W": W, "kappa": kappa}:
-            doc = cand
-            break
+    tools/prof_summary.py sq from one SQ pass of this configuration on the same kernel sources); {} otherwise."""
+    doc = _pmc_doc("sq", d, W, kappa)
     if doc is None:
         return {}
     kern = doc.get("kernels", {})
@@ -299,6 +321,7 @@ def cpu_baseline(d, W_full, kappa):
     return {"value": v_all, "unit": "fold-steps/s", "cores": cores, "kind": "port",
             "sample": f"1 step at W={w_all} on {cores} threads ({t_all:.2f} s; {scaled(w_all)}) and at W={w_one} on "
                       f"1 thread ({t_one:.2f} s; {scaled(w_one)}), d={d}, kappa={kappa}",
+            "sample_short": f"oracle C step, W={w_all} on {cores} threads ({t_all:.1f} s), x{W_full / w_all:g} in W",
             "host": cpu_limits(),
             "single_core": {"value": v_one, "cores": 1}}
 
@@ -681,6 +704,7 @@ def sharded_fold(LA, torch, LD, pg, local, rank, world, d, W, kappa, steps, warm
     transport) on the step's stream (lf_dev_fold_step_sharded)."""
     wl = Workload(LA, torch, local, rank, d, W, kappa, 1, seed_a=SEED_A + 7919 * rank)
     comm = LD.make_comm(wl.ctxs[0], pg, world, rank)
+    comm_size = comm.size if comm is not None else 1  # the rank count RCCL reports (lf_comm_size)
     try:
         dt, (phases, roof) = measure(LA, torch, LD, pg, world, wl, steps, warmup, comm)
     finally:
@@ -705,7 +729,7 @@ def sharded_fold(LA, torch, LD, pg, local, rank, world, d, W, kappa, steps, warm
             "value": steps / dt, "unit": "sharded fold-steps/s", "shard_steps_per_s": world * steps / dt,
             "n_gpus": world, "steps": steps, "ms_per_step": dt / steps * 1e3, "scaling": "weak",
             "roofline": roof, "phases": phases,
-            "verified": verified,
+            "verified": verified, "comm_size": comm_size,
             "verification": f"after timing, every rank's shard of a {world} x 64-group fold through the same RCCL "
                             f"exchange equals the unsharded fold on its GPU, every output bit for bit "
                             f"(latticeum_amd.dist.verify_sharded_step)"}
@@ -1112,6 +1136,119 @@ def zkvm_chain(LA, torch, ctx, M, S, d, n, t, m, steps=16, warmup=2):
 
 EXCLUDED = ("outside the timed step (other tiers): the Poseidon2 transcript and challenge derivation (rho is an "
             "input), linearization, the sumcheck provers and the Mz matrix-vector products")
+EXCLUDED_SHORT = "rho is an input; transcript, linearization, sumchecks, Mz outside the step"
+LINE_LIMIT = 4000  # bytes: the driver keeps only the tail of stdout, so the headline line stays small
+DETAIL_DEFAULT = "gpurun_out/bench_detail.json"
+
+
+def _sig(x, n=4):
+    """floats to n significant digits, recursively (the compact line)"""
+    if isinstance(x, float):
+        return float(f"{x:.{n}g}")
+    if isinstance(x, dict):
+        return {k: _sig(v, n) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_sig(v, n) for v in x]
+    return x
+
+
+def _phase_row(p):
+    """one phase of the compact line: [kernel, ms per step, frac of HBM, PMC bytes per launch, VALU busy]"""
+    return [p["kernel"], p["ms_per_step"], p["frac_hbm"], p.get("traffic_bytes_per_launch"), p.get("valu_busy")]
+
+
+def _side_value(s):
+    if not isinstance(s, dict):
+        return None
+    r = s.get("roofline") or {}
+    return {"value": s.get("value"), "ms": s.get("ms_per_step_per_gpu"), "frac": r.get("frac"),
+            "kernel": r.get("kernel")}
+
+
+def compact_line(out, detail):
+    """The headline JSON line bench.py prints last: the contract's keys, the
+    roofline, the CPU baseline, the step-level HBM figures, one row per phase
+    and one value per side workload; everything else is in the detail file
+    `detail` (the full record). Stays below LINE_LIMIT bytes."""
+    keys = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "warmup_steps_run", "ms_per_step",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data")
+    line = {k: out.get(k) for k in keys}
+    cfg = dict(out.get("config") or {})
+    cfg["workload"] = cfg.get("workload_short", cfg.get("workload"))
+    cfg.pop("workload_short", None)
+    line["config"] = cfg
+    roof = out.get("roofline")
+    if roof:
+        line["roofline"] = {k: roof.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel",
+                                                      "avg_launch_ms", "bytes_per_launch", "valu_busy")}
+    cpu = out.get("cpu_baseline")
+    if cpu:
+        line["cpu_baseline"] = {k: cpu.get(k) for k in ("value", "unit", "cores", "kind")}
+        line["cpu_baseline"]["sample"] = cpu.get("sample_short", cpu.get("sample"))
+        if cpu.get("single_core"):
+            line["cpu_baseline"]["single_core_value"] = cpu["single_core"].get("value")
+    else:
+        line["cpu_baseline"] = cpu
+    sh = out.get("step_hbm") or {}
+    line["step_hbm"] = {"survey_frac": sh.get("survey_frac_hbm"), "needed_frac": sh.get("needed_frac_hbm"),
+                        "pmc_frac": sh.get("pmc_frac_hbm"), "pmc_bytes_per_step": sh.get("pmc_bytes_per_step"),
+                        "steps_per_A_read": sh.get("steps_per_A_read")}
+    ph = out.get("phases") or {}
+    line["phases"] = {"cols": ["kernel", "ms_per_step", "frac_hbm", "pmc_bytes_per_launch", "valu_busy"],
+                      **{k: _phase_row(v) for k, v in ph.items()}}
+    if ph:
+        line["phases"]["sum_ms"] = sum(v["ms_per_step"] for v in ph.values())
+    side = {}
+    for k in ("reference_ring", "small_shape", "configs4_d4096_kappa64"):
+        if k in out:
+            side[k] = _side_value(out[k])
+    rr = out.get("reference_ring") or {}
+    if isinstance(rr.get("cpu_baseline"), dict):
+        side["reference_ring"]["cpu_value"] = rr["cpu_baseline"].get("value")
+    ops = out.get("side_ops") or {}
+    if ops:
+        side["ntt_ms"] = [ops.get("ntt_fwd", {}).get("ms"), ops.get("ntt_inv", {}).get("ms")]
+        side["poseidon2_perms_per_s"] = ops.get("poseidon2_w16", {}).get("perms_per_s")
+    nx = out.get("next_rows") or {}
+    if nx:
+        side["fold_prove_ms"] = [nx.get(k, {}).get("ms_per_fold_prove") for k in ("fold_prove", "fold_prove_scalar")]
+        side["chain_ivc_steps_per_s"] = nx.get("zkvm_chain", {}).get("value")
+    if side:
+        line["side"] = side
+    if "sharded_fold" in out:
+        s = out["sharded_fold"] or {}
+        line["sharded_fold"] = {k: s.get(k) for k in ("value", "unit", "ms_per_step", "verified", "comm_size", "error")
+                                if k in s}
+    if "pmc_files" in out:  # PMC figures are used only when collected on these kernel sources
+        line["pmc_src_hash"] = out["pmc_files"]["src_hash"]
+        line["pmc_stale"] = len(out["pmc_files"]["stale"])
+    line["detail"] = detail
+    line = _sig(line)
+    txt = json.dumps(line, separators=(",", ":"))
+    if len(txt) > LINE_LIMIT:  # never let the headline outgrow the driver's tail: drop the optional parts
+        for k in ("side", "phases", "step_hbm"):
+            line.pop(k, None)
+            txt = json.dumps(line, separators=(",", ":"))
+            if len(txt) <= LINE_LIMIT:
+                break
+    return txt
+
+
+def emit(out, detail_path):
+    """write the full record to `detail_path` (best effort) and print the compact headline line"""
+    out["pmc_files"] = {"src_hash": kernel_source_hash(), "stale": sorted(_PMC_STALE)}
+    detail = None
+    if detail_path:
+        try:
+            p = Path(detail_path)
+            if not p.is_absolute():
+                p = ROOT / p
+            p.parent.mkdir(parents=True, exist_ok=True)
+            p.write_text(json.dumps(out) + "\n")
+            detail = str(detail_path)
+        except OSError as e:
+            detail = f"not written: {e}"
+    print(compact_line(out, detail), flush=True)
 
 
 def main():
@@ -1158,6 +1295,8 @@ def main():
             "data": "synthetic (seeded SplitMix64 inputs, random Ajtai matrix)",
             "config": {"workload": f"commit+fold step, X^{d}+1 ring, w_ccs W={W}, N={N}, kappa={kappa}, "
                                    f"B=2^15 L=5 K=15, 29 Ajtai products in one pass over A; {EXCLUDED}",
+                       "workload_short": f"configs[2] at d={d}: commit+fold step, X^{d}+1, W={W}, kappa={kappa}, "
+                                         f"K=15; {EXCLUDED_SHORT}",
                        "d": d, "W": W, "N": N, "kappa": kappa,
                        "parallelism": f"{world} ranks x {args.streams} independent step streams (weak, "
                                       f"no collective on the data path)"
@@ -1199,7 +1338,7 @@ def main():
         def give_up():
             if out is not None:
                 out["sharded_fold"] = {"error": f"timeout after {SHARDED_LIMIT_S} s"}
-                print(json.dumps(out), flush=True)
+                emit(out, args.detail)
             sys.stderr.flush()
             os._exit(0)
 
@@ -1214,7 +1353,7 @@ def main():
         if out is not None:
             out["sharded_fold"] = sh
     if out is not None:
-        print(json.dumps(out), flush=True)
+        emit(out, args.detail)
     LD.finalize(pg)
     return out
 

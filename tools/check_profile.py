@@ -15,6 +15,7 @@ when the two are within 5 % or within EVENT_US (the HIP event records around a
 phase of a few tens of microseconds).
 """
 import json
+import os
 import sys
 
 # every kernel a phase's HIP-event pair brackets (lf_api.hip fold_commit / fold_finish),
@@ -34,11 +35,17 @@ EVENT_US = 8.0  # a phase's two HIP event records on the stream add a few us aro
 
 
 def line_of(path):
+    """the bench record of a log or json: the printed line names the detail file
+    holding the full record (per-phase times of every workload); follow it"""
     txt = open(path).read()
     for ln in reversed(txt.splitlines()):
         ln = ln.strip()
         if ln.startswith("{") and '"metric"' in ln:
-            return json.loads(ln)
+            rec = json.loads(ln)
+            det = rec.get("detail")
+            if det and os.path.exists(det):
+                return json.load(open(det))
+            return rec
     raise SystemExit(f"no bench line in {path}")
 
 

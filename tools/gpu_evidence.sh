@@ -46,12 +46,12 @@ while IFS= read -r cfg; do
 done <<< "$CFGS"
 fi
 if [ -z "$SKIP_BENCH" ]; then
-timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.log 2>&1
+timeout -k 10 600 python bench.py --detail gpurun_out/bench_detail_$TAG.json > gpurun_out/bench_$TAG.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -c 300 gpurun_out/bench_$TAG.log; [ $rc -eq 0 ] || exit $rc
 fi
 [ -n "$SKIP_PROF" ] && exit 0
 timeout -k 10 600 rocprofv3 --kernel-trace --marker-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- \
-  python bench.py > gpurun_out/benchprof_$TAG.log 2>&1
+  python bench.py --detail gpurun_out/benchprof_detail_$TAG.json > gpurun_out/benchprof_$TAG.log 2>&1
 rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python tools/prof_summary.py stats gpurun_out/prof_$TAG gpurun_out/stats_$TAG.md > /dev/null || exit 1
 python tools/check_profile.py gpurun_out/benchprof_$TAG.log gpurun_out/stats_$TAG.windows.json > gpurun_out/check_$TAG.txt 2>&1

@@ -16,6 +16,9 @@ import subprocess
 import sys
 from collections import defaultdict
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from bench import kernel_source_hash  # noqa: E402  (the hash bench.py checks before using a PMC file)
+
 
 def find(dirname, suffix):
     hits = sorted(glob.glob(os.path.join(dirname, "**", f"*{suffix}"), recursive=True))
@@ -140,7 +143,7 @@ def traffic(fetch_dir, write_dir, out_json, config):
         rev = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
     except Exception:
         rev = "?"
-    doc = {"config": config, "kernels": kernels, "git": rev,
+    doc = {"config": config, "kernels": kernels, "git": rev, "src_hash": kernel_source_hash(),
            "method": "separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py; bytes = "
                      "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE counts 1/2 of wide streaming "
                      "reads, MI355X_MICROARCH.md §HBM)"}
@@ -168,7 +171,7 @@ def sq(sq_dir, out_json, config, simds=1024, xcds=8):
                                    "wait_issue_frac": r["SQ_WAIT_INST_ANY"] / max(r["SQ_WAVE_CYCLES"], 1),
                                    "wait_cnt_frac": r["SQ_WAIT_ANY"] / max(r["SQ_WAVE_CYCLES"], 1)})
     kernels = {k: {f: sum(x[f] for x in v) / len(v) for f in v[0]} | {"launches": len(v)} for k, v in acc.items()}
-    doc = {"config": config, "kernels": kernels,
+    doc = {"config": config, "kernels": kernels, "src_hash": kernel_source_hash(),
            "method": "one rocprofv3 --pmc pass (SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY "
                      "SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_WAVES GRBM_GUI_ACTIVE) of bench.py; "
                      "valu_busy = 4 SQ_ACTIVE_INST_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)"}
