@@ -89,7 +89,8 @@ enum lf_status {
   LF_ERR_DEVICE = 9,                  /* HIP runtime error (see lf_ctx_last_error) */
   LF_ERR_OUT_OF_MEMORY = 10,
   LF_ERR_COMM = 11,                   /* RCCL error (see lf_ctx_last_error) */
-  LF_ERR_VERIFICATION = 12            /* lf_fold_verify rejected the proof (which check: lf_verify_check) */
+  LF_ERR_VERIFICATION = 12,           /* lf_fold_verify rejected the proof (which check: lf_verify_check) */
+  LF_ERR_UNSUPPORTED_CCS = 13         /* lf_prover_create: a multiset names the eq(beta) MLE (see lf_ctx_last_error) */
 };
 enum lf_repr { LF_REPR_CANONICAL = 0, LF_REPR_MONTGOMERY = 1 };
 
@@ -111,6 +112,8 @@ int lf_ctx_create(int device, lf_ctx **out);
 void lf_ctx_destroy(lf_ctx *ctx);
 const char *lf_status_string(int status);
 const char *lf_ctx_last_error(const lf_ctx *ctx);
+/* records msg as the context's last error (for entry points that fail before any object exists) */
+void lf_ctx_set_error(lf_ctx *ctx, const char *msg);
 /* stream used by all work of this context (hipStream_t). A new context uses a
  * non-blocking stream of its own; NULL selects the HIP default (null) stream,
  * which is what torch's default current stream is. */
@@ -559,7 +562,9 @@ int lf_lfproof_serialize(const lf_lfproof *proof, int repr, uint8_t *out, size_t
  *     elements) and multisets S (S_off [q + 1], S_idx) -- CCS (arith.rs:51-74)
  *   lf_prover_create: device scratch for one (scheme, params, CCS) shape;
  *     the CCS must pass sanity_check (m = max((n - l - 1) L, m) rounded up to a
- *     power of two) with N = (n - l - 1) L rounding up to m as well
+ *     power of two) with N = (n - l - 1) L rounding up to m as well; a multiset
+ *     index equal to the number of Mz MLEs (the reference's eq(beta) position) is
+ *     rejected with LF_ERR_UNSUPPORTED_CCS
  *   lf_fold_prove: -> the folded LCCCS, its witness (caller-allocated device
  *     buffers: f, f_coeff N elements, w_ccs W) and the LFProof (nifs.rs:28-34).
  *     repr describes every host buffer (acc, cm_i, x_ccs, out, proof).
@@ -691,7 +696,11 @@ int lf_fold_replay(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *
                    const uint64_t *x_ccs, const lf_lfproof_mut *proof, lf_replay_vars *out, int repr);
 /* the same replay with its challenges taken from the prover's sample log
  * (lf_prover_samples) instead of a second Poseidon2 pass: LF_ERR_INCORRECT_LENGTH
- * unless the replay draws exactly the logged samples */
+ * unless the replay draws exactly the logged samples.
+ * PROVER-SIDE ONLY: the playback transcript drops every observe, so the vars are NOT
+ * bound to the proof's messages -- any log of the right length is accepted. Feed it
+ * only the log of the same prover's own lf_fold_prove call (what lf_fold_prove_vars
+ * does); a received proof must go through lf_fold_replay or lf_fold_verify. */
 int lf_fold_replay_samples(const lf_ccs_desc *ccs, const lf_params *pr, const lf_lcccs *acc, const uint64_t *cm_i,
                            const uint64_t *x_ccs, const lf_lfproof_mut *proof, const uint64_t *samples, size_t nsamples,
                            lf_replay_vars *out, int repr);
@@ -739,7 +748,9 @@ void lf_hash_iter(const uint64_t *in, size_t n, uint64_t out4[4]);
  * transcript returns the logged samples in order and drops every observe, so a
  * transcript pass that absorbs the same messages in the same order (a verifier's
  * replay of a recorded proof) draws the same challenges without one permutation;
- * lf_transcript_playback_status: LF_OK iff exactly the logged samples were drawn. */
+ * lf_transcript_playback_status: LF_OK iff exactly the logged samples were drawn.
+ * A playback transcript binds nothing it observes: use it only to replay the
+ * caller's own recorded transcript, never to check a proof received from elsewhere. */
 void lf_transcript_record(lf_transcript *t);
 size_t lf_transcript_samples(const lf_transcript *t, uint64_t *out, size_t cap);
 lf_transcript *lf_transcript_new_playback(const uint64_t *samples, size_t n);

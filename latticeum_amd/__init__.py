@@ -561,7 +561,8 @@ class Prover:
         h = C.c_void_p()
         rc = self.lib.lf_prover_create(ctx.h, scheme.h, C.byref(params), ccs.h, C.byref(h))
         if rc:
-            raise LfError(rc, "lf_prover_create: " + self.lib.lf_status_string(rc).decode())
+            msg = self.lib.lf_ctx_last_error(ctx.h).decode() if rc == 13 else ""
+            raise LfError(rc, msg or "lf_prover_create: " + self.lib.lf_status_string(rc).decode())
         self.h = h
         self.d, self.l, self.t, self.degree = params.d, l, ccs.t, degree
         self.s = ccs.m.bit_length() - 1
@@ -684,7 +685,10 @@ def fold_replay(params: LfParams, t: int, m: int, l: int, degree: int, c, S, kap
     host: replays a fold() proof (the dict Prover.fold_prove returns) and returns the
     in-CCS verifier's values, keyed as oracle/nifs.py fold_replay names them, each a
     flat u64 array of NTT elements. Phi_72 only; no GPU involved. samples: the
-    prover's sample log (lf_fold_replay_samples: no second Poseidon2 pass)."""
+    prover's sample log (lf_fold_replay_samples: no second Poseidon2 pass).
+    samples is for the prover's OWN proof only: the playback drops every observe,
+    so the vars are not bound to the proof's messages. A proof received from
+    elsewhere must be replayed with samples=None (or checked with fold_verify)."""
     from ._lib import REPLAY_FIELDS, LfCcsDesc, LfLcccs, LfLfproofMut, LfReplayVars, LfRingSlice
     lib, d, K, bs = load(), params.d, params.K, params.b_small
     s, q = m.bit_length() - 1, len(S)

@@ -91,6 +91,7 @@ SIGNATURES = {
     "lf_ctx_destroy": (None, [VP]),
     "lf_status_string": (C.c_char_p, [I]),
     "lf_ctx_last_error": (C.c_char_p, [VP]),
+    "lf_ctx_set_error": (None, [VP, C.c_char_p]),
     "lf_ctx_set_stream": (I, [VP, VP]),
     "lf_ctx_get_stream": (VP, [VP]),
     "lf_stream_create_cu_mask": (I, [I, VP, I, VP]),

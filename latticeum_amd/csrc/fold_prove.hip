@@ -114,7 +114,9 @@ struct Run {
   lf_transcript *T;
   hipStream_t st;
   int rc = LF_OK;
+  std::string *err = nullptr;  // where this Run records its first error (default P->err)
   std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  std::string &errs() { return err ? *err : P->err; }
 
   // close the span that ran since the last mark (only with timing on); sync = false
   // where the device work of the span overlaps the next span's host work (the
@@ -130,14 +132,14 @@ struct Run {
   int check(int r, const char *what) {
     if (r != LF_OK && rc == LF_OK) {
       rc = r;
-      P->err = std::string(what) + ": " + lf_ctx_last_error(P->ctx);
+      errs() = std::string(what) + ": " + lf_ctx_last_error(P->ctx);
     }
     return r;
   }
   int hip(hipError_t e, const char *what) {
     if (e != hipSuccess && rc == LF_OK) {
       rc = e == hipErrorOutOfMemory ? LF_ERR_OUT_OF_MEMORY : LF_ERR_DEVICE;
-      P->err = std::string(what) + ": " + hipGetErrorString(e);
+      errs() = std::string(what) + ": " + hipGetErrorString(e);
     }
     return rc;
   }
@@ -361,6 +363,16 @@ int lf_prover_create(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, const
     P->nlive = (int)P->mz_order.size();
     for (int j = 0; j < t; j++)
       if (pos_of[j] < 0) P->mz_order.push_back(j);
+  }
+  if (P->bad_S) {
+    // The reference's list position lin_list.size() is the eq(beta) MLE itself
+    // (linearization/utils.rs:71-84): a multiset naming it would put a second eq
+    // factor into its term, which the split-eq sumcheck (eq(beta) taken out of every
+    // term) does not express. Rejected here, by name, rather than mid-fold.
+    delete P;
+    lf_ctx_set_error(ctx, "lf_prover_create: a multiset index is past the Mz MLE list (the position of "
+                          "eq(beta) or beyond); multisets over eq(beta) are not supported");
+    return LF_ERR_UNSUPPORTED_CCS;
   }
   if (!P->bad_S) {
     const size_t half = m / 2;
@@ -626,6 +638,8 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
   const bool digits = P->pr.b_small == 2;  // f_hat values in {-1, 0, 1}: read from the coefficient rows
   std::atomic<int> posted{0};
   Run RE = R;
+  std::string err_enq;  // the enqueue thread's own error text, merged into P->err after the join
+  RE.err = &err_enq;
   auto enqueue_side = [&](Run &Q, int side) {
     const uint64_t *eq_s = M + (size_t)(2 * side) * mstride;
     Q.check(lf_dev_fhat_evaluate_eq(C, d, P->fkc[side], N, ND, K, s, eq_s, P->vs + (size_t)side * K * tau * d), "v_s");
@@ -642,7 +656,7 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
       posted.store(side * ng + g + 1, std::memory_order_release);
     }
   };
-  std::thread enq([&] {
+  auto enqueue_all = [&] {
     (void)hipSetDevice(P->device);
     if (RE.rc == LF_OK) {
       enqueue_side(RE, 0);
@@ -652,10 +666,19 @@ int lf_fold_prove(lf_prover *P, const lf_lcccs *acc, const lf_witness *w_acc, co
           RE.hip(lfk::get_fhat(P->fkc[sd], N, d, s, M + (5 + (size_t)sd * K * tau) * mstride, RE.st, K, ND), "f_hat");
     }
     posted.store(1 << 30, std::memory_order_release);  // done (also on an error)
-  });
+  };
+  std::thread enq;
+  try {
+    enq = std::thread(enqueue_all);
+  } catch (const std::exception &) {  // no thread to be had: enqueue everything here first
+    enqueue_all();
+  }
   auto join = [&] {
     if (enq.joinable()) enq.join();
-    if (RE.rc != LF_OK && R.rc == LF_OK) R.rc = RE.rc;
+    if (RE.rc != LF_OK && R.rc == LF_OK) {
+      R.rc = RE.rc;
+      P->err = err_enq;
+    }
     return R.rc;
   };
   R.mark(LF_SPAN_DECOMPOSITION, false);

@@ -680,20 +680,38 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(size_t N, int L, int
         const size_t e = (size_t)kb * N + gg * L + l;
         uint64_t v[32];
         uint64_t *T0 = lds_all + wib * n32::WAVE_U64;
-        mx_stage1(azl, wn, kb, mid_f, T0, r, h);
-        __builtin_amdgcn_sched_barrier(0);  // one element's products and epilogue at a time (registers)
-        mx_stage1(azl, wn + 8, kb, mid_f, T0 + n32::HALF_U64, r, h);
+        // Is digit plane kb of this limb zero on both of the wave's elements? The top
+        // limb of a balanced base-B decomposition of a field element has |digit| <= 8
+        // (signed representative < 2^63, B^(L-1) = 2^60), so its planes 4..K-1 vanish,
+        // and plane K-1 of the other limbs is zero unless a digit is exactly +-B/2. A
+        // zero plane's transform is zero: only the Horner shift and the operand rows
+        // (the offset form of 0) remain. Checked on the data (wave-uniform), so any
+        // input stays exact.
+        uint32_t nz = 0;
+#pragma unroll
+        for (int q = 0; q < 16; q++) nz |= wn[q] >> kb;
+        const bool live = __ballot((nz & 0x10001u) != 0) != 0;
+        if (live) {
+          mx_stage1(azl, wn, kb, mid_f, T0, r, h);
+          __builtin_amdgcn_sched_barrier(0);  // one element's products and epilogue at a time (registers)
+          mx_stage1(azl, wn + 8, kb, mid_f, T0 + n32::HALF_U64, r, h);
+        }
         {  // words for the next limb, in flight through the second stage (at l = 0 a
            // harmless reload of limb L - 1)
           const int ln = l > 0 ? l - 1 : L - 1;
 #pragma unroll
           for (int q = 0; q < 16; q++) wn[q] = word(q, ln);
         }
-        n32::wave_lds_sync();
+        if (live) {
+          n32::wave_lds_sync();
 #pragma unroll
-        for (int j = 0; j < 32; j++) v[j] = T[r * n32::RS + j];  // lane m1 = r of element h: its 32 j1
-        n32::wave_lds_sync();
-        n32::cyc_dif32<false>(v);
+          for (int j = 0; j < 32; j++) v[j] = T[r * n32::RS + j];  // lane m1 = r of element h: its 32 j1
+          n32::wave_lds_sync();
+          n32::cyc_dif32<false>(v);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 32; j++) v[j] = 0;
+        }
         if (f_k) {  // uniform: without f_k the planes live only in the operand rows
           uint64_t *of = (ok ? f_k + e * D : sink) + r;
 #pragma unroll

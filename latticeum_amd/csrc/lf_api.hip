@@ -885,6 +885,7 @@ const char *lf_status_string(int s) {
     case LF_ERR_OUT_OF_MEMORY: return "out of device memory";
     case LF_ERR_COMM: return "RCCL communicator error";
     case LF_ERR_VERIFICATION: return "the folding proof does not verify";
+    case LF_ERR_UNSUPPORTED_CCS: return "unsupported CCS structure";
   }
   return "unknown status";
 }
@@ -946,6 +947,9 @@ void lf_ctx_destroy(lf_ctx *c) {
 }
 
 const char *lf_ctx_last_error(const lf_ctx *c) { return c ? c->last_error.c_str() : ""; }
+void lf_ctx_set_error(lf_ctx *c, const char *msg) {
+  if (c) c->last_error = msg ? msg : "";
+}
 
 size_t lf_witness_split_w(void) { return lfk::witness_split_w(); }
 

@@ -220,6 +220,30 @@ def test_fold_prove_montgomery_boundary():
         ctx.close()
 
 
+def test_prover_rejects_multiset_over_eq_beta():
+    """S_idx names list positions of the linearization's MLE list; the position
+    just past the Mz MLEs is eq(beta) itself (linearization/utils.rs:71-84). The
+    split-eq sumcheck cannot put a second eq factor into one term, so
+    lf_prover_create rejects such a CCS by name (LF_ERR_UNSUPPORTED_CCS)
+    instead of failing inside fold()"""
+    d, W, l, t, deg, kappa = 24, 5, 2, 6, 2, 3
+    pr_o = N.Params(d)
+    ccs = N.satisfied_ccs(d, W, l, t, deg, 77, pr_o)
+    Nn = W * pr_o.L
+    ctx = LA.Context(0)
+    try:
+        sch = LA.AjtaiCommitmentScheme(ctx, O.fill_uniform(kappa * Nn * d, 78).reshape(kappa, Nn, d))
+        M = LA.CCSMatrices(ctx, d, ccs.m, ccs.n, ccs.mats)
+        c = O.fill_uniform(2 * d, 79)
+        # lin_list = [0, 3, 1]: position 3 == len(lin_list) is the eq(beta) slot
+        with pytest.raises(LA.LfError) as e:
+            LA.Prover(ctx, sch, LA.goldilocks_dp(d), M, l, deg, c, [[0, 3], [1]])
+        assert e.value.code == 13 and "eq(beta)" in str(e.value)
+        LA.Prover(ctx, sch, LA.goldilocks_dp(d), M, l, deg, c, [[0, 2], [1]])  # every position a Mz MLE
+    finally:
+        ctx.close()
+
+
 def test_linearize_matches_oracle():
     """lf_linearize (initialize_accumulator's LFLinearizationProver::prove) against the oracle"""
     d, W, l, t, deg, kappa = 24, 13, 4, 6, 3, 4
@@ -309,5 +333,58 @@ def test_fold_prove_zkvm_dimensions():
         ctx.sync()
         assert np.array_equal(host(cm0), out["cm"]) and np.array_equal(host(v0), out["v"])
         assert np.array_equal(host(u0), out["u"])
+        check_wire(pf, out, d, pr.K, t, l, kappa)
     finally:
         ctx.close()
+
+
+def ark_vec(elems, d):
+    """ark-serialize 0.5 of Vec<RingElem>: u64 LE length, then d canonical u64 LE per element"""
+    import struct
+    e = np.asarray(elems, np.uint64).ravel()
+    return struct.pack("<Q", e.size // d) + e.astype("<u8").tobytes()
+
+
+def ark_vecvec(rows, d):
+    import struct
+    return struct.pack("<Q", len(rows)) + b"".join(ark_vec(r, d) for r in rows)
+
+
+def check_wire(pf, out, d, K, t, l, kappa):
+    """SURVEY 8(f) rank 4 on the device path: the LFProof lf_fold_prove produced at the
+    zkvm's shape through lf_lfproof_serialize (CanonicalSerialize, latticefold/src/nifs.rs:28-34),
+    its size by the ark layout formula (the size zkvm/src/main.rs:231-234 reports), the bytes
+    against a plain ark restatement, and the folded LCCCS round-tripping in both reprs"""
+    from latticeum_amd import wire
+    tau, rounds = 3, 17
+    lin_evals = pf["lin_sumcheck"].size // (rounds * d)
+    fold_evals = pf["fold_sumcheck"].size // (rounds * d)
+    assert lin_evals == 9 and fold_evals == 5  # degree 7 + 2 (linearization), the folding's degree 4 + 1
+    dec = [{k: list(pf[k][s].reshape(K, -1)) for k in ("u_s", "v_s", "x_s", "y_s")} for s in range(2)]
+    th = list(pf["theta_s"].reshape(2 * K, tau * d))
+    et = list(pf["eta_s"].reshape(2 * K, t * d))
+    b = wire.serialize_lfproof(d, pf["lin_sumcheck"], rounds, lin_evals, pf["lin_v"], pf["lin_u"], dec,
+                               pf["fold_sumcheck"], rounds, fold_evals, th, et)
+    elems = (rounds * lin_evals + tau + t + 2 * K * (t + tau + (l + 1) + kappa) + rounds * fold_evals
+             + 2 * K * tau + 2 * K * t)
+    lens = (1 + rounds) + 2 + 2 * (4 + 4 * K) + (1 + rounds) + 2 * (1 + 2 * K)
+    assert len(b) == elems * d * 8 + lens * 8, len(b)
+    ls = pf["lin_sumcheck"].reshape(rounds, lin_evals * d)
+    fs = pf["fold_sumcheck"].reshape(rounds, fold_evals * d)
+    want = ark_vecvec(list(ls), d) + ark_vec(pf["lin_v"], d) + ark_vec(pf["lin_u"], d)
+    for s in range(2):
+        want += b"".join(ark_vecvec(dec[s][k], d) for k in ("u_s", "v_s", "x_s", "y_s"))
+    want += ark_vecvec(list(fs), d) + ark_vecvec(th, d) + ark_vecvec(et, d)
+    assert b == want
+    # the folded accumulator: serialise, deserialise, in canonical and Montgomery form
+    lc = wire.serialize_lcccs(d, out["r"], out["v"], out["cm"], out["u"], out["x_w"], out["h"])
+    back = wire.deserialize_lcccs(lc, d)
+    for k in ("r", "v", "cm", "u", "x_w", "h"):
+        assert np.array_equal(back[k], out[k]), k
+    mont = np.vectorize(O.to_mont, otypes=[np.uint64])
+    om = {k: mont(out[k]) for k in ("r", "v", "cm", "u", "x_w", "h")}
+    assert wire.serialize_lcccs(d, om["r"], om["v"], om["cm"], om["u"], om["x_w"], om["h"],
+                                repr=wire.REPR_MONTGOMERY) == lc
+    backm = wire.deserialize_lcccs(lc, d, repr=wire.REPR_MONTGOMERY)
+    for k in om:
+        assert np.array_equal(backm[k], om[k]), k
