@@ -308,19 +308,62 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const
     }
   };
   const int nf = __builtin_amdgcn_readfirstlane((nvec - w + 3) >> 2 < 8 ? (nvec - w + 3) >> 2 : 8);  // wave-uniform
+  // Dead units (DeadUnits: pieces the decomposition did not write, zero): lane l
+  // keeps the mask of chunk c0 + l + 64 m in dm[m], bit 2 q + h for this wave's
+  // vector 4 q + w in unit 2 c + h; lanes 32 h .. 32 h + 31 copy half h of a
+  // vector, and for a dead half they copy zero80's 0x80 bytes (the offset form of
+  // 0) instead, so every chunk still issues the same copies (vm_wait_chunk's
+  // counts hold) and the matrix-core work is unchanged; HBM reads of dead units
+  // are gone. Read here, before any operand copy is in flight.
+  constexpr int NDM = (AJ_CPS + 63) / 64;
+  const DeadUnits du = so_.dead[stp];
+  const bool has_dead = du.flags != nullptr && du.rows != 0;  // uniform
+  uint32_t dm[NDM];
+#pragma unroll
+  for (int m = 0; m < NDM; m++) dm[m] = 0;
+  if (has_dead) {
+#pragma unroll
+    for (int m = 0; m < NDM; m++) {
+      const int c = c0 + lane + 64 * m;
+      if (c < c1) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(du.flags + (size_t)c * 64);  // units 2c, 2c + 1
+        const uint4 a0 = p[0], a1 = p[1], b0 = p[2], b1 = p[3];
+        const uint32_t ua[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};  // dword q: rows 4 q .. 4 q + 3
+        const uint32_t ub[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        uint32_t bits = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+          if ((du.rows >> (4 * q + w)) & 1)
+            bits |= (((ua[q] >> (8 * w)) & 1u) << (2 * q)) | (((ub[q] >> (8 * w)) & 1u) << (2 * q + 1));
+        dm[m] = bits;
+      }
+    }
+  }
+  auto dead_mask = [&](int c) -> uint32_t {  // c uniform
+    if (!has_dead) return 0u;
+    const int ci = c - c0;
+    uint32_t sel = dm[0];
+#pragma unroll
+    for (int m = 1; m < NDM; m++) sel = (ci >> 6) == m ? dm[m] : sel;
+    return __builtin_amdgcn_readlane(sel, ci & 63);
+  };
+  const int hl = lane >> 5;
+  const uint4 *z80 = so_.zero80 + (lane & 31);
+  // (the source is selected as a uint4 pointer in place: a pointer handed to the
+  // builtin through a lambda's return value makes clang drop the host-side kernel stub)
   auto stage_f = [&](int c, int buf) {
+    const uint32_t dmask = dead_mask(c);
 #pragma unroll
     for (int q = 0; q < 8; q++) {
       const int j = 4 * q + w;
-      if (q < nf)
-        __builtin_amdgcn_global_load_lds((const void *)(ft + (size_t)c * FV_CHUNK + j * 64 + fl_pi(j, lane)),
-                                         (lds_void *)&Fl[buf][j * 64], 16, 0, CPF);
+      const uint4 *src = ((dmask >> (2 * q + hl)) & 1u) ? z80 : ft + (size_t)c * FV_CHUNK + j * 64 + fl_pi(j, lane);
+      if (q < nf) __builtin_amdgcn_global_load_lds((const void *)src, (lds_void *)&Fl[buf][j * 64], 16, 0, CPF);
     }
   };
-  auto stage_f_piece = [&](int c, int buf, int q) {
+  auto stage_f_piece = [&](int c, int buf, int q, uint32_t dmask) {
     const int j = 4 * q + w;
-    __builtin_amdgcn_global_load_lds((const void *)(ft + (size_t)c * FV_CHUNK + j * 64 + fl_pi(j, lane)),
-                                     (lds_void *)&Fl[buf][j * 64], 16, 0, CPF);
+    const uint4 *src = ((dmask >> (2 * q + hl)) & 1u) ? z80 : ft + (size_t)c * FV_CHUNK + j * 64 + fl_pi(j, lane);
+    __builtin_amdgcn_global_load_lds((const void *)src, (lds_void *)&Fl[buf][j * 64], 16, 0, CPF);
   };
   const int rh = 2 * (lane & 31) + (lane >> 5), fj = rh >> 1;
   int fpos[8];
@@ -352,6 +395,7 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const
       for (int k = 0; k < 8; k++) asm volatile("ds_read_b128 %0, %1" : "=v"(b[k]) : "v"(fbase + 16u * fpos[k]));
       const bool more_f = c + DP - 1 < c1, more_a = c + DP < c1;
       const int fb = (j + DP - 1) % DP;
+      const uint32_t dmn = more_f ? dead_mask(c + DP - 1) : 0u;
 #pragma unroll
       for (int kb = 0; kb < 8; kb++) {
         lgkm_wait_digit(kb);
@@ -365,10 +409,10 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const
           for (int ka = 0; ka < 8; ka++)
             acc[ka + kb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ra[j][ka], b[kb], acc[ka + kb], 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
-          if (more_f && kb < nf) stage_f_piece(c + DP - 1, fb, kb);
+          if (more_f && kb < nf) stage_f_piece(c + DP - 1, fb, kb, dmn);
           __builtin_amdgcn_sched_barrier(0);
         } else {
-          if (more_f && nf == 8) stage_f_piece(c + DP - 1, fb, 7);
+          if (more_f && nf == 8) stage_f_piece(c + DP - 1, fb, 7, dmn);
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int ka = 0; ka < 8; ka++) {
@@ -528,7 +572,7 @@ hipError_t to_frag(const VecPtrs &rows, int nrows, int row0, const FragGeom &g, 
 hipError_t ajtai_mfma_steps(const uint4 *Af, const uint64_t *kr, size_t kappa, const FragGeom &g, int d, int nvec,
                             int nsteps,
                             const uint4 *const *Ff, uint64_t *const *partial, const OutPtrs *dst, hipStream_t st,
-                            hipEvent_t ev0, hipEvent_t ev1) {
+                            hipEvent_t ev0, hipEvent_t ev1, const DeadUnits *dead, const uint4 *zero80) {
   const int dv = mfma_dim(d);
   const int ktiles = mfma_ktiles(kappa);
   if (!kr || kappa < 1 || ktiles > LF_MAX_KTILES || nvec < 1 || nvec > 32 || dv % 4 || nsteps < 1 ||
@@ -537,10 +581,13 @@ hipError_t ajtai_mfma_steps(const uint4 *Af, const uint64_t *kr, size_t kappa, c
   const int nsplit = mfma_nsplit(g, d), cps = mfma_cps(g, d);
   // the contraction's own outputs: the results (X^d + 1), or Phi_72's virtual-slot sums
   StepOps so{};
+  so.zero80 = zero80;
   for (int s = 0; s < nsteps; s++) {
     so.Ff[s] = Ff[s];
     so.partial[s] = partial[s];
     so.dst[s] = dst[s];
+    // dead units need the constant pieces, and only the X^d + 1 rows carry flags
+    if (dead && zero80 && d != 24) so.dead[s] = dead[s];
     if (d == 24) {
       uint64_t *virt = partial[s] + (nsplit > 1 ? (size_t)nsplit * nvec * kappa * dv : 0);
       for (int v = 0; v < nvec; v++) so.dst[s].p[v] = virt + (size_t)v * kappa * dv;
@@ -594,7 +641,7 @@ hipError_t ajtai_mfma_steps(const uint4 *Af, const uint64_t *kr, size_t kappa, c
 hipError_t ajtai_mfma(const uint4 *Af, const uint64_t *kr, size_t kappa, const FragGeom &g, int d, const VecPtrs &fv,
                       int nvec,
                       bool f_ready, uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st, hipEvent_t ev0,
-                      hipEvent_t ev1, const OutPtrs *dst) {
+                      hipEvent_t ev1, const OutPtrs *dst, const DeadUnits *dead, const uint4 *zero80) {
   if (nvec < 1 || nvec > 32 || (!cm && !dst)) return hipErrorInvalidValue;
   OutPtrs out{};
   for (int v = 0; v < nvec; v++) out.p[v] = cm ? cm + (size_t)v * kappa * d : dst->p[v];
@@ -604,7 +651,7 @@ hipError_t ajtai_mfma(const uint4 *Af, const uint64_t *kr, size_t kappa, const F
   }
   const uint4 *ff[1] = {Ff};
   uint64_t *pp[1] = {partial};
-  return ajtai_mfma_steps(Af, kr, kappa, g, d, nvec, 1, ff, pp, &out, st, ev0, ev1);
+  return ajtai_mfma_steps(Af, kr, kappa, g, d, nvec, 1, ff, pp, &out, st, ev0, ev1, f_ready ? dead : nullptr, zero80);
 }
 
 }  // namespace lfk

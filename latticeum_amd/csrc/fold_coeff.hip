@@ -54,10 +54,14 @@ __device__ __forceinline__ uint32_t spread8(uint32_t x) {
 // (k_pack_sm: smg[(col 16 + qq) 32 + rr] = sm(x[rr + 64 qq]) | sm(x[rr + 64 qq + 32]) << 16,
 // sm = 15-bit magnitude | sign << 15). One thread per (col, h, 4 consecutive q):
 // 128 B in, one 16-B row piece per plane out.
-__global__ void __launch_bounds__(256) k_pack_keys(const uint32_t *smg, size_t ncol, int K, uint32_t *keys) {
+// nz[col] (when given): bit k = plane k of the column has a nonzero digit (the 16
+// threads of a column are 16 consecutive lanes of one wave: OR by shuffles)
+__global__ void __launch_bounds__(256) k_pack_keys(const uint32_t *smg, size_t ncol, int K, uint32_t *keys,
+                                                   uint32_t *nz) {
   const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (t >= ncol * 16) return;
-  const size_t col = t >> 4;
+  if (t >= (ncol * 16 + 63) / 64 * 64) return;  // whole waves stay (the shuffles below)
+  const bool live_t = t < ncol * 16;
+  const size_t col = live_t ? t >> 4 : 0;
   const int h = (int)(t >> 3) & 1, q0 = 4 * (int)(t & 7);
   // coefficient j = 32 q + 16 h + 4 i + m sits in word (qq = q / 2, rr = 16 h + 4 i + m), half q & 1
   uint32_t w[2][16];
@@ -73,6 +77,18 @@ __global__ void __launch_bounds__(256) k_pack_keys(const uint32_t *smg, size_t n
       w[a][4 * v + 3] = x.w;
     }
   }
+  if (nz) {
+    uint32_t m = 0;  // magnitude bits of every coefficient this thread holds
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+      for (int i = 0; i < 16; i++) m |= w[a][i] | (w[a][i] >> 16);
+    m &= 0x7FFFu;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) m |= __shfl_xor(m, o);
+    if (live_t && (t & 15) == 0) nz[col] = m;
+  }
+  if (!live_t) return;
   // per quad: planes 0..7 (lo) and 8..15 (hi, plane 15 = the sign) bit-sliced, bit 4 (k % 8) + m
   uint32_t lo[16], hi[16];
 #pragma unroll
@@ -189,7 +205,7 @@ constexpr int FC_MAXW = 30;  // 2K <= 30
 // even when it has nothing to do), else it returns and the NTT-form fold runs
 __global__ void __launch_bounds__(256, 2) k_fold_coeff(const uint32_t *keys, const uint8_t *tab_g, const int *bad,
                                                       size_t N, int K, uint64_t *f0c, int ks_n, int32_t *part,
-                                                      FoldFallback fb) {
+                                                      FoldFallback fb, int L, const uint32_t *nz) {
   __shared__ __attribute__((aligned(16))) uint8_t rt[FC_MAXW * FOLD_RT];
   __shared__ uint32_t lut[256];
   static_assert(FC_MAXW * FOLD_RT >= 512 * 9 * 8, "fold_frag_block's LDS fits the rho tables'");
@@ -218,11 +234,27 @@ __global__ void __launch_bounds__(256, 2) k_fold_coeff(const uint32_t *keys, con
   const int sh = (-col) & 3;
   // A tile of diagonal dl = t - q for this lane: bytes o .. o + 15, o = obase - 32 dl
   const int obase = 1024 + 16 * h - col;
-  const size_t ntile = (N + 31) / 32;
+  // Tiles are limb-pure: tile (l, gt) holds elements (32 gt + col) L + l, so a
+  // tile of the top limb (whose planes 4.. are zero for any balanced
+  // decomposition of a field element) skips those planes' products; a plane is
+  // skipped only when it is zero on all 32 of the tile's elements (nz: the
+  // per-column plane masks of k_pack_keys), so any input stays exact.
+  const size_t W = N / L, ntl = (W + 31) / 32, ntile = ntl * L;
   for (size_t task = blockIdx.x; task < ntile * ks_n; task += gridDim.x) {
     const size_t tile = task / ks_n;
     const int ks = (int)(task % ks_n), iq0 = 4 * (ks * nw / ks_n), iq1 = 4 * ((ks + 1) * nw / ks_n);
-    const size_t e = tile * 32 + col, ee = e < N ? e : N - 1;
+    const size_t grp = (tile % ntl) * 32 + col;
+    const bool valid = grp < W;
+    const size_t e = grp * L + tile / ntl, ee = valid ? e : 0;
+    uint32_t live = nz ? (valid ? nz[ee] | (nz[N + ee] << K) : 0u) : 0xFFFFFFFFu;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) live |= __shfl_xor(live, o);  // the tile's 32 columns (both halves agree)
+    live = __builtin_amdgcn_readfirstlane(live);
+    // the next iq at or after iq whose plane is live (whole planes are skipped)
+    auto next_live = [&](int iq) {
+      while (iq < iq1 && !((live >> (iq >> 2)) & 1u)) iq = (iq & ~3) + 4;
+      return iq;
+    };
     const uint32_t *kb0 = keys + ee * K * FC_KEYROW + 32 * h, *kb1 = keys + (N + ee) * K * FC_KEYROW + 32 * h;
     v16i acc[8];
 #pragma unroll
@@ -235,13 +267,14 @@ __global__ void __launch_bounds__(256, 2) k_fold_coeff(const uint32_t *keys, con
       const int i = iq >> 2, s = i >= K;
       return (s ? kb1 : kb0) + (i - s * K) * FC_KEYROW + 8 * (iq & 3);
     };
-    uint4 kn0, kn1;
-    {
-      const uint4 *p = reinterpret_cast<const uint4 *>(kaddr(iq0));
+    uint4 kn0 = make_uint4(0, 0, 0, 0), kn1 = kn0;
+    const int iqs = next_live(iq0);
+    if (iqs < iq1) {
+      const uint4 *p = reinterpret_cast<const uint4 *>(kaddr(iqs));
       kn0 = p[0];
       kn1 = p[1];
     }
-    for (int iq = iq0; iq < iq1; iq++) {
+    for (int iq = iqs; iq < iq1; iq = next_live(iq + 1)) {
       const int i = iq >> 2;
       const uint8_t *ri = rt + i * FOLD_RT;
       if ((iq & 3) == 0) {  // a new plane: slots 1..7 take diagonals 8 w + 1 .. 8 w + 7
@@ -250,7 +283,8 @@ __global__ void __launch_bounds__(256, 2) k_fold_coeff(const uint32_t *keys, con
       }
       const uint32_t kw[8] = {kn0.x, kn0.y, kn0.z, kn0.w, kn1.x, kn1.y, kn1.z, kn1.w};
       {
-        const uint4 *p = reinterpret_cast<const uint4 *>(kaddr(iq + 1 < iq1 ? iq + 1 : iq));
+        const int nx = next_live(iq + 1);
+        const uint4 *p = reinterpret_cast<const uint4 *>(kaddr(nx < iq1 ? nx : iq));
         kn0 = p[0];
         kn1 = p[1];
       }
@@ -269,7 +303,7 @@ __global__ void __launch_bounds__(256, 2) k_fold_coeff(const uint32_t *keys, con
           acc[tt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[(tt - qi) & 7], b, acc[tt], 0, 0, 0);
       }
     }
-    if (e < N && ks_n > 1) {
+    if (valid && ks_n > 1) {
       int32_t *out = part + ((size_t)ks * N + e) * FD + 256 * wv + 4 * h;
 #pragma unroll
       for (int tt = 0; tt < 8; tt++)
@@ -277,7 +311,7 @@ __global__ void __launch_bounds__(256, 2) k_fold_coeff(const uint32_t *keys, con
         for (int g = 0; g < 4; g++)
           *reinterpret_cast<v4i *>(out + 32 * tt + 8 * g) =
               (v4i){acc[tt][4 * g], acc[tt][4 * g + 1], acc[tt][4 * g + 2], acc[tt][4 * g + 3]};
-    } else if (e < N) {
+    } else if (valid) {
       // lane (col, h), acc[tt][4 g + r]: row 32 (8 w + tt) + 8 g + 4 h + r of element e
       uint64_t *out = f0c + e * FD + 256 * wv + 4 * h;
       auto fe = [](int x) { return x < 0 ? (uint64_t)(int64_t)x + gl::P : (uint64_t)x; };
@@ -316,10 +350,11 @@ int fold_coeff_splits(size_t N, int K, int ncu) {
   return best;
 }
 
-hipError_t fold_keys(const uint32_t *smg, size_t ncol, int K, uint32_t *keys, hipStream_t st) {
+hipError_t fold_keys(const uint32_t *smg, size_t ncol, int K, uint32_t *keys, hipStream_t st, uint32_t *nz) {
   if (K < 1 || K > 15) return hipErrorInvalidValue;
   if (!ncol) return hipSuccess;
-  hipLaunchKernelGGL(k_pack_keys, dim3((unsigned)((ncol * 16 + 255) / 256)), dim3(256), 0, st, smg, ncol, K, keys);
+  hipLaunchKernelGGL(k_pack_keys, dim3((unsigned)((ncol * 16 + 255) / 256)), dim3(256), 0, st, smg, ncol, K, keys,
+                     nz);
   return hipGetLastError();
 }
 
@@ -333,15 +368,16 @@ hipError_t fold_rho_tables(const uint64_t *rho, int nw, uint64_t *rc, uint8_t *t
 }
 
 hipError_t fold_coeff(const uint32_t *keys, const uint8_t *tab, const int *bad, size_t N, int K, uint64_t *f0c,
-                      int ncu, hipStream_t st, int32_t *part, const FoldFallback *fb) {
+                      int ncu, hipStream_t st, int32_t *part, const FoldFallback *fb, int L, const uint32_t *nz) {
   FoldFallback fbv{};
   if (fb) fbv = *fb;
-  if (K < 1 || 2 * K > FC_MAXW || ncu < 1) return hipErrorInvalidValue;
+  if (K < 1 || 2 * K > FC_MAXW || ncu < 1 || L < 1 || N % L) return hipErrorInvalidValue;
   if (!N) return hipSuccess;
   const int ks_n = part ? fold_coeff_splits(N, K, ncu) : 1;
-  const size_t ntask = (N + 31) / 32 * ks_n, cap = 2 * (size_t)ncu;  // two blocks per CU (LDS 63 KB, 256 registers)
+  const size_t ntile = (N / L + 31) / 32 * L;
+  const size_t ntask = ntile * ks_n, cap = 2 * (size_t)ncu;  // two blocks per CU (LDS 63 KB, 256 registers)
   hipLaunchKernelGGL(k_fold_coeff, dim3((unsigned)(ntask < cap ? ntask : cap)), dim3(256), 0, st, keys, tab, bad, N,
-                     K, f0c, ks_n, part, fbv);
+                     K, f0c, ks_n, part, fbv, L, nz);
   if (ks_n > 1) {
     const size_t n = N * FD;
     hipLaunchKernelGGL(k_fold_coeff_sum, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, part, ks_n, n, bad,

@@ -158,7 +158,10 @@ __device__ __forceinline__ void fold_frag_block(size_t vb, const uint4 *frag, in
 #pragma unroll
   for (int j = 0; j < 16; j++) gl::cacc_zero(acc[j]);
   for (int v = vg; v < fr.n; v += 8) {
-    const uint4 *pc = frag + fv_index(s, nch, c, fr.row[v], h);
+    const int row = fr.row[v];
+    // a unit the decomposition left unwritten holds zero: nothing to add
+    if (fr.dead.flags && ((fr.dead.rows >> row) & 1) && fr.dead.flags[(2 * (size_t)c + h) * 32 + row]) continue;
+    const uint4 *pc = frag + fv_index(s, nch, c, row, h);
     uint4 u[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) u[k] = pc[4 * k];

@@ -21,11 +21,23 @@ struct OutPtrs {
   uint64_t *p[LF_MAX_VECS];
 };
 
+// Dead operand pieces: a fused decomposition does not write the operand rows of a
+// 16-column unit whose digit plane is zero on all 16 columns (the top limb's
+// planes 4..K-1 of a balanced decomposition, plane K-1 of most units), and marks
+// dead[u 32 + row] = 1 instead (0 when written); the flags are valid for the rows
+// in `rows` only. Readers of those rows (the contraction, the operand-row folds)
+// take the offset form of zero there.
+struct DeadUnits {
+  const uint8_t *flags = nullptr;  // [2 nch units][32 rows]
+  uint32_t rows = 0;               // bit r: row r's flags are this step's
+};
 // per-step operands and destinations of a contraction over several independent steps
 struct StepOps {
   const uint4 *Ff[LF_MAX_STEPS];
   uint64_t *partial[LF_MAX_STEPS];
   OutPtrs dst[LF_MAX_STEPS];
+  DeadUnits dead[LF_MAX_STEPS];
+  const uint4 *zero80 = nullptr;  // 32 operand pieces of 0x80 bytes (the offset form of 0) for dead units
 };
 
 hipError_t transform(uint64_t *data, size_t n, int d, bool fwd, const ring::NegaTables &tb,
@@ -106,13 +118,16 @@ size_t ajtai_rowsums_elems(size_t kappa, int d);  // u64 of kr; tmp needs kappa 
 hipError_t ajtai_mfma(const uint4 *Af, const uint64_t *kr, size_t kappa, const FragGeom &g, int d, const VecPtrs &fv,
                       int nvec,
                       bool f_ready, uint4 *Ff, uint64_t *partial, uint64_t *cm, hipStream_t st,
-                      hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, const OutPtrs *dst = nullptr);
+                      hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, const OutPtrs *dst = nullptr,
+                      const DeadUnits *dead = nullptr, const uint4 *zero80 = nullptr);
 // nsteps (<= LF_MAX_STEPS) independent steps in one pass over A: step s's operand
-// rows Ff[s] (f_ready), scratch partial[s] (mfma_scratch_elems), results dst[s]
+// rows Ff[s] (f_ready), scratch partial[s] (mfma_scratch_elems), results dst[s];
+// dead[s] (may be null): step s's dead operand pieces, read as zero80's pieces
 hipError_t ajtai_mfma_steps(const uint4 *Af, const uint64_t *kr, size_t kappa, const FragGeom &g, int d, int nvec,
                             int nsteps,
                             const uint4 *const *Ff, uint64_t *const *partial, const OutPtrs *dst, hipStream_t st,
-                            hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+                            hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, const DeadUnits *dead = nullptr,
+                            const uint4 *zero80 = nullptr);
 
 // d = 1024 kernels on the register-resident 32 x 32 NTT (kernels_n32.hip)
 // W below which from_w_ccs / from_f run one half-wave per (element, limb)
@@ -142,12 +157,14 @@ struct FusedSides {
   uint2 *masks[2] = {nullptr, nullptr};          // d = 24, b_small = 2: digit masks [K][N] (nonzero, negative), or null
   uint32_t *smg[2] = {nullptr, nullptr};         // packed sign|magnitude words: d = 1024 fused [N][512], d = 24 [N][12];
                                                  // d = 4096 fused: [N][K][256] bytes (nibble | signs << 4)
+  uint8_t *dead = nullptr;                       // d = 1024 fused: dead-unit flags of the rows written (DeadUnits)
 };
 // f_0 = sum_v rho_v f_v with every f_v read from the D8 operand rows (k_fold_frag)
 struct FoldRows {
   int row[LF_MAX_VECS];   // operand row of vector v
   int rho[LF_MAX_VECS];   // its rho index
   int n;
+  DeadUnits dead;         // units the decomposition left unwritten (zero)
 };
 hipError_t fold_frag(const uint4 *frag, const FragGeom &g, const FoldRows &fr, const uint64_t *rho, int d, size_t N,
                      uint64_t *out, hipStream_t st, const int *run_if = nullptr);
@@ -161,7 +178,8 @@ hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K,
 // [nw][FOLD_RT] bytes, *bad = 1 if a coefficient is outside [-127, 127];
 // fold_coeff writes f0c = the canonical coefficients of sum_i rho_i f_i unless *bad
 constexpr int FOLD_RT = 2080;
-hipError_t fold_keys(const uint32_t *smg, size_t ncol, int K, uint32_t *keys, hipStream_t st);
+// nz (may be null): [ncol] u32, bit k = plane k of the column has a nonzero digit
+hipError_t fold_keys(const uint32_t *smg, size_t ncol, int K, uint32_t *keys, hipStream_t st, uint32_t *nz = nullptr);
 // sync: two ints, zero before the first launch; every launch leaves them zero
 hipError_t fold_rho_tables(const uint64_t *rho, int nw, uint64_t *rc, uint8_t *tab, int *bad,
                            const ring::NegaTables &inv, int *sync, hipStream_t st);
@@ -178,8 +196,11 @@ struct FoldFallback {
   const uint64_t *rho;
   uint64_t *f0;
 };
+// L: the gadget length (elements g L + l; the tiles are limb-pure); nz: both sides'
+// plane masks [2 N] from fold_keys (null: every plane is multiplied)
 hipError_t fold_coeff(const uint32_t *keys, const uint8_t *tab, const int *bad, size_t N, int K, uint64_t *f0c,
-                      int ncu, hipStream_t st, int32_t *part = nullptr, const FoldFallback *fb = nullptr);
+                      int ncu, hipStream_t st, int32_t *part = nullptr, const FoldFallback *fb = nullptr, int L = 1,
+                      const uint32_t *nz = nullptr);
 // Witness::from_f given f's coefficients: f = NTT(f_coeff), w_ccs = recompose(f); gate: as
 // fold_coeff. With inv, a set gate runs Witness::from_f of f instead (f_coeff = ICRT(f),
 // w_ccs = recompose(f)) in the same launch: the NTT-form fold's fallback path

@@ -635,6 +635,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(size_t N, int L, int
   __shared__ uint64_t lds_all[FD_LDS_U64];
   __shared__ uint64_t mid_f[n32::MID_U64];
   __shared__ uint64_t az_l[1024];  // the 8 KiB of D8 byte planes of zeta^((2 m1 + 1) j2)
+  __shared__ uint32_t vote[2][FD_WAVES];  // per wave: its plane is nonzero in the current unit
   n32::stage_mid(mid_f, mid_fg);
   for (int q = threadIdx.x; q < 1024; q += blockDim.x) az_l[q] = az_g[q];
   __syncthreads();
@@ -645,6 +646,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(size_t N, int L, int
   const size_t W = N / L, nblk = (W + 15) / 16;
   const uint64_t b_pow = gl::mul_pow2(1, lb);  // B = 2^lb
   const int8_t *azl = reinterpret_cast<const int8_t *>(az_l);
+  int nvote = 0;  // units voted on so far (block-uniform)
   // a task is one digit plane of one block of 16 groups of one side (planes
   // are independent: small W still fills the chip); consecutive blocks take
   // the planes of the same groups, so the packed words are shared through L2
@@ -728,12 +730,28 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(size_t N, int L, int
           for (int i = 0; i < 32; i++) acc[i] = gl::add(gl::mul(acc[i], b_pow), v[i]);
         }
         if (frag && (kb > 0 || row_p0 >= 0)) {
+          const size_t u = B * L + l;  // contraction unit of these 16 columns
+          const int row = kb > 0 ? row0 + kb - 1 : row_p0;
+          // a unit whose plane is zero on all 16 columns is not written: its flag
+          // says so, and the readers take the offset form of 0 there (DeadUnits).
+          // The vote slots alternate from unit to unit: a wave cannot rewrite a slot
+          // before every wave has passed the next unit's barrier.
+          const int vs = nvote++ & 1;
+          if (sd.dead && lane == 0) vote[vs][wib] = live ? 1u : 0u;
           __syncthreads();  // every wave is past its transpose: S may overwrite T
+          bool any = true;
+          if (sd.dead) {
+            uint32_t a = 0;
+#pragma unroll
+            for (int q = 0; q < FD_WAVES; q++) a |= vote[vs][q];
+            any = a != 0;
+            if (threadIdx.x == 0) sd.dead[u * 32 + row] = any ? 0 : 1;
+          }
+          if (!any) continue;  // block-uniform: no further barrier for this unit
 #pragma unroll
           for (int i = 0; i < 32; i++) S[(r + 32 * n32::brv5(i)) * FD_SROW + hw] = fenc(v[i]);
           __syncthreads();
-          const size_t u = B * L + l;  // contraction unit of these 16 columns
-          const int c = (int)(u >> 1), uh = (int)(u & 1), row = kb > 0 ? row0 + kb - 1 : row_p0;
+          const int c = (int)(u >> 1), uh = (int)(u & 1);
 #pragma unroll
           for (int rep = 0; rep < 2; rep++) {
             const int s = threadIdx.x + 512 * rep;

@@ -206,6 +206,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_n4k_fused(size_t N, int L,
   __shared__ uint64_t mid_f[n32::MID_U64];
   __shared__ uint64_t twl[Q4];
   __shared__ uint64_t zt[256];
+  __shared__ uint32_t vote[2][FQ_WAVES];  // per wave: its plane is nonzero in the current unit (as decompose_fused)
   const int m0 = (blockIdx.x >> 3) & 3;
   n32::stage_mid(mid_f, mid_fg);
   for (int q = threadIdx.x; q < Q4; q += blockDim.x) twl[q] = tw_g[m0 * Q4 + q];
@@ -218,6 +219,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_n4k_fused(size_t N, int L,
   const size_t W = N / L, nblk = (W + 15) / 16, nunit = sd.nside * nblk * K;
   const uint64_t b_pow = gl::mul_pow2(1, lb);  // B = 2^lb
   const size_t ustride = 8 * (size_t)(gridDim.x >> 5);
+  int nvote = 0;  // units voted on so far (block-uniform)
   for (size_t unit = (blockIdx.x & 7) + 8 * (size_t)(blockIdx.x >> 5); unit < nunit; unit += ustride) {
     const int side = unit >= nblk * K;
     const size_t B = unit / K - side * nblk;
@@ -244,6 +246,13 @@ __global__ void __launch_bounds__(512, 1) k_decompose_n4k_fused(size_t N, int L,
     for (int l = L - 1; l >= 0; l--) {
       const size_t e = (size_t)kb * N + gg * L + l;
       uint64_t v[32], own[32];
+      // plane kb of this limb zero on both of the wave's elements (the top limb's
+      // planes 4..K-1; kernels_n32.hip decompose_fused): the transform is zero.
+      // Every quarter's block reads the same bytes, so the four agree.
+      uint32_t nz = 0;
+#pragma unroll
+      for (int q = 0; q < 8; q++) nz |= wn[q];
+      const bool live = __ballot((nz & 0x0F0F0F0Fu) != 0) != 0;
 #pragma unroll
       for (int k = 0; k < 32; k++) {
         const uint32_t byte = (wn[k >> 2] >> (8 * (k & 3))) & 0xFFu;
@@ -262,9 +271,14 @@ __global__ void __launch_bounds__(512, 1) k_decompose_n4k_fused(size_t N, int L,
 #pragma unroll
         for (int k = 0; k < 32; k++) out_store<NT>(&oc[32 * k], own[k]);
       }
+      if (live) {
 #pragma unroll
-      for (int k = 0; k < 32; k++) v[k] = gl::mul(v[k], twl[r + 32 * k]);
-      n32::forward(v, mid_f, T, r);
+        for (int k = 0; k < 32; k++) v[k] = gl::mul(v[k], twl[r + 32 * k]);
+        n32::forward(v, mid_f, T, r);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 32; k++) v[k] = 0;
+      }
       if (fk) {
         uint64_t *of = (ok ? fk + e * D4 : sink) + m0 + 4 * r;
 #pragma unroll
@@ -272,11 +286,24 @@ __global__ void __launch_bounds__(512, 1) k_decompose_n4k_fused(size_t N, int L,
       }
       horner_step(acc, v, l == L - 1, lb, b_pow);
       if (row >= 0) {  // planes k >= 1, and plane 0 when it has a row (the f_k-free steps fold from the rows)
+        const size_t u = B * L + l;  // contraction unit of these 16 columns
+        // dead units as in decompose_fused: the four quarter blocks of a unit vote
+        // on the same bytes, so they write the same flag
+        const int vs = nvote++ & 1;
+        if (sd.dead && lane == 0) vote[vs][wib] = live ? 1u : 0u;
         __syncthreads();  // every wave is past its transpose: S may overwrite T
+        bool any = true;
+        if (sd.dead) {
+          uint32_t a = 0;
+#pragma unroll
+          for (int q = 0; q < FQ_WAVES; q++) a |= vote[vs][q];
+          any = a != 0;
+          if (threadIdx.x == 0) sd.dead[u * 32 + row] = any ? 0 : 1;
+        }
+        if (!any) continue;  // block-uniform: no further barrier for this unit
 #pragma unroll
         for (int i = 0; i < 32; i++) S[(r + 32 * n32::brv5(i)) * FQ_SROW + hw] = fenc(v[i]);
         __syncthreads();
-        const size_t u = B * L + l;  // contraction unit of these 16 columns
         const int c = (int)(u >> 1), uh = (int)(u & 1);
 #pragma unroll
         for (int rep = 0; rep < 2; rep++) {

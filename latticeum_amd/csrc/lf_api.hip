@@ -60,6 +60,10 @@ struct lf_ctx {
   size_t fpart_elems = 0;
   size_t faux_elems = 0;
   uint64_t *sink = nullptr;     // 32 KiB row the fused decompositions store work past the end into
+  uint8_t *dead = nullptr;      // dead-unit flags of the operand rows (lfk::DeadUnits) [2 nch][32]
+  size_t dead_elems = 0;
+  uint4 *zero80 = nullptr;      // 32 operand pieces of 0x80 bytes: the offset form of 0 (dead units)
+  lfk::DeadUnits dead_units{};  // the last fused decomposition's flags (what the readers of c->frag honour)
   int ncu = 0;                  // compute units of `device`
   uint64_t *stage = nullptr;    // sharded step: the partial commitments [nvec][kappa d]
   size_t stage_elems = 0;
@@ -473,7 +477,7 @@ bool n4k_ok(const Tables *t, int d, int lbs, int K) { return d == 4096 && lbs ==
 int decompose_n4k_sides(lf_ctx *c, const Tables *t, int nside, const uint64_t *const *fc, uint64_t *const *fck,
                         uint64_t *const *fk, uint64_t *const *wk, size_t N, int lb, int L, int K,
                         uint4 *frag = nullptr, int nch = 0, const int *row0 = nullptr, const int *row_p0 = nullptr,
-                        uint64_t *const *planes = nullptr) {
+                        uint64_t *const *planes = nullptr, uint8_t *dead = nullptr) {
   // packed digits: one u64 per 4 coefficients, or (fused) one byte per 4 coefficients and
   // plane -- into the caller's planes when given (the packed step's decomposed witnesses)
   const bool own = !(frag && planes && planes[0]);
@@ -481,6 +485,7 @@ int decompose_n4k_sides(lf_ctx *c, const Tables *t, int nside, const uint64_t *c
   c->smg_sides_n = 0;
   lfk::FusedSides sd{};
   sd.nside = nside;
+  sd.dead = frag ? dead : nullptr;
   for (int s = 0; s < nside; s++) {
     sd.f_coeff[s] = fc[s];
     sd.f_coeff_k[s] = fck[s];
@@ -502,6 +507,8 @@ struct Deferred {
   const uint4 *Ff = nullptr;
   uint64_t *partial = nullptr;
   lfk::OutPtrs dst{};
+  lfk::DeadUnits dead{};
+  const uint4 *zero80 = nullptr;
   int nvec = 0;
   bool set = false;
 };
@@ -532,6 +539,8 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
   c->fold_from_frag = false;
   c->masks24_n = 0;
   c->frag_fallback = false;
+  c->dead_units = lfk::DeadUnits{};
+  c->fold_rows.dead = lfk::DeadUnits{};
   if (b->planes[0] || b->planes[1]) {
     if (!(fused24 || fused || fused4k) || lbs != 1 || !b->planes[0] || !b->planes[1])
       return fail(c, LF_ERR_INVALID_ARG,
@@ -575,14 +584,28 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       // from the rows (fold_finish: k_fold_frag over the quarter-major slots)
       const int row0[2] = {extra, extra + K - 1};
       const int row_p0[2] = {no_fk ? extra + 2 * (K - 1) : -1, no_fk ? extra + 2 * (K - 1) + 1 : -1};
+      // dead units (operand rows left unwritten where a unit's plane is zero), as at d = 1024
+      LF_TRY(grow(c, c->dead, c->dead_elems, (size_t)aj->geom.nch * 64));
+      uint32_t rows = 0;
+      for (int s = 0; s < 2; s++) {
+        for (int k = 1; k < K; k++) rows |= 1u << (row0[s] + k - 1);
+        if (row_p0[s] >= 0) rows |= 1u << row_p0[s];
+      }
+      c->dead_units.flags = c->dead;
+      c->dead_units.rows = rows;
+      c->fold_rows.dead = c->dead_units;
       PhaseTimer pt(c, LF_PHASE_DECOMPOSE);  // both sides in one launch
       LF_TRY(decompose_n4k_sides(c, t, 2, fc_side, b->fk_coeff, b->fk, b->wk, N, lb, L, K, c->frag, aj->geom.nch,
-                                 row0, row_p0, b->planes));
+                                 row0, row_p0, b->planes, c->dead));
     } else if (fused) {
       // the packed words go straight into the caller's planes when given
       if (!b->planes[0]) LF_TRY(grow(c, c->smg, c->smg_elems, 2 * N * 512));
       lfk::FusedSides sd{};
       sd.nside = 2;
+      // dead units: the planes' rows are written only where a unit's plane is nonzero
+      LF_TRY(grow(c, c->dead, c->dead_elems, (size_t)aj->geom.nch * 64));
+      sd.dead = c->dead;
+      uint32_t rows = 0;
       for (int s = 0; s < 2; s++) {
         sd.f_coeff[s] = fc_side[s];
         sd.f_coeff_k[s] = b->fk_coeff[s];
@@ -592,7 +615,12 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
         sd.row_p0[s] = no_fk ? extra + 2 * (K - 1) + s : -1;
         sd.smg[s] = b->planes[0] ? reinterpret_cast<uint32_t *>(b->planes[s]) : c->smg + (size_t)s * N * 512;
         c->smg_side[s] = sd.smg[s];
+        for (int k = 1; k < K; k++) rows |= 1u << (sd.row0[s] + k - 1);
+        if (sd.row_p0[s] >= 0) rows |= 1u << sd.row_p0[s];
       }
+      c->dead_units.flags = c->dead;
+      c->dead_units.rows = rows;
+      c->fold_rows.dead = c->dead_units;
       PhaseTimer pt(c, LF_PHASE_DECOMPOSE);  // both sides in one launch
       LF_HIP(c, lfk::decompose_fused(sd, N, lb, L, K, t->fwd, c->frag, aj->geom.nch, c->d_err,
                                      c->sink, c->ncu, c->cur));
@@ -634,6 +662,8 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       defer->Ff = c->frag;
       defer->partial = c->scratch;
       defer->dst = dst;
+      defer->dead = c->dead_units;
+      defer->zero80 = c->zero80;
       defer->nvec = nvec;
       defer->set = true;
       return LF_OK;
@@ -644,8 +674,7 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       LF_HIP(c, hipEventCreate(&eb));
     }
     LF_HIP(c, lfk::ajtai_mfma(aj->Af, aj->kr, kappa, aj->geom, d, vp, nvec, true, c->frag, c->scratch, nullptr, c->cur,
-                              ea,
-                              eb, &dst));
+                              ea, eb, &dst, &c->dead_units, c->zero80));
     if (c->timing) c->pending.push_back({ea, eb, nvec});
     return LF_OK;
   }
@@ -699,7 +728,9 @@ int fold_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       t->inv.mid) {
     const int nw = 2 * K;
     const size_t tab_u64 = ((size_t)nw * lfk::FOLD_RT + 7) / 8, aux = (size_t)nw * 1024 + tab_u64 + 1;
-    LF_TRY(grow(c, c->fkeys, c->fkeys_elems, 2 * N * (size_t)K * 64));
+    // the digit keys [2 N][K][64] u32, then each column's plane mask [2 N] u32
+    LF_TRY(grow(c, c->fkeys, c->fkeys_elems, 2 * N * (size_t)K * 64 + 2 * N));
+    uint32_t *nz = c->fkeys + 2 * N * (size_t)K * 64;
     LF_TRY(grow(c, c->faux, c->faux_elems, aux));
     uint64_t *rc = c->faux;
     uint8_t *tab = reinterpret_cast<uint8_t *>(c->faux + (size_t)nw * 1024);
@@ -707,7 +738,7 @@ int fold_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
     {
       PhaseTimer pt(c, LF_PHASE_FOLD);
       for (int s = 0; s < 2; s++)
-        LF_HIP(c, lfk::fold_keys(c->smg_side[s], N, K, c->fkeys + (size_t)s * N * K * 64, c->cur));
+        LF_HIP(c, lfk::fold_keys(c->smg_side[s], N, K, c->fkeys + (size_t)s * N * K * 64, c->cur, nz + (size_t)s * N));
       LF_HIP(c, lfk::fold_rho_tables(b->rho, nw, rc, tab, bad, t->inv, c->d_sync, c->cur));
       const int ks_n = lfk::fold_coeff_splits(N, K, c->ncu);
       if (ks_n > 1) LF_TRY(grow(c, c->fpart, c->fpart_elems, (size_t)ks_n * N * 1024));
@@ -723,10 +754,10 @@ int fold_finish(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
         fb.rho = b->rho;
         fb.f0 = b->f0;
         LF_HIP(c, lfk::fold_coeff(c->fkeys, tab, bad, N, K, b->f0_coeff, c->ncu, c->cur,
-                                  ks_n > 1 ? c->fpart : nullptr, &fb));
+                                  ks_n > 1 ? c->fpart : nullptr, &fb, L, nz));
       } else {
         LF_HIP(c, lfk::fold_coeff(c->fkeys, tab, bad, N, K, b->f0_coeff, c->ncu, c->cur,
-                                  ks_n > 1 ? c->fpart : nullptr));
+                                  ks_n > 1 ? c->fpart : nullptr, nullptr, L, nz));
         lfk::VecPtrs fx{};
         for (int s = 0; s < 2; s++)
           for (int k = 0; k < K; k++) fx.p[s * K + k] = b->fk[s] + (size_t)k * N * d;
@@ -908,6 +939,8 @@ int lf_ctx_create(int device, lf_ctx **out) {
   if (hipMalloc(&c->d_sync, 2 * sizeof(int)) != hipSuccess) return LF_ERR_OUT_OF_MEMORY;
   if (hipMemset(c->d_sync, 0, 2 * sizeof(int)) != hipSuccess) return LF_ERR_DEVICE;
   if (hipMalloc(&c->sink, 4096 * sizeof(uint64_t)) != hipSuccess) return LF_ERR_OUT_OF_MEMORY;
+  if (hipMalloc(&c->zero80, 32 * sizeof(uint4)) != hipSuccess) return LF_ERR_OUT_OF_MEMORY;
+  if (hipMemset(c->zero80, 0x80, 32 * sizeof(uint4)) != hipSuccess) return LF_ERR_DEVICE;
   if (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c->ncu < 1)
     return LF_ERR_DEVICE;
   *out = c.release();
@@ -932,6 +965,8 @@ void lf_ctx_destroy(lf_ctx *c) {
   if (c->faux) (void)hipFree(c->faux);
   if (c->fpart) (void)hipFree(c->fpart);
   if (c->sink) (void)hipFree(c->sink);
+  if (c->dead) (void)hipFree(c->dead);
+  if (c->zero80) (void)hipFree(c->zero80);
   if (c->stage) (void)hipFree(c->stage);
   if (c->limb) (void)hipFree(c->limb);
   if (c->tmp) (void)hipFree(c->tmp);
@@ -2361,12 +2396,14 @@ int lf_dev_fold_step_batch(lf_ctx *const *cs, int nsteps, const lf_ajtai *aj, co
   const uint4 *ff[LF_MAX_STEPS];
   uint64_t *pp[LF_MAX_STEPS];
   lfk::OutPtrs dd[LF_MAX_STEPS];
+  lfk::DeadUnits du[LF_MAX_STEPS];
   int n = 0, nvec = 0;
   for (int s = 0; s < nsteps; s++) {
     if (!dfr[s].set) continue;
     ff[n] = dfr[s].Ff;
     pp[n] = dfr[s].partial;
     dd[n] = dfr[s].dst;
+    du[n] = dfr[s].dead;
     nvec = dfr[s].nvec;
     n++;
   }
@@ -2382,7 +2419,8 @@ int lf_dev_fold_step_batch(lf_ctx *const *cs, int nsteps, const lf_ajtai *aj, co
       LF_HIP(c0, hipEventCreate(&ea));
       LF_HIP(c0, hipEventCreate(&eb));
     }
-    LF_HIP(c0, lfk::ajtai_mfma_steps(aj->Af, aj->kr, aj->kappa, aj->geom, pr->d, nvec, n, ff, pp, dd, c0->cur, ea, eb));
+    LF_HIP(c0, lfk::ajtai_mfma_steps(aj->Af, aj->kr, aj->kappa, aj->geom, pr->d, nvec, n, ff, pp, dd, c0->cur, ea, eb, du,
+                                     c0->zero80));
     if (c0->timing) c0->pending.push_back({ea, eb, nvec, n});
     LF_HIP(c0, hipEventRecord(c0->join, c0->cur));
     for (int s = 1; s < nsteps; s++) LF_HIP(cs[s], hipStreamWaitEvent(cs[s]->cur, c0->join, 0));
