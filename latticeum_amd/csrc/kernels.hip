@@ -511,8 +511,19 @@ __global__ void __launch_bounds__(256) k_decompose_phi72_w(FusedSides sd, size_t
       }
     }
     }
+    // Planes that are zero on all 16 groups of this unit (the top limb's planes 4..K-1
+    // of a balanced decomposition of a field element; fused d = 1024 / 4096 do the
+    // same): bit 16 kq + gi of bal = lane's digits nonzero. A wave whose 4 planes are
+    // all zero skips the transform and the operand rounds; a zero plane's operand
+    // rows are left unwritten and flagged (lfk::DeadUnits)
+    const uint64_t bal = __ballot(nz != 0);
     uint64_t c[24];
-    ring::phi72_crt_ternary(nz, ng, c);
+    if (bal) {
+      ring::phi72_crt_ternary(nz, ng, c);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 24; i++) c[i] = 0;
+    }
     // f_k rows through the tile
     if constexpr (ROWS) {
 #pragma unroll
@@ -531,9 +542,12 @@ __global__ void __launch_bounds__(256) k_decompose_phi72_w(FusedSides sd, size_t
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the tile is read before the operand rounds reuse it
     }
-    if (frag) {
+    if (frag && sd.dead && gi == 0 && k >= 1 && k < K)  // one lane per plane writes its flag
+      sd.dead[(G * L + l) * 32 + row0 + k - 1] = ((bal >> (16 * kq)) & 0xFFFFull) ? 0 : 1;
+    if (frag && (bal || !sd.dead)) {
       const size_t u = G * L + l;  // contraction unit of these 16 columns
       const int ch = (int)(u >> 1), uh = (int)(u & 1);
+      const bool live_t = !sd.dead || ((bal >> (16 * kq_t)) & 0xFFFFull) != 0;  // this lane's task's plane
 #pragma unroll
       for (int r = 0; r < 40 / PW_VS; r++) {
         // keep the rounds in order (the compiler would otherwise evaluate all
@@ -548,7 +562,7 @@ __global__ void __launch_bounds__(256) k_decompose_phi72_w(FusedSides sd, size_t
 #pragma unroll
         for (int jj = 0; jj < 16; jj++) w[jj] = row[2 * jj];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read before the next round overwrites the tile
-        if (emit) {
+        if (emit && live_t) {
           // 4 pieces: digit 4 hf_t + b of the 16 columns (byte jj = column jj)
           uint32_t o[4][4];
 #pragma unroll
@@ -1507,9 +1521,10 @@ hipError_t from_f(const uint64_t *f, size_t N, int d, int lb, int L, uint64_t *f
 }
 
 hipError_t decompose_phi72_sides(const FusedSides &sd, size_t N, int lb, int L, int lbs, int K, int *err,
-                                 uint4 *frag, int nch, hipStream_t st, bool *masks_written) {
+                                 uint4 *frag, int nch, hipStream_t st, bool *masks_written, bool *dead_written) {
   const size_t W = N / L;
   if (masks_written) *masks_written = false;
+  if (dead_written) *dead_written = false;
   if (W == 0) return hipSuccess;
   if (DEC_GROUPS * L > 256 || sd.nside < 1 || sd.nside > 2) return hipErrorInvalidValue;
   if (frag) {
@@ -1552,6 +1567,7 @@ hipError_t decompose_phi72_sides(const FusedSides &sd, size_t N, int lb, int L, 
     switch (ntm) { LF_PW(7) LF_PW(12) default: return hipErrorInvalidValue; }
 #undef LF_PW
     if (masks_written) *masks_written = sd.masks[0] != nullptr && (sd.nside < 2 || sd.masks[1] != nullptr);
+    if (dead_written) *dead_written = frag && sd.dead;  // the wave-local kernel flags its zero units
     return hipGetLastError();
   }
   const int srow = frag ? DEC_SROW : 28;

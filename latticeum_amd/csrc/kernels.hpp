@@ -209,9 +209,12 @@ hipError_t from_fcoeff_n32(uint64_t *f_coeff, size_t W, int lb, int L, uint64_t 
                            const ring::NegaTables *inv = nullptr);
 
 // d = 24: both sides of a fold step in one launch (blockIdx.z = side); frag as decompose_witness
-// *masks_written: whether the launch filled sd.masks (the wave-local kernel does)
+// *masks_written: whether the launch filled sd.masks (the wave-local kernel does);
+// *dead_written: whether it left zero units unwritten and flagged them in sd.dead
+// (the wave-local kernel with frag and sd.dead; the block kernel writes every row)
 hipError_t decompose_phi72_sides(const FusedSides &sd, size_t N, int lb, int L, int lbs, int K, int *err,
-                                 uint4 *frag, int nch, hipStream_t st, bool *masks_written = nullptr);
+                                 uint4 *frag, int nch, hipStream_t st, bool *masks_written = nullptr,
+                                 bool *dead_written = nullptr);
 // f_0 in coefficient form from the decomposition's digit masks (d = 24, b_small = 2):
 // rho (2K NTT elements) -> rc [2K][25] packed 16-bit coefficient pairs, *bad = 1 if
 // one is outside [-32, 32]; unless *bad: f0_coeff = sum_i rho_i * D_i, f0 = CRT(f0_coeff),

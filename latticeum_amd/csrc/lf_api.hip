@@ -633,12 +633,17 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       const bool want_masks = lbs == 1;
       if (want_masks && !b->planes[0]) LF_TRY(grow(c, c->fkeys, c->fkeys_elems, 2 * 2 * (size_t)K * N));
       LF_TRY(grow(c, c->smg, c->smg_elems, 2 * N * 12));  // the coefficients as 16-bit sign|magnitude
+      // dead units (the wave-local b_small = 2 kernel flags the zero planes' rows)
+      LF_TRY(grow(c, c->dead, c->dead_elems, (size_t)aj->geom.nch * 64));
+      sd.dead = lbs == 1 ? c->dead : nullptr;
+      uint32_t rows = 0;
       for (int s = 0; s < 2; s++) {
         sd.f_coeff[s] = fc_side[s];
         sd.f_coeff_k[s] = b->fk_coeff[s];
         sd.f_k[s] = b->fk[s];
         sd.w_ccs_k[s] = b->wk[s];
         sd.row0[s] = extra + s * (K - 1);
+        for (int k = 1; k < K; k++) rows |= 1u << (sd.row0[s] + k - 1);
         sd.smg[s] = c->smg + (size_t)s * N * 12;
         if (want_masks)
           sd.masks[s] = b->planes[s] ? reinterpret_cast<uint2 *>(b->planes[s])
@@ -646,10 +651,15 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
         c->masks24[s] = sd.masks[s];
       }
       PhaseTimer pt(c, LF_PHASE_DECOMPOSE);  // both sides in one launch
-      bool masks = false;
-      LF_HIP(c, lfk::decompose_phi72_sides(sd, N, lb, L, lbs, K, c->d_err, c->frag, aj->geom.nch, c->cur, &masks));
+      bool masks = false, dead = false;
+      LF_HIP(c, lfk::decompose_phi72_sides(sd, N, lb, L, lbs, K, c->d_err, c->frag, aj->geom.nch, c->cur, &masks,
+                                           &dead));
       if (packed24 && !masks) return fail(c, LF_ERR_INVALID_ARG, "packed Phi_72 planes need the wave-local decomposition");
       c->masks24_n = masks ? N : 0;
+      if (dead) {  // the wave-local kernel ran: its flags are this step's
+        c->dead_units.flags = c->dead;
+        c->dead_units.rows = rows;
+      }
     }
     lfk::VecPtrs vp{};
     if (commit_f) {
