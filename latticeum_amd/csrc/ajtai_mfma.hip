@@ -383,9 +383,7 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const
         vm_wait_chunk<DP>(nf);
       else
         vm_wait<0>();
-#ifndef LF_EXP_AJ_NOBARRIER
       __builtin_amdgcn_s_barrier();  // every wave's F(c) landed; every wave is done reading F(c - 1)
-#endif
       v4i b[8];
       const uint32_t fbase = (uint32_t)(uintptr_t)&Fl[j][0];
       // the copies ride between the products instead of in front of them: F(c)
@@ -429,182 +427,6 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const
   }
   const int so = qd ? (s % qd) * 4 + s / qd : s;
   mfma_epilogue(acc, lane, kt, kappa, nvec, d, so, js, direct, dst, partial, kr);
-}
-
-// ---------------------------------------------------------------- two waves per SIMD
-// The same contraction with the 15 weight sums split over two waves of one SIMD,
-// so that one wave's copies, LDS reads and waits overlap the other's products
-// (with one wave per SIMD the sixteen 1-KiB copies per chunk -- about 110 cycles
-// of issue each -- and the waits leave the matrix pipe about half idle: SQ
-// counters of k_ajtai_mfma_ra at W = 2^14, MFMA busy 0.53). A block = 8 waves =
-// 4 slots x 2 roles; role 0 owns weights 0..7 (t = 7 only for a <= 3), role 1
-// weights 7..14 (t = 7 for a >= 4): 32 products and 8 accumulators (128 AGPRs)
-// each. Both operands stream into LDS (A: 4 slots x 8 digit tiles, F: the slot
-// quad's vector-major tile; 64 KiB per chunk, two buffers), each wave copying 8
-// of the chunk's 64 pieces; one barrier per chunk. Role 1 scales its sum by
-// 256^7 and hands it to role 0 through LDS, which adds and stores.
-constexpr int W2_NB = 2;
-// sum_{t < 8} 256^t acc_t of one output (|acc_t| < 2^31) mod p: S_j = sum_{t in 4j..4j+3}
-// acc_t 2^(8 (t - 4j)), |S_j| < 2^57, value = S0 + S1 2^32
-__device__ __forceinline__ uint64_t fold8(const int32_t *x) {
-  auto fe = [](int64_t v) { return v < 0 ? (uint64_t)v + gl::P : (uint64_t)v; };  // |v| < 2^63 - p
-  int64_t S0 = 0, S1 = 0;
-#pragma unroll
-  for (int t = 0; t < 4; t++) {
-    S0 += (int64_t)x[t] << (8 * t);
-    S1 += (int64_t)x[t + 4] << (8 * t);
-  }
-  return gl::add(fe(S0), gl::mul_pow2(fe(S1), 32));
-}
-template <int CPA, int CPF>
-__global__ void __launch_bounds__(512, 1) k_ajtai_w2(const uint4 *Af, const uint64_t *kr, StepOps so_, int nsteps,
-                                                    int d, int nch, int nvec, int kappa, int direct, int cps,
-                                                    int ktiles, int nbase, size_t tile_u4, int qd) {
-  __shared__ uint4 Fl[W2_NB][32 * 64];     // the slot quad's F tile per chunk (32 KiB)
-  __shared__ uint4 Al[W2_NB][4 * 8 * 64];  // A: slot q, digit k, lane (32 KiB)
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, w = wv & 3, role = wv >> 2;
-  const int per = 8 * ktiles * nsteps;
-  const int grp = blockIdx.x / per, rem = blockIdx.x - grp * per;
-  const int stp = rem / (8 * ktiles), rem2 = rem - stp * 8 * ktiles;
-  const int kt = rem2 >> 3, bi = grp * 8 + (rem2 & 7);
-  if (bi >= nbase) return;  // uniform over the block
-  const uint4 *Ff = so_.Ff[stp];
-  uint64_t *partial = so_.partial[stp];
-  const OutPtrs &dst = so_.dst[stp];
-  const int gw0 = bi * 4, s0 = gw0 % d, js = gw0 / d, s = s0 + w;  // d % 4 == 0: one split per block
-  if (js >= (nch + cps - 1) / cps) return;  // uniform over the block
-  const int c0 = js * cps, c1 = min(nch, c0 + cps);
-  const uint4 *ft = Ff + (size_t)(s0 >> 2) * nch * FV_CHUNK;
-  const uint4 *at = Af + kt * tile_u4 + (size_t)s0 * nch * 8 * 64;
-  // this wave's pieces of a chunk: F vectors j = wv + 8 m and A tiles i = wv + 8 m (slot i / 8, digit i % 8)
-  int nfw = 0;
-#pragma unroll
-  for (int m = 0; m < 4; m++) nfw += wv + 8 * m < nvec ? 1 : 0;
-  // dead units (DeadUnits, as in k_ajtai_mfma_ra): lane l keeps the mask of chunk
-  // c0 + l + 64 m in dm[m], bit 2 m' + h for vector wv + 8 m' in unit 2 c + h
-  constexpr int NDM = (AJ_CPS + 63) / 64;
-  const DeadUnits du = so_.dead[stp];
-  const bool has_dead = du.flags != nullptr && du.rows != 0;
-  uint32_t dm[NDM];
-#pragma unroll
-  for (int m = 0; m < NDM; m++) dm[m] = 0;
-  if (has_dead) {
-#pragma unroll
-    for (int m = 0; m < NDM; m++) {
-      const int c = c0 + lane + 64 * m;
-      if (c < c1) {
-        const uint8_t *p0 = du.flags + (size_t)c * 64;
-        uint32_t bits = 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const int row = wv + 8 * q;
-          if ((du.rows >> row) & 1)
-            bits |= ((uint32_t)(p0[row] & 1u) << (2 * q)) | ((uint32_t)(p0[32 + row] & 1u) << (2 * q + 1));
-        }
-        dm[m] = bits;
-      }
-    }
-  }
-  auto dead_mask = [&](int c) -> uint32_t {  // c uniform
-    if (!has_dead) return 0u;
-    const int ci = c - c0;
-    uint32_t sel = dm[0];
-#pragma unroll
-    for (int m = 1; m < NDM; m++) sel = (ci >> 6) == m ? dm[m] : sel;
-    return __builtin_amdgcn_readlane(sel, ci & 63);
-  };
-  const int hl = lane >> 5;
-  const uint4 *z80 = so_.zero80 + (lane & 31);
-  auto stage = [&](int c, int buf) {
-    const uint32_t dmask = dead_mask(c);
-#pragma unroll
-    for (int m = 0; m < 4; m++) {
-      const int j = wv + 8 * m;
-      const uint4 *src = ((dmask >> (2 * m + hl)) & 1u) ? z80 : ft + (size_t)c * FV_CHUNK + j * 64 + fl_pi(j, lane);
-      if (m < nfw) __builtin_amdgcn_global_load_lds((const void *)src, (lds_void *)&Fl[buf][j * 64], 16, 0, CPF);
-    }
-#pragma unroll
-    for (int m = 0; m < 4; m++) {
-      const int i = wv + 8 * m, q = i >> 3, k = i & 7;
-      const uint4 *src = at + (((size_t)q * nch + c) * 8 + k) * 64 + lane;
-      __builtin_amdgcn_global_load_lds((const void *)src, (lds_void *)&Al[buf][i * 64], 16, 0, CPA);
-    }
-  };
-  v16i acc[8];
-#pragma unroll
-  for (int t = 0; t < 8; t++) acc[t] = (v16i){0};
-  const int rh = 2 * (lane & 31) + (lane >> 5), fj = rh >> 1;
-  int fpos[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) fpos[k] = fj * 64 + fl_pi(fj, (rh & 1) * 32 + k * 4 + w);
-  if (c0 < c1) stage(c0, 0);
-  for (int c = c0; c < c1; c++) {
-    const int buf = (c - c0) & 1;
-    vm_wait<0>();                  // this wave's copies of chunk c landed (the only ones in flight)
-    __builtin_amdgcn_s_barrier();  // every wave's copies of c landed; every wave is done reading buffer c - 1
-    if (c + 1 < c1) stage(c + 1, buf ^ 1);
-    v4i a[8], b[8];
-    const uint32_t fbase = (uint32_t)(uintptr_t)&Fl[buf][0], abase = (uint32_t)(uintptr_t)&Al[buf][w * 8 * 64 + lane];
-    // operands in the order the products need them: role 0 starts at (0, 0), role 1 at (7, 7)
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const int kk = role ? 7 - k : k;
-      asm volatile("ds_read_b128 %0, %1" : "=v"(a[kk]) : "v"(abase + 1024u * kk));
-      asm volatile("ds_read_b128 %0, %1" : "=v"(b[kk]) : "v"(fbase + 16u * fpos[kk]));
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int k = 0; k < 8; k++) asm volatile("" : "+v"(a[k]), "+v"(b[k]));
-    if (role == 0) {
-#pragma unroll
-      for (int t = 0; t < 8; t++)
-#pragma unroll
-        for (int ka = 0; ka <= t && ka < 8; ka++) {
-          const int kb = t - ka;
-          if (kb < 8 && (t < 7 || ka <= 3)) acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ka], b[kb], acc[t], 0, 0, 0);
-        }
-    } else {
-#pragma unroll
-      for (int t = 7; t < 15; t++)
-#pragma unroll
-        for (int ka = 0; ka < 8; ka++) {
-          const int kb = t - ka;
-          if (kb >= 0 && kb < 8 && (t > 7 || ka >= 4))
-            acc[t - 7] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[ka], b[kb], acc[t - 7], 0, 0, 0);
-        }
-    }
-  }
-  // role 1 -> role 0 through LDS (the F buffers are free once every wave is past its products)
-  __syncthreads();
-  uint64_t *xch = reinterpret_cast<uint64_t *>(&Fl[0][0]) + ((size_t)w * 64 + lane) * 16;  // 4 x 64 x 16 u64 = 32 KiB
-  uint64_t val[16];
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    int32_t x[8];
-#pragma unroll
-    for (int t = 0; t < 8; t++) x[t] = acc[t][i];
-    val[i] = fold8(x);
-  }
-  if (role == 1) {
-#pragma unroll
-    for (int i = 0; i < 16; i++) xch[i] = gl::shl96(val[i], 56);  // 256^7
-  }
-  __syncthreads();
-  if (role == 1) return;
-  const int v = lane & 31, h = lane >> 5;
-  const int so = qd ? (s % qd) * 4 + s / qd : s;
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    uint64_t r = gl::add(val[i], xch[i]);
-    const int row = 32 * kt + (i & 3) + 8 * (i >> 2) + 4 * h;
-    if (v < nvec && row < kappa) {
-      if (js == 0) r = gl::add(r, kr[(size_t)row * d + so]);
-      if (direct)
-        dst.p[v][(size_t)row * d + so] = r;
-      else
-        partial[(((size_t)js * nvec + v) * kappa + row) * d + so] = r;
-    }
-  }
 }
 
 // ---------------------------------------------------------------- f_0 from the operand rows
@@ -782,19 +604,9 @@ hipError_t ajtai_mfma_steps(const uint4 *Af, const uint64_t *kr, size_t kappa, c
   // DESIGN.md section 7)
   const bool big = (size_t)dv * g.nch * 8192 > STREAM_OUT_BYTES;
   const int qd = g.qperm ? d / 4 : 0, direct = nsplit == 1 ? 1 : 0;
-  static const bool w2 = [] {
-    const char *e = getenv("LATTICEUM_AMD_AJTAI");
-    return e && !strcmp(e, "w2");
-  }();
-#define LF_AJ(CA, CF)                                                                                              \
-  do {                                                                                                             \
-    if (w2)                                                                                                        \
-      hipLaunchKernelGGL((k_ajtai_w2<CA, CF>), grid, dim3(512), 0, st, Af, kr, so, nsteps, dv, g.nch, nvec,        \
-                         (int)kappa, direct, cps, ktiles, nbase, tile_u4, qd);                                     \
-    else                                                                                                           \
-      hipLaunchKernelGGL((k_ajtai_mfma_ra<CA, CF, 4>), grid, dim3(256), 0, st, Af, kr, so, nsteps, dv, g.nch,      \
-                         nvec, (int)kappa, direct, cps, ktiles, nbase, tile_u4, qd);                               \
-  } while (0)
+#define LF_AJ(CA, CF)                                                                                     \
+  hipLaunchKernelGGL((k_ajtai_mfma_ra<CA, CF, 4>), grid, dim3(256), 0, st, Af, kr, so, nsteps, dv, g.nch, nvec, \
+                     (int)kappa, direct, cps, ktiles, nbase, tile_u4, qd)
   // batched: A cached so the sibling blocks hit it, F streamed (A/B on one box,
   // W = 2^14, 2 steps: 49.6 steps/s against 49.2 both streamed, 49.4 both
   // cached, 48.3 A streamed / F cached)

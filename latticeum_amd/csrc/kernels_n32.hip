@@ -729,11 +729,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(size_t N, int L, int
 #pragma unroll
           for (int i = 0; i < 32; i++) acc[i] = gl::add(gl::mul(acc[i], b_pow), v[i]);
         }
-#ifdef LF_EXP_DEC_NOEMIT
-        if (false) {
-#else
         if (frag && (kb > 0 || row_p0 >= 0)) {
-#endif
           const size_t u = B * L + l;  // contraction unit of these 16 columns
           const int row = kb > 0 ? row0 + kb - 1 : row_p0;
           // a unit whose plane is zero on all 16 columns is not written: its flag
@@ -766,9 +762,6 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(size_t N, int L, int
             uint4 pu[8];
             d8_transpose16(x, pu);
             uint4 *out = frag + fv_index(s, nch, c, row, uh);
-#ifdef LF_EXP_DEC_NOSTORE
-            if (pu[0].x == 0x12345678u && pu[7].w == 0x9abcdef0u)
-#endif
 #pragma unroll
             for (int b = 0; b < 8; b++) out_store<NT>(&out[4 * b], pu[b]);
           }
