@@ -66,6 +66,10 @@ def parse():
                          "reported beside the default workload")
     ap.add_argument("--cu-partition", action="store_true", default=False,
                     help="give each step stream its own contiguous block of CUs (lf_stream_create_cu_mask)")
+    ap.add_argument("--cu-split", type=int, default=0,
+                    help="N > 0 (batched groups): each group's contraction runs on a stream of the last N CUs "
+                         "(lf_ctx_set_contract_stream) and the step streams on the others, so a group's "
+                         "contraction runs beside the next group's decompositions")
     ap.add_argument("--packed", type=int, default=None,
                     help="1: keep the decomposed witnesses as packed digit planes (no u64 f_k / f_coeff_k rows); "
                          "0: write the rows; default: the ring's default (Workload)")
@@ -384,7 +388,7 @@ class Workload:
     each an lf context on its own HIP stream with its own w_ccs and outputs."""
 
     def __init__(self, LA, torch, local, rank, d, W, kappa, streams, seed_a=SEED_A, keep_fk=True, cu_partition=False,
-                 packed=None, batch=False):
+                 packed=None, batch=False, cu_split=0):
         # keep_fk=False (fused X^1024+1 path only): the decomposed planes live only
         # as MFMA operand rows (lf.h: f_k buffers omitted) -- 20 GB less HBM at
         # W = 2^14, but slower (DESIGN.md section 7), so the bench keeps f_k.
@@ -459,9 +463,17 @@ class Workload:
                         getattr(bufs, k)[s] = v[s].data_ptr() if v[s] is not None else None
                 else:
                     setattr(bufs, k, v.data_ptr())
+            ncu = torch.cuda.get_device_properties(local).multi_processor_count
             if cu_partition and streams > 1:
-                ncu = torch.cuda.get_device_properties(local).multi_processor_count
                 c.use_cu_mask(range(i * ncu // streams, (i + 1) * ncu // streams))
+            elif cu_split and self.batch:
+                # step streams on CUs [0, ncu - cu_split), every group's contraction on one
+                # stream of the last cu_split CUs (shared: the groups' contractions queue)
+                c.use_cu_mask(range(ncu - cu_split))
+                if i == 0:
+                    self.cstream = c.cu_mask_stream(range(ncu - cu_split, ncu))
+                if i % self.group == 0:
+                    c.set_contract_stream(self.cstream)
             c.reserve(kappa, N, d, 2 * (K - 1) + 1)
             self.ctxs.append(c)
             self.keeps.append(keep)
@@ -1270,6 +1282,7 @@ def main():
 
     d, W, kappa = args.d, args.w, args.kappa
     wl = Workload(LA, torch, local, rank, d, W, kappa, args.streams, cu_partition=args.cu_partition,
+                  cu_split=args.cu_split,
                   packed=None if args.packed is None else bool(args.packed), batch=args.batch)
     batched, group = wl.batch, wl.group
     warmup_run = warmup_steps(wl, args.warmup)
@@ -1301,7 +1314,9 @@ def main():
                        "parallelism": f"{world} ranks x {args.streams} independent step streams (weak, "
                                       f"no collective on the data path)"
                                       + (f"; groups of {group} steps whose contractions are one launch "
-                                         f"(one pass over A per group)" if batched else "")},
+                                         f"(one pass over A per group)" if batched else "")
+                                      + (f"; each group's contraction on the last {args.cu_split} CUs, the step "
+                                         f"streams on the others" if args.cu_split and batched else "")},
             "hbm_gbs_step_algorithmic": step_bytes * value / world / 1e9,
             "step_hbm": step_hbm(d, W, kappa, group if batched else 1, phases, value / world, L, K),
             # the dominant phase by device time per step (HIP events on the launch

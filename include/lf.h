@@ -130,6 +130,14 @@ int lf_stream_destroy(void *stream);
  * coefficient-form fold), so a context on a CU-masked stream fills its part
  * of the chip in one round */
 int lf_ctx_set_cu_count(lf_ctx *ctx, int ncu);
+/* stream on which lf_dev_fold_step_batch runs the batched contraction of the
+ * steps it is called with when ctx is their first context (NULL, the default:
+ * ctx's own stream). Every step stream's work before the contraction is
+ * ordered before it and the work after it waits for it (HIP events; nothing
+ * waits on the host), so with a CU-masked stream here and the step streams on
+ * the remaining CUs one group's contraction runs beside the next group's
+ * decompositions. The stream must be on ctx's device and outlive its use. */
+int lf_ctx_set_contract_stream(lf_ctx *ctx, void *hip_stream);
 /* wait for the stream; returns LF_ERR_DECOMPOSITION_OVERFLOW (and clears it)
  * if any device decomposition since the last sync ran out of digits */
 int lf_ctx_sync(lf_ctx *ctx);

@@ -92,6 +92,20 @@ class Context:
         """run this context's work on a stream of its own restricted to the
         compute units `cus` (iterable of CU indices); lf_stream_create_cu_mask"""
         cus = list(cus)
+        st = self.cu_mask_stream(cus)
+        self.set_stream(st)
+        self.check(self.lib.lf_ctx_set_cu_count(self.h, len(set(cus))))
+        return st
+
+    def set_contract_stream(self, hip_stream: int | None):
+        """where dev_fold_step_batch led by this context runs the group's
+        contraction (lf_ctx_set_contract_stream; None: this context's stream)"""
+        self.check(self.lib.lf_ctx_set_contract_stream(self.h, hip_stream))
+
+    def cu_mask_stream(self, cus):
+        """a stream of this context's device restricted to the compute units
+        `cus`, released with the context (lf_stream_create_cu_mask)"""
+        cus = list(cus)
         words = (max(cus) // 32 + 1) if cus else 1
         mask = (C.c_uint32 * words)()
         for i in cus:
@@ -100,8 +114,6 @@ class Context:
         rc = self.lib.lf_stream_create_cu_mask(self.device, mask, words, C.byref(st))
         if rc != 0:
             raise LfError(rc, "lf_stream_create_cu_mask")
-        self.set_stream(st.value)
-        self.check(self.lib.lf_ctx_set_cu_count(self.h, len(set(cus))))
         self._masked = getattr(self, "_masked", []) + [st.value]
         return st.value
 

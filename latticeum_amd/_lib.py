@@ -97,6 +97,7 @@ SIGNATURES = {
     "lf_stream_create_cu_mask": (I, [I, VP, I, VP]),
     "lf_stream_destroy": (I, [VP]),
     "lf_ctx_set_cu_count": (I, [VP, I]),
+    "lf_ctx_set_contract_stream": (I, [VP, VP]),
     "lf_ctx_sync": (I, [VP]),
     "lf_ctx_reserve": (I, [VP, SZ, SZ, I, I]),
     "lf_ctx_kernel_timing": (I, [VP, I]),

@@ -575,7 +575,9 @@ hipError_t ajtai_mfma_steps(const uint4 *Af, const uint64_t *kr, size_t kappa, c
                             hipEvent_t ev0, hipEvent_t ev1, const DeadUnits *dead, const uint4 *zero80) {
   const int dv = mfma_dim(d);
   const int ktiles = mfma_ktiles(kappa);
-  if (!kr || kappa < 1 || ktiles > LF_MAX_KTILES || nvec < 1 || nvec > 32 || dv % 4 || nsteps < 1 ||
+  // zero80 (32 pieces of 0x80 bytes) is the copy source of every operand piece
+  // that is not read from the rows: dead units and the vectors past nvec
+  if (!kr || !zero80 || kappa < 1 || ktiles > LF_MAX_KTILES || nvec < 1 || nvec > 32 || dv % 4 || nsteps < 1 ||
       nsteps > LF_MAX_STEPS)
     return hipErrorInvalidValue;
   const int nsplit = mfma_nsplit(g, d), cps = mfma_cps(g, d);

@@ -84,6 +84,8 @@ struct lf_ctx {
   bool frag_fallback = false;   // packed d = 1024 planes: fold_rows serve the not-short-rho fallback
   bool timing = false;
   hipEvent_t join = nullptr;    // lf_dev_fold_step_batch: this stream's point to wait for / be waited on
+  hipStream_t contract = nullptr;  // lf_ctx_set_contract_stream: where batched contractions led by this context run
+  hipEvent_t cjoin = nullptr;   // the end of the last such contraction
   std::vector<TimedLaunch> pending;
   std::map<int, std::pair<double, long>> stats;  // nvec -> (ms, count)
 };
@@ -390,8 +392,7 @@ int ajtai_launch(lf_ctx *c, const lf_ajtai *aj, const uint64_t *const *vecs, int
   }
   if (aj->Af)
     LF_HIP(c, lfk::ajtai_mfma(aj->Af, aj->kr, aj->kappa, aj->geom, aj->d, vp, nvec, false, c->frag, c->scratch, cm,
-                              c->cur,
-                              a, b));
+                              c->cur, a, b, nullptr, nullptr, c->zero80));
   else
     LF_HIP(c, lfk::ajtai_commit(aj->A, aj->kappa, aj->ncols, aj->d, vp, nvec, c->scratch, cm, c->cur, a, b));
   if (c->timing) c->pending.push_back({a, b, nvec});
@@ -985,6 +986,7 @@ void lf_ctx_destroy(lf_ctx *c) {
   if (c->sel) (void)hipFree(c->sel);
   if (c->hmsg) (void)hipHostFree(c->hmsg);
   if (c->join) (void)hipEventDestroy(c->join);
+  if (c->cjoin) (void)hipEventDestroy(c->cjoin);
   if (c->d_err) (void)hipFree(c->d_err);
   if (c->d_sync) (void)hipFree(c->d_sync);
   if (c->own) (void)hipStreamDestroy(c->own);
@@ -1014,6 +1016,11 @@ int lf_stream_create_cu_mask(int device, const uint32_t *mask, int nwords, void 
   hipStream_t s = nullptr;
   if (hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, mask) != hipSuccess) return LF_ERR_DEVICE;
   *stream = (void *)s;
+  return LF_OK;
+}
+int lf_ctx_set_contract_stream(lf_ctx *c, void *s) {
+  if (!c) return LF_ERR_INVALID_ARG;
+  c->contract = (hipStream_t)s;
   return LF_OK;
 }
 int lf_ctx_set_cu_count(lf_ctx *c, int ncu) {
@@ -2420,20 +2427,30 @@ int lf_dev_fold_step_batch(lf_ctx *const *cs, int nsteps, const lf_ajtai *aj, co
   for (int s = 0; s < nsteps; s++)
     if (!cs[s]->join) LF_HIP(cs[s], hipEventCreateWithFlags(&cs[s]->join, hipEventDisableTiming));
   if (n) {
-    for (int s = 1; s < nsteps; s++) {
+    // the contraction runs on c0's stream, or on c0's contraction stream when one
+    // is set (lf_ctx_set_contract_stream: e.g. a CU-masked stream beside the step
+    // streams' CUs), after every step stream's decomposition
+    const hipStream_t cst = c0->contract ? c0->contract : c0->cur;
+    for (int s = c0->contract ? 0 : 1; s < nsteps; s++) {
       LF_HIP(c0, hipEventRecord(cs[s]->join, cs[s]->cur));
-      LF_HIP(c0, hipStreamWaitEvent(c0->cur, cs[s]->join, 0));
+      LF_HIP(c0, hipStreamWaitEvent(cst, cs[s]->join, 0));
     }
     hipEvent_t ea = nullptr, eb = nullptr;
     if (c0->timing) {
       LF_HIP(c0, hipEventCreate(&ea));
       LF_HIP(c0, hipEventCreate(&eb));
     }
-    LF_HIP(c0, lfk::ajtai_mfma_steps(aj->Af, aj->kr, aj->kappa, aj->geom, pr->d, nvec, n, ff, pp, dd, c0->cur, ea, eb, du,
+    LF_HIP(c0, lfk::ajtai_mfma_steps(aj->Af, aj->kr, aj->kappa, aj->geom, pr->d, nvec, n, ff, pp, dd, cst, ea, eb, du,
                                      c0->zero80));
     if (c0->timing) c0->pending.push_back({ea, eb, nvec, n});
-    LF_HIP(c0, hipEventRecord(c0->join, c0->cur));
-    for (int s = 1; s < nsteps; s++) LF_HIP(cs[s], hipStreamWaitEvent(cs[s]->cur, c0->join, 0));
+    if (c0->contract) {
+      if (!c0->cjoin) LF_HIP(c0, hipEventCreateWithFlags(&c0->cjoin, hipEventDisableTiming));
+      LF_HIP(c0, hipEventRecord(c0->cjoin, cst));
+      for (int s = 0; s < nsteps; s++) LF_HIP(cs[s], hipStreamWaitEvent(cs[s]->cur, c0->cjoin, 0));
+    } else {
+      LF_HIP(c0, hipEventRecord(c0->join, c0->cur));
+      for (int s = 1; s < nsteps; s++) LF_HIP(cs[s], hipStreamWaitEvent(cs[s]->cur, c0->join, 0));
+    }
   }
   for (int s = 0; s < nsteps; s++) {
     DevGuard gs(cs[s]);

@@ -59,13 +59,18 @@ def expand(ctx, torch, pr, keep, N, d):
         keep["fk_coeff"][s], keep["fk"][s] = fck, fk
 
 
-def run_batch(d, W, kappa, S, packed, rounds=1, rho_long=False):
+def run_batch(d, W, kappa, S, packed, rounds=1, rho_long=False, cu_split=0):
     import torch
     pr = params(d)
     N = W * pr.L
     A = rand(kappa * N * d, 7000 + d)
     ctxs = [LA.Context(0) for _ in range(S)]
     try:
+        if cu_split:  # bench.py --cu-split: step streams and the contraction on disjoint CUs
+            ncu = torch.cuda.get_device_properties(0).multi_processor_count
+            for c in ctxs:
+                c.use_cu_mask(range(ncu - cu_split))
+            ctxs[0].set_contract_stream(ctxs[0].cu_mask_stream(range(ncu - cu_split, ncu)))
         At = torch.from_numpy(A.view(np.int64)).cuda()
         sch = LA.AjtaiCommitmentScheme(ctxs[0], device_tensor=At, kappa=kappa, ncols=N, d=d)
         for rnd in range(rounds):
@@ -99,6 +104,14 @@ def test_fold_step_batch_packed_planes(d, W, S):
     batches on the same contexts (each batch's contraction must see its own rows);
     d = 4096 folds f_0 from the quarter-major operand rows (k_fold_frag)"""
     run_batch(d, W, 3 if d == 24 else 2, S, packed=True, rounds=2)
+
+
+@pytest.mark.parametrize("d,S", [(1024, 4), (24, 2), (4096, 2)])
+def test_fold_step_batch_contract_stream(d, S):
+    """the group's contraction on a stream of its own (lf_ctx_set_contract_stream,
+    a CU-masked stream beside the step streams' CUs): every step waits for its
+    decomposition before the contraction and for the contraction after it"""
+    run_batch(d, 37 if d == 1024 else 17, 3 if d == 24 else 2, S, packed=True, rounds=2, cu_split=64)
 
 
 def test_fold_step_batch_wide_kappa():
