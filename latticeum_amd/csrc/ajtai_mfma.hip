@@ -434,12 +434,14 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const
 // as operand rows (offset form; the fused d = 1024 / 4096 decompositions with f_k = null): one
 // block per fold_frag_block (frag.hpp). The packed-plane step runs the same
 // blocks inside k_fold_coeff's launch instead (fold_coeff.hip).
-__global__ void __launch_bounds__(256) k_fold_frag(const uint4 *frag, int nch, int Lp, size_t Wp, FoldRows fr,
+// (8 columns per thread, 512 threads, 114 VGPRs: four waves per SIMD instead of two;
+// configs[4]'s fold 1.34 -> 1.17 ms)
+__global__ void __launch_bounds__(512) k_fold_frag(const uint4 *frag, int nch, int Lp, size_t Wp, FoldRows fr,
                                                   const uint64_t *rho, int d, size_t N, uint64_t *out,
                                                   const int *run_if, int qd) {
   if (run_if && !*run_if) return;  // uniform: the coefficient-form fold produced f_0
   __shared__ uint64_t red[512 * 9];  // [output (column, slot)][vector group], rows padded to 9
-  fold_frag_block(blockIdx.x, frag, nch, Lp, Wp, fr, rho, d, N, out, red, qd);
+  fold_frag_block<8>(blockIdx.x, frag, nch, Lp, Wp, fr, rho, d, N, out, red, qd);
 }
 
 hipError_t fold_frag(const uint4 *frag, const FragGeom &g, const FoldRows &fr, const uint64_t *rho, int d, size_t N,
@@ -447,7 +449,7 @@ hipError_t fold_frag(const uint4 *frag, const FragGeom &g, const FoldRows &fr, c
   if (d == 24 || d % 16 || fr.n < 1 || fr.n > LF_MAX_VECS) return hipErrorInvalidValue;
   if (!N) return hipSuccess;
   const size_t nb = (size_t)(d / 16) * g.nch;
-  hipLaunchKernelGGL(k_fold_frag, dim3((unsigned)nb), dim3(256), 0, st, frag, g.nch, g.Lp, g.Wp, fr, rho, d, N, out,
+  hipLaunchKernelGGL(k_fold_frag, dim3((unsigned)nb), dim3(512), 0, st, frag, g.nch, g.Lp, g.Wp, fr, rho, d, N, out,
                      run_if, g.qperm ? d / 4 : 0);
   return hipGetLastError();
 }

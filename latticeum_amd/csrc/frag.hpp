@@ -138,46 +138,91 @@ __device__ __forceinline__ size_t frag_column(int c, int t, int Lp, size_t Wp, b
 }
 
 // folding.rs:258-268 compute_f_0 from the D8 operand rows (the packed / f_k-free
-// steps' fallback for a rho that is not short): virtual block vb < (d / 16) nch
-// takes 16 slots (four slot quads, one 128-B line of every element) of one
-// 32-column chunk; thread (quad, slot, half, vector group) undoes the byte
-// transposition of its 16 columns for vectors v = vg, vg + 8, .. and
-// multiply-accumulates rho_v (.) f_v lazily; the 8 vector groups meet in LDS
+// steps' fallback for a rho that is not short, and d = 4096's fold): virtual block
+// vb < (d / 16) nch takes 16 slots (four slot quads, one 128-B line of every
+// element) of one 32-column chunk; thread (quad, slot, half, column part, vector
+// group) undoes the byte transposition of its CW columns (CW = 16: all of its
+// half's, 256 threads; CW = 8: one of two parts, 512 threads and about half the
+// registers, so twice the waves keep loads in flight) for vectors v = vg, vg + 8,
+// .. and multiply-accumulates rho_v (.) f_v lazily; the 8 vector groups meet in LDS
 // (red: 512 x 9 u64) and each output column's 16 slots go out as one 128-B run.
-// 256 threads; block-uniform (it synchronises the block). qd > 0: the operand slots
-// are quarter-major (FragGeom::qperm, d = 4096): operand slot o holds slot
+// Each thread reads its rows' dead flags and rho values before any operand row.
+// Block-uniform (it synchronises the block). qd > 0: the operand slots are
+// quarter-major (FragGeom::qperm, d = 4096): operand slot o holds slot
 // (o % qd) 4 + o / qd, so one block's 16 operand slots are every 4th slot.
 __device__ __forceinline__ int frag_slot(int o, int qd) { return qd ? (o % qd) * 4 + o / qd : o; }
+template <int CW = 16>
 __device__ __forceinline__ void fold_frag_block(size_t vb, const uint4 *frag, int nch, int Lp, size_t Wp,
                                                 const FoldRows &fr, const uint64_t *rho, int d, size_t N,
                                                 uint64_t *out, uint64_t *red, int qd = 0) {
-  const int tid = threadIdx.x, vg = tid & 7, h = (tid >> 3) & 1, sl = (tid >> 4) & 3, qq = tid >> 6;
+  static_assert(CW == 16 || CW == 8, "16 or 8 columns per thread");
+  constexpr int NT = CW == 16 ? 256 : 512;  // threads of the block
+  // CW = 16: tid = (qq, sl, h, vg); CW = 8: tid = (qq, vg, h, sl, cp), so the 8 lanes
+  // of one (vector, half) read one 64-B run (4 slots x 2 column parts x 8 B)
+  const int tid = threadIdx.x;
+  const int vg = CW == 8 ? (tid >> 4) & 7 : tid & 7;
+  const int cp = CW == 8 ? tid & 1 : 0;  // which 8 of the half's 16 columns
+  const int h = CW == 8 ? (tid >> 3) & 1 : (tid >> 3) & 1;
+  const int sl = CW == 8 ? (tid >> 1) & 3 : (tid >> 4) & 3;
+  const int qq = CW == 8 ? tid >> 7 : tid >> 6;
   const int ng = d >> 4, G = (int)(vb % ng), c = (int)(vb / ng);
   const int s = 16 * G + 4 * qq + sl, sr = frag_slot(s, qd);
-  gl::CAcc acc[16];
+  constexpr int MAXR = (LF_MAX_VECS + 7) / 8;  // rows per vector group
+  bool use[MAXR];
+  uint64_t rv[MAXR];
+  const uint4 *pr[MAXR];
 #pragma unroll
-  for (int j = 0; j < 16; j++) gl::cacc_zero(acc[j]);
-  for (int v = vg; v < fr.n; v += 8) {
-    const int row = fr.row[v];
+  for (int i = 0; i < MAXR; i++) {
+    const int v = vg + 8 * i;
+    use[i] = v < fr.n;
+    const int row = use[i] ? fr.row[v] : 0;
     // a unit the decomposition left unwritten holds zero: nothing to add
-    if (fr.dead.flags && ((fr.dead.rows >> row) & 1) && fr.dead.flags[(2 * (size_t)c + h) * 32 + row]) continue;
-    const uint4 *pc = frag + fv_index(s, nch, c, row, h);
-    uint4 u[8];
+    if (use[i] && fr.dead.flags && ((fr.dead.rows >> row) & 1))
+      use[i] = !fr.dead.flags[(2 * (size_t)c + h) * 32 + row];
+    rv[i] = use[i] ? rho[(size_t)fr.rho[v] * d + sr] : 0;
+    pr[i] = frag + fv_index(s, nch, c, row, h);
+  }
+  gl::CAcc acc[CW];
 #pragma unroll
-    for (int k = 0; k < 8; k++) u[k] = pc[4 * k];
-    const uint64_t rv = rho[(size_t)fr.rho[v] * d + sr];
-    uint64_t x[16];
-    fenc_untranspose16(u, x);
+  for (int j = 0; j < CW; j++) gl::cacc_zero(acc[j]);
 #pragma unroll
-    for (int j = 0; j < 16; j++) gl::cacc_mad(acc[j], rv, x[j]);
+  for (int i = 0; i < MAXR; i++) {
+    if (!use[i]) continue;
+    uint64_t x[CW];
+    if (CW == 16) {
+      uint4 u[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) u[k] = pr[i][4 * k];
+      fenc_untranspose16(u, x);
+    } else {
+      // columns 8 cp .. 8 cp + 7 are bytes 8 cp .. 8 cp + 7 of each digit's piece
+      uint2 u2[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) u2[k] = reinterpret_cast<const uint2 *>(pr[i] + 4 * k)[cp];
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        uint32_t w[8], lo[4], hi[4];
+#pragma unroll
+        for (int k = 0; k < 8; k++) w[k] = q == 0 ? u2[k].x : u2[k].y;
+        byte_tr4(w, lo);
+        byte_tr4(w + 4, hi);
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++) x[4 * q + cc] = ((uint64_t)lo[cc] | ((uint64_t)hi[cc] << 32)) ^ FOFF;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CW; j++) gl::cacc_mad(acc[j], rv[i], x[j]);
   }
   // output o = column (32) x slot (16): o = (16 h + jj) 16 + 4 qq + sl
 #pragma unroll
-  for (int jj = 0; jj < 16; jj++) red[((16 * h + jj) * 16 + 4 * qq + sl) * 9 + vg] = gl::cacc_reduce(acc[jj]);
+  for (int j = 0; j < CW; j++) {
+    const int jj = CW * cp + j;
+    red[((16 * h + jj) * 16 + 4 * qq + sl) * 9 + vg] = gl::cacc_reduce(acc[j]);
+  }
   __syncthreads();
 #pragma unroll
-  for (int rep = 0; rep < 2; rep++) {
-    const int o = tid + 256 * rep, j = o >> 4, s16 = o & 15;
+  for (int rep = 0; rep < 512 / NT; rep++) {
+    const int o = tid + NT * rep, j = o >> 4, s16 = o & 15;
     uint64_t t = red[o * 9];
 #pragma unroll
     for (int g = 1; g < 8; g++) t = gl::add(t, red[o * 9 + g]);
