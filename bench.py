@@ -10,9 +10,9 @@ Default workload (BASELINE.json configs[2], "Ajtai commit + single LatticeFold
 step on 2^14 synthetic CCS witnesses", at the metric's d=1024): ring
 Fq[X]/(X^1024+1), w_ccs = 2^14 ring elements, kappa = 32, B=2^15, L=5, K=15.
 
-Each GPU runs `--streams` (default 4) independent step streams -- independent
+Each GPU runs `--streams` (default 8) independent step streams -- independent
 witness / accumulator pairs, the trace-batch shard of BASELINE configs[3] --
-and, with `--batch G` (default 4), every G of them are one
+and, with `--batch G` (default 8), every G of them are one
 lf_dev_fold_step_batch call: each step's arithmetic on its own stream, their
 Ajtai contractions one launch, so the 21.5 GB matrix A is read from HBM once
 per G steps. Every step is complete; nothing is shared
@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--d", type=int, default=1024)
     ap.add_argument("--w", type=int, default=1 << 14, help="w_ccs length W (ring elements)")
     ap.add_argument("--kappa", type=int, default=32)
-    ap.add_argument("--streams", type=int, default=4,
+    ap.add_argument("--streams", type=int, default=8,
                     help="concurrent step streams per GPU (independent witness / accumulator pairs)")
     ap.add_argument("--no-small-shape", dest="small", action="store_false", default=True,
                     help="skip the W=464 / d=24 multi-stream measurements and the NTT / Poseidon2 timings "
@@ -73,7 +73,7 @@ def parse():
     ap.add_argument("--packed", type=int, default=None,
                     help="1: keep the decomposed witnesses as packed digit planes (no u64 f_k / f_coeff_k rows); "
                          "0: write the rows; default: the ring's default (Workload)")
-    ap.add_argument("--batch", type=int, default=4,
+    ap.add_argument("--batch", type=int, default=8,
                     help="G > 1: the step streams form groups of G whose G steps' contractions run as one "
                          "launch (lf_dev_fold_step_batch: one pass over A for the group); 1: all streams")
     ap.add_argument("--cpu-baseline", dest="cpu", action="store_true", default=True)
@@ -493,6 +493,12 @@ class Workload:
                 self.ctxs[j].dev_fold_step_batch(self.ctxs[j + 1:j + g], self.sch, self.pr, self.W,
                                                  self.bufs[j:j + g])
             i = steps // g * g
+            r = steps - i
+            if r > 1:  # a partial last group is one smaller batch (every step still one full step)
+                j = ((steps // g) % (S // g)) * g
+                self.ctxs[j].dev_fold_step_batch(self.ctxs[j + 1:j + r], self.sch, self.pr, self.W,
+                                                 self.bufs[j:j + r])
+                i = steps
         for i in range(i, steps):
             if comm is None:
                 self.ctxs[i % S].dev_fold_step(self.sch, self.pr, self.W, self.bufs[i % S])

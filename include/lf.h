@@ -291,7 +291,7 @@ int lf_dev_expand_planes(lf_ctx *ctx, const lf_params *pr, const uint64_t *plane
 /* commit(z) followed by the commit+fold arithmetic of fold(), all on device */
 int lf_dev_fold_step(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, size_t W,
                      const lf_fold_step_bufs *b);
-/* nsteps (<= 4) independent commit+fold steps against one Ajtai scheme (trace-batch
+/* nsteps (<= 8) independent commit+fold steps against one Ajtai scheme (trace-batch
  * shard: independent witness / accumulator pairs, SURVEY.md 8(e) configs[3]), each
  * with its own context (stream) and buffers. Every step runs lf_dev_fold_step's
  * arithmetic on its own stream, except that their commitment contractions run

@@ -8,7 +8,7 @@
 
 #define LF_MAX_VECS 32
 #define LF_MAX_KTILES 4
-#define LF_MAX_STEPS 4
+#define LF_MAX_STEPS 8  // steps per batched contraction (lf_dev_fold_step_batch)
 
 namespace lfk {
 

@@ -98,9 +98,9 @@ def test_fold_step_batch_matches_oracle(d, W, kappa, S):
     run_batch(d, W, kappa, S, packed=False)
 
 
-@pytest.mark.parametrize("d,W,S", [(1024, 37, 4), (24, 70, 4), (4096, 17, 4), (4096, 33, 2)])
+@pytest.mark.parametrize("d,W,S", [(1024, 37, 4), (1024, 37, 8), (24, 70, 4), (4096, 17, 4), (4096, 33, 2)])
 def test_fold_step_batch_packed_planes(d, W, S):
-    """the bench's configuration: packed digit planes, four steps per batch, two
+    """the bench's configuration: packed digit planes, four or eight steps per batch, two
     batches on the same contexts (each batch's contraction must see its own rows);
     d = 4096 folds f_0 from the quarter-major operand rows (k_fold_frag)"""
     run_batch(d, W, 3 if d == 24 else 2, S, packed=True, rounds=2)
@@ -138,10 +138,10 @@ def test_fold_step_batch_rejects_bad_arguments():
         st = make_step(torch, A, kappa, d, W, 5, packed=True)
         with pytest.raises(LA.LfError):  # the same context twice
             c.dev_fold_step_batch([c], sch, pr, W, [st["b"], st["b"]])
-        others = [LA.Context(0) for _ in range(4)]
+        others = [LA.Context(0) for _ in range(8)]
         try:
-            with pytest.raises(LA.LfError):  # more steps than one launch takes
-                c.dev_fold_step_batch(others, sch, pr, W, [st["b"]] * 5)
+            with pytest.raises(LA.LfError):  # more steps than one launch takes (8)
+                c.dev_fold_step_batch(others, sch, pr, W, [st["b"]] * 9)
         finally:
             for o in others:
                 o.close()
