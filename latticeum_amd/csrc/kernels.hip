@@ -1473,9 +1473,10 @@ hipError_t mont(uint64_t *x, size_t n, bool to, hipStream_t st) {
 
 hipError_t from_w_ccs(const uint64_t *w_ccs, size_t W, int d, int lb, int L, uint64_t *f_coeff,
                       uint64_t *f, const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err,
-                      hipStream_t st) {
+                      hipStream_t st, uint32_t *smg) {
   if (W == 0) return hipSuccess;
-  if (d == 1024 && fwd.mid && inv.mid) return from_w_ccs_n32(w_ccs, W, lb, L, f_coeff, f, fwd, inv, err, st);
+  if (smg && (d != 1024 || lb > 15 || !fwd.mid || !inv.mid)) return hipErrorInvalidValue;
+  if (d == 1024 && fwd.mid && inv.mid) return from_w_ccs_n32(w_ccs, W, lb, L, f_coeff, f, fwd, inv, err, st, smg);
   if (d == 4096 && fwd.tw4 && inv.tw4) return from_w_ccs_n4k(w_ccs, W, lb, L, f_coeff, f, fwd, inv, err, st);
   if (d == 24) {
     hipLaunchKernelGGL(k_from_w_ccs_phi72, dim3(blocks(W * L, 128)), dim3(128), 0, st, w_ccs, W, lb,

@@ -45,9 +45,12 @@ hipError_t transform(uint64_t *data, size_t n, int d, bool fwd, const ring::Nega
 hipError_t slot_mul(const uint64_t *a, const uint64_t *b, uint64_t *out, size_t n, int d,
                     hipStream_t st);
 hipError_t mont(uint64_t *x, size_t n, bool to, hipStream_t st);
+// smg (d = 1024 only, may be null): also write the digits as the fused
+// decomposition's packed sign|magnitude words ([W L][512] u32, k_pack_sm's layout),
+// so that launch need not re-read f_coeff (the digits fit 15 bits when lb <= 15)
 hipError_t from_w_ccs(const uint64_t *w_ccs, size_t W, int d, int lb, int L, uint64_t *f_coeff,
                       uint64_t *f, const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err,
-                      hipStream_t st);
+                      hipStream_t st, uint32_t *smg = nullptr);
 // run_if (X^1024 + 1 and Phi_72): when given, the kernels do nothing unless *run_if != 0
 // (the fallbacks of the coefficient-form fold, fold_coeff.hip)
 hipError_t from_f(const uint64_t *f, size_t N, int d, int lb, int L, uint64_t *f_coeff,
@@ -136,7 +139,8 @@ size_t witness_split_w();
 hipError_t transform_n32(uint64_t *data, size_t n, bool fwd, const ring::NegaTables &tb, hipStream_t st,
                          const uint64_t *src = nullptr);
 hipError_t from_w_ccs_n32(const uint64_t *w_ccs, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *f,
-                          const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err, hipStream_t st);
+                          const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err, hipStream_t st,
+                          uint32_t *smg = nullptr);
 hipError_t from_f_n32(const uint64_t *f, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *w_ccs,
                       const ring::NegaTables &inv, hipStream_t st, const int *run_if = nullptr);
 hipError_t decompose_n32(const uint64_t *f_coeff, size_t N, int lb, int L, int K, uint64_t *f_coeff_k,
@@ -158,6 +162,8 @@ struct FusedSides {
   uint32_t *smg[2] = {nullptr, nullptr};         // packed sign|magnitude words: d = 1024 fused [N][512], d = 24 [N][12];
                                                  // d = 4096 fused: [N][K][256] bytes (nibble | signs << 4)
   uint8_t *dead = nullptr;                       // d = 1024 fused: dead-unit flags of the rows written (DeadUnits)
+  int prepacked = 0;                             // d = 1024 fused: bit s = side s's smg is already written
+                                                 // (from_w_ccs wrote it; only side 1 may be)
 };
 // f_0 = sum_v rho_v f_v with every f_v read from the D8 operand rows (k_fold_frag)
 struct FoldRows {

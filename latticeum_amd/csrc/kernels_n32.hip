@@ -86,9 +86,22 @@ __device__ __forceinline__ void inverse_gmid(uint64_t *v, const uint64_t *mid_ig
 // The inverse middle factors read from global (L1-resident 8 KiB table),
 // no next-element prefetch, so two blocks (8 waves) fit a CU: 0.71 -> 0.52 ms at
 // W = 16 384 against the LDS-table, prefetching form (one block per CU)
+// the fused decomposition's packed words of one limb row (k_pack_sm's layout:
+// word (q, r) = sm(x[r + 64 q]) | sm(x[r + 64 q + 32]) << 16, sm = 15-bit magnitude |
+// sign << 15) straight from the digits this lane holds (x[r + 32 k] = d[k])
+__device__ __forceinline__ uint32_t sm16(int64_t d) {
+  return (uint32_t)(d < 0 ? -d : d) | (d < 0 ? 0x8000u : 0u);
+}
+// (from the field elements, so no digit array stays live beside the transform's registers)
+__device__ __forceinline__ void store_sm_row(const uint64_t *v, uint32_t *row, int r) {
+#pragma unroll
+  for (int q = 0; q < 16; q++)
+    row[q * 32 + r] = sm16(signed_rep(v[2 * q])) | (sm16(signed_rep(v[2 * q + 1])) << 16);
+}
+// smg (may be null): the digits' packed words too (from_w_ccs's comment in kernels.hpp)
 __global__ void __launch_bounds__(256, 2) k_from_w_ccs_n32(const uint64_t *w_ccs, size_t W, int lb, int L,
                                                           uint64_t *f_coeff, uint64_t *f, const uint64_t *mid_fg,
-                                                          const uint64_t *mid_ig, int *err) {
+                                                          const uint64_t *mid_ig, int *err, uint32_t *smg) {
   __shared__ uint64_t lds_all[WPB * n32::WAVE_U64];
   __shared__ uint64_t mid_f[n32::MID_U64];
   n32::stage_mid(mid_f, mid_fg);
@@ -113,6 +126,7 @@ __global__ void __launch_bounds__(256, 2) k_from_w_ccs_n32(const uint64_t *w_ccs
         v[k] = from_signed(bal_digit(cur[k], lb));
         if (ok) oc[32 * k] = v[k];
       }
+      if (smg && ok) store_sm_row(v, smg + (j * L + l) * 512, x.r);
       n32::forward(v, mid_f, x.lds, x.r);
       if (ok) {
         uint64_t *of = f + (j * L + l) * D + x.r;
@@ -269,7 +283,8 @@ __device__ __forceinline__ void split_unit(size_t u, int L, size_t &j, int &l) {
 // launch of (element, limb) units that each redid their element's inverse
 // transform: W + W L transforms instead of 2 W L, in two short latency chains
 __global__ void __launch_bounds__(256) k_from_w_ccs_digits(const uint64_t *w_ccs, size_t W, int lb, int L,
-                                                          uint64_t *f_coeff, const uint64_t *mid_ig, int *err) {
+                                                          uint64_t *f_coeff, const uint64_t *mid_ig, int *err,
+                                                          uint32_t *smg) {
   __shared__ uint64_t lds_all[WPB * n32::WAVE_U64];
   Half x = half_ctx(lds_all);
   for (size_t j = x.unit; j < pair_bound(W); j += x.stride) {
@@ -282,11 +297,13 @@ __global__ void __launch_bounds__(256) k_from_w_ccs_digits(const uint64_t *w_ccs
     for (int k = 0; k < 32; k++) cur[k] = signed_rep(v[k]);
     for (int l = 0; l < L; l++) {
       uint64_t *oc = f_coeff + ((ok ? j : 0) * L + l) * D + x.r;
+      uint64_t dv[32];
 #pragma unroll
       for (int k = 0; k < 32; k++) {
-        const uint64_t dg = from_signed(bal_digit(cur[k], lb));
-        if (ok) oc[32 * k] = dg;
+        dv[k] = from_signed(bal_digit(cur[k], lb));
+        if (ok) oc[32 * k] = dv[k];
       }
+      if (smg && ok) store_sm_row(dv, smg + (j * L + l) * 512, x.r);
     }
     bool bad = false;
 #pragma unroll
@@ -806,8 +823,14 @@ hipError_t decompose_fused(const FusedSides &sd, size_t N, int lb, int L, int K,
   if (K > 15 || !fwd.mid || !sink || ncu < 1 || sd.nside < 1 || sd.nside > 2) return hipErrorInvalidValue;
   for (int s = 0; s < sd.nside; s++)
     if (!sd.smg[s]) return hipErrorInvalidValue;
-  const size_t words = sd.nside * N * 512;
-  hipLaunchKernelGGL(k_pack_sm, dim3((unsigned)((words / 4 + 255) / 256)), dim3(256), 0, st, sd, N, K, err);
+  // sides whose words from_w_ccs already wrote (only side 1, the step's new witness) are not re-packed
+  if ((sd.prepacked & ~2) || ((sd.prepacked & 2) && sd.nside != 2)) return hipErrorInvalidValue;
+  FusedSides sp = sd;
+  if (sd.prepacked & 2) sp.nside = 1;  // side 0 only
+  {
+    const size_t words = sp.nside * N * 512;
+    hipLaunchKernelGGL(k_pack_sm, dim3((unsigned)((words / 4 + 255) / 256)), dim3(256), 0, st, sp, N, K, err);
+  }
   // one 8-wave block per CU (LDS-bound); ntask = nblk K tasks spread evenly
   const size_t ntask = (N / L + 15) / 16 * (size_t)K * sd.nside;
   // every block takes the same number of tasks (no tail round on part of the
@@ -855,16 +878,17 @@ hipError_t transform_n32(uint64_t *data, size_t n, bool fwd, const ring::NegaTab
 constexpr size_t SPLIT_W = LF_SPLIT_W;
 size_t witness_split_w() { return SPLIT_W; }
 hipError_t from_w_ccs_n32(const uint64_t *w_ccs, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *f,
-                          const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err, hipStream_t st) {
+                          const ring::NegaTables &fwd, const ring::NegaTables &inv, int *err, hipStream_t st,
+                          uint32_t *smg) {
   if (W < SPLIT_W) {
     hipLaunchKernelGGL(k_from_w_ccs_digits, dim3(half_blocks(W, 4096)), dim3(256), 0, st, w_ccs, W, lb, L, f_coeff,
-                       inv.mid, err);
+                       inv.mid, err, smg);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return transform_n32(f, W * (size_t)L, true, fwd, st, f_coeff);
   }
   hipLaunchKernelGGL(k_from_w_ccs_n32, dim3(half_blocks(W, 4096)), dim3(256), 0, st, w_ccs, W, lb, L, f_coeff,
-                     f, fwd.mid, inv.mid, err);
+                     f, fwd.mid, inv.mid, err, smg);
   return hipGetLastError();
 }
 hipError_t from_f_n32(const uint64_t *f, size_t W, int lb, int L, uint64_t *f_coeff, uint64_t *w_ccs,

@@ -85,6 +85,7 @@ struct lf_ctx {
   bool timing = false;
   hipEvent_t join = nullptr;    // lf_dev_fold_step_batch: this stream's point to wait for / be waited on
   hipStream_t contract = nullptr;  // lf_ctx_set_contract_stream: where batched contractions led by this context run
+  bool prepacked1 = false;      // step_commit wrote side 1's packed words (fold_commit's fused d = 1024 path)
   hipEvent_t cjoin = nullptr;   // the end of the last such contraction
   std::vector<TimedLaunch> pending;
   std::map<int, std::pair<double, long>> stats;  // nvec -> (ms, count)
@@ -622,6 +623,9 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       c->dead_units.flags = c->dead;
       c->dead_units.rows = rows;
       c->fold_rows.dead = c->dead_units;
+      // side 1's words, when step_commit's from_w_ccs wrote them into this very buffer
+      sd.prepacked = c->prepacked1 && wi_f_coeff == b->f_coeff ? 2 : 0;
+      c->prepacked1 = false;
       PhaseTimer pt(c, LF_PHASE_DECOMPOSE);  // both sides in one launch
       LF_HIP(c, lfk::decompose_fused(sd, N, lb, L, K, t->fwd, c->frag, aj->geom.nch, c->d_err,
                                      c->sink, c->ncu, c->cur));
@@ -1478,9 +1482,26 @@ static int step_check(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t
 }
 static int step_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t W, const lf_fold_step_bufs *b,
                        int lb, int lbs, const lfk::OutPtrs &dst, Deferred *defer = nullptr) {
+  c->prepacked1 = false;
   {
     PhaseTimer pt(c, LF_PHASE_FROM_W_CCS);
-    LF_TRY(lf_dev_witness_from_w_ccs(c, pr, b->w_ccs, W, b->f_coeff, b->f));
+    // the fused X^1024 + 1 decomposition that fold_commit runs next packs both
+    // sides' digits into sign|magnitude words; the new witness's (side 1) are
+    // written here, by the kernel that makes its digits, instead of re-read
+    Tables *t;
+    LF_TRY(get_tables(c, pr->d, t));
+    const int L = pr->L, K = pr->K, d = pr->d;
+    const size_t N = W * (size_t)L;
+    const bool fused = aj->Af && aj->geom.Lp == L && d == 1024 && lbs == 1 && K <= 15 && t->fwd.mid &&
+                       t->inv.mid && lb <= K && aj->ncols == N && (!b->planes[0]) == (!b->planes[1]);
+    uint32_t *smg1 = nullptr;
+    if (fused) {
+      if (!b->planes[0]) LF_TRY(grow(c, c->smg, c->smg_elems, 2 * N * 512));
+      smg1 = b->planes[1] ? reinterpret_cast<uint32_t *>(b->planes[1]) : c->smg + N * 512;
+    }
+    if (!b->w_ccs || !b->f_coeff || !b->f) return fail(c, LF_ERR_INVALID_ARG, "null step buffer");
+    LF_HIP(c, lfk::from_w_ccs(b->w_ccs, W, d, lb, L, b->f_coeff, b->f, t->fwd, t->inv, c->d_err, c->cur, smg1));
+    c->prepacked1 = smg1 != nullptr;
   }
   return fold_commit(c, aj, pr, lb, lbs, W, b, b->f_coeff, b->f, dst, defer);
 }
