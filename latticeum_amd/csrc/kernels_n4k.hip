@@ -9,6 +9,9 @@
 // for another and there is no s_barrier in the loop. The four waves of one
 // work item share a block (one CU, one L2), so their interleaved slot stores
 // (stride 4) merge into whole lines before they reach HBM.
+#include <stdlib.h>
+#include <string.h>
+
 #include "digits.hpp"
 #include "frag.hpp"
 #include "kernels.hpp"
@@ -327,6 +330,195 @@ __global__ void __launch_bounds__(512, 1) k_decompose_n4k_fused(size_t N, int L,
   }
 }
 
+// ---------------------------------------------------------------- stage 1 on the matrix cores
+// The same step as k_decompose_n4k_fused with each quarter's stage 1 as one ternary
+// i8 product (tools/ntt4096_mx_model.py): with a = j1 + 32 j2 the quarter's input
+// is y[a] = s^a sum_b c_b x_b[a] (s = psi^(2 m0 - 3), c_b = 2^(120 b (2 m0 + 1))), so
+//   Y[j1][m1] s^-j1 = sum_{b, j2} Z2[m1][32 b + j2] x_b[j1 + 32 j2],
+//   Z2[m1][32 b + j2] = zeta^((2 m1 + 1) j2) s^(32 j2) c_b,
+// a K = 128 product of Z2's 8 D8 byte planes with the digits, and s^j1 joins the
+// middle factors (midq). The product runs transposed (A = the digits, rows j1; B =
+// Z2, columns m1), so lane (m1 = r, h) gets rows j1 = (i & 3) + 8 (i >> 2) + 4 h
+// of column m1, and one exchange between the wave's halves (32-bit shuffles) gives
+// lane (r, h) all 32 j1 of element h: no transpose tile. Without it the staging tile
+// of the operand rows fits in halves (512 slots, two rounds per unit) beside the
+// 32 KiB of Z2 planes and the middle factors. The lookup of the radix-4 butterfly,
+// the twist (32 products) and the 80 stage-1 butterflies per lane are gone.
+// Packed steps only (no f_coeff_k rows): the digits are read as the MFMA's A operand.
+constexpr int FM_SROW = 17;                   // staging row stride in u64 (16 groups + pad)
+constexpr int FM_S_U64 = (Q4 / 2) * FM_SROW;  // half the quarter's slots per round
+// digit bytes (nibble = |digit| bits of the four quarters b, signs << 4) -> the
+// signed ternary bytes of quarter b
+__device__ __forceinline__ int tern4(uint32_t w, int b) {
+  const uint32_t y = (w >> b) & 0x01010101u, sg = (w >> (4 + b)) & 0x01010101u;
+  return (int)(y | ((y & sg) * 0xFEu));
+}
+// one element's stage 1 into 16 values: out[i] = Y'[j1 = (i & 3) + 8 (i >> 2) + 4 h][m1 = r]
+// times its middle factor; w4: this lane's 16 digit bytes (j2 = 16 h .. 16 h + 15)
+__device__ __forceinline__ void mx_stage1_q(const int8_t *zl, const uint32_t *w4, const uint64_t *midl, int r, int h,
+                                            uint64_t *out) {
+  v4i a[4];
+#pragma unroll
+  for (int b = 0; b < 4; b++) a[b] = (v4i){tern4(w4[0], b), tern4(w4[1], b), tern4(w4[2], b), tern4(w4[3], b)};
+  auto zpiece = [&](int t, int b) { return *reinterpret_cast<const v4i *>(zl + (t * 32 + r) * 128 + 32 * b + 16 * h); };
+  auto plane = [&](int t) {
+    v16i acc = (v16i){0};
+#pragma unroll
+    for (int b = 0; b < 4; b++) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[b], zpiece(t, b), acc, 0, 0, 0);
+    return acc;
+  };
+  // Q = sum_t 2^(8t) D_t over 4 planes (|D_t| <= 128 x 128: pairs fit int32)
+  auto quarter = [&](int t0, int64_t *q) {
+    v16i a0 = plane(t0), a1 = plane(t0 + 1);
+    int32_t p[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) p[i] = a0[i] + a1[i] * 256;
+    a0 = plane(t0 + 2);
+    a1 = plane(t0 + 3);
+#pragma unroll
+    for (int i = 0; i < 16; i++) q[i] = (int64_t)p[i] + (int64_t)a0[i] * 65536 + (int64_t)a1[i] * (1ll << 24);
+  };
+  int64_t q0[16], q1[16];
+  quarter(0, q0);
+  quarter(4, q1);
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    // Y = Q0 + Q1 2^32 (|Q| < 2^39) folded as in kernels_n32.hip mx_stage1
+    const int64_t q1h = q1[i] >> 32;
+    const int64_t A = q0[i] - q1h;
+    const int64_t T = (A >> 32) + (int64_t)(uint32_t)q1[i] + q1h;
+    const uint64_t U = ((uint64_t)T << 32) | (uint32_t)A;
+    const uint64_t y = U + (uint64_t)((T >> 32) * (int64_t)gl::EPS);
+    const int j1 = (i & 3) + 8 * (i >> 2) + 4 * h;
+    out[i] = gl::mul(y, midl[j1 * 32 + n32::brv5(r)]);
+  }
+}
+
+template <bool NT>
+__global__ void __launch_bounds__(512, 1) k_decompose_n4k_mx(size_t N, int L, int lb, int K, FusedSides sd,
+                                                            const uint64_t *midq_g, const uint64_t *zq_g,
+                                                            uint4 *frag, int nch, uint64_t *sink) {
+  __shared__ uint64_t S[FM_S_U64];
+  __shared__ uint64_t midl[n32::MID_U64];
+  __shared__ uint4 zl4[2048];  // this quarter's 32 KiB of Z2 planes [t][m1][K]
+  __shared__ uint32_t vote[2][FQ_WAVES];
+  const int m0 = (blockIdx.x >> 3) & 3;
+  for (int q = threadIdx.x; q < n32::MID_U64; q += blockDim.x) midl[q] = midq_g[m0 * 1024 + q];
+  {
+    const uint4 *src = reinterpret_cast<const uint4 *>(zq_g) + (size_t)m0 * 2048;
+    for (int q = threadIdx.x; q < 2048; q += blockDim.x) zl4[q] = src[q];
+  }
+  __syncthreads();
+  const int8_t *zl = reinterpret_cast<const int8_t *>(zl4);
+  const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5, hw = 2 * wib + h;  // hw: this half's group within the block
+  const size_t W = N / L, nblk = (W + 15) / 16, nunit = sd.nside * nblk * K;
+  const uint64_t b_pow = gl::mul_pow2(1, lb);  // B = 2^lb
+  const size_t ustride = 8 * (size_t)(gridDim.x >> 5);
+  int nvote = 0;  // units voted on so far (block-uniform)
+  for (size_t unit = (blockIdx.x & 7) + 8 * (size_t)(blockIdx.x >> 5); unit < nunit; unit += ustride) {
+    const int side = unit >= nblk * K;
+    const size_t B = unit / K - side * nblk;
+    const int kb = (int)(unit % K);
+    const size_t g = 16 * B + hw;
+    const bool ok = g < W;
+    // the wave's two groups (past W: group 0); lane (r, h) reads bytes 16 h .. 16 h + 15 of both
+    const size_t ge0 = 16 * B + 2 * wib < W ? 16 * B + 2 * wib : 0;
+    const size_t ge1 = 16 * B + 2 * wib + 1 < W ? 16 * B + 2 * wib + 1 : 0;
+    const uint32_t *sm8 = sd.smg[side];
+    auto bytes_of = [&](size_t ge, int l) {
+      return reinterpret_cast<const uint4 *>(sm8 + (((ge * L + l) * K + kb) * 32 + r) * 8) + h;
+    };
+    uint64_t *fk = sd.f_k[side];
+    const int row = kb > 0 ? sd.row0[side] + kb - 1 : sd.row_p0[side];
+    uint32_t wn[8];
+    {
+      const uint4 a = *bytes_of(ge0, L - 1), c = *bytes_of(ge1, L - 1);
+      wn[0] = a.x, wn[1] = a.y, wn[2] = a.z, wn[3] = a.w, wn[4] = c.x, wn[5] = c.y, wn[6] = c.z, wn[7] = c.w;
+    }
+    asm volatile("" : "+v"(wn[0]), "+v"(wn[1]), "+v"(wn[2]), "+v"(wn[3]), "+v"(wn[4]), "+v"(wn[5]), "+v"(wn[6]),
+                 "+v"(wn[7]));
+    uint64_t acc[32];
+    for (int l = L - 1; l >= 0; l--) {
+      const size_t e = (size_t)kb * N + (ok ? g : 0) * L + l;
+      uint64_t v[32];
+      uint32_t nz = 0;
+#pragma unroll
+      for (int q = 0; q < 8; q++) nz |= wn[q];
+      const bool live = __ballot((nz & 0x0F0F0F0Fu) != 0) != 0;  // both elements, every quarter's bit
+      if (live) {
+        uint64_t y0[16], y1[16];
+        mx_stage1_q(zl, wn, midl, r, h, y0);
+        __builtin_amdgcn_sched_barrier(0);
+        mx_stage1_q(zl, wn + 4, midl, r, h, y1);
+        // lane (r, h) keeps element h: its own rows j1 = .. + 4 h, and the other half's
+        // rows of the same element from lane (r, 1 - h)
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+          const uint64_t give = h ? y0[i] : y1[i], keep = h ? y1[i] : y0[i];
+          const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)give, 32);
+          const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(give >> 32), 32);
+          const uint64_t got = ((uint64_t)hi << 32) | lo;
+          const int j = (i & 3) + 8 * (i >> 2);
+          v[j] = h ? got : keep;      // rows j1 = j      (half 0's)
+          v[j + 4] = h ? keep : got;  // rows j1 = j + 4  (half 1's)
+        }
+        n32::cyc_dif32<false>(v);  // v[i] = X[r + 32 brv5(i)]
+      } else {
+#pragma unroll
+        for (int k = 0; k < 32; k++) v[k] = 0;
+      }
+      {  // the next limb's bytes (at l = 0 a harmless reload of limb L - 1)
+        const int ln = l > 0 ? l - 1 : L - 1;
+        const uint4 a = *bytes_of(ge0, ln), c = *bytes_of(ge1, ln);
+        wn[0] = a.x, wn[1] = a.y, wn[2] = a.z, wn[3] = a.w, wn[4] = c.x, wn[5] = c.y, wn[6] = c.z, wn[7] = c.w;
+      }
+      if (fk) {
+        uint64_t *of = (ok ? fk + e * D4 : sink) + m0 + 4 * r;
+#pragma unroll
+        for (int i = 0; i < 32; i++) of[128 * n32::brv5(i)] = v[i];
+      }
+      horner_step(acc, v, l == L - 1, lb, b_pow);
+      if (row >= 0) {
+        const size_t u = B * L + l;  // contraction unit of these 16 columns
+        const int vs = nvote++ & 1;
+        if (sd.dead && lane == 0) vote[vs][wib] = live ? 1u : 0u;
+        __syncthreads();  // votes visible; every wave done reading the previous unit's staging
+        bool any = true;
+        if (sd.dead) {
+          uint32_t a = 0;
+#pragma unroll
+          for (int q = 0; q < FQ_WAVES; q++) a |= vote[vs][q];
+          any = a != 0;
+          if (threadIdx.x == 0) sd.dead[u * 32 + row] = any ? 0 : 1;
+        }
+        if (!any) continue;  // block-uniform
+        const int c = (int)(u >> 1), uh = (int)(u & 1);
+#pragma unroll
+        for (int hs = 0; hs < 2; hs++) {  // slots r + 32 brv5(i): i even -> < 512, i odd -> >= 512
+          if (hs) __syncthreads();  // every wave done reading the first half
+#pragma unroll
+          for (int i = hs; i < 32; i += 2) S[(r + 32 * n32::brv5(i) - 512 * hs) * FM_SROW + hw] = fenc(v[i]);
+          __syncthreads();
+          const int m1 = threadIdx.x + 512 * hs;
+          const uint64_t *src = S + threadIdx.x * FM_SROW;
+          uint64_t x[16];
+#pragma unroll
+          for (int j = 0; j < 16; j++) x[j] = src[j];
+          uint4 pu[8];
+          d8_transpose16(x, pu);
+          uint4 *out = frag + fv_index((size_t)m0 * Q4 + m1, nch, c, row, uh);
+#pragma unroll
+          for (int b = 0; b < 8; b++) out_store<NT>(&out[4 * b], pu[b]);
+        }
+      }
+    }
+    uint64_t *ow = (ok ? sd.w_ccs_k[side] + ((size_t)kb * W + g) * D4 : sink) + m0 + 4 * r;
+#pragma unroll
+    for (int i = 0; i < 32; i++) ow[128 * n32::brv5(i)] = gl::canon(acc[i]);
+  }
+}
+
 // the packed bytes (k_pack_sm8's layout) -> the K digit planes in coefficient form:
 // f_coeff_k[k][e][a + 1024 b] = digit k of that coefficient, one thread per output
 __global__ void k_expand_sm8(const uint32_t *sm8, size_t N, int K, uint64_t *fck) {
@@ -586,12 +778,29 @@ hipError_t decompose_n4k(const FusedSides &sd, size_t N, int lb, int L, int K, u
     // 32 blocks per group of 8 units (8 XCDs x 4 quarters), one block per CU
     const unsigned grid = (unsigned)(ncu / 32 * 32);
     // outputs: f_coeff_k, f_k, the operand rows (each K N d words per side) and w_ccs_k
-    if (dec_streaming(sd.nside * (size_t)K * N * D4 * 8 * 3, refold))
+    const bool nt = dec_streaming(sd.nside * (size_t)K * N * D4 * 8 * 3, refold);
+    // stage 1 on the matrix cores when no f_coeff_k rows are wanted (the packed steps);
+    // LATTICEUM_AMD_N4K=valu keeps the VALU form (A/B runs)
+    static const bool valu = [] {
+      const char *e = getenv("LATTICEUM_AMD_N4K");
+      return e && !strcmp(e, "valu");
+    }();
+    bool mx = fwd.zq && fwd.midq && !valu;
+    for (int s = 0; s < sd.nside; s++) mx = mx && !sd.f_coeff_k[s];
+    if (mx) {
+      if (nt)
+        hipLaunchKernelGGL(k_decompose_n4k_mx<true>, dim3(grid), dim3(512), 0, st, N, L, lb, K, s8, fwd.midq,
+                           fwd.zq, frag, nch, sink);
+      else
+        hipLaunchKernelGGL(k_decompose_n4k_mx<false>, dim3(grid), dim3(512), 0, st, N, L, lb, K, s8, fwd.midq,
+                           fwd.zq, frag, nch, sink);
+    } else if (nt) {
       hipLaunchKernelGGL(k_decompose_n4k_fused<true>, dim3(grid), dim3(512), 0, st, N, L, lb, K, s8, fwd.mid,
                          fwd.tw4, fwd.ztab, frag, nch, sink);
-    else
+    } else {
       hipLaunchKernelGGL(k_decompose_n4k_fused<false>, dim3(grid), dim3(512), 0, st, N, L, lb, K, s8, fwd.mid,
                          fwd.tw4, fwd.ztab, frag, nch, sink);
+    }
     return hipGetLastError();
   }
   const size_t words = sd.nside * N * Q4;

@@ -210,9 +210,10 @@ int get_tables(lf_ctx *c, int d, Tables *&out) {
     // 1024-point sub-transforms, then the radix-4 twists (fwd, inv) and the digit
     // butterfly table (kernels_n4k.hip)
     const size_t extra = d == 1024 ? 2048 : d == 4096 ? 2048 + 2 * 4096 + 1024 : 0;
-    // d = 1024: then the D8 byte planes of zeta^((2 m1 + 1) j2) for the matrix-core stage 1 (1024 u64)
+    // d = 1024: then the D8 byte planes of zeta^((2 m1 + 1) j2) for the matrix-core stage 1 (1024 u64);
+    // d = 4096: the quarters' stage-1 planes Z''_m0 (4 x 4096 u64) and middle factors (4 x 1024)
     const size_t az_off = 4 * (size_t)d + extra;
-    std::vector<uint64_t> h(az_off + (d == 1024 ? 1024 : 0));
+    std::vector<uint64_t> h(az_off + (d == 1024 ? 1024 : d == 4096 ? 4 * 4096 + 4 * 1024 : 0));
     const uint64_t psi = gl::pow(7, (gl::P - 1) / (2 * (uint64_t)d));
     const uint64_t psi_inv = gl::inv(psi), w = gl::mul(psi, psi), w_inv = gl::mul(psi_inv, psi_inv);
     const uint64_t dinv = gl::inv((uint64_t)d);
@@ -280,6 +281,31 @@ int get_tables(lf_ctx *c, int d, Tables *&out) {
             zt[m0 * 256 + idx] = z;
           }
         }
+        // stage 1 of quarter m0 as one ternary i8 product (tools/ntt4096_mx_model.py): with
+        // a = j1 + 32 j2 the twist psi^((2 m0 - 3) a) = s^j1 s^(32 j2), so
+        //   Z''_m0[m1][32 b + j2] = zeta^((2 m1 + 1) j2) s^(32 j2) 2^(120 b (2 m0 + 1))
+        //   midq[m0][j1][i] = p1^((2 brv5(i) + 1) j1) s^j1
+        int8_t *zq = reinterpret_cast<int8_t *>(h.data() + az_off);
+        uint64_t *mq = h.data() + az_off + 4 * 4096;
+        const uint64_t zeta = gl::pow(p1, 32);
+        for (int m0 = 0; m0 < 4; m0++) {
+          const uint64_t s = gl::pow(psi, (uint64_t)((2 * m0 - 3 + 8192) % 8192));
+          const uint64_t s32 = gl::pow(s, 32);
+          for (int m1 = 0; m1 < 32; m1++)
+            for (int b = 0; b < 4; b++)
+              for (int j2 = 0; j2 < 32; j2++) {
+                const uint64_t cb = gl::mul_pow2(1, (120 * b * (2 * m0 + 1)) % 192);
+                const uint64_t x = gl::mul(gl::mul(gl::pow(zeta, (uint64_t)(2 * m1 + 1) * j2), gl::pow(s32, j2)), cb);
+                const uint64_t tt = x <= 0x7F7F7F7F7F7F7F7Full ? x : x + 0xFFFFFFFFull;
+                const uint64_t dd = (tt + 0x8080808080808080ull) ^ 0x8080808080808080ull;
+                for (int t = 0; t < 8; t++)
+                  zq[(((size_t)m0 * 8 + t) * 32 + m1) * 128 + 32 * b + j2] = (int8_t)(uint8_t)(dd >> (8 * t));
+              }
+          for (int j1 = 0; j1 < 32; j1++) {
+            const uint64_t sj = gl::pow(s, j1);
+            for (int i = 0; i < 32; i++) mq[(size_t)m0 * 1024 + j1 * 32 + i] = gl::mul(h[4 * d + j1 * 32 + i], sj);
+          }
+        }
       }
     }
     LF_HIP(c, hipMalloc(&t.mem, h.size() * 8));
@@ -293,6 +319,8 @@ int get_tables(lf_ctx *c, int d, Tables *&out) {
       t.fwd.tw4 = t.mem + 4 * d + 2048;
       t.inv.tw4 = t.fwd.tw4 + 4096;
       t.fwd.ztab = t.inv.tw4 + 4096;
+      t.fwd.zq = t.mem + az_off;
+      t.fwd.midq = t.mem + az_off + 4 * 4096;
     }
   }
   out = &(c->tables[d] = t);

@@ -218,6 +218,9 @@ struct NegaTables {
   const uint64_t *tw4 = nullptr;   // d = 4096: radix-4 twists [m0][a] (fwd psi^((2m0-3)a), inv 4^-1 psi^-((2m0-3)a))
   const uint64_t *ztab = nullptr;  // d = 4096 fwd: butterflies of four balanced bits [m0][nibble | signs << 4]
   const uint64_t *az = nullptr;    // d = 1024 fwd: D8 byte planes of zeta^((2 m1 + 1) j2), int8 [8][32][32]
+  // d = 4096 fwd, stage 1 of each quarter m0 on the matrix cores (kernels_n4k.hip k_decompose_n4k_mx):
+  const uint64_t *zq = nullptr;    // D8 byte planes of Z''_m0[m1][32 b + j2], int8 [4][8][32][128]
+  const uint64_t *midq = nullptr;  // middle factors with the j1 twist, [4][j1 32][brv5(m1) 32]
 };
 
 // Radix-4 Stockham DFT of size D over LDS buffers x -> y (ping-pong), T threads.
