@@ -165,7 +165,10 @@ def kernel_names(LA, d, W, layout, keep_fk=True, packed=False):
                 else "k_from_f_split" if small else "k_from_f_n32",
                 "to_frag": "k_to_frag<true, false, true>"}
     if d == 4096:  # packed planes fold f_0 from the operand rows
-        return {"decompose": "k_decompose_n4k_fused" if layout == 1 else "k_decompose_n4k",
+        # packed steps run the matrix-core stage 1 (k_decompose_n4k_mx) unless LATTICEUM_AMD_N4K=valu
+        mx = packed and os.environ.get("LATTICEUM_AMD_N4K") != "valu"
+        return {"decompose": ("k_decompose_n4k_mx" if mx else "k_decompose_n4k_fused") if layout == 1
+                else "k_decompose_n4k",
                 "ajtai": mfma if layout == 1 else "k_ajtai_nega",
                 "fold": "k_fold_frag" if packed else "k_fold_nega", "from_w_ccs": "k_from_w_ccs_n4k",
                 "from_f": "k_from_f_n4k",

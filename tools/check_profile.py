@@ -21,7 +21,7 @@ import sys
 # every kernel a phase's HIP-event pair brackets (lf_api.hip fold_commit / fold_finish),
 # by base name; the primary kernel (launched once per phase record) comes first
 PHASE_KERNELS = {
-    "decompose": ("k_decompose_fused", "k_decompose_phi72_w", "k_decompose_n4k_fused", "k_decompose_n4k",
+    "decompose": ("k_decompose_fused", "k_decompose_phi72_w", "k_decompose_n4k_mx", "k_decompose_n4k_fused", "k_decompose_n4k",
                   "k_pack_sm", "k_pack_sm24", "k_pack_sm8", "k_pack_sm4", "k_expand_sm"),
     "fold": ("k_fold_coeff", "k_fold_coeff_phi72", "k_fold_nega", "k_fold_frag", "k_fold_coeff_sum", "k_pack_keys",
              "k_rho_prep", "k_rho_phi72", "k_fold_phi72_masks"),
