@@ -17,13 +17,15 @@ def planes_u64(d, K, N):
     return K * N if d == 24 else N * 256 if d == 1024 else N * K * 128
 
 
-def make_step(torch, A, kappa, d, W, seed, packed, keep_fk=True, rho=None):
+def make_step(torch, A, kappa, d, W, seed, packed, keep_fk=True, rho=None, zero_w=False):
     pr = params(d)
     K, L = pr.K, pr.L
     N = W * L
     dev = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.int64)).cuda()
     z = lambda n: torch.zeros(n, dtype=torch.int64, device="cuda")
-    w_ccs = rand(W * d, seed)
+    # zero_w: a zero witness, so every digit plane of the step's new side is zero
+    # (all its operand units dead: never written, read as the offset form of 0)
+    w_ccs = np.zeros(W * d, np.uint64) if zero_w else rand(W * d, seed)
     acc_fc, acc_f = valid_f_coeff(d, W, seed + 1)
     acc_cm = O.ajtai_commit(A, kappa, N, d, acc_f)
     if rho is None:
@@ -59,7 +61,7 @@ def expand(ctx, torch, pr, keep, N, d):
         keep["fk_coeff"][s], keep["fk"][s] = fck, fk
 
 
-def run_batch(d, W, kappa, S, packed, rounds=1, rho_long=False, cu_split=0):
+def run_batch(d, W, kappa, S, packed, rounds=1, rho_long=False, cu_split=0, zero_w=False):
     import torch
     pr = params(d)
     N = W * pr.L
@@ -75,7 +77,8 @@ def run_batch(d, W, kappa, S, packed, rounds=1, rho_long=False, cu_split=0):
         sch = LA.AjtaiCommitmentScheme(ctxs[0], device_tensor=At, kappa=kappa, ncols=N, d=d)
         for rnd in range(rounds):
             steps = [make_step(torch, A, kappa, d, W, 100 * rnd + 10 * i + 1, packed,
-                               rho=rand(2 * pr.K * d, 900 + i) if rho_long and i % 2 else None)
+                               rho=rand(2 * pr.K * d, 900 + i) if rho_long and i % 2 else None,
+                               zero_w=zero_w and i % 2 == 1)
                      for i in range(S)]
             torch.cuda.synchronize()  # torch wrote the inputs on its own stream
             ctxs[0].dev_fold_step_batch(ctxs[1:], sch, pr, W, [st["b"] for st in steps])
@@ -112,6 +115,16 @@ def test_fold_step_batch_contract_stream(d, S):
     a CU-masked stream beside the step streams' CUs): every step waits for its
     decomposition before the contraction and for the contraction after it"""
     run_batch(d, 37 if d == 1024 else 17, 3 if d == 24 else 2, S, packed=True, rounds=2, cu_split=64)
+
+
+@pytest.mark.parametrize("d", [24, 1024, 4096])
+def test_fold_step_batch_zero_witness(d):
+    """every other step of the batch folds a zero witness: all of its new side's
+    digit planes are zero, so every one of its operand units is dead (unwritten,
+    read as the offset form of 0) next to steps whose units are live, and the
+    d = 4096 matrix-core stage 1 and the fold from the rows skip them"""
+    run_batch(d, 37 if d == 1024 else 17, 3 if d == 24 else 2, 4 if d != 4096 else 2, packed=True, rounds=2,
+              zero_w=True)
 
 
 def test_fold_step_batch_wide_kappa():
