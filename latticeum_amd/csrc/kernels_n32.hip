@@ -537,19 +537,18 @@ __global__ void __launch_bounds__(256, 1) k_decompose_n32(const uint64_t *f_coef
 // plane k >= 1 and limb l the block holds one 16-column unit of the Ajtai
 // contraction order (ajtai_mfma.hip, Lp = L) and writes it straight into the
 // vector-major operand buffer -- the planes never make a second trip through
-// HBM to be re-laid out. Per (k, l): NTT (per-wave transpose tile T), then the
-// D8 words of the 16 outputs go through a slot-major staging tile S that
-// overlaps T (three barriers separate the uses), and each thread emits two
-// slots' 128-byte operand pieces.
+// HBM to be re-laid out. Per (k, l): NTT (stage 1 on the matrix cores, its
+// transpose a half exchange in registers), then the D8 words of the 16 outputs
+// go through a slot-major staging tile S (two barriers per unit: the first also
+// orders the previous unit's reads before the new writes), and each thread
+// emits two slots' 128-byte operand pieces.
 //
 // The group's coefficients come pre-packed as 16-bit sign|magnitude
 // (k_pack_sm: smg[(col 16 + q) 32 + r] = x[r + 32(2q)] | x[r + 32(2q+1)] << 16),
 // read back per (k, l), one plane ahead.
 constexpr int FD_WAVES = 8;
 constexpr int FD_SROW = 17;  // staging row stride in u64 (16 columns + pad: conflict-free)
-constexpr int FD_T_U64 = FD_WAVES * n32::WAVE_U64;
 constexpr int FD_S_U64 = D * FD_SROW;
-constexpr int FD_LDS_U64 = FD_T_U64 > FD_S_U64 ? FD_T_U64 : FD_S_U64;
 
 // four packed words per thread (t0 = 4 * thread): 2 x 32 contiguous bytes in,
 // one 16-B store out
@@ -608,18 +607,22 @@ __device__ __forceinline__ v4i mx_digits(const uint32_t *w8, int kb) {
 __device__ __forceinline__ v4i az_piece(const int8_t *azl, int t, int r, int h) {
   return *reinterpret_cast<const v4i *>(azl + (t * 32 + r) * 32 + 16 * h);
 }
-__device__ __forceinline__ void mx_stage1(const int8_t *azl, const uint32_t *w8, int kb, const uint64_t *midT,
-                                          uint64_t *Te, int r, int h) {
+// Transposed: digits as the A operand (rows j1, K = j2), Z as B (K = j2, columns
+// m1), so lane (r, h) gets Y[j1][m1 = r] for j1 = (i & 3) + 8 (i >> 2) + 4 h in
+// register i -- the rows of column m1 = r that stage 2 wants in lane r, split
+// between the two halves. mid2[j1][m1] = psi^((2 m1 + 1) j1) (mid2_stage).
+__device__ __forceinline__ void mx_stage1_t(const int8_t *azl, const uint32_t *w8, int kb, const uint64_t *mid2,
+                                            uint64_t *y, int r, int h) {
   const v4i b = mx_digits(w8, kb);
   // Q = sum_t 2^(8t) D_t over 4 planes, two planes at a time (|partial| < 2^21 in int32)
   auto quarter = [&](int t0, int64_t *q) {
-    v16i a0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(az_piece(azl, t0, r, h), b, (v16i){0}, 0, 0, 0);
-    v16i a1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(az_piece(azl, t0 + 1, r, h), b, (v16i){0}, 0, 0, 0);
+    v16i a0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(b, az_piece(azl, t0, r, h), (v16i){0}, 0, 0, 0);
+    v16i a1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(b, az_piece(azl, t0 + 1, r, h), (v16i){0}, 0, 0, 0);
     int32_t p[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) p[i] = a0[i] + a1[i] * 256;
-    a0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(az_piece(azl, t0 + 2, r, h), b, (v16i){0}, 0, 0, 0);
-    a1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(az_piece(azl, t0 + 3, r, h), b, (v16i){0}, 0, 0, 0);
+    a0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(b, az_piece(azl, t0 + 2, r, h), (v16i){0}, 0, 0, 0);
+    a1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(b, az_piece(azl, t0 + 3, r, h), (v16i){0}, 0, 0, 0);
 #pragma unroll
     for (int i = 0; i < 16; i++) q[i] = (int64_t)(p[i] + a0[i] * 65536) + (int64_t)a1[i] * (1ll << 24);
   };
@@ -636,29 +639,30 @@ __device__ __forceinline__ void mx_stage1(const int8_t *azl, const uint32_t *w8,
     const int64_t A = q0[i] - q1h;
     const int64_t T = (A >> 32) + (int64_t)(uint32_t)q1[i] + q1h;
     const uint64_t U = ((uint64_t)T << 32) | (uint32_t)A;
-    const uint64_t y = U + (uint64_t)((T >> 32) * (int64_t)gl::EPS);
-    const int m1 = (i & 3) + 8 * (i >> 2) + 4 * h;
-    // midT[i'][j1] = psi^((2 brv5(i') + 1) j1): row brv5(m1) = brv5(m1 without 4 h) | 4 h
-    const int row = n32::brv5((i & 3) + 8 * (i >> 2)) | (4 * h);
-    Te[m1 * n32::RS + r] = gl::mul(y, midT[row * 32 + r]);
+    const uint64_t yv = U + (uint64_t)((T >> 32) * (int64_t)gl::EPS);
+    const int j1 = (i & 3) + 8 * (i >> 2) + 4 * h;
+    y[i] = gl::mul(yv, mid2[j1 * 32 + r]);
   }
 }
-
+// mid2[j1][m1] = psi^((2 m1 + 1) j1) from the launcher's table mid[j1][i'] =
+// psi^((2 brv5(i') + 1) j1) (n32::stage_mid's source layout)
+__device__ __forceinline__ void mid2_stage(uint64_t *mid2, const uint64_t *mid) {
+  for (int q = threadIdx.x; q < n32::MID_U64; q += blockDim.x) mid2[q] = mid[(q & ~31) | n32::brv5(q & 31)];
+}
 template <bool NT>
 __global__ void __launch_bounds__(512, 1) k_decompose_fused(size_t N, int L, int lb,
                                                            int K, FusedSides sd, const uint64_t *mid_fg,
                                                            const uint64_t *az_g, uint4 *frag, int nch,
                                                            uint64_t *sink) {
-  __shared__ uint64_t lds_all[FD_LDS_U64];
-  __shared__ uint64_t mid_f[n32::MID_U64];
+  __shared__ uint64_t lds_all[FD_S_U64];
+  __shared__ uint64_t mid2[n32::MID_U64];
   __shared__ uint64_t az_l[1024];  // the 8 KiB of D8 byte planes of zeta^((2 m1 + 1) j2)
   __shared__ uint32_t vote[2][FD_WAVES];  // per wave: its plane is nonzero in the current unit
-  n32::stage_mid(mid_f, mid_fg);
+  mid2_stage(mid2, mid_fg);
   for (int q = threadIdx.x; q < 1024; q += blockDim.x) az_l[q] = az_g[q];
   __syncthreads();
   const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5, hw = 2 * wib + h;  // hw: this half's group within the block
-  uint64_t *T = lds_all + wib * n32::WAVE_U64 + h * n32::HALF_U64;
   uint64_t *S = lds_all;
   const size_t W = N / L, nblk = (W + 15) / 16;
   const uint64_t b_pow = gl::mul_pow2(1, lb);  // B = 2^lb
@@ -698,7 +702,6 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(size_t N, int L, int
       for (int l = L - 1; l >= 0; l--) {
         const size_t e = (size_t)kb * N + gg * L + l;
         uint64_t v[32];
-        uint64_t *T0 = lds_all + wib * n32::WAVE_U64;
         // Is digit plane kb of this limb zero on both of the wave's elements? The top
         // limb of a balanced base-B decomposition of a field element has |digit| <= 8
         // (signed representative < 2^63, B^(L-1) = 2^60), so its planes 4..K-1 vanish,
@@ -711,9 +714,11 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(size_t N, int L, int
         for (int q = 0; q < 16; q++) nz |= wn[q] >> kb;
         const bool live = __ballot((nz & 0x10001u) != 0) != 0;
         if (live) {
-          mx_stage1(azl, wn, kb, mid_f, T0, r, h);
+          uint64_t y0[16], y1[16];
+          mx_stage1_t(azl, wn, kb, mid2, y0, r, h);
           __builtin_amdgcn_sched_barrier(0);  // one element's products and epilogue at a time (registers)
-          mx_stage1(azl, wn + 8, kb, mid_f, T0 + n32::HALF_U64, r, h);
+          mx_stage1_t(azl, wn + 8, kb, mid2, y1, r, h);
+          n32::halves_to_elements(y0, y1, v);  // lane m1 = r of element h: its 32 j1
         }
         {  // words for the next limb, in flight through the second stage (at l = 0 a
            // harmless reload of limb L - 1)
@@ -722,10 +727,6 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(size_t N, int L, int
           for (int q = 0; q < 16; q++) wn[q] = word(q, ln);
         }
         if (live) {
-          n32::wave_lds_sync();
-#pragma unroll
-          for (int j = 0; j < 32; j++) v[j] = T[r * n32::RS + j];  // lane m1 = r of element h: its 32 j1
-          n32::wave_lds_sync();
           n32::cyc_dif32<false>(v);
         } else {
 #pragma unroll
@@ -755,7 +756,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(size_t N, int L, int
           // before every wave has passed the next unit's barrier.
           const int vs = nvote++ & 1;
           if (sd.dead && lane == 0) vote[vs][wib] = live ? 1u : 0u;
-          __syncthreads();  // every wave is past its transpose: S may overwrite T
+          __syncthreads();  // votes visible; every wave is done reading the previous unit's S
           bool any = true;
           if (sd.dead) {
             uint32_t a = 0;
@@ -782,7 +783,6 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(size_t N, int L, int
 #pragma unroll
             for (int b = 0; b < 8; b++) out_store<NT>(&out[4 * b], pu[b]);
           }
-          __syncthreads();  // S consumed before the next transpose
         }
       }
       if (ok) {

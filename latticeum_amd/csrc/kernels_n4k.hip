@@ -451,18 +451,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_n4k_mx(size_t N, int L, in
         mx_stage1_q(zl, wn, midl, r, h, y0);
         __builtin_amdgcn_sched_barrier(0);
         mx_stage1_q(zl, wn + 4, midl, r, h, y1);
-        // lane (r, h) keeps element h: its own rows j1 = .. + 4 h, and the other half's
-        // rows of the same element from lane (r, 1 - h)
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-          const uint64_t give = h ? y0[i] : y1[i], keep = h ? y1[i] : y0[i];
-          const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)give, 32);
-          const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(give >> 32), 32);
-          const uint64_t got = ((uint64_t)hi << 32) | lo;
-          const int j = (i & 3) + 8 * (i >> 2);
-          v[j] = h ? got : keep;      // rows j1 = j      (half 0's)
-          v[j + 4] = h ? keep : got;  // rows j1 = j + 4  (half 1's)
-        }
+        n32::halves_to_elements(y0, y1, v);  // lane (r, h): element h, all 32 rows j1
         n32::cyc_dif32<false>(v);  // v[i] = X[r + 32 brv5(i)]
       } else {
 #pragma unroll

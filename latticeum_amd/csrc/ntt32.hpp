@@ -185,6 +185,21 @@ __device__ __forceinline__ void transpose_inv_w(uint64_t *v, uint32_t *lds, int 
   wave_lds_sync();
 }
 
+// The two halves' rows to one element per lane: y0 / y1 hold elements 0 / 1 at
+// rows j1 = (i & 3) + 8 (i >> 2) + 4 h; a half exchange (lanes 32-63 of the first
+// operand with lanes 0-31 of the second) leaves lane (r, h) element h's rows
+// j1 = .. in the first and j1 = .. + 4 in the second.
+__device__ __forceinline__ void halves_to_elements(const uint64_t *y0, const uint64_t *y1, uint64_t *v) {
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)y0[i], (uint32_t)y1[i], false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(y0[i] >> 32), (uint32_t)(y1[i] >> 32), false, false);
+    const int j = (i & 3) + 8 * (i >> 2);
+    v[j] = ((uint64_t)hi[0] << 32) | lo[0];
+    v[j + 4] = ((uint64_t)hi[1] << 32) | lo[1];
+  }
+}
+
 // middle factors: v[i] *= mid[r][i]. The 32 x 32 table is staged once per
 // block into LDS as midT[i][r] (conflict-free column reads; LDS waits do not
 // drain the wave's outstanding global stores the way a vmcnt wait would).
