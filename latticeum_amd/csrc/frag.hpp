@@ -168,37 +168,58 @@ __device__ __forceinline__ void fold_frag_block(size_t vb, const uint4 *frag, in
   const int ng = d >> 4, G = (int)(vb % ng), c = (int)(vb / ng);
   const int s = 16 * G + 4 * qq + sl, sr = frag_slot(s, qd);
   constexpr int MAXR = (LF_MAX_VECS + 7) / 8;  // rows per vector group
+  // Three rounds of independent loads (no load waits on another of its round):
+  // the rows' metadata, then their dead flags and rho values, then every live
+  // row's operand bytes -- so a block pays three memory latencies, not one per row
   bool use[MAXR];
-  uint64_t rv[MAXR];
-  const uint4 *pr[MAXR];
+  int row[MAXR], rix[MAXR];
 #pragma unroll
   for (int i = 0; i < MAXR; i++) {
     const int v = vg + 8 * i;
     use[i] = v < fr.n;
-    const int row = use[i] ? fr.row[v] : 0;
+    row[i] = fr.row[use[i] ? v : 0];
+    rix[i] = fr.rho[use[i] ? v : 0];
+  }
+  uint64_t rv[MAXR];
+  const uint4 *pr[MAXR];
+  if (fr.dead.flags) {  // uniform
     // a unit the decomposition left unwritten holds zero: nothing to add
-    if (use[i] && fr.dead.flags && ((fr.dead.rows >> row) & 1))
-      use[i] = !fr.dead.flags[(2 * (size_t)c + h) * 32 + row];
-    rv[i] = use[i] ? rho[(size_t)fr.rho[v] * d + sr] : 0;
-    pr[i] = frag + fv_index(s, nch, c, row, h);
+    uint8_t fl[MAXR];
+#pragma unroll
+    for (int i = 0; i < MAXR; i++) fl[i] = fr.dead.flags[(2 * (size_t)c + h) * 32 + row[i]];
+#pragma unroll
+    for (int i = 0; i < MAXR; i++)
+      if (((fr.dead.rows >> row[i]) & 1) && fl[i]) use[i] = false;
+  }
+#pragma unroll
+  for (int i = 0; i < MAXR; i++) {
+    rv[i] = rho[(size_t)rix[i] * d + sr];
+    pr[i] = frag + fv_index(s, nch, c, row[i], h);
   }
   gl::CAcc acc[CW];
 #pragma unroll
   for (int j = 0; j < CW; j++) gl::cacc_zero(acc[j]);
+  if (CW == 16) {
 #pragma unroll
-  for (int i = 0; i < MAXR; i++) {
-    if (!use[i]) continue;
-    uint64_t x[CW];
-    if (CW == 16) {
+    for (int i = 0; i < MAXR; i++) {
+      if (!use[i]) continue;
+      uint64_t x[CW];
       uint4 u[8];
 #pragma unroll
       for (int k = 0; k < 8; k++) u[k] = pr[i][4 * k];
       fenc_untranspose16(u, x);
-    } else {
+#pragma unroll
+      for (int j = 0; j < CW; j++) gl::cacc_mad(acc[j], rv[i], x[j]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < MAXR; i++) {
+      if (!use[i]) continue;
       // columns 8 cp .. 8 cp + 7 are bytes 8 cp .. 8 cp + 7 of each digit's piece
       uint2 u2[8];
 #pragma unroll
       for (int k = 0; k < 8; k++) u2[k] = reinterpret_cast<const uint2 *>(pr[i] + 4 * k)[cp];
+      uint64_t x[CW];
 #pragma unroll
       for (int q = 0; q < 2; q++) {
         uint32_t w[8], lo[4], hi[4];
@@ -209,9 +230,9 @@ __device__ __forceinline__ void fold_frag_block(size_t vb, const uint4 *frag, in
 #pragma unroll
         for (int cc = 0; cc < 4; cc++) x[4 * q + cc] = ((uint64_t)lo[cc] | ((uint64_t)hi[cc] << 32)) ^ FOFF;
       }
-    }
 #pragma unroll
-    for (int j = 0; j < CW; j++) gl::cacc_mad(acc[j], rv[i], x[j]);
+      for (int j = 0; j < CW; j++) gl::cacc_mad(acc[j], rv[i], x[j]);
+    }
   }
   // output o = column (32) x slot (16): o = (16 h + jj) 16 + 4 qq + sl
 #pragma unroll
