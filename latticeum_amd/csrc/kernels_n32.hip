@@ -610,9 +610,9 @@ __device__ __forceinline__ v4i az_piece(const int8_t *azl, int t, int r, int h) 
 // Transposed: digits as the A operand (rows j1, K = j2), Z as B (K = j2, columns
 // m1), so lane (r, h) gets Y[j1][m1 = r] for j1 = (i & 3) + 8 (i >> 2) + 4 h in
 // register i -- the rows of column m1 = r that stage 2 wants in lane r, split
-// between the two halves. mid2[j1][m1] = psi^((2 m1 + 1) j1) (mid2_stage).
-__device__ __forceinline__ void mx_stage1_t(const int8_t *azl, const uint32_t *w8, int kb, const uint64_t *mid2,
-                                            uint64_t *y, int r, int h) {
+// between the two halves. The middle factors come after both elements
+// (mid2_apply: mid2[j1][m1] = psi^((2 m1 + 1) j1), staged by mid2_stage).
+__device__ __forceinline__ void mx_stage1_t(const int8_t *azl, const uint32_t *w8, int kb, uint64_t *y, int r, int h) {
   const v4i b = mx_digits(w8, kb);
   // Q = sum_t 2^(8t) D_t over 4 planes, two planes at a time (|partial| < 2^21 in int32)
   auto quarter = [&](int t0, int64_t *q) {
@@ -640,8 +640,17 @@ __device__ __forceinline__ void mx_stage1_t(const int8_t *azl, const uint32_t *w
     const int64_t T = (A >> 32) + (int64_t)(uint32_t)q1[i] + q1h;
     const uint64_t U = ((uint64_t)T << 32) | (uint32_t)A;
     const uint64_t yv = U + (uint64_t)((T >> 32) * (int64_t)gl::EPS);
+    y[i] = yv;  // the middle factors follow for both elements at once (mid2_apply)
+  }
+}
+// y0, y1 *= mid2[j1][m1 = r] with one table read per row for both elements
+__device__ __forceinline__ void mid2_apply(const uint64_t *mid2, uint64_t *y0, uint64_t *y1, int r, int h) {
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
     const int j1 = (i & 3) + 8 * (i >> 2) + 4 * h;
-    y[i] = gl::mul(yv, mid2[j1 * 32 + r]);
+    const uint64_t m = mid2[j1 * 32 + r];
+    y0[i] = gl::mul(y0[i], m);
+    y1[i] = gl::mul(y1[i], m);
   }
 }
 // mid2[j1][m1] = psi^((2 m1 + 1) j1) from the launcher's table mid[j1][i'] =
@@ -715,9 +724,10 @@ __global__ void __launch_bounds__(512, 1) k_decompose_fused(size_t N, int L, int
         const bool live = __ballot((nz & 0x10001u) != 0) != 0;
         if (live) {
           uint64_t y0[16], y1[16];
-          mx_stage1_t(azl, wn, kb, mid2, y0, r, h);
+          mx_stage1_t(azl, wn, kb, y0, r, h);
           __builtin_amdgcn_sched_barrier(0);  // one element's products and epilogue at a time (registers)
-          mx_stage1_t(azl, wn + 8, kb, mid2, y1, r, h);
+          mx_stage1_t(azl, wn + 8, kb, y1, r, h);
+          mid2_apply(mid2, y0, y1, r, h);
           n32::halves_to_elements(y0, y1, v);  // lane m1 = r of element h: its 32 j1
         }
         {  // words for the next limb, in flight through the second stage (at l = 0 a

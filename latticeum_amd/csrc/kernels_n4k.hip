@@ -339,7 +339,7 @@ __global__ void __launch_bounds__(512, 1) k_decompose_n4k_fused(size_t N, int L,
 // a K = 128 product of Z2's 8 D8 byte planes with the digits, and s^j1 joins the
 // middle factors (midq). The product runs transposed (A = the digits, rows j1; B =
 // Z2, columns m1), so lane (m1 = r, h) gets rows j1 = (i & 3) + 8 (i >> 2) + 4 h
-// of column m1, and one exchange between the wave's halves (32-bit shuffles) gives
+// of column m1, and one exchange between the wave's halves (v_permlane32_swap) gives
 // lane (r, h) all 32 j1 of element h: no transpose tile. Without it the staging tile
 // of the operand rows fits in halves (512 slots, two rounds per unit) beside the
 // 32 KiB of Z2 planes and the middle factors. The lookup of the radix-4 butterfly,
@@ -354,9 +354,8 @@ __device__ __forceinline__ int tern4(uint32_t w, int b) {
   return (int)(y | ((y & sg) * 0xFEu));
 }
 // one element's stage 1 into 16 values: out[i] = Y'[j1 = (i & 3) + 8 (i >> 2) + 4 h][m1 = r]
-// times its middle factor; w4: this lane's 16 digit bytes (j2 = 16 h .. 16 h + 15)
-__device__ __forceinline__ void mx_stage1_q(const int8_t *zl, const uint32_t *w4, const uint64_t *midl, int r, int h,
-                                            uint64_t *out) {
+// (before its middle factor, midq_apply); w4: this lane's 16 digit bytes (j2 = 16 h .. 16 h + 15)
+__device__ __forceinline__ void mx_stage1_q(const int8_t *zl, const uint32_t *w4, int r, int h, uint64_t *out) {
   v4i a[4];
 #pragma unroll
   for (int b = 0; b < 4; b++) a[b] = (v4i){tern4(w4[0], b), tern4(w4[1], b), tern4(w4[2], b), tern4(w4[3], b)};
@@ -389,8 +388,17 @@ __device__ __forceinline__ void mx_stage1_q(const int8_t *zl, const uint32_t *w4
     const int64_t T = (A >> 32) + (int64_t)(uint32_t)q1[i] + q1h;
     const uint64_t U = ((uint64_t)T << 32) | (uint32_t)A;
     const uint64_t y = U + (uint64_t)((T >> 32) * (int64_t)gl::EPS);
+    out[i] = y;  // the middle factors follow for both elements at once (midq_apply)
+  }
+}
+// y0, y1 *= midq[j1][brv5(r)], one table read per row for both elements
+__device__ __forceinline__ void midq_apply(const uint64_t *midl, uint64_t *y0, uint64_t *y1, int r, int h) {
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
     const int j1 = (i & 3) + 8 * (i >> 2) + 4 * h;
-    out[i] = gl::mul(y, midl[j1 * 32 + n32::brv5(r)]);
+    const uint64_t m = midl[j1 * 32 + n32::brv5(r)];
+    y0[i] = gl::mul(y0[i], m);
+    y1[i] = gl::mul(y1[i], m);
   }
 }
 
@@ -448,9 +456,10 @@ __global__ void __launch_bounds__(512, 1) k_decompose_n4k_mx(size_t N, int L, in
       const bool live = __ballot((nz & 0x0F0F0F0Fu) != 0) != 0;  // both elements, every quarter's bit
       if (live) {
         uint64_t y0[16], y1[16];
-        mx_stage1_q(zl, wn, midl, r, h, y0);
+        mx_stage1_q(zl, wn, r, h, y0);
         __builtin_amdgcn_sched_barrier(0);
-        mx_stage1_q(zl, wn + 4, midl, r, h, y1);
+        mx_stage1_q(zl, wn + 4, r, h, y1);
+        midq_apply(midl, y0, y1, r, h);
         n32::halves_to_elements(y0, y1, v);  // lane (r, h): element h, all 32 rows j1
         n32::cyc_dif32<false>(v);  // v[i] = X[r + 32 brv5(i)]
       } else {
