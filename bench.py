@@ -531,7 +531,13 @@ class Workload:
         self.sync()
         self.sch = None
         self.keeps, self.bufs = [], []
-        for c in self.ctxs:
+        if getattr(self, "cstream", None) is not None:
+            # the group leaders hold ctx 0's CU-masked contract stream: clear it
+            # everywhere before ctx 0 (its owner) releases it
+            for c in self.ctxs:
+                c.set_contract_stream(None)
+            self.cstream = None
+        for c in self.ctxs[1:] + self.ctxs[:1]:  # ctx 0, the owner of shared streams, last
             c.close()
         self.ctxs = []
 
@@ -1194,7 +1200,7 @@ def compact_line(out, detail):
     keys = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "warmup_steps_run", "ms_per_step",
             "higher_is_better", "scaling", "vs_baseline", "dtype", "data")
     line = {k: out.get(k) for k in keys}
-    cfg = dict(out.get("config") or {})
+    cfg = {k: v for k, v in (out.get("config") or {}).items() if v is not None}
     cfg["workload"] = cfg.get("workload_short", cfg.get("workload"))
     cfg.pop("workload_short", None)
     line["config"] = cfg
@@ -1325,7 +1331,15 @@ def main():
                                       + (f"; groups of {group} steps whose contractions are one launch "
                                          f"(one pass over A per group)" if batched else "")
                                       + (f"; each group's contraction on the last {args.cu_split} CUs, the step "
-                                         f"streams on the others" if args.cu_split and batched else "")},
+                                         f"streams on the others" if args.cu_split and batched else ""),
+                       # BASELINE configs[3] names an "RCCL accumulator reduce": in LatticeFold
+                       # that is the column-sharded fold's all-reduce of the partial commitments,
+                       # timed in `sharded_fold` (N > 1); the independent step streams of `value`
+                       # have nothing to reduce (summing unrelated accumulators has no meaning)
+                       "configs3_reduce": ("the RCCL accumulator reduce of configs[3] is the column-sharded fold's "
+                                           "mod-p all-reduce of the 29 partial commitments per step, timed in "
+                                           "sharded_fold; value counts independent step streams (no collective)")
+                       if world > 1 else None},
             "hbm_gbs_step_algorithmic": step_bytes * value / world / 1e9,
             "step_hbm": step_hbm(d, W, kappa, group if batched else 1, phases, value / world, L, K),
             # the dominant phase by device time per step (HIP events on the launch

@@ -339,13 +339,29 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const
       }
     }
   }
-  auto dead_mask = [&](int c) -> uint32_t {  // c uniform
+  // c uniform. Each dm[m] is read with its own readlane and the word picked on
+  // the scalar side: a per-lane select over dm[] made the compiler keep the
+  // array in LDS, and that read's lgkmcnt(0) wait drained the chunk's 8 operand
+  // reads before its first product.
+  auto dead_mask = [&](int c) -> uint32_t {
     if (!has_dead) return 0u;
-    const int ci = c - c0;
-    uint32_t sel = dm[0];
+#ifdef LF_AB_OLD_DM
+    {
+      const int ci = c - c0;
+      uint32_t sel = dm[0];
 #pragma unroll
-    for (int m = 1; m < NDM; m++) sel = (ci >> 6) == m ? dm[m] : sel;
-    return __builtin_amdgcn_readlane(sel, ci & 63);
+      for (int m = 1; m < NDM; m++) sel = (ci >> 6) == m ? dm[m] : sel;
+      return __builtin_amdgcn_readlane(sel, ci & 63);
+    }
+#endif
+    const int ci = c - c0, m = ci >> 6, l = ci & 63;
+    uint32_t r = __builtin_amdgcn_readlane(dm[0], l);
+#pragma unroll
+    for (int k = 1; k < NDM; k++) {
+      const uint32_t x = __builtin_amdgcn_readlane(dm[k], l);
+      r = m == k ? x : r;
+    }
+    return r;
   };
   const int hl = lane >> 5;
   const uint4 *z80 = so_.zero80 + (lane & 31);
@@ -392,7 +408,13 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const
       // A(c + DP)'s loads follow the last product reading that register
       // (the issue order F then A is unchanged, so vm_wait_chunk still holds)
 #pragma unroll
-      for (int k = 0; k < 8; k++) asm volatile("ds_read_b128 %0, %1" : "=v"(b[k]) : "v"(fbase + 16u * fpos[k]));
+      for (int k = 0; k < 8; k++) {
+#ifdef LF_T_NODS  // timing-only probe: no operand reads (wrong results)
+        b[k] = (v4i){(int)fbase, k, 0, 0};
+#else
+        asm volatile("ds_read_b128 %0, %1" : "=v"(b[k]) : "v"(fbase + 16u * fpos[k]));
+#endif
+      }
       const bool more_f = c + DP - 1 < c1, more_a = c + DP < c1;
       const int fb = (j + DP - 1) % DP;
       const uint32_t dmn = more_f ? dead_mask(c + DP - 1) : 0u;
@@ -409,16 +431,22 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const
           for (int ka = 0; ka < 8; ka++)
             acc[ka + kb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ra[j][ka], b[kb], acc[ka + kb], 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
+#ifndef LF_T_NOF  // timing-only probe: no F copies in the loop (wrong results)
           if (more_f && kb < nf) stage_f_piece(c + DP - 1, fb, kb, dmn);
+#endif
           __builtin_amdgcn_sched_barrier(0);
         } else {
+#ifndef LF_T_NOF
           if (more_f && nf == 8) stage_f_piece(c + DP - 1, fb, 7, dmn);
+#endif
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int ka = 0; ka < 8; ka++) {
             acc[ka + 7] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ra[j][ka], b[7], acc[ka + 7], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
+#ifndef LF_T_NOA  // timing-only probe: no A loads in the loop (wrong results)
             if (more_a) ra[j][ka] = gload16<CPA>(pa + ((size_t)(c + DP) * 8 + ka) * 64);
+#endif
             __builtin_amdgcn_sched_barrier(0);
           }
         }
@@ -577,9 +605,11 @@ hipError_t ajtai_mfma_steps(const uint4 *Af, const uint64_t *kr, size_t kappa, c
                             hipEvent_t ev0, hipEvent_t ev1, const DeadUnits *dead, const uint4 *zero80) {
   const int dv = mfma_dim(d);
   const int ktiles = mfma_ktiles(kappa);
-  // zero80 (32 pieces of 0x80 bytes) is the copy source of every operand piece
-  // that is not read from the rows: dead units and the vectors past nvec
-  if (!kr || !zero80 || kappa < 1 || ktiles > LF_MAX_KTILES || nvec < 1 || nvec > 32 || dv % 4 || nsteps < 1 ||
+  // zero80 (32 pieces of 0x80 bytes) is the copy source of the dead units'
+  // operand pieces: required only when some step has dead-unit flags
+  bool any_dead = false;
+  for (int s = 0; dead && s < nsteps && s < LF_MAX_STEPS; s++) any_dead |= dead[s].flags != nullptr;
+  if (!kr || (any_dead && !zero80) || kappa < 1 || ktiles > LF_MAX_KTILES || nvec < 1 || nvec > 32 || dv % 4 || nsteps < 1 ||
       nsteps > LF_MAX_STEPS)
     return hipErrorInvalidValue;
   const int nsplit = mfma_nsplit(g, d), cps = mfma_cps(g, d);

@@ -348,7 +348,14 @@ int lf_prover_create(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, const
     P->S_live.resize(P->S_idx.size());
     for (size_t k = 0; k < P->S_idx.size(); k++) {
       const int p = P->S_idx[k];
-      if (p < 0 || (size_t)p >= P->lin_list.size()) {
+      if (p < 0 || (size_t)p > P->lin_list.size()) {
+        // past the eq(beta) slot or negative: malformed, the reference would panic on the index
+        delete P;
+        lf_ctx_set_error(ctx, "lf_prover_create: a multiset index is negative or past the Mz MLE list and its "
+                              "eq(beta) slot");
+        return LF_ERR_INVALID_ARG;
+      }
+      if ((size_t)p == P->lin_list.size()) {
         P->bad_S = true;
         P->S_live[k] = 0;
         continue;
@@ -370,8 +377,8 @@ int lf_prover_create(lf_ctx *ctx, const lf_ajtai *aj, const lf_params *pr, const
     // factor into its term, which the split-eq sumcheck (eq(beta) taken out of every
     // term) does not express. Rejected here, by name, rather than mid-fold.
     delete P;
-    lf_ctx_set_error(ctx, "lf_prover_create: a multiset index is past the Mz MLE list (the position of "
-                          "eq(beta) or beyond); multisets over eq(beta) are not supported");
+    lf_ctx_set_error(ctx, "lf_prover_create: a multiset index is the position of eq(beta) in the MLE list; "
+                          "multisets over eq(beta) are not supported");
     return LF_ERR_UNSUPPORTED_CCS;
   }
   if (!P->bad_S) {

@@ -85,7 +85,6 @@ struct lf_ctx {
   bool timing = false;
   hipEvent_t join = nullptr;    // lf_dev_fold_step_batch: this stream's point to wait for / be waited on
   hipStream_t contract = nullptr;  // lf_ctx_set_contract_stream: where batched contractions led by this context run
-  bool prepacked1 = false;      // step_commit wrote side 1's packed words (fold_commit's fused d = 1024 path)
   hipEvent_t cjoin = nullptr;   // the end of the last such contraction
   std::vector<TimedLaunch> pending;
   std::map<int, std::pair<double, long>> stats;  // nvec -> (ms, count)
@@ -341,6 +340,15 @@ int grow(lf_ctx *c, T *&buf, size_t &have, size_t need) {
   return LF_OK;
 }
 int reserve(lf_ctx *c, size_t elems) { return grow(c, c->scratch, c->scratch_elems, elems); }
+// the dead-unit flags: zeroed when (re)allocated, so a padding unit that no
+// decomposition writes (unit 2c + 1 when nblk L is odd) reads as live, never as
+// uninitialised memory
+int grow_dead(lf_ctx *c, size_t need) {
+  if (need <= c->dead_elems) return LF_OK;
+  LF_TRY(grow(c, c->dead, c->dead_elems, need));
+  LF_HIP(c, hipMemsetAsync(c->dead, 0, need, c->cur));
+  return LF_OK;
+}
 // a round message back through pinned memory (a pageable destination costs an extra
 // staging copy per round)
 int pinned(lf_ctx *c, size_t elems) {
@@ -545,7 +553,11 @@ struct Deferred {
 
 int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int lbs, size_t W,
                 const lf_fold_step_bufs *b, const uint64_t *wi_f_coeff, const uint64_t *commit_f,
-                const lfk::OutPtrs &dst, Deferred *defer = nullptr) {
+                const lfk::OutPtrs &dst, Deferred *defer = nullptr, const uint32_t *prepacked1 = nullptr) {
+  // prepacked1: the buffer into which step_commit's from_w_ccs has just written
+  // side 1's sign|magnitude words (fused d = 1024 path), or null. It is an
+  // argument, not context state, so a failed step cannot leave it set for a
+  // later call.
   const int d = pr->d, L = pr->L, K = pr->K;
   const size_t N = W * (size_t)L, kappa = aj->kappa;
   const int extra = commit_f ? 1 : 0, nvec = fold_nvec(pr, commit_f != nullptr);
@@ -615,7 +627,7 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       const int row0[2] = {extra, extra + K - 1};
       const int row_p0[2] = {no_fk ? extra + 2 * (K - 1) : -1, no_fk ? extra + 2 * (K - 1) + 1 : -1};
       // dead units (operand rows left unwritten where a unit's plane is zero), as at d = 1024
-      LF_TRY(grow(c, c->dead, c->dead_elems, (size_t)aj->geom.nch * 64));
+      LF_TRY(grow_dead(c, (size_t)aj->geom.nch * 64));
       uint32_t rows = 0;
       for (int s = 0; s < 2; s++) {
         for (int k = 1; k < K; k++) rows |= 1u << (row0[s] + k - 1);
@@ -633,7 +645,7 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       lfk::FusedSides sd{};
       sd.nside = 2;
       // dead units: the planes' rows are written only where a unit's plane is nonzero
-      LF_TRY(grow(c, c->dead, c->dead_elems, (size_t)aj->geom.nch * 64));
+      LF_TRY(grow_dead(c, (size_t)aj->geom.nch * 64));
       sd.dead = c->dead;
       uint32_t rows = 0;
       for (int s = 0; s < 2; s++) {
@@ -652,8 +664,7 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       c->dead_units.rows = rows;
       c->fold_rows.dead = c->dead_units;
       // side 1's words, when step_commit's from_w_ccs wrote them into this very buffer
-      sd.prepacked = c->prepacked1 && wi_f_coeff == b->f_coeff ? 2 : 0;
-      c->prepacked1 = false;
+      sd.prepacked = prepacked1 && prepacked1 == sd.smg[1] && wi_f_coeff == b->f_coeff ? 2 : 0;
       PhaseTimer pt(c, LF_PHASE_DECOMPOSE);  // both sides in one launch
       LF_HIP(c, lfk::decompose_fused(sd, N, lb, L, K, t->fwd, c->frag, aj->geom.nch, c->d_err,
                                      c->sink, c->ncu, c->cur));
@@ -667,7 +678,7 @@ int fold_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, int lb, int 
       if (want_masks && !b->planes[0]) LF_TRY(grow(c, c->fkeys, c->fkeys_elems, 2 * 2 * (size_t)K * N));
       LF_TRY(grow(c, c->smg, c->smg_elems, 2 * N * 12));  // the coefficients as 16-bit sign|magnitude
       // dead units (the wave-local b_small = 2 kernel flags the zero planes' rows)
-      LF_TRY(grow(c, c->dead, c->dead_elems, (size_t)aj->geom.nch * 64));
+      LF_TRY(grow_dead(c, (size_t)aj->geom.nch * 64));
       sd.dead = lbs == 1 ? c->dead : nullptr;
       uint32_t rows = 0;
       for (int s = 0; s < 2; s++) {
@@ -994,6 +1005,9 @@ void lf_ctx_destroy(lf_ctx *c) {
   if (!c) return;
   DevGuard g(c);
   (void)hipStreamSynchronize(c->cur);
+  // a batched contraction this context led on the caller's contract stream reads its buffers
+  if (c->contract) (void)hipStreamSynchronize(c->contract);
+  c->contract = nullptr;
   for (auto &t : c->pending) {
     (void)hipEventDestroy(t.a);
     (void)hipEventDestroy(t.b);
@@ -1052,6 +1066,12 @@ int lf_stream_create_cu_mask(int device, const uint32_t *mask, int nwords, void 
 }
 int lf_ctx_set_contract_stream(lf_ctx *c, void *s) {
   if (!c) return LF_ERR_INVALID_ARG;
+  if (s) {  // the caller keeps ownership; it must be a stream of this context's device
+    hipDevice_t dev = -1;
+    if (hipStreamGetDevice((hipStream_t)s, &dev) != hipSuccess)
+      return fail(c, LF_ERR_INVALID_ARG, "contract stream: not a valid stream");
+    if (dev != c->device) return fail(c, LF_ERR_INVALID_ARG, "contract stream is on another device");
+  }
   c->contract = (hipStream_t)s;
   return LF_OK;
 }
@@ -1510,7 +1530,7 @@ static int step_check(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t
 }
 static int step_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_t W, const lf_fold_step_bufs *b,
                        int lb, int lbs, const lfk::OutPtrs &dst, Deferred *defer = nullptr) {
-  c->prepacked1 = false;
+  uint32_t *smg1 = nullptr;
   {
     PhaseTimer pt(c, LF_PHASE_FROM_W_CCS);
     // the fused X^1024 + 1 decomposition that fold_commit runs next packs both
@@ -1522,16 +1542,14 @@ static int step_commit(lf_ctx *c, const lf_ajtai *aj, const lf_params *pr, size_
     const size_t N = W * (size_t)L;
     const bool fused = aj->Af && aj->geom.Lp == L && d == 1024 && lbs == 1 && K <= 15 && t->fwd.mid &&
                        t->inv.mid && lb <= K && aj->ncols == N && (!b->planes[0]) == (!b->planes[1]);
-    uint32_t *smg1 = nullptr;
     if (fused) {
       if (!b->planes[0]) LF_TRY(grow(c, c->smg, c->smg_elems, 2 * N * 512));
       smg1 = b->planes[1] ? reinterpret_cast<uint32_t *>(b->planes[1]) : c->smg + N * 512;
     }
     if (!b->w_ccs || !b->f_coeff || !b->f) return fail(c, LF_ERR_INVALID_ARG, "null step buffer");
     LF_HIP(c, lfk::from_w_ccs(b->w_ccs, W, d, lb, L, b->f_coeff, b->f, t->fwd, t->inv, c->d_err, c->cur, smg1));
-    c->prepacked1 = smg1 != nullptr;
   }
-  return fold_commit(c, aj, pr, lb, lbs, W, b, b->f_coeff, b->f, dst, defer);
+  return fold_commit(c, aj, pr, lb, lbs, W, b, b->f_coeff, b->f, dst, defer, smg1);
 }
 
 int lf_dev_fold_lcccs(lf_ctx *c, int d, int nwit, const uint64_t *rho, const uint64_t *rho_coeff, const uint64_t *eta,

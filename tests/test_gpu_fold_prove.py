@@ -10,6 +10,8 @@ import latticeum_amd as LA
 import nifs as N
 import oracle as O
 
+LF_ERR_INVALID_ARG = 1  # lf.h
+
 pytestmark = pytest.mark.gpu
 
 
@@ -239,6 +241,14 @@ def test_prover_rejects_multiset_over_eq_beta():
         with pytest.raises(LA.LfError) as e:
             LA.Prover(ctx, sch, LA.goldilocks_dp(d), M, l, deg, c, [[0, 3], [1]])
         assert e.value.code == 13 and "eq(beta)" in str(e.value)
+        # position 5 is past the eq(beta) slot: malformed (the reference panics on the index), not unsupported
+        for bad in ([[0, 5], [1]], [[0, 4], [1]]):
+            with pytest.raises(LA.LfError) as e:
+                LA.Prover(ctx, sch, LA.goldilocks_dp(d), M, l, deg, c, bad)
+            assert e.value.code == LF_ERR_INVALID_ARG and "negative or past" in str(e.value)
+        with pytest.raises(LA.LfError) as e:  # negative: refused with the CCS structure already
+            LA.Prover(ctx, sch, LA.goldilocks_dp(d), M, l, deg, c, [[0, -1], [1]])
+        assert e.value.code == LF_ERR_INVALID_ARG
         LA.Prover(ctx, sch, LA.goldilocks_dp(d), M, l, deg, c, [[0, 2], [1]])  # every position a Mz MLE
     finally:
         ctx.close()

@@ -412,6 +412,57 @@ def test_dev_fold_step_packed_planes_repeated(ctx):
     check_dev_fold_step(ctx, 1024, 37, 2, steps=3, packed=True)
 
 
+def test_failed_packed_step_then_decompose_commit(ctx):
+    """A d = 1024 packed step whose commit(z) half has run (from_w_ccs wrote the
+    new witness's sign|magnitude words into planes[1]) but whose fold_commit then
+    fails on a buffer argument must leave nothing behind: a following
+    lf_dev_decompose_commit on the same context decomposes the f_coeff it is
+    given, not the failed step's packed words (the pre-packed flag is
+    an argument, not context state)."""
+    import torch
+    d, W, kappa = 1024, 17, 2
+    pr = params(d)
+    K, L = pr.K, pr.L
+    N = W * L
+    A = rand(kappa * N * d, 4100)
+    sch = LA.AjtaiCommitmentScheme(ctx, device_tensor=torch.from_numpy(A.view(np.int64)).cuda(), kappa=kappa,
+                                   ncols=N, d=d)
+    acc_fc, acc_f = valid_f_coeff(d, W, 4101)
+    acc_cm = O.ajtai_commit(A, kappa, N, d, acc_f)
+    dev = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.int64)).cuda()
+    z = lambda n: torch.zeros(n, dtype=torch.int64, device="cuda")
+    keep = {"w_ccs": dev(rand(W * d, 4102)), "acc_cm": dev(acc_cm), "acc_f_coeff": dev(acc_fc),
+            "rho": dev(make_rho(d, K, 4103)), "f_coeff": z(N * d), "f": z(N * d), "cm": z(kappa * d),
+            "wk": [z(K * W * d) for _ in range(2)], "y": [z(K * kappa * d) for _ in range(2)],
+            "f0": z(N * d), "f0_coeff": z(N * d), "w_ccs0": z(W * d), "cm0": z(kappa * d),
+            "planes": [z(N * 256) for _ in range(2)], "bad": z(K * N * d)}
+    b = LA.LfFoldStepBufs()
+    for k in ("w_ccs", "acc_cm", "acc_f_coeff", "rho", "f_coeff", "f", "cm", "f0", "f0_coeff", "w_ccs0", "cm0"):
+        setattr(b, k, keep[k].data_ptr())
+    for s in range(2):
+        b.wk[s], b.y[s], b.planes[s] = keep["wk"][s].data_ptr(), keep["y"][s].data_ptr(), keep["planes"][s].data_ptr()
+    b.fk_coeff[0] = keep["bad"].data_ptr()  # one side only: fold_commit refuses it after from_w_ccs ran
+    torch.cuda.synchronize()
+    with pytest.raises(LA.LfError):
+        ctx.dev_fold_step(sch, pr, W, b)
+    ctx.sync()
+    b.fk_coeff[0] = None
+    # a different linearized instance in the same f_coeff buffer
+    wi_fc, wi_f = valid_f_coeff(d, W, 4104)
+    keep["f_coeff"].copy_(dev(wi_fc))
+    keep["cm"].copy_(dev(O.ajtai_commit(A, kappa, N, d, wi_f)))
+    torch.cuda.synchronize()
+    ctx.check(ctx.lib.lf_dev_decompose_commit(ctx.h, sch.h, LA._lib.C.byref(pr), W, LA._lib.C.byref(b)))
+    ctx.sync()
+    h = lambda t: t.cpu().numpy().view(np.uint64)
+    for s, fc in ((0, acc_fc), (1, wi_fc)):
+        _, ofk, owk = O.decompose_witness(fc, d, pr.B, L, pr.b_small, K)
+        assert np.array_equal(h(keep["wk"][s]), owk), f"w_ccs_k side {s}"
+        y = h(keep["y"][s]).reshape(K, kappa * d)
+        oy = O.ajtai_commit(A, kappa, N, d, ofk.reshape(K, N * d)[1:].ravel(), K - 1).reshape(K - 1, kappa * d)
+        assert np.array_equal(y[1:], oy), f"y side {s}"
+
+
 def check_dev_fold_step(ctx, d, W, kappa, steps=1, keep_fk=True, rho=None, packed=False):
     import torch
     pr = params(d)

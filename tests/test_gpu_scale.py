@@ -43,9 +43,56 @@ def blocks_to_groups(W, nblk_pick):
     return np.array(groups)
 
 
-def check_workload(wl, seed_w, picks, cm_rows, y_rows, stream=0):
-    """bench.Workload `wl` has run one step on step stream `stream`; compare it
-    against the oracle."""
+class _LeanPlanes:
+    """The packed digit planes (d = 1024 / 4096: column-major, one fixed-size
+    record per element) expanded a column block at a time, so a check never holds
+    a side's K x N u64 rows (20 GB per step at W = 2^14) beside bench.py's
+    8-stream workload (about 240 of the 288 GB)."""
+
+    def __init__(self, wl, planes, block=8192):
+        self.wl, self.planes, self.block = wl, planes, block
+        K, d = wl.pr.K, wl.d
+        self.per_col = 256 if d == 1024 else K * 128  # int64 words per element (lf.h planes layout)
+
+    def _expand(self, s, c0, n):
+        import torch
+        wl = self.wl
+        K, d = wl.pr.K, wl.d
+        p = self.planes[s]
+        fck, fk = (torch.empty(K * n * d, dtype=torch.int64, device=p.device) for _ in range(2))
+        wl.ctxs[0].dev_expand_planes(wl.pr, p.data_ptr() + 8 * c0 * self.per_col, n, fck, fk)
+        wl.ctxs[0].sync()
+        return fck.view(K, n, d), fk.view(K, n, d)
+
+    def full_planes(self, s, ks):
+        """host f_k rows of planes `ks` over all N columns: {k: [N d] u64}"""
+        N, d = self.wl.N, self.wl.d
+        out = {k: np.empty(N * d, np.uint64) for k in ks}
+        for c0 in range(0, N, self.block):
+            n = min(self.block, N - c0)
+            _, fk = self._expand(s, c0, n)
+            for k in ks:
+                out[k][c0 * d:(c0 + n) * d] = host(fk[k].contiguous())
+            del fk
+        return out
+
+    def cols(self, s, groups):
+        """host (f_coeff_k, f_k) [K][len(cols)][d] of the columns of `groups` (whole 16-group blocks)"""
+        L = self.wl.pr.L
+        fcs, fks = [], []
+        blocks = sorted(set(int(g) // 16 for g in groups))
+        for B in blocks:
+            g0, g1 = 16 * B, min(self.wl.W, 16 * B + 16)
+            fck, fk = self._expand(s, g0 * L, (g1 - g0) * L)
+            fcs.append(host(fck.contiguous()).reshape(fck.shape))
+            fks.append(host(fk.contiguous()).reshape(fk.shape))
+        return np.concatenate(fcs, axis=1), np.concatenate(fks, axis=1)
+
+
+def check_workload(wl, seed_w, picks, cm_rows, y_rows, stream=0, lean_expand=False):
+    """bench.Workload `wl` has run its steps on step stream `stream`; compare the
+    outputs against the oracle. lean_expand: expand packed planes column block
+    by column block (HBM-tight workloads)."""
     import torch
     d, W, kappa, pr = wl.d, wl.W, wl.kappa, wl.pr
     K, L, N = pr.K, pr.L, wl.N
@@ -78,15 +125,19 @@ def check_workload(wl, seed_w, picks, cm_rows, y_rows, stream=0):
     # y rows of both sides: the decomposition's own operand rows through the contraction
     y = [host(t).reshape(K, kappa, d) for t in keep["y"]]
     fk_dev, fck_dev = keep["fk"], keep["fk_coeff"]
+    lean = None  # packed planes expanded column block by column block (bench.py's 8-stream HBM footprint)
     if keep.get("planes", [None])[0] is not None and fk_dev[0] is None:
-        # the step kept its planes packed: the u64 rows as lf_dev_expand_planes makes them
-        fk_dev, fck_dev = [], []
-        for s in range(2):
-            fck, fk = (torch.empty(K * N * d, dtype=torch.int64, device=keep["f"].device) for _ in range(2))
-            wl.ctxs[0].dev_expand_planes(pr, keep["planes"][s], N, fck, fk)
-            fk_dev.append(fk)
-            fck_dev.append(fck)
-        wl.ctxs[0].sync()
+        if lean_expand and d in (1024, 4096):
+            lean = _LeanPlanes(wl, keep["planes"])
+        else:
+            # the step kept its planes packed: the u64 rows as lf_dev_expand_planes makes them
+            fk_dev, fck_dev = [], []
+            for s in range(2):
+                fck, fk = (torch.empty(K * N * d, dtype=torch.int64, device=keep["f"].device) for _ in range(2))
+                wl.ctxs[0].dev_expand_planes(pr, keep["planes"][s], N, fck, fk)
+                fk_dev.append(fk)
+                fck_dev.append(fck)
+            wl.ctxs[0].sync()
     elif fk_dev[0] is None:
         # the step kept its planes only as operand rows: decompose both sides
         # again through the standalone entry (parity-tested on its own)
@@ -99,8 +150,11 @@ def check_workload(wl, seed_w, picks, cm_rows, y_rows, stream=0):
             assert torch.equal(fck, keep["fk_coeff"][s]) and torch.equal(wk, keep["wk"][s]), f"side {s}"
             del fck, wk
             fk_dev.append(fk)
+    if lean is not None:
+        want_k = {s: sorted({k for s2, k, _ in y_rows if s2 == s}) for s in range(2)}
+        planes_k = {s: lean.full_planes(s, want_k[s]) for s in range(2) if want_k[s]}
     for s, k, row in y_rows:
-        fk = host(fk_dev[s][k * N * d:(k + 1) * N * d])
+        fk = planes_k[s][k] if lean is not None else host(fk_dev[s][k * N * d:(k + 1) * N * d])
         got = O.ajtai_rows_seeded(bench.SEED_A, N, d, fk, [row])
         assert np.array_equal(y[s][k, row], got), f"y side {s} k {k} row {row}"
     # y_0 = cm - sum 2^k y_k and cm_0 = sum rho_i y_i, recomputed from the device's y
@@ -120,8 +174,13 @@ def check_workload(wl, seed_w, picks, cm_rows, y_rows, stream=0):
         sub = fc.reshape(N, d)[cols].ravel()
         ofck, ofk, owk = O.decompose_witness(sub, d, pr.B, L, pr.b_small, K)
         ofck, ofk, owk = ofck.reshape(K, -1, d), ofk.reshape(K, -1, d), owk.reshape(K, ng, d)
-        for name, got_t, want, idx in (("f_coeff_k", fck_dev[s], ofck, cols), ("f_k", fk_dev[s], ofk, cols),
-                                       ("w_ccs_k", keep["wk"][s], owk, groups)):
+        if lean is not None:
+            lfck, lfk = lean.cols(s, groups)
+            assert np.array_equal(lfck, ofck), f"f_coeff_k side {s}"
+            assert np.array_equal(lfk, ofk), f"f_k side {s}"
+        rows = (("w_ccs_k", keep["wk"][s], owk, groups),) if lean is not None else \
+            (("f_coeff_k", fck_dev[s], ofck, cols), ("f_k", fk_dev[s], ofk, cols), ("w_ccs_k", keep["wk"][s], owk, groups))
+        for name, got_t, want, idx in rows:
             n_per = N if name != "w_ccs_k" else W
             g = got_t.view(K, n_per, d)[:, torch.from_numpy(idx).to(got_t.device)]
             assert np.array_equal(host(g.contiguous()).reshape(K, len(idx), d), want), f"{name} side {s}"
@@ -137,11 +196,14 @@ def check_workload(wl, seed_w, picks, cm_rows, y_rows, stream=0):
     assert np.array_equal(host(keep["w_ccs0"].view(W, d)[gidx].contiguous()).ravel(), ow), "w_ccs_0"
 
 
-def run_workload(d, W, kappa, streams=1, batch=0, packed=None):
+def run_workload(d, W, kappa, streams=1, batch=0, packed=None, steps=None):
+    """bench.Workload after `steps` steps (default: one per stream), run the way
+    bench.py runs its timed steps (Workload.run: whole groups, a partial last group
+    as one smaller batch)"""
     import torch
     wl = bench.Workload(LA, torch, 0, 0, d, W, kappa, streams, batch=batch, packed=packed)
     try:
-        wl.run(streams)
+        wl.run(streams if steps is None else steps)
         wl.sync()
         return wl
     except Exception:
@@ -150,7 +212,7 @@ def run_workload(d, W, kappa, streams=1, batch=0, packed=None):
 
 
 def test_fold_step_bench_shape_d1024():
-    """bench.py's default workload: d=1024, W=2^14, kappa=32 (streaming-store
+    """bench.py's default workload shape: d=1024, W=2^14, kappa=32 (streaming-store
     decomposition, nt-copy contraction over the 21.5 GB fragment matrix)"""
     import torch
     wl = run_workload(1024, 1 << 14, 32)
@@ -167,10 +229,10 @@ def test_fold_step_bench_shape_d1024():
 
 @pytest.mark.parametrize("streams", [2, 4])
 def test_fold_step_bench_shape_d1024_batched(streams):
-    """bench.py's default (4 step streams, one batch) and the pairs form: the
-    steps' contractions are one launch over the 21.5 GB fragment matrix (A with
-    the default cache policy, the operand rows streamed: the instance only this
-    size runs); every step against the oracle"""
+    """smaller groups than bench.py's default (8 streams, test below): 2 and 4
+    step streams in one batch, the steps' contractions one launch over the
+    21.5 GB fragment matrix (A with the default cache policy, the operand rows
+    streamed); every step against the oracle"""
     import torch
     wl = run_workload(1024, 1 << 14, 32, streams=streams, batch=streams)
     try:
@@ -179,6 +241,64 @@ def test_fold_step_bench_shape_d1024_batched(streams):
         for st in range(streams):
             check_workload(wl, bench.SEED_W, [st, nblk // 3, nblk - 1 - st], [0, 17, 31],
                            [(0, 1, 3), (1, 14, 30), (st % 2, 9 + st, 16)], stream=st)
+    finally:
+        wl.close()
+        del wl
+        torch.cuda.empty_cache()
+
+
+def test_fold_step_bench_headline_schedule():
+    """the headline's exact timed instance: bench.py's defaults (8 step streams,
+    --batch 8) at d=1024, W=2^14, kappa=32, run through bench.py's 20-step
+    schedule -- two 8-step contraction launches (k_ajtai_mfma_ra<0, 2, 4> with
+    nsteps = 8 over the 21.5 GB fragment matrix) and a trailing 4-step batch.
+    Every one of the 8 streams against the oracle (streams 0-3 last ran in the
+    4-step batch, 4-7 in the second 8-step launch). The packed planes are expanded
+    a column block at a time: the workload holds about 240 of the 288 GB."""
+    import torch
+    wl = run_workload(1024, 1 << 14, 32, streams=8, batch=8, steps=20)
+    try:
+        assert wl.batch and wl.group == 8 and wl.packed
+        nblk = (wl.W + 15) // 16
+        for st in range(8):
+            check_workload(wl, bench.SEED_W, [st, nblk // 2 + st, nblk - 1 - st], [0, 31],
+                           [(st % 2, 1 + st, 7), (1 - st % 2, 14 - st, 24)], stream=st, lean_expand=True)
+    finally:
+        wl.close()
+        del wl
+        torch.cuda.empty_cache()
+
+
+def test_fold_step_w464_bench_pairs():
+    """the W=464 line (SURVEY 8(d)'s byte-equivalent shape) as bench.py times it:
+    4 step streams in groups of 2 (each pair one contraction launch, the pairs
+    taking turns), 8 steps; every stream against the oracle"""
+    import torch
+    wl = run_workload(1024, 464, 32, streams=4, batch=2, steps=8)
+    try:
+        assert wl.batch and wl.group == 2
+        nblk = (wl.W + 15) // 16
+        for st in range(4):
+            check_workload(wl, bench.SEED_W, [0, st + 5, nblk - 1], [0, 1, 16, 31],
+                           [(0, 1, st), (1, 14, 31 - st), (st % 2, 3 + st, 16)], stream=st)
+    finally:
+        wl.close()
+        del wl
+        torch.cuda.empty_cache()
+
+
+def test_fold_step_configs4_bench_pair():
+    """configs[4]'s line as bench.py times it: d=4096, W=1024, kappa=64, 2 step
+    streams whose contractions are one launch (batch 2), 20 steps; both streams
+    against the oracle"""
+    import torch
+    wl = run_workload(4096, 1024, 64, streams=2, batch=2, steps=20)
+    try:
+        assert wl.batch and wl.group == 2 and wl.packed
+        nblk = (wl.W + 15) // 16
+        for st in range(2):
+            check_workload(wl, bench.SEED_W, [st, nblk // 2, nblk - 1], [0, 31, 32, 63],
+                           [(0, 1, 5 + st), (1, 14, 63 - st), (st, 3, 33)], stream=st)
     finally:
         wl.close()
         del wl

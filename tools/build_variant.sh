@@ -6,7 +6,7 @@ NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 SRC=$ROOT/latticeum_amd/csrc
 OUT=/tmp/lf_variant_$NAME
-mkdir -p "$OUT" "$ROOT/abl"
+mkdir -p "$OUT" "$ROOT/abv"
 SRCS="kernels.hip kernels_n32.hip kernels_n4k.hip ajtai_mfma.hip fold_coeff.hip sumcheck.hip mz.hip merkle.hip fold_prove.hip lf_api.hip transcript.cpp serialize.cpp replay.cpp"
 pids=()
 for f in $SRCS; do
@@ -15,5 +15,5 @@ for f in $SRCS; do
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait "$p"; done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/abl/lib$NAME.so" "$OUT"/*.o
-echo "abl/lib$NAME.so"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/abv/lib$NAME.so" "$OUT"/*.o
+echo "abv/lib$NAME.so"
