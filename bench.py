@@ -209,16 +209,17 @@ def kernel_source_hash():
 _PMC_STALE = set()
 
 
-def _pmc_doc(kind, d, W, kappa):
-    """profiles/pmc_<kind>_d<d>_W<W>_k<kappa>.json when it is this configuration's
-    and was collected on the current kernel sources; None otherwise (a stale file
-    is recorded in _PMC_STALE and reported as such, never paired with new timings)"""
-    name = f"pmc_{kind}_d{d}_W{W}_k{kappa}.json"
+def _pmc_doc(kind, d, W, kappa, name=None, config=None):
+    """profiles/pmc_<kind>_d<d>_W<W>_k<kappa>.json (or `name` with `config`) when it
+    is this configuration's and was collected on the current kernel sources; None
+    otherwise (a stale file is recorded in _PMC_STALE and reported as such, never
+    paired with new timings)"""
+    name = name or f"pmc_{kind}_d{d}_W{W}_k{kappa}.json"
     try:
         doc = json.loads((ROOT / "profiles" / name).read_text())
     except (OSError, ValueError):
         return None
-    if doc.get("config") != {"d": d, "W": W, "kappa": kappa}:
+    if doc.get("config") != (config or {"d": d, "W": W, "kappa": kappa}):
         return None
     if doc.get("src_hash") != kernel_source_hash():
         _PMC_STALE.add(name)
@@ -793,8 +794,22 @@ def side_ops(LA, torch, local):
     st = torch.empty(16 * m, dtype=torch.int64, device=f"cuda:{local}")
     ctx.dev_fill_uniform(st, 0x4C460007)
     ms = ev_ms(lambda: ctx.dev_poseidon2_permute(st))
-    out["poseidon2_w16"] = {"states": m, "ms": ms, "perms_per_s": m / ms * 1e3}
+    out["poseidon2_w16"] = {"states": m, "ms": ms, "perms_per_s": m / ms * 1e3,
+                            "achieved_gbs": 2 * 16 * 8 * m / ms / 1e6}
     del st
+    # the side ops' own PMC passes (tools/gpu_pmc_side.sh: these launches at these sizes)
+    cfg = {"side_ops": True}
+    tr = _pmc_doc("traffic", 0, 0, 0, "pmc_traffic_side_ops.json", cfg) or {}
+    sq = _pmc_doc("sq", 0, 0, 0, "pmc_sq_side_ops.json", cfg) or {}
+    for key, kern in (("ntt_fwd", "k_xform_n32<true>"), ("ntt_inv", "k_xform_n32<false>"),
+                      ("poseidon2_w16", "k_p2_permute")):
+        t = (tr.get("kernels") or {}).get(kern) or {}
+        q = (sq.get("kernels") or {}).get(kern) or {}
+        b = t.get("hbm_bytes_per_launch")
+        out[key]["pmc"] = {"kernel": kern, "traffic_bytes_per_launch": b,
+                           "frac_hbm_pmc": b / (out[key]["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS if b else None,
+                           "valu_busy": q.get("valu_busy"), "wait_cnt_frac": q.get("wait_cnt_frac"),
+                           "wait_issue_frac": q.get("wait_issue_frac")}
     ctx.sync()
     ctx.close()
     torch.cuda.empty_cache()
@@ -1236,6 +1251,10 @@ def compact_line(out, detail):
     if ops:
         side["ntt_ms"] = [ops.get("ntt_fwd", {}).get("ms"), ops.get("ntt_inv", {}).get("ms")]
         side["poseidon2_perms_per_s"] = ops.get("poseidon2_w16", {}).get("perms_per_s")
+        # [valu_busy, PMC fraction of HBM] per side op (null when no PMC file matches these sources)
+        side["side_ops_pmc"] = {k: [(ops.get(k, {}).get("pmc") or {}).get("valu_busy"),
+                                    (ops.get(k, {}).get("pmc") or {}).get("frac_hbm_pmc")]
+                                for k in ("ntt_fwd", "ntt_inv", "poseidon2_w16")}
     nx = out.get("next_rows") or {}
     if nx:
         side["fold_prove_ms"] = [nx.get(k, {}).get("ms_per_fold_prove") for k in ("fold_prove", "fold_prove_scalar")]

@@ -571,9 +571,10 @@ class Prover:
         idx = np.array([j for x in S for j in x] or [0], np.int32)
         ctx.check(self.lib.lf_ccs_set_structure(ctx.h, ccs.h, l, degree, len(S), _ptr(c), _ptr(off), _ptr(idx), repr))
         h = C.c_void_p()
+        self.lib.lf_ctx_set_error(ctx.h, b"")  # so a message read below is this call's
         rc = self.lib.lf_prover_create(ctx.h, scheme.h, C.byref(params), ccs.h, C.byref(h))
         if rc:
-            msg = self.lib.lf_ctx_last_error(ctx.h).decode() if rc == 13 else ""
+            msg = self.lib.lf_ctx_last_error(ctx.h).decode()
             raise LfError(rc, msg or "lf_prover_create: " + self.lib.lf_status_string(rc).decode())
         self.h = h
         self.d, self.l, self.t, self.degree = params.d, l, ccs.t, degree

@@ -345,15 +345,6 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const
   // reads before its first product.
   auto dead_mask = [&](int c) -> uint32_t {
     if (!has_dead) return 0u;
-#ifdef LF_AB_OLD_DM
-    {
-      const int ci = c - c0;
-      uint32_t sel = dm[0];
-#pragma unroll
-      for (int m = 1; m < NDM; m++) sel = (ci >> 6) == m ? dm[m] : sel;
-      return __builtin_amdgcn_readlane(sel, ci & 63);
-    }
-#endif
     const int ci = c - c0, m = ci >> 6, l = ci & 63;
     uint32_t r = __builtin_amdgcn_readlane(dm[0], l);
 #pragma unroll
@@ -408,13 +399,7 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const
       // A(c + DP)'s loads follow the last product reading that register
       // (the issue order F then A is unchanged, so vm_wait_chunk still holds)
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-#ifdef LF_T_NODS  // timing-only probe: no operand reads (wrong results)
-        b[k] = (v4i){(int)fbase, k, 0, 0};
-#else
-        asm volatile("ds_read_b128 %0, %1" : "=v"(b[k]) : "v"(fbase + 16u * fpos[k]));
-#endif
-      }
+      for (int k = 0; k < 8; k++) asm volatile("ds_read_b128 %0, %1" : "=v"(b[k]) : "v"(fbase + 16u * fpos[k]));
       const bool more_f = c + DP - 1 < c1, more_a = c + DP < c1;
       const int fb = (j + DP - 1) % DP;
       const uint32_t dmn = more_f ? dead_mask(c + DP - 1) : 0u;
@@ -431,22 +416,16 @@ __global__ void __launch_bounds__(256, 1) k_ajtai_mfma_ra(const uint4 *Af, const
           for (int ka = 0; ka < 8; ka++)
             acc[ka + kb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ra[j][ka], b[kb], acc[ka + kb], 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
-#ifndef LF_T_NOF  // timing-only probe: no F copies in the loop (wrong results)
           if (more_f && kb < nf) stage_f_piece(c + DP - 1, fb, kb, dmn);
-#endif
           __builtin_amdgcn_sched_barrier(0);
         } else {
-#ifndef LF_T_NOF
           if (more_f && nf == 8) stage_f_piece(c + DP - 1, fb, 7, dmn);
-#endif
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int ka = 0; ka < 8; ka++) {
             acc[ka + 7] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ra[j][ka], b[7], acc[ka + 7], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
-#ifndef LF_T_NOA  // timing-only probe: no A loads in the loop (wrong results)
             if (more_a) ra[j][ka] = gload16<CPA>(pa + ((size_t)(c + DP) * 8 + ka) * 64);
-#endif
             __builtin_amdgcn_sched_barrier(0);
           }
         }

@@ -72,7 +72,7 @@ class _LeanPlanes:
             n = min(self.block, N - c0)
             _, fk = self._expand(s, c0, n)
             for k in ks:
-                out[k][c0 * d:(c0 + n) * d] = host(fk[k].contiguous())
+                out[k][c0 * d:(c0 + n) * d] = host(fk[k].contiguous()).ravel()
             del fk
         return out
 

@@ -37,13 +37,15 @@ while IFS= read -r cfg; do
   python tools/prof_summary.py traffic gpurun_out/pmcf_${TAG}_$n gpurun_out/pmcw_${TAG}_$n \
     gpurun_out/pmc_traffic_$n.json $d $W $k > /dev/null || exit 1
   timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
-    SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_WAVES GRBM_GUI_ACTIVE -d gpurun_out/pmcs_${TAG}_$n -o run --output-format csv -- \
+    SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE -d gpurun_out/pmcs_${TAG}_$n -o run --output-format csv -- \
     python bench.py $Q $args > gpurun_out/pmcs_${TAG}_$n.log 2>&1
   rc=$?; echo "sq $n rc=$rc"; [ $rc -eq 0 ] || exit $rc
   python tools/prof_summary.py sq gpurun_out/pmcs_${TAG}_$n gpurun_out/pmc_sq_$n.json $d $W $k > /dev/null || exit 1
   cp gpurun_out/pmc_traffic_$n.json gpurun_out/pmc_sq_$n.json profiles/
   rm -rf gpurun_out/pmcf_${TAG}_$n gpurun_out/pmcw_${TAG}_$n gpurun_out/pmcs_${TAG}_$n
 done <<< "$CFGS"
+# the side ops (configs[1]'s 2^16 NTT / INTT, the 2^20-state Poseidon2 batch) at their own sizes
+tools/gpu_pmc_side.sh || exit 1
 fi
 if [ -z "$SKIP_BENCH" ]; then
 timeout -k 10 600 python bench.py --detail gpurun_out/bench_detail_$TAG.json > gpurun_out/bench_$TAG.log 2>&1

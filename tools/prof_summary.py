@@ -154,11 +154,16 @@ def traffic(fetch_dir, write_dir, out_json, config):
 def sq(sq_dir, out_json, config, simds=1024, xcds=8):
     """Per kernel: the VALU pipes' busy fraction from one SQ pass,
     SQ_ACTIVE_INST_VALU (quad-cycles) x 4 / (SIMDs x GRBM_GUI_ACTIVE / XCDs)
-    (GRBM_GUI_ACTIVE is summed over the XCDs), averaged over launches."""
+    (GRBM_GUI_ACTIVE is summed over the XCDs), averaged over launches; with
+    SQ_VALU_MFMA_BUSY_CYCLES in the pass also the matrix pipes' busy fraction
+    (that counter counts cycles, summed over the SIMDs) and the clock."""
     per = {}
     for c in ("SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
-              "SQ_WAIT_INST_ANY"):
-        vals, meta = counter_per_dispatch(sq_dir, c)
+              "SQ_WAIT_INST_ANY", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAIT_INST_LDS"):
+        try:
+            vals, meta = counter_per_dispatch(sq_dir, c)
+        except SystemExit:
+            continue
         for did, v in vals.items():
             per.setdefault(did, {"name": meta[did][0]})[c] = v
     acc = defaultdict(list)
@@ -169,22 +174,33 @@ def sq(sq_dir, out_json, config, simds=1024, xcds=8):
                                    "valu_insts_per_cu_cycle": r["SQ_INSTS_VALU"] / (simds / 4 * cyc),
                                    "cycles": cyc,
                                    "wait_issue_frac": r["SQ_WAIT_INST_ANY"] / max(r["SQ_WAVE_CYCLES"], 1),
-                                   "wait_cnt_frac": r["SQ_WAIT_ANY"] / max(r["SQ_WAVE_CYCLES"], 1)})
+                                   "wait_cnt_frac": r["SQ_WAIT_ANY"] / max(r["SQ_WAVE_CYCLES"], 1),
+                                   **({"mfma_busy": r["SQ_VALU_MFMA_BUSY_CYCLES"] / (simds * cyc)}
+                                      if "SQ_VALU_MFMA_BUSY_CYCLES" in r else {}),
+                                   **({"wait_lds_frac": r["SQ_WAIT_INST_LDS"] / max(r["SQ_WAVE_CYCLES"], 1)}
+                                      if "SQ_WAIT_INST_LDS" in r else {})})
     kernels = {k: {f: sum(x[f] for x in v) / len(v) for f in v[0]} | {"launches": len(v)} for k, v in acc.items()}
+    counters = sorted({c for r in per.values() for c in r if c != "name"})
     doc = {"config": config, "kernels": kernels, "src_hash": kernel_source_hash(),
-           "method": "one rocprofv3 --pmc pass (SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY "
-                     "SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_WAVES GRBM_GUI_ACTIVE) of bench.py; "
-                     "valu_busy = 4 SQ_ACTIVE_INST_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)"}
+           "method": f"one rocprofv3 --pmc pass ({' '.join(counters)}); "
+                     "valu_busy = 4 SQ_ACTIVE_INST_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8); "
+                     "mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)"}
     json.dump(doc, open(out_json, "w"), indent=1)
     print(json.dumps(doc, indent=1))
+
+
+def _config(argv, pos):
+    """--config '<json>' anywhere in argv, else d W kappa at argv[pos:pos + 3]"""
+    if "--config" in argv:
+        return json.loads(argv[argv.index("--config") + 1])
+    d, W, kappa = (int(x) for x in argv[pos:pos + 3]) if len(argv) >= pos + 3 else (1024, 16384, 32)
+    return {"d": d, "W": W, "kappa": kappa}
 
 
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], sys.argv[3])
     elif sys.argv[1] == "traffic":
-        d, W, kappa = (int(x) for x in sys.argv[5:8]) if len(sys.argv) >= 8 else (1024, 16384, 32)
-        traffic(sys.argv[2], sys.argv[3], sys.argv[4], {"d": d, "W": W, "kappa": kappa})
+        traffic(sys.argv[2], sys.argv[3], sys.argv[4], _config(sys.argv, 5))
     elif sys.argv[1] == "sq":
-        d, W, kappa = (int(x) for x in sys.argv[4:7]) if len(sys.argv) >= 7 else (1024, 16384, 32)
-        sq(sys.argv[2], sys.argv[3], {"d": d, "W": W, "kappa": kappa})
+        sq(sys.argv[2], sys.argv[3], _config(sys.argv, 4))
