@@ -244,14 +244,15 @@ def load_traffic(d, W, kappa):
     return t
 
 
-def load_sq(d, W, kappa):
-    """PMC-measured VALU busy fraction per kernel (profiles/pmc_sq_d<d>_W<W>_k<kappa>.json, written by
-    tools/prof_summary.py sq from one SQ pass of this configuration on the same kernel sources); {} otherwise."""
+def load_sq(d, W, kappa, field="valu_busy"):
+    """PMC-measured VALU (or, field="mfma_busy", matrix-pipe) busy fraction per kernel
+    (profiles/pmc_sq_d<d>_W<W>_k<kappa>.json, written by tools/prof_summary.py sq from one
+    SQ pass of this configuration on the same kernel sources); {} otherwise."""
     doc = _pmc_doc("sq", d, W, kappa)
     if doc is None:
         return {}
     kern = doc.get("kernels", {})
-    t = {k: v.get("valu_busy") for k, v in kern.items()}
+    t = {k: v.get(field) for k, v in kern.items()}
     by_base(t, kern)
     return t
 
@@ -622,6 +623,7 @@ def phase_report(LA, wl, tot, steps):
     kernel_of = kernel_names(LA, d, W, wl.sch.layout, wl.keep_fk or wl.packed, wl.packed)
     traffic = load_traffic(d, W, kappa)
     valu = load_sq(d, W, kappa)
+    mfma = load_sq(d, W, kappa, "mfma_busy")
     phases = {}
     for ph, (ms, cnt) in tot.items():
         if not cnt:
@@ -644,6 +646,15 @@ def phase_report(LA, wl, tot, steps):
                            + operand.get(ph, 0) * sides}
         else:
             phases_note = {}
+        if ph == "ajtai" and wl.sch.layout == 1:
+            # the matrix-core work one step's contraction issues: per (virtual) slot, 32-row
+            # tile and 32-column chunk, 64 v_mfma_i32_32x32x32_i8 (8 x 8 byte planes)
+            dv = 40 if d == 24 else d
+            nch = ((wl.W + 15) // 16 * wl.pr.L + 1) // 2
+            macs = dv * ((kappa + 31) // 32) * nch * 64 * 32 ** 3
+            tops = 2 * macs / (avg * 1e-3) / 1e12
+            phases_note["matrix"] = {"bound": "mfma", "i8_macs_per_step": macs, "achieved_tops": tops,
+                                     "peak_tops": I8_DENSE_TOPS, "frac_mfma": tops / I8_DENSE_TOPS}
         if cf24:  # digit masks in (8 B per element and plane); f0_coeff, f0 (E each) and w_ccs0 out (from_f's outputs)
             a = wl.N * (2 * wl.pr.K * 8 + 2 * 8 * d) + wl.W * 8 * d
         if ph == "ajtai" and wl.batch:
@@ -652,8 +663,8 @@ def phase_report(LA, wl, tot, steps):
             # and A counts 1 / group of its bytes (SURVEY B1 + B3 count it twice per step)
             E = 8 * d
             nvec = 2 * (wl.pr.K - 1) + 1
-            phases_note = {"steps_per_launch": wl.group, "launch_ms": avg * wl.group,
-                           "survey_bytes_per_step": alg[ph]}
+            phases_note.update({"steps_per_launch": wl.group, "launch_ms": avg * wl.group,
+                                "survey_bytes_per_step": alg[ph]})
             a = E * (kappa * wl.N / wl.group + nvec * wl.N + nvec * kappa)
         gbs = a / (avg * 1e-3) / 1e9
         extra = operand.get(ph, 0) * sides
@@ -668,7 +679,7 @@ def phase_report(LA, wl, tot, steps):
                       "operand_bytes_per_launch": extra,
                       "achieved_gbs_incl_operands": (a + extra) / (avg * 1e-3) / 1e9,
                       "traffic_bytes_per_launch": tr,
-                      "valu_busy": valu.get(kernel_of[ph]), **phases_note}
+                      "valu_busy": valu.get(kernel_of[ph]), "mfma_busy": mfma.get(kernel_of[ph]), **phases_note}
         if cf:
             # an exact i8 GEMM: 1024 coefficients x 2K 1024 digit rows x N elements
             macs = 1024 * 2 * wl.pr.K * 1024 * wl.N
@@ -1195,8 +1206,10 @@ def _sig(x, n=4):
 
 
 def _phase_row(p):
-    """one phase of the compact line: [kernel, ms per step, frac of HBM, PMC bytes per launch, VALU busy]"""
-    return [p["kernel"], p["ms_per_step"], p["frac_hbm"], p.get("traffic_bytes_per_launch"), p.get("valu_busy")]
+    """one phase of the compact line: [kernel, ms per step, frac of HBM, PMC bytes per launch, VALU busy,
+    matrix-pipe busy]"""
+    return [p["kernel"], p["ms_per_step"], p["frac_hbm"], p.get("traffic_bytes_per_launch"), p.get("valu_busy"),
+            p.get("mfma_busy")]
 
 
 def _side_value(s):
@@ -1236,10 +1249,14 @@ def compact_line(out, detail):
                         "pmc_frac": sh.get("pmc_frac_hbm"), "pmc_bytes_per_step": sh.get("pmc_bytes_per_step"),
                         "steps_per_A_read": sh.get("steps_per_A_read")}
     ph = out.get("phases") or {}
-    line["phases"] = {"cols": ["kernel", "ms_per_step", "frac_hbm", "pmc_bytes_per_launch", "valu_busy"],
+    line["phases"] = {"cols": ["kernel", "ms_per_step", "frac_hbm", "pmc_bytes_per_launch", "valu_busy", "mfma_busy"],
                       **{k: _phase_row(v) for k, v in ph.items()}}
     if ph:
         line["phases"]["sum_ms"] = sum(v["ms_per_step"] for v in ph.values())
+        # the matrix-core kernels against the dense i8 peak: [achieved TOPS, fraction]
+        mx = {k: (v.get("matrix") or v.get("coefficient_form") or {}) for k, v in ph.items()}
+        line["i8_mfma"] = {k: [m.get("achieved_tops"), m.get("frac_mfma")] for k, m in mx.items()
+                           if m.get("achieved_tops") is not None}
     side = {}
     for k in ("reference_ring", "small_shape", "configs4_d4096_kappa64"):
         if k in out:
