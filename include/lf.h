@@ -136,7 +136,9 @@ int lf_ctx_set_cu_count(lf_ctx *ctx, int ncu);
  * ordered before it and the work after it waits for it (HIP events; nothing
  * waits on the host), so with a CU-masked stream here and the step streams on
  * the remaining CUs one group's contraction runs beside the next group's
- * decompositions. The stream must be on ctx's device and outlive its use. */
+ * decompositions. The stream must be on ctx's device (LF_ERR_INVALID_ARG
+ * otherwise) and outlive its use; the caller keeps ownership, and
+ * lf_ctx_destroy waits for it before the context's buffers go. */
 int lf_ctx_set_contract_stream(lf_ctx *ctx, void *hip_stream);
 /* wait for the stream; returns LF_ERR_DECOMPOSITION_OVERFLOW (and clears it)
  * if any device decomposition since the last sync ran out of digits */
@@ -572,7 +574,9 @@ int lf_lfproof_serialize(const lf_lfproof *proof, int repr, uint8_t *out, size_t
  *     the CCS must pass sanity_check (m = max((n - l - 1) L, m) rounded up to a
  *     power of two) with N = (n - l - 1) L rounding up to m as well; a multiset
  *     index equal to the number of Mz MLEs (the reference's eq(beta) position) is
- *     rejected with LF_ERR_UNSUPPORTED_CCS
+ *     rejected with LF_ERR_UNSUPPORTED_CCS, a negative index or one past that
+ *     position (malformed: the reference panics on it) with LF_ERR_INVALID_ARG;
+ *     lf_ctx_last_error names the reason
  *   lf_fold_prove: -> the folded LCCCS, its witness (caller-allocated device
  *     buffers: f, f_coeff N elements, w_ccs W) and the LFProof (nifs.rs:28-34).
  *     repr describes every host buffer (acc, cm_i, x_ccs, out, proof).
