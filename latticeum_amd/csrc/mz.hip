@@ -198,30 +198,48 @@ __global__ void k_zcomb(const uint64_t *pw, const uint64_t *z, int nz, int t, si
   s_store(y + jc * d + s * TB, sacc_final(acc));
 }
 
-// out[i][j] = sum_c w[j][c] (.) z_i[c]: one block per (i, j, slot chunk, column split);
-// with nsplit > 1 the block sums columns [split n / nsplit, (split + 1) n / nsplit) into
-// out[split][i][j] (the partial sums k_dots_sum adds up)
+// out[i][j] = sum_c w[j][c] (.) z_i[c]: one block per (j, group of DOTS_NB instances,
+// slot chunk, column split), so each weight word is read once for the group's
+// instances (one block per instance read the 474 MB of weights of the zkvm's CCS
+// once per instance: 4.3 ms of k_dots per fold() for u_s and eta_s in pairs);
+// with nsplit > 1 the block sums columns [split n / nsplit, (split + 1) n / nsplit)
+// into out[split][i][j] (the partial sums k_dots_sum adds up)
+constexpr int DOTS_NB = 4;
 template <int TB>
 __global__ void __launch_bounds__(MT) k_dots(const uint64_t *w, const uint64_t *z, int t, int nz, size_t n, int d,
                                             int spb, int nsplit, uint64_t *out) {
-  __shared__ uint64_t red[MT * TB];
+  __shared__ uint64_t red[DOTS_NB * MT * TB];
   const int slot_l = threadIdx.x % spb, lane_c = threadIdx.x / spb, cpb = MT / spb;
   const int split = blockIdx.z % nsplit, slot = (blockIdx.z / nsplit) * spb + slot_l;
-  const int i = blockIdx.y, j = blockIdx.x;
-  const uint64_t *wj = w + (size_t)j * n * d + slot * TB, *zi = z + (size_t)i * n * d + slot * TB;
+  const int i0 = blockIdx.y * DOTS_NB, j = blockIdx.x;
+  const int nb = nz - i0 < DOTS_NB ? nz - i0 : DOTS_NB;  // uniform
+  const uint64_t *wj = w + (size_t)j * n * d + slot * TB, *zb = z + (size_t)i0 * n * d + slot * TB;
   const size_t c0 = n * split / nsplit, c1 = n * (split + 1) / nsplit;
-  SAcc<TB> la;
-  sacc_zero(la);
-  for (size_t c = c0 + lane_c; c < c1; c += cpb) sacc_mad(la, s_load<TB>(wj + c * d), s_load<TB>(zi + c * d));
-  s_store(red + threadIdx.x * TB, sacc_final(la));
+  SAcc<TB> la[DOTS_NB];
+#pragma unroll
+  for (int b = 0; b < DOTS_NB; b++) sacc_zero(la[b]);
+  for (size_t c = c0 + lane_c; c < c1; c += cpb) {
+    const Sv<TB> wv = s_load<TB>(wj + c * d);
+#pragma unroll
+    for (int b = 0; b < DOTS_NB; b++)
+      if (b < nb) sacc_mad(la[b], wv, s_load<TB>(zb + ((size_t)b * n + c) * d));
+  }
+#pragma unroll
+  for (int b = 0; b < DOTS_NB; b++) s_store(red + ((size_t)b * MT + threadIdx.x) * TB, sacc_final(la[b]));
   __syncthreads();
   for (int h = cpb / 2; h > 0; h >>= 1) {
     if (lane_c < h)
-      s_store(red + threadIdx.x * TB, s_add(s_load<TB>(red + threadIdx.x * TB), s_load<TB>(red + (threadIdx.x + h * spb) * TB)));
+#pragma unroll
+      for (int b = 0; b < DOTS_NB; b++) {
+        uint64_t *r0 = red + ((size_t)b * MT + threadIdx.x) * TB;
+        s_store(r0, s_add(s_load<TB>(r0), s_load<TB>(r0 + (size_t)h * spb * TB)));
+      }
     __syncthreads();
   }
   if (lane_c == 0)
-    s_store(out + (((size_t)split * nz + i) * t + j) * d + slot * TB, s_load<TB>(red + threadIdx.x * TB));
+    for (int b = 0; b < nb; b++)
+      s_store(out + (((size_t)split * nz + i0 + b) * t + j) * d + slot * TB,
+              s_load<TB>(red + ((size_t)b * MT + threadIdx.x) * TB));
 }
 // out[x] = sum_s part[s][x], one thread per word
 __global__ void k_dots_sum(const uint64_t *part, int nsplit, size_t len, uint64_t *out) {
@@ -234,7 +252,7 @@ __global__ void k_dots_sum(const uint64_t *part, int nsplit, size_t len, uint64_
 // column splits: enough blocks for the chip (about 2048) when t nz is small
 int dots_nsplit(const CcsDev &M, int nz) {
   const int tb = slot_words(M.d), ns = M.d / tb, spb = ns < MT ? ns : MT;
-  const size_t blocks = (size_t)M.t * nz * (ns / spb);
+  const size_t blocks = (size_t)M.t * ((nz + DOTS_NB - 1) / DOTS_NB) * (ns / spb);
   int k = (int)((2048 + blocks - 1) / blocks);
   if (k > 16) k = 16;
   if ((size_t)k * 64 > M.n) k = (int)(M.n / 64) > 1 ? (int)(M.n / 64) : 1;
@@ -405,7 +423,7 @@ hipError_t mz_dots(const CcsDev &M, const uint64_t *w, const uint64_t *z, int nz
   const int tb = slot_words(M.d), ns = M.d / tb, spb = ns < MT ? ns : MT;
   const int nsplit = partial ? dots_nsplit(M, nz) : 1;
   uint64_t *dst = nsplit > 1 ? partial : out;
-  const dim3 grid((unsigned)M.t, (unsigned)nz, (unsigned)(ns / spb * nsplit));
+  const dim3 grid((unsigned)M.t, (unsigned)((nz + DOTS_NB - 1) / DOTS_NB), (unsigned)(ns / spb * nsplit));
   if (tb == 3)
     hipLaunchKernelGGL(k_dots<3>, grid, dim3(MT), 0, st, w, z, M.t, nz, M.n, M.d, spb, nsplit, dst);
   else
