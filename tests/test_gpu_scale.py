@@ -254,7 +254,11 @@ def test_fold_step_bench_headline_schedule():
     nsteps = 8 over the 21.5 GB fragment matrix) and a trailing 4-step batch.
     Every one of the 8 streams against the oracle (streams 0-3 last ran in the
     4-step batch, 4-7 in the second 8-step launch). The packed planes are expanded
-    a column block at a time: the workload holds about 240 of the 288 GB."""
+    a column block at a time: the workload holds about 240 of the 288 GB.
+    Reference: decompose_witness + commit_witnesses
+    (latticefold/src/nifs/decomposition.rs:162-201) and the Ajtai mat-vec
+    (stark-rings/crates/linear_algebra/src/matrix.rs:168-178), as the oracle
+    restates them."""
     import torch
     wl = run_workload(1024, 1 << 14, 32, streams=8, batch=8, steps=20)
     try:
