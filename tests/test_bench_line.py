@@ -95,3 +95,26 @@ def test_stale_pmc_files_are_not_used(tmp_path, monkeypatch):
     doc["src_hash"] = bench.kernel_source_hash()
     (prof / "pmc_traffic_d1024_W16384_k32.json").write_text(json.dumps(doc))
     assert bench.load_traffic(1024, 16384, 32)["k_decompose_fused"] == 1.0
+
+
+def test_round6_line_carries_matrix_and_side_op_counters():
+    """the r06 evidence line: each phase row has the matrix-pipe busy column, the
+    matrix-core kernels are priced against the dense i8 peak, the side ops carry
+    their own PMC figures, and the compact line still fits"""
+    full = json.loads((ROOT / "profiles" / "r06_bench_detail.json").read_text())
+    line = json.loads(bench.compact_line(full, "d.json"))
+    assert line["phases"]["cols"][-1] == "mfma_busy"
+    assert len(line["phases"]["ajtai"]) == len(line["phases"]["cols"])
+    tops, frac = line["i8_mfma"]["ajtai"]
+    assert 0 < frac < 1 and abs(tops / bench.I8_DENSE_TOPS - frac) < 1e-3
+    m = full["phases"]["ajtai"]["matrix"]
+    # d = 1024, W = 2^14, kappa = 32: 1024 slots x 2560 chunks x 64 products of 32^3
+    assert m["i8_macs_per_step"] == 1024 * 2560 * 64 * 32 ** 3
+    for k in ("ntt_fwd", "ntt_inv", "poseidon2_w16"):
+        assert k in line["side"]["side_ops_pmc"]
+    assert len(json.dumps(line)) < bench.LINE_LIMIT
+
+
+def test_side_ops_pmc_config_is_separate():
+    """the side ops' PMC files are keyed by their own config, never mistaken for a step line's"""
+    assert bench._pmc_doc("traffic", 1024, 16384, 32, "pmc_traffic_side_ops.json", {"d": 1024}) is None
