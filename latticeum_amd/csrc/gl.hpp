@@ -55,6 +55,21 @@ LF_HD uint64_t sub(uint64_t a, uint64_t b) {  // canonical in -> canonical out
 
 LF_HD uint64_t neg(uint64_t a) { return a ? P - a : 0; }
 
+// X + Y 2^32 (mod p), canonical, for signed |X|, |Y| < 2^62 (the i8-MFMA epilogues' quarter
+// sums): Y 2^32 = yh 2^64 + yl 2^32 == yh (2^32 - 1) + yl 2^32 (yh = Y >> 32), and
+// U = yl + yh = c 2^32 + ul (c in {-1, 0, 1}) folds the same way, leaving V + ul 2^32 with
+// V = X - yh + c (2^32 - 1); that 65-bit sum is t + k 2^64 with k = carry - [V < 0],
+// == t + k (2^32 - 1) without wrapping (t < 2^63 when k = 1, t > 2^63 when k = -1)
+LF_HD uint64_t from_x_y32(int64_t X, int64_t Y) {
+  const int64_t yh = Y >> 32;
+  const int64_t U = (int64_t)(uint32_t)Y + yh;
+  const int64_t c = U >> 32;
+  const int64_t V = X - yh + c * (int64_t)EPS;
+  uint64_t t;
+  const int k = (int)addc64((uint64_t)V, (uint64_t)(uint32_t)U << 32, t) - (V < 0);
+  return canon(t + (uint64_t)((int64_t)k * (int64_t)EPS));
+}
+
 // 64x64 -> 128 from four 32x32 -> 64 multiply-adds (v_mad_u64_u32 each; no
 // intermediate sum overflows: (2^32-1)^2 + 2 (2^32-1) = 2^64 - 1)
 LF_HD void mul_wide(uint64_t a, uint64_t b, uint64_t &lo, uint64_t &hi) {

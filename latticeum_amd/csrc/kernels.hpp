@@ -349,13 +349,16 @@ struct CcsDev {
   const uint32_t *cidx;
 };
 size_t mz_scratch_elems(const CcsDev &M, int nz, int nv);
+// scratch words of one side of mz_challenged(_pair): the zeta powers, for d = 24 the
+// matrix-core operand pieces, and y = sum_i zeta_i^(j+1) z_i ([t][n][d])
+size_t mz_chall_elems(const CcsDev &M, int nz);
 // out [nz][t][2^nv][d] = MLE(M_j z_i), zero-padded; z [nz][n][d]
 // sel (device, optional): out holds the MLEs of matrices sel[0 .. nsel) in that order
 hipError_t mz_mles(const CcsDev &M, const uint64_t *z, int nz, int nv, uint64_t *out, hipStream_t st,
                    const int *sel = nullptr, int nsel = 0);
 // out [2^nv][d] = sum_i sum_j zeta_i^(j+1) MLE(M_j z_i)
 // mz_challenged for two (z, zeta) at once over one pass of the row-merged matrix;
-// scratch: 2 (2 t nz d + t n d) elements
+// scratch: 2 mz_chall_elems elements
 hipError_t mz_challenged_pair(const CcsDev &M, const uint64_t *z0, const uint64_t *zeta0, const uint64_t *z1,
                               const uint64_t *zeta1, int nz, int nv, uint64_t *out0, uint64_t *out1,
                               uint64_t *scratch, hipStream_t st);

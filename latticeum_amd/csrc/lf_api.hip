@@ -2321,7 +2321,7 @@ int lf_dev_mz_challenged_pair(lf_ctx *c, const lf_ccs *M, const uint64_t *z0, co
   DevGuard g(c);
   LF_TRY(mz_check(c, M, nz, nv));
   const lfk::CcsDev &D = M->dev;
-  LF_TRY(grow(c, c->tmp, c->tmp_elems, 2 * (2 * (size_t)D.t * nz * D.d + (size_t)D.t * D.n * D.d)));
+  LF_TRY(grow(c, c->tmp, c->tmp_elems, 2 * lfk::mz_chall_elems(D, nz)));
   LF_HIP(c, lfk::mz_challenged_pair(D, z0, zeta0, z1, zeta1, nz, nv, out0, out1, c->tmp, c->cur));
   return LF_OK;
 }

@@ -14,6 +14,7 @@
 // the evaluations MLE(M_j z_i)(r) = sum_x eq(r, x) (M_j z_i)[x] run as
 // w_j = M_j^T eq(r) and dot products w_j . z_i -- the same field elements
 // without materialising the t x nz MLEs of 2^s ring elements each.
+#include "frag.hpp"
 #include "kernels.hpp"
 #include "slot.hpp"
 
@@ -110,76 +111,186 @@ __global__ void __launch_bounds__(MT) k_csr_pair(const uint64_t *rp, const uint3
   s_store(out1 + r * d + slot * TB, sacc_final(a1));
 }
 
-// pw[j][i] = zeta_i^(j+1)
+// pw[j][i] = zeta_i^(j+1), one thread per (j, instance, slot) by square-and-multiply
+// (a chain of t dependent products per (instance, slot) was 60 us of latency)
 template <int TB>
 __global__ void k_zeta_pows(const uint64_t *zeta, int nz, int t, int d, uint64_t *pw) {
   const int ns = d / TB;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (instance, slot)
-  if (i >= nz * ns) return;
-  const int zi = i / ns, s = i - zi * ns;
-  const Sv<TB> zt = s_load<TB>(zeta + (size_t)zi * d + s * TB);
-  Sv<TB> p = zt;
-  for (int j = 0; j < t; j++) {
-    s_store(pw + ((size_t)j * nz + zi) * d + s * TB, p);
-    p = s_mul(p, zt);
+  const size_t u = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // (j nz + instance) ns + slot
+  if (u >= (size_t)t * nz * ns) return;
+  const int s = (int)(u % ns);
+  const size_t ji = u / ns;
+  const int zi = (int)(ji % nz);
+  unsigned e = (unsigned)(ji / nz) + 1;
+  Sv<TB> b = s_load<TB>(zeta + (size_t)zi * d + s * TB), p = s_one<TB>();
+  for (; e; e >>= 1) {
+    if (e & 1) p = s_mul(p, b);
+    if (e > 1) b = s_mul(b, b);
   }
+  s_store(pw + ji * d + s * TB, p);
 }
 
-// Fq3 (d = 24): the powers with their pairwise sums, pk[j][i][slot] = (p0, p1, p2,
-// p0 + p1, p0 + p2, p1 + p2), for the Karatsuba form of k_zcomb3
-__global__ void k_zeta_pows3k(const uint64_t *zeta, int nz, int t, int d, uint64_t *pk) {
-  const int ns = d / 3;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (instance, slot)
-  if (i >= nz * ns) return;
-  const int zi = i / ns, s = i - zi * ns;
-  const Sv<3> zt = s_load<3>(zeta + (size_t)zi * d + s * 3);
-  Sv<3> p = zt;
-  for (int j = 0; j < t; j++) {
-    uint64_t *o = pk + ((size_t)j * nz + zi) * 2 * d + s * 6;
-    o[0] = p.c[0];
-    o[1] = p.c[1];
-    o[2] = p.c[2];
-    o[3] = gl::add(p.c[0], p.c[1]);
-    o[4] = gl::add(p.c[0], p.c[2]);
-    o[5] = gl::add(p.c[1], p.c[2]);
-    p = s_mul(p, zt);
+// The zeta combination on the matrix cores (d = 24, Fq3 slots): per slot s,
+// y_s[j][c] = sum_i P_s[j][i] z_i[c][s] with P = zeta_i^(j+1) in Fq3 = F[u]/(u^3 - 2^40)
+// (calculate_challenged_mz_mle, folding.rs:208-234, through its linearity) is the
+// product of the M-form matrix A_s[(j, a)][(i, b)] = m_ab(P_s[j][i]) -- m_ab = p_(a-b),
+// or 2^40 p_(a-b+3) when a < b, so that c_a = sum_b m_ab z_b is the Fq3 product
+// (goldilocks/mod.rs:34-54) -- with B_s[(i, b)][c] = z_i[c][s][b]: (3t x 3nz) by
+// (3nz x n) per slot. Both operands go to the D8 signed-byte form (8 digits each,
+// frag.hpp) and the 64 digit products run as v_mfma_i32_16x16x64_i8 into the 15
+// weights the ajtai contraction's epilogue folds (ajtai_mfma.hip mfma_epilogue):
+// |acc_t| <= kcn 64 * 8 * 128^2 = kcn 2^23. Tiles: 16 rows = ZC_J = 5 values of j
+// times 3 components (row 15 zero) by 16 columns, K = 3 nz in chunks of 64.
+// Operand pieces (one 16-byte piece per lane and digit, 1 KiB per digit):
+// lane l holds A[row l & 15][k = 16 (l >> 4) + jj] and B[k = 16 (l >> 4) + jj][col l & 15]
+// in byte jj; D register i of lane l is row 4 (l >> 4) + i, column l & 15.
+constexpr int ZC_J = 5, ZC_WAVES = 4, ZC_D = 24;
+
+// af[((s nrt + rt) kcn + kc) 8 + digit][lane]: the M-form tiles from pw[j][i][slot] (k_zeta_pows<3>)
+__global__ void k_zc_afrag(const uint64_t *pw, int nz, int t, int nrt, int kcn, v4i *af) {
+  constexpr int ns = ZC_D / 3;
+  const size_t u = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (u >= (size_t)ns * nrt * kcn * 64) return;
+  const int l = (int)(u & 63);
+  const size_t q = u >> 6;
+  const int kc = (int)(q % kcn), rt = (int)(q / kcn % nrt), s = (int)(q / kcn / nrt);
+  const int r = l & 15, g = l >> 4, jl = r / 3, a = r - 3 * jl, j = ZC_J * rt + jl;
+  uint64_t x[16];
+#pragma unroll
+  for (int jj = 0; jj < 16; jj++) {
+    const int k = 64 * kc + 16 * g + jj, i = k / 3, b = k - 3 * i;
+    uint64_t v = 0;
+    if (r < 3 * ZC_J && j < t && i < nz) {
+      const uint64_t *p = pw + ((size_t)j * nz + i) * ZC_D + s * 3;
+      v = a >= b ? p[a - b] : gl::shl96(p[a - b + 3], 40);
+    }
+    x[jj] = d8(v);
   }
+  uint4 pc[8];
+  d8_transpose16(x, pc);
+#pragma unroll
+  for (int dg = 0; dg < 8; dg++) af[(q * 8 + dg) * 64 + l] = *reinterpret_cast<const v4i *>(&pc[dg]);
 }
-// y[j][c] = sum_i pw[j][i] (.) z_i[c] in Fq3 with Karatsuba's six products per term, each
-// summed lazily over i (P_k = sum p_k z_k, Q_kl = sum (p_k + p_l)(z_k + z_l)) and combined
-// once: a1 b2 + a2 b1 = Q12 - P1 - P2 and so on; c0 = P0 + 2^40 (a1 b2 + a2 b1),
-// c1 = (a0 b1 + a1 b0) + 2^40 P2, c2 = (a0 b2 + a2 b0) + P1. Six multiply-accumulates
-// and three additions per term instead of nine and two shifts (goldilocks/mod.rs:34-54).
-__global__ void k_zcomb3k(const uint64_t *pk, const uint64_t *z, int nz, int t, size_t n, int d, uint64_t *y) {
-  const int ns = d / 3;
-  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // (j, c, slot)
-  if (i >= (size_t)t * n * ns) return;
-  const size_t jc = i / ns;
-  const int s = (int)(i - jc * ns);
-  const size_t j = jc / n, c = jc - j * n;
-  gl::CAcc a[6];
+
+// bf[((ct ns + s) kcn + kc) 8 + digit][lane]: the z operand of column tile ct (16 columns)
+__global__ void k_zc_bfrag(const uint64_t *z, int nz, size_t n, int kcn, size_t nct, v4i *bf) {
+  constexpr int ns = ZC_D / 3;
+  const size_t u = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (u >= nct * ns * kcn * 64) return;
+  const int l = (int)(u & 63);
+  const size_t q = u >> 6;  // (ct, kc, s): one block of 8 waves reads a column tile's whole rows
+  const int s = (int)(q % ns), kc = (int)(q / ns % kcn);
+  const size_t ct = q / ns / kcn, c = 16 * ct + (l & 15);
+  const int g = l >> 4;
+  uint64_t x[16];
 #pragma unroll
-  for (int k = 0; k < 6; k++) gl::cacc_zero(a[k]);
-  for (int zi = 0; zi < nz; zi++) {
-    const uint64_t *pp = pk + (j * nz + zi) * 2 * d + s * 6;
-    const Sv<3> zv = s_load<3>(z + (zi * n + c) * d + s * 3);
-    gl::cacc_mad(a[0], pp[0], zv.c[0]);
-    gl::cacc_mad(a[1], pp[1], zv.c[1]);
-    gl::cacc_mad(a[2], pp[2], zv.c[2]);
-    gl::cacc_mad(a[3], pp[3], gl::add(zv.c[0], zv.c[1]));
-    gl::cacc_mad(a[4], pp[4], gl::add(zv.c[0], zv.c[2]));
-    gl::cacc_mad(a[5], pp[5], gl::add(zv.c[1], zv.c[2]));
+  for (int jj = 0; jj < 16; jj++) {
+    const int k = 64 * kc + 16 * g + jj, i = k / 3, b = k - 3 * i;
+    x[jj] = d8(c < n && i < nz ? z[((size_t)i * n + c) * ZC_D + s * 3 + b] : 0);
   }
-  uint64_t v[6];
+  uint4 pc[8];
+  d8_transpose16(x, pc);
+  const size_t o = ((ct * ns + s) * kcn + kc) * 8;
 #pragma unroll
-  for (int k = 0; k < 6; k++) v[k] = gl::cacc_reduce(a[k]);
-  const uint64_t m12 = gl::sub(gl::sub(v[5], v[1]), v[2]);  // sum a1 b2 + a2 b1
-  const uint64_t m01 = gl::sub(gl::sub(v[3], v[0]), v[1]);
-  const uint64_t m02 = gl::sub(gl::sub(v[4], v[0]), v[2]);
-  uint64_t *o = y + jc * d + s * 3;
-  o[0] = gl::add(v[0], gl::shl96(m12, 40));
-  o[1] = gl::add(m01, gl::shl96(v[2], 40));
-  o[2] = gl::add(m02, v[1]);
+  for (int dg = 0; dg < 8; dg++) bf[(o + dg) * 64 + l] = *reinterpret_cast<const v4i *>(&pc[dg]);
+}
+
+// one wave per (column tile ct, row tile rt), the block's waves on consecutive rt of
+// one ct (their z pieces come from the same L1 lines), and the blocks of one ct on one
+// XCD (blocks are dealt round-robin over the 8 XCDs: block b runs on XCD b & 7), so a
+// column tile's pieces come into one L2 once. Per slot 64 MFMAs per K chunk, the next
+// chunk's pieces loaded behind them, and the epilogue into the wave's LDS rows
+// [jl][c][24]; then one pass of whole 192-byte (j, c) elements out (16 consecutive
+// columns: 3 KiB contiguous per j)
+// the 64 digit products of one K chunk into the 15 weights; FIRST: the chunk that starts
+// the sums (each weight's first product, (0, t) or (t - 7, 7), takes a zero accumulator)
+template <bool FIRST>
+__device__ __forceinline__ void zc_products(const v4i *A, const v4i *B, v4i *acc) {
+#pragma unroll
+  for (int ka = 0; ka < 8; ka++)
+#pragma unroll
+    for (int kb = 0; kb < 8; kb++)
+      acc[ka + kb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+          A[ka], B[kb], FIRST && (ka == 0 || kb == 7) ? (v4i){0, 0, 0, 0} : acc[ka + kb], 0, 0, 0);
+}
+
+// SK (3 nz < 64, one K chunk with a zero tail: |acc_t| <= 3 nz 8 128^2 < 2^31 / 257): the
+// weights pair up in 32 bits first, W_m = acc_2m + 2^8 acc_2m+1, halving the 64-bit work
+template <bool SK>
+__global__ void __launch_bounds__(64 * ZC_WAVES) k_zcomb_mfma(const v4i *af, const v4i *bf, int t, size_t n, int nrt,
+                                                           int kcn, size_t nct, uint64_t *y) {
+  constexpr int ns = ZC_D / 3;
+  __shared__ uint64_t stg[ZC_WAVES][ZC_J * 16 * ZC_D];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int nbr = (nrt + ZC_WAVES - 1) / ZC_WAVES;  // blocks per column tile
+  const size_t k = blockIdx.x >> 3, ct = (k / nbr) * 8 + (blockIdx.x & 7);
+  const int rt = (int)(k % nbr) * ZC_WAVES + w;
+  if (ct >= nct || rt >= nrt) return;  // no block-wide synchronisation below
+  uint64_t *sg = stg[w];
+  v4i A[8], B[8], acc[15];
+  auto load = [&](int u) {
+    const int s = u / kcn, kc = u - s * kcn;
+    const v4i *ap = af + (((size_t)s * nrt + rt) * kcn + kc) * 512 + l;
+    const v4i *bp = bf + ((ct * ns + s) * kcn + kc) * 512 + l;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      A[q] = ap[64 * q];
+      B[q] = bp[64 * q];
+    }
+  };
+  load(0);
+  for (int u = 0; u < ns * kcn; u++) {
+    const int s = u / kcn, kc = u - s * kcn;
+    if (kc == 0)
+      zc_products<true>(A, B, acc);
+    else
+      zc_products<false>(A, B, acc);
+    if (u + 1 < ns * kcn) load(u + 1);
+    if (kc < kcn - 1) continue;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      int64_t S[4] = {0, 0, 0, 0};
+      if (SK) {
+        int32_t W[8];
+#pragma unroll
+        for (int m = 0; m < 7; m++) W[m] = acc[2 * m][i] + acc[2 * m + 1][i] * 256;
+        W[7] = acc[14][i];
+#pragma unroll
+        for (int q = 0; q < 4; q++) S[q] = (int64_t)W[2 * q] + (int64_t)W[2 * q + 1] * 65536;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 15; q++) S[q >> 2] += (int64_t)acc[q][i] << (8 * (q & 3));
+      }
+      const uint64_t v = gl::from_x_y32(S[0] - S[2] - S[3], S[1] + S[2]);  // sum_t 2^(8t) acc_t
+      const int row = 4 * (l >> 4) + i, jl = row / 3, a = row - 3 * jl;
+      if (row < 3 * ZC_J) sg[(jl * 16 + (l & 15)) * ZC_D + s * 3 + a] = v;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint4 *sq = reinterpret_cast<const uint4 *>(sg);
+  constexpr int PJ = 16 * ZC_D / 2, NQ = ZC_J * PJ / 64;  // 16-byte pieces per j, per lane
+  if (ZC_J * (rt + 1) <= t && 16 * (ct + 1) <= n) {  // a whole tile: all reads, then all stores
+    uint4 v[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; q++) v[q] = sq[64 * q + l];
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+      const int x = 64 * q + l, jl = x / PJ;
+      reinterpret_cast<uint4 *>(y + ((size_t)(ZC_J * rt + jl) * n + 16 * ct) * ZC_D)[x - jl * PJ] = v[q];
+    }
+    return;
+  }
+  const int words = (int)((n - 16 * ct < 16 ? n - 16 * ct : 16) * ZC_D);
+  for (int jl = 0; jl < ZC_J; jl++) {
+    const int j = ZC_J * rt + jl;
+    if (j >= t) break;
+    uint64_t *dst = y + ((size_t)j * n + 16 * ct) * ZC_D;
+    const uint64_t *src = sg + jl * 16 * ZC_D;
+    for (int o = 2 * l; o < words; o += 128)
+      *reinterpret_cast<uint4 *>(dst + o) = *reinterpret_cast<const uint4 *>(src + o);
+  }
 }
 
 // y[j][c] = sum_i pw[j][i] (.) z_i[c]
@@ -297,11 +408,49 @@ hipError_t csr(const CcsDev &M, const uint64_t *rp, size_t rp_stride, int na, co
   return hipGetLastError();
 }
 
+// words of one side's scratch before y: the powers pw and, for d = 24, the operand pieces
+size_t zc_front(const CcsDev &M, int nz) {
+  if (slot_words(M.d) != 3) return 2 * (size_t)M.t * nz * M.d;
+  const size_t kcn = (3 * (size_t)nz + 63) / 64, nrt = ((size_t)M.t + ZC_J - 1) / ZC_J, nct = (M.n + 15) / 16;
+  return (size_t)M.t * nz * M.d + (nrt + nct) * (ZC_D / 3) * kcn * 512 * 2;
+}
+
+// y[j][c] = sum_i zeta_i^(j+1) (.) z_i[c] in one side's scratch (pw | pieces | y)
+hipError_t zcomb(const CcsDev &M, const uint64_t *z, const uint64_t *zeta, int nz, uint64_t *scr, uint64_t *&y,
+                 hipStream_t st) {
+  const int tb = slot_words(M.d), ns = M.d / tb;
+  uint64_t *pw = scr;
+  y = scr + zc_front(M, nz);
+  if (!M.t || !M.n || nz < 1) return hipSuccess;
+  if (tb == 3) {
+    if (M.d != ZC_D) return hipErrorInvalidValue;
+    const int kcn = (3 * nz + 63) / 64, nrt = (M.t + ZC_J - 1) / ZC_J;
+    const size_t nct = (M.n + 15) / 16;
+    v4i *af = reinterpret_cast<v4i *>(scr + (size_t)M.t * nz * M.d), *bf = af + (size_t)ns * nrt * kcn * 512;
+    hipLaunchKernelGGL(k_zeta_pows<3>, dim3(nblk((size_t)M.t * nz * ns, 256)), dim3(256), 0, st, zeta, nz, M.t, M.d, pw);
+    hipLaunchKernelGGL(k_zc_afrag, dim3(nblk((size_t)ns * nrt * kcn * 64, 256)), dim3(256), 0, st, pw, nz, M.t, nrt,
+                       kcn, af);
+    hipLaunchKernelGGL(k_zc_bfrag, dim3(nblk(nct * ns * kcn * 64, 512)), dim3(512), 0, st, z, nz, M.n, kcn, nct, bf);
+    const dim3 grid((unsigned)(8 * ((nct + 7) / 8) * ((nrt + ZC_WAVES - 1) / ZC_WAVES)));
+    if (3 * nz < 64)
+      hipLaunchKernelGGL(k_zcomb_mfma<true>, grid, dim3(64 * ZC_WAVES), 0, st, af, bf, M.t, M.n, nrt, kcn, nct, y);
+    else
+      hipLaunchKernelGGL(k_zcomb_mfma<false>, grid, dim3(64 * ZC_WAVES), 0, st, af, bf, M.t, M.n, nrt, kcn, nct, y);
+  } else {
+    hipLaunchKernelGGL(k_zeta_pows<1>, dim3(nblk((size_t)M.t * nz * ns, 256)), dim3(256), 0, st, zeta, nz, M.t, M.d, pw);
+    hipLaunchKernelGGL(k_zcomb<1>, dim3(nblk((size_t)M.t * M.n * ns, 256)), dim3(256), 0, st, pw, z, nz, M.t, M.n,
+                       M.d, y);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
+
+size_t mz_chall_elems(const CcsDev &M, int nz) { return zc_front(M, nz) + (size_t)M.t * M.n * M.d; }
 
 size_t mz_scratch_elems(const CcsDev &M, int nz, int nv) {
   const size_t e = ((size_t)1 << nv) * M.d, tn = (size_t)M.t * M.n * M.d;
-  const size_t chall = 2 * (size_t)M.t * nz * M.d + tn, eval = e + tn + mz_dots_partial_elems(M, nz);
+  const size_t chall = mz_chall_elems(M, nz), eval = e + tn + mz_dots_partial_elems(M, nz);
   return chall > eval ? chall : eval;
 }
 
@@ -324,18 +473,8 @@ hipError_t mz_challenged(const CcsDev &M, const uint64_t *z, const uint64_t *zet
                          uint64_t *scratch, hipStream_t st) {
   const size_t len = ((size_t)1 << nv) * M.d;
   if (M.m > ((size_t)1 << nv)) return hipErrorInvalidValue;
-  const int tb = slot_words(M.d), ns = M.d / tb;
-  uint64_t *pw = scratch, *y = scratch + 2 * (size_t)M.t * nz * M.d;
-  if (tb == 3)
-    hipLaunchKernelGGL(k_zeta_pows3k, dim3(nblk((size_t)nz * ns, 256)), dim3(256), 0, st, zeta, nz, M.t, M.d, pw);
-  else
-    hipLaunchKernelGGL(k_zeta_pows<1>, dim3(nblk((size_t)nz * ns, 256)), dim3(256), 0, st, zeta, nz, M.t, M.d, pw);
-  const size_t ny = (size_t)M.t * M.n * ns;
-  if (tb == 3)
-    hipLaunchKernelGGL(k_zcomb3k, dim3(nblk(ny, 256)), dim3(256), 0, st, pw, z, nz, M.t, M.n, M.d, y);
-  else
-    hipLaunchKernelGGL(k_zcomb<1>, dim3(nblk(ny, 256)), dim3(256), 0, st, pw, z, nz, M.t, M.n, M.d, y);
-  hipError_t e = hipGetLastError();
+  uint64_t *y;
+  hipError_t e = zcomb(M, z, zeta, nz, scratch, y, st);
   if (e != hipSuccess) return e;
   if (len > M.m * M.d) {
     e = hipMemsetAsync(out + M.m * M.d, 0, (len - M.m * M.d) * 8, st);
@@ -350,23 +489,11 @@ hipError_t mz_challenged_pair(const CcsDev &M, const uint64_t *z0, const uint64_
   const size_t len = ((size_t)1 << nv) * M.d;
   if (M.m > ((size_t)1 << nv)) return hipErrorInvalidValue;
   const int tb = slot_words(M.d), ns = M.d / tb;
-  const size_t per = 2 * (size_t)M.t * nz * M.d + (size_t)M.t * M.n * M.d;  // pw | y of one side
+  const size_t per = mz_chall_elems(M, nz);  // pw | pieces | y of one side
   const uint64_t *zs[2] = {z0, z1}, *zetas[2] = {zeta0, zeta1};
   uint64_t *ys[2], *outs[2] = {out0, out1};
   for (int q = 0; q < 2; q++) {
-    uint64_t *pw = scratch + q * per, *y = pw + 2 * (size_t)M.t * nz * M.d;
-    ys[q] = y;
-    if (tb == 3)
-      hipLaunchKernelGGL(k_zeta_pows3k, dim3(nblk((size_t)nz * ns, 256)), dim3(256), 0, st, zetas[q], nz, M.t, M.d, pw);
-    else
-      hipLaunchKernelGGL(k_zeta_pows<1>, dim3(nblk((size_t)nz * ns, 256)), dim3(256), 0, st, zetas[q], nz, M.t, M.d,
-                         pw);
-    const size_t ny = (size_t)M.t * M.n * ns;
-    if (tb == 3)
-      hipLaunchKernelGGL(k_zcomb3k, dim3(nblk(ny, 256)), dim3(256), 0, st, pw, zs[q], nz, M.t, M.n, M.d, y);
-    else
-      hipLaunchKernelGGL(k_zcomb<1>, dim3(nblk(ny, 256)), dim3(256), 0, st, pw, zs[q], nz, M.t, M.n, M.d, y);
-    hipError_t e = hipGetLastError();
+    hipError_t e = zcomb(M, zs[q], zetas[q], nz, scratch + q * per, ys[q], st);
     if (e != hipSuccess) return e;
     if (len > M.m * M.d) {
       e = hipMemsetAsync(outs[q] + M.m * M.d, 0, (len - M.m * M.d) * 8, st);

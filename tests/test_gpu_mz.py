@@ -114,6 +114,33 @@ def test_mz_products_match_oracle(ctx, d, scalar):
     assert np.array_equal(host(ev), np.concatenate([O.mle_evaluate(w[k], nv, d, point) for k in range(nz * t)]))
 
 
+@pytest.mark.parametrize("t,n,nz", [(12, 50, 22), (1, 1, 1), (7, 33, 64), (6, 16, 21)])
+def test_mz_challenged_tiles(ctx, t, n, nz):
+    """the matrix-core zeta combination (d = 24, mz.hip k_zcomb_mfma) at tile edges:
+    a last row tile of fewer than 5 values of j, a last column tile of fewer than 16
+    columns, K = 3 nz over one, two and three 64-wide chunks (with and without a
+    zero tail), one column and one matrix; both sides of the pair form"""
+    d, m, nv = 24, 40, 6
+    mats = random_ccs(t, m, n, d, 900 + t + n + nz, scalar=(nz % 2 == 0))
+    M = LA.CCSMatrices(ctx, d, m, n, mats)
+    zs = [O.fill_uniform(n * d, 910 + i) for i in range(nz)]
+    zs[0][:d] = P - 1  # the largest residues in the first column
+    zeta = O.fill_uniform(nz * d, 920)
+    zeta[:3] = P - 1
+    want = O.mz_challenged(mats, zs, [zeta[i * d:(i + 1) * d] for i in range(nz)], nv, d)
+    ch = dev(n=(1 << nv) * d)
+    M.mz_challenged(dev(np.concatenate(zs)), dev(zeta), nz, nv, ch)
+    ctx.sync()
+    assert np.array_equal(host(ch), want)
+    zs2 = [O.fill_uniform(n * d, 930 + i) for i in range(nz)]
+    zeta2 = O.fill_uniform(nz * d, 940)
+    c0, c1 = dev(n=(1 << nv) * d), dev(n=(1 << nv) * d)
+    M.mz_challenged_pair(dev(np.concatenate(zs)), dev(zeta), dev(np.concatenate(zs2)), dev(zeta2), nz, nv, c0, c1)
+    ctx.sync()
+    assert np.array_equal(host(c0), want)
+    assert np.array_equal(host(c1), O.mz_challenged(mats, zs2, [zeta2[i * d:(i + 1) * d] for i in range(nz)], nv, d))
+
+
 def test_mz_zkvm_dimensions(ctx):
     """m = 2^17, n = 19 768, t = 125 (zkvm ccs.rs:43-67) with ~2 entries per row
     per matrix: sampled rows of the materialised products against the oracle,
