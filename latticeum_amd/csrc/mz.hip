@@ -27,8 +27,9 @@ constexpr int MT = 256;
 // out[task][r] = sum_k val[vidx ? vidx[k] : k] (.) z[col[k]], k in [rp[r], rp[r+1]);
 // task = (a, b) = (task % na, task / na) selects rp + A rp_stride (A = sel ? sel[a] : a)
 // and z + b z_stride. SC: val holds one scalar per entry (CcsDev::sval), the zkvm's
-// matrices (R::one(), from_goldilocks constants: zkvm/src/constraints.rs:127-364)
-template <int TB, bool SC>
+// matrices (R::one(), from_goldilocks constants: zkvm/src/constraints.rs:127-364).
+// NT: streaming stores (outputs larger than the caches; CSR_NT_BYTES)
+template <int TB, bool SC, bool NT>
 __global__ void __launch_bounds__(MT) k_csr(const uint64_t *rp, size_t rp_stride, int na, const int *sel,
                                            const uint32_t *col, const uint32_t *vidx, const uint64_t *val,
                                            size_t nrows, int d, const uint64_t *z, size_t z_stride, uint64_t *out,
@@ -64,7 +65,10 @@ __global__ void __launch_bounds__(MT) k_csr(const uint64_t *rp, size_t rp_stride
     for (int u = 0; u < 4; u++) term(vi[u], c[u]);
   }
   for (; k < e; k++) term(vidx ? vidx[k] : k, col[k]);
-  s_store(out + task * out_stride + r * d + slot * TB, sacc_final(acc));
+  const Sv<TB> v = sacc_final(acc);
+  uint64_t *o = out + task * out_stride + r * d + slot * TB;
+#pragma unroll
+  for (int w = 0; w < TB; w++) out_store<NT>(o + w, v.c[w]);
 }
 
 // Two challenged products over the same rows (the folding prover's g1 and g3, one per
@@ -372,6 +376,11 @@ int dots_nsplit(const CcsDev &M, int nz) {
 
 unsigned nblk(size_t n, int t) { return (unsigned)((n + t - 1) / t); }
 
+// Mz MLE outputs above this many bytes are written with streaming stores: the zkvm's
+// 3.1 GB otherwise cycle through L2 and evict the z rows the gathers re-read (k_csr
+// 1.43 -> 1.32 ms; the transposes' 474 MB of weights gain nothing and keep plain stores)
+constexpr size_t CSR_NT_BYTES = (size_t)256 << 20;
+
 // out[i][from + x] = 0 for x < tail, i < total / tail (MLE i of len u64)
 __global__ void k_zero_tails(uint64_t *out, size_t len, size_t from, size_t tail, size_t total) {
   const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -384,25 +393,32 @@ __global__ void k_zero_tails(uint64_t *out, size_t len, size_t from, size_t tail
 // without vidx; otherwise the ring values through vidx
 hipError_t csr(const CcsDev &M, const uint64_t *rp, size_t rp_stride, int na, const uint32_t *col,
                const uint32_t *vidx, const uint64_t *sv, size_t nrows, const uint64_t *z, size_t z_stride,
-               uint64_t *out, size_t out_stride, int ntask, hipStream_t st, const int *sel = nullptr) {
+               uint64_t *out, size_t out_stride, int ntask, hipStream_t st, const int *sel = nullptr,
+               bool nt = false) {
   if (!nrows || !ntask) return hipSuccess;
   const int d = M.d, tb = slot_words(d), ns = d / tb, spb = ns < MT ? ns : MT;
   const dim3 grid(nblk(nrows, MT / spb), (unsigned)ntask, (unsigned)(ns / spb));
   const uint64_t *val = M.sval ? sv : M.val;
   if (M.sval) vidx = nullptr;
-#define LF_CSR(TB, SC)                                                                                            \
-  hipLaunchKernelGGL((k_csr<TB, SC>), grid, dim3(MT), 0, st, rp, rp_stride, na, sel, col, vidx, val, nrows, d, z, \
-                     z_stride, out, out_stride, spb)
+#define LF_CSR(TB, SC)                                                                                          \
+  if (nt)                                                                                                       \
+    hipLaunchKernelGGL((k_csr<TB, SC, true>), grid, dim3(MT), 0, st, rp, rp_stride, na, sel, col, vidx, val, nrows, \
+                       d, z, z_stride, out, out_stride, spb);                                                   \
+  else                                                                                                          \
+    hipLaunchKernelGGL((k_csr<TB, SC, false>), grid, dim3(MT), 0, st, rp, rp_stride, na, sel, col, vidx, val,     \
+                       nrows, d, z, z_stride, out, out_stride, spb)
   if (tb == 3) {
-    if (M.sval)
+    if (M.sval) {
       LF_CSR(3, true);
-    else
+    } else {
       LF_CSR(3, false);
+    }
   } else {
-    if (M.sval)
+    if (M.sval) {
       LF_CSR(1, true);
-    else
+    } else {
       LF_CSR(1, false);
+    }
   }
 #undef LF_CSR
   return hipGetLastError();
@@ -466,7 +482,8 @@ hipError_t mz_mles(const CcsDev &M, const uint64_t *z, int nz, int nv, uint64_t 
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  return csr(M, M.rp, M.m + 1, na, M.col, nullptr, M.sval, M.m, z, M.n * M.d, out, len, nz * na, st, sel);
+  return csr(M, M.rp, M.m + 1, na, M.col, nullptr, M.sval, M.m, z, M.n * M.d, out, len, nz * na, st, sel,
+             (size_t)nz * na * len * 8 >= CSR_NT_BYTES);
 }
 
 hipError_t mz_challenged(const CcsDev &M, const uint64_t *z, const uint64_t *zeta, int nz, int nv, uint64_t *out,
