@@ -341,6 +341,9 @@ struct CcsDev {
   const uint64_t *sval = nullptr;  // [nnz] when every entry is a scalar (v in every slot word 0, zero elsewhere)
   const uint64_t *svh = nullptr;   // sval in the row-merged order (svh[k] = sval[hidx[k]])
   const uint64_t *svc = nullptr;   // sval in the transposes' order (svc[k] = sval[cidx[k]])
+  // ring-valued entries in the row-merged and transposes' orders (vh[k] = val[hidx[k]],
+  // vc[k] = val[cidx[k]], d words each; null: those products gather through hidx / cidx)
+  const uint64_t *vh = nullptr, *vc = nullptr;
   const uint64_t *hrp;  // [m + 1]
   const uint32_t *hcol;  // j n + col
   const uint32_t *hidx;  // value index
@@ -349,6 +352,8 @@ struct CcsDev {
   const uint32_t *cidx;
 };
 size_t mz_scratch_elems(const CcsDev &M, int nz, int nv);
+// out[k] = val[idx[k]] for k < nnz, d words each (CcsDev::vh / vc)
+hipError_t gather_entries(const uint64_t *val, const uint32_t *idx, size_t nnz, int d, uint64_t *out, hipStream_t st);
 // scratch words of one side of mz_challenged(_pair): the zeta powers, for d = 24 the
 // matrix-core operand pieces, and y = sum_i zeta_i^(j+1) z_i ([t][n][d])
 size_t mz_chall_elems(const CcsDev &M, int nz);

@@ -2156,6 +2156,9 @@ int lf_ccs_set_structure(lf_ctx *c, lf_ccs *M, size_t l, int degree, int q, cons
   return LF_OK;
 }
 
+// the largest pair of reordered ring-valued entry copies lf_ccs_create keeps (CcsDev::vh / vc)
+constexpr size_t CCS_REORDER_BYTES = (size_t)16 << 30;
+
 int lf_ccs_create(lf_ctx *c, int d, int t, size_t m, size_t n, const uint64_t *row_ptr, const uint32_t *col,
                   const uint64_t *val, int repr, lf_ccs **out) {
   if (!c || !out || t < 1 || !m || !n || !row_ptr) return LF_ERR_INVALID_ARG;
@@ -2270,6 +2273,20 @@ int lf_ccs_create(lf_ctx *c, int d, int t, size_t m, size_t n, const uint64_t *r
   D.crow = (const uint32_t *)p;
   LF_TRY(put(cidx.data(), nnz * 4, &p));
   D.cidx = (const uint32_t *)p;
+  // ring-valued entries: copies in the row-merged and transposes' orders, so the
+  // challenged pass and the Mz weights read their values sequentially instead of
+  // gathering d words per entry through hidx / cidx (at the zkvm's shape 2 x 3.15 GB;
+  // above CCS_REORDER_BYTES the gathers stay)
+  if (!D.sval && nnz && 2 * nnz * d * 8 <= CCS_REORDER_BYTES) {
+    const uint32_t *ix[2] = {D.hidx, D.cidx};
+    const uint64_t **dst[2] = {&D.vh, &D.vc};
+    for (int q = 0; q < 2; q++) {
+      LF_HIP(c, hipMalloc(&p, nnz * d * 8));
+      M->bufs.push_back(p);
+      LF_HIP(c, lfk::gather_entries(D.val, ix[q], nnz, d, (uint64_t *)p, c->cur));
+      *dst[q] = (const uint64_t *)p;
+    }
+  }
   LF_HIP(c, hipStreamSynchronize(c->cur));  // the host vectors go out of scope
   *out = M.release();
   return LF_OK;

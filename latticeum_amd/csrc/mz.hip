@@ -394,12 +394,14 @@ __global__ void k_zero_tails(uint64_t *out, size_t len, size_t from, size_t tail
 hipError_t csr(const CcsDev &M, const uint64_t *rp, size_t rp_stride, int na, const uint32_t *col,
                const uint32_t *vidx, const uint64_t *sv, size_t nrows, const uint64_t *z, size_t z_stride,
                uint64_t *out, size_t out_stride, int ntask, hipStream_t st, const int *sel = nullptr,
-               bool nt = false) {
+               bool nt = false, const uint64_t *rv = nullptr) {
   if (!nrows || !ntask) return hipSuccess;
   const int d = M.d, tb = slot_words(d), ns = d / tb, spb = ns < MT ? ns : MT;
   const dim3 grid(nblk(nrows, MT / spb), (unsigned)ntask, (unsigned)(ns / spb));
-  const uint64_t *val = M.sval ? sv : M.val;
-  if (M.sval) vidx = nullptr;
+  // the entries' values in this product's own order when there is a copy (sv: scalar,
+  // rv: ring-valued), else gathered through vidx
+  const uint64_t *val = M.sval ? sv : (rv ? rv : M.val);
+  if (M.sval || rv) vidx = nullptr;
 #define LF_CSR(TB, SC)                                                                                          \
   if (nt)                                                                                                       \
     hipLaunchKernelGGL((k_csr<TB, SC, true>), grid, dim3(MT), 0, st, rp, rp_stride, na, sel, col, vidx, val, nrows, \
@@ -460,7 +462,20 @@ hipError_t zcomb(const CcsDev &M, const uint64_t *z, const uint64_t *zeta, int n
   return hipGetLastError();
 }
 
+__global__ void k_gather_entries(const uint64_t *val, const uint32_t *idx, size_t nnz, int d, uint64_t *out) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // (entry, word)
+  if (i >= nnz * d) return;
+  const size_t k = i / d;
+  out[i] = val[(size_t)idx[k] * d + (i - k * d)];
+}
+
 }  // namespace
+
+hipError_t gather_entries(const uint64_t *val, const uint32_t *idx, size_t nnz, int d, uint64_t *out, hipStream_t st) {
+  if (!nnz) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_entries, dim3(nblk(nnz * d, 256)), dim3(256), 0, st, val, idx, nnz, d, out);
+  return hipGetLastError();
+}
 
 size_t mz_chall_elems(const CcsDev &M, int nz) { return zc_front(M, nz) + (size_t)M.t * M.n * M.d; }
 
@@ -497,7 +512,7 @@ hipError_t mz_challenged(const CcsDev &M, const uint64_t *z, const uint64_t *zet
     e = hipMemsetAsync(out + M.m * M.d, 0, (len - M.m * M.d) * 8, st);
     if (e != hipSuccess) return e;
   }
-  return csr(M, M.hrp, 0, 1, M.hcol, M.hidx, M.svh, M.m, y, 0, out, 0, 1, st);
+  return csr(M, M.hrp, 0, 1, M.hcol, M.hidx, M.svh, M.m, y, 0, out, 0, 1, st, nullptr, false, M.vh);
 }
 
 hipError_t mz_challenged_pair(const CcsDev &M, const uint64_t *z0, const uint64_t *zeta0, const uint64_t *z1,
@@ -520,8 +535,8 @@ hipError_t mz_challenged_pair(const CcsDev &M, const uint64_t *z0, const uint64_
   if (!M.m) return hipSuccess;
   const int spb = ns < MT ? ns : MT;
   const dim3 grid(nblk(M.m, MT / spb), 1, (unsigned)(ns / spb));
-  const uint64_t *val = M.sval ? M.svh : M.val;
-  const uint32_t *vidx = M.sval ? nullptr : M.hidx;
+  const uint64_t *val = M.sval ? M.svh : (M.vh ? M.vh : M.val);
+  const uint32_t *vidx = M.sval || M.vh ? nullptr : M.hidx;
 #define LF_CSRP(TB, SC)                                                                                       \
   hipLaunchKernelGGL((k_csr_pair<TB, SC>), grid, dim3(MT), 0, st, M.hrp, M.hcol, vidx, val, M.m, M.d, ys[0], ys[1], \
                      out0, out1, spb)
@@ -542,7 +557,7 @@ hipError_t mz_challenged_pair(const CcsDev &M, const uint64_t *z0, const uint64_
 
 hipError_t mz_weights(const CcsDev &M, const uint64_t *eq, uint64_t *w, hipStream_t st) {
   // w_j[c] = sum over column c of M_j of value (.) eq[row]
-  return csr(M, M.crp, M.n + 1, M.t, M.crow, M.cidx, M.svc, M.n, eq, 0, w, M.n * M.d, M.t, st);
+  return csr(M, M.crp, M.n + 1, M.t, M.crow, M.cidx, M.svc, M.n, eq, 0, w, M.n * M.d, M.t, st, nullptr, false, M.vc);
 }
 
 hipError_t mz_evaluate(const CcsDev &M, const uint64_t *z, int nz, int nv, const uint64_t *point, uint64_t *out,
