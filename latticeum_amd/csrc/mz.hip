@@ -199,13 +199,6 @@ __global__ void k_zc_bfrag(const uint64_t *z, int nz, size_t n, int kcn, size_t 
   for (int dg = 0; dg < 8; dg++) bf[(o + dg) * 64 + l] = *reinterpret_cast<const v4i *>(&pc[dg]);
 }
 
-// one wave per (column tile ct, row tile rt), the block's waves on consecutive rt of
-// one ct (their z pieces come from the same L1 lines), and the blocks of one ct on one
-// XCD (blocks are dealt round-robin over the 8 XCDs: block b runs on XCD b & 7), so a
-// column tile's pieces come into one L2 once. Per slot 64 MFMAs per K chunk, the next
-// chunk's pieces loaded behind them, and the epilogue into the wave's LDS rows
-// [jl][c][24]; then one pass of whole 192-byte (j, c) elements out (16 consecutive
-// columns: 3 KiB contiguous per j)
 // the 64 digit products of one K chunk into the 15 weights; FIRST: the chunk that starts
 // the sums (each weight's first product, (0, t) or (t - 7, 7), takes a zero accumulator)
 template <bool FIRST>
@@ -218,6 +211,13 @@ __device__ __forceinline__ void zc_products(const v4i *A, const v4i *B, v4i *acc
           A[ka], B[kb], FIRST && (ka == 0 || kb == 7) ? (v4i){0, 0, 0, 0} : acc[ka + kb], 0, 0, 0);
 }
 
+// one wave per (column tile ct, row tile rt), the block's waves on consecutive rt of
+// one ct (their z pieces come from the same L1 lines), and the blocks of one ct on one
+// XCD (blocks are dealt round-robin over the 8 XCDs: block b runs on XCD b & 7), so a
+// column tile's pieces come into one L2 once. Per slot 64 MFMAs per K chunk, the next
+// chunk's pieces loaded behind them, and the epilogue into the wave's LDS rows
+// [jl][c][24]; then one pass of whole 192-byte (j, c) elements out (16 consecutive
+// columns: 3 KiB contiguous per j).
 // SK (3 nz < 64, one K chunk with a zero tail: |acc_t| <= 3 nz 8 128^2 < 2^31 / 257): the
 // weights pair up in 32 bits first, W_m = acc_2m + 2^8 acc_2m+1, halving the 64-bit work
 template <bool SK>
